@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark: job placements/sec at 4096 clusters x 256 nodes (BASELINE.json).
+
+One "step" = one full pass of the hot path over one batch of synthetic input: mcs_run simulates the
+reference FIFO loop (pkg/scheduler/scheduler.go:216-296) for every cluster of the shard from its
+spec until every job is placed.  Inputs (job streams) are generated on the device before the timed
+region and stay resident in HBM.
+
+Multi-GPU: one process per GPU (torchrun), clusters sharded by rank with NO data-path collective
+(clusters are independent); per-GPU work is fixed (4096 clusters per rank) -> "scaling": "weak".
+torch.distributed is used only for the barrier and the max-over-ranks of the timed region.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with "roofline" (HBM-bound:
+28 algorithmic bytes per placement) and "cpu_baseline" (the oracle, rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "multi-cluster-simulator_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+BYTES_PER_PLACEMENT = 28  # 16 B job record read + 12 B result write
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--clusters", type=int, default=4096, help="clusters per GPU (weak scaling)")
+    ap.add_argument("--nodes", type=int, default=256)
+    ap.add_argument("--jobs-per-cluster", type=int, default=16384)
+    ap.add_argument("--load", type=float, default=0.9, help="offered memory load of the scaled arrivals")
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x4D43535F53494D31)
+    ap.add_argument("--cpu-sample-clusters", type=int, default=512)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
+                    help="per-launch HBM bytes measured by a separate rocprofv3 --pmc pass")
+    return ap.parse_args()
+
+
+def rank_seed(seed: int, rank: int) -> int:
+    # distinct streams per rank: cluster k of rank r is keyed (seed ^ mix(r)) ^ k
+    z = (rank + 1) * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    return seed ^ (z if rank else 0)
+
+
+def cpu_baseline(args, lam, n_threads):
+    """The oracle (CPU restatement, deliberately naive, -O3) on a bounded sample of the same
+    workload: the first cpu_sample_clusters clusters of rank 0, full job streams, OpenMP over
+    clusters.  Test infrastructure used as the reported baseline only."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ref as O
+    from mcs_amd import GenParams, replicate, uniform_cluster
+    from mcs_amd.engine import gen_streams_host
+
+    k = min(args.cpu_sample_clusters, args.clusters)
+    arrays = replicate(uniform_cluster(args.nodes), k)
+    gp = GenParams(seed=rank_seed(args.seed, 0), arrival_mode=1, lam=lam)
+    streams = gen_streams_host(gp, arrays, args.jobs_per_cluster)
+    O.lib()
+    t0 = time.perf_counter()
+    node, st, fi, sd = O.fifo_run_batch(arrays, streams, n_threads=n_threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": streams.n_jobs / dt,
+        "unit": "placements/s",
+        "cores": n_threads,
+        "kind": "port",
+        "sample": f"{k} of {args.clusters} clusters x {args.nodes} nodes x {args.jobs_per_cluster} jobs "
+                  f"({streams.n_jobs} placements), oracle/mcs_oracle.c -O3, OpenMP over clusters, "
+                  f"{dt:.2f} s wall",
+        "seconds": dt,
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    dist_on = world > 1
+    if dist_on:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend="nccl")
+    dev = torch.device("cuda", local_rank)
+
+    from mcs_amd import Engine, GenParams, replicate, uniform_cluster
+    from mcs_amd.engine import scaled_lambda
+
+    lam = scaled_lambda(args.nodes, load=args.load)
+    eng = Engine(local_rank)
+    arrays = replicate(uniform_cluster(args.nodes), args.clusters)
+    eng.load_clusters(arrays)
+    gp = GenParams(seed=rank_seed(args.seed, rank), arrival_mode=1, lam=lam)
+    eng.generate_jobs(gp, args.jobs_per_cluster)
+    n_jobs = eng.num_jobs
+
+    def barrier():
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        st = eng.run()
+        if st.placed + st.unplaced != n_jobs:
+            raise RuntimeError(f"warmup run accounted {st.placed}+{st.unplaced} of {n_jobs} jobs")
+
+    barrier()
+    t0 = time.perf_counter()
+    kernel_ms = []
+    placed = 0
+    escalations = 0
+    for _ in range(args.steps):
+        st = eng.run()
+        kernel_ms.append(st.kernel_ms)
+        placed += st.placed
+        escalations += st.escalations
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    t = torch.tensor([elapsed, float(placed)], dtype=torch.float64, device=dev)
+    if dist_on:
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum[1:], op=dist.ReduceOp.SUM)
+        elapsed_max = float(tmax[0])
+        placed_all = float(tsum[1])
+    else:
+        elapsed_max, placed_all = elapsed, float(placed)
+
+    if rank == 0:
+        avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+        placements_per_launch = placed / args.steps  # this rank
+        achieved = placements_per_launch * BYTES_PER_PLACEMENT / avg_kernel_s / 1e9
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if (tj.get("clusters"), tj.get("nodes"), tj.get("jobs_per_cluster")) == \
+                    (args.clusters, args.nodes, args.jobs_per_cluster):
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            n_thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(args, lam, n_thr)
+        value = placed_all / elapsed_max
+        out = {
+            "metric": "job placements/sec (whole node) at 4096 clusters x 256 nodes",
+            "value": value,
+            "unit": "placements/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded device generator restating pkg/client/client.go distributions; "
+                    "scaled Poisson arrivals)",
+            "config": {
+                "workload": f"C4: {args.clusters} clusters x {args.nodes} nodes per GPU, FIFO, no trading, "
+                            f"{args.jobs_per_cluster} jobs/cluster, scaled arrivals at {args.load:.0%} memory load "
+                            f"(lambda={lam:.4f}/s)",
+                "clusters_per_gpu": args.clusters,
+                "nodes": args.nodes,
+                "jobs_per_cluster": args.jobs_per_cluster,
+                "placements_per_step_per_gpu": placements_per_launch,
+                "parallelism": f"dp{world} (independent cluster shards, no collective on the data path)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "mcs::fifo_kernel",
+                "kernel_ms_avg": avg_kernel_s * 1e3,
+                "bytes_per_placement": BYTES_PER_PLACEMENT,
+            },
+            "cpu_baseline": cpu,
+            "slot_pool_escalations": escalations,
+        }
+        print(json.dumps(out), flush=True)
+
+    eng.close()
+    if dist_on:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

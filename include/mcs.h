@@ -1,0 +1,193 @@
+/*
+ * mcs.h — C ABI of the MI355X batched FIFO placement engine (libmcs.so).
+ *
+ * Drop-in boundary for the data-parallel hot path of hamzalsheikh/multi-cluster-simulator
+ * (reference snapshot 2024-10-16).  The reference has no FFI: the path is a set of Go methods on
+ * a global singleton.  Each entry point below names the reference symbol it replaces
+ * (path:line relative to the reference root).  A Go cgo binding is shown in INTEGRATION.md.
+ *
+ * Rules of the ABI:
+ *   - plain C99, no C++ types, no callbacks; every call is blocking;
+ *   - the caller owns every host array; the engine copies inputs in during the call and never
+ *     keeps host pointers; the engine owns all device memory and frees it in mcs_engine_destroy;
+ *   - a handle is NOT thread-safe: one host thread (one cgo goroutine) per handle, one handle per GPU;
+ *   - status codes are ints (mcs_status); details via mcs_last_error(); no exception crosses the ABI.
+ *
+ * Units: every time is a whole number of SECONDS in a uint32 (deviation D8 of SURVEY Appendix A:
+ * the reference only produces whole seconds — pkg/client/client.go:98 and all sleeps).
+ */
+#ifndef MCS_H
+#define MCS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCS_ABI_VERSION 1
+
+/* ---- status codes --------------------------------------------------------------------------- */
+typedef enum mcs_status {
+    MCS_OK = 0,
+    /* ScheduleJob's error "not enough resources in cluster" (pkg/scheduler/scheduler.go:138) */
+    MCS_NO_FIT = 1,
+    MCS_E_INVALID = -1,  /* bad argument / inconsistent sizes                                     */
+    MCS_E_CAPACITY = -2, /* running-slot pool overflow that survived capacity escalation          */
+    MCS_E_HIP = -3,      /* a HIP runtime call failed                                             */
+    MCS_E_RCCL = -4,     /* an RCCL call failed                                                   */
+    MCS_E_STATE = -5,    /* call out of order (e.g. mcs_run before mcs_load_clusters)             */
+    MCS_E_NOMEM = -6     /* host or device allocation failed                                      */
+} mcs_status;
+
+/* Node index written for a job that is never placed (head-of-line deadlock: the wait-queue head
+ * cannot fit even on an empty cluster, so the reference's Fifo loop retries it forever,
+ * scheduler.go:219-251).  start/finish are then MCS_TIME_NONE. */
+#define MCS_NODE_UNPLACED (-1)
+#define MCS_TIME_NONE 0xFFFFFFFFu
+
+/* per-cluster flag bits (mcs_cluster_stats.flags) */
+#define MCS_FLAG_DEADLOCK 0x1u /* head-of-line job can never fit; rest of the stream unplaced     */
+#define MCS_FLAG_OVERFLOW 0x2u /* running-slot pool overflow (engine re-runs with a larger pool)   */
+#define MCS_FLAG_CLOCK_OVERFLOW 0x4u /* the uint32 seconds clock would wrap; results after it invalid */
+
+/* ---- configuration ------------------------------------------------------------------------- */
+typedef enum mcs_policy {
+    MCS_POLICY_FIFO = 0,  /* Scheduler.Fifo (scheduler.go:216-296); selected by config (D4)       */
+    MCS_POLICY_DELAY = 1  /* Scheduler.Delay (scheduler.go:298-369); not implemented in ABI v1    */
+} mcs_policy;
+
+typedef struct mcs_config {
+    uint32_t policy;         /* mcs_policy; ABI v1 accepts MCS_POLICY_FIFO only                    */
+    uint32_t borrow;         /* FIFO cross-cluster borrow (server.go:160-248); must be 0 in v1     */
+    uint32_t trader;         /* trader offer exchange (trader.go:193-325); must be 0 in v1         */
+    uint32_t wait_sleep_s;   /* sleep after a wait-queue attempt, scheduler.go:250 (must be 1)     */
+    uint32_t idle_sleep_s;   /* sleep when all queues are empty, scheduler.go:294 (must be 1)      */
+    uint32_t slot_pool;      /* initial running-slot pool per cluster in units of 64 (0 = auto)    */
+    uint32_t reserved[10];
+} mcs_config;
+
+/* Fills the reference defaults (FIFO, no borrow, no trader, 1 s sleeps). */
+void mcs_config_default(mcs_config* cfg);
+
+/* ---- synthetic job stream (input synthesis; restates pkg/client/client.go:85-147) ----------- */
+typedef enum mcs_arrival_mode {
+    MCS_ARRIVAL_REF = 0,    /* per minute n ~ Poisson(lambda), spacing floor(60/n) s (client.go:107-125);
+                               n == 0 is an idle minute of 60 s (D5)                                 */
+    MCS_ARRIVAL_SCALED = 1  /* per second n ~ Poisson(lambda) arrivals at that second               */
+} mcs_arrival_mode;
+
+typedef struct mcs_gen_params {
+    uint64_t seed;        /* base seed; cluster k uses key = mix(seed ^ k)                           */
+    uint32_t arrival_mode;/* mcs_arrival_mode                                                        */
+    uint32_t max_dur_s;   /* durations U{0..max_dur_s-1}; 600 = rand.Intn(600) (client.go:98)        */
+    double lambda;        /* Poisson mean per minute (REF, 10 in client.go:108) or per second (SCALED) */
+    uint32_t max_cores;   /* 0 = per-cluster max node Cores (setMaxCluster, client.go:68-83)          */
+    uint32_t max_mem;     /* 0 = per-cluster max node Memory                                          */
+    uint32_t reserved[4];
+} mcs_gen_params;
+
+void mcs_gen_params_default(mcs_gen_params* p);
+
+/* Host generator (same arithmetic as the device generator, bit-identical output).  Generates the
+ * jobs of ONE cluster (index `cluster`) with the given max cores/mem. */
+int mcs_gen_cluster_host(const mcs_gen_params* p, uint32_t cluster, uint32_t max_cores,
+                         uint32_t max_mem, uint64_t n_jobs, uint32_t* arrival_s, uint32_t* dur_s,
+                         uint32_t* cores, uint32_t* mem);
+
+/* Per-second lambda giving `load` offered memory load for n_nodes nodes of node_mem memory
+ * (SCALED mode): lambda = load * n_nodes * node_mem / (E[mem] * E[dur]). */
+double mcs_gen_scaled_lambda(uint32_t n_nodes, uint32_t node_mem, uint32_t max_mem,
+                             uint32_t max_dur_s, double load);
+
+/* ---- engine ---------------------------------------------------------------------------------- */
+typedef struct mcs_engine mcs_engine;
+
+typedef struct mcs_stats {
+    uint64_t jobs;          /* jobs in the submitted streams                                     */
+    uint64_t placed;        /* jobs placed on a node                                             */
+    uint64_t waited;        /* jobs that entered the wait queue (scheduler.go:264-268)           */
+    uint64_t unplaced;      /* jobs never placed (deadlocked clusters)                           */
+    uint32_t clusters;
+    uint32_t deadlocked;    /* clusters with MCS_FLAG_DEADLOCK                                   */
+    uint32_t escalations;   /* slot-pool re-runs performed                                       */
+    uint32_t slot_pool;     /* largest slot pool used (x64)                                      */
+    double kernel_ms;       /* device time of the placement kernel(s), HIP events on the engine stream */
+    double wall_ms;         /* host wall time of the whole mcs_run call                           */
+} mcs_stats;
+
+typedef struct mcs_cluster_stats {
+    uint32_t t_end;         /* simulated clock when the cluster's queues drained (seconds)       */
+    uint32_t placed;
+    uint32_t waited;
+    uint32_t peak_running;  /* peak jobs holding resources (dur > 0)                              */
+    uint32_t flags;         /* MCS_FLAG_*                                                         */
+    uint32_t pool;          /* slot pool (x64) the final result was produced with                */
+    uint32_t reserved[2];
+} mcs_cluster_stats;
+
+/* scheduler.Run (scheduler.go:101-124) builds a Scheduler; here one engine batches many clusters
+ * on ONE GPU (`device` = HIP ordinal). */
+int mcs_engine_create(const mcs_config* cfg, int device, mcs_engine** out);
+int mcs_engine_destroy(mcs_engine* eng);
+const char* mcs_last_error(const mcs_engine* eng);
+int mcs_abi_version(void);
+
+/* Cluster specs (assets/cluster_*.json, Cluster/Node in pkg/scheduler/cluster.go:14-24,127-138):
+ * nodes of cluster c are [node_offsets[c], node_offsets[c+1]) in JSON array order; free_* are the
+ * JSON CoresAvailable/MemoryAvailable, kept as-is by Run (scheduler.go:101-109, KAT5).
+ * At most 1024 nodes per cluster in ABI v1. */
+int mcs_load_clusters(mcs_engine* eng, const uint32_t* cap_c, const uint32_t* cap_m,
+                      const uint32_t* free_c, const uint32_t* free_m,
+                      const uint32_t* node_offsets, uint32_t n_clusters);
+
+/* Job streams (the ReadyQueue filled by the "/" handler, server.go:23-51): jobs of cluster c are
+ * [job_offsets[c], job_offsets[c+1]), sorted by arrival (non-decreasing); job id = index. */
+int mcs_submit_jobs(mcs_engine* eng, const uint32_t* arrival_s, const uint32_t* dur_s,
+                    const uint32_t* cores, const uint32_t* mem, const uint64_t* job_offsets);
+
+/* Same as mcs_submit_jobs but synthesises n_jobs per cluster on the device (bit-identical to
+ * mcs_gen_cluster_host for every cluster). */
+int mcs_generate_jobs(mcs_engine* eng, const mcs_gen_params* p, uint64_t jobs_per_cluster);
+
+/* Copies the (submitted or generated) job streams back to the host (sizes from the offsets). */
+int mcs_read_jobs(mcs_engine* eng, uint32_t* arrival_s, uint32_t* dur_s, uint32_t* cores,
+                  uint32_t* mem);
+
+/* Runs the FIFO policy loop (Scheduler.Fifo, scheduler.go:216-296, over ScheduleJob
+ * scheduler.go:127-139 and Node.RunJob cluster.go:141-161) for every cluster from its loaded spec
+ * until every job is placed (t_end_s = MCS_TIME_NONE; other horizons are reserved in v1).
+ * Serialized semantics SFIFO, SURVEY Appendix A. */
+int mcs_run(mcs_engine* eng, uint32_t t_end_s, mcs_stats* stats);
+
+/* Per-job results of the last mcs_run, indexed like the submitted jobs. */
+int mcs_read_placements(mcs_engine* eng, int32_t* node, uint32_t* start_s, uint32_t* finish_s);
+int mcs_read_cluster_stats(mcs_engine* eng, mcs_cluster_stats* out, uint32_t n_clusters);
+
+uint32_t mcs_num_clusters(const mcs_engine* eng);
+uint64_t mcs_num_jobs(const mcs_engine* eng);
+
+/* ---- single-job mirrors (live cluster state, initialised from the spec at load time) -------- */
+/* Scheduler.ScheduleJob (scheduler.go:127-139) with the commit of Node.RunJob (cluster.go:144-148)
+ * done synchronously (D2): first node in order with CoresAvailable >= cores && MemoryAvailable >=
+ * mem.  Returns MCS_OK and *node, or MCS_NO_FIT with *node = MCS_NODE_UNPLACED. */
+int mcs_schedule_one(mcs_engine* eng, uint32_t cluster, uint32_t cores, uint32_t mem,
+                     int32_t* node);
+/* The completion half of Node.RunJob (cluster.go:153-157): node gives back cores/mem. */
+int mcs_release_one(mcs_engine* eng, uint32_t cluster, uint32_t node, uint32_t cores,
+                    uint32_t mem);
+/* Scheduler.Lend (scheduler.go:194-202): strict '>' existence test, no commit. */
+int mcs_lend_check(mcs_engine* eng, uint32_t cluster, uint32_t cores, uint32_t mem, int32_t* ok);
+/* Live free vectors of one cluster (n = node count of the cluster). */
+int mcs_read_live_state(mcs_engine* eng, uint32_t cluster, uint32_t* free_c, uint32_t* free_m,
+                        uint32_t n);
+/* Cluster.GetResourceUtilization (cluster.go:46-63) over the live state: float32 sums in node
+ * order divided by float32 totals (SetTotalResources, cluster.go:26-40). */
+int mcs_resource_utilization(mcs_engine* eng, uint32_t cluster, float* core_util,
+                             float* mem_util);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MCS_H */

@@ -1,0 +1,584 @@
+// mcs_engine.cpp — C ABI of libmcs.so (include/mcs.h): device memory, HBM layout, launch policy,
+// slot-pool escalation and the single-job mirrors.  Host code; compiled by hipcc.
+//
+// No CPU fallback exists anywhere in this library: every placement decision is made by a gfx950
+// kernel (mcs_kernels.hip).  If no HIP device is usable every compute entry point fails with
+// MCS_E_HIP and a message.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "mcs_gen.h"
+#include "mcs_internal.h"
+
+struct mcs_engine {
+    mcs_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+
+    uint32_t C = 0;
+    uint32_t max_n = 0;
+    uint64_t total_nodes = 0, total_jobs = 0;
+    std::vector<uint32_t> node_off;
+    std::vector<uint64_t> job_off;
+
+    uint2* d_free0 = nullptr;
+    uint2* d_cap = nullptr;
+    uint32_t* d_node_off = nullptr;
+    uint32_t* d_live_c = nullptr;
+    uint32_t* d_live_m = nullptr;
+    uint32_t* d_max_c = nullptr;
+    uint32_t* d_max_m = nullptr;
+    uint4* d_jobs = nullptr;
+    uint64_t* d_job_off = nullptr;
+    int32_t* d_out_node = nullptr;
+    uint32_t* d_out_start = nullptr;
+    uint32_t* d_out_finish = nullptr;
+    mcs_cluster_stats* d_cstats = nullptr;
+    mcs::Totals* d_totals = nullptr;
+    uint32_t* d_list = nullptr;
+    int32_t* d_scratch = nullptr;
+    float* d_util = nullptr;
+    bool has_clusters = false, has_jobs = false, has_run = false;
+};
+
+namespace {
+
+int fail(mcs_engine* e, int code, const std::string& msg) {
+    if (e) e->err = msg;
+    return code;
+}
+
+#define HIPCHK(e, call)                                                                      \
+    do {                                                                                     \
+        hipError_t _st = (call);                                                             \
+        if (_st != hipSuccess)                                                               \
+            return fail((e), MCS_E_HIP,                                                      \
+                        std::string(#call) + ": " + hipGetErrorString(_st));                 \
+    } while (0)
+
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+void free_clusters(mcs_engine* e) {
+    dfree(e->d_free0);
+    dfree(e->d_cap);
+    dfree(e->d_node_off);
+    dfree(e->d_live_c);
+    dfree(e->d_live_m);
+    dfree(e->d_max_c);
+    dfree(e->d_max_m);
+    dfree(e->d_cstats);
+    dfree(e->d_list);
+}
+
+void free_jobs(mcs_engine* e) {
+    dfree(e->d_jobs);
+    dfree(e->d_job_off);
+    dfree(e->d_out_node);
+    dfree(e->d_out_start);
+    dfree(e->d_out_finish);
+}
+
+int npl_for(uint32_t max_n) {
+    const int opts[] = {1, 2, 4, 8, 16};
+    for (int o : opts)
+        if ((uint32_t)(o * mcs::kWave) >= max_n) return o;
+    return -1;
+}
+
+// Initial running-slot pool (registers per lane): room for ~4 running jobs per node, rounded to a
+// power of two in [2, 32].  Escalation doubles it for clusters that overflow.
+int auto_pool(uint32_t max_n) {
+    const uint32_t want = (4u * max_n + 63u) / 64u;
+    int p = 2;
+    while ((uint32_t)p < want && p < mcs::kMaxPool) p *= 2;
+    return p;
+}
+
+int check_engine(mcs_engine* e) {
+    if (!e) return MCS_E_INVALID;
+    hipError_t st = hipSetDevice(e->device);
+    if (st != hipSuccess) return fail(e, MCS_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(st));
+    return MCS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mcs_abi_version(void) { return MCS_ABI_VERSION; }
+
+void mcs_config_default(mcs_config* cfg) {
+    if (!cfg) return;
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->policy = MCS_POLICY_FIFO;
+    cfg->borrow = 0;
+    cfg->trader = 0;
+    cfg->wait_sleep_s = 1; /* scheduler.go:250 */
+    cfg->idle_sleep_s = 1; /* scheduler.go:294 */
+    cfg->slot_pool = 0;
+}
+
+void mcs_gen_params_default(mcs_gen_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->seed = MCS_GEN_SEED_DEFAULT;
+    p->arrival_mode = MCS_ARRIVAL_REF;
+    p->max_dur_s = 600; /* rand.Intn(600), client.go:98 */
+    p->lambda = 10.0;   /* distuv.Poisson{Lambda: 10}, client.go:107-110 */
+    p->max_cores = 0;
+    p->max_mem = 0;
+}
+
+int mcs_gen_cluster_host(const mcs_gen_params* p, uint32_t cluster, uint32_t max_cores,
+                         uint32_t max_mem, uint64_t n_jobs, uint32_t* arrival_s, uint32_t* dur_s,
+                         uint32_t* cores, uint32_t* mem) {
+    if (!p || (n_jobs && (!arrival_s || !dur_s || !cores || !mem))) return MCS_E_INVALID;
+    if (!(p->lambda > 0.0) || p->lambda > 128.0 || p->arrival_mode > 1u || p->max_dur_s == 0)
+        return MCS_E_INVALID;
+    const uint64_t key = mcs_cluster_key(p->seed, cluster);
+    for (uint64_t i = 0; i < n_jobs; ++i)
+        mcs_gen_job_attrs(key, i, max_cores, max_mem, p->max_dur_s, &dur_s[i], &cores[i], &mem[i]);
+    mcs_gen_arrivals(key, p->arrival_mode, std::exp(-p->lambda), n_jobs, arrival_s);
+    return MCS_OK;
+}
+
+double mcs_gen_scaled_lambda(uint32_t n_nodes, uint32_t node_mem, uint32_t max_mem,
+                             uint32_t max_dur_s, double load) {
+    const double e_mem = 0.5 * (double)max_mem - 0.5;   /* E[floor(B*max)], B ~ Beta(2,2) */
+    const double e_dur = 0.5 * ((double)max_dur_s - 1.0); /* E[U{0..max-1}] */
+    if (e_mem <= 0.0 || e_dur <= 0.0) return 0.0;
+    return load * (double)n_nodes * (double)node_mem / (e_mem * e_dur);
+}
+
+int mcs_engine_create(const mcs_config* cfg, int device, mcs_engine** out) {
+    if (!out) return MCS_E_INVALID;
+    *out = nullptr;
+    mcs_config c;
+    if (cfg)
+        c = *cfg;
+    else
+        mcs_config_default(&c);
+    if (c.policy != MCS_POLICY_FIFO || c.borrow != 0 || c.trader != 0 || c.wait_sleep_s != 1 ||
+        c.idle_sleep_s != 1)
+        return MCS_E_INVALID; /* ABI v1: FIFO, no borrow, no trader, reference sleeps */
+    if (c.slot_pool != 0 && !mcs::fifo_variant_exists(1, (int)c.slot_pool)) return MCS_E_INVALID;
+    mcs_engine* e = new (std::nothrow) mcs_engine();
+    if (!e) return MCS_E_NOMEM;
+    e->cfg = c;
+    e->device = device;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+        delete e;
+        return MCS_E_HIP;
+    }
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess ||
+        hipMalloc(&e->d_totals, sizeof(mcs::Totals)) != hipSuccess ||
+        hipMalloc(&e->d_scratch, 64) != hipSuccess || hipMalloc(&e->d_util, 64) != hipSuccess) {
+        mcs_engine_destroy(e);
+        return MCS_E_HIP;
+    }
+    *out = e;
+    return MCS_OK;
+}
+
+int mcs_engine_destroy(mcs_engine* e) {
+    if (!e) return MCS_E_INVALID;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    free_clusters(e);
+    free_jobs(e);
+    dfree(e->d_totals);
+    dfree(e->d_scratch);
+    dfree(e->d_util);
+    if (e->ev0) (void)hipEventDestroy(e->ev0);
+    if (e->ev1) (void)hipEventDestroy(e->ev1);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return MCS_OK;
+}
+
+const char* mcs_last_error(const mcs_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+uint32_t mcs_num_clusters(const mcs_engine* e) { return e ? e->C : 0; }
+uint64_t mcs_num_jobs(const mcs_engine* e) { return e ? e->total_jobs : 0; }
+
+int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_m,
+                      const uint32_t* free_c, const uint32_t* free_m,
+                      const uint32_t* node_offsets, uint32_t n_clusters) {
+    if (int st = check_engine(e)) return st;
+    if (!node_offsets || n_clusters == 0) return fail(e, MCS_E_INVALID, "no clusters");
+    if (node_offsets[0] != 0) return fail(e, MCS_E_INVALID, "node_offsets[0] must be 0");
+    uint32_t max_n = 0;
+    for (uint32_t c = 0; c < n_clusters; ++c) {
+        if (node_offsets[c + 1] < node_offsets[c])
+            return fail(e, MCS_E_INVALID, "node_offsets must be non-decreasing");
+        max_n = std::max(max_n, node_offsets[c + 1] - node_offsets[c]);
+    }
+    if (max_n > (uint32_t)(mcs::kMaxNpl * mcs::kWave))
+        return fail(e, MCS_E_INVALID, "more than 1024 nodes in a cluster (ABI v1 limit)");
+    const uint64_t nn = node_offsets[n_clusters];
+    if (nn && (!cap_c || !cap_m || !free_c || !free_m))
+        return fail(e, MCS_E_INVALID, "null node array");
+
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    free_clusters(e);
+    free_jobs(e);
+    e->has_clusters = e->has_jobs = e->has_run = false;
+    e->C = n_clusters;
+    e->max_n = max_n;
+    e->total_nodes = nn;
+    e->total_jobs = 0;
+    e->node_off.assign(node_offsets, node_offsets + n_clusters + 1);
+    e->job_off.clear();
+
+    std::vector<uint2> free0(nn ? nn : 1), cap(nn ? nn : 1);
+    std::vector<uint32_t> lc(nn ? nn : 1), lm(nn ? nn : 1), mxc(n_clusters), mxm(n_clusters);
+    for (uint64_t i = 0; i < nn; ++i) {
+        free0[i] = make_uint2(free_c[i], free_m[i]);
+        cap[i] = make_uint2(cap_c[i], cap_m[i]);
+        lc[i] = free_c[i];
+        lm[i] = free_m[i];
+    }
+    for (uint32_t c = 0; c < n_clusters; ++c) { /* setMaxCluster, client.go:68-83 */
+        uint32_t a = 0, b = 0;
+        for (uint32_t i = node_offsets[c]; i < node_offsets[c + 1]; ++i) {
+            a = std::max(a, cap_c[i]);
+            b = std::max(b, cap_m[i]);
+        }
+        mxc[c] = a;
+        mxm[c] = b;
+    }
+    const size_t nb = (nn ? nn : 1);
+    HIPCHK(e, hipMalloc(&e->d_free0, nb * sizeof(uint2)));
+    HIPCHK(e, hipMalloc(&e->d_cap, nb * sizeof(uint2)));
+    HIPCHK(e, hipMalloc(&e->d_live_c, nb * sizeof(uint32_t)));
+    HIPCHK(e, hipMalloc(&e->d_live_m, nb * sizeof(uint32_t)));
+    HIPCHK(e, hipMalloc(&e->d_node_off, (n_clusters + 1) * sizeof(uint32_t)));
+    HIPCHK(e, hipMalloc(&e->d_max_c, n_clusters * sizeof(uint32_t)));
+    HIPCHK(e, hipMalloc(&e->d_max_m, n_clusters * sizeof(uint32_t)));
+    HIPCHK(e, hipMalloc(&e->d_cstats, n_clusters * sizeof(mcs_cluster_stats)));
+    HIPCHK(e, hipMalloc(&e->d_list, n_clusters * sizeof(uint32_t)));
+    HIPCHK(e, hipMemcpy(e->d_free0, free0.data(), nb * sizeof(uint2), hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_cap, cap.data(), nb * sizeof(uint2), hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_live_c, lc.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_live_m, lm.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_node_off, node_offsets, (n_clusters + 1) * sizeof(uint32_t),
+                        hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_max_c, mxc.data(), n_clusters * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_max_m, mxm.data(), n_clusters * sizeof(uint32_t), hipMemcpyHostToDevice));
+    e->has_clusters = true;
+    return MCS_OK;
+}
+
+static int alloc_jobs(mcs_engine* e, const uint64_t* job_offsets) {
+    free_jobs(e);
+    e->has_jobs = e->has_run = false;
+    e->job_off.assign(job_offsets, job_offsets + e->C + 1);
+    e->total_jobs = job_offsets[e->C];
+    const size_t nj = e->total_jobs ? e->total_jobs : 1;
+    HIPCHK(e, hipMalloc(&e->d_jobs, nj * sizeof(uint4)));
+    HIPCHK(e, hipMalloc(&e->d_job_off, (e->C + 1) * sizeof(uint64_t)));
+    HIPCHK(e, hipMalloc(&e->d_out_node, nj * sizeof(int32_t)));
+    HIPCHK(e, hipMalloc(&e->d_out_start, nj * sizeof(uint32_t)));
+    HIPCHK(e, hipMalloc(&e->d_out_finish, nj * sizeof(uint32_t)));
+    HIPCHK(e, hipMemcpy(e->d_job_off, job_offsets, (e->C + 1) * sizeof(uint64_t),
+                        hipMemcpyHostToDevice));
+    return MCS_OK;
+}
+
+static int check_job_offsets(mcs_engine* e, const uint64_t* job_offsets) {
+    if (!job_offsets) return fail(e, MCS_E_INVALID, "null job_offsets");
+    if (job_offsets[0] != 0) return fail(e, MCS_E_INVALID, "job_offsets[0] must be 0");
+    for (uint32_t c = 0; c < e->C; ++c) {
+        if (job_offsets[c + 1] < job_offsets[c])
+            return fail(e, MCS_E_INVALID, "job_offsets must be non-decreasing");
+        if (job_offsets[c + 1] - job_offsets[c] > 0xFFFFFFFFull)
+            return fail(e, MCS_E_INVALID, "more than 2^32-1 jobs in one cluster");
+    }
+    return MCS_OK;
+}
+
+int mcs_submit_jobs(mcs_engine* e, const uint32_t* arrival_s, const uint32_t* dur_s,
+                    const uint32_t* cores, const uint32_t* mem, const uint64_t* job_offsets) {
+    if (int st = check_engine(e)) return st;
+    if (!e->has_clusters) return fail(e, MCS_E_STATE, "mcs_load_clusters first");
+    if (int st = check_job_offsets(e, job_offsets)) return st;
+    const uint64_t nj = job_offsets[e->C];
+    if (nj && (!arrival_s || !dur_s || !cores || !mem)) return fail(e, MCS_E_INVALID, "null job array");
+    for (uint32_t c = 0; c < e->C; ++c) { /* the ReadyQueue is filled in arrival order (server.go:41) */
+        /* the clock never passes the last arrival + sum(dur + 1): keep that inside uint32 (D8) */
+        uint64_t horizon = job_offsets[c + 1] > job_offsets[c] ? arrival_s[job_offsets[c + 1] - 1] : 0;
+        for (uint64_t i = job_offsets[c]; i < job_offsets[c + 1]; ++i) {
+            if (i > job_offsets[c] && arrival_s[i] < arrival_s[i - 1])
+                return fail(e, MCS_E_INVALID, "arrivals must be non-decreasing within a cluster");
+            horizon += (uint64_t)dur_s[i] + 1u;
+        }
+        if (horizon >= 0xFFFFFFFFull)
+            return fail(e, MCS_E_INVALID, "simulated clock could exceed 2^32-1 seconds");
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (int st = alloc_jobs(e, job_offsets)) return st;
+    std::vector<uint4> h(nj ? nj : 1);
+    for (uint64_t i = 0; i < nj; ++i) h[i] = make_uint4(arrival_s[i], dur_s[i], cores[i], mem[i]);
+    HIPCHK(e, hipMemcpy(e->d_jobs, h.data(), (nj ? nj : 1) * sizeof(uint4), hipMemcpyHostToDevice));
+    e->has_jobs = true;
+    return MCS_OK;
+}
+
+int mcs_generate_jobs(mcs_engine* e, const mcs_gen_params* p, uint64_t jobs_per_cluster) {
+    if (int st = check_engine(e)) return st;
+    if (!e->has_clusters) return fail(e, MCS_E_STATE, "mcs_load_clusters first");
+    if (!p || !(p->lambda > 0.0) || p->lambda > 128.0 || p->arrival_mode > 1u || p->max_dur_s == 0)
+        return fail(e, MCS_E_INVALID, "bad generator parameters");
+    if (jobs_per_cluster > 0xFFFFFFFFull) return fail(e, MCS_E_INVALID, "too many jobs per cluster");
+    std::vector<uint64_t> off(e->C + 1);
+    for (uint32_t c = 0; c <= e->C; ++c) off[c] = (uint64_t)c * jobs_per_cluster;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (int st = alloc_jobs(e, off.data())) return st;
+    const uint32_t* mc = e->d_max_c;
+    const uint32_t* mm = e->d_max_m;
+    std::vector<uint32_t> fixc, fixm;
+    uint32_t* tmp = nullptr;
+    if (p->max_cores || p->max_mem) { /* explicit maxima override setMaxCluster */
+        std::vector<uint32_t> hc(e->C), hm(e->C);
+        HIPCHK(e, hipMemcpy(hc.data(), e->d_max_c, e->C * 4, hipMemcpyDeviceToHost));
+        HIPCHK(e, hipMemcpy(hm.data(), e->d_max_m, e->C * 4, hipMemcpyDeviceToHost));
+        for (uint32_t c = 0; c < e->C; ++c) {
+            if (p->max_cores) hc[c] = p->max_cores;
+            if (p->max_mem) hm[c] = p->max_mem;
+        }
+        HIPCHK(e, hipMalloc(&tmp, 2 * e->C * sizeof(uint32_t)));
+        HIPCHK(e, hipMemcpy(tmp, hc.data(), e->C * 4, hipMemcpyHostToDevice));
+        HIPCHK(e, hipMemcpy(tmp + e->C, hm.data(), e->C * 4, hipMemcpyHostToDevice));
+        mc = tmp;
+        mm = tmp + e->C;
+    }
+    hipError_t st = mcs::launch_gen_attrs(e->d_jobs, e->d_job_off, mc, mm, e->C, p->seed,
+                                          p->max_dur_s, e->stream);
+    if (st == hipSuccess)
+        st = mcs::launch_gen_arrivals(e->d_jobs, e->d_job_off, e->C, p->seed, p->arrival_mode,
+                                      std::exp(-p->lambda), e->stream);
+    if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+    if (tmp) (void)hipFree(tmp);
+    if (st != hipSuccess)
+        return fail(e, MCS_E_HIP, std::string("job generation: ") + hipGetErrorString(st));
+    e->has_jobs = true;
+    return MCS_OK;
+}
+
+int mcs_read_jobs(mcs_engine* e, uint32_t* arrival_s, uint32_t* dur_s, uint32_t* cores,
+                  uint32_t* mem) {
+    if (int st = check_engine(e)) return st;
+    if (!e->has_jobs) return fail(e, MCS_E_STATE, "no jobs");
+    const uint64_t nj = e->total_jobs;
+    if (!nj) return MCS_OK;
+    if (!arrival_s || !dur_s || !cores || !mem) return fail(e, MCS_E_INVALID, "null output");
+    std::vector<uint4> h(nj);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(h.data(), e->d_jobs, nj * sizeof(uint4), hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < nj; ++i) {
+        arrival_s[i] = h[i].x;
+        dur_s[i] = h[i].y;
+        cores[i] = h[i].z;
+        mem[i] = h[i].w;
+    }
+    return MCS_OK;
+}
+
+int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
+    if (int st = check_engine(e)) return st;
+    if (!e->has_clusters || !e->has_jobs) return fail(e, MCS_E_STATE, "load clusters and jobs first");
+    if (t_end_s != MCS_TIME_NONE) return fail(e, MCS_E_INVALID, "finite horizons are reserved in ABI v1");
+    const auto w0 = std::chrono::steady_clock::now();
+    const int npl = npl_for(e->max_n ? e->max_n : 1);
+    int pool = e->cfg.slot_pool ? (int)e->cfg.slot_pool : auto_pool(e->max_n);
+    if (npl < 0) return fail(e, MCS_E_INVALID, "cluster too large");
+
+    mcs::FifoArgs a{};
+    a.node_free0 = e->d_free0;
+    a.node_off = e->d_node_off;
+    a.jobs = e->d_jobs;
+    a.job_off = e->d_job_off;
+    a.cluster_list = nullptr;
+    a.out_node = e->d_out_node;
+    a.out_start = e->d_out_start;
+    a.out_finish = e->d_out_finish;
+    a.cstats = e->d_cstats;
+    a.totals = e->d_totals;
+    a.n_items = e->C;
+
+    double kms = 0.0;
+    uint32_t escalations = 0;
+    int pool_used = pool;
+    HIPCHK(e, hipMemsetAsync(e->d_totals, 0, sizeof(mcs::Totals), e->stream));
+    mcs::Totals tot{};
+    for (;;) {
+        HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+        HIPCHK(e, mcs::launch_fifo(a, npl, pool, e->stream));
+        HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+        HIPCHK(e, hipMemcpyAsync(&tot, e->d_totals, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        float ms = 0.0f;
+        HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+        kms += ms;
+        pool_used = pool;
+        if (tot.overflowed == 0) break;
+        /* capacity escalation: re-run only the overflowed clusters with a doubled pool */
+        if (pool * 2 > mcs::kMaxPool)
+            return fail(e, MCS_E_CAPACITY, "running-slot pool overflow at 2048 slots per cluster");
+        std::vector<mcs_cluster_stats> cs(e->C);
+        HIPCHK(e, hipMemcpy(cs.data(), e->d_cstats, e->C * sizeof(mcs_cluster_stats),
+                            hipMemcpyDeviceToHost));
+        std::vector<uint32_t> list;
+        for (uint32_t c = 0; c < e->C; ++c)
+            if (cs[c].flags & MCS_FLAG_OVERFLOW) list.push_back(c);
+        HIPCHK(e, hipMemcpy(e->d_list, list.data(), list.size() * sizeof(uint32_t),
+                            hipMemcpyHostToDevice));
+        HIPCHK(e, hipMemsetAsync(&e->d_totals->overflowed, 0, sizeof(unsigned int), e->stream));
+        a.cluster_list = e->d_list;
+        a.n_items = (uint32_t)list.size();
+        pool *= 2;
+        ++escalations;
+    }
+    e->has_run = true;
+    if (stats) {
+        stats->jobs = e->total_jobs;
+        stats->placed = tot.placed;
+        stats->waited = tot.waited;
+        stats->unplaced = tot.unplaced;
+        stats->clusters = e->C;
+        stats->deadlocked = tot.deadlocked;
+        stats->escalations = escalations;
+        stats->slot_pool = (uint32_t)pool_used;
+        stats->kernel_ms = kms;
+        stats->wall_ms =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+    }
+    return MCS_OK;
+}
+
+int mcs_read_placements(mcs_engine* e, int32_t* node, uint32_t* start_s, uint32_t* finish_s) {
+    if (int st = check_engine(e)) return st;
+    if (!e->has_run) return fail(e, MCS_E_STATE, "mcs_run first");
+    const uint64_t nj = e->total_jobs;
+    if (!nj) return MCS_OK;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (node) HIPCHK(e, hipMemcpy(node, e->d_out_node, nj * 4, hipMemcpyDeviceToHost));
+    if (start_s) HIPCHK(e, hipMemcpy(start_s, e->d_out_start, nj * 4, hipMemcpyDeviceToHost));
+    if (finish_s) HIPCHK(e, hipMemcpy(finish_s, e->d_out_finish, nj * 4, hipMemcpyDeviceToHost));
+    return MCS_OK;
+}
+
+int mcs_read_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n_clusters) {
+    if (int st = check_engine(e)) return st;
+    if (!e->has_run) return fail(e, MCS_E_STATE, "mcs_run first");
+    if (!out || n_clusters > e->C) return fail(e, MCS_E_INVALID, "bad output");
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(out, e->d_cstats, n_clusters * sizeof(mcs_cluster_stats),
+                        hipMemcpyDeviceToHost));
+    return MCS_OK;
+}
+
+/* ---- single-job mirrors ------------------------------------------------------------------ */
+static int cluster_slice(mcs_engine* e, uint32_t cluster, uint32_t* n0, uint32_t* n) {
+    if (!e->has_clusters) return fail(e, MCS_E_STATE, "mcs_load_clusters first");
+    if (cluster >= e->C) return fail(e, MCS_E_INVALID, "cluster index out of range");
+    *n0 = e->node_off[cluster];
+    *n = e->node_off[cluster + 1] - *n0;
+    return MCS_OK;
+}
+
+int mcs_schedule_one(mcs_engine* e, uint32_t cluster, uint32_t cores, uint32_t mem,
+                     int32_t* node) {
+    if (int st = check_engine(e)) return st;
+    uint32_t n0, n;
+    if (int st = cluster_slice(e, cluster, &n0, &n)) return st;
+    if (!node) return fail(e, MCS_E_INVALID, "null node");
+    HIPCHK(e, mcs::launch_schedule_one(e->d_live_c + n0, e->d_live_m + n0, n, cores, mem,
+                                       e->d_scratch, e->stream));
+    HIPCHK(e, hipMemcpyAsync(node, e->d_scratch, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (*node < 0) {
+        *node = MCS_NODE_UNPLACED;
+        e->err = "not enough resources in cluster"; /* scheduler.go:138 */
+        return MCS_NO_FIT;
+    }
+    return MCS_OK;
+}
+
+int mcs_release_one(mcs_engine* e, uint32_t cluster, uint32_t node, uint32_t cores,
+                    uint32_t mem) {
+    if (int st = check_engine(e)) return st;
+    uint32_t n0, n;
+    if (int st = cluster_slice(e, cluster, &n0, &n)) return st;
+    if (node >= n) return fail(e, MCS_E_INVALID, "node index out of range");
+    uint32_t v[2];
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(&v[0], e->d_live_c + n0 + node, 4, hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpy(&v[1], e->d_live_m + n0 + node, 4, hipMemcpyDeviceToHost));
+    v[0] += cores; /* cluster.go:155-156 */
+    v[1] += mem;
+    HIPCHK(e, hipMemcpy(e->d_live_c + n0 + node, &v[0], 4, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_live_m + n0 + node, &v[1], 4, hipMemcpyHostToDevice));
+    return MCS_OK;
+}
+
+int mcs_lend_check(mcs_engine* e, uint32_t cluster, uint32_t cores, uint32_t mem, int32_t* ok) {
+    if (int st = check_engine(e)) return st;
+    uint32_t n0, n;
+    if (int st = cluster_slice(e, cluster, &n0, &n)) return st;
+    if (!ok) return fail(e, MCS_E_INVALID, "null ok");
+    HIPCHK(e, mcs::launch_lend_check(e->d_live_c + n0, e->d_live_m + n0, n, cores, mem,
+                                     e->d_scratch, e->stream));
+    HIPCHK(e, hipMemcpyAsync(ok, e->d_scratch, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return MCS_OK;
+}
+
+int mcs_read_live_state(mcs_engine* e, uint32_t cluster, uint32_t* free_c, uint32_t* free_m,
+                        uint32_t n_out) {
+    if (int st = check_engine(e)) return st;
+    uint32_t n0, n;
+    if (int st = cluster_slice(e, cluster, &n0, &n)) return st;
+    if (n_out < n || !free_c || !free_m) return fail(e, MCS_E_INVALID, "output too small");
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (n) {
+        HIPCHK(e, hipMemcpy(free_c, e->d_live_c + n0, n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(e, hipMemcpy(free_m, e->d_live_m + n0, n * 4, hipMemcpyDeviceToHost));
+    }
+    return MCS_OK;
+}
+
+int mcs_resource_utilization(mcs_engine* e, uint32_t cluster, float* core_util,
+                             float* mem_util) {
+    if (int st = check_engine(e)) return st;
+    uint32_t n0, n;
+    if (int st = cluster_slice(e, cluster, &n0, &n)) return st;
+    if (!core_util || !mem_util) return fail(e, MCS_E_INVALID, "null output");
+    float out[2];
+    HIPCHK(e, mcs::launch_utilization(e->d_cap + n0, e->d_live_c + n0, e->d_live_m + n0, n,
+                                      e->d_util, e->stream));
+    HIPCHK(e, hipMemcpyAsync(out, e->d_util, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    *core_util = out[0];
+    *mem_util = out[1];
+    return MCS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,59 @@
+// mcs_internal.h — device data layout shared by the kernels and the C-ABI engine (libmcs.so).
+//
+// HBM layout:
+//   jobs      uint4  {arrival_s, dur_s, cores, mem} per job, clusters contiguous (CSR job_off)  16 B/job
+//   out_node  int32  per job; out_start, out_finish uint32 per job (SoA)                      12 B/job
+//   node_free0 uint2 {free_c, free_m} per node (JSON CoresAvailable/MemoryAvailable), CSR node_off
+//   node_cap   uint2 {cores, memory} per node; live_c/live_m uint32 per node (single-job mirrors)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mcs.h"
+
+namespace mcs {
+
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;  // empty running slot (finish time never reached)
+constexpr int kWave = 64;
+constexpr int kMaxNpl = 16;   // nodes per lane -> at most 1024 nodes per cluster in ABI v1
+constexpr int kMaxPool = 32;  // running-slot registers per lane -> 2048 slots per cluster
+
+struct Totals {  // device-side accumulation of mcs_stats (only clusters that did not overflow)
+    unsigned long long placed;
+    unsigned long long waited;
+    unsigned long long unplaced;
+    unsigned int deadlocked;
+    unsigned int overflowed;
+};
+
+struct FifoArgs {
+    const uint2* node_free0;
+    const uint32_t* node_off;
+    const uint4* jobs;
+    const uint64_t* job_off;
+    const uint32_t* cluster_list;  // grid item -> cluster (nullptr = identity)
+    int32_t* out_node;
+    uint32_t* out_start;
+    uint32_t* out_finish;
+    mcs_cluster_stats* cstats;
+    Totals* totals;
+    uint32_t n_items;
+};
+
+// Launchers (mcs_kernels.hip).  Return hipSuccess or the launch error.
+hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, hipStream_t s);
+bool fifo_variant_exists(int npl, int pool);
+hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t* max_c,
+                            const uint32_t* max_m, uint32_t n_clusters, uint64_t seed,
+                            uint32_t max_dur, hipStream_t s);
+hipError_t launch_gen_arrivals(uint4* jobs, const uint64_t* job_off, uint32_t n_clusters,
+                               uint64_t seed, uint32_t mode, double exp_neg_lambda,
+                               hipStream_t s);
+hipError_t launch_schedule_one(uint32_t* live_c, uint32_t* live_m, uint32_t n, uint32_t c,
+                               uint32_t m, int32_t* out_node, hipStream_t s);
+hipError_t launch_lend_check(const uint32_t* live_c, const uint32_t* live_m, uint32_t n,
+                             uint32_t c, uint32_t m, int32_t* out_ok, hipStream_t s);
+hipError_t launch_utilization(const uint2* cap, const uint32_t* live_c, const uint32_t* live_m,
+                              uint32_t n, float* out2, hipStream_t s);
+
+}  // namespace mcs

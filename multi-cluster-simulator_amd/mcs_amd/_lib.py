@@ -1,0 +1,157 @@
+"""ctypes binding of libmcs.so (include/mcs.h).
+
+The library is loaded from this package directory (built in-tree by ``make`` /
+``__graft_entry__.build()``).  There is no fallback: if the library is missing, or no HIP device
+is usable, calls raise :class:`MCSError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmcs.so")
+
+MCS_OK = 0
+MCS_NO_FIT = 1
+MCS_E_INVALID = -1
+MCS_E_CAPACITY = -2
+MCS_E_HIP = -3
+MCS_E_RCCL = -4
+MCS_E_STATE = -5
+MCS_E_NOMEM = -6
+
+MCS_NODE_UNPLACED = -1
+MCS_TIME_NONE = 0xFFFFFFFF
+MCS_FLAG_DEADLOCK = 0x1
+MCS_FLAG_OVERFLOW = 0x2
+MCS_FLAG_CLOCK_OVERFLOW = 0x4
+
+MCS_POLICY_FIFO = 0
+MCS_POLICY_DELAY = 1
+MCS_ARRIVAL_REF = 0
+MCS_ARRIVAL_SCALED = 1
+
+STATUS_NAMES = {
+    MCS_OK: "MCS_OK",
+    MCS_NO_FIT: "MCS_NO_FIT",
+    MCS_E_INVALID: "MCS_E_INVALID",
+    MCS_E_CAPACITY: "MCS_E_CAPACITY",
+    MCS_E_HIP: "MCS_E_HIP",
+    MCS_E_RCCL: "MCS_E_RCCL",
+    MCS_E_STATE: "MCS_E_STATE",
+    MCS_E_NOMEM: "MCS_E_NOMEM",
+}
+
+
+class MCSError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        self.code = code
+        super().__init__(f"{STATUS_NAMES.get(code, code)}: {msg}")
+
+
+class mcs_config(C.Structure):
+    _fields_ = [
+        ("policy", C.c_uint32),
+        ("borrow", C.c_uint32),
+        ("trader", C.c_uint32),
+        ("wait_sleep_s", C.c_uint32),
+        ("idle_sleep_s", C.c_uint32),
+        ("slot_pool", C.c_uint32),
+        ("reserved", C.c_uint32 * 10),
+    ]
+
+
+class mcs_gen_params(C.Structure):
+    _fields_ = [
+        ("seed", C.c_uint64),
+        ("arrival_mode", C.c_uint32),
+        ("max_dur_s", C.c_uint32),
+        ("lambda_", C.c_double),
+        ("max_cores", C.c_uint32),
+        ("max_mem", C.c_uint32),
+        ("reserved", C.c_uint32 * 4),
+    ]
+
+
+class mcs_stats(C.Structure):
+    _fields_ = [
+        ("jobs", C.c_uint64),
+        ("placed", C.c_uint64),
+        ("waited", C.c_uint64),
+        ("unplaced", C.c_uint64),
+        ("clusters", C.c_uint32),
+        ("deadlocked", C.c_uint32),
+        ("escalations", C.c_uint32),
+        ("slot_pool", C.c_uint32),
+        ("kernel_ms", C.c_double),
+        ("wall_ms", C.c_double),
+    ]
+
+
+class mcs_cluster_stats(C.Structure):
+    _fields_ = [
+        ("t_end", C.c_uint32),
+        ("placed", C.c_uint32),
+        ("waited", C.c_uint32),
+        ("peak_running", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("pool", C.c_uint32),
+        ("reserved", C.c_uint32 * 2),
+    ]
+
+
+u32p = C.POINTER(C.c_uint32)
+i32p = C.POINTER(C.c_int32)
+u64p = C.POINTER(C.c_uint64)
+f32p = C.POINTER(C.c_float)
+vp = C.c_void_p
+
+# (name, restype, argtypes) for every symbol include/mcs.h declares
+SIGNATURES = [
+    ("mcs_abi_version", C.c_int, []),
+    ("mcs_config_default", None, [C.POINTER(mcs_config)]),
+    ("mcs_gen_params_default", None, [C.POINTER(mcs_gen_params)]),
+    ("mcs_gen_cluster_host", C.c_int,
+     [C.POINTER(mcs_gen_params), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, u32p, u32p, u32p, u32p]),
+    ("mcs_gen_scaled_lambda", C.c_double, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double]),
+    ("mcs_engine_create", C.c_int, [C.POINTER(mcs_config), C.c_int, C.POINTER(vp)]),
+    ("mcs_engine_destroy", C.c_int, [vp]),
+    ("mcs_last_error", C.c_char_p, [vp]),
+    ("mcs_load_clusters", C.c_int, [vp, u32p, u32p, u32p, u32p, u32p, C.c_uint32]),
+    ("mcs_submit_jobs", C.c_int, [vp, u32p, u32p, u32p, u32p, u64p]),
+    ("mcs_generate_jobs", C.c_int, [vp, C.POINTER(mcs_gen_params), C.c_uint64]),
+    ("mcs_read_jobs", C.c_int, [vp, u32p, u32p, u32p, u32p]),
+    ("mcs_run", C.c_int, [vp, C.c_uint32, C.POINTER(mcs_stats)]),
+    ("mcs_read_placements", C.c_int, [vp, i32p, u32p, u32p]),
+    ("mcs_read_cluster_stats", C.c_int, [vp, C.POINTER(mcs_cluster_stats), C.c_uint32]),
+    ("mcs_num_clusters", C.c_uint32, [vp]),
+    ("mcs_num_jobs", C.c_uint64, [vp]),
+    ("mcs_schedule_one", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32, i32p]),
+    ("mcs_release_one", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    ("mcs_lend_check", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32, i32p]),
+    ("mcs_read_live_state", C.c_int, [vp, C.c_uint32, u32p, u32p, C.c_uint32]),
+    ("mcs_resource_utilization", C.c_int, [vp, C.c_uint32, f32p, f32p]),
+]
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libmcs.so (once).  Raises MCSError if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MCSError(MCS_E_STATE, f"{LIB_PATH} not built (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def ptr(a, ct):
+    """numpy array -> ctypes pointer (the array must stay alive during the call)."""
+    return a.ctypes.data_as(C.POINTER(ct))

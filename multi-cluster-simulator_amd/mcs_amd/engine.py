@@ -1,0 +1,271 @@
+"""Python front end of the C ABI (include/mcs.h) — device-resident batched FIFO engine.
+
+Every compute call goes to libmcs.so (gfx950 kernels).  There is no CPU fallback: without the
+library or a HIP device the calls raise MCSError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+from .cluster import Cluster, ClusterArrays, pack_clusters
+
+
+def _check(eng_handle, rc: int):
+    if rc != L.MCS_OK:
+        msg = ""
+        if eng_handle:
+            m = L.lib().mcs_last_error(eng_handle)
+            msg = m.decode() if m else ""
+        raise L.MCSError(rc, msg)
+
+
+@dataclass
+class GenParams:
+    """mcs_gen_params (include/mcs.h); defaults restate pkg/client/client.go:85-147."""
+
+    seed: int = 0x4D43535F53494D31
+    arrival_mode: int = L.MCS_ARRIVAL_REF
+    max_dur_s: int = 600
+    lam: float = 10.0
+    max_cores: int = 0
+    max_mem: int = 0
+
+    def to_c(self) -> L.mcs_gen_params:
+        p = L.mcs_gen_params()
+        L.lib().mcs_gen_params_default(C.byref(p))
+        p.seed = self.seed & 0xFFFFFFFFFFFFFFFF
+        p.arrival_mode = self.arrival_mode
+        p.max_dur_s = self.max_dur_s
+        p.lambda_ = float(self.lam)
+        p.max_cores = self.max_cores
+        p.max_mem = self.max_mem
+        return p
+
+
+def scaled_lambda(n_nodes: int, node_mem: int = 24000, max_mem: int = 24000, max_dur_s: int = 600,
+                  load: float = 0.9) -> float:
+    """Per-second Poisson rate giving `load` offered memory load (SURVEY §8d 'scaled' mode)."""
+    return float(L.lib().mcs_gen_scaled_lambda(n_nodes, node_mem, max_mem, max_dur_s, load))
+
+
+def gen_cluster_host(params: GenParams, cluster: int, max_cores: int, max_mem: int, n_jobs: int):
+    """Host generator (bit-identical to the device generator).  Returns (arrival, dur, cores, mem)."""
+    a = np.empty(n_jobs, np.uint32)
+    d = np.empty(n_jobs, np.uint32)
+    c = np.empty(n_jobs, np.uint32)
+    m = np.empty(n_jobs, np.uint32)
+    p = params.to_c()
+    rc = L.lib().mcs_gen_cluster_host(C.byref(p), cluster, max_cores, max_mem, n_jobs,
+                                      L.ptr(a, C.c_uint32), L.ptr(d, C.c_uint32), L.ptr(c, C.c_uint32),
+                                      L.ptr(m, C.c_uint32))
+    _check(None, rc)
+    return a, d, c, m
+
+
+@dataclass
+class JobStreams:
+    """CSR job streams: jobs of cluster k are [job_off[k], job_off[k+1])."""
+
+    arrival: np.ndarray
+    dur: np.ndarray
+    cores: np.ndarray
+    mem: np.ndarray
+    job_off: np.ndarray
+
+    @property
+    def n_jobs(self) -> int:
+        return int(self.job_off[-1])
+
+    def of(self, k: int) -> slice:
+        return slice(int(self.job_off[k]), int(self.job_off[k + 1]))
+
+
+def gen_streams_host(params: GenParams, arrays: ClusterArrays, jobs_per_cluster: int) -> JobStreams:
+    n = arrays.n_clusters
+    tot = n * jobs_per_cluster
+    out = [np.empty(tot, np.uint32) for _ in range(4)]
+    for k in range(n):
+        sl = arrays.nodes_of(k)
+        mc = params.max_cores or int(arrays.cap_c[sl].max(initial=0))
+        mm = params.max_mem or int(arrays.cap_m[sl].max(initial=0))
+        a, d, c, m = gen_cluster_host(params, k, mc, mm, jobs_per_cluster)
+        s = slice(k * jobs_per_cluster, (k + 1) * jobs_per_cluster)
+        out[0][s], out[1][s], out[2][s], out[3][s] = a, d, c, m
+    off = np.arange(n + 1, dtype=np.uint64) * jobs_per_cluster
+    return JobStreams(out[0], out[1], out[2], out[3], off)
+
+
+@dataclass
+class RunStats:
+    jobs: int
+    placed: int
+    waited: int
+    unplaced: int
+    clusters: int
+    deadlocked: int
+    escalations: int
+    slot_pool: int
+    kernel_ms: float
+    wall_ms: float
+
+
+CLUSTER_STATS_DTYPE = np.dtype([("t_end", "<u4"), ("placed", "<u4"), ("waited", "<u4"),
+                                ("peak_running", "<u4"), ("flags", "<u4"), ("pool", "<u4"),
+                                ("reserved", "<u4", (2,))])
+
+
+class Engine:
+    """One engine = one GPU (mcs_engine_create(cfg, device))."""
+
+    def __init__(self, device: int = 0, slot_pool: int = 0):
+        cfg = L.mcs_config()
+        L.lib().mcs_config_default(C.byref(cfg))
+        cfg.slot_pool = slot_pool
+        h = C.c_void_p()
+        rc = L.lib().mcs_engine_create(C.byref(cfg), device, C.byref(h))
+        if rc != L.MCS_OK:
+            raise L.MCSError(rc, f"mcs_engine_create(device={device}) failed (is a HIP device visible?)")
+        self._h = h
+        self.device = device
+        self.arrays: Optional[ClusterArrays] = None
+        self.job_off: Optional[np.ndarray] = None
+
+    # -- lifecycle --------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib().mcs_engine_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _c(self, rc):
+        _check(self._h, rc)
+
+    # -- inputs -----------------------------------------------------------------------------
+    def load_clusters(self, clusters) -> ClusterArrays:
+        arr = clusters if isinstance(clusters, ClusterArrays) else pack_clusters(list(clusters))
+        cc = [np.ascontiguousarray(x, dtype=np.uint32) for x in (arr.cap_c, arr.cap_m, arr.free_c, arr.free_m)]
+        off = np.ascontiguousarray(arr.node_off, dtype=np.uint32)
+        self._c(L.lib().mcs_load_clusters(self._h, *[L.ptr(x, C.c_uint32) for x in cc],
+                                          L.ptr(off, C.c_uint32), arr.n_clusters))
+        self.arrays = arr
+        self.job_off = None
+        return arr
+
+    def submit_jobs(self, s: JobStreams):
+        a = [np.ascontiguousarray(x, dtype=np.uint32) for x in (s.arrival, s.dur, s.cores, s.mem)]
+        off = np.ascontiguousarray(s.job_off, dtype=np.uint64)
+        self._c(L.lib().mcs_submit_jobs(self._h, *[L.ptr(x, C.c_uint32) for x in a], L.ptr(off, C.c_uint64)))
+        self.job_off = off
+
+    def generate_jobs(self, params: GenParams, jobs_per_cluster: int):
+        p = params.to_c()
+        self._c(L.lib().mcs_generate_jobs(self._h, C.byref(p), jobs_per_cluster))
+        n = self.num_clusters
+        self.job_off = np.arange(n + 1, dtype=np.uint64) * jobs_per_cluster
+
+    def read_jobs(self) -> JobStreams:
+        n = self.num_jobs
+        out = [np.empty(n, np.uint32) for _ in range(4)]
+        self._c(L.lib().mcs_read_jobs(self._h, *[L.ptr(x, C.c_uint32) for x in out]))
+        return JobStreams(out[0], out[1], out[2], out[3], self.job_off.copy())
+
+    @property
+    def num_clusters(self) -> int:
+        return int(L.lib().mcs_num_clusters(self._h))
+
+    @property
+    def num_jobs(self) -> int:
+        return int(L.lib().mcs_num_jobs(self._h))
+
+    # -- the hot path ---------------------------------------------------------------------------
+    def run(self) -> RunStats:
+        st = L.mcs_stats()
+        self._c(L.lib().mcs_run(self._h, L.MCS_TIME_NONE, C.byref(st)))
+        return RunStats(st.jobs, st.placed, st.waited, st.unplaced, st.clusters, st.deadlocked,
+                        st.escalations, st.slot_pool, st.kernel_ms, st.wall_ms)
+
+    def placements(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        n = self.num_jobs
+        node = np.empty(n, np.int32)
+        start = np.empty(n, np.uint32)
+        fin = np.empty(n, np.uint32)
+        self._c(L.lib().mcs_read_placements(self._h, L.ptr(node, C.c_int32), L.ptr(start, C.c_uint32),
+                                            L.ptr(fin, C.c_uint32)))
+        return node, start, fin
+
+    def cluster_stats(self) -> np.ndarray:
+        n = self.num_clusters
+        out = np.zeros(n, CLUSTER_STATS_DTYPE)
+        self._c(L.lib().mcs_read_cluster_stats(self._h, out.ctypes.data_as(C.POINTER(L.mcs_cluster_stats)), n))
+        return out
+
+    # -- single-job mirrors (live state) --------------------------------------------------------
+    def schedule_one(self, cluster: int, cores: int, mem: int) -> int:
+        node = C.c_int32(-1)
+        rc = L.lib().mcs_schedule_one(self._h, cluster, cores, mem, C.byref(node))
+        if rc == L.MCS_NO_FIT:
+            return L.MCS_NODE_UNPLACED
+        self._c(rc)
+        return node.value
+
+    def release_one(self, cluster: int, node: int, cores: int, mem: int):
+        self._c(L.lib().mcs_release_one(self._h, cluster, node, cores, mem))
+
+    def lend_check(self, cluster: int, cores: int, mem: int) -> bool:
+        ok = C.c_int32(0)
+        self._c(L.lib().mcs_lend_check(self._h, cluster, cores, mem, C.byref(ok)))
+        return bool(ok.value)
+
+    def live_state(self, cluster: int):
+        sl = self.arrays.nodes_of(cluster)
+        n = sl.stop - sl.start
+        fc = np.empty(max(n, 1), np.uint32)
+        fm = np.empty(max(n, 1), np.uint32)
+        self._c(L.lib().mcs_read_live_state(self._h, cluster, L.ptr(fc, C.c_uint32), L.ptr(fm, C.c_uint32), n))
+        return fc[:n], fm[:n]
+
+    def resource_utilization(self, cluster: int) -> Tuple[float, float]:
+        cu = C.c_float()
+        mu = C.c_float()
+        self._c(L.lib().mcs_resource_utilization(self._h, cluster, C.byref(cu), C.byref(mu)))
+        return cu.value, mu.value
+
+
+def device_count() -> int:
+    """HIP devices visible to this process (via torch, which does not initialise the GPU)."""
+    try:
+        import torch
+
+        return int(torch.cuda.device_count())
+    except Exception:
+        return 0
+
+
+def algorithmic_bytes_per_placement() -> int:
+    """16 B job record read + 12 B result write."""
+    return 28
+
+
+def roofline_placements_per_s(peak_bytes_per_s: float = 8.0e12) -> float:
+    return peak_bytes_per_s / algorithmic_bytes_per_placement()
+
+
+__all__ = ["Engine", "GenParams", "JobStreams", "RunStats", "gen_cluster_host", "gen_streams_host",
+           "scaled_lambda", "device_count", "CLUSTER_STATS_DTYPE", "math"]

@@ -1,0 +1,92 @@
+/*
+ * mcs_oracle.h — CPU ORACLE for the MI355X engine.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and
+ * only as the checker (or the timed CPU baseline), never as the product path.
+ *
+ * It is a deliberately naive single-threaded restatement of the reference Go code
+ * (hamzalsheikh/multi-cluster-simulator @ 2024-10-16), following it function by function; every
+ * function cites the reference file:line it restates.  The semantics are SFIFO (SURVEY.md
+ * Appendix A): the Go FIFO loop with each goroutine step serialized, deviations D1-D9.
+ *
+ * PINNING: the reference has no tests, fixtures or golden vectors, and its Go toolchain and module
+ * cache are absent here, so it cannot be built or run.  This oracle is pinned by the
+ * hand-derived known-answer tests KAT1-KAT9 of SURVEY Appendix B (traced from the reference
+ * source), committed as tests/golden/kats.json.  Anything those KATs do not cover is
+ * "parity unpinned" against the Go binary itself.
+ */
+#ifndef MCS_ORACLE_H
+#define MCS_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_stats {
+    uint32_t t_end;
+    uint32_t placed;
+    uint32_t waited;
+    uint32_t peak_running;
+    uint32_t flags; /* 1 = deadlock */
+    uint32_t pad;
+    uint64_t ticks; /* loop iterations executed (literal mode: one per simulated second step) */
+} or_stats;
+
+/* FIFO run of ONE cluster.  Node arrays are the JSON order; jobs sorted by arrival.
+ * literal != 0 advances the clock one second per sleep exactly as the Go loop does
+ * (scheduler.go:250,289,294); literal == 0 uses the fast-forward of Appendix A.3.
+ * Outputs: node (-1 unplaced), start, finish (0xFFFFFFFF unplaced).  Returns 0. */
+int or_fifo_run(uint32_t n_nodes, const uint32_t* cap_c, const uint32_t* cap_m,
+                const uint32_t* free_c, const uint32_t* free_m, uint64_t n_jobs,
+                const uint32_t* arrival, const uint32_t* dur, const uint32_t* cores,
+                const uint32_t* mem, int literal, int32_t* out_node, uint32_t* out_start,
+                uint32_t* out_finish, or_stats* st);
+
+/* Many clusters (CSR offsets like mcs.h); n_threads > 1 uses OpenMP over clusters. */
+int or_fifo_run_batch(uint32_t n_clusters, const uint32_t* node_off, const uint32_t* cap_c,
+                      const uint32_t* cap_m, const uint32_t* free_c, const uint32_t* free_m,
+                      const uint64_t* job_off, const uint32_t* arrival, const uint32_t* dur,
+                      const uint32_t* cores, const uint32_t* mem, int n_threads,
+                      int32_t* out_node, uint32_t* out_start, uint32_t* out_finish,
+                      or_stats* st);
+
+/* Scheduler.ScheduleJob first-fit (scheduler.go:127-139): index or -1 (uint64 node counters). */
+int or_schedule_job(uint32_t n, const uint64_t* free_c, const uint64_t* free_m, uint64_t c,
+                    uint64_t m);
+/* Scheduler.Lend (scheduler.go:194-202): 1 when some node has strictly more of both. */
+int or_lend(uint32_t n, const uint64_t* free_c, const uint64_t* free_m, uint64_t c, uint64_t m);
+
+/* Cluster.GetResourceUtilization (cluster.go:46-63), float32 accumulation in node order. */
+void or_resource_utilization(uint32_t n, const uint64_t* cap_c, const uint64_t* cap_m,
+                             const uint64_t* free_c, const uint64_t* free_m, uint32_t total_c,
+                             uint32_t total_m, float* cu, float* mu);
+
+/* Trader.ApproveTrade (trader.go:141-167) with newTrader's approvePolicy (trader.go:47-52). */
+int or_approve_trade(uint32_t total_c, uint32_t total_m, float core_util, float mem_util,
+                     uint32_t req_cores, uint32_t req_mem, int64_t req_time_ns, float req_price);
+
+/* Go container/heap over contractResHeap (trader.go:169-191): push prices in order, then pop
+ * everything; writes the pop order (indices into prices[]). */
+void or_heap_order(uint32_t n, const float* prices, uint32_t* order);
+
+/* Cluster.AllocateVirtualNodeResources (cluster.go:87-125) on uint64 node counters.  Foreign jobs
+ * launched (go node.RunJob, cluster.go:116) are committed in place and reported (node, c, m);
+ * returns 0 on success, 1 for "couldn't schedule enough resources" (cluster.go:119-121). */
+int or_allocate_virtual_node(uint32_t n, uint64_t* free_c, uint64_t* free_m, uint32_t req_c,
+                             uint32_t req_m, uint32_t* n_foreign, uint32_t* f_node, uint64_t* f_c,
+                             uint64_t* f_m);
+
+/* calculateFastNodeSize (scheduler_client.go:126-170) / calculateSmallNodeSize (201-289) over a
+ * Level1 list delivered in ProvideJobs batches of 20 padded with zero jobs (trader_server.go:75-91,
+ * D9).  MaximimumCoreCost/MemoryCost = 0 and Budget = -1 as in newTrader (trader.go:34-35,53).
+ * Outputs cores, mem, time (ns), price. */
+void or_contract_fast(uint32_t n, const uint32_t* c, const uint32_t* m, const uint32_t* dur_s,
+                      uint32_t* oc, uint32_t* om, int64_t* otime_ns, float* oprice);
+void or_contract_small(uint32_t n, const uint32_t* c, const uint32_t* m, const uint32_t* dur_s,
+                       uint32_t* oc, uint32_t* om, int64_t* otime_ns, float* oprice);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

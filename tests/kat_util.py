@@ -1,0 +1,72 @@
+"""Helpers shared by the oracle and GPU parity tests."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+from mcs_amd import Cluster, JobStreams, pack_clusters, uniform_cluster
+from mcs_amd.engine import GenParams, gen_streams_host
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+UNPLACED_T = 0xFFFFFFFF
+
+
+def load_kats():
+    with open(os.path.join(GOLDEN, "kats.json")) as f:
+        return json.load(f)
+
+
+def kat_cluster(k) -> Cluster:
+    cl = Cluster.load(os.path.join(REPO, "assets", k["cluster"] + ".json"))
+    for idx, (fc, fm) in k.get("override_free", {}).items():
+        cl.Nodes[int(idx)].CoresAvailable = fc
+        cl.Nodes[int(idx)].MemoryAvailable = fm
+    return cl
+
+
+def kat_streams(k):
+    jobs = sorted(k["jobs"], key=lambda j: j[0])
+    n = len(jobs)
+    a = np.array([j[1] for j in jobs], np.uint32)
+    c = np.array([j[2] for j in jobs], np.uint32)
+    m = np.array([j[3] for j in jobs], np.uint32)
+    d = np.array([j[4] for j in jobs], np.uint32)
+    return JobStreams(a, d, c, m, np.array([0, n], np.uint64))
+
+
+def kat_expect(k):
+    n = len(k["jobs"])
+    node = np.zeros(n, np.int32)
+    st = np.zeros(n, np.uint32)
+    fi = np.zeros(n, np.uint32)
+    for sid, (nd, s, f) in k["expect"].items():
+        i = int(sid)
+        node[i], st[i], fi[i] = nd, s, f
+    return node, st, fi
+
+
+def seeded_workload(kind: str, n_clusters: int, jobs_per_cluster: int, seed: int = 0x4D43535F53494D31):
+    """Seeded synthetic workloads of BASELINE.json's configs at reduced sizes.
+    kind: 'small' (cluster_small, REF arrivals), 'big' (cluster_big, REF), 'n256' (256 nodes,
+    SCALED arrivals at 90% memory load), 'n256_hot' (256 nodes, 120% load: heavy waiting)."""
+    from mcs_amd.engine import scaled_lambda
+    from mcs_amd import replicate
+
+    if kind == "small":
+        spec, gp = Cluster.load(os.path.join(REPO, "assets", "cluster_small.json")), GenParams(seed=seed)
+    elif kind == "big":
+        spec, gp = Cluster.load(os.path.join(REPO, "assets", "cluster_big.json")), GenParams(seed=seed)
+    elif kind.startswith("n"):
+        parts = kind[1:].split("_")
+        nn = int(parts[0])
+        load = 1.2 if (len(parts) > 1 and parts[1] == "hot") else 0.9
+        spec = uniform_cluster(nn)
+        gp = GenParams(seed=seed, arrival_mode=1, lam=scaled_lambda(nn, load=load))
+    else:
+        raise ValueError(kind)
+    arrays = replicate(spec, n_clusters)
+    streams = gen_streams_host(gp, arrays, jobs_per_cluster)
+    return arrays, streams, gp

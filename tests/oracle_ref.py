@@ -1,0 +1,172 @@
+"""ctypes binding of the CPU ORACLE (oracle/libmcs_oracle.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this, and only as
+the checker / timed CPU baseline (see oracle/mcs_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "libmcs_oracle.so")
+
+
+class or_stats(C.Structure):
+    _fields_ = [("t_end", C.c_uint32), ("placed", C.c_uint32), ("waited", C.c_uint32),
+                ("peak_running", C.c_uint32), ("flags", C.c_uint32), ("pad", C.c_uint32),
+                ("ticks", C.c_uint64)]
+
+
+_lib = None
+u32p = C.POINTER(C.c_uint32)
+i32p = C.POINTER(C.c_int32)
+u64p = C.POINTER(C.c_uint64)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
+        L = C.CDLL(ORACLE_SO)
+        L.or_fifo_run.argtypes = [C.c_uint32, u32p, u32p, u32p, u32p, C.c_uint64, u32p, u32p, u32p, u32p,
+                                  C.c_int, i32p, u32p, u32p, C.POINTER(or_stats)]
+        L.or_fifo_run.restype = C.c_int
+        L.or_fifo_run_batch.argtypes = [C.c_uint32, u32p, u32p, u32p, u32p, u32p, u64p, u32p, u32p, u32p,
+                                        u32p, C.c_int, i32p, u32p, u32p, C.POINTER(or_stats)]
+        L.or_fifo_run_batch.restype = C.c_int
+        L.or_schedule_job.argtypes = [C.c_uint32, u64p, u64p, C.c_uint64, C.c_uint64]
+        L.or_schedule_job.restype = C.c_int
+        L.or_lend.argtypes = [C.c_uint32, u64p, u64p, C.c_uint64, C.c_uint64]
+        L.or_lend.restype = C.c_int
+        L.or_resource_utilization.argtypes = [C.c_uint32, u64p, u64p, u64p, u64p, C.c_uint32, C.c_uint32,
+                                              C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.or_resource_utilization.restype = None
+        L.or_approve_trade.argtypes = [C.c_uint32, C.c_uint32, C.c_float, C.c_float, C.c_uint32, C.c_uint32,
+                                       C.c_int64, C.c_float]
+        L.or_approve_trade.restype = C.c_int
+        L.or_heap_order.argtypes = [C.c_uint32, C.POINTER(C.c_float), u32p]
+        L.or_heap_order.restype = None
+        L.or_allocate_virtual_node.argtypes = [C.c_uint32, u64p, u64p, C.c_uint32, C.c_uint32, u32p, u32p,
+                                               u64p, u64p]
+        L.or_allocate_virtual_node.restype = C.c_int
+        for nm in ("or_contract_fast", "or_contract_small"):
+            f = getattr(L, nm)
+            f.argtypes = [C.c_uint32, u32p, u32p, u32p, u32p, u32p, C.POINTER(C.c_int64), C.POINTER(C.c_float)]
+            f.restype = None
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def fifo_run(free_c, free_m, arrival, dur, cores, mem, literal=False, cap_c=None, cap_m=None):
+    """One cluster.  Returns (node, start, finish, stats-dict)."""
+    free_c = np.ascontiguousarray(free_c, np.uint32)
+    free_m = np.ascontiguousarray(free_m, np.uint32)
+    cap_c = free_c if cap_c is None else np.ascontiguousarray(cap_c, np.uint32)
+    cap_m = free_m if cap_m is None else np.ascontiguousarray(cap_m, np.uint32)
+    a, d, c, m = (np.ascontiguousarray(x, np.uint32) for x in (arrival, dur, cores, mem))
+    n = len(a)
+    node = np.empty(max(n, 1), np.int32)
+    st = np.empty(max(n, 1), np.uint32)
+    fi = np.empty(max(n, 1), np.uint32)
+    s = or_stats()
+    lib().or_fifo_run(len(free_c), _p(cap_c, C.c_uint32), _p(cap_m, C.c_uint32), _p(free_c, C.c_uint32),
+                      _p(free_m, C.c_uint32), n, _p(a, C.c_uint32), _p(d, C.c_uint32), _p(c, C.c_uint32),
+                      _p(m, C.c_uint32), 1 if literal else 0, _p(node, C.c_int32), _p(st, C.c_uint32),
+                      _p(fi, C.c_uint32), C.byref(s))
+    stats = dict(t_end=s.t_end, placed=s.placed, waited=s.waited, peak_running=s.peak_running,
+                 flags=s.flags, ticks=s.ticks)
+    return node[:n], st[:n], fi[:n], stats
+
+
+def fifo_run_batch(arrays, streams, n_threads=1):
+    """Many clusters (CSR).  Returns (node, start, finish, stats structured array)."""
+    n = streams.n_jobs
+    node = np.empty(max(n, 1), np.int32)
+    st = np.empty(max(n, 1), np.uint32)
+    fi = np.empty(max(n, 1), np.uint32)
+    k = arrays.n_clusters
+    stats = (or_stats * k)()
+    cc = [np.ascontiguousarray(x, np.uint32) for x in (arrays.cap_c, arrays.cap_m, arrays.free_c, arrays.free_m)]
+    off = np.ascontiguousarray(arrays.node_off, np.uint32)
+    joff = np.ascontiguousarray(streams.job_off, np.uint64)
+    js = [np.ascontiguousarray(x, np.uint32) for x in (streams.arrival, streams.dur, streams.cores, streams.mem)]
+    lib().or_fifo_run_batch(k, _p(off, C.c_uint32), *[_p(x, C.c_uint32) for x in cc], _p(joff, C.c_uint64),
+                            *[_p(x, C.c_uint32) for x in js], n_threads, _p(node, C.c_int32),
+                            _p(st, C.c_uint32), _p(fi, C.c_uint32), stats)
+    sd = np.array([(s.t_end, s.placed, s.waited, s.peak_running, s.flags) for s in stats],
+                  dtype=[("t_end", "<u4"), ("placed", "<u4"), ("waited", "<u4"), ("peak_running", "<u4"),
+                         ("flags", "<u4")])
+    return node[:n], st[:n], fi[:n], sd
+
+
+def schedule_job(free_c, free_m, c, m):
+    fc = np.ascontiguousarray(free_c, np.uint64)
+    fm = np.ascontiguousarray(free_m, np.uint64)
+    return lib().or_schedule_job(len(fc), _p(fc, C.c_uint64), _p(fm, C.c_uint64), c, m)
+
+
+def lend(free_c, free_m, c, m):
+    fc = np.ascontiguousarray(free_c, np.uint64)
+    fm = np.ascontiguousarray(free_m, np.uint64)
+    return bool(lib().or_lend(len(fc), _p(fc, C.c_uint64), _p(fm, C.c_uint64), c, m))
+
+
+def resource_utilization(cap_c, cap_m, free_c, free_m):
+    arrs = [np.ascontiguousarray(x, np.uint64) for x in (cap_c, cap_m, free_c, free_m)]
+    tc = int(np.sum(np.asarray(cap_c, np.uint64))) & 0xFFFFFFFF
+    tm = int(np.sum(np.asarray(cap_m, np.uint64))) & 0xFFFFFFFF
+    cu = C.c_float()
+    mu = C.c_float()
+    lib().or_resource_utilization(len(arrs[0]), *[_p(x, C.c_uint64) for x in arrs], tc, tm, C.byref(cu),
+                                  C.byref(mu))
+    return cu.value, mu.value
+
+
+def approve_trade(total_c, total_m, cu, mu, cores, mem, time_ns, price):
+    return bool(lib().or_approve_trade(total_c, total_m, cu, mu, cores, mem, time_ns, price))
+
+
+def heap_order(prices):
+    p = np.ascontiguousarray(prices, np.float32)
+    o = np.empty(max(len(p), 1), np.uint32)
+    lib().or_heap_order(len(p), _p(p, C.c_float), _p(o, C.c_uint32))
+    return [int(x) for x in o[: len(p)]]
+
+
+def allocate_virtual_node(free_c, free_m, req_c, req_m):
+    fc = np.ascontiguousarray(free_c, np.uint64).copy()
+    fm = np.ascontiguousarray(free_m, np.uint64).copy()
+    n = len(fc)
+    nf = C.c_uint32()
+    fnode = np.empty(max(n, 1), np.uint32)
+    f_c = np.empty(max(n, 1), np.uint64)
+    f_m = np.empty(max(n, 1), np.uint64)
+    rc = lib().or_allocate_virtual_node(n, _p(fc, C.c_uint64), _p(fm, C.c_uint64), req_c, req_m, C.byref(nf),
+                                        _p(fnode, C.c_uint32), _p(f_c, C.c_uint64), _p(f_m, C.c_uint64))
+    k = nf.value
+    return rc, fc, fm, [(int(fnode[i]), int(f_c[i]), int(f_m[i])) for i in range(k)]
+
+
+def contract(kind, jobs):
+    """jobs: list of (cores, mem, dur_s).  kind 'fast' or 'small'."""
+    n = len(jobs)
+    c = np.ascontiguousarray([j[0] for j in jobs] or [0], np.uint32)
+    m = np.ascontiguousarray([j[1] for j in jobs] or [0], np.uint32)
+    d = np.ascontiguousarray([j[2] for j in jobs] or [0], np.uint32)
+    oc, om = C.c_uint32(), C.c_uint32()
+    ot = C.c_int64()
+    op = C.c_float()
+    f = lib().or_contract_fast if kind == "fast" else lib().or_contract_small
+    f(n, _p(c, C.c_uint32), _p(m, C.c_uint32), _p(d, C.c_uint32), C.byref(oc), C.byref(om), C.byref(ot),
+      C.byref(op))
+    return oc.value, om.value, ot.value, op.value

@@ -1,0 +1,105 @@
+"""CPU tests of the C-ABI library (no compute calls that need a GPU): it loads, exports exactly
+what include/mcs.h declares, the host generator is deterministic and has the reference
+distributions, and the spec loader follows Go's encoding/json rules."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import mcs_amd
+from mcs_amd import Cluster, GenParams, gen_cluster_host, scaled_lambda
+from mcs_amd import _lib as L
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "mcs.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(mcs_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_loads_and_exports_header_symbols():
+    lib = mcs_amd.lib()
+    declared = header_functions()
+    assert len(declared) >= 20
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = set(re.findall(r"\bT (mcs_[a-z0-9_]+)$", out.stdout, flags=re.M))
+    missing = [f for f in declared if f not in exported]
+    assert not missing, missing
+    # every declared function has a ctypes signature in the binding
+    bound = {name for name, _, _ in L.SIGNATURES}
+    assert set(declared) == bound
+    assert lib.mcs_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", L.LIB_PATH], capture_output=True, text=True)
+    blob = open(L.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_engine_create_without_device_fails_loudly():
+    # In this container there is no GPU: the engine must refuse, not fall back to the CPU.
+    import torch
+
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a device is visible")
+    with pytest.raises(mcs_amd.MCSError):
+        mcs_amd.Engine(0)
+
+
+def test_generator_deterministic_and_seeded():
+    gp = GenParams(seed=7)
+    a1 = gen_cluster_host(gp, 3, 32, 24000, 5000)
+    a2 = gen_cluster_host(gp, 3, 32, 24000, 5000)
+    for x, y in zip(a1, a2):
+        np.testing.assert_array_equal(x, y)
+    b = gen_cluster_host(gp, 4, 32, 24000, 5000)
+    assert not np.array_equal(a1[2], b[2])
+    # prefix property of the counter-based attributes
+    p = gen_cluster_host(gp, 3, 32, 24000, 1000)
+    for x, y in zip(p, a1):
+        np.testing.assert_array_equal(x, y[:1000])
+
+
+def test_generator_distributions_ref_mode():
+    a, d, c, m = gen_cluster_host(GenParams(seed=11), 0, 32, 24000, 200_000)
+    assert (np.diff(a.astype(np.int64)) >= 0).all()
+    assert c.max() <= 31 and m.max() <= 23999 and d.max() <= 599
+    # Beta(2,2): mean 1/2, variance 1/20
+    u = c / 32.0
+    assert abs(u.mean() - 0.5 + 1 / 64) < 0.01
+    v = m / 24000.0
+    assert abs(v.var() - 0.05) < 0.003
+    assert abs(d.mean() - 299.5) < 2.0
+    # Poisson(10) per minute with floor(60/n) spacing: ~ 10 jobs per <= 60 s minute
+    jobs_per_s = len(a) / (a[-1] + 1)
+    assert 0.16 < jobs_per_s < 0.20
+
+
+def test_generator_scaled_mode_rate():
+    lam = scaled_lambda(256, load=0.9)
+    assert 1.5 < lam < 1.6
+    a, d, c, m = gen_cluster_host(GenParams(seed=3, arrival_mode=1, lam=lam), 0, 32, 24000, 100_000)
+    rate = len(a) / (a[-1] + 1)
+    assert abs(rate - lam) / lam < 0.02
+
+
+def test_generator_rejects_bad_params():
+    with pytest.raises(mcs_amd.MCSError):
+        gen_cluster_host(GenParams(lam=0.0), 0, 32, 24000, 10)
+
+
+def test_cluster_json_go_rules(tmp_path):
+    cl = Cluster.load(os.path.join(REPO, "assets", "cluster_big.json"))
+    assert len(cl.Nodes) == 10 and cl.GetTotalResources() == (320, 240000)
+    # case-insensitive keys, unknown keys ignored, missing keys zero (encoding/json)
+    c2 = Cluster.from_json('{"id": 4, "nodes": [{"CORES": 8, "memory": 100, "coresavailable": 3, "x": 1}]}')
+    assert c2.Id == 4 and c2.Nodes[0].Cores == 8 and c2.Nodes[0].CoresAvailable == 3
+    assert c2.Nodes[0].MemoryAvailable == 0
+    with pytest.raises(ValueError):
+        Cluster.from_json('{"Id": 1, "Nodes": [{"Cores": -1}]}')

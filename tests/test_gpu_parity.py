@@ -1,0 +1,230 @@
+"""GPU parity: the gfx950 FIFO kernel (through the C ABI, libmcs.so) against the CPU oracle and the
+known-answer vectors.  Bit-exact on every field: node index, start and finish seconds, and the
+per-cluster statistics.  Run on a real MI355X: ``pytest -m gpu``.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ref as O
+from kat_util import kat_cluster, kat_expect, kat_streams, load_kats, seeded_workload
+from mcs_amd import (CLUSTER_STATS_DTYPE, Cluster, Engine, GenParams, JobStreams, pack_clusters, replicate,
+                     uniform_cluster)
+from mcs_amd import _lib as L
+from mcs_amd.engine import gen_streams_host
+
+pytestmark = pytest.mark.gpu
+KATS = load_kats()
+
+
+def run_engine(eng, arrays, streams):
+    eng.load_clusters(arrays)
+    eng.submit_jobs(streams)
+    st = eng.run()
+    node, start, fin = eng.placements()
+    return node, start, fin, st, eng.cluster_stats()
+
+
+def assert_parity(arrays, streams, node, start, fin, cstats, n_threads=8):
+    on, os_, of, osd = O.fifo_run_batch(arrays, streams, n_threads=n_threads)
+    bad = np.nonzero((node != on) | (start != os_) | (fin != of))[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at job {bad[:5]}: gpu {node[bad[:5]]},{start[bad[:5]]} " \
+                          f"oracle {on[bad[:5]]},{os_[bad[:5]]}"
+    for key in ("t_end", "placed", "waited", "peak_running", "flags"):
+        np.testing.assert_array_equal(cstats[key], osd[key], err_msg=key)
+
+
+@pytest.mark.parametrize("k", KATS["fifo"], ids=[k["name"] for k in KATS["fifo"]])
+def test_gpu_fifo_kats(engine, k):
+    arrays = pack_clusters([kat_cluster(k)])
+    node, start, fin, st, cs = run_engine(engine, arrays, kat_streams(k))
+    en, es, ef = kat_expect(k)
+    np.testing.assert_array_equal(node, en)
+    np.testing.assert_array_equal(start, es)
+    np.testing.assert_array_equal(fin, ef)
+    assert st.placed == int((en >= 0).sum())
+    assert st.unplaced == int((en < 0).sum())
+
+
+def test_gpu_kats_batched_in_one_launch(engine):
+    """All FIFO KATs as different clusters of ONE launch (independent waves)."""
+    ks = KATS["fifo"]
+    arrays = pack_clusters([kat_cluster(k) for k in ks])
+    parts = [kat_streams(k) for k in ks]
+    off = np.zeros(len(parts) + 1, np.uint64)
+    off[1:] = np.cumsum([p.n_jobs for p in parts])
+    s = JobStreams(*(np.concatenate([getattr(p, f) for p in parts]) for f in ("arrival", "dur", "cores", "mem")),
+                   off)
+    node, start, fin, st, cs = run_engine(engine, arrays, s)
+    for i, k in enumerate(ks):
+        en, es, ef = kat_expect(k)
+        js = s.of(i)
+        np.testing.assert_array_equal(node[js], en, err_msg=k["name"])
+        np.testing.assert_array_equal(start[js], es, err_msg=k["name"])
+    assert_parity(arrays, s, node, start, fin, cs)
+
+
+def test_scheduler_mirror_kat1():
+    from mcs_amd.scheduler import Job, Scheduler
+
+    k = KATS["fifo"][0]
+    s = Scheduler(device=0)
+    s.Run(kat_cluster(k))
+    jobs = [Job(Id=j[0], CoresNeeded=j[2], MemoryNeeded=j[3], Duration=j[4]) for j in k["jobs"]]
+    pl = s.Fifo([j[1] for j in k["jobs"]], jobs)
+    assert [(p.Node, p.Start, p.Finish) for p in pl] == [tuple(k["expect"][str(j[0])]) for j in k["jobs"]]
+    # single-job mirrors on the live state (scheduler.go:127-139, 194-202; cluster.go:46-63,153-157)
+    assert s.ScheduleJob(Job(CoresNeeded=20, MemoryNeeded=1000)) is None and s.LastNode() == 0
+    assert s.ScheduleJob(Job(CoresNeeded=20, MemoryNeeded=1000)) is None and s.LastNode() == 1
+    assert s.ScheduleJob(Job(CoresNeeded=33, MemoryNeeded=1)).Error() == "not enough resources in cluster"
+    assert s.Lend(Job(CoresNeeded=31, MemoryNeeded=23999)) is None
+    assert s.Lend(Job(CoresNeeded=32, MemoryNeeded=1)).Error() == "can't lend"
+    cu, mu = s.GetResourceUtilization()
+    ocu, omu = O.resource_utilization([32] * 5, [24000] * 5, [12, 12, 32, 32, 32], [23000, 23000] + [24000] * 3)
+    assert (np.float32(cu), np.float32(mu)) == (np.float32(ocu), np.float32(omu))
+    s.JobFinished(Job(CoresNeeded=20, MemoryNeeded=1000), 0)
+    fc, fm = s.engine.live_state(0)
+    assert list(fc) == [32, 12, 32, 32, 32] and list(fm) == [24000, 23000, 24000, 24000, 24000]
+    s.engine.close()
+
+
+def test_device_generator_matches_host(engine):
+    for kind, gp in (("small", GenParams(seed=42)),
+                     ("n256", GenParams(seed=43, arrival_mode=1, lam=1.5386))):
+        spec = Cluster.load(os.path.join(os.path.dirname(__file__), "..", "assets", "cluster_small.json")) \
+            if kind == "small" else uniform_cluster(256)
+        arrays = replicate(spec, 37)
+        engine.load_clusters(arrays)
+        engine.generate_jobs(gp, 3001)
+        dev = engine.read_jobs()
+        host = gen_streams_host(gp, arrays, 3001)
+        for f in ("arrival", "dur", "cores", "mem"):
+            np.testing.assert_array_equal(getattr(dev, f), getattr(host, f), err_msg=f"{kind}:{f}")
+
+
+def test_config1_cluster_small_10k(engine):
+    """BASELINE config 1 at its own size: cluster_small, FIFO, 10k seeded jobs."""
+    arrays, streams, _ = seeded_workload("small", 1, 10_000)
+    node, start, fin, st, cs = run_engine(engine, arrays, streams)
+    assert st.placed == 10_000
+    assert_parity(arrays, streams, node, start, fin, cs)
+
+
+def test_config2_cluster_big_1m(engine):
+    """BASELINE config 2 at full size: cluster_big, FIFO, 1M jobs, one cluster — bit-exact."""
+    arrays, streams, _ = seeded_workload("big", 1, 1_000_000)
+    node, start, fin, st, cs = run_engine(engine, arrays, streams)
+    assert st.placed == 1_000_000
+    assert_parity(arrays, streams, node, start, fin, cs)
+
+
+def test_config3_small_replicas(engine):
+    """BASELINE config 3 shape: 1024 cluster_small replicas (distinct seeds), 4k jobs each."""
+    arrays, streams, _ = seeded_workload("small", 1024, 4000)
+    node, start, fin, st, cs = run_engine(engine, arrays, streams)
+    assert st.placed == streams.n_jobs
+    assert_parity(arrays, streams, node, start, fin, cs)
+
+
+@pytest.mark.parametrize("kind", ["n256", "n256_hot"])
+def test_config4_shape_reduced(engine, kind):
+    """BASELINE config 4 shape (256 nodes, scaled arrivals) at 128 clusters x 6k jobs."""
+    arrays, streams, _ = seeded_workload(kind, 128, 6000)
+    node, start, fin, st, cs = run_engine(engine, arrays, streams)
+    assert_parity(arrays, streams, node, start, fin, cs)
+
+
+def test_config4_full_size_sampled_parity(engine):
+    """BASELINE config 4 at full size on one GPU: 4096 clusters x 256 nodes x 16384 jobs (64M
+    placements).  Clusters are independent, so bit-exact parity is checked on a sample of clusters
+    against the oracle, and size-independent properties on all of them."""
+    from mcs_amd.engine import scaled_lambda
+
+    n, J = 4096, 16384
+    arrays = replicate(uniform_cluster(256), n)
+    gp = GenParams(seed=0x4D43535F53494D31, arrival_mode=1, lam=scaled_lambda(256, load=0.9))
+    engine.load_clusters(arrays)
+    engine.generate_jobs(gp, J)
+    st = engine.run()
+    assert st.placed == n * J and st.unplaced == 0
+    node, start, fin = engine.placements()
+    jobs = engine.read_jobs()
+    cs = engine.cluster_stats()
+    # properties on everything
+    assert (node >= 0).all() and (node < 256).all()
+    np.testing.assert_array_equal(fin, start + jobs.dur)
+    assert (start >= jobs.arrival).all()
+    s2 = start.reshape(n, J).astype(np.int64)
+    assert (np.diff(s2, axis=1) >= 0).all()  # strict FIFO: starts non-decreasing in job order
+    assert (cs["placed"] == J).all()
+    # bit-exact on a sample of clusters
+    sample = [0, 1, 7, 513, 2047, 3000, 4095]
+    for k in sample:
+        js = jobs.of(k)
+        on, os_, of, ost = O.fifo_run(arrays.free_c[:256], arrays.free_m[:256], jobs.arrival[js], jobs.dur[js],
+                                      jobs.cores[js], jobs.mem[js])
+        np.testing.assert_array_equal(node[js], on, err_msg=f"cluster {k}")
+        np.testing.assert_array_equal(start[js], os_, err_msg=f"cluster {k}")
+        assert cs[k]["t_end"] == ost["t_end"] and cs[k]["waited"] == ost["waited"]
+
+
+def test_heterogeneous_cluster_sizes(engine):
+    """Clusters of 0..1024 nodes in one launch (variant chosen by the largest)."""
+    sizes = [0, 1, 5, 63, 64, 65, 200, 1024]
+    rng = np.random.default_rng(5)
+    clusters = []
+    for i, nn in enumerate(sizes):
+        cl = uniform_cluster(nn, cores=int(rng.integers(4, 64)), memory=int(rng.integers(1000, 50000)))
+        for nd in cl.Nodes:  # partial JSON availability (KAT5 rule)
+            nd.CoresAvailable = int(rng.integers(0, nd.Cores + 1))
+        clusters.append(cl)
+    arrays = pack_clusters(clusters)
+    parts = []
+    for i, cl in enumerate(clusters):
+        mc = max([nd.Cores for nd in cl.Nodes], default=8)
+        mm = max([nd.Memory for nd in cl.Nodes], default=1000)
+        from mcs_amd.engine import gen_cluster_host
+
+        parts.append(gen_cluster_host(GenParams(seed=77, arrival_mode=1, lam=0.02 * max(len(cl.Nodes), 1) + 0.2),
+                                      i, mc, mm, 1500))
+    off = np.arange(len(parts) + 1, dtype=np.uint64) * 1500
+    s = JobStreams(*(np.concatenate([p[f] for p in parts]) for f in range(4)), off)
+    node, start, fin, st, cs = run_engine(engine, arrays, s)
+    assert_parity(arrays, s, node, start, fin, cs)
+    assert cs[0]["flags"] & L.MCS_FLAG_DEADLOCK  # zero nodes: the first job never fits
+
+
+def test_slot_pool_escalation():
+    """Force the smallest pool (128 slots) with >128 concurrently running jobs: the engine must
+    detect the overflow, re-run those clusters with a larger pool, and still be bit-exact."""
+    eng = Engine(0, slot_pool=2)
+    arrays = replicate(uniform_cluster(5), 3)
+    n = 900
+    a = np.repeat(np.arange(n // 3, dtype=np.uint32), 3)[:n]
+    d = np.full(n, 400, np.uint32)
+    c = np.zeros(n, np.uint32)
+    m = np.ones(n, np.uint32)
+    s = JobStreams(np.tile(a, 3), np.tile(d, 3), np.tile(c, 3), np.tile(m, 3),
+                   np.arange(4, dtype=np.uint64) * n)
+    node, start, fin, st, cs = run_engine(eng, arrays, s)
+    assert st.escalations >= 1 and st.slot_pool > 2
+    assert_parity(arrays, s, node, start, fin, cs)
+    eng.close()
+
+
+def test_extreme_values(engine):
+    """uint32 needs and capacities near 2^32: comparisons are unsigned and exact."""
+    big = 0xFFFFFFF0
+    cl = Cluster(Id=1, Nodes=[])
+    from mcs_amd.cluster import Node
+
+    cl.Nodes = [Node(Id=1, Cores=big, Memory=big, CoresAvailable=big, MemoryAvailable=big),
+                Node(Id=2, Cores=big, Memory=big, CoresAvailable=big, MemoryAvailable=big)]
+    arrays = pack_clusters([cl])
+    jobs = [(0, big - 5, 7, 10), (0, 10, big, 3), (1, 6, 5, 0), (2, 1, 1, 2), (2, big, big, 1)]
+    s = JobStreams(np.array([j[0] for j in jobs], np.uint32), np.array([j[3] for j in jobs], np.uint32),
+                   np.array([j[1] for j in jobs], np.uint32), np.array([j[2] for j in jobs], np.uint32),
+                   np.array([0, len(jobs)], np.uint64))
+    node, start, fin, st, cs = run_engine(engine, arrays, s)
+    assert_parity(arrays, s, node, start, fin, cs, n_threads=1)
