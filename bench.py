@@ -46,13 +46,6 @@ def parse():
     return ap.parse_args()
 
 
-def rank_seed(seed: int, rank: int) -> int:
-    # distinct streams per rank: cluster k of rank r is keyed (seed ^ mix(r)) ^ k
-    z = (rank + 1) * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF
-    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
-    return seed ^ (z if rank else 0)
-
-
 def cpu_baseline(args, lam, n_threads):
     """The oracle (CPU restatement, deliberately naive, -O3) on a bounded sample of the same
     workload: the first cpu_sample_clusters clusters of rank 0, full job streams, OpenMP over
@@ -61,6 +54,7 @@ def cpu_baseline(args, lam, n_threads):
     import oracle_ref as O
     from mcs_amd import GenParams, replicate, uniform_cluster
     from mcs_amd.engine import gen_streams_host
+    from mcs_amd.shard import rank_seed
 
     k = min(args.cpu_sample_clusters, args.clusters)
     arrays = replicate(uniform_cluster(args.nodes), k)
@@ -99,6 +93,7 @@ def main():
 
     from mcs_amd import Engine, GenParams, replicate, uniform_cluster
     from mcs_amd.engine import scaled_lambda
+    from mcs_amd.shard import aggregate, rank_seed
 
     lam = scaled_lambda(args.nodes, load=args.load)
     eng = Engine(local_rank)
@@ -131,16 +126,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
 
-    t = torch.tensor([elapsed, float(placed)], dtype=torch.float64, device=dev)
-    if dist_on:
-        tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum[1:], op=dist.ReduceOp.SUM)
-        elapsed_max = float(tmax[0])
-        placed_all = float(tsum[1])
-    else:
-        elapsed_max, placed_all = elapsed, float(placed)
+    elapsed_max, placed_all = aggregate(elapsed, placed, device=dev)
 
     if rank == 0:
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3

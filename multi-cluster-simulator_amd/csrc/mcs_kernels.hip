@@ -245,11 +245,16 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         if (attempt) {
             const int k = first_fit(jc, jm);
             if (k >= 0) {
-                commit(k, jc, jm);
                 place(ji, k, t, t + jd);
-                if (jd != 0u && !insert(t + jd, jc, jm, (uint32_t)k)) {
-                    flags |= MCS_FLAG_OVERFLOW;
-                    break;
+                // A zero-duration job is committed and released before the next decision can
+                // read the node (RunJob sleeps 0; the release precedes the next branch, D3), so
+                // it leaves no trace on the cluster: only its fit test matters.
+                if (jd != 0u) {
+                    commit(k, jc, jm);
+                    if (!insert(t + jd, jc, jm, (uint32_t)k)) {
+                        flags |= MCS_FLAG_OVERFLOW;
+                        break;
+                    }
                 }
                 if (have_w) {       // WaitQueue = WaitQueue[1:] (:226; D1)
                     have_w = false;

@@ -1,0 +1,43 @@
+"""Multi-GPU sharding of independent clusters.
+
+Clusters are independent, so the data path has NO collective: each rank (one process per GPU)
+simulates its own shard.  torch.distributed is used only around the timed region (barrier, max of
+the elapsed time, sum of the placements).
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+M64 = 0xFFFFFFFFFFFFFFFF
+
+
+def rank_seed(seed: int, rank: int) -> int:
+    """Distinct job streams per rank for weak scaling: rank r keys its clusters with
+    seed ^ mix(r) (rank 0 keeps the base seed, so N=1 reproduces the single-GPU stream)."""
+    if rank == 0:
+        return seed & M64
+    z = ((rank + 1) * 0x9E3779B97F4A7C15) & M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    return (seed ^ z) & M64
+
+
+def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous block of clusters for strong scaling: [lo, hi), sizes differ by at most one."""
+    base, extra = divmod(total, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def aggregate(elapsed_s: float, placed: int, device=None) -> Tuple[float, float]:
+    """(max elapsed over ranks, total placements over ranks).  Without an initialised process
+    group returns the local values."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return float(elapsed_s), float(placed)
+    t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
+    p = torch.tensor([float(placed)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(p, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(p.item())

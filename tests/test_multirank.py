@@ -1,0 +1,71 @@
+"""The N>1 path on CPU: 2 ranks over gloo (127.0.0.1), each simulating its own shard of
+independent clusters with no data-path collective, then the bench aggregation (max elapsed, sum of
+placements).  The per-rank work is done by the oracle here (CPU); the GPU engine is the same call
+per rank on its own device."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from mcs_amd.shard import rank_seed, shard_range
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "multi-cluster-simulator_amd"), here]
+    import torch.distributed as dist
+
+    import oracle_ref as O
+    from mcs_amd import GenParams, replicate, uniform_cluster
+    from mcs_amd.engine import gen_streams_host
+    from mcs_amd.shard import aggregate, rank_seed
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    arrays = replicate(uniform_cluster(64), 4)
+    gp = GenParams(seed=rank_seed(123, rank), arrival_mode=1, lam=0.4)
+    streams = gen_streams_host(gp, arrays, 500)
+    node, st, fi, sd = O.fifo_run_batch(arrays, streams)
+    elapsed = 1.0 + rank  # synthetic per-rank time: the max must win
+    emax, ptot = aggregate(elapsed, int((node >= 0).sum()))
+    q.put((rank, emax, ptot, int(st.sum() % 1000003)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_shards_and_aggregation():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, e0, p0, h0), (r1, e1, p1, h1) = res
+    assert e0 == e1 == 2.0  # max over ranks
+    assert p0 == p1 == 2 * 4 * 500  # every job of both shards placed, summed over ranks
+    assert h0 != h1  # the two ranks simulated different streams
+
+
+def test_rank_seed_and_shard_range():
+    assert rank_seed(5, 0) == 5
+    assert len({rank_seed(5, r) for r in range(8)}) == 8
+    spans = [shard_range(4097, 8, r) for r in range(8)]
+    assert spans[0][0] == 0 and spans[-1][1] == 4097
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
