@@ -127,6 +127,14 @@ def main():
     elapsed = time.perf_counter() - t0
 
     elapsed_max, placed_all = aggregate(elapsed, placed, device=dev)
+    cs = eng.cluster_stats()  # outside the timed region: per-cluster decision-loop diagnostics
+    diag = {
+        "loop_passes_per_job": float(cs["iterations"].sum()) / max(n_jobs, 1),
+        "release_scans_per_job": float(cs["release_scans"].sum()) / max(n_jobs, 1),
+        "waited_frac": float(cs["waited"].sum()) / max(n_jobs, 1),
+        "peak_running_max": int(cs["peak_running"].max()),
+        "slot_pool": int(cs["pool"].max()),
+    }
 
     if rank == 0:
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
@@ -183,6 +191,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "slot_pool_escalations": escalations,
+            "diagnostics": diag,
         }
         print(json.dumps(out), flush=True)
 

@@ -124,7 +124,8 @@ typedef struct mcs_cluster_stats {
     uint32_t peak_running;  /* peak jobs holding resources (dur > 0)                              */
     uint32_t flags;         /* MCS_FLAG_*                                                         */
     uint32_t pool;          /* slot pool (x64) the final result was produced with                */
-    uint32_t reserved[2];
+    uint32_t iterations;    /* diagnostics: decision-loop passes                                  */
+    uint32_t release_scans; /* diagnostics: clock advances that released running jobs            */
 } mcs_cluster_stats;
 
 /* scheduler.Run (scheduler.go:101-124) builds a Scheduler; here one engine batches many clusters

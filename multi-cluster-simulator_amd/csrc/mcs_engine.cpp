@@ -99,10 +99,11 @@ int npl_for(uint32_t max_n) {
     return -1;
 }
 
-// Initial running-slot pool (registers per lane): room for ~4 running jobs per node, rounded to a
-// power of two in [2, 32].  Escalation doubles it for clusters that overflow.
+// Initial running-slot pool (slot rows of 64): room for ~2 running jobs per node, rounded to a
+// power of two in [2, 32] (the C4 workload peaks at ~1.7 per node).  Escalation doubles it for the
+// clusters that overflow, so the choice only trades occupancy against rare re-runs.
 int auto_pool(uint32_t max_n) {
-    const uint32_t want = (4u * max_n + 63u) / 64u;
+    const uint32_t want = (2u * max_n + 63u) / 64u;
     int p = 2;
     while ((uint32_t)p < want && p < mcs::kMaxPool) p *= 2;
     return p;

@@ -6,19 +6,27 @@
 // workgroup, under the serialized semantics SFIFO of SURVEY Appendix A with the exact fast-forward
 // of A.3.  Every decision is wave-uniform, so the wave never diverges on control flow:
 //
-//   * node free vectors live in VGPRs: lane l holds nodes l, l+64, ... (NPL nodes per lane);
-//     first fit = one v_cmp pair per 64-node chunk whose SGPR mask IS the ballot, then s_ff1;
-//   * the running set is a pool of 64*P slots (row p, lane l): finish times in VGPRs (one row per
-//     register), payload {cores, mem, node} in LDS as three [P][64] u32 arrays (lane-contiguous,
-//     bank-conflict-free); a free slot is found by ballot over finish == EMPTY;
-//   * releases at a clock advance are wave-parallel: every lane whose slot expired scatters its
-//     cores/mem into a per-node LDS accumulator with ds_add_u32 (order-free integer adds), and
-//     each node owner lane folds its accumulator back with one ds_wrxchg per chunk;
+//   * node free vectors are staged in LDS as packed u64 {free_c, free_m}, lane l owning nodes
+//     l, l+64, ... (NPL per lane); first fit = one ds_read_b64 per 64-node chunk, a per-lane
+//     lowest-fitting-node select and a DPP wave minimum (no LDS round trip, no SALU chain);
+//     commit is one ds_sub_u64 and a release one ds_add_u64 (the packed halves never borrow or
+//     carry because a placed job fits and resources are conserved);
+//   * the running set is a pool of 64*P slots (row p, lane l): finish times in VGPRs (one
+//     register per row, static indices only), payload {cores|mem, node} in LDS [P][64]
+//     (lane-contiguous, bank-conflict-free); a free slot is the lowest free row of the lowest
+//     lane that has one (ballot + ffbl);
+//   * releases at a clock advance are wave-parallel: each lane tests its P rows, then scatters
+//     its expired payloads into the node array with ds_add_u64 (order-free integer adds); the
+//     next completion time is a DPP wave minimum;
 //   * job records are streamed from HBM 64 at a time with one coalesced 16 B/lane load (uint4
 //     {arrival, dur, cores, mem}), double-buffered one batch ahead, and broadcast to the scalar
 //     unit with v_readlane;
 //   * results are gathered 64 jobs per register batch (placements happen in job order because
 //     FIFO head-of-line blocking is strict) and written with three coalesced 256 B stores.
+//
+// Codegen notes (measured with rocprofv3 SQ counters, profiles/): the kernel is issue-bound on
+// the CU's shared scalar unit and VALU, not on HBM.  Keeping node state in LDS and the loop
+// single-exit removed the whole-state register copies LLVM inserted at control-flow merges.
 //
 // Compiled with -ffp-contract=off (no FP in this file's hot kernel; the utilization mirror is
 // float32 and must round like Go).
@@ -32,42 +40,53 @@ __device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 
+// unsigned min over the wave with DPP row shifts and row broadcasts (no LDS round trip):
+// rows of 16 lanes are scanned with row_shr 1/2/4/8, then row_bcast:15 / row_bcast:31 carry the
+// row minima upward; lane 63 ends with the wave minimum.  Lanes with no DPP source keep `old` =
+// kEmpty, the identity of min.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_min_step(uint32_t v) {
+    const uint32_t w =
+        (uint32_t)__builtin_amdgcn_update_dpp((int)kEmpty, (int)v, CTRL, ROW_MASK, 0xf, false);
+    return w < v ? w : v;
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t w = (uint32_t)__shfl_xor((int)v, o);
-        v = w < v ? w : v;
-    }
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    v = dpp_min_step<0x111, 0xf>(v);  // row_shr:1
+    v = dpp_min_step<0x112, 0xf>(v);  // row_shr:2
+    v = dpp_min_step<0x114, 0xf>(v);  // row_shr:4
+    v = dpp_min_step<0x118, 0xf>(v);  // row_shr:8
+    v = dpp_min_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    v = dpp_min_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+    return readlane(v, 63);
 }
 
 template <int NPL, int P>
 __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
+    static_assert(P <= 32, "free-row mask is one u32 per lane");
     const uint32_t item = blockIdx.x;
     const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
     const uint32_t lane = threadIdx.x;
 
-    __shared__ uint32_t rel_c[NPL * kWave];  // release scatter accumulators, one per node
-    __shared__ uint32_t rel_m[NPL * kWave];
-    __shared__ uint32_t pay_c[P * kWave];    // running-slot payload, slot (p, l) at p*64 + l
-    __shared__ uint32_t pay_m[P * kWave];
-    __shared__ uint32_t pay_n[P * kWave];
+    // Node free vectors staged in LDS as packed u64 {free_c, free_m}: commit is one ds_sub_u64
+    // (the job fits, so the low half never borrows) and a release one ds_add_u64 (resources are
+    // conserved, so the low half never carries).  Node k lives at nodes[k]; nodes[NPL*64 + l] is
+    // lane l's write sink for lanes that do not commit.
+    __shared__ uint64_t nodes[(NPL + 1) * kWave];
+    __shared__ uint64_t pay_cm[(P + 1) * kWave];  // slot payload {cores, mem}; row P = write sink
+    __shared__ uint32_t pay_n[(P + 1) * kWave];   // slot node index
 
     // ---- cluster spec: Run() keeps the JSON availability (scheduler.go:101-109) ----
     const uint32_t n0 = a.node_off[ci];
     const uint32_t N = a.node_off[ci + 1] - n0;
-    uint32_t fc[NPL], fm[NPL];
-    uint64_t valid[NPL];
+    uint32_t nid[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
         const uint32_t idx = k * kWave + lane;
         uint2 v = make_uint2(0u, 0u);
         if (idx < N) v = a.node_free0[n0 + idx];
-        fc[k] = v.x;
-        fm[k] = v.y;
-        valid[k] = __ballot(idx < N);
-        rel_c[idx] = 0u;
-        rel_m[idx] = 0u;
+        nodes[idx] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        nid[k] = idx < N ? idx : kEmpty;  // node index, or never-fits for padding lanes
     }
 
     // ---- job stream ----
@@ -85,107 +104,48 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         return v;
     };
 
-    // running-slot finish times: row p of the pool in register sf[p] (static indices only)
+    // running-slot finish times: row p in register sf[p] (static indices only); frm = this lane's
+    // free rows (bit p)
     uint32_t sf[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) sf[p] = kEmpty;
+    uint32_t frm = (P == 32) ? 0xFFFFFFFFu : ((1u << P) - 1u);
 
     uint32_t cb = 0;
     uint4 cur = load_batch(0);
     uint4 nxt = load_batch(kWave);
 
     uint32_t t = 0, r = 0, minf = kEmpty, used = 0, peak = 0, waited = 0, placed = 0, flags = 0;
+    uint32_t n_iter = 0, n_rel = 0;  // diagnostics: loop passes, release scans
     bool have_w = false;
     uint32_t wi = 0, wc = 0, wm = 0, wd = 0;
     int32_t on = -1;
     uint32_t os = kEmpty, of = kEmpty;
 
-    // first fit — ScheduleJob, scheduler.go:129-137 (lowest node index with both >=)
-    auto first_fit = [&](uint32_t c, uint32_t m) __attribute__((always_inline)) -> int {
-#pragma unroll
-        for (int k = 0; k < NPL; ++k) {
-            const uint64_t hit = __ballot(fc[k] >= c && fm[k] >= m) & valid[k];
-            if (hit) return k * kWave + (int)__builtin_ctzll(hit);
-        }
-        return -1;
-    };
-
-    // commit — Node.RunJob, cluster.go:146-147 (synchronous, D2)
-    auto commit = [&](int k, uint32_t c, uint32_t m) __attribute__((always_inline)) {
-        const int kc = k >> 6;
-        const uint32_t kl = (uint32_t)(k & 63);
-#pragma unroll
-        for (int kk = 0; kk < NPL; ++kk) {
-            if (kk == kc && lane == kl) {
-                fc[kk] -= c;
-                fm[kk] -= m;
-            }
-        }
-    };
-
-    // running set insert (finish = start + Duration, cluster.go:151): first free slot in row-major
-    // order; the finish goes to its register row by a select (no dynamic register index), the
-    // payload to LDS by the one owning lane
-    auto insert = [&](uint32_t fin, uint32_t c, uint32_t m, uint32_t node)
-                      __attribute__((always_inline)) -> bool {
-        int ps = -1;
-        uint64_t e = 0;
-#pragma unroll
-        for (int p = P - 1; p >= 0; --p) {
-            const uint64_t b = __ballot(sf[p] == kEmpty);
-            if (b) {
-                ps = p;
-                e = b;
-            }
-        }
-        if (ps < 0) return false;
-        const uint32_t L = (uint32_t)__builtin_ctzll(e);
-        const bool me = lane == L;
-#pragma unroll
-        for (int p = 0; p < P; ++p) sf[p] = (me && p == ps) ? fin : sf[p];
-        if (me) {
-            const uint32_t a = (uint32_t)ps * kWave + L;
-            pay_c[a] = c;
-            pay_m[a] = m;
-            pay_n[a] = node;
-        }
-        ++used;
-        peak = used > peak ? used : peak;
-        minf = fin < minf ? fin : minf;
-        return true;
-    };
-
     // release every running job with finish <= t (cluster.go:153-157; A.2 step 1)
     auto release = [&]() __attribute__((always_inline)) {
-        if (minf > t) return;
-        uint32_t nexp = 0;
+        ++n_rel;
+        uint32_t xm = 0u;  // this lane's expired rows
+        uint32_t lm = kEmpty;
 #pragma unroll
         for (int p = 0; p < P; ++p) {
             const bool ex = sf[p] <= t;
-            const uint64_t b = __ballot(ex);
-            if (b) {
-                nexp += (uint32_t)__builtin_popcountll(b);
-                if (ex) {
-                    const uint32_t a = (uint32_t)p * kWave + lane;
-                    const uint32_t nd = pay_n[a];
-                    atomicAdd(&rel_c[nd], pay_c[a]);
-                    atomicAdd(&rel_m[nd], pay_m[a]);
-                }
-                sf[p] = ex ? kEmpty : sf[p];
+            xm |= ex ? (1u << p) : 0u;
+            sf[p] = ex ? kEmpty : sf[p];
+            lm = sf[p] < lm ? sf[p] : lm;
+        }
+        frm |= xm;
+        // give the expired payloads back to their nodes, one expired row per lane per pass
+        for (;;) {
+            const uint64_t b = __ballot(xm != 0u);
+            if (!b) break;
+            used -= (uint32_t)__builtin_popcountll(b);
+            if (xm != 0u) {
+                const uint32_t ad = (uint32_t)(__ffs(xm) - 1) * kWave + lane;
+                xm &= xm - 1u;
+                atomicAdd((unsigned long long*)&nodes[pay_n[ad]], (unsigned long long)pay_cm[ad]);
             }
         }
-        used -= nexp;
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#pragma unroll
-        for (int k = 0; k < NPL; ++k) {
-            if (valid[k]) {
-                fc[k] += atomicExch(&rel_c[k * kWave + lane], 0u);
-                fm[k] += atomicExch(&rel_m[k * kWave + lane], 0u);
-            }
-        }
-        uint32_t lm = kEmpty;
-#pragma unroll
-        for (int p = 0; p < P; ++p) lm = sf[p] < lm ? sf[p] : lm;
         minf = wave_min_u32(lm);
     };
 
@@ -198,68 +158,85 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         }
     };
 
-    auto place = [&](uint32_t ji, int k, uint32_t start, uint32_t fin) __attribute__((always_inline)) {
-        const uint32_t ol = ji & 63u;
-        if (lane == ol) {
-            on = k;
-            os = start;
-            of = fin;
-        }
-        ++placed;
-        if (ol == 63u) flush(ji - 63u);
-    };
-
     // ---- Scheduler.Fifo (scheduler.go:216-296) ----
-    // One pass = one decision.  Every helper has a single call site (one inlined copy each), and
-    // the clock only moves at the bottom, where the completions due by then are released.
-    for (;;) {
-        uint32_t tn = t;
-        bool attempt = true;
-        uint32_t ji, jc, jm, jd;
-        if (have_w) {  // len(WaitQueue) > 0, scheduler.go:219 -> ScheduleJob(WaitQueue[0]) :222
-            ji = wi;
-            jc = wc;
-            jm = wm;
-            jd = wd;
-        } else {
-            if (r >= J) break;
-            if (r - cb >= (uint32_t)kWave) {
-                cur = nxt;
-                cb += kWave;
-                nxt = load_batch(cb + kWave);
-            }
-            const uint32_t l = r - cb;
-            const uint32_t arr = readlane(cur.x, l);
-            // ReadyQueue head (:255-260); the job is in the queue once its arrival has passed
-            ji = r;
-            jd = readlane(cur.y, l);
-            jc = readlane(cur.z, l);
-            jm = readlane(cur.w, l);
-            if (arr > t) {  // all queues empty: 1 s sleeps until the arrival (:294, A.3)
-                tn = arr;
-                attempt = false;
-            } else {
-                ++r;
-            }
+    // One pass = one decision; the loop has a single exit (the structurizer then needs no flow
+    // copies of the loop-carried registers).
+    bool stop = false;
+    do {
+        ++n_iter;
+        // ReadyQueue head (:255-260): the next stream job, queued once its arrival has passed
+        if (!have_w && r - cb >= (uint32_t)kWave && r < J) {
+            cur = nxt;
+            cb += kWave;
+            nxt = load_batch(cb + kWave);
         }
-        if (attempt) {
-            const int k = first_fit(jc, jm);
-            if (k >= 0) {
-                place(ji, k, t, t + jd);
+        const uint32_t l = (r - cb) & 63u;
+        const uint32_t arr = readlane(cur.x, l);
+        // candidate: the wait head (:219-222) or the ready head
+        const uint32_t ji = have_w ? wi : r;
+        const uint32_t jd = have_w ? wd : readlane(cur.y, l);
+        const uint32_t jc = have_w ? wc : readlane(cur.z, l);
+        const uint32_t jm = have_w ? wm : readlane(cur.w, l);
+        uint32_t tn = t;
+        if (!have_w && r >= J) {  // every job decided
+            stop = true;
+        } else if (!have_w && arr > t) {  // all queues empty: 1 s sleeps to the arrival (:294)
+            tn = arr;
+        } else {
+            // first fit — ScheduleJob, scheduler.go:129-137: lowest node index with both >=;
+            // each lane keeps its lowest fitting node, then a DPP wave minimum
+            uint32_t best = kEmpty;
+#pragma unroll
+            for (int k = NPL - 1; k >= 0; --k) {
+                const uint64_t v = nodes[k * kWave + lane];
+                const uint32_t x = (uint32_t)v >= jc ? nid[k] : kEmpty;
+                best = (uint32_t)(v >> 32) >= jm ? (x < best ? x : best) : best;
+            }
+            const uint32_t k = wave_min_u32(best);
+            if (k != kEmpty) {
+                // placement record, 64 jobs per register batch (jobs are placed in job order)
+                const uint32_t ol = ji & 63u;
+                const uint32_t fin = t + jd;
+                const bool pme = lane == ol;
+                on = pme ? (int32_t)k : on;
+                os = pme ? t : os;
+                of = pme ? fin : of;
+                ++placed;
+                if (ol == 63u) flush(ji - 63u);
                 // A zero-duration job is committed and released before the next decision can
-                // read the node (RunJob sleeps 0; the release precedes the next branch, D3), so
-                // it leaves no trace on the cluster: only its fit test matters.
+                // read the node (RunJob sleeps 0; the release precedes the next branch, D3).
                 if (jd != 0u) {
-                    commit(k, jc, jm);
-                    if (!insert(t + jd, jc, jm, (uint32_t)k)) {
+                    const uint64_t need = (uint64_t)jc | ((uint64_t)jm << 32);
+                    // commit — Node.RunJob, cluster.go:146-147 (synchronous, D2)
+                    const uint32_t cad = lane == (k & 63u) ? k : NPL * kWave + lane;
+                    atomicSub((unsigned long long*)&nodes[cad], (unsigned long long)need);
+                    // slot insert: the lowest lane with a free row, its lowest free row
+                    const uint64_t any = __ballot(frm != 0u);
+                    if (!any) {
                         flags |= MCS_FLAG_OVERFLOW;
-                        break;
+                        stop = true;
+                    } else {
+                        const uint32_t L = (uint32_t)__builtin_ctzll(any);
+                        const bool ime = lane == L;
+                        uint32_t frme = ime ? (uint32_t)(__ffs(frm) - 1) : 0xFFu;
+                        asm volatile("" : "+v"(frme));  // keep the row test per-lane VALU
+#pragma unroll
+                        for (int p = 0; p < P; ++p) sf[p] = frme == (uint32_t)p ? fin : sf[p];
+                        frm = ime ? (frm & (frm - 1u)) : frm;
+                        const uint32_t ad = ime ? frme * kWave + lane : (uint32_t)P * kWave + lane;
+                        pay_cm[ad] = need;
+                        pay_n[ad] = k;
+                        ++used;
+                        peak = used > peak ? used : peak;
+                        minf = fin < minf ? fin : minf;
                     }
                 }
-                if (have_w) {       // WaitQueue = WaitQueue[1:] (:226; D1)
+                if (have_w) {     // WaitQueue = WaitQueue[1:] (:226; D1)
                     have_w = false;
-                    tn = t + 1u;    // time.Sleep(1 s) after every wait attempt (:250)
-                }                   // ready path: no sleep (:272)
+                    tn = t + 1u;  // time.Sleep(1 s) after every wait attempt (:250)
+                } else {
+                    ++r;          // ready path: no sleep (:272)
+                }
             } else {
                 if (!have_w) {  // State = WAITING; WaitQueue append (:264-268)
                     have_w = true;
@@ -268,26 +245,28 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                     wm = jm;
                     wd = jd;
                     ++waited;
-                    // The next pass of the Go loop retries the head at this same instant on an
-                    // unchanged cluster (certain to fail) before sleeping: folded in here.
+                    ++r;
+                    // The Go loop's next pass retries the new head at this same instant on an
+                    // unchanged cluster (certain to fail), then sleeps: folded in here.
                 }
-                // no lender without borrowing (:234, server.go:220)
                 if (minf == kEmpty) {  // nothing running: the head can never fit
                     flags |= MCS_FLAG_DEADLOCK;
-                    break;
+                    stop = true;
+                } else {  // A.3: 1 s retries until the next completion (no lender, :234)
+                    tn = minf > t + 1u ? minf : t + 1u;
                 }
-                tn = (minf > t + 1u) ? minf : t + 1u;  // A.3: 1 s retries until a completion
             }
         }
-        if (tn != t) {
+        if (!stop && tn != t) {
             if (tn < t) {  // the u32 seconds clock would wrap (D8 range exceeded): stop, flagged
                 flags |= MCS_FLAG_CLOCK_OVERFLOW;
-                break;
+                stop = true;
+            } else {
+                t = tn;
+                if (minf <= t) release();
             }
-            t = tn;
-            release();
         }
-    }
+    } while (!stop);
 
     if (flags & MCS_FLAG_DEADLOCK) {
         // jobs wi..J-1 are never placed (the Go loop retries the head forever)
@@ -315,8 +294,8 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         st.peak_running = peak;
         st.flags = flags;
         st.pool = (uint32_t)P;
-        st.reserved[0] = 0u;
-        st.reserved[1] = 0u;
+        st.iterations = n_iter;
+        st.release_scans = n_rel;
         a.cstats[ci] = st;
         if (flags & MCS_FLAG_OVERFLOW) {
             atomicAdd(&a.totals->overflowed, 1u);

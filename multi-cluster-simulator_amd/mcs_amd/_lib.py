@@ -97,7 +97,8 @@ class mcs_cluster_stats(C.Structure):
         ("peak_running", C.c_uint32),
         ("flags", C.c_uint32),
         ("pool", C.c_uint32),
-        ("reserved", C.c_uint32 * 2),
+        ("iterations", C.c_uint32),
+        ("release_scans", C.c_uint32),
     ]
 
 

@@ -117,7 +117,7 @@ class RunStats:
 
 CLUSTER_STATS_DTYPE = np.dtype([("t_end", "<u4"), ("placed", "<u4"), ("waited", "<u4"),
                                 ("peak_running", "<u4"), ("flags", "<u4"), ("pool", "<u4"),
-                                ("reserved", "<u4", (2,))])
+                                ("iterations", "<u4"), ("release_scans", "<u4")])
 
 
 class Engine:

@@ -12,6 +12,7 @@ OUT="$ROOT/gpurun_out/$TAG"
 mkdir -p "$OUT"
 cd "$ROOT"
 export PYTHONUNBUFFERED=1
+BENCH_ARGS="${BENCH_ARGS:-}"
 
 fatal() {  # rc of a GPU step -> 0 continue, 1 stop
     case "$1" in
@@ -39,18 +40,33 @@ for s in $STEPS; do
         echo "== rocprofv3 kernel trace"
         ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats \
             --output-format csv -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 \
-            --no-cpu-baseline ) > "$OUT/prof.log" 2>&1
+            --no-cpu-baseline $BENCH_ARGS ) > "$OUT/prof.log" 2>&1
         rc=$?; tail -5 "$OUT/prof.log"; echo "prof rc=$rc"
         find "$OUT/prof" -name "*stats*.csv" -exec sh -c 'echo "--- $1"; head -20 "$1"' _ {} \;
         fatal $rc || exit $rc ;;
     pmc)
-        echo "== rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE, LDS)"
-        for ctr in FETCH_SIZE WRITE_SIZE "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
-            name=$(echo "$ctr" | tr ' ' '_')
+        echo "== rocprofv3 PMC passes (one counter group per pass; no tracing domains combined)"
+        gi=0
+        for ctr in "FETCH_SIZE" "WRITE_SIZE" \
+                   "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES" \
+                   "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
+                   "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INST_CYCLES_SALU"; do
+            gi=$((gi+1))
             ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace \
-                --output-format csv -d "$OUT/pmc_$name" -o pmc -- python3 "$ROOT/bench.py" --steps 1 \
-                --warmup 0 --no-cpu-baseline ) > "$OUT/pmc_$name.log" 2>&1
-            rc=$?; tail -3 "$OUT/pmc_$name.log"; echo "pmc $name rc=$rc"; fatal $rc || exit $rc
+                --output-format csv -d "$OUT/pmc_g$gi" -o pmc -- python3 "$ROOT/bench.py" --steps 1 \
+                --warmup 0 --no-cpu-baseline $BENCH_ARGS ) > "$OUT/pmc_g$gi.log" 2>&1
+            rc=$?; tail -3 "$OUT/pmc_g$gi.log"; echo "pmc group $gi ($ctr) rc=$rc"; fatal $rc || exit $rc
+        done ;;
+    pmcq)
+        echo "== rocprofv3 PMC quick (instruction mix + wait states)"
+        gi=0
+        for ctr in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES" \
+                   "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
+            gi=$((gi+1))
+            ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace \
+                --output-format csv -d "$OUT/pmcq_g$gi" -o pmc -- python3 "$ROOT/bench.py" --steps 1 \
+                --warmup 0 --no-cpu-baseline $BENCH_ARGS ) > "$OUT/pmcq_g$gi.log" 2>&1
+            rc=$?; echo "pmcq group $gi rc=$rc"; fatal $rc || exit $rc
         done ;;
     *) echo "unknown step $s" ;;
     esac
