@@ -22,6 +22,29 @@ class or_stats(C.Structure):
                 ("ticks", C.c_uint64)]
 
 
+class or_trade_cfg(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("borrow", "trader", "period_s", "trade_ok_sleep_s",
+                                          "trade_fail_sleep_s", "lock_s", "sample_period_s", "t_max")]
+
+
+class or_lent_rec(C.Structure):
+    _fields_ = [("lender", C.c_uint32), ("borrower", C.c_uint32), ("job", C.c_uint64), ("node", C.c_uint32),
+                ("start", C.c_uint32), ("finish", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class or_trade_rec(C.Structure):
+    _fields_ = [("t", C.c_uint32), ("requester", C.c_uint32), ("winner", C.c_int32), ("approvals", C.c_uint32)]
+
+
+class or_trade_cluster_stats(C.Structure):
+    _fields_ = [("virtual_nodes", C.c_uint32), ("decided", C.c_uint32), ("lent_pending", C.c_uint32),
+                ("pad", C.c_uint32)]
+
+
+LENT_DTYPE = np.dtype([("lender", "<u4"), ("borrower", "<u4"), ("job", "<u8"), ("node", "<u4"),
+                       ("start", "<u4"), ("finish", "<u4"), ("pad", "<u4")])
+TRADE_DTYPE = np.dtype([("t", "<u4"), ("requester", "<u4"), ("winner", "<i4"), ("approvals", "<u4")])
+
 _lib = None
 u32p = C.POINTER(C.c_uint32)
 i32p = C.POINTER(C.c_int32)
@@ -59,6 +82,10 @@ def lib():
             f = getattr(L, nm)
             f.argtypes = [C.c_uint32, u32p, u32p, u32p, u32p, u32p, C.POINTER(C.c_int64), C.POINTER(C.c_float)]
             f.restype = None
+        L.or_trade_run.argtypes = [C.c_uint32, u32p, u32p, u32p, u32p, u32p, u64p, u32p, u32p, u32p, u32p,
+                                   C.POINTER(or_trade_cfg), i32p, u32p, u32p, C.c_void_p, C.c_uint64, u64p,
+                                   C.c_void_p, C.c_uint64, u64p, C.POINTER(or_trade_cluster_stats), u32p]
+        L.or_trade_run.restype = C.c_int
         _lib = L
     return _lib
 
@@ -170,3 +197,34 @@ def contract(kind, jobs):
     f(n, _p(c, C.c_uint32), _p(m, C.c_uint32), _p(d, C.c_uint32), C.byref(oc), C.byref(om), C.byref(ot),
       C.byref(op))
     return oc.value, om.value, ot.value, op.value
+
+
+def trade_run(arrays, streams, borrow=True, trader=True, t_max=0xFFFFFFFE, lent_cap=1 << 20, trade_cap=1 << 20,
+              period_s=10, trade_ok_sleep_s=240, trade_fail_sleep_s=120, lock_s=20, sample_period_s=5):
+    """Lock-step trading run (C5 semantics, oracle/mcs_oracle_trade.c).  Returns a dict with node,
+    start, finish (own jobs), lent (LENT_DTYPE records in execution order), trades (TRADE_DTYPE),
+    virtual_nodes, decided, lent_pending (per cluster) and t_final."""
+    n = streams.n_jobs
+    k = arrays.n_clusters
+    node = np.empty(max(n, 1), np.int32)
+    st = np.empty(max(n, 1), np.uint32)
+    fi = np.empty(max(n, 1), np.uint32)
+    lent = np.zeros(max(lent_cap, 1), LENT_DTYPE)
+    trades = np.zeros(max(trade_cap, 1), TRADE_DTYPE)
+    nl, nt, tf = C.c_uint64(), C.c_uint64(), C.c_uint32()
+    cs = (or_trade_cluster_stats * max(k, 1))()
+    cfg = or_trade_cfg(int(borrow), int(trader), period_s, trade_ok_sleep_s, trade_fail_sleep_s, lock_s,
+                       sample_period_s, t_max)
+    cc = [np.ascontiguousarray(x, np.uint32) for x in (arrays.cap_c, arrays.cap_m, arrays.free_c, arrays.free_m)]
+    off = np.ascontiguousarray(arrays.node_off, np.uint32)
+    joff = np.ascontiguousarray(streams.job_off, np.uint64)
+    js = [np.ascontiguousarray(x, np.uint32) for x in (streams.arrival, streams.dur, streams.cores, streams.mem)]
+    lib().or_trade_run(k, _p(off, C.c_uint32), *[_p(x, C.c_uint32) for x in cc], _p(joff, C.c_uint64),
+                       *[_p(x, C.c_uint32) for x in js], C.byref(cfg), _p(node, C.c_int32), _p(st, C.c_uint32),
+                       _p(fi, C.c_uint32), lent.ctypes.data, lent_cap, C.byref(nl), trades.ctypes.data, trade_cap,
+                       C.byref(nt), cs, C.byref(tf))
+    return dict(node=node[:n], start=st[:n], finish=fi[:n], lent=lent[: min(nl.value, lent_cap)].copy(),
+                n_lent=nl.value, trades=trades[: min(nt.value, trade_cap)].copy(), n_trades=nt.value,
+                virtual_nodes=np.array([c.virtual_nodes for c in cs[:k]], np.uint32),
+                decided=np.array([c.decided for c in cs[:k]], np.uint32),
+                lent_pending=np.array([c.lent_pending for c in cs[:k]], np.uint32), t_final=tf.value)
