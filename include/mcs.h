@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MCS_ABI_VERSION 1
+#define MCS_ABI_VERSION 2
 
 /* ---- status codes --------------------------------------------------------------------------- */
 typedef enum mcs_status {
@@ -45,12 +45,18 @@ typedef enum mcs_status {
  * cannot fit even on an empty cluster, so the reference's Fifo loop retries it forever,
  * scheduler.go:219-251).  start/finish are then MCS_TIME_NONE. */
 #define MCS_NODE_UNPLACED (-1)
+/* Node index written for a job moved to the BorrowedQueue (scheduler.go:237-242; mcs_trade.h):
+ * start = the borrow tick, finish = MCS_TIME_NONE; the lender's run is in mcs_read_lent. */
+#define MCS_NODE_BORROWED (-2)
 #define MCS_TIME_NONE 0xFFFFFFFFu
 
 /* per-cluster flag bits (mcs_cluster_stats.flags) */
 #define MCS_FLAG_DEADLOCK 0x1u /* head-of-line job can never fit; rest of the stream unplaced     */
 #define MCS_FLAG_OVERFLOW 0x2u /* running-slot pool overflow (engine re-runs with a larger pool)   */
 #define MCS_FLAG_CLOCK_OVERFLOW 0x4u /* the uint32 seconds clock would wrap; results after it invalid */
+#define MCS_FLAG_LENT_OVERFLOW 0x8u  /* a LentQueue exceeded lent_queue_cap (lock-step runs)          */
+#define MCS_FLAG_LOG_OVERFLOW 0x10u  /* lent/trade log capacity exceeded: records dropped, counts kept */
+#define MCS_FLAG_T_MAX 0x20u         /* lock-step run stopped at t_max_s with work left               */
 
 /* ---- configuration ------------------------------------------------------------------------- */
 typedef enum mcs_policy {
@@ -59,16 +65,24 @@ typedef enum mcs_policy {
 } mcs_policy;
 
 typedef struct mcs_config {
-    uint32_t policy;         /* mcs_policy; ABI v1 accepts MCS_POLICY_FIFO only                    */
-    uint32_t borrow;         /* FIFO cross-cluster borrow (server.go:160-248); must be 0 in v1     */
-    uint32_t trader;         /* trader offer exchange (trader.go:193-325); must be 0 in v1         */
+    uint32_t policy;         /* mcs_policy; MCS_POLICY_FIFO only                                    */
+    uint32_t borrow;         /* FIFO cross-cluster borrow (server.go:160-248; mcs_trade.h)          */
+    uint32_t trader;         /* trader offer exchange (trader.go:193-325; mcs_trade.h)              */
     uint32_t wait_sleep_s;   /* sleep after a wait-queue attempt, scheduler.go:250 (must be 1)     */
     uint32_t idle_sleep_s;   /* sleep when all queues are empty, scheduler.go:294 (must be 1)      */
-    uint32_t slot_pool;      /* initial running-slot pool per cluster in units of 64 (0 = auto)    */
-    uint32_t reserved[10];
+    uint32_t slot_pool;      /* running-slot pool per cluster in units of 64 (0 = auto)            */
+    /* lock-step trading cadences (used when borrow or trader is set; mcs_trade.h) */
+    uint32_t trader_period_s;    /* 10: time.Sleep(10 s) per monitor pass, trader.go:323            */
+    uint32_t trade_ok_sleep_s;   /* 240: after a successful trade, trader.go:297                    */
+    uint32_t trade_fail_sleep_s; /* 120: after a failed trade, trader.go:300                        */
+    uint32_t lock_s;             /* 20: responder contract lock, pkg/trader/server.go:48-57         */
+    uint32_t sample_period_s;    /* 5: scheduler state stream period, trader_server.go:44           */
+    uint32_t lent_queue_cap;     /* LentQueue entries per cluster (0 = 4096)                        */
+    uint32_t t_max_s;            /* stop the lock-step clock after this tick (0 = 0xFFFFFFFE)       */
+    uint32_t reserved[3];
 } mcs_config;
 
-/* Fills the reference defaults (FIFO, no borrow, no trader, 1 s sleeps). */
+/* Fills the reference defaults (FIFO, no borrow, no trader, 1 s sleeps, trader cadences above). */
 void mcs_config_default(mcs_config* cfg);
 
 /* ---- synthetic job stream (input synthesis; restates pkg/client/client.go:85-147) ----------- */
@@ -158,8 +172,9 @@ int mcs_read_jobs(mcs_engine* eng, uint32_t* arrival_s, uint32_t* dur_s, uint32_
 
 /* Runs the FIFO policy loop (Scheduler.Fifo, scheduler.go:216-296, over ScheduleJob
  * scheduler.go:127-139 and Node.RunJob cluster.go:141-161) for every cluster from its loaded spec
- * until every job is placed (t_end_s = MCS_TIME_NONE; other horizons are reserved in v1).
- * Serialized semantics SFIFO, SURVEY Appendix A. */
+ * until every job is placed (t_end_s = MCS_TIME_NONE; other horizons are reserved).
+ * Serialized semantics SFIFO, SURVEY Appendix A.  With cfg.borrow or cfg.trader set the clusters
+ * instead advance in lock-step with the borrow and trade exchanges (mcs_trade.h). */
 int mcs_run(mcs_engine* eng, uint32_t t_end_s, mcs_stats* stats);
 
 /* Per-job results of the last mcs_run, indexed like the submitted jobs. */

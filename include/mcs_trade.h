@@ -1,0 +1,109 @@
+/*
+ * mcs_trade.h — lock-step trading extension of the MI355X engine (libmcs.so): the FIFO borrow
+ * protocol and the per-cluster trader, batched over many clusters and sharded over GPUs.
+ *
+ * Replaces (reference snapshot 2024-10-16):
+ *   Scheduler.BorrowResources        pkg/scheduler/server.go:160-248  (borrow broadcast)
+ *   "/borrow" handler + Lend         pkg/scheduler/server.go:80-113, scheduler.go:194-202
+ *   LentQueue service in Fifo        pkg/scheduler/scheduler.go:277-290
+ *   Trader.RequestPolicyMonitor      pkg/trader/trader.go:280-325
+ *   Trader.Trade + contractResHeap   pkg/trader/trader.go:169-278
+ *   traderServer.RequestResource /
+ *   ApproveContract                  pkg/trader/server.go:31-85
+ *   ApproveTrade                     pkg/trader/trader.go:141-167
+ *   Start (state stream)             pkg/scheduler/trader_server.go:24-47
+ *   AddVirtualNode /
+ *   AllocateVirtualNodeResources     pkg/scheduler/cluster.go:65-125
+ * Semantics: the lock-step serialization of DESIGN.md §9 (tick T: scheduler steps, borrow
+ * exchange, state samples, trader rounds), bit-identical to oracle/mcs_oracle_trade.c.
+ *
+ * Sharding: the clusters are split in equal contiguous blocks over `world` engines (one per GPU,
+ * usually one process each).  Every tick needs three all-gathers of small fixed-size records.
+ * Two transports:
+ *   - RCCL (mcs_comm_unique_id on rank 0, shared out of band, then mcs_comm_init on every rank):
+ *     mcs_run drives the whole lock-step loop with ncclAllGather over xGMI;
+ *   - caller-driven (no communicator): the caller runs the ticks with mcs_trade_phase and moves
+ *     the bytes between ranks itself (any transport; tests use torch.distributed gloo).
+ * With world == 1 neither is needed: mcs_run keeps the exchange in HBM.
+ */
+#ifndef MCS_TRADE_H
+#define MCS_TRADE_H
+
+#include "mcs.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One lent-job execution: the lender ran the borrower's job (index within the BORROWER's stream)
+ * after accepting it on a /borrow request.  Every acceptor runs its own copy (server.go:232-237). */
+typedef struct mcs_lent_rec {
+    uint32_t lender, borrower; /* global cluster indices */
+    uint64_t job;              /* job index in the borrower's stream */
+    uint32_t node, start_s, finish_s, pad;
+} mcs_lent_rec;
+
+/* One trader round whose request policy broke (trader.go:288-303). */
+typedef struct mcs_trade_rec {
+    uint32_t t_s;       /* tick of the round */
+    uint32_t requester; /* global cluster index */
+    int32_t winner;     /* responder whose virtual node was received, -1 = "couldn't acquire resources" */
+    uint32_t approvals; /* approving responses pushed on the heap */
+} mcs_trade_rec;
+
+typedef struct mcs_trade_stats {
+    uint64_t placed;       /* own jobs placed locally */
+    uint64_t borrowed;     /* own jobs moved to the BorrowedQueue */
+    uint64_t waited;       /* own jobs that entered the WaitQueue */
+    uint64_t undecided;    /* own jobs neither placed nor borrowed (t_max reached) */
+    uint64_t lent_runs;    /* lent-job executions on this engine's clusters */
+    uint64_t lent_pending; /* LentQueue entries never run */
+    uint64_t trades;       /* trader rounds with a broken policy (all clusters, replicated) */
+    uint64_t trades_won;   /* ... that received a virtual node */
+    uint32_t ticks;        /* lock-step ticks executed (fast-forward skips idle seconds) */
+    uint32_t t_final;      /* last tick */
+    uint32_t flags;        /* OR of MCS_FLAG_* over clusters and logs */
+    uint32_t pad;
+    double kernel_ms;      /* device time of the lock-step loop (HIP events) */
+    double wall_ms;
+} mcs_trade_stats;
+
+/* ---- sharding and transport ------------------------------------------------------------------- */
+typedef struct mcs_comm_id {
+    char bytes[128]; /* ncclUniqueId */
+} mcs_comm_id;
+
+/* This engine holds clusters [rank*C, rank*C + C) of world*C (C = mcs_num_clusters).  Call after
+ * mcs_load_clusters; default is rank 0 of 1. */
+int mcs_set_shard(mcs_engine* eng, uint32_t rank, uint32_t world);
+/* RCCL transport: ncclGetUniqueId (rank 0) and ncclCommInitRank on this engine's device. */
+int mcs_comm_unique_id(mcs_comm_id* out);
+int mcs_comm_init(mcs_engine* eng, const mcs_comm_id* id);
+
+/* ---- caller-driven lock-step ---------------------------------------------------------------- */
+/* One tick is phases 0..3.  Phase p reads `in` (the all-gather, in rank order, of every rank's
+ * `out` of phase p-1; phase 0 takes no input) and writes this rank's slice for the next
+ * exchange.  Phase 3's input is the gathered phase-2 output; its `out` is empty.  Sizes per
+ * phase from mcs_trade_xfer_bytes.  *done becomes 1 (identically on every rank) after the phase 3
+ * that ends the run; keep calling phase 0..3 until then.  mcs_trade_begin resets the lock-step
+ * state; mcs_trade_end fills the stats and makes the results readable. */
+int mcs_trade_begin(mcs_engine* eng);
+int mcs_trade_xfer_bytes(mcs_engine* eng, uint32_t phase, uint64_t* in_bytes, uint64_t* out_bytes);
+int mcs_trade_phase(mcs_engine* eng, uint32_t phase, const void* in, uint64_t in_bytes, void* out,
+                    uint64_t out_bytes, uint32_t* done);
+int mcs_trade_end(mcs_engine* eng, mcs_stats* stats);
+
+/* ---- results (after mcs_run or mcs_trade_end) ---------------------------------------------- */
+int mcs_read_trade_stats(mcs_engine* eng, mcs_trade_stats* out);
+/* Lent runs executed by this engine's clusters, sorted by (start_s, lender, borrower, job).
+ * *n = total count (may exceed cap: then only cap records are written). */
+int mcs_read_lent(mcs_engine* eng, mcs_lent_rec* out, uint64_t cap, uint64_t* n);
+/* Trader rounds of ALL clusters in (t_s, requester) order (identical on every rank). */
+int mcs_read_trades(mcs_engine* eng, mcs_trade_rec* out, uint64_t cap, uint64_t* n);
+/* Zero-capacity virtual nodes received by each of the world*C clusters (AddVirtualNode). */
+int mcs_read_virtual_nodes(mcs_engine* eng, uint32_t* out, uint32_t n_total);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MCS_TRADE_H */

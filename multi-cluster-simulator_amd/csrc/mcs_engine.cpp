@@ -15,62 +15,11 @@
 #include <string>
 #include <vector>
 
+#include "mcs_engine_impl.h"
 #include "mcs_gen.h"
 #include "mcs_internal.h"
 
-struct mcs_engine {
-    mcs_config cfg{};
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    std::string err;
-
-    uint32_t C = 0;
-    uint32_t max_n = 0;
-    uint64_t total_nodes = 0, total_jobs = 0;
-    std::vector<uint32_t> node_off;
-    std::vector<uint64_t> job_off;
-
-    uint2* d_free0 = nullptr;
-    uint2* d_cap = nullptr;
-    uint32_t* d_node_off = nullptr;
-    uint32_t* d_live_c = nullptr;
-    uint32_t* d_live_m = nullptr;
-    uint32_t* d_max_c = nullptr;
-    uint32_t* d_max_m = nullptr;
-    uint4* d_jobs = nullptr;
-    uint64_t* d_job_off = nullptr;
-    int32_t* d_out_node = nullptr;
-    uint32_t* d_out_start = nullptr;
-    uint32_t* d_out_finish = nullptr;
-    mcs_cluster_stats* d_cstats = nullptr;
-    mcs::Totals* d_totals = nullptr;
-    uint32_t* d_list = nullptr;
-    int32_t* d_scratch = nullptr;
-    float* d_util = nullptr;
-    bool has_clusters = false, has_jobs = false, has_run = false;
-};
-
 namespace {
-
-int fail(mcs_engine* e, int code, const std::string& msg) {
-    if (e) e->err = msg;
-    return code;
-}
-
-#define HIPCHK(e, call)                                                                      \
-    do {                                                                                     \
-        hipError_t _st = (call);                                                             \
-        if (_st != hipSuccess)                                                               \
-            return fail((e), MCS_E_HIP,                                                      \
-                        std::string(#call) + ": " + hipGetErrorString(_st));                 \
-    } while (0)
-
-template <class T>
-void dfree(T*& p) {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-}
 
 void free_clusters(mcs_engine* e) {
     dfree(e->d_free0);
@@ -109,12 +58,6 @@ int auto_pool(uint32_t max_n) {
     return p;
 }
 
-int check_engine(mcs_engine* e) {
-    if (!e) return MCS_E_INVALID;
-    hipError_t st = hipSetDevice(e->device);
-    if (st != hipSuccess) return fail(e, MCS_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(st));
-    return MCS_OK;
-}
 
 }  // namespace
 
@@ -131,6 +74,13 @@ void mcs_config_default(mcs_config* cfg) {
     cfg->wait_sleep_s = 1; /* scheduler.go:250 */
     cfg->idle_sleep_s = 1; /* scheduler.go:294 */
     cfg->slot_pool = 0;
+    cfg->trader_period_s = 10;     /* trader.go:323 */
+    cfg->trade_ok_sleep_s = 240;   /* trader.go:297 */
+    cfg->trade_fail_sleep_s = 120; /* trader.go:300 */
+    cfg->lock_s = 20;              /* pkg/trader/server.go:49 */
+    cfg->sample_period_s = 5;      /* trader_server.go:44 */
+    cfg->lent_queue_cap = 0;
+    cfg->t_max_s = 0;
 }
 
 void mcs_gen_params_default(mcs_gen_params* p) {
@@ -173,10 +123,18 @@ int mcs_engine_create(const mcs_config* cfg, int device, mcs_engine** out) {
         c = *cfg;
     else
         mcs_config_default(&c);
-    if (c.policy != MCS_POLICY_FIFO || c.borrow != 0 || c.trader != 0 || c.wait_sleep_s != 1 ||
+    if (c.policy != MCS_POLICY_FIFO || c.borrow > 1 || c.trader > 1 || c.wait_sleep_s != 1 ||
         c.idle_sleep_s != 1)
-        return MCS_E_INVALID; /* ABI v1: FIFO, no borrow, no trader, reference sleeps */
-    if (c.slot_pool != 0 && !mcs::fifo_variant_exists(1, (int)c.slot_pool)) return MCS_E_INVALID;
+        return MCS_E_INVALID; /* FIFO with the reference sleeps */
+    if (c.borrow || c.trader) {
+        if (c.trader && (c.trader_period_s == 0 || c.sample_period_s == 0 || c.lock_s == 0))
+            return MCS_E_INVALID;
+        if (c.trader && c.trader_period_s % c.sample_period_s != 0)
+            return MCS_E_INVALID; /* rounds must fall on state samples */
+        if (c.slot_pool > 64) return MCS_E_INVALID; /* lock-step slots: 64 * slot_pool <= 4096 */
+    } else if (c.slot_pool != 0 && !mcs::fifo_variant_exists(1, (int)c.slot_pool)) {
+        return MCS_E_INVALID;
+    }
     mcs_engine* e = new (std::nothrow) mcs_engine();
     if (!e) return MCS_E_NOMEM;
     e->cfg = c;
@@ -202,6 +160,8 @@ int mcs_engine_destroy(mcs_engine* e) {
     if (!e) return MCS_E_INVALID;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    mcs::trade_free(e);
+    mcs::comm_free(e);
     free_clusters(e);
     free_jobs(e);
     dfree(e->d_totals);
@@ -240,6 +200,7 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
     HIPCHK(e, hipStreamSynchronize(e->stream));
     free_clusters(e);
     free_jobs(e);
+    mcs::trade_free(e);
     e->has_clusters = e->has_jobs = e->has_run = false;
     e->C = n_clusters;
     e->max_n = max_n;
@@ -289,6 +250,7 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
 
 static int alloc_jobs(mcs_engine* e, const uint64_t* job_offsets) {
     free_jobs(e);
+    mcs::trade_free(e);
     e->has_jobs = e->has_run = false;
     e->job_off.assign(job_offsets, job_offsets + e->C + 1);
     e->total_jobs = job_offsets[e->C];
@@ -370,11 +332,14 @@ int mcs_generate_jobs(mcs_engine* e, const mcs_gen_params* p, uint64_t jobs_per_
         mc = tmp;
         mm = tmp + e->C;
     }
+    /* clusters are keyed by their global index rank*C + c (mcs_set_shard), so a sharded system
+     * generates exactly the streams of the same system on one engine */
+    const uint32_t base = e->rank * e->C;
     hipError_t st = mcs::launch_gen_attrs(e->d_jobs, e->d_job_off, mc, mm, e->C, p->seed,
-                                          p->max_dur_s, e->stream);
+                                          p->max_dur_s, base, e->stream);
     if (st == hipSuccess)
         st = mcs::launch_gen_arrivals(e->d_jobs, e->d_job_off, e->C, p->seed, p->arrival_mode,
-                                      std::exp(-p->lambda), e->stream);
+                                      std::exp(-p->lambda), base, e->stream);
     if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
     if (tmp) (void)hipFree(tmp);
     if (st != hipSuccess)
@@ -405,7 +370,9 @@ int mcs_read_jobs(mcs_engine* e, uint32_t* arrival_s, uint32_t* dur_s, uint32_t*
 int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     if (int st = check_engine(e)) return st;
     if (!e->has_clusters || !e->has_jobs) return fail(e, MCS_E_STATE, "load clusters and jobs first");
-    if (t_end_s != MCS_TIME_NONE) return fail(e, MCS_E_INVALID, "finite horizons are reserved in ABI v1");
+    if (t_end_s != MCS_TIME_NONE) return fail(e, MCS_E_INVALID, "finite horizons are reserved");
+    if (e->cfg.borrow || e->cfg.trader) return mcs::trade_run(e, stats);
+    e->trade_run = false;
     const auto w0 = std::chrono::steady_clock::now();
     const int npl = npl_for(e->max_n ? e->max_n : 1);
     int pool = e->cfg.slot_pool ? (int)e->cfg.slot_pool : auto_pool(e->max_n);
@@ -490,6 +457,7 @@ int mcs_read_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n_clu
     if (int st = check_engine(e)) return st;
     if (!e->has_run) return fail(e, MCS_E_STATE, "mcs_run first");
     if (!out || n_clusters > e->C) return fail(e, MCS_E_INVALID, "bad output");
+    if (e->trade_run) return mcs::trade_cluster_stats(e, out, n_clusters);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipMemcpy(out, e->d_cstats, n_clusters * sizeof(mcs_cluster_stats),
                         hipMemcpyDeviceToHost));

@@ -1,0 +1,84 @@
+// mcs_engine_impl.h — the engine handle behind the C ABI (mcs.h, mcs_trade.h), shared by the
+// FIFO engine (mcs_engine.cpp) and the lock-step trading path (mcs_trade.cpp).  Host code.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/mcs_trade.h"
+#include "mcs_internal.h"
+
+namespace mcs {
+struct TradeDev;  // mcs_trade.cpp
+void trade_free(mcs_engine* e);
+void comm_free(mcs_engine* e);
+int trade_run(mcs_engine* e, mcs_stats* stats);
+int trade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n_clusters);
+}  // namespace mcs
+
+struct mcs_engine {
+    mcs_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+
+    uint32_t C = 0;
+    uint32_t max_n = 0;
+    uint64_t total_nodes = 0, total_jobs = 0;
+    std::vector<uint32_t> node_off;
+    std::vector<uint64_t> job_off;
+
+    uint2* d_free0 = nullptr;
+    uint2* d_cap = nullptr;
+    uint32_t* d_node_off = nullptr;
+    uint32_t* d_live_c = nullptr;
+    uint32_t* d_live_m = nullptr;
+    uint32_t* d_max_c = nullptr;
+    uint32_t* d_max_m = nullptr;
+    uint4* d_jobs = nullptr;
+    uint64_t* d_job_off = nullptr;
+    int32_t* d_out_node = nullptr;
+    uint32_t* d_out_start = nullptr;
+    uint32_t* d_out_finish = nullptr;
+    mcs_cluster_stats* d_cstats = nullptr;
+    mcs::Totals* d_totals = nullptr;
+    uint32_t* d_list = nullptr;
+    int32_t* d_scratch = nullptr;
+    float* d_util = nullptr;
+    bool has_clusters = false, has_jobs = false, has_run = false;
+    // sharding (mcs_set_shard) and the lock-step trading state (mcs_trade.cpp)
+    uint32_t rank = 0, world = 1;
+    void* comm = nullptr;  // ncclComm_t
+    mcs::TradeDev* td = nullptr;
+    bool trade_run = false;  // results of the last run come from the lock-step path
+    uint32_t tr_lq = 0, tr_slots = 0;  // capacity escalation of the lock-step path (0 = auto)
+};
+
+inline int fail(mcs_engine* e, int code, const std::string& msg) {
+    if (e) e->err = msg;
+    return code;
+}
+
+#define HIPCHK(e, call)                                                                      \
+    do {                                                                                     \
+        hipError_t _st = (call);                                                             \
+        if (_st != hipSuccess)                                                               \
+            return fail((e), MCS_E_HIP,                                                      \
+                        std::string(#call) + ": " + hipGetErrorString(_st));                 \
+    } while (0)
+
+template <class T>
+inline void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+
+inline int check_engine(mcs_engine* e) {
+    if (!e) return MCS_E_INVALID;
+    hipError_t st = hipSetDevice(e->device);
+    if (st != hipSuccess) return fail(e, MCS_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(st));
+    return MCS_OK;
+}

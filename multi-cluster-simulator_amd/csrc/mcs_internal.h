@@ -45,10 +45,10 @@ hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, hipStream_t s);
 bool fifo_variant_exists(int npl, int pool);
 hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t* max_c,
                             const uint32_t* max_m, uint32_t n_clusters, uint64_t seed,
-                            uint32_t max_dur, hipStream_t s);
+                            uint32_t max_dur, uint32_t cluster_base, hipStream_t s);
 hipError_t launch_gen_arrivals(uint4* jobs, const uint64_t* job_off, uint32_t n_clusters,
                                uint64_t seed, uint32_t mode, double exp_neg_lambda,
-                               hipStream_t s);
+                               uint32_t cluster_base, hipStream_t s);
 hipError_t launch_schedule_one(uint32_t* live_c, uint32_t* live_m, uint32_t n, uint32_t c,
                                uint32_t m, int32_t* out_node, hipStream_t s);
 hipError_t launch_lend_check(const uint32_t* live_c, const uint32_t* live_m, uint32_t n,

@@ -33,33 +33,9 @@
 #define MCS_GEN_FN __host__ __device__ static inline
 #include "mcs_gen.h"
 #include "mcs_internal.h"
+#include "mcs_wave.h"
 
 namespace mcs {
-
-__device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
-}
-
-// unsigned min over the wave with DPP row shifts and row broadcasts (no LDS round trip):
-// rows of 16 lanes are scanned with row_shr 1/2/4/8, then row_bcast:15 / row_bcast:31 carry the
-// row minima upward; lane 63 ends with the wave minimum.  Lanes with no DPP source keep `old` =
-// kEmpty, the identity of min.
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint32_t dpp_min_step(uint32_t v) {
-    const uint32_t w =
-        (uint32_t)__builtin_amdgcn_update_dpp((int)kEmpty, (int)v, CTRL, ROW_MASK, 0xf, false);
-    return w < v ? w : v;
-}
-
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-    v = dpp_min_step<0x111, 0xf>(v);  // row_shr:1
-    v = dpp_min_step<0x112, 0xf>(v);  // row_shr:2
-    v = dpp_min_step<0x114, 0xf>(v);  // row_shr:4
-    v = dpp_min_step<0x118, 0xf>(v);  // row_shr:8
-    v = dpp_min_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
-    v = dpp_min_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
-    return readlane(v, 63);
-}
 
 template <int NPL, int P>
 __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
@@ -349,10 +325,10 @@ hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, hipStream_t s) {
 __global__ __launch_bounds__(256) void gen_attrs_kernel(uint4* jobs, const uint64_t* job_off,
                                                        const uint32_t* max_c,
                                                        const uint32_t* max_m, uint64_t seed,
-                                                       uint32_t max_dur) {
+                                                       uint32_t max_dur, uint32_t base) {
     const uint32_t c = blockIdx.y;
     const uint64_t j0 = job_off[c], J = job_off[c + 1] - j0;
-    const uint64_t key = mcs_cluster_key(seed, c);
+    const uint64_t key = mcs_cluster_key(seed, base + c);  // keyed by the global cluster index
     const uint32_t mc = max_c[c], mm = max_m[c];
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < J;
          i += (uint64_t)gridDim.x * blockDim.x) {
@@ -364,11 +340,11 @@ __global__ __launch_bounds__(256) void gen_attrs_kernel(uint4* jobs, const uint6
 
 __global__ __launch_bounds__(64) void gen_arrivals_kernel(uint4* jobs, const uint64_t* job_off,
                                                          uint32_t n_clusters, uint64_t seed,
-                                                         uint32_t mode, double enl) {
+                                                         uint32_t mode, double enl, uint32_t base) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_clusters) return;
     const uint64_t j0 = job_off[c], J = job_off[c + 1] - j0;
-    const uint64_t akey = mcs_arrival_key(mcs_cluster_key(seed, c));
+    const uint64_t akey = mcs_arrival_key(mcs_cluster_key(seed, base + c));
     uint64_t j = 0, period = 0;
     uint32_t T = 0;
     // same scan as mcs_gen_arrivals (mcs_gen.h), writing into the .x lane of the records
@@ -397,19 +373,19 @@ __global__ __launch_bounds__(64) void gen_arrivals_kernel(uint4* jobs, const uin
 
 hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t* max_c,
                             const uint32_t* max_m, uint32_t n_clusters, uint64_t seed,
-                            uint32_t max_dur, hipStream_t s) {
+                            uint32_t max_dur, uint32_t base, hipStream_t s) {
     if (n_clusters == 0) return hipSuccess;
     hipLaunchKernelGGL(gen_attrs_kernel, dim3(64, n_clusters), dim3(256), 0, s, jobs, job_off,
-                       max_c, max_m, seed, max_dur);
+                       max_c, max_m, seed, max_dur, base);
     return hipGetLastError();
 }
 
 hipError_t launch_gen_arrivals(uint4* jobs, const uint64_t* job_off, uint32_t n_clusters,
                                uint64_t seed, uint32_t mode, double exp_neg_lambda,
-                               hipStream_t s) {
+                               uint32_t base, hipStream_t s) {
     if (n_clusters == 0) return hipSuccess;
     hipLaunchKernelGGL(gen_arrivals_kernel, dim3((n_clusters + 63) / 64), dim3(64), 0, s, jobs,
-                       job_off, n_clusters, seed, mode, exp_neg_lambda);
+                       job_off, n_clusters, seed, mode, exp_neg_lambda, base);
     return hipGetLastError();
 }
 

@@ -1,0 +1,534 @@
+// mcs_trade.cpp — C ABI of the lock-step trading path (include/mcs_trade.h): device state,
+// the tick loop (hipGraph replay on one GPU, RCCL all-gathers over xGMI across GPUs, or the
+// caller-driven phase API), and the result readers.  Host code; compiled by hipcc.
+//
+// Every decision is made by the gfx950 kernels of mcs_trade.hip; there is no CPU path.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "mcs_engine_impl.h"
+#include "mcs_trade_internal.h"
+
+namespace mcs {
+
+struct TradeDev {
+    TradeArgs a_local{};  // exchange in HBM (one engine holds the whole system)
+    TradeArgs a_xfer{};   // exchange through acc_all (RCCL or caller-driven)
+    unsigned long long* tn = nullptr;
+    TrCluster* cl = nullptr;
+    uint32_t* sfin = nullptr;
+    uint32_t* snode = nullptr;
+    unsigned long long* scm = nullptr;
+    TrLq* lq = nullptr;
+    TrRecA* recA = nullptr;
+    uint32_t* acc_l = nullptr;
+    uint32_t* acc_all = nullptr;
+    TrRecC* recC = nullptr;
+    TrTrader* tr = nullptr;
+    TrCtl* ctl = nullptr;
+    mcs_lent_rec* lent = nullptr;
+    mcs_trade_rec* trades = nullptr;
+    TrCtl* h_ctl = nullptr;  // pinned
+    hipGraphExec_t graph = nullptr;
+    uint32_t graph_ticks = 0;
+    bool begun = false;
+    std::chrono::steady_clock::time_point w0;
+};
+
+namespace {
+
+constexpr uint32_t kGraphTicks = 64;  // ticks per graph replay (one host poll per replay)
+
+int hip_fail(mcs_engine* e, const char* what, hipError_t st) {
+    return fail(e, MCS_E_HIP, std::string(what) + ": " + hipGetErrorString(st));
+}
+
+uint32_t auto_slots(uint32_t max_n) {
+    uint32_t s = 256;
+    while (s < 4u * max_n && s < kTrMaxSlots) s *= 2;
+    return s;
+}
+
+constexpr uint32_t kMaxLq = 1u << 24;  // LentQueue entries per cluster (512 MB per cluster)
+
+// Every acceptor of a borrow request keeps its own copy (server.go:232-237) and an overloaded
+// lender serves its LentQueue only when idle, so queues grow with the stream: start at 4 entries
+// per own job of the largest cluster (measured peaks: 3-12 per job on C3/C5-shaped workloads)
+uint32_t auto_lq(const mcs_engine* e) {
+    uint64_t mj = 0;
+    for (uint32_t c = 0; c < e->C; ++c) mj = std::max<uint64_t>(mj, e->job_off[c + 1] - e->job_off[c]);
+    uint64_t q = 4096;
+    while (q < 4 * mj && q < kMaxLq) q *= 2;
+    return (uint32_t)q;
+}
+
+int trade_alloc(mcs_engine* e) {
+    if (e->td) return MCS_OK;
+    if (!e->has_clusters || !e->has_jobs) return fail(e, MCS_E_STATE, "load clusters and jobs first");
+    const uint32_t Cl = e->C, Ct = e->C * e->world;
+    if (Ct > kTrMaxClusters) return fail(e, MCS_E_INVALID, "more than 1024 clusters in a trading system");
+    if (e->max_n > kTrMaxNodes) return fail(e, MCS_E_INVALID, "more than 1024 nodes in a cluster");
+    const uint32_t S = e->cfg.slot_pool ? 64u * e->cfg.slot_pool
+                                        : (e->tr_slots ? e->tr_slots : auto_slots(e->max_n));
+    if (S > kTrMaxSlots) return fail(e, MCS_E_INVALID, "slot pool above 4096");
+    const uint32_t LQ = e->cfg.lent_queue_cap ? e->cfg.lent_queue_cap : (e->tr_lq ? e->tr_lq : auto_lq(e));
+    TradeDev* td = new (std::nothrow) TradeDev();
+    if (!td) return fail(e, MCS_E_NOMEM, "trade state");
+    e->td = td;
+    const uint64_t lent_cap = std::max<uint64_t>(1ull << 16, 16ull * e->total_jobs);
+    const uint64_t trade_cap = 1ull << 22;
+    HIPCHK(e, hipMalloc(&td->tn, std::max<uint64_t>(e->total_nodes, 1) * 8));
+    HIPCHK(e, hipMalloc(&td->cl, Cl * sizeof(TrCluster)));
+    HIPCHK(e, hipMalloc(&td->sfin, (size_t)Cl * S * 4));
+    HIPCHK(e, hipMalloc(&td->snode, (size_t)Cl * S * 4));
+    HIPCHK(e, hipMalloc(&td->scm, (size_t)Cl * S * 8));
+    HIPCHK(e, hipMalloc(&td->lq, (size_t)Cl * LQ * sizeof(TrLq)));
+    HIPCHK(e, hipMalloc(&td->recA, Ct * sizeof(TrRecA)));
+    HIPCHK(e, hipMalloc(&td->acc_l, Ct * 4));
+    HIPCHK(e, hipMalloc(&td->acc_all, (size_t)e->world * Ct * 4));
+    HIPCHK(e, hipMalloc(&td->recC, Ct * sizeof(TrRecC)));
+    HIPCHK(e, hipMalloc(&td->tr, Ct * sizeof(TrTrader)));
+    HIPCHK(e, hipMalloc(&td->ctl, sizeof(TrCtl)));
+    HIPCHK(e, hipMalloc(&td->lent, lent_cap * sizeof(mcs_lent_rec)));
+    HIPCHK(e, hipMalloc(&td->trades, trade_cap * sizeof(mcs_trade_rec)));
+    HIPCHK(e, hipHostMalloc(&td->h_ctl, sizeof(TrCtl), hipHostMallocDefault));
+
+    TradeArgs& a = td->a_local;
+    a.Cl = Cl;
+    a.Ct = Ct;
+    a.base = e->rank * Cl;
+    a.world = e->world;
+    a.S = S;
+    a.LQ = LQ;
+    a.borrow = e->cfg.borrow;
+    a.trader = e->cfg.trader;
+    a.period = e->cfg.trader_period_s;
+    a.ok_sleep = e->cfg.trade_ok_sleep_s;
+    a.fail_sleep = e->cfg.trade_fail_sleep_s;
+    a.lock_s = e->cfg.lock_s;
+    a.sample_period = e->cfg.sample_period_s ? e->cfg.sample_period_s : 5u;
+    a.t_max = e->cfg.t_max_s ? e->cfg.t_max_s : 0xFFFFFFFEu;
+    a.lent_cap = lent_cap;
+    a.trade_cap = trade_cap;
+    a.node_off = e->d_node_off;
+    a.cap = e->d_cap;
+    a.free0 = e->d_free0;
+    a.tn = td->tn;
+    a.jobs = e->d_jobs;
+    a.job_off = e->d_job_off;
+    a.out_node = e->d_out_node;
+    a.out_start = e->d_out_start;
+    a.out_finish = e->d_out_finish;
+    a.cl = td->cl;
+    a.sfin = td->sfin;
+    a.snode = td->snode;
+    a.scm = td->scm;
+    a.lq = td->lq;
+    a.recA = td->recA;
+    a.acc_l = td->acc_l;
+    a.acc_all = td->acc_l;  // world 1: the local acceptances are the gathered ones
+    a.recC = td->recC;
+    a.tr = td->tr;
+    a.ctl = td->ctl;
+    a.lent_log = td->lent;
+    a.trade_log = td->trades;
+    td->a_xfer = a;
+    td->a_xfer.acc_all = td->acc_all;
+    return MCS_OK;
+}
+
+int launch_phase(mcs_engine* e, const TradeArgs& a, int phase) {
+    const hipError_t st = launch_trade_phase(a, phase, e->stream);
+    if (st != hipSuccess) return hip_fail(e, "trade kernel launch", st);
+    return MCS_OK;
+}
+
+int poll_ctl(mcs_engine* e) {
+    HIPCHK(e, hipMemcpyAsync(e->td->h_ctl, e->td->ctl, sizeof(TrCtl), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return MCS_OK;
+}
+
+// one engine holds the whole system: the four phases of kGraphTicks ticks captured once, replayed
+int run_local(mcs_engine* e) {
+    TradeDev* td = e->td;
+    if (!td->graph) {
+        hipGraph_t g = nullptr;
+        HIPCHK(e, hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+        for (uint32_t t = 0; t < kGraphTicks; ++t)
+            for (int p = 0; p < 4; ++p) {
+                const hipError_t st = launch_trade_phase(td->a_local, p, e->stream);
+                if (st != hipSuccess) {
+                    (void)hipStreamEndCapture(e->stream, &g);
+                    if (g) (void)hipGraphDestroy(g);
+                    return hip_fail(e, "trade kernel capture", st);
+                }
+            }
+        HIPCHK(e, hipStreamEndCapture(e->stream, &g));
+        const hipError_t st = hipGraphInstantiate(&td->graph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (st != hipSuccess) return hip_fail(e, "hipGraphInstantiate", st);
+        td->graph_ticks = kGraphTicks;
+    }
+    for (;;) {
+        HIPCHK(e, hipGraphLaunch(td->graph, e->stream));
+        if (int s = poll_ctl(e)) return s;
+        if (td->h_ctl->done) return MCS_OK;
+    }
+}
+
+int nccl_fail(mcs_engine* e, const char* what, ncclResult_t r) {
+    return fail(e, MCS_E_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+// N engines (one per GPU): the three record exchanges of a tick are ncclAllGather over xGMI
+int run_rccl(mcs_engine* e) {
+    TradeDev* td = e->td;
+    const TradeArgs& a = td->a_xfer;
+    ncclComm_t comm = (ncclComm_t)e->comm;
+    const size_t base = (size_t)e->rank * e->C;
+    for (;;) {
+        for (uint32_t t = 0; t < kGraphTicks; ++t) {
+            if (int s = launch_phase(e, a, 0)) return s;
+            ncclResult_t r = ncclAllGather(td->recA + base, td->recA, e->C * (sizeof(TrRecA) / 4),
+                                           ncclUint32, comm, e->stream);
+            if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(borrow requests)", r);
+            if (int s = launch_phase(e, a, 1)) return s;
+            r = ncclAllGather(td->acc_l, td->acc_all, a.Ct, ncclUint32, comm, e->stream);
+            if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(acceptances)", r);
+            if (int s = launch_phase(e, a, 2)) return s;
+            r = ncclAllGather(td->recC + base, td->recC, e->C * (sizeof(TrRecC) / 4), ncclUint32,
+                              comm, e->stream);
+            if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(state samples)", r);
+            if (int s = launch_phase(e, a, 3)) return s;
+        }
+        if (int s = poll_ctl(e)) return s;
+        if (td->h_ctl->done) return MCS_OK;
+    }
+}
+
+int fill_stats(mcs_engine* e, mcs_trade_stats* ts, mcs_stats* st) {
+    TradeDev* td = e->td;
+    std::vector<TrCluster> cl(e->C);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(cl.data(), td->cl, e->C * sizeof(TrCluster), hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpy(td->h_ctl, td->ctl, sizeof(TrCtl), hipMemcpyDeviceToHost));
+    const TrCtl& c = *td->h_ctl;
+    mcs_trade_stats s{};
+    uint32_t flags = c.flags;
+    for (uint32_t k = 0; k < e->C; ++k) {
+        const uint64_t J = e->job_off[k + 1] - e->job_off[k];
+        s.placed += cl[k].placed;
+        s.borrowed += cl[k].borrowed;
+        s.waited += cl[k].waited;
+        s.undecided += J - cl[k].decided;
+        s.lent_runs += cl[k].lent_runs;
+        s.lent_pending += cl[k].lq_len;
+        flags |= cl[k].flags;
+    }
+    if (c.n_lent > td->a_local.lent_cap || c.n_trades > td->a_local.trade_cap) flags |= MCS_FLAG_LOG_OVERFLOW;
+    s.trades = c.n_trades;
+    s.trades_won = c.n_won;
+    s.ticks = c.ticks;
+    s.t_final = c.T;
+    s.flags = flags;
+    if (ts) *ts = s;
+    if (st) {
+        st->jobs = e->total_jobs;
+        st->placed = s.placed;
+        st->waited = s.waited;
+        st->unplaced = s.undecided;
+        st->clusters = e->C;
+        st->deadlocked = 0;
+        st->escalations = 0;
+        st->slot_pool = td->a_local.S / 64u;
+    }
+    return MCS_OK;
+}
+
+}  // namespace
+
+void comm_free(mcs_engine* e) {
+    if (e->comm) (void)ncclCommDestroy((ncclComm_t)e->comm);
+    e->comm = nullptr;
+}
+
+void trade_free(mcs_engine* e) {
+    TradeDev* td = e->td;
+    if (!td) return;
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (td->graph) (void)hipGraphExecDestroy(td->graph);
+    dfree(td->tn);
+    dfree(td->cl);
+    dfree(td->sfin);
+    dfree(td->snode);
+    dfree(td->scm);
+    dfree(td->lq);
+    dfree(td->recA);
+    dfree(td->acc_l);
+    dfree(td->acc_all);
+    dfree(td->recC);
+    dfree(td->tr);
+    dfree(td->ctl);
+    dfree(td->lent);
+    dfree(td->trades);
+    if (td->h_ctl) (void)hipHostFree(td->h_ctl);
+    delete td;
+    e->td = nullptr;
+    e->trade_run = false;
+}
+
+int trade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n) {
+    TradeDev* td = e->td;
+    if (!td) return fail(e, MCS_E_STATE, "no lock-step run");
+    std::vector<TrCluster> cl(e->C);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(cl.data(), td->cl, e->C * sizeof(TrCluster), hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpy(td->h_ctl, td->ctl, sizeof(TrCtl), hipMemcpyDeviceToHost));
+    for (uint32_t k = 0; k < n; ++k) {
+        mcs_cluster_stats s{};
+        s.t_end = td->h_ctl->T;
+        s.placed = cl[k].placed;
+        s.waited = cl[k].waited;
+        s.peak_running = cl[k].peak;
+        s.flags = cl[k].flags;
+        s.pool = td->a_local.S / 64u;
+        s.iterations = td->h_ctl->ticks;
+        s.release_scans = 0;
+        out[k] = s;
+    }
+    return MCS_OK;
+}
+
+int trade_run(mcs_engine* e, mcs_stats* stats) {
+    if (e->world > 1 && !e->comm)
+        return fail(e, MCS_E_STATE, "sharded lock-step run needs mcs_comm_init (or mcs_trade_phase)");
+    e->tr_lq = e->tr_slots = 0;
+    uint32_t escalations = 0;
+    for (;;) {
+        if (int s = mcs_trade_begin(e)) return s;
+        if (int s = e->world == 1 ? run_local(e) : run_rccl(e)) return s;
+        const int s = mcs_trade_end(e, stats);
+        if (s != MCS_E_CAPACITY) {
+            if (stats) stats->escalations = escalations;
+            return s;
+        }
+        // capacity escalation: the flags are replicated on every rank, so all ranks re-run alike
+        const uint32_t flags = e->td->h_ctl->flags, LQ = e->td->a_local.LQ, S = e->td->a_local.S;
+        bool grew = false;
+        if ((flags & MCS_FLAG_LENT_OVERFLOW) && !e->cfg.lent_queue_cap && LQ < kMaxLq) {
+            e->tr_lq = std::min<uint32_t>(LQ * 4u, kMaxLq);
+            grew = true;
+        }
+        if ((flags & MCS_FLAG_OVERFLOW) && !e->cfg.slot_pool && S < kTrMaxSlots) {
+            e->tr_slots = S * 2u;
+            grew = true;
+        }
+        if (!grew) return s;
+        const uint32_t lq = e->tr_lq, sl = e->tr_slots;
+        trade_free(e);
+        e->tr_lq = lq;
+        e->tr_slots = sl;
+        ++escalations;
+    }
+}
+
+}  // namespace mcs
+
+extern "C" {
+
+int mcs_set_shard(mcs_engine* e, uint32_t rank, uint32_t world) {
+    if (int st = check_engine(e)) return st;
+    if (!e->has_clusters) return fail(e, MCS_E_STATE, "mcs_load_clusters first");
+    if (world == 0 || rank >= world) return fail(e, MCS_E_INVALID, "rank must be < world");
+    if ((uint64_t)world * e->C > 0xFFFFFFFFull) return fail(e, MCS_E_INVALID, "too many clusters");
+    mcs::trade_free(e);
+    e->rank = rank;
+    e->world = world;
+    return MCS_OK;
+}
+
+int mcs_comm_unique_id(mcs_comm_id* out) {
+    if (!out) return MCS_E_INVALID;
+    static_assert(sizeof(mcs_comm_id) == sizeof(ncclUniqueId), "ncclUniqueId size");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return MCS_E_RCCL;
+    std::memcpy(out->bytes, &id, sizeof(id));
+    return MCS_OK;
+}
+
+int mcs_comm_init(mcs_engine* e, const mcs_comm_id* id) {
+    if (int st = check_engine(e)) return st;
+    if (!id) return fail(e, MCS_E_INVALID, "null id");
+    if (e->comm) {
+        (void)ncclCommDestroy((ncclComm_t)e->comm);
+        e->comm = nullptr;
+    }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id->bytes, sizeof(uid));
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&comm, (int)e->world, uid, (int)e->rank);
+    if (r != ncclSuccess) return fail(e, MCS_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    e->comm = comm;
+    return MCS_OK;
+}
+
+int mcs_trade_begin(mcs_engine* e) {
+    if (int st = check_engine(e)) return st;
+    if (!(e->cfg.borrow || e->cfg.trader)) return fail(e, MCS_E_STATE, "engine config has no borrow/trader");
+    if (int st = mcs::trade_alloc(e)) return st;
+    mcs::TradeDev* td = e->td;
+    td->w0 = std::chrono::steady_clock::now();
+    const hipError_t st = mcs::launch_trade_init(td->a_local, e->stream);
+    if (st != hipSuccess) return mcs::hip_fail(e, "trade init", st);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipEventRecord(e->ev0, e->stream));  // kernel_ms: the lock-step loop only
+    td->begun = true;
+    e->has_run = false;
+    e->trade_run = false;
+    return MCS_OK;
+}
+
+int mcs_trade_xfer_bytes(mcs_engine* e, uint32_t phase, uint64_t* in_bytes, uint64_t* out_bytes) {
+    if (!e || !in_bytes || !out_bytes || phase > 3) return MCS_E_INVALID;
+    const uint64_t Cl = e->C, Ct = (uint64_t)e->C * e->world;
+    switch (phase) {
+        case 0: *in_bytes = 0; *out_bytes = Cl * sizeof(mcs::TrRecA); break;
+        case 1: *in_bytes = Ct * sizeof(mcs::TrRecA); *out_bytes = Ct * 4; break;
+        case 2: *in_bytes = (uint64_t)e->world * Ct * 4; *out_bytes = Cl * sizeof(mcs::TrRecC); break;
+        default: *in_bytes = Ct * sizeof(mcs::TrRecC); *out_bytes = 0; break;
+    }
+    return MCS_OK;
+}
+
+int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_bytes, void* out,
+                    uint64_t out_bytes, uint32_t* done) {
+    if (int st = check_engine(e)) return st;
+    mcs::TradeDev* td = e->td;
+    if (!td || !td->begun) return fail(e, MCS_E_STATE, "mcs_trade_begin first");
+    uint64_t ib = 0, ob = 0;
+    if (int st = mcs_trade_xfer_bytes(e, phase, &ib, &ob)) return fail(e, st, "bad phase");
+    if (in_bytes != ib || out_bytes != ob || (ib && !in) || (ob && !out))
+        return fail(e, MCS_E_INVALID, "exchange buffer sizes do not match mcs_trade_xfer_bytes");
+    const mcs::TradeArgs& a = td->a_xfer;
+    const size_t base = (size_t)e->rank * e->C;
+    switch (phase) {
+        case 0:
+            if (int s = mcs::launch_phase(e, a, 0)) return s;
+            HIPCHK(e, hipMemcpyAsync(out, td->recA + base, ob, hipMemcpyDeviceToHost, e->stream));
+            break;
+        case 1:
+            HIPCHK(e, hipMemcpyAsync(td->recA, in, ib, hipMemcpyHostToDevice, e->stream));
+            if (int s = mcs::launch_phase(e, a, 1)) return s;
+            HIPCHK(e, hipMemcpyAsync(out, td->acc_l, ob, hipMemcpyDeviceToHost, e->stream));
+            break;
+        case 2:
+            HIPCHK(e, hipMemcpyAsync(td->acc_all, in, ib, hipMemcpyHostToDevice, e->stream));
+            if (int s = mcs::launch_phase(e, a, 2)) return s;
+            HIPCHK(e, hipMemcpyAsync(out, td->recC + base, ob, hipMemcpyDeviceToHost, e->stream));
+            break;
+        default:
+            HIPCHK(e, hipMemcpyAsync(td->recC, in, ib, hipMemcpyHostToDevice, e->stream));
+            if (int s = mcs::launch_phase(e, a, 3)) return s;
+            HIPCHK(e, hipMemcpyAsync(td->h_ctl, td->ctl, sizeof(mcs::TrCtl), hipMemcpyDeviceToHost,
+                                     e->stream));
+            break;
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (done) *done = phase == 3 ? td->h_ctl->done : 0u;
+    return MCS_OK;
+}
+
+int mcs_trade_end(mcs_engine* e, mcs_stats* stats) {
+    if (int st = check_engine(e)) return st;
+    mcs::TradeDev* td = e->td;
+    if (!td || !td->begun) return fail(e, MCS_E_STATE, "mcs_trade_begin first");
+    HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->has_run = true;
+    e->trade_run = true;
+    mcs_trade_stats ts{};
+    mcs_stats st{};
+    if (int s = mcs::fill_stats(e, &ts, &st)) return s;
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) ms = 0.0f;
+    st.kernel_ms = ms;
+    st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td->w0).count();
+    if (stats) *stats = st;
+    if (ts.flags & MCS_FLAG_OVERFLOW)
+        return fail(e, MCS_E_CAPACITY, "running-slot pool overflow (raise mcs_config.slot_pool)");
+    if (ts.flags & MCS_FLAG_LENT_OVERFLOW)
+        return fail(e, MCS_E_CAPACITY, "LentQueue overflow (raise mcs_config.lent_queue_cap)");
+    return MCS_OK;
+}
+
+int mcs_read_trade_stats(mcs_engine* e, mcs_trade_stats* out) {
+    if (int st = check_engine(e)) return st;
+    if (!out) return fail(e, MCS_E_INVALID, "null output");
+    if (!e->trade_run || !e->td) return fail(e, MCS_E_STATE, "no lock-step run");
+    mcs_stats st{};
+    if (int s = mcs::fill_stats(e, out, &st)) return s;
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) ms = 0.0f;
+    out->kernel_ms = ms;
+    out->wall_ms = 0.0;
+    return MCS_OK;
+}
+
+int mcs_read_lent(mcs_engine* e, mcs_lent_rec* out, uint64_t cap, uint64_t* n) {
+    if (int st = check_engine(e)) return st;
+    if (!n || (cap && !out)) return fail(e, MCS_E_INVALID, "bad output");
+    if (!e->trade_run || !e->td) return fail(e, MCS_E_STATE, "no lock-step run");
+    mcs::TradeDev* td = e->td;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(td->h_ctl, td->ctl, sizeof(mcs::TrCtl), hipMemcpyDeviceToHost));
+    const uint64_t total = td->h_ctl->n_lent;
+    const uint64_t have = std::min<uint64_t>(total, td->a_local.lent_cap);
+    std::vector<mcs_lent_rec> v(have);
+    if (have) HIPCHK(e, hipMemcpy(v.data(), td->lent, have * sizeof(mcs_lent_rec), hipMemcpyDeviceToHost));
+    std::sort(v.begin(), v.end(), [](const mcs_lent_rec& x, const mcs_lent_rec& y) {
+        if (x.start_s != y.start_s) return x.start_s < y.start_s;
+        if (x.lender != y.lender) return x.lender < y.lender;
+        if (x.borrower != y.borrower) return x.borrower < y.borrower;
+        return x.job < y.job;
+    });
+    const uint64_t k = std::min<uint64_t>(have, cap);
+    if (k) std::memcpy(out, v.data(), k * sizeof(mcs_lent_rec));
+    *n = total;
+    return MCS_OK;
+}
+
+int mcs_read_trades(mcs_engine* e, mcs_trade_rec* out, uint64_t cap, uint64_t* n) {
+    if (int st = check_engine(e)) return st;
+    if (!n || (cap && !out)) return fail(e, MCS_E_INVALID, "bad output");
+    if (!e->trade_run || !e->td) return fail(e, MCS_E_STATE, "no lock-step run");
+    mcs::TradeDev* td = e->td;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(td->h_ctl, td->ctl, sizeof(mcs::TrCtl), hipMemcpyDeviceToHost));
+    const uint64_t total = td->h_ctl->n_trades;
+    const uint64_t k = std::min<uint64_t>(std::min<uint64_t>(total, td->a_local.trade_cap), cap);
+    if (k) HIPCHK(e, hipMemcpy(out, td->trades, k * sizeof(mcs_trade_rec), hipMemcpyDeviceToHost));
+    *n = total;
+    return MCS_OK;
+}
+
+int mcs_read_virtual_nodes(mcs_engine* e, uint32_t* out, uint32_t n_total) {
+    if (int st = check_engine(e)) return st;
+    if (!e->trade_run || !e->td) return fail(e, MCS_E_STATE, "no lock-step run");
+    const uint32_t Ct = e->C * e->world;
+    if (!out || n_total > Ct) return fail(e, MCS_E_INVALID, "bad output");
+    std::vector<mcs::TrTrader> t(Ct);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(t.data(), e->td->tr, Ct * sizeof(mcs::TrTrader), hipMemcpyDeviceToHost));
+    for (uint32_t k = 0; k < n_total; ++k) out[k] = t[k].vnodes;
+    return MCS_OK;
+}
+
+}  // extern "C"

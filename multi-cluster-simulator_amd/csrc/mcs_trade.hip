@@ -1,0 +1,528 @@
+// mcs_trade.hip — gfx950 kernels of the lock-step trading path (mcs_trade.h).
+//
+// One tick of the lock-step semantics is four launches on the engine stream, each a kernel
+// boundary (= grid-wide barrier) and, on N GPUs, an RCCL all-gather of fixed-size records between
+// them:
+//   A tr_step_kernel    one wave per cluster: releases, arrivals, the Fifo decisions of the tick
+//                       (scheduler.go:216-296) and the tick's borrow request (server.go:160-248)
+//   B tr_lend_kernel    one wave per cluster as lender: Lend (strict '>', scheduler.go:194-202)
+//                       against every request of the tick, in borrower order; LentQueue appends
+//   C tr_post_kernel    one wave per cluster as borrower: BorrowedQueue move when some lender
+//                       accepted (scheduler.go:237-242); float32 utilization sample
+//                       (cluster.go:46-63) on trader ticks; clock hints
+//   D tr_trader_kernel  one wave for the whole system, replicated on every rank: trader rounds
+//                       in cluster order (trader.go:280-325, 193-278; server.go:31-85) with the
+//                       responders evaluated across lanes, then the next tick (fast-forward)
+// Work per tick is a handful of decisions per cluster: the path is launch/latency-bound, so the
+// engine replays the four launches from a captured hipGraph.  Within a kernel the per-cluster
+// state a wave both writes and re-reads (node free vectors, slot finish times, trader locks) is
+// staged in LDS: an L2 atomic or store followed by a plain global load of the same line from the
+// same wave could be served stale by the non-coherent vector L1.
+#include "mcs_trade_internal.h"
+#include "mcs_wave.h"
+
+namespace mcs {
+namespace {
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x; }
+
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void tr_init_kernel(TradeArgs a) {
+    const uint32_t c = blockIdx.x, lane = lane_id();
+    const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
+    uint32_t sc = 0, sm = 0;
+    for (uint32_t i = lane; i < N; i += kWave) {
+        const uint2 f = a.free0[n0 + i];
+        a.tn[n0 + i] = (unsigned long long)f.x | ((unsigned long long)f.y << 32);
+        const uint2 cp = a.cap[n0 + i];
+        sc += cp.x;  // uint32 sums, wrapping like SetTotalResources (cluster.go:34-37)
+        sm += cp.y;
+    }
+    sc = wave_sum_u32(sc);
+    sm = wave_sum_u32(sm);
+    for (uint32_t s = lane; s < a.S; s += kWave) a.sfin[(size_t)c * a.S + s] = kEmpty;
+    const uint64_t j0 = a.job_off[c], j1 = a.job_off[c + 1];
+    for (uint64_t j = j0 + lane; j < j1; j += kWave) {
+        a.out_node[j] = MCS_NODE_UNPLACED;
+        a.out_start[j] = MCS_TIME_NONE;
+        a.out_finish[j] = MCS_TIME_NONE;
+    }
+    if (lane == 0) {
+        TrCluster z{};
+        z.minf = kEmpty;
+        z.total_c = sc;
+        z.total_m = sm;
+        a.cl[c] = z;
+    }
+    if (c == 0) {
+        for (uint32_t g = lane; g < a.Ct; g += kWave) {
+            TrTrader t{};
+            t.next_id = 1u;  // s.id = rand.Uint32() (pkg/trader/server.go:26), seeded: 1
+            a.tr[g] = t;
+            a.acc_l[g] = 0u;
+        }
+        if (lane == 0) {
+            TrCtl z{};
+            *a.ctl = z;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Phase A: the cluster's scheduler step at tick T.
+__global__ __launch_bounds__(64) void tr_step_kernel(TradeArgs a) {
+    __shared__ unsigned long long nodes[kTrMaxNodes];
+    __shared__ uint32_t sfin[kTrMaxSlots];
+    if (a.ctl->done) return;
+    const uint32_t T = a.ctl->T;
+    const uint32_t c = blockIdx.x, lane = lane_id(), g = a.base + c;
+    const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
+    const uint64_t j0 = a.job_off[c];
+    const uint32_t J = (uint32_t)(a.job_off[c + 1] - j0);
+    const uint4* __restrict__ jobs = a.jobs + j0;
+    const size_t sb = (size_t)c * a.S;
+    const uint32_t S = a.S;
+    const uint32_t vn = a.tr[g].vnodes;
+    TrCluster st = a.cl[c];
+
+    for (uint32_t i = lane; i < N; i += kWave) nodes[i] = a.tn[n0 + i];
+    for (uint32_t s = lane; s < S; s += kWave) sfin[s] = a.sfin[sb + s];
+    __syncthreads();
+
+    // releases due at T (cluster.go:153-157), before the tick's decisions
+    if (st.minf <= T) {
+        uint32_t lm = kEmpty, nrel = 0;
+        for (uint32_t s = lane; s < S; s += kWave) {
+            const uint32_t f = sfin[s];
+            if (f <= T) {
+                const uint32_t nd = a.snode[sb + s];
+                if (nd < N) atomicAdd(&nodes[nd], a.scm[sb + s]);
+                sfin[s] = kEmpty;
+                ++nrel;
+            } else {
+                lm = f < lm ? f : lm;
+            }
+        }
+        st.nrun -= wave_sum_u32(nrel);
+        st.minf = wave_min_u32(lm);
+        __syncthreads();
+    }
+    // arrivals up to T join the ReadyQueue (jobs are sorted by arrival)
+    while (st.next_arr < J) {
+        const uint32_t i = st.next_arr + lane;
+        const bool ok = i < J && jobs[i].x <= T;
+        const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(ok));
+        st.next_arr += n;
+        if (n < (uint32_t)kWave) break;
+    }
+
+    // ScheduleJob (scheduler.go:127-139): lowest node with both >=; zero-capacity virtual nodes
+    // (AddVirtualNode, cluster.go:79) follow the physical ones
+    auto first_fit = [&](uint32_t jc, uint32_t jm) -> uint32_t {
+        uint32_t best = kEmpty;
+        for (uint32_t b = 0; b < N; b += kWave) {
+            const uint32_t i = b + lane;
+            if (i < N) {
+                const unsigned long long v = nodes[i];
+                if ((uint32_t)v >= jc && (uint32_t)(v >> 32) >= jm) best = i;
+            }
+            if (__ballot(best != kEmpty)) break;
+        }
+        uint32_t k = wave_min_u32(best);
+        if (k == kEmpty && jc == 0u && jm == 0u && vn > 0u) k = N;
+        return k;
+    };
+    // Node.RunJob commit (cluster.go:144-148) + running-slot insert; false on slot overflow
+    auto commit = [&](uint32_t k, uint32_t jc, uint32_t jm, uint32_t fin) -> bool {
+        const unsigned long long need = (unsigned long long)jc | ((unsigned long long)jm << 32);
+        uint32_t slot = kEmpty;
+        for (uint32_t b = 0; b < S; b += kWave) {
+            const unsigned long long fr = __ballot(sfin[b + lane] == kEmpty);
+            if (fr) {
+                slot = b + (uint32_t)__builtin_ctzll(fr);
+                break;
+            }
+        }
+        if (slot == kEmpty) return false;
+        if (lane == 0) {
+            if (k < N) atomicSub(&nodes[k], need);
+            sfin[slot] = fin;
+            a.snode[sb + slot] = k;
+            a.scm[sb + slot] = need;
+        }
+        __syncthreads();
+        ++st.nrun;
+        st.peak = st.nrun > st.peak ? st.nrun : st.peak;
+        st.minf = fin < st.minf ? fin : st.minf;
+        return true;
+    };
+    auto place_own = [&](uint32_t j, uint32_t k, uint4 jb) -> bool {
+        const uint32_t fin = T + jb.y;
+        if (jb.y != 0u && !commit(k, jb.z, jb.w, fin)) return false;
+        if (lane == 0) {
+            a.out_node[j0 + j] = (int32_t)k;
+            a.out_start[j0 + j] = T;
+            a.out_finish[j0 + j] = fin;
+        }
+        ++st.placed;
+        ++st.decided;
+        return true;
+    };
+
+    TrRecA req{kEmpty, 0u, 0u, 0u};
+    for (;;) {
+        if (st.has_w) {  // WaitQueue head (scheduler.go:219-251)
+            const uint4 jb = jobs[st.w];
+            const uint32_t k = first_fit(jb.z, jb.w);
+            if (k != kEmpty) {
+                if (!place_own(st.w, k, jb)) {
+                    st.flags |= MCS_FLAG_OVERFLOW;
+                    break;
+                }
+                st.has_w = 0u;
+            } else if (a.borrow) {
+                req = TrRecA{st.w, jb.z, jb.w, jb.y};  // BorrowResources (:234)
+            }
+            break;  // time.Sleep(1 s), :250
+        }
+        if (st.rq_head < st.next_arr) {  // ReadyQueue head (:255-272), no sleep
+            const uint32_t j = st.rq_head++;
+            const uint4 jb = jobs[j];
+            const uint32_t k = first_fit(jb.z, jb.w);
+            if (k != kEmpty) {
+                if (!place_own(j, k, jb)) {
+                    st.flags |= MCS_FLAG_OVERFLOW;
+                    break;
+                }
+            } else {
+                st.has_w = 1u;
+                st.w = j;
+                ++st.waited;
+            }
+            continue;
+        }
+        if (st.lq_len > 0u) {  // LentQueue head (:277-290)
+            const TrLq e = a.lq[(size_t)c * a.LQ + st.lq_head];
+            const uint32_t k = first_fit(e.c, e.m);
+            if (k != kEmpty) {
+                const uint32_t fin = T + e.dur;
+                if (e.dur != 0u && !commit(k, e.c, e.m, fin)) {
+                    st.flags |= MCS_FLAG_OVERFLOW;
+                    break;
+                }
+                if (lane == 0) {
+                    const unsigned long long idx = atomicAdd(&a.ctl->n_lent, 1ull);
+                    if (idx < a.lent_cap) {
+                        mcs_lent_rec r;
+                        r.lender = g;
+                        r.borrower = e.borrower;
+                        r.job = e.job;
+                        r.node = k;
+                        r.start_s = T;
+                        r.finish_s = fin;
+                        r.pad = 0u;
+                        a.lent_log[idx] = r;
+                    }
+                }
+                ++st.lent_runs;
+                st.lq_head = st.lq_head + 1u == a.LQ ? 0u : st.lq_head + 1u;
+                --st.lq_len;
+            }
+            break;  // sleep 1 s (:289)
+        }
+        break;  // idle sleep (:294)
+    }
+
+    __syncthreads();
+    for (uint32_t i = lane; i < N; i += kWave) a.tn[n0 + i] = nodes[i];
+    for (uint32_t s = lane; s < S; s += kWave) a.sfin[sb + s] = sfin[s];
+    if (lane == 0) {
+        a.cl[c] = st;
+        a.recA[g] = req;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Phase B: the cluster as lender, requests in borrower order ("/borrow", server.go:80-113).
+__global__ __launch_bounds__(64) void tr_lend_kernel(TradeArgs a) {
+    if (a.ctl->done) return;
+    const uint32_t c = blockIdx.x, lane = lane_id(), g = a.base + c;
+    const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
+    const unsigned long long* __restrict__ tn = a.tn + n0;
+    uint32_t lq_len = a.cl[c].lq_len, lq_head = a.cl[c].lq_head, flags = a.cl[c].flags;
+    const uint32_t LQ = a.LQ;
+    for (uint32_t b0 = 0; b0 < a.Ct; b0 += kWave) {
+        const uint32_t bl = b0 + lane;
+        const bool has = bl < a.Ct && bl != g && a.recA[bl].job != kEmpty;  // self skipped (:176)
+        unsigned long long pend = __ballot(has);
+        while (pend) {
+            const uint32_t b = b0 + (uint32_t)__builtin_ctzll(pend);
+            pend &= pend - 1ull;
+            const TrRecA r = a.recA[b];
+            bool ok = false;
+            for (uint32_t i0 = 0; i0 < N; i0 += kWave) {
+                const uint32_t i = i0 + lane;
+                if (i < N) {
+                    const unsigned long long v = tn[i];
+                    ok = ok || ((uint32_t)v > r.c && (uint32_t)(v >> 32) > r.m);
+                }
+                if (__ballot(ok)) break;
+            }
+            if (!__ballot(ok)) continue;  // "can't lend" (scheduler.go:201)
+            if (lq_len >= LQ) {
+                flags |= MCS_FLAG_LENT_OVERFLOW;
+                continue;
+            }
+            if (lane == 0) {
+                uint32_t at = lq_head + lq_len;
+                at = at >= LQ ? at - LQ : at;
+                TrLq e{};
+                e.borrower = b;
+                e.job = r.job;
+                e.c = r.c;
+                e.m = r.m;
+                e.dur = r.dur;
+                a.lq[(size_t)c * LQ + at] = e;
+                a.acc_l[b] = 1u;
+            }
+            ++lq_len;
+        }
+    }
+    if (lane == 0) {
+        a.cl[c].lq_len = lq_len;
+        a.cl[c].flags = flags;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Phase C: the cluster as borrower, utilization sample, clock hints.
+__global__ __launch_bounds__(64) void tr_post_kernel(TradeArgs a) {
+    __shared__ float dc[kTrMaxNodes], dm[kTrMaxNodes];
+    if (a.ctl->done) return;
+    const uint32_t T = a.ctl->T;
+    const uint32_t c = blockIdx.x, lane = lane_id(), g = a.base + c;
+    const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
+    const uint64_t j0 = a.job_off[c];
+    const uint32_t J = (uint32_t)(a.job_off[c + 1] - j0);
+    TrCluster st = a.cl[c];
+
+    const TrRecA r = a.recA[g];
+    if (r.job != kEmpty) {
+        uint32_t acc = 0;
+        for (uint32_t w = 0; w < a.world; ++w) acc |= a.acc_all[(size_t)w * a.Ct + g];
+        if (acc) {  // BorrowedQueue append, WaitQueue pop (scheduler.go:237-242)
+            if (lane == 0) {
+                a.out_node[j0 + r.job] = MCS_NODE_BORROWED;
+                a.out_start[j0 + r.job] = T;
+                a.out_finish[j0 + r.job] = MCS_TIME_NONE;
+            }
+            st.has_w = 0u;
+            ++st.decided;
+            ++st.borrowed;
+        }
+    }
+    // GetResourceUtilization (cluster.go:46-63) when a trader reads it at this tick: the state
+    // stream samples every sample_period_s (trader_server.go:24-47) and trader rounds fall on
+    // multiples of the period, so the sample a round reads is the one taken at its own tick
+    if (a.trader && T % a.sample_period == 0u) {
+        bool due = false;
+        for (uint32_t q = lane; q < a.Ct; q += kWave) due = due || a.tr[q].next_due <= T;
+        if (__ballot(due)) {
+            for (uint32_t i = lane; i < N; i += kWave) {
+                const unsigned long long v = a.tn[n0 + i];
+                const uint2 cp = a.cap[n0 + i];
+                dc[i] = __fsub_rn((float)cp.x, (float)(uint32_t)v);
+                dm[i] = __fsub_rn((float)cp.y, (float)(uint32_t)(v >> 32));
+            }
+            __syncthreads();
+            if (lane == 0) {
+                float sc = 0.0f, sm = 0.0f;
+                for (uint32_t i = 0; i < N; ++i) {  // node order, float32 (Go)
+                    sc = __fadd_rn(sc, dc[i]);
+                    sm = __fadd_rn(sm, dm[i]);
+                }
+                st.cu = __fdiv_rn(sc, (float)st.total_c);
+                st.mu = __fdiv_rn(sm, (float)st.total_m);
+            }
+            st.cu = __shfl(st.cu, 0);
+            st.mu = __shfl(st.mu, 0);
+        }
+    }
+    if (lane == 0) {
+        TrRecC o;
+        o.cu = st.cu;
+        o.mu = st.mu;
+        o.total_c = st.total_c;
+        o.total_m = st.total_m;
+        o.busy = (st.has_w || st.lq_len > 0u || st.rq_head < st.next_arr) ? 1u : 0u;
+        o.next_arr_t = st.next_arr < J ? a.jobs[j0 + st.next_arr].x : kEmpty;
+        o.done = (st.decided == J && st.lq_len == 0u) ? 1u : 0u;
+        o.flags = st.flags;
+        a.recC[g] = o;
+        a.cl[c] = st;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// ApproveTrade (trader.go:141-167) of the contract {cores, mem, time 0 s, price 0} that every
+// FIFO trade carries (the small-node contract over an empty Level1), on the responder's sample.
+__device__ __forceinline__ bool approve_zero_contract(uint32_t tc, uint32_t tm, float cu, float mu) {
+    if (!(cu < 0.8f && mu < 0.8f)) return false;  // :147
+    const float ftm = (float)tm, ftc = (float)tc;
+    const float avail_mem = __fsub_rn(ftm, __fmul_rn(ftm, mu));   // :148
+    const float avail_core = __fsub_rn(ftc, __fmul_rn(ftc, cu));  // :149
+    if (!(avail_core >= 0.0f && avail_mem >= 0.0f)) return false;  // :151
+    // incentive = -1*0*0 + -1*0*0 = -0.0 (float64); price 0 >= -0.0 (:154-155)
+    return true;
+}
+
+// Phase D: trader rounds (replicated) and the next tick.
+__global__ __launch_bounds__(64) void tr_trader_kernel(TradeArgs a) {
+    __shared__ TrTrader trs[kTrMaxClusters];
+    if (a.ctl->done) return;
+    const uint32_t T = a.ctl->T;
+    const uint32_t lane = lane_id();
+    const uint32_t Ct = a.Ct;
+    for (uint32_t q = lane; q < Ct; q += kWave) trs[q] = a.tr[q];
+    __syncthreads();
+    unsigned long long n_trades = a.ctl->n_trades, n_won = a.ctl->n_won;
+    uint32_t lflags = 0;
+
+    if (a.trader) {
+        for (uint32_t q0 = 0; q0 < Ct; q0 += kWave) {
+            const uint32_t ql = q0 + lane;
+            unsigned long long due = __ballot(ql < Ct && trs[ql].next_due <= T);
+            while (due) {  // RequestPolicyMonitor of requester q (trader.go:282-324), index order
+                const uint32_t q = q0 + (uint32_t)__builtin_ctzll(due);
+                due &= due - 1ull;
+                const TrRecC rq = a.recC[q];
+                // policies [WaitTime, Utilization] (trader.go:55-62): WaitTime never breaks under
+                // FIFO (its average is only fed by /delay); Utilization (trader.go:127-130)
+                const bool broken = rq.cu > 0.8f || rq.mu > 0.8f;
+                if (!broken) {
+                    if (lane == 0) trs[q].next_due = T + a.period;
+                    __syncthreads();
+                    continue;
+                }
+                // Trade (trader.go:193-278): RequestResource to every other trader, index order
+                uint32_t napp = 0, winner = kEmpty;
+                for (uint32_t r0 = 0; r0 < Ct; r0 += kWave) {
+                    const uint32_t r = r0 + lane;
+                    bool app = false;
+                    if (r < Ct && r != q) {
+                        TrTrader t = trs[r];
+                        if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
+                        if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
+                            const TrRecC rr = a.recC[r];
+                            app = approve_zero_contract(rr.total_c, rr.total_m, rr.cu, rr.mu);
+                            t.lock_id = t.next_id++;  // set even when not approving (:44-46)
+                            t.lock_until = T + a.lock_s;
+                        }
+                        trs[r] = t;
+                    }
+                    const unsigned long long ab = __ballot(app);
+                    napp += (uint32_t)__builtin_popcountll(ab);
+                    // every response echoes the requester's price (server.go:44): the Go heap of
+                    // equal keys pops the first push first (Appendix C), whose lock still matches
+                    // (nothing intervenes), and the zero allocation cannot fail -> first approver
+                    if (winner == kEmpty && ab) winner = r0 + (uint32_t)__builtin_ctzll(ab);
+                }
+                __syncthreads();
+                if (lane == 0) {
+                    if (winner != kEmpty) {
+                        trs[winner].lock_id = 0u;  // ApproveContract resets currentContract (:83)
+                        trs[q].vnodes += 1u;       // AddVirtualNode(0 cores, 0 memory)
+                        ++n_won;
+                    }
+                    if (n_trades < a.trade_cap) {
+                        mcs_trade_rec rec;
+                        rec.t_s = T;
+                        rec.requester = q;
+                        rec.winner = winner == kEmpty ? -1 : (int32_t)winner;
+                        rec.approvals = napp;
+                        a.trade_log[n_trades] = rec;
+                    } else {
+                        lflags |= MCS_FLAG_LOG_OVERFLOW;
+                    }
+                    trs[q].next_due = T + (winner != kEmpty ? a.ok_sleep : a.fail_sleep) + a.period;
+                }
+                ++n_trades;
+                __syncthreads();
+            }
+        }
+    }
+
+    // the next tick: T+1 while any queue is busy, else the next arrival or trader round
+    bool all_done = true, busy = false;
+    uint32_t nxt = kEmpty, fl = 0;
+    for (uint32_t q = lane; q < Ct; q += kWave) {
+        const TrRecC rc = a.recC[q];
+        all_done = all_done && rc.done;
+        busy = busy || rc.busy;
+        nxt = rc.next_arr_t < nxt ? rc.next_arr_t : nxt;
+        if (a.trader) nxt = trs[q].next_due < nxt ? trs[q].next_due : nxt;
+        fl |= rc.flags;
+        a.acc_l[q] = 0u;
+    }
+    const bool done_all = !__ballot(!all_done);
+    const bool busy_any = __ballot(busy) != 0ull;
+    nxt = wave_min_u32(nxt);
+    for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o);
+    __syncthreads();
+    for (uint32_t q = lane; q < Ct; q += kWave) a.tr[q] = trs[q];
+    if (lane == 0) {
+        TrCtl* ctl = a.ctl;
+        uint32_t flags = ctl->flags | fl | lflags;
+        uint32_t done = 0, Tn = T;
+        const uint32_t fatal = MCS_FLAG_OVERFLOW | MCS_FLAG_LENT_OVERFLOW;
+        if (done_all || (flags & fatal)) {
+            done = 1u;
+        } else if (T >= a.t_max || (!busy_any && nxt == kEmpty)) {
+            done = 1u;
+            flags |= MCS_FLAG_T_MAX;
+        } else {
+            Tn = (busy_any || nxt <= T + 1u) ? T + 1u : nxt;
+        }
+        ctl->T = Tn;
+        ctl->done = done;
+        ctl->ticks += 1u;
+        ctl->flags = flags;
+        ctl->n_trades = n_trades;
+        ctl->n_won = n_won;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_trade_init(const TradeArgs& a, hipStream_t s) {
+    if (a.Cl == 0) return hipSuccess;
+    hipLaunchKernelGGL(tr_init_kernel, dim3(a.Cl), dim3(kWave), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_trade_phase(const TradeArgs& a, int phase, hipStream_t s) {
+    switch (phase) {
+        case 0:
+            hipLaunchKernelGGL(tr_step_kernel, dim3(a.Cl), dim3(kWave), 0, s, a);
+            break;
+        case 1:
+            hipLaunchKernelGGL(tr_lend_kernel, dim3(a.Cl), dim3(kWave), 0, s, a);
+            break;
+        case 2:
+            hipLaunchKernelGGL(tr_post_kernel, dim3(a.Cl), dim3(kWave), 0, s, a);
+            break;
+        case 3:
+            hipLaunchKernelGGL(tr_trader_kernel, dim3(1), dim3(kWave), 0, s, a);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mcs

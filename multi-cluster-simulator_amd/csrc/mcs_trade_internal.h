@@ -1,0 +1,110 @@
+// mcs_trade_internal.h — device layout of the lock-step trading path (mcs_trade.h).
+//
+// HBM, per local cluster c (C_l of them) unless noted:
+//   tn      u64 packed {free_c | free_m << 32} per node (CSR node_off), live across ticks
+//   cl      TrCluster: queue cursors, counters, last utilization sample
+//   sfin    u32 [S] running-slot finish times (kEmpty = free); snode u32 [S]; scm u64 [S]
+//   lq      TrLq [LQ] LentQueue ring
+// Exchange records, indexed by GLOBAL cluster (C_t = world * C_l), all-gathered every tick:
+//   recA    TrRecA   borrow request of the tick (phase A -> B)
+//   acc_l   u32 [C_t] "some lender of this rank accepted borrower b" (phase B -> C);
+//   acc_all u32 [world][C_t] its gather
+//   recC    TrRecC   utilization sample + clock hints (phase C -> D)
+//   tr      TrTrader [C_t] trader/lock state, REPLICATED: every rank runs the identical trader
+//           rounds on identical gathered inputs
+//   ctl     TrCtl    the lock-step clock and log counters (replicated)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mcs_trade.h"
+#include "mcs_internal.h"
+
+namespace mcs {
+
+constexpr uint32_t kTrMaxNodes = 1024;     // nodes per cluster (LDS staging, 8 KB)
+constexpr uint32_t kTrMaxSlots = 4096;     // running slots per cluster (LDS staging, 16 KB)
+constexpr uint32_t kTrMaxClusters = 1024;  // clusters in one trading system (trader LDS state)
+
+struct TrCluster {
+    uint32_t next_arr;  // first job (local index) not yet queued; ready queue = [rq_head, next_arr)
+    uint32_t rq_head;
+    uint32_t has_w;     // WaitQueue head present (scheduler.go:219)
+    uint32_t w;         // its local index
+    uint32_t lq_head;   // LentQueue ring cursor and length
+    uint32_t lq_len;
+    uint32_t decided;   // own jobs placed or borrowed
+    uint32_t placed;
+    uint32_t waited;
+    uint32_t borrowed;
+    uint32_t minf;      // earliest running finish (kEmpty = none)
+    uint32_t nrun;
+    uint32_t peak;
+    uint32_t flags;     // MCS_FLAG_*
+    uint32_t lent_runs;
+    uint32_t total_c;   // SetTotalResources (cluster.go:26-40): uint32 sums of capacities
+    uint32_t total_m;
+    float cu, mu;       // latest utilization sample
+    uint32_t pad[3];
+};
+
+struct TrRecA {  // phase A -> B: the tick's borrow request (job == kEmpty: none)
+    uint32_t job, c, m, dur;
+};
+
+struct TrRecC {  // phase C -> D
+    float cu, mu;
+    uint32_t total_c, total_m;
+    uint32_t busy;        // wait head, ready jobs or lent jobs pending: next tick is T+1
+    uint32_t next_arr_t;  // arrival of the next unqueued job (kEmpty = none)
+    uint32_t done;        // every own job decided and the LentQueue empty
+    uint32_t flags;
+};
+
+struct TrTrader {  // replicated per global cluster
+    uint32_t lock_id, lock_until, next_id, next_due, vnodes;
+};
+
+struct TrLq {
+    uint32_t borrower, job, c, m, dur, pad0, pad1, pad2;
+};
+
+struct TrCtl {
+    uint32_t T, done, ticks, flags;
+    unsigned long long n_lent, n_trades, n_won;
+};
+
+struct TradeArgs {
+    uint32_t Cl, Ct, base, world;
+    uint32_t S, LQ, borrow, trader;
+    uint32_t period, ok_sleep, fail_sleep, lock_s;
+    uint32_t sample_period, t_max;
+    unsigned long long lent_cap, trade_cap;
+    const uint32_t* node_off;  // local CSR
+    const uint2* cap;          // {cores, memory} per node
+    const uint2* free0;        // JSON availability
+    unsigned long long* tn;
+    const uint4* jobs;
+    const uint64_t* job_off;
+    int32_t* out_node;
+    uint32_t* out_start;
+    uint32_t* out_finish;
+    TrCluster* cl;
+    uint32_t* sfin;
+    uint32_t* snode;
+    unsigned long long* scm;
+    TrLq* lq;
+    TrRecA* recA;
+    uint32_t* acc_l;
+    const uint32_t* acc_all;
+    TrRecC* recC;
+    TrTrader* tr;
+    TrCtl* ctl;
+    mcs_lent_rec* lent_log;
+    mcs_trade_rec* trade_log;
+};
+
+hipError_t launch_trade_init(const TradeArgs& a, hipStream_t s);
+hipError_t launch_trade_phase(const TradeArgs& a, int phase, hipStream_t s);
+
+}  // namespace mcs

@@ -1,0 +1,35 @@
+// mcs_wave.h — wave64 helpers shared by the gfx950 kernels (DPP reductions, lane broadcast).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mcs_internal.h"
+
+namespace mcs {
+
+__device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
+// unsigned min over the wave with DPP row shifts and row broadcasts (no LDS round trip):
+// rows of 16 lanes are scanned with row_shr 1/2/4/8, then row_bcast:15 / row_bcast:31 carry the
+// row minima upward; lane 63 ends with the wave minimum.  Lanes with no DPP source keep `old` =
+// kEmpty, the identity of min.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_min_step(uint32_t v) {
+    const uint32_t w =
+        (uint32_t)__builtin_amdgcn_update_dpp((int)kEmpty, (int)v, CTRL, ROW_MASK, 0xf, false);
+    return w < v ? w : v;
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = dpp_min_step<0x111, 0xf>(v);  // row_shr:1
+    v = dpp_min_step<0x112, 0xf>(v);  // row_shr:2
+    v = dpp_min_step<0x114, 0xf>(v);  // row_shr:4
+    v = dpp_min_step<0x118, 0xf>(v);  // row_shr:8
+    v = dpp_min_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    v = dpp_min_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+    return readlane(v, 63);
+}
+
+}  // namespace mcs

@@ -1,4 +1,4 @@
-"""ctypes binding of libmcs.so (include/mcs.h).
+"""ctypes binding of libmcs.so (include/mcs.h, include/mcs_trade.h).
 
 The library is loaded from this package directory (built in-tree by ``make`` /
 ``__graft_entry__.build()``).  There is no fallback: if the library is missing, or no HIP device
@@ -22,10 +22,14 @@ MCS_E_STATE = -5
 MCS_E_NOMEM = -6
 
 MCS_NODE_UNPLACED = -1
+MCS_NODE_BORROWED = -2
 MCS_TIME_NONE = 0xFFFFFFFF
 MCS_FLAG_DEADLOCK = 0x1
 MCS_FLAG_OVERFLOW = 0x2
 MCS_FLAG_CLOCK_OVERFLOW = 0x4
+MCS_FLAG_LENT_OVERFLOW = 0x8
+MCS_FLAG_LOG_OVERFLOW = 0x10
+MCS_FLAG_T_MAX = 0x20
 
 MCS_POLICY_FIFO = 0
 MCS_POLICY_DELAY = 1
@@ -58,7 +62,14 @@ class mcs_config(C.Structure):
         ("wait_sleep_s", C.c_uint32),
         ("idle_sleep_s", C.c_uint32),
         ("slot_pool", C.c_uint32),
-        ("reserved", C.c_uint32 * 10),
+        ("trader_period_s", C.c_uint32),
+        ("trade_ok_sleep_s", C.c_uint32),
+        ("trade_fail_sleep_s", C.c_uint32),
+        ("lock_s", C.c_uint32),
+        ("sample_period_s", C.c_uint32),
+        ("lent_queue_cap", C.c_uint32),
+        ("t_max_s", C.c_uint32),
+        ("reserved", C.c_uint32 * 3),
     ]
 
 
@@ -102,6 +113,38 @@ class mcs_cluster_stats(C.Structure):
     ]
 
 
+class mcs_lent_rec(C.Structure):
+    _fields_ = [("lender", C.c_uint32), ("borrower", C.c_uint32), ("job", C.c_uint64), ("node", C.c_uint32),
+                ("start_s", C.c_uint32), ("finish_s", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class mcs_trade_rec(C.Structure):
+    _fields_ = [("t_s", C.c_uint32), ("requester", C.c_uint32), ("winner", C.c_int32), ("approvals", C.c_uint32)]
+
+
+class mcs_trade_stats(C.Structure):
+    _fields_ = [
+        ("placed", C.c_uint64),
+        ("borrowed", C.c_uint64),
+        ("waited", C.c_uint64),
+        ("undecided", C.c_uint64),
+        ("lent_runs", C.c_uint64),
+        ("lent_pending", C.c_uint64),
+        ("trades", C.c_uint64),
+        ("trades_won", C.c_uint64),
+        ("ticks", C.c_uint32),
+        ("t_final", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("pad", C.c_uint32),
+        ("kernel_ms", C.c_double),
+        ("wall_ms", C.c_double),
+    ]
+
+
+class mcs_comm_id(C.Structure):
+    _fields_ = [("bytes", C.c_char * 128)]
+
+
 u32p = C.POINTER(C.c_uint32)
 i32p = C.POINTER(C.c_int32)
 u64p = C.POINTER(C.c_uint64)
@@ -133,6 +176,18 @@ SIGNATURES = [
     ("mcs_lend_check", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32, i32p]),
     ("mcs_read_live_state", C.c_int, [vp, C.c_uint32, u32p, u32p, C.c_uint32]),
     ("mcs_resource_utilization", C.c_int, [vp, C.c_uint32, f32p, f32p]),
+    # include/mcs_trade.h
+    ("mcs_set_shard", C.c_int, [vp, C.c_uint32, C.c_uint32]),
+    ("mcs_comm_unique_id", C.c_int, [C.POINTER(mcs_comm_id)]),
+    ("mcs_comm_init", C.c_int, [vp, C.POINTER(mcs_comm_id)]),
+    ("mcs_trade_begin", C.c_int, [vp]),
+    ("mcs_trade_xfer_bytes", C.c_int, [vp, C.c_uint32, u64p, u64p]),
+    ("mcs_trade_phase", C.c_int, [vp, C.c_uint32, vp, C.c_uint64, vp, C.c_uint64, u32p]),
+    ("mcs_trade_end", C.c_int, [vp, C.POINTER(mcs_stats)]),
+    ("mcs_read_trade_stats", C.c_int, [vp, C.POINTER(mcs_trade_stats)]),
+    ("mcs_read_lent", C.c_int, [vp, C.POINTER(mcs_lent_rec), C.c_uint64, u64p]),
+    ("mcs_read_trades", C.c_int, [vp, C.POINTER(mcs_trade_rec), C.c_uint64, u64p]),
+    ("mcs_read_virtual_nodes", C.c_int, [vp, u32p, C.c_uint32]),
 ]
 
 _lib = None

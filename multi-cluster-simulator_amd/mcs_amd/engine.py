@@ -120,13 +120,29 @@ CLUSTER_STATS_DTYPE = np.dtype([("t_end", "<u4"), ("placed", "<u4"), ("waited", 
                                 ("iterations", "<u4"), ("release_scans", "<u4")])
 
 
+LENT_DTYPE = np.dtype([("lender", "<u4"), ("borrower", "<u4"), ("job", "<u8"), ("node", "<u4"),
+                       ("start", "<u4"), ("finish", "<u4"), ("pad", "<u4")])
+TRADE_DTYPE = np.dtype([("t", "<u4"), ("requester", "<u4"), ("winner", "<i4"), ("approvals", "<u4")])
+
+
 class Engine:
     """One engine = one GPU (mcs_engine_create(cfg, device))."""
 
-    def __init__(self, device: int = 0, slot_pool: int = 0):
+    def __init__(self, device: int = 0, slot_pool: int = 0, borrow: bool = False, trader: bool = False,
+                 **cadences):
+        """borrow/trader select the lock-step trading path (include/mcs_trade.h); cadences
+        override mcs_config fields (trader_period_s, trade_ok_sleep_s, trade_fail_sleep_s, lock_s,
+        sample_period_s, lent_queue_cap, t_max_s)."""
         cfg = L.mcs_config()
         L.lib().mcs_config_default(C.byref(cfg))
         cfg.slot_pool = slot_pool
+        cfg.borrow = int(borrow)
+        cfg.trader = int(trader)
+        for k, v in cadences.items():
+            if k not in dict(L.mcs_config._fields_) or k in ("reserved", "policy"):
+                raise TypeError(f"unknown config field {k}")
+            setattr(cfg, k, int(v))
+        self.cfg = cfg
         h = C.c_void_p()
         rc = L.lib().mcs_engine_create(C.byref(cfg), device, C.byref(h))
         if rc != L.MCS_OK:
@@ -193,6 +209,82 @@ class Engine:
     @property
     def num_jobs(self) -> int:
         return int(L.lib().mcs_num_jobs(self._h))
+
+    # -- sharding / lock-step trading (include/mcs_trade.h) -----------------------------------
+    def set_shard(self, rank: int, world: int):
+        """This engine holds clusters [rank*C, rank*C+C) of world*C (call before generate_jobs:
+        generation is keyed by the global cluster index)."""
+        self._c(L.lib().mcs_set_shard(self._h, rank, world))
+        self.rank, self.world = rank, world
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        cid = L.mcs_comm_id()
+        rc = L.lib().mcs_comm_unique_id(C.byref(cid))
+        if rc != L.MCS_OK:
+            raise L.MCSError(rc, "mcs_comm_unique_id")
+        return bytes(C.string_at(C.addressof(cid), 128))
+
+    def comm_init(self, uid: bytes):
+        cid = L.mcs_comm_id()
+        C.memmove(C.addressof(cid), uid, 128)
+        self._c(L.lib().mcs_comm_init(self._h, C.byref(cid)))
+
+    def trade_begin(self):
+        self._c(L.lib().mcs_trade_begin(self._h))
+
+    def trade_xfer_bytes(self, phase: int):
+        i, o = C.c_uint64(), C.c_uint64()
+        self._c(L.lib().mcs_trade_xfer_bytes(self._h, phase, C.byref(i), C.byref(o)))
+        return i.value, o.value
+
+    def trade_phase(self, phase: int, inp: Optional[np.ndarray]):
+        """One phase of a tick (caller-driven transport).  Returns (out bytes as uint8 array, done)."""
+        ib, ob = self.trade_xfer_bytes(phase)
+        inp = np.ascontiguousarray(inp if inp is not None else np.zeros(0, np.uint8)).view(np.uint8)
+        if inp.nbytes != ib:
+            raise ValueError(f"phase {phase}: input has {inp.nbytes} bytes, expected {ib}")
+        out = np.empty(ob, np.uint8)
+        done = C.c_uint32()
+        self._c(L.lib().mcs_trade_phase(self._h, phase, inp.ctypes.data if ib else None, ib,
+                                        out.ctypes.data if ob else None, ob, C.byref(done)))
+        return out, bool(done.value)
+
+    def trade_end(self) -> RunStats:
+        st = L.mcs_stats()
+        self._c(L.lib().mcs_trade_end(self._h, C.byref(st)))
+        return RunStats(st.jobs, st.placed, st.waited, st.unplaced, st.clusters, st.deadlocked,
+                        st.escalations, st.slot_pool, st.kernel_ms, st.wall_ms)
+
+    def trade_stats(self) -> dict:
+        ts = L.mcs_trade_stats()
+        self._c(L.lib().mcs_read_trade_stats(self._h, C.byref(ts)))
+        return {k: getattr(ts, k) for k, _ in L.mcs_trade_stats._fields_ if k != "pad"}
+
+    def lent(self) -> np.ndarray:
+        """Lent runs of this engine's clusters (LENT_DTYPE), sorted by (start, lender, borrower, job)."""
+        n = C.c_uint64()
+        self._c(L.lib().mcs_read_lent(self._h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, LENT_DTYPE)
+        if n.value:
+            self._c(L.lib().mcs_read_lent(self._h, out.ctypes.data_as(C.POINTER(L.mcs_lent_rec)), n.value,
+                                          C.byref(n)))
+        return out
+
+    def trades(self) -> np.ndarray:
+        n = C.c_uint64()
+        self._c(L.lib().mcs_read_trades(self._h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, TRADE_DTYPE)
+        if n.value:
+            self._c(L.lib().mcs_read_trades(self._h, out.ctypes.data_as(C.POINTER(L.mcs_trade_rec)), n.value,
+                                            C.byref(n)))
+        return out
+
+    def virtual_nodes(self, n_total: Optional[int] = None) -> np.ndarray:
+        n_total = n_total if n_total is not None else self.num_clusters * getattr(self, "world", 1)
+        out = np.zeros(n_total, np.uint32)
+        self._c(L.lib().mcs_read_virtual_nodes(self._h, L.ptr(out, C.c_uint32), n_total))
+        return out
 
     # -- the hot path ---------------------------------------------------------------------------
     def run(self) -> RunStats:

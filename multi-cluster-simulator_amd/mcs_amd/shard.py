@@ -41,3 +41,38 @@ def aggregate(elapsed_s: float, placed: int, device=None) -> Tuple[float, float]
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dist.all_reduce(p, op=dist.ReduceOp.SUM)
     return float(t.item()), float(p.item())
+
+
+# ---- lock-step trading over a caller-provided transport (include/mcs_trade.h) ----------------
+def run_lockstep(engine, allgather):
+    """Drive the lock-step trading run of one shard through mcs_trade_phase.
+
+    `allgather(buf: np.ndarray[uint8]) -> np.ndarray[uint8]` must return the concatenation, in
+    rank order, of every rank's `buf` (all ranks call it the same number of times).  Every tick
+    is phases 0..3 with an all-gather between consecutive phases; phase 3 reports `done`
+    identically on every rank.  Returns the engine's RunStats."""
+    engine.trade_begin()
+    while True:
+        out, _ = engine.trade_phase(0, None)
+        out, _ = engine.trade_phase(1, allgather(out))
+        out, _ = engine.trade_phase(2, allgather(out))
+        _, done = engine.trade_phase(3, allgather(out))
+        if done:
+            return engine.trade_end()
+
+
+def torch_allgather(group=None):
+    """An `allgather` for run_lockstep over torch.distributed (e.g. gloo on the host)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+
+    def gather(buf):
+        t = torch.from_numpy(np.ascontiguousarray(buf, dtype=np.uint8).copy())
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t, group=group)
+        return torch.cat(outs).numpy()
+
+    return gather

@@ -61,7 +61,7 @@ typedef struct {
     int has_w;
     uint64_t w;                /* local index of the wait head */
     tr_lent* lq;
-    uint64_t lq_head, lq_len, lq_cap;
+    uint64_t lq_head, lq_len, lq_cap, lq_peak;
     tr_run* run;
     uint64_t nrun, caprun;
     uint32_t minf;             /* earliest finish among run[] (0xFFFFFFFF when empty) */
@@ -260,6 +260,7 @@ int or_trade_run(uint32_t C, const uint32_t* node_off, const uint32_t* cap_c, co
                         L->lq[L->lq_head + L->lq_len].borrower = b;
                         L->lq[L->lq_head + L->lq_len].job = g;
                         ++L->lq_len;
+                        if (L->lq_len > L->lq_peak) L->lq_peak = L->lq_len;
                         accepted = 1;
                     }
                 }
@@ -351,6 +352,7 @@ int or_trade_run(uint32_t C, const uint32_t* node_off, const uint32_t* cap_c, co
             cstats[c].virtual_nodes = cl[c].virtual_nodes;
             cstats[c].decided = (uint32_t)cl[c].decided;
             cstats[c].lent_pending = (uint32_t)cl[c].lq_len;
+            cstats[c].lent_peak = (uint32_t)cl[c].lq_peak;
         }
         free(cl[c].cap_c);
         free(cl[c].cap_m);

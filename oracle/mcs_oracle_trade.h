@@ -40,7 +40,7 @@ typedef struct {
 } or_trade_rec;
 
 typedef struct {
-    uint32_t virtual_nodes, decided, lent_pending, pad;
+    uint32_t virtual_nodes, decided, lent_pending, lent_peak; /* lent_peak: LentQueue high-water */
 } or_trade_cluster_stats;
 
 /* Lock-step run of C clusters (semantics in mcs_oracle_trade.c).  Own jobs: node >= 0 placed,

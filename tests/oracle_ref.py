@@ -38,7 +38,7 @@ class or_trade_rec(C.Structure):
 
 class or_trade_cluster_stats(C.Structure):
     _fields_ = [("virtual_nodes", C.c_uint32), ("decided", C.c_uint32), ("lent_pending", C.c_uint32),
-                ("pad", C.c_uint32)]
+                ("lent_peak", C.c_uint32)]
 
 
 LENT_DTYPE = np.dtype([("lender", "<u4"), ("borrower", "<u4"), ("job", "<u8"), ("node", "<u4"),
@@ -227,4 +227,5 @@ def trade_run(arrays, streams, borrow=True, trader=True, t_max=0xFFFFFFFE, lent_
                 n_lent=nl.value, trades=trades[: min(nt.value, trade_cap)].copy(), n_trades=nt.value,
                 virtual_nodes=np.array([c.virtual_nodes for c in cs[:k]], np.uint32),
                 decided=np.array([c.decided for c in cs[:k]], np.uint32),
-                lent_pending=np.array([c.lent_pending for c in cs[:k]], np.uint32), t_final=tf.value)
+                lent_pending=np.array([c.lent_pending for c in cs[:k]], np.uint32),
+                lent_peak=np.array([c.lent_peak for c in cs[:k]], np.uint32), t_final=tf.value)

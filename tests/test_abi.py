@@ -1,5 +1,5 @@
 """CPU tests of the C-ABI library (no compute calls that need a GPU): it loads, exports exactly
-what include/mcs.h declares, the host generator is deterministic and has the reference
+what include/*.h declare, the host generator is deterministic and has the reference
 distributions, and the spec loader follows Go's encoding/json rules."""
 import os
 import re
@@ -13,19 +13,22 @@ from mcs_amd import Cluster, GenParams, gen_cluster_host, scaled_lambda
 from mcs_amd import _lib as L
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(REPO, "include", "mcs.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in sorted(os.listdir(os.path.join(REPO, "include")))
+           if h.endswith(".h")]
 
 
 def header_functions():
-    txt = open(HEADER).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(mcs_[a-z0-9_]+)\s*\(", txt)))
+    names = set()
+    for h in HEADERS:
+        txt = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(mcs_[a-z0-9_]+)\s*\(", txt))
+    return sorted(names)
 
 
 def test_library_loads_and_exports_header_symbols():
     lib = mcs_amd.lib()
     declared = header_functions()
-    assert len(declared) >= 20
+    assert len(declared) >= 33
     out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True)
     exported = set(re.findall(r"\bT (mcs_[a-z0-9_]+)$", out.stdout, flags=re.M))
     missing = [f for f in declared if f not in exported]
@@ -33,7 +36,7 @@ def test_library_loads_and_exports_header_symbols():
     # every declared function has a ctypes signature in the binding
     bound = {name for name, _, _ in L.SIGNATURES}
     assert set(declared) == bound
-    assert lib.mcs_abi_version() == 1
+    assert lib.mcs_abi_version() == 2
 
 
 def test_library_is_gfx950_code_object():
@@ -103,3 +106,39 @@ def test_cluster_json_go_rules(tmp_path):
     assert c2.Nodes[0].MemoryAvailable == 0
     with pytest.raises(ValueError):
         Cluster.from_json('{"Id": 1, "Nodes": [{"Cores": -1}]}')
+
+
+def test_struct_layouts_match_headers(tmp_path):
+    """The ctypes mirrors have the C layout of include/*.h (sizes and every field offset)."""
+    import ctypes as C
+
+    structs = [L.mcs_config, L.mcs_gen_params, L.mcs_stats, L.mcs_cluster_stats, L.mcs_lent_rec,
+               L.mcs_trade_rec, L.mcs_trade_stats, L.mcs_comm_id]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mcs_trade.h"', "int main(void) {"]
+    for s in structs:
+        n = s.__name__
+        lines.append(f'printf("{n} %zu\\n", sizeof({n}));')
+        for f, _ in s._fields_:
+            cf = f.rstrip("_")  # ctypes name lambda_ -> C member lambda
+            lines.append(f'printf("{n}.{f} %zu\\n", offsetof({n}, {cf}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(REPO, "include"), "-o", str(exe), str(src)], check=True)
+    out = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                          check=True).stdout.split("\n") if l)
+    for s in structs:
+        n = s.__name__
+        assert int(out[n]) == C.sizeof(s), n
+        for f, _ in s._fields_:
+            assert int(out[f"{n}.{f}"]) == getattr(s, f).offset, f"{n}.{f}"
+
+
+def test_trading_engine_without_device_fails_loudly():
+    import torch
+
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a device is visible")
+    with pytest.raises(mcs_amd.MCSError):
+        mcs_amd.Engine(0, borrow=True, trader=True)

@@ -1,0 +1,119 @@
+"""GPU parity of the lock-step trading path (include/mcs_trade.h, mcs_trade.hip) against the CPU
+oracle (oracle/mcs_oracle_trade.c) and the hand-derived trade KATs.  Bit-exact on every output:
+own placements (node / borrowed, start, finish), the lent-run log, the trade log, the virtual
+nodes and the final tick.  Run on a real MI355X: ``pytest -m gpu``."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_ref as O
+from kat_util import seeded_workload
+from mcs_amd import Engine
+from mcs_amd.shard import run_lockstep
+from test_trade_oracle import kat_inputs, lent_rows, load_trade_kats, trade_rows
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def gpu_trade(arrays, streams, borrow=True, trader=True, driven=False, **cad):
+    cad.setdefault("t_max_s", 20_000_000)  # a stuck clock ends the run (flagged) instead of spinning
+    with Engine(0, borrow=borrow, trader=trader, **cad) as eng:
+        eng.load_clusters(arrays)
+        eng.submit_jobs(streams)
+        if driven:  # caller-driven transport with one rank: the gather is the identity
+            st = run_lockstep(eng, lambda b: b)
+        else:
+            st = eng.run()
+        node, start, fin = eng.placements()
+        return dict(node=node, start=start, finish=fin, lent=eng.lent(), trades=eng.trades(),
+                    virtual_nodes=eng.virtual_nodes(), stats=st, tstats=eng.trade_stats())
+
+
+def oracle_lent_local(res, streams):
+    """oracle lent records with the job as an index within the borrower's stream (the ABI's)."""
+    rows = lent_rows(res["lent"])
+    for r in rows:
+        r[2] -= int(streams.job_off[r[1]])
+    return sorted(rows)
+
+
+def assert_trade_parity(arrays, streams, g, borrow=True, trader=True):
+    o = O.trade_run(arrays, streams, borrow=borrow, trader=trader)
+    for k in ("node", "start", "finish"):
+        bad = np.flatnonzero(g[k] != o[k])
+        assert bad.size == 0, f"{k}: {bad.size} mismatches, first jobs {bad[:5]}: gpu {g[k][bad[:5]]} " \
+                              f"oracle {o[k][bad[:5]]}"
+    assert lent_rows(g["lent"]) == oracle_lent_local(o, streams)
+    assert trade_rows(g["trades"]) == trade_rows(o["trades"])
+    np.testing.assert_array_equal(g["virtual_nodes"], o["virtual_nodes"])
+    assert g["tstats"]["t_final"] == o["t_final"]
+    assert g["tstats"]["flags"] == 0, g["tstats"]["flags"]
+    return o
+
+
+@pytest.mark.parametrize("k", load_trade_kats(), ids=lambda k: k["name"].split()[0])
+def test_gpu_trade_kats(k):
+    arrays, streams = kat_inputs(k)
+    g = gpu_trade(arrays, streams, borrow=bool(k["borrow"]), trader=bool(k["trader"]))
+    e = k["expect"]
+    assert g["node"].tolist() == e["node"]
+    assert g["start"].tolist() == e["start"]
+    assert g["finish"].tolist() == e["finish"]
+    exp_lent = sorted([r[0], r[1], r[2] - int(streams.job_off[r[1]]), r[3], r[4], r[5]] for r in e["lent"])
+    assert lent_rows(g["lent"]) == exp_lent
+    assert trade_rows(g["trades"]) == e["trades"]
+    assert g["virtual_nodes"].tolist() == e["virtual_nodes"]
+    assert g["tstats"]["t_final"] == e["t_final"]
+
+
+@pytest.mark.parametrize("kind,C,J", [("small", 16, 2000), ("n64", 8, 3000), ("n64_hot", 8, 3000),
+                                      ("n256", 64, 1500)])
+def test_gpu_trade_seeded(kind, C, J):
+    arrays, streams, _ = seeded_workload(kind, C, J)
+    g = gpu_trade(arrays, streams)
+    o = assert_trade_parity(arrays, streams, g)
+    assert g["tstats"]["borrowed"] == int(np.sum(o["node"] == -2))
+
+
+@pytest.mark.parametrize("borrow,trader", [(True, False), (False, True)])
+def test_gpu_trade_one_side(borrow, trader):
+    arrays, streams, _ = seeded_workload("n64_hot", 6, 2000)
+    g = gpu_trade(arrays, streams, borrow=borrow, trader=trader)
+    assert_trade_parity(arrays, streams, g, borrow=borrow, trader=trader)
+
+
+def test_gpu_trade_caller_driven_equals_run():
+    arrays, streams, _ = seeded_workload("n64_hot", 8, 1500)
+    a = gpu_trade(arrays, streams)
+    b = gpu_trade(arrays, streams, driven=True)
+    for k in ("node", "start", "finish", "virtual_nodes"):
+        np.testing.assert_array_equal(a[k], b[k])
+    assert lent_rows(a["lent"]) == lent_rows(b["lent"])
+    assert trade_rows(a["trades"]) == trade_rows(b["trades"])
+
+
+def test_gpu_trade_cadences_and_small_lent_queue():
+    """Non-default cadences reach the kernels; a LentQueue overflow is reported, not ignored."""
+    arrays, streams, _ = seeded_workload("n64_hot", 6, 1500)
+    g = gpu_trade(arrays, streams, trader_period_s=20, trade_ok_sleep_s=60, trade_fail_sleep_s=30, lock_s=7)
+    o = O.trade_run(arrays, streams, period_s=20, trade_ok_sleep_s=60, trade_fail_sleep_s=30, lock_s=7)
+    assert trade_rows(g["trades"]) == trade_rows(o["trades"])
+    np.testing.assert_array_equal(g["node"], o["node"])
+    from mcs_amd import MCSError
+
+    with pytest.raises(MCSError):
+        gpu_trade(arrays, streams, lent_queue_cap=1)
+
+
+def test_gpu_trade_two_ranks_one_gpu():
+    """world = 2 shards (two processes, two engines on device 0) exchanging records over gloo via
+    the caller-driven phase API == one engine holding all clusters == the oracle."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29581")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "trade_2rank.py")], env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "TRADE-2RANK OK" in r.stdout
