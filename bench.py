@@ -43,7 +43,145 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes measured by a separate rocprofv3 --pmc pass")
-    return ap.parse_args()
+    ap.add_argument("--config", choices=["c4", "c5"], default="c4",
+                    help="c4: the headline FIFO benchmark; c5: the lock-step borrow + trader system "
+                         "(--clusters = clusters of the WHOLE system, sharded over the ranks)")
+    a = ap.parse_args()
+    if a.config == "c5":  # BASELINE.json configs[4]: 64 trading clusters, 10M jobs
+        if a.clusters == 4096:
+            a.clusters = 64
+        if a.jobs_per_cluster == 16384:
+            a.jobs_per_cluster = 156250
+        if a.cpu_sample_clusters == 512:
+            a.cpu_sample_clusters = 64
+    return a
+
+
+def cpu_baseline_c5(args, lam, sample_jobs):
+    """The trading oracle (oracle/mcs_oracle_trade.c, sequential lock-step, 1 thread) on the same
+    64-cluster system with shorter streams (sample_jobs per cluster)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ref as O
+    from mcs_amd import GenParams, replicate, uniform_cluster
+    from mcs_amd.engine import gen_streams_host
+
+    arrays = replicate(uniform_cluster(args.nodes), args.clusters)
+    gp = GenParams(seed=args.seed, arrival_mode=1, lam=lam)
+    streams = gen_streams_host(gp, arrays, sample_jobs)
+    O.lib()
+    t0 = time.perf_counter()
+    r = O.trade_run(arrays, streams, lent_cap=1, trade_cap=1)
+    dt = time.perf_counter() - t0
+    return {
+        "value": streams.n_jobs / dt,
+        "unit": "job decisions/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{args.clusters} clusters x {args.nodes} nodes x {sample_jobs} jobs ({streams.n_jobs} jobs, "
+                  f"{r['n_lent']} lent runs, {r['t_final']} ticks), oracle/mcs_oracle_trade.c -O3, 1 thread, "
+                  f"{dt:.2f} s wall",
+        "seconds": dt,
+    }
+
+
+def main_c5(args, world, rank, local_rank):
+    """C5: the whole trading system (args.clusters clusters) split in equal blocks over the ranks,
+    one lock-step run per step; the three per-tick record exchanges are RCCL all-gathers over xGMI
+    when world > 1 (mcs_trade.h)."""
+    import torch
+    import torch.distributed as dist
+
+    from mcs_amd import Engine, GenParams, replicate, uniform_cluster
+    from mcs_amd.engine import scaled_lambda
+    from mcs_amd.shard import aggregate
+
+    dist_on = world > 1
+    if dist_on:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend="nccl")
+    dev = torch.device("cuda", local_rank)
+    if args.clusters % world:
+        raise SystemExit(f"--clusters {args.clusters} must divide over {world} ranks")
+    per = args.clusters // world
+    lam = scaled_lambda(args.nodes, load=args.load)
+    eng = Engine(local_rank, borrow=True, trader=True)
+    eng.load_clusters(replicate(uniform_cluster(args.nodes), per))
+    eng.set_shard(rank, world)
+    eng.generate_jobs(GenParams(seed=args.seed, arrival_mode=1, lam=lam), args.jobs_per_cluster)
+    if dist_on:
+        box = [Engine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        eng.comm_init(box[0])
+    n_jobs = eng.num_jobs
+
+    def barrier():
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        eng.run()
+    barrier()
+    t0 = time.perf_counter()
+    kernel_ms, decided = [], 0
+    for _ in range(args.steps):
+        st = eng.run()
+        kernel_ms.append(st.kernel_ms)
+        decided += st.placed + (n_jobs - st.placed - st.unplaced)  # placed + borrowed
+    barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed_max, decided_all = aggregate(elapsed, decided, device=dev)
+    ts = eng.trade_stats()
+    _, lent_all = aggregate(0.0, ts["lent_runs"], device=dev)
+    if rank == 0:
+        avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+        per_launch = decided / args.steps
+        achieved = per_launch * BYTES_PER_PLACEMENT / avg_kernel_s / 1e9
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline_c5(args, lam, max(1, min(args.jobs_per_cluster, 8192)))
+        out = {
+            "metric": "trading-system job decisions/sec (placed locally or borrowed) at 64 clusters x 256 nodes",
+            "value": decided_all / elapsed_max,
+            "unit": "decisions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded device generator; scaled Poisson arrivals)",
+            "config": {
+                "workload": f"C5: {args.clusters} clusters x {args.nodes} nodes, FIFO + borrow + trader in lock-step, "
+                            f"{args.jobs_per_cluster} jobs/cluster ({args.clusters * args.jobs_per_cluster} jobs), "
+                            f"scaled arrivals at {args.load:.0%} memory load",
+                "clusters_total": args.clusters,
+                "nodes": args.nodes,
+                "jobs_per_cluster": args.jobs_per_cluster,
+                "parallelism": f"{world} shard(s); per-tick RCCL all-gathers" if dist_on else "1 GPU, exchange in HBM",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel": "lock-step tick (tr_step/tr_lend/tr_post/tr_trader), launch/latency-bound",
+                "kernel_ms_avg": avg_kernel_s * 1e3,
+                "bytes_per_placement": BYTES_PER_PLACEMENT,
+            },
+            "cpu_baseline": cpu,
+            "trading": {"ticks": ts["ticks"], "t_final": ts["t_final"], "us_per_tick": avg_kernel_s * 1e6 / max(ts["ticks"], 1),
+                        "borrowed": ts["borrowed"], "lent_runs_all_ranks": lent_all, "trades": ts["trades"],
+                        "trades_won": ts["trades_won"], "flags": ts["flags"]},
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist_on:
+        dist.destroy_process_group()
 
 
 def cpu_baseline(args, lam, n_threads):
@@ -81,6 +219,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    if args.config == "c5":
+        return main_c5(args, world, rank, local_rank)
 
     import torch
     import torch.distributed as dist

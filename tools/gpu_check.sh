@@ -13,6 +13,7 @@ mkdir -p "$OUT"
 cd "$ROOT"
 export PYTHONUNBUFFERED=1
 BENCH_ARGS="${BENCH_ARGS:-}"
+C5_ARGS="${C5_ARGS:-}"
 
 fatal() {  # rc of a GPU step -> 0 continue, 1 stop
     case "$1" in
@@ -28,6 +29,24 @@ for s in $STEPS; do
         timeout -k 10 840 python -m pytest tests -m gpu -q --timeout 400 -p no:cacheprovider \
             > "$OUT/pytest_gpu.log" 2>&1
         rc=$?; tail -25 "$OUT/pytest_gpu.log"; echo "pytest rc=$rc"; fatal $rc || exit $rc ;;
+    tradetests)
+        echo "== pytest -m gpu tests/test_gpu_trade.py"
+        timeout -k 10 600 python -m pytest tests/test_gpu_trade.py -m gpu -q --timeout 400 -p no:cacheprovider \
+            > "$OUT/pytest_trade.log" 2>&1
+        rc=$?; tail -25 "$OUT/pytest_trade.log"; echo "pytest rc=$rc"; fatal $rc || exit $rc ;;
+    c5)
+        echo "== bench C5 (lock-step trading)"
+        timeout -k 10 900 python bench.py --config c5 --steps 1 --warmup 1 $C5_ARGS > "$OUT/bench_c5.json" \
+            2> "$OUT/bench_c5.err"
+        rc=$?; cat "$OUT/bench_c5.json"; tail -5 "$OUT/bench_c5.err"; echo "c5 rc=$rc"; fatal $rc || exit $rc ;;
+    c5prof)
+        echo "== rocprofv3 kernel trace, C5"
+        ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats \
+            --output-format csv -d "$OUT/prof_c5" -o c5 -- python3 "$ROOT/bench.py" --config c5 --steps 1 \
+            --warmup 0 --no-cpu-baseline $C5_ARGS ) > "$OUT/prof_c5.log" 2>&1
+        rc=$?; tail -5 "$OUT/prof_c5.log"; echo "c5prof rc=$rc"
+        find "$OUT/prof_c5" -name "*stats*.csv" -exec sh -c 'echo "--- $1"; head -20 "$1"' _ {} \;
+        fatal $rc || exit $rc ;;
     smoke)
         echo "== smoke"
         timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
