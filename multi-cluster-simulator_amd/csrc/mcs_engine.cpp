@@ -255,7 +255,10 @@ static int alloc_jobs(mcs_engine* e, const uint64_t* job_offsets) {
     e->job_off.assign(job_offsets, job_offsets + e->C + 1);
     e->total_jobs = job_offsets[e->C];
     const size_t nj = e->total_jobs ? e->total_jobs : 1;
-    HIPCHK(e, hipMalloc(&e->d_jobs, nj * sizeof(uint4)));
+    /* kJobPad records of slack after the last cluster: the FIFO kernel streams 64-record batches
+     * one ahead without bounds masks (records past a cluster's end are read, never used) */
+    HIPCHK(e, hipMalloc(&e->d_jobs, (nj + mcs::kJobPad) * sizeof(uint4)));
+    HIPCHK(e, hipMemset(e->d_jobs + nj, 0, mcs::kJobPad * sizeof(uint4)));
     HIPCHK(e, hipMalloc(&e->d_job_off, (e->C + 1) * sizeof(uint64_t)));
     HIPCHK(e, hipMalloc(&e->d_out_node, nj * sizeof(int32_t)));
     HIPCHK(e, hipMalloc(&e->d_out_start, nj * sizeof(uint32_t)));

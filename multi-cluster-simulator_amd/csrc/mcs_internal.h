@@ -17,6 +17,7 @@ constexpr uint32_t kEmpty = 0xFFFFFFFFu;  // empty running slot (finish time nev
 constexpr int kWave = 64;
 constexpr int kMaxNpl = 16;   // nodes per lane -> at most 1024 nodes per cluster in ABI v1
 constexpr int kMaxPool = 32;  // running-slot registers per lane -> 2048 slots per cluster
+constexpr uint32_t kJobPad = 128;  // records of slack after the job array (unmasked batch loads)
 
 struct Totals {  // device-side accumulation of mcs_stats (only clusters that did not overflow)
     unsigned long long placed;

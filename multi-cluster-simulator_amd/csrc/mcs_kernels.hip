@@ -46,11 +46,11 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
 
     // Node free vectors staged in LDS as packed u64 {free_c, free_m}: commit is one ds_sub_u64
     // (the job fits, so the low half never borrows) and a release one ds_add_u64 (resources are
-    // conserved, so the low half never carries).  Node k lives at nodes[k]; nodes[NPL*64 + l] is
-    // lane l's write sink for lanes that do not commit.
-    __shared__ uint64_t nodes[(NPL + 1) * kWave];
-    __shared__ uint64_t pay_cm[(P + 1) * kWave];  // slot payload {cores, mem}; row P = write sink
-    __shared__ uint32_t pay_n[(P + 1) * kWave];   // slot node index
+    // conserved, so the low half never carries).  Node k lives at nodes[k].
+    __shared__ uint64_t nodes[NPL * kWave];
+    // running slots, row-major [P][64]: {cores | mem << 32} and {node | finish << 32}
+    __shared__ uint64_t pay_cm[P * kWave];
+    __shared__ uint64_t pay_nf[P * kWave];
 
     // ---- cluster spec: Run() keeps the JSON availability (scheduler.go:101-109) ----
     const uint32_t n0 = a.node_off[ci];
@@ -73,27 +73,32 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     uint32_t* __restrict__ o_start = a.out_start + j0;
     uint32_t* __restrict__ o_finish = a.out_finish + j0;
 
+    // Unmasked: the job array has kJobPad records of slack, and records past this cluster's end
+    // (the next cluster's, or the pad) are read but never used, because r < J guards every use.
+    // An unmasked load can land straight in the loop-carried batch registers, so the prefetch one
+    // batch ahead is not waited for until that batch is needed.
     auto load_batch = [&](uint32_t base) __attribute__((always_inline)) -> uint4 {
-        const uint32_t i = base + lane;
-        uint4 v = make_uint4(kEmpty, 0u, 0u, 0u);
-        if (i < J) v = jobs[i];
-        return v;
+        return jobs[base + lane];
     };
 
-    // running-slot finish times: row p in register sf[p] (static indices only); frm = this lane's
-    // free rows (bit p)
-    uint32_t sf[P];
-#pragma unroll
-    for (int p = 0; p < P; ++p) sf[p] = kEmpty;
+    // running slots: frm = this lane's free rows (bit p), lmin = earliest finish among its
+    // occupied rows (kEmpty if none); finish times and payloads live in LDS
     uint32_t frm = (P == 32) ? 0xFFFFFFFFu : ((1u << P) - 1u);
+    uint32_t lmin = kEmpty;
+#pragma unroll
+    for (int p = 0; p < P; ++p) pay_nf[p * kWave + lane] = (uint64_t)kEmpty << 32;  // free: never expires
 
     uint32_t cb = 0;
     uint4 cur = load_batch(0);
     uint4 nxt = load_batch(kWave);
 
-    uint32_t t = 0, r = 0, minf = kEmpty, used = 0, peak = 0, waited = 0, placed = 0, flags = 0;
+    uint32_t t = 0, r = 0, minf = kEmpty, flags = 0;
+    // Counters that no decision reads live in VGPRs (the asm hides their uniformity): the CU's
+    // one scalar unit is shared by 16 cluster waves and is the scarcer issue resource.
+    uint32_t used = 0, peak = 0, waited = 0, placed = 0;
     uint32_t n_iter = 0, n_rel = 0;  // diagnostics: loop passes, release scans
-    bool have_w = false;
+    asm volatile("" : "+v"(used), "+v"(peak), "+v"(waited), "+v"(placed), "+v"(n_iter), "+v"(n_rel));
+    uint32_t have_w = 0u;
     uint32_t wi = 0, wc = 0, wm = 0, wd = 0;
     int32_t on = -1;
     uint32_t os = kEmpty, of = kEmpty;
@@ -102,15 +107,19 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     auto release = [&]() __attribute__((always_inline)) {
         ++n_rel;
         uint32_t xm = 0u;  // this lane's expired rows
-        uint32_t lm = kEmpty;
+        uint32_t lm = lmin;
+        if (lmin <= t) {  // only lanes holding an expired slot scan their rows
+            lm = kEmpty;
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-            const bool ex = sf[p] <= t;
-            xm |= ex ? (1u << p) : 0u;
-            sf[p] = ex ? kEmpty : sf[p];
-            lm = sf[p] < lm ? sf[p] : lm;
+            for (int p = 0; p < P; ++p) {  // free rows hold kEmpty: never expired, min-neutral
+                const uint32_t f = (uint32_t)(pay_nf[p * kWave + lane] >> 32);
+                const bool live = f > t;
+                xm |= live ? 0u : (1u << p);
+                lm = live ? (f < lm ? f : lm) : lm;
+            }
+            frm |= xm;
         }
-        frm |= xm;
+        lmin = lm;
         // give the expired payloads back to their nodes, one expired row per lane per pass
         for (;;) {
             const uint64_t b = __ballot(xm != 0u);
@@ -119,10 +128,12 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
             if (xm != 0u) {
                 const uint32_t ad = (uint32_t)(__ffs(xm) - 1) * kWave + lane;
                 xm &= xm - 1u;
-                atomicAdd((unsigned long long*)&nodes[pay_n[ad]], (unsigned long long)pay_cm[ad]);
+                const uint64_t nf = pay_nf[ad];
+                atomicAdd((unsigned long long*)&nodes[(uint32_t)nf], (unsigned long long)pay_cm[ad]);
+                pay_nf[ad] = nf | ((uint64_t)kEmpty << 32);  // the row is free again
             }
         }
-        minf = wave_min_u32(lm);
+        minf = wave_min_u32(lmin);
     };
 
     auto flush = [&](uint32_t base) __attribute__((always_inline)) {
@@ -137,7 +148,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     // ---- Scheduler.Fifo (scheduler.go:216-296) ----
     // One pass = one decision; the loop has a single exit (the structurizer then needs no flow
     // copies of the loop-carried registers).
-    bool stop = false;
+    uint32_t stop = 0u;
     do {
         ++n_iter;
         // ReadyQueue head (:255-260): the next stream job, queued once its arrival has passed
@@ -148,14 +159,17 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         }
         const uint32_t l = (r - cb) & 63u;
         const uint32_t arr = readlane(cur.x, l);
+        const uint32_t rd = readlane(cur.y, l);
+        const uint32_t rc = readlane(cur.z, l);
+        const uint32_t rm = readlane(cur.w, l);
         // candidate: the wait head (:219-222) or the ready head
         const uint32_t ji = have_w ? wi : r;
-        const uint32_t jd = have_w ? wd : readlane(cur.y, l);
-        const uint32_t jc = have_w ? wc : readlane(cur.z, l);
-        const uint32_t jm = have_w ? wm : readlane(cur.w, l);
+        const uint32_t jd = have_w ? wd : rd;
+        const uint32_t jc = have_w ? wc : rc;
+        const uint32_t jm = have_w ? wm : rm;
         uint32_t tn = t;
         if (!have_w && r >= J) {  // every job decided
-            stop = true;
+            stop = 1u;
         } else if (!have_w && arr > t) {  // all queues empty: 1 s sleeps to the arrival (:294)
             tn = arr;
         } else {
@@ -184,38 +198,33 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                 if (jd != 0u) {
                     const uint64_t need = (uint64_t)jc | ((uint64_t)jm << 32);
                     // commit — Node.RunJob, cluster.go:146-147 (synchronous, D2)
-                    const uint32_t cad = lane == (k & 63u) ? k : NPL * kWave + lane;
-                    atomicSub((unsigned long long*)&nodes[cad], (unsigned long long)need);
+                    if (lane == (k & 63u)) atomicSub((unsigned long long*)&nodes[k], (unsigned long long)need);
                     // slot insert: the lowest lane with a free row, its lowest free row
                     const uint64_t any = __ballot(frm != 0u);
                     if (!any) {
                         flags |= MCS_FLAG_OVERFLOW;
-                        stop = true;
+                        stop = 1u;
                     } else {
-                        const uint32_t L = (uint32_t)__builtin_ctzll(any);
-                        const bool ime = lane == L;
-                        uint32_t frme = ime ? (uint32_t)(__ffs(frm) - 1) : 0xFFu;
-                        asm volatile("" : "+v"(frme));  // keep the row test per-lane VALU
-#pragma unroll
-                        for (int p = 0; p < P; ++p) sf[p] = frme == (uint32_t)p ? fin : sf[p];
-                        frm = ime ? (frm & (frm - 1u)) : frm;
-                        const uint32_t ad = ime ? frme * kWave + lane : (uint32_t)P * kWave + lane;
-                        pay_cm[ad] = need;
-                        pay_n[ad] = k;
+                        if (lane == (uint32_t)__builtin_ctzll(any)) {
+                            const uint32_t ad = (uint32_t)(__ffs(frm) - 1) * kWave + lane;
+                            frm &= frm - 1u;
+                            pay_cm[ad] = need;
+                            pay_nf[ad] = (uint64_t)k | ((uint64_t)fin << 32);
+                            lmin = fin < lmin ? fin : lmin;
+                        }
                         ++used;
                         peak = used > peak ? used : peak;
                         minf = fin < minf ? fin : minf;
                     }
                 }
-                if (have_w) {     // WaitQueue = WaitQueue[1:] (:226; D1)
-                    have_w = false;
-                    tn = t + 1u;  // time.Sleep(1 s) after every wait attempt (:250)
-                } else {
-                    ++r;          // ready path: no sleep (:272)
-                }
+                // wait head: WaitQueue = WaitQueue[1:] (:226; D1) and time.Sleep(1 s) (:250);
+                // ready head: next job, no sleep (:272)
+                tn = t + have_w;
+                r += 1u - have_w;
+                have_w = 0u;
             } else {
                 if (!have_w) {  // State = WAITING; WaitQueue append (:264-268)
-                    have_w = true;
+                    have_w = 1u;
                     wi = ji;
                     wc = jc;
                     wm = jm;
@@ -227,7 +236,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                 }
                 if (minf == kEmpty) {  // nothing running: the head can never fit
                     flags |= MCS_FLAG_DEADLOCK;
-                    stop = true;
+                    stop = 1u;
                 } else {  // A.3: 1 s retries until the next completion (no lender, :234)
                     tn = minf > t + 1u ? minf : t + 1u;
                 }
@@ -236,7 +245,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         if (!stop && tn != t) {
             if (tn < t) {  // the u32 seconds clock would wrap (D8 range exceeded): stop, flagged
                 flags |= MCS_FLAG_CLOCK_OVERFLOW;
-                stop = true;
+                stop = 1u;
             } else {
                 t = tn;
                 if (minf <= t) release();

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmcs.so")
+# MCS_LIB overrides the library path (A/B timing of kernel variants, tools/ab_bench.py)
+LIB_PATH = os.environ.get("MCS_LIB") or os.path.join(_HERE, "libmcs.so")
 
 MCS_OK = 0
 MCS_NO_FIT = 1

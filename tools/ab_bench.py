@@ -1,0 +1,52 @@
+"""A/B timing of libmcs.so kernel variants on the C4 workload in ONE process per variant,
+alternating variants round-robin so box-to-box and thermal drift cancel.
+
+usage: python tools/ab_bench.py lib_a.so lib_b.so [...] [--rounds 3] [--steps 5]
+Each variant runs in its own subprocess (MCS_LIB=<path>) per round; prints median kernel ms."""
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r'''
+import json, os, sys
+sys.path.insert(0, os.path.join(os.environ["REPO"], "multi-cluster-simulator_amd"))
+from mcs_amd import Engine, GenParams, replicate, uniform_cluster
+from mcs_amd.engine import scaled_lambda
+steps = int(os.environ["STEPS"])
+eng = Engine(0)
+eng.load_clusters(replicate(uniform_cluster(256), 4096))
+eng.generate_jobs(GenParams(arrival_mode=1, lam=scaled_lambda(256, load=0.9)), 16384)
+eng.run()
+ms = [eng.run().kernel_ms for _ in range(steps)]
+print(json.dumps({"ms": ms}))
+'''
+
+
+def main():
+    args = sys.argv[1:]
+    rounds, steps = 3, 5
+    if "--rounds" in args:
+        i = args.index("--rounds"); rounds = int(args[i + 1]); del args[i:i + 2]
+    if "--steps" in args:
+        i = args.index("--steps"); steps = int(args[i + 1]); del args[i:i + 2]
+    res = {a: [] for a in args}
+    for _ in range(rounds):
+        for lib in args:
+            env = dict(os.environ, MCS_LIB=os.path.abspath(lib), REPO=REPO, STEPS=str(steps))
+            out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True,
+                                 timeout=300)
+            if out.returncode != 0:
+                print(lib, "FAILED", out.stderr[-2000:])
+                sys.exit(1)
+            res[lib] += json.loads(out.stdout.strip().splitlines()[-1])["ms"]
+    for lib, ms in res.items():
+        print(f"{os.path.basename(lib):28s} median {statistics.median(ms):8.3f} ms  min {min(ms):8.3f}  "
+              f"max {max(ms):8.3f}  ({67108864 / statistics.median(ms) / 1e6:.3f}e9 placements/s)")
+
+
+if __name__ == "__main__":
+    main()
