@@ -98,8 +98,9 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     uint32_t used = 0, peak = 0, waited = 0, placed = 0;
     uint32_t n_iter = 0, n_rel = 0;  // diagnostics: loop passes, release scans
     asm volatile("" : "+v"(used), "+v"(peak), "+v"(waited), "+v"(placed), "+v"(n_iter), "+v"(n_rel));
+    // have_w: the job at the ready cursor r already failed once and is the WaitQueue head
+    // (|WaitQueue| <= 1, scheduler.go:264-268), so the candidate is always job r
     uint32_t have_w = 0u;
-    uint32_t wi = 0, wc = 0, wm = 0, wd = 0;
     int32_t on = -1;
     uint32_t os = kEmpty, of = kEmpty;
 
@@ -152,26 +153,21 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     do {
         ++n_iter;
         // ReadyQueue head (:255-260): the next stream job, queued once its arrival has passed
-        if (!have_w && r - cb >= (uint32_t)kWave && r < J) {
+        if (r - cb >= (uint32_t)kWave) {
             cur = nxt;
             cb += kWave;
             nxt = load_batch(cb + kWave);
         }
         const uint32_t l = (r - cb) & 63u;
         const uint32_t arr = readlane(cur.x, l);
-        const uint32_t rd = readlane(cur.y, l);
-        const uint32_t rc = readlane(cur.z, l);
-        const uint32_t rm = readlane(cur.w, l);
-        // candidate: the wait head (:219-222) or the ready head
-        const uint32_t ji = have_w ? wi : r;
-        const uint32_t jd = have_w ? wd : rd;
-        const uint32_t jc = have_w ? wc : rc;
-        const uint32_t jm = have_w ? wm : rm;
+        const uint32_t jd = readlane(cur.y, l);
+        const uint32_t jc = readlane(cur.z, l);
+        const uint32_t jm = readlane(cur.w, l);
         uint32_t tn = t;
-        if (!have_w && r >= J) {  // every job decided
+        if (r >= J) {  // every job decided
             stop = 1u;
-        } else if (!have_w && arr > t) {  // all queues empty: 1 s sleeps to the arrival (:294)
-            tn = arr;
+        } else if (arr > t) {  // all queues empty: 1 s sleeps to the arrival (:294); a wait head
+            tn = arr;          // has always arrived, so this is never taken with have_w
         } else {
             // first fit — ScheduleJob, scheduler.go:129-137: lowest node index with both >=;
             // each lane keeps its lowest fitting node, then a DPP wave minimum
@@ -185,14 +181,14 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
             const uint32_t k = wave_min_u32(best);
             if (k != kEmpty) {
                 // placement record, 64 jobs per register batch (jobs are placed in job order)
-                const uint32_t ol = ji & 63u;
+                const uint32_t ol = r & 63u;
                 const uint32_t fin = t + jd;
                 const bool pme = lane == ol;
                 on = pme ? (int32_t)k : on;
                 os = pme ? t : os;
                 of = pme ? fin : of;
                 ++placed;
-                if (ol == 63u) flush(ji - 63u);
+                if (ol == 63u) flush(r - 63u);
                 // A zero-duration job is committed and released before the next decision can
                 // read the node (RunJob sleeps 0; the release precedes the next branch, D3).
                 if (jd != 0u) {
@@ -220,20 +216,14 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                 // wait head: WaitQueue = WaitQueue[1:] (:226; D1) and time.Sleep(1 s) (:250);
                 // ready head: next job, no sleep (:272)
                 tn = t + have_w;
-                r += 1u - have_w;
+                ++r;
                 have_w = 0u;
             } else {
-                if (!have_w) {  // State = WAITING; WaitQueue append (:264-268)
-                    have_w = 1u;
-                    wi = ji;
-                    wc = jc;
-                    wm = jm;
-                    wd = jd;
-                    ++waited;
-                    ++r;
-                    // The Go loop's next pass retries the new head at this same instant on an
-                    // unchanged cluster (certain to fail), then sleeps: folded in here.
-                }
+                // State = WAITING; WaitQueue append (:264-268).  The Go loop's next pass retries
+                // the new head at this same instant on an unchanged cluster (certain to fail),
+                // then sleeps: folded into the fast-forward below.
+                waited += 1u - have_w;
+                have_w = 1u;
                 if (minf == kEmpty) {  // nothing running: the head can never fit
                     flags |= MCS_FLAG_DEADLOCK;
                     stop = 1u;
@@ -254,9 +244,9 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     } while (!stop);
 
     if (flags & MCS_FLAG_DEADLOCK) {
-        // jobs wi..J-1 are never placed (the Go loop retries the head forever)
-        const uint32_t b0 = wi & ~63u;
-        if (lane >= (wi & 63u)) {
+        // jobs r..J-1 are never placed (the Go loop retries the head forever)
+        const uint32_t b0 = r & ~63u;
+        if (lane >= (r & 63u)) {
             on = MCS_NODE_UNPLACED;
             os = MCS_TIME_NONE;
             of = MCS_TIME_NONE;
