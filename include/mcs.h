@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MCS_ABI_VERSION 2
+#define MCS_ABI_VERSION 3
 
 /* ---- status codes --------------------------------------------------------------------------- */
 typedef enum mcs_status {
@@ -61,11 +61,12 @@ typedef enum mcs_status {
 /* ---- configuration ------------------------------------------------------------------------- */
 typedef enum mcs_policy {
     MCS_POLICY_FIFO = 0,  /* Scheduler.Fifo (scheduler.go:216-296); selected by config (D4)       */
-    MCS_POLICY_DELAY = 1  /* Scheduler.Delay (scheduler.go:298-369); not implemented in ABI v1    */
+    MCS_POLICY_DELAY = 1  /* Scheduler.Delay (scheduler.go:298-369), the reference default (:116);
+                             serialized semantics SDELAY; ABI v3                   */
 } mcs_policy;
 
 typedef struct mcs_config {
-    uint32_t policy;         /* mcs_policy; MCS_POLICY_FIFO only                                    */
+    uint32_t policy;         /* mcs_policy                                                         */
     uint32_t borrow;         /* FIFO cross-cluster borrow (server.go:160-248; mcs_trade.h)          */
     uint32_t trader;         /* trader offer exchange (trader.go:193-325; mcs_trade.h)              */
     uint32_t wait_sleep_s;   /* sleep after a wait-queue attempt, scheduler.go:250 (must be 1)     */
@@ -79,7 +80,8 @@ typedef struct mcs_config {
     uint32_t sample_period_s;    /* 5: scheduler state stream period, trader_server.go:44           */
     uint32_t lent_queue_cap;     /* LentQueue entries per cluster (0 = 4096)                        */
     uint32_t t_max_s;            /* stop the lock-step clock after this tick (0 = 0xFFFFFFFE)       */
-    uint32_t reserved[3];
+    uint32_t max_wait_s;         /* DELAY: Policy.MaxWaitTime, 10 s (scheduler.go:115,353)          */
+    uint32_t reserved[2];
 } mcs_config;
 
 /* Fills the reference defaults (FIFO, no borrow, no trader, 1 s sleeps, trader cadences above). */
@@ -142,6 +144,18 @@ typedef struct mcs_cluster_stats {
     uint32_t release_scans; /* diagnostics: clock advances that released running jobs            */
 } mcs_cluster_stats;
 
+/* DELAY-policy statistics of one cluster (MCS_POLICY_DELAY runs; mcs_read_delay_stats). */
+typedef struct mcs_delay_cluster_stats {
+    int64_t total_wait_ms;  /* WaitTime.TotalTime at t_end (scheduler.go:48-54,309-312,338-341):
+                               1000 * (start - arrival) per placed job, 1000 * (t_end - arrival)
+                               per job left in Level1                                             */
+    int64_t jobs_count;     /* WaitTime.JobsCount: jobs received by "/delay" (server.go:72)         */
+    uint32_t moved_l1;      /* Level0 -> Level1 moves after MaxWaitTime (scheduler.go:353-359)      */
+    uint32_t placed_l1;     /* placements made by the Level1 pass (scheduler.go:302-329)           */
+    uint32_t peak_l1;       /* peak len(Level1)                                                    */
+    uint32_t l1_left;       /* Level1 jobs that can never fit (MCS_FLAG_DEADLOCK)                  */
+} mcs_delay_cluster_stats;
+
 /* scheduler.Run (scheduler.go:101-124) builds a Scheduler; here one engine batches many clusters
  * on ONE GPU (`device` = HIP ordinal). */
 int mcs_engine_create(const mcs_config* cfg, int device, mcs_engine** out);
@@ -170,16 +184,23 @@ int mcs_generate_jobs(mcs_engine* eng, const mcs_gen_params* p, uint64_t jobs_pe
 int mcs_read_jobs(mcs_engine* eng, uint32_t* arrival_s, uint32_t* dur_s, uint32_t* cores,
                   uint32_t* mem);
 
-/* Runs the FIFO policy loop (Scheduler.Fifo, scheduler.go:216-296, over ScheduleJob
- * scheduler.go:127-139 and Node.RunJob cluster.go:141-161) for every cluster from its loaded spec
- * until every job is placed (t_end_s = MCS_TIME_NONE; other horizons are reserved).
- * Serialized semantics SFIFO, SURVEY Appendix A.  With cfg.borrow or cfg.trader set the clusters
- * instead advance in lock-step with the borrow and trade exchanges (mcs_trade.h). */
+/* Runs the configured policy loop for every cluster from its loaded spec until every job is
+ * placed (t_end_s = MCS_TIME_NONE; other horizons are reserved), over ScheduleJob
+ * (scheduler.go:127-139) and Node.RunJob (cluster.go:141-161):
+ *   MCS_POLICY_FIFO  — Scheduler.Fifo (scheduler.go:216-296), serialized semantics SFIFO
+ *                      (SURVEY Appendix A); with cfg.borrow or cfg.trader set the clusters instead
+ *                      advance in lock-step with the borrow and trade exchanges (mcs_trade.h);
+ *   MCS_POLICY_DELAY — Scheduler.Delay (scheduler.go:298-369) with jobs ingested by the "/delay"
+ *                      handler (server.go:53-78), serialized semantics SDELAY.
+ *                      MCS_FLAG_DEADLOCK marks clusters whose Level1 keeps jobs that can never
+ *                      fit; those jobs get MCS_NODE_UNPLACED and every other job is placed. */
 int mcs_run(mcs_engine* eng, uint32_t t_end_s, mcs_stats* stats);
 
 /* Per-job results of the last mcs_run, indexed like the submitted jobs. */
 int mcs_read_placements(mcs_engine* eng, int32_t* node, uint32_t* start_s, uint32_t* finish_s);
 int mcs_read_cluster_stats(mcs_engine* eng, mcs_cluster_stats* out, uint32_t n_clusters);
+/* DELAY statistics of the last MCS_POLICY_DELAY run (MCS_E_STATE after a FIFO run). */
+int mcs_read_delay_stats(mcs_engine* eng, mcs_delay_cluster_stats* out, uint32_t n_clusters);
 
 uint32_t mcs_num_clusters(const mcs_engine* eng);
 uint64_t mcs_num_jobs(const mcs_engine* eng);

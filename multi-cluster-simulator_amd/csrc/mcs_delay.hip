@@ -1,0 +1,436 @@
+// mcs_delay.hip — gfx950 kernel of the DELAY policy (Scheduler.Delay, pkg/scheduler/scheduler.go:
+// 298-369, the reference's shipped default, scheduler.go:116) for one cluster per wave64
+// workgroup, under the serialized semantics SDELAY (oracle/mcs_oracle_delay.c).
+//
+// One Delay iteration at time t (every iteration ends in time.Sleep(1 s), :367):
+//   * releases due at t (cluster.go:153-157) — the same wave-parallel slot scan as fifo_kernel;
+//   * the Level1 pass (:302-329): every Level1 job in list order gets ScheduleJob; a placed job is
+//     removed with append(Level1[:i], Level1[i+1:]...) and no i--, so the job sliding into slot i
+//     is skipped this pass (D6, replicated);
+//   * the Level0 head (:332-366): ScheduleJob; on failure it moves to the Level1 tail once it has
+//     waited MaxWaitTime (10 s, :353).
+//
+// Layout and the MI355X choices:
+//   * node free vectors, running slots and releases are fifo_kernel's (LDS packed u64 nodes,
+//     first fit = per-lane select + DPP wave minimum, commit = one ds_sub_u64);
+//   * Level0 is a cursor h into the arrival-sorted SoA stream (jobs leave Level0 in stream order,
+//     either placed or moved), streamed 64 records at a time like fifo_kernel's ready queue;
+//   * Level1 is a dense list in HBM scratch (capacity = the cluster's job count, so it never
+//     overflows): {cores | mem << 32} and {job | dur << 32}, 16 B per entry.  A pass reads it 64
+//     entries per coalesced load (sc1: served by L2, never a stale L1 line of this CU) and
+//     compacts it in the same sweep, so removals cost no extra pass;
+//   * an exact per-lane fit filter rejects most Level1 entries without a first fit: lane l holds
+//     best[l] = max free memory over nodes with min(free cores, 63) >= l (an LDS ds_max_u32
+//     histogram + a wave suffix max), so job (c, m) can fit iff c <= max free cores and
+//     best[min(c, 63)] >= m (exact for c < 63, conservative above).  Resources only shrink
+//     inside a pass, so a job rejected at the start of the pass stays rejected; the survivors get
+//     a real first fit in list order;
+//   * Level0 results leave in 64-job register batches (masked: moved jobs are written when Level1
+//     places them); Level1 results are three single-lane stores.
+// Fast-forward: after an iteration that placed and moved nothing, the next iteration that can
+// change anything is the next release, the Level0 head's MaxWaitTime move, or (empty Level0) the
+// next arrival — the skipped iterations repeat the same failures (exact, oracle-tested).
+#define MCS_GEN_FN __host__ __device__ static inline
+#include "mcs_internal.h"
+#include "mcs_wave.h"
+
+namespace mcs {
+
+// unsigned max over the wave (DPP row shifts + row broadcasts, identity 0), see wave_min_u32
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#define MCS_DPP_MAX(CTRL, RM)                                                                      \
+    {                                                                                              \
+        const uint32_t w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xf, false); \
+        v = w > v ? w : v;                                                                         \
+    }
+    MCS_DPP_MAX(0x111, 0xf)
+    MCS_DPP_MAX(0x112, 0xf)
+    MCS_DPP_MAX(0x114, 0xf)
+    MCS_DPP_MAX(0x118, 0xf)
+    MCS_DPP_MAX(0x142, 0xa)
+    MCS_DPP_MAX(0x143, 0xc)
+#undef MCS_DPP_MAX
+    return readlane(v, 63);
+}
+
+// HBM scratch of the Level1 list, read by the wave that wrote it: bypass this CU's vector L1.
+__device__ __forceinline__ uint64_t ld_l2(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NPL, int P>
+__global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
+    static_assert(P <= 32, "free-row mask is one u32 per lane");
+    const uint32_t item = blockIdx.x;
+    const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
+    const uint32_t lane = threadIdx.x;
+
+    __shared__ uint64_t nodes[NPL * kWave];
+    __shared__ uint64_t pay_cm[P * kWave];
+    __shared__ uint64_t pay_nf[P * kWave];
+    __shared__ uint32_t hist[kWave];
+
+    // ---- cluster spec: Run() keeps the JSON availability (scheduler.go:101-109) ----
+    const uint32_t n0 = a.node_off[ci];
+    const uint32_t N = a.node_off[ci + 1] - n0;
+    uint32_t nid[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+        const uint32_t idx = k * kWave + lane;
+        uint2 v = make_uint2(0u, 0u);
+        if (idx < N) v = a.node_free0[n0 + idx];
+        nodes[idx] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        nid[k] = idx < N ? idx : kEmpty;
+    }
+
+    const uint64_t j0 = a.job_off[ci];
+    const uint32_t J = (uint32_t)(a.job_off[ci + 1] - j0);
+    const uint4* __restrict__ jobs = a.jobs + j0;
+    int32_t* __restrict__ o_node = a.out_node + j0;
+    uint32_t* __restrict__ o_start = a.out_start + j0;
+    uint32_t* __restrict__ o_finish = a.out_finish + j0;
+    uint64_t* l1_cm = a.l1_cm + j0;  // Level1 entries: {cores | mem << 32}
+    uint64_t* l1_jd = a.l1_jd + j0;  //                  {job | dur << 32}
+    const uint32_t max_wait = a.max_wait_s;
+
+    uint32_t frm = (P == 32) ? 0xFFFFFFFFu : ((1u << P) - 1u);
+    uint32_t lmin = kEmpty;
+#pragma unroll
+    for (int p = 0; p < P; ++p) pay_nf[p * kWave + lane] = (uint64_t)kEmpty << 32;
+
+    uint32_t cb = 0;
+    uint4 cur = jobs[lane];
+    uint4 nxt = jobs[kWave + lane];
+
+    uint32_t t = 0, h = 0, l1n = 0, minf = kEmpty, flags = 0;
+    uint32_t used = 0, peak = 0, placed = 0, moved = 0, placed_l1 = 0, peak_l1 = 0;
+    uint32_t n_iter = 0, n_rel = 0;
+    uint64_t sum_start = 0, sum_arr = 0;  // WaitTime.TotalTime = 1000 * (sum_start - sum_arr)
+    asm volatile("" : "+v"(used), "+v"(peak), "+v"(n_iter), "+v"(n_rel));
+    // Level0 result batch: lane (job & 63) holds its record; ov = written by Level0
+    int32_t on = -1;
+    uint32_t os = kEmpty, of = kEmpty, ov = 0u;
+
+    auto release = [&]() __attribute__((always_inline)) {
+        ++n_rel;
+        uint32_t xm = 0u;
+        uint32_t lm = lmin;
+        if (lmin <= t) {
+            lm = kEmpty;
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const uint32_t f = (uint32_t)(pay_nf[p * kWave + lane] >> 32);
+                const bool live = f > t;
+                xm |= live ? 0u : (1u << p);
+                lm = live ? (f < lm ? f : lm) : lm;
+            }
+            frm |= xm;
+        }
+        lmin = lm;
+        for (;;) {
+            const uint64_t b = __ballot(xm != 0u);
+            if (!b) break;
+            used -= (uint32_t)__builtin_popcountll(b);
+            if (xm != 0u) {
+                const uint32_t ad = (uint32_t)(__ffs(xm) - 1) * kWave + lane;
+                xm &= xm - 1u;
+                const uint64_t nf = pay_nf[ad];
+                atomicAdd((unsigned long long*)&nodes[(uint32_t)nf], (unsigned long long)pay_cm[ad]);
+                pay_nf[ad] = nf | ((uint64_t)kEmpty << 32);
+            }
+        }
+        minf = wave_min_u32(lmin);
+    };
+
+    // ScheduleJob (scheduler.go:127-139): lowest node index with both >=
+    auto first_fit = [&](uint32_t jc, uint32_t jm) __attribute__((always_inline)) -> uint32_t {
+        asm volatile("" ::: "memory");  // another lane may have committed since the last read
+        uint32_t best = kEmpty;
+#pragma unroll
+        for (int k = NPL - 1; k >= 0; --k) {
+            const uint64_t v = nodes[k * kWave + lane];
+            const uint32_t x = (uint32_t)v >= jc ? nid[k] : kEmpty;
+            best = (uint32_t)(v >> 32) >= jm ? (x < best ? x : best) : best;
+        }
+        return wave_min_u32(best);
+    };
+
+    // Node.RunJob commit (cluster.go:144-148, synchronous D2) and the running slot; returns false
+    // on slot-pool overflow.  A zero-duration job is committed and released before the next
+    // ScheduleJob can read the node, so it changes nothing.
+    auto commit = [&](uint32_t k, uint32_t jc, uint32_t jm, uint32_t fin, uint32_t jd)
+        __attribute__((always_inline)) -> bool {
+        if (jd == 0u) return true;
+        const uint64_t need = (uint64_t)jc | ((uint64_t)jm << 32);
+        if (lane == (k & 63u)) atomicSub((unsigned long long*)&nodes[k], (unsigned long long)need);
+        const uint64_t any = __ballot(frm != 0u);
+        if (!any) return false;
+        if (lane == (uint32_t)__builtin_ctzll(any)) {
+            const uint32_t ad = (uint32_t)(__ffs(frm) - 1) * kWave + lane;
+            frm &= frm - 1u;
+            pay_cm[ad] = need;
+            pay_nf[ad] = (uint64_t)k | ((uint64_t)fin << 32);
+            lmin = fin < lmin ? fin : lmin;
+        }
+        ++used;
+        peak = used > peak ? used : peak;
+        minf = fin < minf ? fin : minf;
+        return true;
+    };
+
+    auto flush = [&](uint32_t base) __attribute__((always_inline)) {
+        const uint32_t i = base + lane;
+        if (ov && i < J) {
+            __builtin_nontemporal_store(on, o_node + i);
+            __builtin_nontemporal_store(os, o_start + i);
+            __builtin_nontemporal_store(of, o_finish + i);
+        }
+        ov = 0u;
+    };
+
+    uint32_t stop = (J == 0u) ? 1u : 0u;
+    while (!stop) {
+        ++n_iter;
+        uint32_t changed = 0u;
+        // node and slot state in LDS is updated by single lanes and read by all: no value may be
+        // carried in registers across iterations
+        asm volatile("" ::: "memory");
+
+        // ---- Level1 pass (scheduler.go:302-329) ----
+        if (l1n != 0u) {
+            // fit filter: best[l] = max free mem over nodes with min(free cores, 63) >= l
+            hist[lane] = 0u;
+            uint32_t mc = 0u;
+#pragma unroll
+            for (int k = 0; k < NPL; ++k) {
+                const uint64_t v = nodes[k * kWave + lane];
+                const uint32_t fc = (uint32_t)v;
+                if (nid[k] != kEmpty) {
+                    atomicMax(&hist[fc < 63u ? fc : 63u], (uint32_t)(v >> 32));
+                    mc = fc > mc ? fc : mc;
+                }
+            }
+            const uint32_t max_c = wave_max_u32(mc);
+            // the histogram is written by other lanes: without a fence the compiler may forward
+            // this lane's own 0 store to the load below (it reasons per thread)
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            uint32_t best = hist[lane];
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const uint32_t w = (uint32_t)__shfl_down((int)best, o);
+                best = (lane + o < (uint32_t)kWave && w > best) ? w : best;
+            }
+
+            uint32_t wr = 0u, skip = kEmpty;
+            for (uint32_t base = 0; base < l1n && !stop; base += kWave) {
+                const uint32_t pos = base + lane;
+                const bool live = pos < l1n;
+                const uint64_t cm = live ? ld_l2(l1_cm + pos) : 0ull;
+                const uint64_t jdv = live ? ld_l2(l1_jd + pos) : 0ull;
+                const uint32_t c = (uint32_t)cm, m = (uint32_t)(cm >> 32);
+                const uint32_t bm = (uint32_t)__shfl((int)best, (int)(c < 63u ? c : 63u));
+                uint64_t cand = __ballot(live && c <= max_c && bm >= m);
+                uint64_t rem = 0ull;
+                while (cand) {
+                    const uint32_t b = (uint32_t)__builtin_ctzll(cand);
+                    cand &= cand - 1ull;
+                    if (base + b == skip) continue;  // slid into slot i: not examined (D6)
+                    const uint32_t jc = readlane(c, b), jm = readlane(m, b);
+                    const uint32_t k = first_fit(jc, jm);
+                    if (k == kEmpty) continue;
+                    const uint32_t jw = readlane((uint32_t)jdv, b);
+                    const uint32_t jd = readlane((uint32_t)(jdv >> 32), b);
+                    const uint32_t fin = t + jd;
+                    if (!commit(k, jc, jm, fin, jd)) {
+                        flags |= MCS_FLAG_OVERFLOW;
+                        stop = 1u;
+                        break;
+                    }
+                    if (lane == 0u) {
+                        o_node[jw] = (int32_t)k;
+                        o_start[jw] = t;
+                        o_finish[jw] = fin;
+                    }
+                    rem |= 1ull << b;
+                    skip = base + b + 1u;
+                    ++placed;
+                    ++placed_l1;
+                    sum_start += t;
+                    changed = 1u;
+                }
+                // compaction in the same sweep: survivors move down to the write cursor
+                const uint64_t kept = __ballot(live) & ~rem;
+                if ((wr != base || rem != 0ull) && live && !((rem >> lane) & 1ull)) {
+                    const uint32_t np = wr + (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                                                 (uint32_t)(kept >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)kept, 0u));
+                    if (np != pos) {
+                        l1_cm[np] = cm;
+                        l1_jd[np] = jdv;
+                    }
+                }
+                wr += (uint32_t)__builtin_popcountll(kept);
+            }
+            if (!stop) l1n = wr;
+        }
+
+        // ---- Level0 head (scheduler.go:332-366) ----
+        if (!stop && h < J) {
+            if (h - cb >= (uint32_t)kWave) {
+                cur = nxt;
+                cb += kWave;
+                nxt = jobs[cb + kWave + lane];
+            }
+            const uint32_t l = (h - cb) & 63u;
+            const uint32_t arr = readlane(cur.x, l);
+            if (arr <= t) {  // Level0 is non-empty: its head has arrived
+                const uint32_t jd = readlane(cur.y, l);
+                const uint32_t jc = readlane(cur.z, l);
+                const uint32_t jm = readlane(cur.w, l);
+                const uint32_t k = first_fit(jc, jm);
+                const uint32_t ol = h & 63u;
+                if (k != kEmpty) {
+                    const uint32_t fin = t + jd;
+                    if (!commit(k, jc, jm, fin, jd)) {
+                        flags |= MCS_FLAG_OVERFLOW;
+                        stop = 1u;
+                    } else {
+                        const bool pme = lane == ol;
+                        on = pme ? (int32_t)k : on;
+                        os = pme ? t : os;
+                        of = pme ? fin : of;
+                        ov = pme ? 1u : ov;
+                        ++placed;
+                        sum_start += t;
+                        sum_arr += arr;
+                        ++h;
+                        changed = 1u;
+                    }
+                } else if (t - arr >= max_wait) {  // time.Since(WaitTime) >= MaxWaitTime (:353)
+                    if (lane == 0u) {
+                        l1_cm[l1n] = (uint64_t)jc | ((uint64_t)jm << 32);
+                        l1_jd[l1n] = (uint64_t)h | ((uint64_t)jd << 32);
+                    }
+                    ++l1n;
+                    peak_l1 = l1n > peak_l1 ? l1n : peak_l1;
+                    ++moved;
+                    sum_arr += arr;
+                    ++h;
+                    changed = 1u;
+                }
+                if (changed && (h & 63u) == 0u) flush(h - 64u);
+            }
+        }
+        // Level1 stores must be visible to the next pass's L2 loads
+        if (changed) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+
+        // ---- time.Sleep(1 s) (:367) and the fast-forward ----
+        if (stop) break;
+        if (h >= J && l1n == 0u) {  // every job placed: the run ends at the next iteration
+            t += 1u;
+            break;
+        }
+        if (!changed && minf == kEmpty && h >= J) {  // Level1 jobs that can never fit
+            flags |= MCS_FLAG_DEADLOCK;
+            break;
+        }
+        uint32_t tn = t + 1u;
+        if (!changed) {
+            uint32_t ev = minf;
+            if (h < J) {
+                const uint32_t arr = readlane(cur.x, (h - cb) & 63u);
+                const uint32_t e2 = arr <= t ? arr + max_wait : arr;
+                ev = e2 < ev ? e2 : ev;
+            }
+            tn = ev > tn ? ev : tn;
+        }
+        if (tn <= t) {
+            flags |= MCS_FLAG_CLOCK_OVERFLOW;
+            break;
+        }
+        t = tn;
+        if (minf <= t) release();
+    }
+
+    if (!(flags & (MCS_FLAG_OVERFLOW | MCS_FLAG_CLOCK_OVERFLOW))) {
+        if ((h & 63u) != 0u) flush(h & ~63u);
+        if (flags & MCS_FLAG_DEADLOCK) {
+            // the Level1 jobs left are retried forever: never placed
+            for (uint32_t base = 0; base < l1n; base += kWave) {
+                const uint32_t pos = base + lane;
+                if (pos < l1n) {
+                    const uint32_t jw = (uint32_t)ld_l2(l1_jd + pos);
+                    o_node[jw] = MCS_NODE_UNPLACED;
+                    o_start[jw] = MCS_TIME_NONE;
+                    o_finish[jw] = MCS_TIME_NONE;
+                }
+            }
+        }
+    }
+    // WaitTime.TotalTime (scheduler.go:309-312,338-341): a placed job keeps 1000 * (start -
+    // arrival); a job left in Level1 holds 1000 * (t - arrival) from the last pass.  sum_arr
+    // already counts every job Level0 placed or moved, so the left jobs add l1n * t.
+    const uint32_t left = (flags & MCS_FLAG_DEADLOCK) ? l1n : 0u;
+    const uint64_t wait_s = sum_start + (uint64_t)left * t - sum_arr;
+
+    if (lane == 0) {
+        mcs_cluster_stats st;
+        st.t_end = t;
+        st.placed = placed;
+        st.waited = moved;
+        st.peak_running = peak;
+        st.flags = flags;
+        st.pool = (uint32_t)P;
+        st.iterations = n_iter;
+        st.release_scans = n_rel;
+        a.cstats[ci] = st;
+        mcs_delay_cluster_stats ds;
+        ds.total_wait_ms = (int64_t)(wait_s * 1000ull);
+        ds.jobs_count = (int64_t)J;  // every job has arrived when the run ends
+        ds.moved_l1 = moved;
+        ds.placed_l1 = placed_l1;
+        ds.peak_l1 = peak_l1;
+        ds.l1_left = left;
+        a.dstats[ci] = ds;
+        if (flags & MCS_FLAG_OVERFLOW) {
+            atomicAdd(&a.totals->overflowed, 1u);
+        } else {
+            atomicAdd(&a.totals->placed, (unsigned long long)placed);
+            atomicAdd(&a.totals->waited, (unsigned long long)moved);
+            atomicAdd(&a.totals->unplaced, (unsigned long long)(J - placed));
+            if (flags & MCS_FLAG_DEADLOCK) atomicAdd(&a.totals->deadlocked, 1u);
+        }
+    }
+}
+
+template <int NPL, int P>
+static hipError_t launch_delay_one(const DelayArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((delay_kernel<NPL, P>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    return hipGetLastError();
+}
+
+template <int NPL>
+static hipError_t launch_delay_npl(const DelayArgs& a, int pool, hipStream_t s) {
+    switch (pool) {
+        case 2: return launch_delay_one<NPL, 2>(a, s);
+        case 4: return launch_delay_one<NPL, 4>(a, s);
+        case 8: return launch_delay_one<NPL, 8>(a, s);
+        case 16: return launch_delay_one<NPL, 16>(a, s);
+        case 32: return launch_delay_one<NPL, 32>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_delay(const DelayArgs& a, int npl, int pool, hipStream_t s) {
+    if (a.n_items == 0) return hipSuccess;
+    switch (npl) {
+        case 1: return launch_delay_npl<1>(a, pool, s);
+        case 2: return launch_delay_npl<2>(a, pool, s);
+        case 4: return launch_delay_npl<4>(a, pool, s);
+        case 8: return launch_delay_npl<8>(a, pool, s);
+        case 16: return launch_delay_npl<16>(a, pool, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace mcs

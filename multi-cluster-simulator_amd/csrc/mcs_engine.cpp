@@ -30,6 +30,7 @@ void free_clusters(mcs_engine* e) {
     dfree(e->d_max_c);
     dfree(e->d_max_m);
     dfree(e->d_cstats);
+    dfree(e->d_dstats);
     dfree(e->d_list);
 }
 
@@ -39,6 +40,8 @@ void free_jobs(mcs_engine* e) {
     dfree(e->d_out_node);
     dfree(e->d_out_start);
     dfree(e->d_out_finish);
+    dfree(e->d_l1_cm);
+    dfree(e->d_l1_jd);
 }
 
 int npl_for(uint32_t max_n) {
@@ -81,6 +84,7 @@ void mcs_config_default(mcs_config* cfg) {
     cfg->sample_period_s = 5;      /* trader_server.go:44 */
     cfg->lent_queue_cap = 0;
     cfg->t_max_s = 0;
+    cfg->max_wait_s = 10; /* sched.Policy.MaxWaitTime = 10 * time.Second, scheduler.go:115 */
 }
 
 void mcs_gen_params_default(mcs_gen_params* p) {
@@ -123,9 +127,11 @@ int mcs_engine_create(const mcs_config* cfg, int device, mcs_engine** out) {
         c = *cfg;
     else
         mcs_config_default(&c);
-    if (c.policy != MCS_POLICY_FIFO || c.borrow > 1 || c.trader > 1 || c.wait_sleep_s != 1 ||
+    if (c.policy > MCS_POLICY_DELAY || c.borrow > 1 || c.trader > 1 || c.wait_sleep_s != 1 ||
         c.idle_sleep_s != 1)
-        return MCS_E_INVALID; /* FIFO with the reference sleeps */
+        return MCS_E_INVALID; /* FIFO or DELAY with the reference sleeps */
+    if (c.policy == MCS_POLICY_DELAY && (c.borrow || c.trader))
+        return MCS_E_INVALID; /* Delay never borrows (scheduler.go:298-369); DELAY trading: mcs_trade.h */
     if (c.borrow || c.trader) {
         if (c.trader && (c.trader_period_s == 0 || c.sample_period_s == 0 || c.lock_s == 0))
             return MCS_E_INVALID;
@@ -235,6 +241,7 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
     HIPCHK(e, hipMalloc(&e->d_max_c, n_clusters * sizeof(uint32_t)));
     HIPCHK(e, hipMalloc(&e->d_max_m, n_clusters * sizeof(uint32_t)));
     HIPCHK(e, hipMalloc(&e->d_cstats, n_clusters * sizeof(mcs_cluster_stats)));
+    HIPCHK(e, hipMalloc(&e->d_dstats, n_clusters * sizeof(mcs_delay_cluster_stats)));
     HIPCHK(e, hipMalloc(&e->d_list, n_clusters * sizeof(uint32_t)));
     HIPCHK(e, hipMemcpy(e->d_free0, free0.data(), nb * sizeof(uint2), hipMemcpyHostToDevice));
     HIPCHK(e, hipMemcpy(e->d_cap, cap.data(), nb * sizeof(uint2), hipMemcpyHostToDevice));
@@ -376,6 +383,13 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     if (t_end_s != MCS_TIME_NONE) return fail(e, MCS_E_INVALID, "finite horizons are reserved");
     if (e->cfg.borrow || e->cfg.trader) return mcs::trade_run(e, stats);
     e->trade_run = false;
+    const bool delay = e->cfg.policy == MCS_POLICY_DELAY;
+    e->delay_run = delay;
+    if (delay && !e->d_l1_cm) { /* Level1 can hold every job of its cluster: never overflows */
+        const size_t nj = e->total_jobs ? e->total_jobs : 1;
+        HIPCHK(e, hipMalloc(&e->d_l1_cm, nj * sizeof(uint64_t)));
+        HIPCHK(e, hipMalloc(&e->d_l1_jd, nj * sizeof(uint64_t)));
+    }
     const auto w0 = std::chrono::steady_clock::now();
     const int npl = npl_for(e->max_n ? e->max_n : 1);
     int pool = e->cfg.slot_pool ? (int)e->cfg.slot_pool : auto_pool(e->max_n);
@@ -393,6 +407,22 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     a.cstats = e->d_cstats;
     a.totals = e->d_totals;
     a.n_items = e->C;
+    mcs::DelayArgs da{};
+    da.node_free0 = e->d_free0;
+    da.node_off = e->d_node_off;
+    da.jobs = e->d_jobs;
+    da.job_off = e->d_job_off;
+    da.cluster_list = nullptr;
+    da.out_node = e->d_out_node;
+    da.out_start = e->d_out_start;
+    da.out_finish = e->d_out_finish;
+    da.l1_cm = e->d_l1_cm;
+    da.l1_jd = e->d_l1_jd;
+    da.cstats = e->d_cstats;
+    da.dstats = e->d_dstats;
+    da.totals = e->d_totals;
+    da.max_wait_s = e->cfg.max_wait_s;
+    da.n_items = e->C;
 
     double kms = 0.0;
     uint32_t escalations = 0;
@@ -401,7 +431,10 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     mcs::Totals tot{};
     for (;;) {
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));
-        HIPCHK(e, mcs::launch_fifo(a, npl, pool, e->stream));
+        if (delay)
+            HIPCHK(e, mcs::launch_delay(da, npl, pool, e->stream));
+        else
+            HIPCHK(e, mcs::launch_fifo(a, npl, pool, e->stream));
         HIPCHK(e, hipEventRecord(e->ev1, e->stream));
         HIPCHK(e, hipMemcpyAsync(&tot, e->d_totals, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -422,8 +455,8 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
         HIPCHK(e, hipMemcpy(e->d_list, list.data(), list.size() * sizeof(uint32_t),
                             hipMemcpyHostToDevice));
         HIPCHK(e, hipMemsetAsync(&e->d_totals->overflowed, 0, sizeof(unsigned int), e->stream));
-        a.cluster_list = e->d_list;
-        a.n_items = (uint32_t)list.size();
+        a.cluster_list = da.cluster_list = e->d_list;
+        a.n_items = da.n_items = (uint32_t)list.size();
         pool *= 2;
         ++escalations;
     }
@@ -463,6 +496,16 @@ int mcs_read_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n_clu
     if (e->trade_run) return mcs::trade_cluster_stats(e, out, n_clusters);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipMemcpy(out, e->d_cstats, n_clusters * sizeof(mcs_cluster_stats),
+                        hipMemcpyDeviceToHost));
+    return MCS_OK;
+}
+
+int mcs_read_delay_stats(mcs_engine* e, mcs_delay_cluster_stats* out, uint32_t n_clusters) {
+    if (int st = check_engine(e)) return st;
+    if (!e->has_run || !e->delay_run) return fail(e, MCS_E_STATE, "no DELAY run");
+    if (!out || n_clusters > e->C) return fail(e, MCS_E_INVALID, "bad output");
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(out, e->d_dstats, n_clusters * sizeof(mcs_delay_cluster_stats),
                         hipMemcpyDeviceToHost));
     return MCS_OK;
 }

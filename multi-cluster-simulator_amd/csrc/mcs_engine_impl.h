@@ -43,6 +43,10 @@ struct mcs_engine {
     uint32_t* d_out_start = nullptr;
     uint32_t* d_out_finish = nullptr;
     mcs_cluster_stats* d_cstats = nullptr;
+    mcs_delay_cluster_stats* d_dstats = nullptr;
+    uint64_t* d_l1_cm = nullptr;  // DELAY Level1 scratch (allocated by the first DELAY run)
+    uint64_t* d_l1_jd = nullptr;
+    bool delay_run = false;       // results of the last run come from the DELAY kernel
     mcs::Totals* d_totals = nullptr;
     uint32_t* d_list = nullptr;
     int32_t* d_scratch = nullptr;

@@ -41,6 +41,26 @@ struct FifoArgs {
     uint32_t n_items;
 };
 
+struct DelayArgs {
+    const uint2* node_free0;
+    const uint32_t* node_off;
+    const uint4* jobs;
+    const uint64_t* job_off;
+    const uint32_t* cluster_list;  // grid item -> cluster (nullptr = identity)
+    int32_t* out_node;
+    uint32_t* out_start;
+    uint32_t* out_finish;
+    uint64_t* l1_cm;  // Level1 scratch, one entry per job: {cores | mem << 32}
+    uint64_t* l1_jd;  //                                    {job | dur << 32}
+    mcs_cluster_stats* cstats;
+    mcs_delay_cluster_stats* dstats;
+    Totals* totals;
+    uint32_t max_wait_s;
+    uint32_t n_items;
+};
+
+hipError_t launch_delay(const DelayArgs& a, int npl, int pool, hipStream_t s);  // mcs_delay.hip
+
 // Launchers (mcs_kernels.hip).  Return hipSuccess or the launch error.
 hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, hipStream_t s);
 bool fifo_variant_exists(int npl, int pool);

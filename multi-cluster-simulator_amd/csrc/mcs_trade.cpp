@@ -454,6 +454,7 @@ int mcs_trade_end(mcs_engine* e, mcs_stats* stats) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
     e->has_run = true;
     e->trade_run = true;
+    e->delay_run = false;
     mcs_trade_stats ts{};
     mcs_stats st{};
     if (int s = mcs::fill_stats(e, &ts, &st)) return s;

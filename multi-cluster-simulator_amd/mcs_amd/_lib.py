@@ -70,7 +70,8 @@ class mcs_config(C.Structure):
         ("sample_period_s", C.c_uint32),
         ("lent_queue_cap", C.c_uint32),
         ("t_max_s", C.c_uint32),
-        ("reserved", C.c_uint32 * 3),
+        ("max_wait_s", C.c_uint32),
+        ("reserved", C.c_uint32 * 2),
     ]
 
 
@@ -111,6 +112,17 @@ class mcs_cluster_stats(C.Structure):
         ("pool", C.c_uint32),
         ("iterations", C.c_uint32),
         ("release_scans", C.c_uint32),
+    ]
+
+
+class mcs_delay_cluster_stats(C.Structure):
+    _fields_ = [
+        ("total_wait_ms", C.c_int64),
+        ("jobs_count", C.c_int64),
+        ("moved_l1", C.c_uint32),
+        ("placed_l1", C.c_uint32),
+        ("peak_l1", C.c_uint32),
+        ("l1_left", C.c_uint32),
     ]
 
 
@@ -170,6 +182,7 @@ SIGNATURES = [
     ("mcs_run", C.c_int, [vp, C.c_uint32, C.POINTER(mcs_stats)]),
     ("mcs_read_placements", C.c_int, [vp, i32p, u32p, u32p]),
     ("mcs_read_cluster_stats", C.c_int, [vp, C.POINTER(mcs_cluster_stats), C.c_uint32]),
+    ("mcs_read_delay_stats", C.c_int, [vp, C.POINTER(mcs_delay_cluster_stats), C.c_uint32]),
     ("mcs_num_clusters", C.c_uint32, [vp]),
     ("mcs_num_jobs", C.c_uint64, [vp]),
     ("mcs_schedule_one", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32, i32p]),

@@ -120,6 +120,9 @@ CLUSTER_STATS_DTYPE = np.dtype([("t_end", "<u4"), ("placed", "<u4"), ("waited", 
                                 ("iterations", "<u4"), ("release_scans", "<u4")])
 
 
+DELAY_STATS_DTYPE = np.dtype([("total_wait_ms", "<i8"), ("jobs_count", "<i8"), ("moved_l1", "<u4"),
+                              ("placed_l1", "<u4"), ("peak_l1", "<u4"), ("l1_left", "<u4")])
+
 LENT_DTYPE = np.dtype([("lender", "<u4"), ("borrower", "<u4"), ("job", "<u8"), ("node", "<u4"),
                        ("start", "<u4"), ("finish", "<u4"), ("pad", "<u4")])
 TRADE_DTYPE = np.dtype([("t", "<u4"), ("requester", "<u4"), ("winner", "<i4"), ("approvals", "<u4")])
@@ -129,12 +132,17 @@ class Engine:
     """One engine = one GPU (mcs_engine_create(cfg, device))."""
 
     def __init__(self, device: int = 0, slot_pool: int = 0, borrow: bool = False, trader: bool = False,
-                 **cadences):
-        """borrow/trader select the lock-step trading path (include/mcs_trade.h); cadences
-        override mcs_config fields (trader_period_s, trade_ok_sleep_s, trade_fail_sleep_s, lock_s,
-        sample_period_s, lent_queue_cap, t_max_s)."""
+                 policy: str = "FIFO", **cadences):
+        """policy "FIFO" (Scheduler.Fifo) or "DELAY" (Scheduler.Delay, the reference default);
+        borrow/trader select the lock-step trading path (include/mcs_trade.h); cadences override
+        mcs_config fields (trader_period_s, trade_ok_sleep_s, trade_fail_sleep_s, lock_s,
+        sample_period_s, lent_queue_cap, t_max_s, max_wait_s)."""
         cfg = L.mcs_config()
         L.lib().mcs_config_default(C.byref(cfg))
+        if policy not in ("FIFO", "DELAY"):
+            raise ValueError(f"unknown policy {policy!r}")
+        cfg.policy = L.MCS_POLICY_DELAY if policy == "DELAY" else L.MCS_POLICY_FIFO
+        self.policy = policy
         cfg.slot_pool = slot_pool
         cfg.borrow = int(borrow)
         cfg.trader = int(trader)
@@ -308,6 +316,14 @@ class Engine:
         self._c(L.lib().mcs_read_cluster_stats(self._h, out.ctypes.data_as(C.POINTER(L.mcs_cluster_stats)), n))
         return out
 
+    def delay_stats(self) -> np.ndarray:
+        """Per-cluster DELAY statistics of the last DELAY run (DELAY_STATS_DTYPE)."""
+        n = self.num_clusters
+        out = np.zeros(n, DELAY_STATS_DTYPE)
+        self._c(L.lib().mcs_read_delay_stats(self._h, out.ctypes.data_as(C.POINTER(L.mcs_delay_cluster_stats)),
+                                             n))
+        return out
+
     # -- single-job mirrors (live state) --------------------------------------------------------
     def schedule_one(self, cluster: int, cores: int, mem: int) -> int:
         node = C.c_int32(-1)
@@ -360,4 +376,4 @@ def roofline_placements_per_s(peak_bytes_per_s: float = 8.0e12) -> float:
 
 
 __all__ = ["Engine", "GenParams", "JobStreams", "RunStats", "gen_cluster_host", "gen_streams_host",
-           "scaled_lambda", "device_count", "CLUSTER_STATS_DTYPE", "math"]
+           "scaled_lambda", "device_count", "CLUSTER_STATS_DTYPE", "DELAY_STATS_DTYPE", "math"]

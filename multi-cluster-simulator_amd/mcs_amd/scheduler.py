@@ -8,6 +8,9 @@ Same names, argument meaning and error behaviour as the Go code (errors are *ret
   Scheduler.Lend(j) -> error        scheduler.go:194-202
   Scheduler.JobFinished(j, node)    cluster.go:153-160 (the release half of Node.RunJob)
   Scheduler.Fifo(stream)            scheduler.go:216-296, run to completion over a job stream
+  Scheduler.Delay(stream)           scheduler.go:298-369 (the reference default, :116), jobs
+                                    ingested by "/delay" (server.go:53-78); WaitTime statistics
+  WaitTime.GetAverage()             scheduler.go:56-63
   Cluster.GetResourceUtilization()  cluster.go:46-63 (here Scheduler.GetResourceUtilization)
 
 All decisions run on the GPU through libmcs.so.
@@ -63,14 +66,30 @@ class Placement:
     Finish: int
 
 
-class Scheduler:
-    """One reference scheduler process == one cluster on an engine."""
+@dataclass
+class WaitTime:
+    """scheduler.go:47-54 — wait-time statistics in milliseconds, as of the end of the last run."""
 
-    def __init__(self, engine: Optional[Engine] = None, device: int = 0):
-        self._eng = engine if engine is not None else Engine(device)
-        self.SchedulingAlgorithm = FIFO
+    TotalTime: int = 0
+    JobsCount: int = 0
+
+    def GetAverage(self) -> float:
+        """scheduler.go:56-63."""
+        if self.JobsCount != 0:
+            return float(self.TotalTime) / float(self.JobsCount)
+        return 0.0
+
+
+class Scheduler:
+    """One reference scheduler process == one cluster on an engine.  policy FIFO or DELAY (the
+    reference hard-codes DELAY at scheduler.go:116; here it is selected, D4)."""
+
+    def __init__(self, engine: Optional[Engine] = None, device: int = 0, policy: str = FIFO):
+        self._eng = engine if engine is not None else Engine(device, policy=policy)
+        self.SchedulingAlgorithm = self._eng.policy
         self.Cluster: Optional[Cluster] = None
         self.URL = ""
+        self.WaitTime = WaitTime()
 
     @property
     def engine(self) -> Engine:
@@ -109,6 +128,21 @@ class Scheduler:
     def Fifo(self, arrivals: Sequence[int], jobs: Sequence[Job]) -> List[Placement]:
         """Scheduler.Fifo over a whole stream (jobs enter the ReadyQueue at their arrival second,
         server.go:23-51).  Runs from the cluster spec loaded by Run, on the GPU."""
+        if self.SchedulingAlgorithm != FIFO:
+            raise ValueError("this scheduler runs DELAY")
+        return self._run(arrivals, jobs)
+
+    def Delay(self, arrivals: Sequence[int], jobs: Sequence[Job]) -> List[Placement]:
+        """Scheduler.Delay over a whole stream (jobs enter Level0 through "/delay" at their arrival
+        second, server.go:53-78).  Fills self.WaitTime like the reference's statistics."""
+        if self.SchedulingAlgorithm != DELAY:
+            raise ValueError("this scheduler runs FIFO")
+        out = self._run(arrivals, jobs)
+        ds = self._eng.delay_stats()[0]
+        self.WaitTime = WaitTime(int(ds["total_wait_ms"]), int(ds["jobs_count"]))
+        return out
+
+    def _run(self, arrivals: Sequence[int], jobs: Sequence[Job]) -> List[Placement]:
         n = len(jobs)
         s = JobStreams(
             np.asarray(arrivals, np.uint32),
@@ -123,5 +157,5 @@ class Scheduler:
         return [Placement(jobs[i].Id, int(node[i]), int(start[i]), int(fin[i])) for i in range(n)]
 
 
-__all__ = ["Scheduler", "Job", "Placement", "error", "errors_New", "FIFO", "DELAY", "READY", "RUNNING",
+__all__ = ["Scheduler", "WaitTime", "Job", "Placement", "error", "errors_New", "FIFO", "DELAY", "READY", "RUNNING",
            "WAITING", "FINISHED", "L"]

@@ -86,6 +86,33 @@ void or_contract_fast(uint32_t n, const uint32_t* c, const uint32_t* m, const ui
 void or_contract_small(uint32_t n, const uint32_t* c, const uint32_t* m, const uint32_t* dur_s,
                        uint32_t* oc, uint32_t* om, int64_t* otime_ns, float* oprice);
 
+/* ---- DELAY policy (mcs_oracle_delay.c) ------------------------------------------------------- */
+typedef struct or_delay_stats {
+    uint32_t t_end;
+    uint32_t placed;
+    uint32_t moved_l1;     /* Level0 -> Level1 moves (scheduler.go:353-359) */
+    uint32_t placed_l1;    /* placements from the Level1 pass (scheduler.go:302-329) */
+    uint32_t peak_l1;      /* peak len(Level1) */
+    uint32_t peak_running;
+    uint32_t flags;        /* 1 = Level1 jobs that can never fit; 4 = clock wrap */
+    uint32_t l1_left;      /* len(Level1) at the end (the never-fitting jobs) */
+    int64_t total_wait_ms; /* WaitTime.TotalTime at t_end (scheduler.go:48-54) */
+    int64_t jobs_count;    /* WaitTime.JobsCount (server.go:72) */
+    uint64_t ticks;        /* Delay iterations (literal and fast-forward count the same) */
+} or_delay_stats;
+
+/* Scheduler.Delay (scheduler.go:298-369) over one cluster, SDELAY semantics (see
+ * mcs_oracle_delay.c).  max_wait_s = Policy.MaxWaitTime (10 s, scheduler.go:115). */
+int or_delay_run(uint32_t n_nodes, const uint32_t* free_c, const uint32_t* free_m, uint64_t n_jobs,
+                 const uint32_t* arrival, const uint32_t* dur, const uint32_t* cores,
+                 const uint32_t* mem, uint32_t max_wait_s, int literal, int32_t* out_node,
+                 uint32_t* out_start, uint32_t* out_finish, or_delay_stats* st);
+int or_delay_run_batch(uint32_t n_clusters, const uint32_t* node_off, const uint32_t* free_c,
+                       const uint32_t* free_m, const uint64_t* job_off, const uint32_t* arrival,
+                       const uint32_t* dur, const uint32_t* cores, const uint32_t* mem,
+                       uint32_t max_wait_s, int n_threads, int32_t* out_node, uint32_t* out_start,
+                       uint32_t* out_finish, or_delay_stats* st);
+
 #ifdef __cplusplus
 }
 #endif

@@ -51,7 +51,8 @@ def kat_expect(k):
 def seeded_workload(kind: str, n_clusters: int, jobs_per_cluster: int, seed: int = 0x4D43535F53494D31):
     """Seeded synthetic workloads of BASELINE.json's configs at reduced sizes.
     kind: 'small' (cluster_small, REF arrivals), 'big' (cluster_big, REF), 'n256' (256 nodes,
-    SCALED arrivals at 90% memory load), 'n256_hot' (256 nodes, 120% load: heavy waiting)."""
+    SCALED arrivals at 90% memory load), 'n256_hot' (256 nodes, 120% load: heavy waiting),
+    'n256_delay' (0.8 arrivals per second: just under DELAY's one Level0 decision per second)."""
     from mcs_amd.engine import scaled_lambda
     from mcs_amd import replicate
 
@@ -63,6 +64,8 @@ def seeded_workload(kind: str, n_clusters: int, jobs_per_cluster: int, seed: int
         parts = kind[1:].split("_")
         nn = int(parts[0])
         load = 1.2 if (len(parts) > 1 and parts[1] == "hot") else 0.9
+        if len(parts) > 1 and parts[1] == "delay":  # DELAY drains Level0 at one job per second
+            load = 0.8 * 1.0 / scaled_lambda(nn, load=1.0)
         spec = uniform_cluster(nn)
         gp = GenParams(seed=seed, arrival_mode=1, lam=scaled_lambda(nn, load=load))
     else:

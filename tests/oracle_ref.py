@@ -41,6 +41,16 @@ class or_trade_cluster_stats(C.Structure):
                 ("lent_peak", C.c_uint32)]
 
 
+class or_delay_stats(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("t_end", "placed", "moved_l1", "placed_l1", "peak_l1", "peak_running",
+                                          "flags", "l1_left")] + \
+               [("total_wait_ms", C.c_int64), ("jobs_count", C.c_int64), ("ticks", C.c_uint64)]
+
+
+DELAY_STATS_DTYPE = np.dtype([("t_end", "<u4"), ("placed", "<u4"), ("moved_l1", "<u4"), ("placed_l1", "<u4"),
+                              ("peak_l1", "<u4"), ("peak_running", "<u4"), ("flags", "<u4"), ("l1_left", "<u4"),
+                              ("total_wait_ms", "<i8"), ("jobs_count", "<i8"), ("ticks", "<u8")])
+
 LENT_DTYPE = np.dtype([("lender", "<u4"), ("borrower", "<u4"), ("job", "<u8"), ("node", "<u4"),
                        ("start", "<u4"), ("finish", "<u4"), ("pad", "<u4")])
 TRADE_DTYPE = np.dtype([("t", "<u4"), ("requester", "<u4"), ("winner", "<i4"), ("approvals", "<u4")])
@@ -86,6 +96,12 @@ def lib():
                                    C.POINTER(or_trade_cfg), i32p, u32p, u32p, C.c_void_p, C.c_uint64, u64p,
                                    C.c_void_p, C.c_uint64, u64p, C.POINTER(or_trade_cluster_stats), u32p]
         L.or_trade_run.restype = C.c_int
+        L.or_delay_run.argtypes = [C.c_uint32, u32p, u32p, C.c_uint64, u32p, u32p, u32p, u32p, C.c_uint32, C.c_int,
+                                   i32p, u32p, u32p, C.POINTER(or_delay_stats)]
+        L.or_delay_run.restype = C.c_int
+        L.or_delay_run_batch.argtypes = [C.c_uint32, u32p, u32p, u32p, u64p, u32p, u32p, u32p, u32p, C.c_uint32,
+                                         C.c_int, i32p, u32p, u32p, C.c_void_p]
+        L.or_delay_run_batch.restype = C.c_int
         _lib = L
     return _lib
 
@@ -229,3 +245,42 @@ def trade_run(arrays, streams, borrow=True, trader=True, t_max=0xFFFFFFFE, lent_
                 decided=np.array([c.decided for c in cs[:k]], np.uint32),
                 lent_pending=np.array([c.lent_pending for c in cs[:k]], np.uint32),
                 lent_peak=np.array([c.lent_peak for c in cs[:k]], np.uint32), t_final=tf.value)
+
+
+def _stats_dict(s):
+    return {n: getattr(s, n) for n, _ in s._fields_}
+
+
+def delay_run(free_c, free_m, arrival, dur, cores, mem, literal=False, max_wait_s=10):
+    """DELAY policy over one cluster (oracle/mcs_oracle_delay.c).  Returns (node, start, finish, stats)."""
+    fc = np.ascontiguousarray(free_c, np.uint32)
+    fm = np.ascontiguousarray(free_m, np.uint32)
+    a, d, c, m = (np.ascontiguousarray(x, np.uint32) for x in (arrival, dur, cores, mem))
+    n = len(a)
+    node = np.empty(max(n, 1), np.int32)
+    st = np.empty(max(n, 1), np.uint32)
+    fi = np.empty(max(n, 1), np.uint32)
+    s = or_delay_stats()
+    lib().or_delay_run(len(fc), _p(fc, C.c_uint32), _p(fm, C.c_uint32), n, _p(a, C.c_uint32), _p(d, C.c_uint32),
+                       _p(c, C.c_uint32), _p(m, C.c_uint32), max_wait_s, 1 if literal else 0,
+                       _p(node, C.c_int32), _p(st, C.c_uint32), _p(fi, C.c_uint32), C.byref(s))
+    return node[:n], st[:n], fi[:n], _stats_dict(s)
+
+
+def delay_run_batch(arrays, streams, n_threads=1, max_wait_s=10):
+    """DELAY over many clusters (CSR).  Returns (node, start, finish, DELAY_STATS_DTYPE array)."""
+    n = streams.n_jobs
+    node = np.empty(max(n, 1), np.int32)
+    st = np.empty(max(n, 1), np.uint32)
+    fi = np.empty(max(n, 1), np.uint32)
+    k = arrays.n_clusters
+    stats = np.zeros(max(k, 1), DELAY_STATS_DTYPE)
+    fc = np.ascontiguousarray(arrays.free_c, np.uint32)
+    fm = np.ascontiguousarray(arrays.free_m, np.uint32)
+    off = np.ascontiguousarray(arrays.node_off, np.uint32)
+    joff = np.ascontiguousarray(streams.job_off, np.uint64)
+    js = [np.ascontiguousarray(x, np.uint32) for x in (streams.arrival, streams.dur, streams.cores, streams.mem)]
+    lib().or_delay_run_batch(k, _p(off, C.c_uint32), _p(fc, C.c_uint32), _p(fm, C.c_uint32), _p(joff, C.c_uint64),
+                             *[_p(x, C.c_uint32) for x in js], max_wait_s, n_threads, _p(node, C.c_int32),
+                             _p(st, C.c_uint32), _p(fi, C.c_uint32), stats.ctypes.data)
+    return node[:n], st[:n], fi[:n], stats[:k]

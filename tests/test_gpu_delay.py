@@ -1,0 +1,132 @@
+"""GPU parity of the DELAY policy: the gfx950 delay_kernel (through the C ABI, libmcs.so, engine
+policy MCS_POLICY_DELAY) against the CPU oracle (oracle/mcs_oracle_delay.c) and the hand-derived
+known-answer vectors.  Bit-exact on node, start, finish and on the per-cluster statistics (Delay
+iterations, Level1 moves/placements/peak, WaitTime.TotalTime).  Run on a real MI355X."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ref as O
+from kat_util import GOLDEN, kat_cluster, kat_expect, kat_streams, seeded_workload
+from mcs_amd import Engine, JobStreams, pack_clusters, replicate, uniform_cluster
+from mcs_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+DKATS = json.load(open(os.path.join(GOLDEN, "kats_delay.json")))["delay"]
+
+
+@pytest.fixture(scope="module")
+def delay_engine():
+    e = Engine(0, policy="DELAY")
+    yield e
+    e.close()
+
+
+def run(eng, arrays, streams):
+    eng.load_clusters(arrays)
+    eng.submit_jobs(streams)
+    st = eng.run()
+    node, start, fin = eng.placements()
+    return node, start, fin, st, eng.cluster_stats(), eng.delay_stats()
+
+
+def assert_delay_parity(arrays, streams, node, start, fin, cs, ds):
+    on, os_, of, od = O.delay_run_batch(arrays, streams, n_threads=8)
+    bad = np.nonzero((node != on) | (start != os_) | (fin != of))[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}: gpu {node[bad[:5]]},{start[bad[:5]]} " \
+                          f"oracle {on[bad[:5]]},{os_[bad[:5]]}"
+    np.testing.assert_array_equal(cs["t_end"], od["t_end"], err_msg="t_end")
+    np.testing.assert_array_equal(cs["placed"], od["placed"], err_msg="placed")
+    np.testing.assert_array_equal(cs["waited"], od["moved_l1"], err_msg="moved")
+    np.testing.assert_array_equal(cs["peak_running"], od["peak_running"], err_msg="peak_running")
+    np.testing.assert_array_equal(cs["flags"], od["flags"], err_msg="flags")
+    for key in ("total_wait_ms", "jobs_count", "moved_l1", "placed_l1", "peak_l1", "l1_left"):
+        np.testing.assert_array_equal(ds[key], od[key], err_msg=key)
+
+
+@pytest.mark.parametrize("k", DKATS, ids=[k["name"] for k in DKATS])
+def test_gpu_delay_kats(delay_engine, k):
+    arrays = pack_clusters([kat_cluster(k)])
+    node, start, fin, st, cs, ds = run(delay_engine, arrays, kat_streams(k))
+    en, es, ef = kat_expect(k)
+    np.testing.assert_array_equal(node, en)
+    np.testing.assert_array_equal(start, es)
+    np.testing.assert_array_equal(fin, ef)
+    for key, v in k["stats"].items():
+        got = ds[key][0] if key in ds.dtype.names else cs[key][0]
+        assert got == v, key
+
+
+def test_gpu_delay_kats_one_launch(delay_engine):
+    arrays = pack_clusters([kat_cluster(k) for k in DKATS])
+    parts = [kat_streams(k) for k in DKATS]
+    off = np.zeros(len(parts) + 1, np.uint64)
+    off[1:] = np.cumsum([p.n_jobs for p in parts])
+    s = JobStreams(*(np.concatenate([getattr(p, f) for p in parts]) for f in ("arrival", "dur", "cores", "mem")),
+                   off)
+    node, start, fin, st, cs, ds = run(delay_engine, arrays, s)
+    assert_delay_parity(arrays, s, node, start, fin, cs, ds)
+
+
+@pytest.mark.parametrize("kind,n_clusters,jobs", [
+    ("small", 64, 1500),       # cluster_small at the reference client's rate: Level1-heavy
+    ("big", 32, 3000),         # cluster_big, reference rate
+    ("n256_delay", 64, 4000),  # 256 nodes just under one arrival per second
+    ("n256", 32, 3000),        # 256 nodes above DELAY's drain rate: Level0 backlog
+    ("n64_hot", 32, 3000),     # 64 nodes at 120% memory load
+])
+def test_gpu_delay_seeded_parity(delay_engine, kind, n_clusters, jobs):
+    arrays, streams, _ = seeded_workload(kind, n_clusters, jobs)
+    node, start, fin, st, cs, ds = run(delay_engine, arrays, streams)
+    assert_delay_parity(arrays, streams, node, start, fin, cs, ds)
+    assert st.placed + st.unplaced == streams.n_jobs
+
+
+def test_gpu_delay_mixed_cluster_sizes(delay_engine):
+    """cluster_small, cluster_big and 256-node clusters in one launch (NPL of the largest)."""
+    a1, s1, _ = seeded_workload("small", 4, 800)
+    a2, s2, _ = seeded_workload("n256_delay", 3, 800, seed=99)
+    from mcs_amd import ClusterArrays
+    arrays = ClusterArrays(*(np.concatenate([getattr(a1, f), getattr(a2, f)]) for f in
+                             ("cap_c", "cap_m", "free_c", "free_m")),
+                           np.concatenate([a1.node_off, a1.node_off[-1] + a2.node_off[1:]]))
+    off = np.concatenate([s1.job_off, s1.job_off[-1] + s2.job_off[1:]])
+    s = JobStreams(*(np.concatenate([getattr(s1, f), getattr(s2, f)]) for f in ("arrival", "dur", "cores", "mem")),
+                   off)
+    node, start, fin, st, cs, ds = run(delay_engine, arrays, s)
+    assert_delay_parity(arrays, s, node, start, fin, cs, ds)
+
+
+def test_gpu_delay_slot_pool_escalation():
+    """A 2-row pool (128 slots) overflows on 256-node clusters; the engine re-runs those clusters
+    with a doubled pool and the results still match the oracle."""
+    arrays, streams, _ = seeded_workload("n256_delay", 8, 3000)
+    with Engine(0, policy="DELAY", slot_pool=2) as eng:
+        node, start, fin, st, cs, ds = run(eng, arrays, streams)
+    assert st.escalations >= 1
+    assert_delay_parity(arrays, streams, node, start, fin, cs, ds)
+
+
+def test_gpu_delay_stats_state_errors(delay_engine):
+    with Engine(0) as fifo:
+        arrays = pack_clusters([kat_cluster(DKATS[0])])
+        fifo.load_clusters(arrays)
+        fifo.submit_jobs(kat_streams(DKATS[0]))
+        fifo.run()
+        with pytest.raises(L.MCSError):
+            fifo.delay_stats()
+
+
+def test_scheduler_mirror_delay():
+    """The pkg/scheduler mirror with the reference's default policy (scheduler.go:116)."""
+    from mcs_amd.scheduler import DELAY, Job, Scheduler
+
+    k = [x for x in DKATS if x["name"] == "DKAT3"][0]
+    s = Scheduler(device=0, policy=DELAY)
+    s.Run(kat_cluster(k))
+    jobs = [Job(Id=j[0], CoresNeeded=j[2], MemoryNeeded=j[3], Duration=j[4]) for j in k["jobs"]]
+    pl = s.Delay([j[1] for j in k["jobs"]], jobs)
+    assert [(p.Node, p.Start, p.Finish) for p in pl] == [tuple(k["expect"][str(j[0])]) for j in k["jobs"]]
+    assert s.WaitTime.GetAverage() == 101000 / 8
