@@ -41,12 +41,18 @@ def parse():
     ap.add_argument("--cpu-sample-clusters", type=int, default=512)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
+    ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes measured by a separate rocprofv3 --pmc pass")
+    ap.add_argument("--policy", choices=["fifo", "delay"], default="fifo",
+                    help="c4 policy: fifo (the headline, Scheduler.Fifo) or delay (Scheduler.Delay, "
+                         "the reference's default policy, scheduler.go:116)")
     ap.add_argument("--config", choices=["c4", "c5"], default="c4",
                     help="c4: the headline FIFO benchmark; c5: the lock-step borrow + trader system "
                          "(--clusters = clusters of the WHOLE system, sharded over the ranks)")
     a = ap.parse_args()
+    if a.traffic_json is None:
+        a.traffic_json = os.path.join(REPO, "profiles", "traffic_latest_delay.json" if a.policy == "delay"
+                                      else "traffic_latest.json")
     if a.config == "c5":  # BASELINE.json configs[4]: 64 trading clusters, 10M jobs
         if a.clusters == 4096:
             a.clusters = 64
@@ -200,15 +206,19 @@ def cpu_baseline(args, lam, n_threads):
     streams = gen_streams_host(gp, arrays, args.jobs_per_cluster)
     O.lib()
     t0 = time.perf_counter()
-    node, st, fi, sd = O.fifo_run_batch(arrays, streams, n_threads=n_threads)
+    if args.policy == "delay":
+        O.delay_run_batch(arrays, streams, n_threads=n_threads)
+    else:
+        O.fifo_run_batch(arrays, streams, n_threads=n_threads)
     dt = time.perf_counter() - t0
+    src = "oracle/mcs_oracle_delay.c" if args.policy == "delay" else "oracle/mcs_oracle.c"
     return {
         "value": streams.n_jobs / dt,
         "unit": "placements/s",
         "cores": n_threads,
         "kind": "port",
         "sample": f"{k} of {args.clusters} clusters x {args.nodes} nodes x {args.jobs_per_cluster} jobs "
-                  f"({streams.n_jobs} placements), oracle/mcs_oracle.c -O3, OpenMP over clusters, "
+                  f"({streams.n_jobs} placements), {src} -O3, OpenMP over clusters, "
                   f"{dt:.2f} s wall",
         "seconds": dt,
     }
@@ -237,7 +247,8 @@ def main():
     from mcs_amd.shard import aggregate, rank_seed
 
     lam = scaled_lambda(args.nodes, load=args.load)
-    eng = Engine(local_rank)
+    delay = args.policy == "delay"
+    eng = Engine(local_rank, policy="DELAY" if delay else "FIFO")
     arrays = replicate(uniform_cluster(args.nodes), args.clusters)
     eng.load_clusters(arrays)
     gp = GenParams(seed=rank_seed(args.seed, rank), arrival_mode=1, lam=lam)
@@ -276,6 +287,13 @@ def main():
         "peak_running_max": int(cs["peak_running"].max()),
         "slot_pool": int(cs["pool"].max()),
     }
+    if delay:
+        ds = eng.delay_stats()
+        diag.pop("waited_frac")
+        diag["delay_iterations_per_job"] = diag.pop("loop_passes_per_job")
+        diag["level1_moved_frac"] = float(ds["moved_l1"].sum()) / max(n_jobs, 1)
+        diag["level1_peak_max"] = int(ds["peak_l1"].max())
+        diag["avg_wait_s"] = float(ds["total_wait_ms"].sum()) / max(float(ds["jobs_count"].sum()), 1.0) / 1e3
 
     if rank == 0:
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
@@ -285,8 +303,8 @@ def main():
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if (tj.get("clusters"), tj.get("nodes"), tj.get("jobs_per_cluster")) == \
-                    (args.clusters, args.nodes, args.jobs_per_cluster):
+            if (tj.get("clusters"), tj.get("nodes"), tj.get("jobs_per_cluster"), tj.get("policy", "fifo")) == \
+                    (args.clusters, args.nodes, args.jobs_per_cluster, args.policy):
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -296,7 +314,8 @@ def main():
             cpu = cpu_baseline(args, lam, n_thr)
         value = placed_all / elapsed_max
         out = {
-            "metric": "job placements/sec (whole node) at 4096 clusters x 256 nodes",
+            "metric": "job placements/sec (whole node) at 4096 clusters x 256 nodes"
+                      + (", DELAY policy" if delay else ""),
             "value": value,
             "unit": "placements/s",
             "n_gpus": world,
@@ -310,7 +329,8 @@ def main():
             "data": "synthetic (seeded device generator restating pkg/client/client.go distributions; "
                     "scaled Poisson arrivals)",
             "config": {
-                "workload": f"C4: {args.clusters} clusters x {args.nodes} nodes per GPU, FIFO, no trading, "
+                "workload": f"C4: {args.clusters} clusters x {args.nodes} nodes per GPU, "
+                            f"{'DELAY' if delay else 'FIFO'}, no trading, "
                             f"{args.jobs_per_cluster} jobs/cluster, scaled arrivals at {args.load:.0%} memory load "
                             f"(lambda={lam:.4f}/s)",
                 "clusters_per_gpu": args.clusters,
@@ -326,7 +346,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "mcs::fifo_kernel",
+                "kernel": "mcs::delay_kernel" if delay else "mcs::fifo_kernel",
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "bytes_per_placement": BYTES_PER_PLACEMENT,
             },

@@ -19,12 +19,13 @@
 //     overflows): {cores | mem << 32} and {job | dur << 32}, 16 B per entry.  A pass reads it 64
 //     entries per coalesced load (sc1: served by L2, never a stale L1 line of this CU) and
 //     compacts it in the same sweep, so removals cost no extra pass;
-//   * an exact per-lane fit filter rejects most Level1 entries without a first fit: lane l holds
-//     best[l] = max free memory over nodes with min(free cores, 63) >= l (an LDS ds_max_u32
-//     histogram + a wave suffix max), so job (c, m) can fit iff c <= max free cores and
-//     best[min(c, 63)] >= m (exact for c < 63, conservative above).  Resources only shrink
-//     inside a pass, so a job rejected at the start of the pass stays rejected; the survivors get
-//     a real first fit in list order;
+//   * a per-lane fit filter rejects most Level1 entries without a first fit: for clusters of up
+//     to 128 nodes lane l holds best[l] = max free memory over nodes with min(free cores, 63) >= l
+//     (an LDS ds_max_u32 histogram + a wave suffix max), so job (c, m) can fit iff c <= max free
+//     cores and best[min(c, 63)] >= m (exact for c < 63, conservative above); bigger clusters use
+//     the two per-resource maxima, keeping fifo_kernel's 10 KB of LDS per wave (16 waves per CU).
+//     Resources only shrink inside a pass, so a job rejected at the start of the pass stays
+//     rejected; the survivors get a real first fit in list order;
 //   * Level0 results leave in 64-job register batches (masked: moved jobs are written when Level1
 //     places them); Level1 results are three single-lane stores.
 // Fast-forward: after an iteration that placed and moved nothing, the next iteration that can
@@ -61,6 +62,7 @@ __device__ __forceinline__ uint64_t ld_l2(const uint64_t* p) {
 template <int NPL, int P>
 __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     static_assert(P <= 32, "free-row mask is one u32 per lane");
+    constexpr bool kHist = NPL <= 2;  // exact Level1 fit histogram (256 B of LDS)
     const uint32_t item = blockIdx.x;
     const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
     const uint32_t lane = threadIdx.x;
@@ -68,7 +70,6 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     __shared__ uint64_t nodes[NPL * kWave];
     __shared__ uint64_t pay_cm[P * kWave];
     __shared__ uint64_t pay_nf[P * kWave];
-    __shared__ uint32_t hist[kWave];
 
     // ---- cluster spec: Run() keeps the JSON availability (scheduler.go:101-109) ----
     const uint32_t n0 = a.node_off[ci];
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     uint64_t* l1_jd = a.l1_jd + j0;  //                  {job | dur << 32}
     const uint32_t max_wait = a.max_wait_s;
 
-    uint32_t frm = (P == 32) ? 0xFFFFFFFFu : ((1u << P) - 1u);
+    uint32_t frm = (P == 32) ? 0xFFFFFFFFu : ((1u << (P & 31)) - 1u);
     uint32_t lmin = kEmpty;
 #pragma unroll
     for (int p = 0; p < P; ++p) pay_nf[p * kWave + lane] = (uint64_t)kEmpty << 32;
@@ -103,10 +104,16 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     uint4 nxt = jobs[kWave + lane];
 
     uint32_t t = 0, h = 0, l1n = 0, minf = kEmpty, flags = 0;
+    // Counters and the WaitTime sums live in VGPRs (the asm hides their uniformity): the CU's scalar
+    // unit is the scarcer issue resource (fifo_kernel's measurements).
     uint32_t used = 0, peak = 0, placed = 0, moved = 0, placed_l1 = 0, peak_l1 = 0;
     uint32_t n_iter = 0, n_rel = 0;
-    uint64_t sum_start = 0, sum_arr = 0;  // WaitTime.TotalTime = 1000 * (sum_start - sum_arr)
-    asm volatile("" : "+v"(used), "+v"(peak), "+v"(n_iter), "+v"(n_rel));
+    // WaitTime.TotalTime / 1000 = sum over placed jobs of (start - arrival) [+ left jobs]:
+    //   wacc  per lane: Level0 placements of that lane's batch slots, added at each batch flush;
+    //   l1_t  t of every Level1 placement;  mv_a  arrival of every job moved to Level1
+    uint64_t wacc = 0, l1_t = 0, mv_a = 0;
+    asm volatile("" : "+v"(used), "+v"(peak), "+v"(n_iter), "+v"(n_rel), "+v"(placed), "+v"(moved),
+                 "+v"(placed_l1), "+v"(peak_l1), "+v"(l1_t), "+v"(mv_a));
     // Level0 result batch: lane (job & 63) holds its record; ov = written by Level0
     int32_t on = -1;
     uint32_t os = kEmpty, of = kEmpty, ov = 0u;
@@ -178,47 +185,61 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         return true;
     };
 
+    // writes the Level0 results of batch [base, base + 64); `cur` holds that batch's records
     auto flush = [&](uint32_t base) __attribute__((always_inline)) {
         const uint32_t i = base + lane;
         if (ov && i < J) {
             __builtin_nontemporal_store(on, o_node + i);
             __builtin_nontemporal_store(os, o_start + i);
             __builtin_nontemporal_store(of, o_finish + i);
+            wacc += (uint64_t)(os - cur.x);
         }
         ov = 0u;
     };
 
-    uint32_t stop = (J == 0u) ? 1u : 0u;
-    while (!stop) {
+    uint32_t stop = 0u;
+    if (J != 0u) do {
         ++n_iter;
-        uint32_t changed = 0u;
-        // node and slot state in LDS is updated by single lanes and read by all: no value may be
-        // carried in registers across iterations
-        asm volatile("" ::: "memory");
+        uint32_t changed = 0u, l1w = 0u;
 
         // ---- Level1 pass (scheduler.go:302-329) ----
         if (l1n != 0u) {
-            // fit filter: best[l] = max free mem over nodes with min(free cores, 63) >= l
-            hist[lane] = 0u;
-            uint32_t mc = 0u;
+            // fit filter, lane l: best = max free mem over nodes with min(free cores, 63) >= l.
+            // Exact histogram + suffix max for clusters of <= 128 nodes; bigger clusters keep
+            // their LDS budget at 16 waves per CU and use the per-resource maxima instead
+            // (conservative: survivors still get a real first fit).
+            uint32_t mc = 0u, mm = 0u;
 #pragma unroll
             for (int k = 0; k < NPL; ++k) {
                 const uint64_t v = nodes[k * kWave + lane];
-                const uint32_t fc = (uint32_t)v;
+                const uint32_t fc = (uint32_t)v, fm = (uint32_t)(v >> 32);
                 if (nid[k] != kEmpty) {
-                    atomicMax(&hist[fc < 63u ? fc : 63u], (uint32_t)(v >> 32));
                     mc = fc > mc ? fc : mc;
+                    mm = fm > mm ? fm : mm;
                 }
             }
             const uint32_t max_c = wave_max_u32(mc);
-            // the histogram is written by other lanes: without a fence the compiler may forward
-            // this lane's own 0 store to the load below (it reasons per thread)
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-            uint32_t best = hist[lane];
+            uint32_t best;
+            if constexpr (kHist) {
+                __shared__ uint32_t hist[kWave];
+                hist[lane] = 0u;
 #pragma unroll
-            for (int o = 1; o < kWave; o <<= 1) {
-                const uint32_t w = (uint32_t)__shfl_down((int)best, o);
-                best = (lane + o < (uint32_t)kWave && w > best) ? w : best;
+                for (int k = 0; k < NPL; ++k) {
+                    const uint64_t v = nodes[k * kWave + lane];
+                    const uint32_t fc = (uint32_t)v;
+                    if (nid[k] != kEmpty) atomicMax(&hist[fc < 63u ? fc : 63u], (uint32_t)(v >> 32));
+                }
+                // the histogram is written by other lanes: without a fence the compiler may
+                // forward this lane's own 0 store to the load below (it reasons per thread)
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                best = hist[lane];
+#pragma unroll
+                for (int o = 1; o < kWave; o <<= 1) {
+                    const uint32_t w = (uint32_t)__shfl_down((int)best, o);
+                    best = (lane + o < (uint32_t)kWave && w > best) ? w : best;
+                }
+            } else {
+                best = wave_max_u32(mm);
             }
 
             uint32_t wr = 0u, skip = kEmpty;
@@ -228,7 +249,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                 const uint64_t cm = live ? ld_l2(l1_cm + pos) : 0ull;
                 const uint64_t jdv = live ? ld_l2(l1_jd + pos) : 0ull;
                 const uint32_t c = (uint32_t)cm, m = (uint32_t)(cm >> 32);
-                const uint32_t bm = (uint32_t)__shfl((int)best, (int)(c < 63u ? c : 63u));
+                const uint32_t bm = kHist ? (uint32_t)__shfl((int)best, (int)(c < 63u ? c : 63u)) : best;
                 uint64_t cand = __ballot(live && c <= max_c && bm >= m);
                 uint64_t rem = 0ull;
                 while (cand) {
@@ -255,7 +276,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                     skip = base + b + 1u;
                     ++placed;
                     ++placed_l1;
-                    sum_start += t;
+                    l1_t += t;
                     changed = 1u;
                 }
                 // compaction in the same sweep: survivors move down to the write cursor
@@ -269,88 +290,87 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                         l1_jd[np] = jdv;
                     }
                 }
+                l1w |= (wr != base || rem != 0ull) ? 1u : 0u;
                 wr += (uint32_t)__builtin_popcountll(kept);
             }
             if (!stop) l1n = wr;
         }
 
         // ---- Level0 head (scheduler.go:332-366) ----
-        if (!stop && h < J) {
-            if (h - cb >= (uint32_t)kWave) {
-                cur = nxt;
-                cb += kWave;
-                nxt = jobs[cb + kWave + lane];
-            }
-            const uint32_t l = (h - cb) & 63u;
-            const uint32_t arr = readlane(cur.x, l);
-            if (arr <= t) {  // Level0 is non-empty: its head has arrived
-                const uint32_t jd = readlane(cur.y, l);
-                const uint32_t jc = readlane(cur.z, l);
-                const uint32_t jm = readlane(cur.w, l);
-                const uint32_t k = first_fit(jc, jm);
-                const uint32_t ol = h & 63u;
-                if (k != kEmpty) {
-                    const uint32_t fin = t + jd;
-                    if (!commit(k, jc, jm, fin, jd)) {
-                        flags |= MCS_FLAG_OVERFLOW;
-                        stop = 1u;
-                    } else {
-                        const bool pme = lane == ol;
-                        on = pme ? (int32_t)k : on;
-                        os = pme ? t : os;
-                        of = pme ? fin : of;
-                        ov = pme ? 1u : ov;
-                        ++placed;
-                        sum_start += t;
-                        sum_arr += arr;
-                        ++h;
-                        changed = 1u;
-                    }
-                } else if (t - arr >= max_wait) {  // time.Since(WaitTime) >= MaxWaitTime (:353)
-                    if (lane == 0u) {
-                        l1_cm[l1n] = (uint64_t)jc | ((uint64_t)jm << 32);
-                        l1_jd[l1n] = (uint64_t)h | ((uint64_t)jd << 32);
-                    }
-                    ++l1n;
-                    peak_l1 = l1n > peak_l1 ? l1n : peak_l1;
-                    ++moved;
-                    sum_arr += arr;
+        // Unmasked batch advance: the job array has kJobPad records of slack, so the prefetch one
+        // batch ahead is always in bounds and lands straight in the loop-carried registers.
+        if (h - cb >= (uint32_t)kWave) {
+            cur = nxt;
+            cb += kWave;
+            nxt = jobs[cb + kWave + lane];
+        }
+        const uint32_t l = (h - cb) & 63u;
+        const uint32_t arr = readlane(cur.x, l);
+        if (!stop && h < J && arr <= t) {  // Level0 is non-empty: its head has arrived
+            const uint32_t jd = readlane(cur.y, l);
+            const uint32_t jc = readlane(cur.z, l);
+            const uint32_t jm = readlane(cur.w, l);
+            const uint32_t k = first_fit(jc, jm);
+            const uint32_t ol = h & 63u;
+            if (k != kEmpty) {
+                const uint32_t fin = t + jd;
+                if (!commit(k, jc, jm, fin, jd)) {
+                    flags |= MCS_FLAG_OVERFLOW;
+                    stop = 1u;
+                } else {
+                    const bool pme = lane == ol;
+                    on = pme ? (int32_t)k : on;
+                    os = pme ? t : os;
+                    of = pme ? fin : of;
+                    ov = pme ? 1u : ov;
+                    ++placed;
                     ++h;
                     changed = 1u;
                 }
-                if (changed && (h & 63u) == 0u) flush(h - 64u);
+            } else if (t - arr >= max_wait) {  // time.Since(WaitTime) >= MaxWaitTime (:353)
+                if (lane == 0u) {
+                    l1_cm[l1n] = (uint64_t)jc | ((uint64_t)jm << 32);
+                    l1_jd[l1n] = (uint64_t)h | ((uint64_t)jd << 32);
+                }
+                ++l1n;
+                peak_l1 = l1n > peak_l1 ? l1n : peak_l1;
+                ++moved;
+                mv_a += arr;
+                ++h;
+                changed = 1u;
+                l1w = 1u;
             }
+            if (changed && (h & 63u) == 0u) flush(h - 64u);
         }
-        // Level1 stores must be visible to the next pass's L2 loads
-        if (changed) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        // Level1 stores must have reached L2 before the next pass's sc1 loads
+        if (l1w) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 
-        // ---- time.Sleep(1 s) (:367) and the fast-forward ----
-        if (stop) break;
-        if (h >= J && l1n == 0u) {  // every job placed: the run ends at the next iteration
-            t += 1u;
-            break;
-        }
-        if (!changed && minf == kEmpty && h >= J) {  // Level1 jobs that can never fit
-            flags |= MCS_FLAG_DEADLOCK;
-            break;
-        }
+        // ---- time.Sleep(1 s) (:367) and the fast-forward; one exit, tested at the bottom ----
         uint32_t tn = t + 1u;
         if (!changed) {
+            // the next iteration that can differ: a release, the head's MaxWaitTime move, or
+            // (empty Level0) the next arrival; arr is still job h's arrival
             uint32_t ev = minf;
-            if (h < J) {
-                const uint32_t arr = readlane(cur.x, (h - cb) & 63u);
-                const uint32_t e2 = arr <= t ? arr + max_wait : arr;
-                ev = e2 < ev ? e2 : ev;
-            }
+            const uint32_t e2 = arr <= t ? arr + max_wait : arr;
+            ev = (h < J && e2 < ev) ? e2 : ev;
             tn = ev > tn ? ev : tn;
         }
-        if (tn <= t) {
-            flags |= MCS_FLAG_CLOCK_OVERFLOW;
-            break;
+        if (!stop) {
+            if (h >= J && l1n == 0u) {  // every job placed: the run ends at the next iteration
+                t = t + 1u;
+                stop = 1u;
+            } else if (!changed && tn == kEmpty) {  // nothing runs or arrives: Level1 never fits
+                flags |= MCS_FLAG_DEADLOCK;
+                stop = 1u;
+            } else if (tn <= t) {
+                flags |= MCS_FLAG_CLOCK_OVERFLOW;
+                stop = 1u;
+            } else {
+                t = tn;
+                if (minf <= t) release();
+            }
         }
-        t = tn;
-        if (minf <= t) release();
-    }
+    } while (!stop);
 
     if (!(flags & (MCS_FLAG_OVERFLOW | MCS_FLAG_CLOCK_OVERFLOW))) {
         if ((h & 63u) != 0u) flush(h & ~63u);
@@ -368,10 +388,17 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         }
     }
     // WaitTime.TotalTime (scheduler.go:309-312,338-341): a placed job keeps 1000 * (start -
-    // arrival); a job left in Level1 holds 1000 * (t - arrival) from the last pass.  sum_arr
-    // already counts every job Level0 placed or moved, so the left jobs add l1n * t.
+    // arrival); a job left in Level1 holds 1000 * (t - arrival) from the last pass.  Every moved
+    // job's arrival is in mv_a, so Level1 contributes l1_t + left * t - mv_a.
     const uint32_t left = (flags & MCS_FLAG_DEADLOCK) ? l1n : 0u;
-    const uint64_t wait_s = sum_start + (uint64_t)left * t - sum_arr;
+    uint64_t wsum = wacc;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)wsum, o);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(wsum >> 32), o);
+        wsum += (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    const uint64_t wait_s = wsum + l1_t + (uint64_t)left * t - mv_a;
 
     if (lane == 0) {
         mcs_cluster_stats st;

@@ -19,8 +19,11 @@ run, out = sys.argv[1], sys.argv[2]
 os.makedirs(out, exist_ok=True)
 
 
+KERNEL = os.environ.get("MCS_KERNEL", "fifo_kernel")  # delay_kernel for --policy delay runs
+
+
 def fifo_rows(path):
-    return [r for r in csv.DictReader(open(path)) if "fifo_kernel" in r.get("Kernel_Name", r.get("Name", ""))]
+    return [r for r in csv.DictReader(open(path)) if KERNEL in r.get("Kernel_Name", r.get("Name", ""))]
 
 
 summary = {}
@@ -28,7 +31,7 @@ stats = glob.glob(f"{run}/prof/*kernel_stats.csv")
 if stats:
     shutil.copy(stats[0], f"{out}/kernel_stats.csv")
     for r in csv.DictReader(open(stats[0])):
-        if "fifo_kernel" in r["Name"]:
+        if KERNEL in r["Name"]:
             summary["kernel"] = r["Name"]
             summary["calls"] = int(r["Calls"])
             summary["avg_ns"] = float(r["AverageNs"])
@@ -56,6 +59,7 @@ if bench and "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
         "clusters": bench["config"]["clusters_per_gpu"],
         "nodes": bench["config"]["nodes"],
         "jobs_per_cluster": bench["config"]["jobs_per_cluster"],
+        "policy": "delay" if "DELAY" in bench["metric"] else "fifo",
         "hbm_bytes_per_launch": fetch + write,
         "fetch_bytes_corrected": fetch,
         "write_bytes": write,
@@ -67,7 +71,8 @@ if bench and "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
     summary["traffic"] = traffic
     with open(f"{out}/traffic.json", "w") as f:
         json.dump(traffic, f, indent=1)
-    with open("profiles/traffic_latest.json", "w") as f:
+    with open("profiles/traffic_latest.json" if traffic["policy"] == "fifo" else
+              "profiles/traffic_latest_delay.json", "w") as f:
         json.dump(traffic, f, indent=1)
 if "SQ_INSTS_SALU" in counters and bench:
     jobs = bench["config"]["placements_per_step_per_gpu"]

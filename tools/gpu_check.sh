@@ -53,7 +53,7 @@ for s in $STEPS; do
         rc=$?; tail -5 "$OUT/smoke.log"; echo "smoke rc=$rc"; fatal $rc || exit $rc ;;
     bench)
         echo "== bench"
-        timeout -k 10 900 python bench.py --steps 5 --warmup 1 > "$OUT/bench.json" 2> "$OUT/bench.err"
+        timeout -k 10 900 python bench.py --steps 5 --warmup 1 $BENCH_ARGS > "$OUT/bench.json" 2> "$OUT/bench.err"
         rc=$?; cat "$OUT/bench.json"; tail -5 "$OUT/bench.err"; echo "bench rc=$rc"; fatal $rc || exit $rc ;;
     prof)
         echo "== rocprofv3 kernel trace"
