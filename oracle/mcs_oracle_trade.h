@@ -54,6 +54,49 @@ int or_trade_run(uint32_t C, const uint32_t* node_off, const uint32_t* cap_c, co
                  uint64_t lent_cap, uint64_t* n_lent, or_trade_rec* trade_log, uint64_t trade_cap,
                  uint64_t* n_trades, or_trade_cluster_stats* cstats, uint32_t* t_final);
 
+/* ---- trading with DELAY schedulers (mcs_oracle_dtrade.c) ------------------- */
+typedef struct {
+    uint32_t period_s;           /* 10: trader.go:323 (0 = no traders: independent Delay loops) */
+    uint32_t trade_ok_sleep_s;   /* 240: trader.go:297,316 */
+    uint32_t trade_fail_sleep_s; /* 120: trader.go:300,319 */
+    uint32_t lock_s;             /* 20: server.go:49 */
+    uint32_t sample_period_s;    /* 5: trader_server.go:42 */
+    uint32_t max_wait_s;         /* 10: scheduler.go:115 */
+    uint32_t max_vnodes;         /* virtual nodes a cluster can receive (capacity of the arrays) */
+    uint32_t t_max;              /* stop after this tick even if work remains */
+} or_dtrade_cfg;
+
+typedef struct {
+    uint32_t t, requester;
+    int32_t winner;     /* responder whose allocation succeeded, -1 = "couldn't acquire resources" */
+    uint32_t approvals; /* approving responses pushed on the heap */
+    uint32_t policy;    /* 0 = WaitTime (fast node), 1 = Utilization (small node) */
+    uint32_t cores, mem, time_s; /* the contract */
+    uint32_t failed;    /* popped approvals that failed (lock lost or allocation error) */
+    uint32_t pad;
+} or_dtrade_rec;
+
+typedef struct { /* one Foreign job launched by AllocateVirtualNodeResources on a responder */
+    uint32_t requester, responder, node, start, finish, pad;
+    uint64_t c, m; /* uint(core_diff), uint(mem_diff) (cluster.go:116) */
+} or_foreign_rec;
+
+typedef struct {
+    uint32_t virtual_nodes, decided, moved_l1, placed_l1;
+    int64_t total_wait_ms, jobs_count;
+} or_dtrade_cluster_stats;
+
+/* Lock-step run of C DELAY clusters with traders.  vnode_c/vnode_m: [C][max_vnodes] capacities
+ * of the virtual nodes received (may be NULL).  Foreign jobs are logged in execution order. */
+int or_dtrade_run(uint32_t C, const uint32_t* node_off, const uint32_t* cap_c, const uint32_t* cap_m,
+                  const uint32_t* free_c, const uint32_t* free_m, const uint64_t* job_off,
+                  const uint32_t* arrival, const uint32_t* dur, const uint32_t* cores,
+                  const uint32_t* mem, const or_dtrade_cfg* cfg, int32_t* out_node,
+                  uint32_t* out_start, uint32_t* out_finish, or_dtrade_rec* trade_log,
+                  uint64_t trade_cap, uint64_t* n_trades, or_foreign_rec* foreign_log,
+                  uint64_t foreign_cap, uint64_t* n_foreign, uint32_t* vnode_c, uint32_t* vnode_m,
+                  or_dtrade_cluster_stats* cstats, uint32_t* t_final);
+
 #ifdef __cplusplus
 }
 #endif

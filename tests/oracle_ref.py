@@ -51,6 +51,19 @@ DELAY_STATS_DTYPE = np.dtype([("t_end", "<u4"), ("placed", "<u4"), ("moved_l1", 
                               ("peak_l1", "<u4"), ("peak_running", "<u4"), ("flags", "<u4"), ("l1_left", "<u4"),
                               ("total_wait_ms", "<i8"), ("jobs_count", "<i8"), ("ticks", "<u8")])
 
+class or_dtrade_cfg(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("period_s", "trade_ok_sleep_s", "trade_fail_sleep_s", "lock_s",
+                                          "sample_period_s", "max_wait_s", "max_vnodes", "t_max")]
+
+
+DTRADE_DTYPE = np.dtype([("t", "<u4"), ("requester", "<u4"), ("winner", "<i4"), ("approvals", "<u4"),
+                         ("policy", "<u4"), ("cores", "<u4"), ("mem", "<u4"), ("time_s", "<u4"), ("failed", "<u4"),
+                         ("pad", "<u4")])
+FOREIGN_DTYPE = np.dtype([("requester", "<u4"), ("responder", "<u4"), ("node", "<u4"), ("start", "<u4"),
+                          ("finish", "<u4"), ("pad", "<u4"), ("c", "<u8"), ("m", "<u8")])
+DTRADE_STATS_DTYPE = np.dtype([("virtual_nodes", "<u4"), ("decided", "<u4"), ("moved_l1", "<u4"),
+                               ("placed_l1", "<u4"), ("total_wait_ms", "<i8"), ("jobs_count", "<i8")])
+
 LENT_DTYPE = np.dtype([("lender", "<u4"), ("borrower", "<u4"), ("job", "<u8"), ("node", "<u4"),
                        ("start", "<u4"), ("finish", "<u4"), ("pad", "<u4")])
 TRADE_DTYPE = np.dtype([("t", "<u4"), ("requester", "<u4"), ("winner", "<i4"), ("approvals", "<u4")])
@@ -96,6 +109,10 @@ def lib():
                                    C.POINTER(or_trade_cfg), i32p, u32p, u32p, C.c_void_p, C.c_uint64, u64p,
                                    C.c_void_p, C.c_uint64, u64p, C.POINTER(or_trade_cluster_stats), u32p]
         L.or_trade_run.restype = C.c_int
+        L.or_dtrade_run.argtypes = [C.c_uint32, u32p, u32p, u32p, u32p, u32p, u64p, u32p, u32p, u32p, u32p,
+                                    C.POINTER(or_dtrade_cfg), i32p, u32p, u32p, C.c_void_p, C.c_uint64, u64p,
+                                    C.c_void_p, C.c_uint64, u64p, u32p, u32p, C.c_void_p, u32p]
+        L.or_dtrade_run.restype = C.c_int
         L.or_delay_run.argtypes = [C.c_uint32, u32p, u32p, C.c_uint64, u32p, u32p, u32p, u32p, C.c_uint32, C.c_int,
                                    i32p, u32p, u32p, C.POINTER(or_delay_stats)]
         L.or_delay_run.restype = C.c_int
@@ -284,3 +301,39 @@ def delay_run_batch(arrays, streams, n_threads=1, max_wait_s=10):
                              *[_p(x, C.c_uint32) for x in js], max_wait_s, n_threads, _p(node, C.c_int32),
                              _p(st, C.c_uint32), _p(fi, C.c_uint32), stats.ctypes.data)
     return node[:n], st[:n], fi[:n], stats[:k]
+
+
+def dtrade_run(arrays, streams, t_max=0xFFFFFFFE, trader=True, max_vnodes=64, period_s=10, trade_ok_sleep_s=240,
+               trade_fail_sleep_s=120, lock_s=20, sample_period_s=5, max_wait_s=10, trade_cap=1 << 16,
+               foreign_cap=1 << 20):
+    """Lock-step DELAY clusters with traders (oracle/mcs_oracle_dtrade.c).  Returns a dict with node,
+    start, finish, trades (DTRADE_DTYPE), foreign (FOREIGN_DTYPE), vnodes (list per cluster of (c, m)),
+    stats (DTRADE_STATS_DTYPE) and t_final."""
+    n = streams.n_jobs
+    k = arrays.n_clusters
+    node = np.empty(max(n, 1), np.int32)
+    st = np.empty(max(n, 1), np.uint32)
+    fi = np.empty(max(n, 1), np.uint32)
+    trades = np.zeros(max(trade_cap, 1), DTRADE_DTYPE)
+    foreign = np.zeros(max(foreign_cap, 1), FOREIGN_DTYPE)
+    vc = np.zeros(max(k * max_vnodes, 1), np.uint32)
+    vm = np.zeros(max(k * max_vnodes, 1), np.uint32)
+    stats = np.zeros(max(k, 1), DTRADE_STATS_DTYPE)
+    nt, nf, tf = C.c_uint64(), C.c_uint64(), C.c_uint32()
+    cfg = or_dtrade_cfg(period_s if trader else 0, trade_ok_sleep_s, trade_fail_sleep_s, lock_s, sample_period_s,
+                        max_wait_s, max_vnodes, t_max)
+    cc = [np.ascontiguousarray(x, np.uint32) for x in (arrays.cap_c, arrays.cap_m, arrays.free_c, arrays.free_m)]
+    off = np.ascontiguousarray(arrays.node_off, np.uint32)
+    joff = np.ascontiguousarray(streams.job_off, np.uint64)
+    js = [np.ascontiguousarray(x, np.uint32) for x in (streams.arrival, streams.dur, streams.cores, streams.mem)]
+    lib().or_dtrade_run(k, _p(off, C.c_uint32), *[_p(x, C.c_uint32) for x in cc], _p(joff, C.c_uint64),
+                        *[_p(x, C.c_uint32) for x in js], C.byref(cfg), _p(node, C.c_int32), _p(st, C.c_uint32),
+                        _p(fi, C.c_uint32), trades.ctypes.data, trade_cap, C.byref(nt), foreign.ctypes.data,
+                        foreign_cap, C.byref(nf), _p(vc, C.c_uint32), _p(vm, C.c_uint32), stats.ctypes.data,
+                        C.byref(tf))
+    stats = stats[:k].copy()
+    vnodes = [[(int(vc[c * max_vnodes + i]), int(vm[c * max_vnodes + i])) for i in range(int(stats["virtual_nodes"][c]))]
+              for c in range(k)]
+    return dict(node=node[:n], start=st[:n], finish=fi[:n], trades=trades[: min(nt.value, trade_cap)].copy(),
+                n_trades=nt.value, foreign=foreign[: min(nf.value, foreign_cap)].copy(), n_foreign=nf.value,
+                vnodes=vnodes, stats=stats, t_final=tf.value)

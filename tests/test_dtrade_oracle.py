@@ -1,0 +1,96 @@
+"""CPU tests of the lock-step trading oracle with DELAY schedulers (oracle/mcs_oracle_dtrade.c):
+hand-derived scenarios (tests/golden/kats_dtrade.json) and the exact reduction to independent
+Delay loops when the traders are off or never break a policy.  No GPU needed."""
+import copy
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ref as O
+from kat_util import GOLDEN, REPO, seeded_workload
+from mcs_amd import Cluster, JobStreams, pack_clusters
+
+DT = json.load(open(os.path.join(GOLDEN, "kats_dtrade.json")))["dtrade"]
+
+
+def dt_system(k):
+    cls = []
+    for i, name in enumerate(k["clusters"]):
+        cl = copy.deepcopy(Cluster.load(os.path.join(REPO, "assets", name + ".json")))
+        for node, (fc, fm) in k["override_free"].get(str(i), {}).items():
+            cl.Nodes[int(node)].CoresAvailable = fc
+            cl.Nodes[int(node)].MemoryAvailable = fm
+        cls.append(cl)
+    jobs = k["jobs"]
+    n = len(jobs)
+    off = np.array([0, n] + [n] * (len(cls) - 1), np.uint64)
+    s = JobStreams(np.array([j[1] for j in jobs], np.uint32), np.array([j[4] for j in jobs], np.uint32),
+                   np.array([j[2] for j in jobs], np.uint32), np.array([j[3] for j in jobs], np.uint32), off)
+    return pack_clusters(cls), s
+
+
+def check_kat(k, node, start, fin, trades, foreign, n_foreign, vnodes, t_final):
+    for jid, (nd, s, f) in k["expect"].items():
+        assert (int(node[int(jid)]), int(start[int(jid)]), int(fin[int(jid)])) == (nd, s, f)
+    got = [[int(r[f]) for f in ("t", "requester", "winner", "approvals", "policy", "cores", "mem", "time_s",
+                                "failed")] for r in trades]
+    assert got == k["trades"]
+    ff = [[int(r[f]) for f in ("requester", "responder", "node", "start", "finish", "c", "m")]
+          for r in foreign[:len(k["foreign_first"])]]
+    assert ff == k["foreign_first"]
+    assert n_foreign == k["n_foreign"]
+    assert vnodes == [[tuple(v) for v in vs] for vs in k["vnodes"]]
+    assert t_final == k["t_final"]
+
+
+@pytest.mark.parametrize("k", DT, ids=[k["name"] for k in DT])
+def test_dtrade_oracle_kats(k):
+    arrays, s = dt_system(k)
+    r = O.dtrade_run(arrays, s, t_max=k["t_max"])
+    check_kat(k, r["node"], r["start"], r["finish"], r["trades"], r["foreign"], r["n_foreign"], r["vnodes"],
+              r["t_final"])
+    for key, v in k.get("stats0", {}).items():
+        assert r["stats"][key][0] == v, key
+
+
+@pytest.mark.parametrize("kind,C,J", [("small", 4, 300), ("big", 3, 400), ("n64_hot", 3, 800)])
+def test_dtrade_without_traders_is_independent_delay(kind, C, J):
+    """period 0 = no traders: every cluster runs its own Delay loop, exactly or_delay_run."""
+    arrays, streams, _ = seeded_workload(kind, C, J)
+    r = O.dtrade_run(arrays, streams, trader=False)
+    node, st, fi, ds = O.delay_run_batch(arrays, streams)
+    np.testing.assert_array_equal(r["node"], node)
+    np.testing.assert_array_equal(r["start"], st)
+    np.testing.assert_array_equal(r["finish"], fi)
+    np.testing.assert_array_equal(r["stats"]["total_wait_ms"], ds["total_wait_ms"])
+    assert r["n_trades"] == 0 and r["n_foreign"] == 0
+
+
+def test_dtrade_unbroken_policies_change_nothing():
+    """Light load: no WaitTime or Utilization policy ever breaks, so traders never trade and the
+    placements equal the independent Delay loops."""
+    arrays, streams, _ = seeded_workload("n256_delay", 3, 800)
+    r = O.dtrade_run(arrays, streams)
+    node, st, fi, ds = O.delay_run_batch(arrays, streams)
+    assert r["n_trades"] == 0
+    np.testing.assert_array_equal(r["node"], node)
+    np.testing.assert_array_equal(r["start"], st)
+
+
+def test_dtrade_overloaded_system_trades_and_uses_virtual_nodes():
+    """cluster_small at the reference client's rate: waits exceed 600 s, traders size fast/small-node
+    contracts from Level1, some trades win, and jobs run on the virtual nodes received."""
+    arrays, streams, _ = seeded_workload("small", 8, 300)
+    r = O.dtrade_run(arrays, streams)
+    tr = r["trades"]
+    assert r["n_trades"] > 100 and (tr["winner"] >= 0).sum() > 0
+    assert set(np.unique(tr["policy"])) == {0, 1}
+    nphys = np.repeat(np.diff(arrays.node_off), 300)
+    assert (r["node"] >= nphys).sum() > 0 and (r["node"] >= 0).all()
+    # every winning trade appended exactly one virtual node with the contract's capacity
+    won = tr[tr["winner"] >= 0]
+    for q in range(8):
+        wq = won[won["requester"] == q]
+        assert [(int(a), int(b)) for a, b in zip(wq["cores"], wq["mem"])] == r["vnodes"][q]
