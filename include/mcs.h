@@ -57,6 +57,8 @@ typedef enum mcs_status {
 #define MCS_FLAG_LENT_OVERFLOW 0x8u  /* a LentQueue exceeded lent_queue_cap (lock-step runs)          */
 #define MCS_FLAG_LOG_OVERFLOW 0x10u  /* lent/trade log capacity exceeded: records dropped, counts kept */
 #define MCS_FLAG_T_MAX 0x20u         /* lock-step run stopped at t_max_s with work left               */
+#define MCS_FLAG_VNODE_OVERFLOW 0x40u /* DELAY trading: a cluster received more virtual nodes than the
+                                         engine holds (engine re-runs with more)                      */
 
 /* ---- configuration ------------------------------------------------------------------------- */
 typedef enum mcs_policy {

@@ -15,7 +15,10 @@
  *   AddVirtualNode /
  *   AllocateVirtualNodeResources     pkg/scheduler/cluster.go:65-125
  * Semantics: the lock-step serialization of DESIGN.md §9 (tick T: scheduler steps, borrow
- * exchange, state samples, trader rounds), bit-identical to oracle/mcs_oracle_trade.c.
+ * exchange, state samples, trader rounds), bit-identical to oracle/mcs_oracle_trade.c.  With
+ * MCS_POLICY_DELAY the schedulers run Scheduler.Delay and the traders size real contracts from
+ * Level1 (oracle/mcs_oracle_dtrade.c): Foreign jobs on responders, virtual nodes
+ * with capacity on requesters.  DELAY trading runs on one engine (world == 1).
  *
  * Sharding: the clusters are split in equal contiguous blocks over `world` engines (one per GPU,
  * usually one process each).  Every tick needs three all-gathers of small fixed-size records.
@@ -50,6 +53,26 @@ typedef struct mcs_trade_rec {
     int32_t winner;     /* responder whose virtual node was received, -1 = "couldn't acquire resources" */
     uint32_t approvals; /* approving responses pushed on the heap */
 } mcs_trade_rec;
+
+/* One trader round of a DELAY system (MCS_POLICY_DELAY + trader), with its contract
+ * (calculateFastNodeSize / calculateSmallNodeSize, pkg/trader/scheduler_client.go:126-289). */
+typedef struct mcs_contract_rec {
+    uint32_t t_s, requester;
+    int32_t winner;     /* responder whose AllocateVirtualNodeResources succeeded, -1 = none    */
+    uint32_t approvals;
+    uint32_t policy;    /* 0 = WaitTime (fast node, trader.go:304-320), 1 = Utilization (small) */
+    uint32_t cores, mem, time_s; /* the ContractRequest (trader.proto:20-27); price is 0        */
+    uint32_t failed;    /* popped approvals whose ApproveContract failed before the winner       */
+    uint32_t pad;
+} mcs_contract_rec;
+
+/* One Foreign job launched on a responder by AllocateVirtualNodeResources (cluster.go:87-125):
+ * it holds {c, m} of node `node` of cluster `responder` from start_s to finish_s.  c and m are
+ * Go uint values (cluster.go:116): they may exceed what the node had (the counter wraps). */
+typedef struct mcs_foreign_rec {
+    uint32_t requester, responder, node, start_s, finish_s, pad;
+    uint64_t c, m;
+} mcs_foreign_rec;
 
 typedef struct mcs_trade_stats {
     uint64_t placed;       /* own jobs placed locally */
@@ -100,8 +123,19 @@ int mcs_read_trade_stats(mcs_engine* eng, mcs_trade_stats* out);
 int mcs_read_lent(mcs_engine* eng, mcs_lent_rec* out, uint64_t cap, uint64_t* n);
 /* Trader rounds of ALL clusters in (t_s, requester) order (identical on every rank). */
 int mcs_read_trades(mcs_engine* eng, mcs_trade_rec* out, uint64_t cap, uint64_t* n);
-/* Zero-capacity virtual nodes received by each of the world*C clusters (AddVirtualNode). */
+/* Virtual nodes received by each of the world*C clusters (AddVirtualNode, cluster.go:65-85):
+ * zero-capacity under FIFO, the contract's capacity under DELAY. */
 int mcs_read_virtual_nodes(mcs_engine* eng, uint32_t* out, uint32_t n_total);
+
+/* ---- DELAY trading (MCS_POLICY_DELAY with cfg.trader; one engine holds the system) ---------- */
+/* Trader rounds with their contracts, in (t_s, requester) order; *n = total count. */
+int mcs_read_contracts(mcs_engine* eng, mcs_contract_rec* out, uint64_t cap, uint64_t* n);
+/* Foreign jobs in launch order; *n = total count. */
+int mcs_read_foreign(mcs_engine* eng, mcs_foreign_rec* out, uint64_t cap, uint64_t* n);
+/* Capacities {cores, memory} of the virtual nodes cluster `cluster` received, in order (node
+ * index n_physical + i); *n = their count. */
+int mcs_read_virtual_node_caps(mcs_engine* eng, uint32_t cluster, uint32_t* cores, uint32_t* mem,
+                               uint32_t cap, uint32_t* n);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,378 @@
+// mcs_dtrade.cpp — host side of the lock-step trading system with DELAY schedulers (DESIGN.md
+// §11): device state, the tick loop (three kernels per tick, 64 ticks per captured hipGraph,
+// one host poll per replay), capacity escalation and the result readers of mcs_trade.h.
+// Every decision is made by the gfx950 kernels of mcs_dtrade.hip; there is no CPU path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "mcs_dtrade_internal.h"
+#include "mcs_engine_impl.h"
+
+namespace mcs {
+
+struct DtradeDev {
+    DtArgs a{};
+    unsigned long long* tn = nullptr;
+    unsigned long long* vn = nullptr;
+    uint2* vcap = nullptr;
+    uint32_t* sfin = nullptr;
+    uint32_t* snode = nullptr;
+    unsigned long long* scm = nullptr;
+    uint32_t* l1 = nullptr;
+    long long* jmap = nullptr;
+    DtCluster* cl = nullptr;
+    DtTrader* tr = nullptr;
+    DtCtl* ctl = nullptr;
+    mcs_contract_rec* trades = nullptr;
+    mcs_foreign_rec* foreign = nullptr;
+    DtCtl* h_ctl = nullptr;
+    hipGraphExec_t graph = nullptr;
+};
+
+namespace {
+
+constexpr uint32_t kDtGraphTicks = 64;
+
+int dt_hip_fail(mcs_engine* e, const char* what, hipError_t st) {
+    return fail(e, MCS_E_HIP, std::string(what) + ": " + hipGetErrorString(st));
+}
+
+uint32_t dt_auto_slots(uint32_t max_n) {
+    uint32_t s = 256;
+    while (s < 4u * max_n && s < kDtMaxSlots) s *= 2;
+    return s;
+}
+
+int dtrade_alloc(mcs_engine* e) {
+    if (e->dtd) return MCS_OK;
+    const uint32_t C = e->C;
+    if (C > kDtMaxClusters) return fail(e, MCS_E_INVALID, "more than 1024 clusters in a trading system");
+    if (e->max_n > kDtMaxNodes) return fail(e, MCS_E_INVALID, "more than 1024 nodes in a cluster");
+    const uint32_t S = e->cfg.slot_pool ? 64u * e->cfg.slot_pool : (e->tr_slots ? e->tr_slots : dt_auto_slots(e->max_n));
+    if (S > kDtMaxSlots) return fail(e, MCS_E_INVALID, "slot pool above 4096");
+    const uint32_t V = e->dt_vnodes ? e->dt_vnodes : 16u;
+    DtradeDev* d = new (std::nothrow) DtradeDev();
+    if (!d) return fail(e, MCS_E_NOMEM, "DELAY trading state");
+    e->dtd = d;
+    const size_t nj = e->total_jobs ? e->total_jobs : 1;
+    const uint64_t trade_cap = 1ull << 20, foreign_cap = 1ull << 22;
+    HIPCHK(e, hipMalloc(&d->tn, std::max<uint64_t>(e->total_nodes, 1) * 8));
+    HIPCHK(e, hipMalloc(&d->vn, (size_t)C * V * 8));
+    HIPCHK(e, hipMalloc(&d->vcap, (size_t)C * V * sizeof(uint2)));
+    HIPCHK(e, hipMalloc(&d->sfin, (size_t)C * S * 4));
+    HIPCHK(e, hipMalloc(&d->snode, (size_t)C * S * 4));
+    HIPCHK(e, hipMalloc(&d->scm, (size_t)C * S * 8));
+    HIPCHK(e, hipMalloc(&d->l1, nj * 4));
+    HIPCHK(e, hipMalloc(&d->jmap, nj * 8));
+    HIPCHK(e, hipMalloc(&d->cl, C * sizeof(DtCluster)));
+    HIPCHK(e, hipMalloc(&d->tr, C * sizeof(DtTrader)));
+    HIPCHK(e, hipMalloc(&d->ctl, sizeof(DtCtl)));
+    HIPCHK(e, hipMalloc(&d->trades, trade_cap * sizeof(mcs_contract_rec)));
+    HIPCHK(e, hipMalloc(&d->foreign, foreign_cap * sizeof(mcs_foreign_rec)));
+    HIPCHK(e, hipHostMalloc(&d->h_ctl, sizeof(DtCtl), hipHostMallocDefault));
+    DtArgs& a = d->a;
+    a.C = C;
+    a.V = V;
+    a.S = S;
+    a.period = e->cfg.trader_period_s;
+    a.ok_sleep = e->cfg.trade_ok_sleep_s;
+    a.fail_sleep = e->cfg.trade_fail_sleep_s;
+    a.lock_s = e->cfg.lock_s;
+    a.sample_period = e->cfg.sample_period_s ? e->cfg.sample_period_s : 5u;
+    a.max_wait = e->cfg.max_wait_s;
+    a.t_max = e->cfg.t_max_s ? e->cfg.t_max_s : 0xFFFFFFFEu;
+    a.trade_cap = trade_cap;
+    a.foreign_cap = foreign_cap;
+    a.node_off = e->d_node_off;
+    a.cap = e->d_cap;
+    a.free0 = e->d_free0;
+    a.tn = d->tn;
+    a.vn = d->vn;
+    a.vcap = d->vcap;
+    a.jobs = e->d_jobs;
+    a.job_off = e->d_job_off;
+    a.out_node = e->d_out_node;
+    a.out_start = e->d_out_start;
+    a.out_finish = e->d_out_finish;
+    a.sfin = d->sfin;
+    a.snode = d->snode;
+    a.scm = d->scm;
+    a.l1 = d->l1;
+    a.jmap = d->jmap;
+    a.cl = d->cl;
+    a.tr = d->tr;
+    a.ctl = d->ctl;
+    a.trade_log = d->trades;
+    a.foreign_log = d->foreign;
+    return MCS_OK;
+}
+
+int dt_poll(mcs_engine* e) {
+    HIPCHK(e, hipMemcpyAsync(e->dtd->h_ctl, e->dtd->ctl, sizeof(DtCtl), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return MCS_OK;
+}
+
+int dt_run_once(mcs_engine* e, double* kernel_ms) {
+    DtradeDev* d = e->dtd;
+    hipError_t st = launch_dtrade_init(d->a, e->stream);
+    if (st != hipSuccess) return dt_hip_fail(e, "DELAY trading init", st);
+    if (!d->graph) {
+        hipGraph_t g = nullptr;
+        HIPCHK(e, hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+        for (uint32_t t = 0; t < kDtGraphTicks; ++t) {
+            st = launch_dtrade_tick(d->a, e->stream);
+            if (st != hipSuccess) {
+                (void)hipStreamEndCapture(e->stream, &g);
+                if (g) (void)hipGraphDestroy(g);
+                return dt_hip_fail(e, "DELAY trading capture", st);
+            }
+        }
+        HIPCHK(e, hipStreamEndCapture(e->stream, &g));
+        st = hipGraphInstantiate(&d->graph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (st != hipSuccess) return dt_hip_fail(e, "hipGraphInstantiate", st);
+    }
+    HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+    for (;;) {
+        HIPCHK(e, hipGraphLaunch(d->graph, e->stream));
+        if (int s = dt_poll(e)) return s;
+        if (d->h_ctl->done) break;
+    }
+    HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    float ms = 0.0f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+    *kernel_ms = ms;
+    return MCS_OK;
+}
+
+int dt_clusters(mcs_engine* e, std::vector<DtCluster>& cl) {
+    cl.resize(e->C);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(cl.data(), e->dtd->cl, e->C * sizeof(DtCluster), hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpy(e->dtd->h_ctl, e->dtd->ctl, sizeof(DtCtl), hipMemcpyDeviceToHost));
+    return MCS_OK;
+}
+
+}  // namespace
+
+void dtrade_free(mcs_engine* e) {
+    DtradeDev* d = e->dtd;
+    if (!d) return;
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (d->graph) (void)hipGraphExecDestroy(d->graph);
+    dfree(d->tn);
+    dfree(d->vn);
+    dfree(d->vcap);
+    dfree(d->sfin);
+    dfree(d->snode);
+    dfree(d->scm);
+    dfree(d->l1);
+    dfree(d->jmap);
+    dfree(d->cl);
+    dfree(d->tr);
+    dfree(d->ctl);
+    dfree(d->trades);
+    dfree(d->foreign);
+    if (d->h_ctl) (void)hipHostFree(d->h_ctl);
+    delete d;
+    e->dtd = nullptr;
+    e->dtrade_run = false;
+}
+
+int dtrade_run(mcs_engine* e, mcs_stats* stats) {
+    if (e->world > 1)
+        return fail(e, MCS_E_INVALID, "DELAY trading runs on one engine holding the whole system (world 1)");
+    const auto w0 = std::chrono::steady_clock::now();
+    e->tr_slots = 0;
+    e->dt_vnodes = 0;
+    uint32_t escalations = 0;
+    double kms = 0.0;
+    for (;;) {
+        if (int s = dtrade_alloc(e)) return s;
+        double ms = 0.0;
+        if (int s = dt_run_once(e, &ms)) return s;
+        kms += ms;
+        std::vector<DtCluster> cl;
+        if (int s = dt_clusters(e, cl)) return s;
+        uint32_t flags = e->dtd->h_ctl->flags;
+        for (const auto& k : cl) flags |= k.flags;
+        const uint32_t S = e->dtd->a.S, V = e->dtd->a.V;
+        bool grow_s = (flags & MCS_FLAG_OVERFLOW) != 0, grow_v = (flags & MCS_FLAG_VNODE_OVERFLOW) != 0;
+        if (!grow_s && !grow_v) break;
+        if ((grow_s && (e->cfg.slot_pool || S >= kDtMaxSlots)) || (grow_v && V >= kDtMaxVnodes))
+            return fail(e, MCS_E_CAPACITY, "DELAY trading capacity exhausted (slots or virtual nodes)");
+        const uint32_t ns = grow_s ? S * 2u : S, nv = grow_v ? std::min<uint32_t>(V * 4u, kDtMaxVnodes) : V;
+        dtrade_free(e);
+        e->tr_slots = ns;
+        e->dt_vnodes = nv;
+        ++escalations;
+    }
+    e->has_run = true;
+    e->dtrade_run = true;
+    e->trade_run = false;
+    e->delay_run = true;
+    if (stats) {
+        std::vector<DtCluster> cl;
+        if (int s = dt_clusters(e, cl)) return s;
+        mcs_stats st{};
+        st.jobs = e->total_jobs;
+        for (uint32_t k = 0; k < e->C; ++k) {
+            st.placed += cl[k].decided;
+            st.waited += cl[k].moved;
+        }
+        st.unplaced = e->total_jobs - st.placed;
+        st.clusters = e->C;
+        st.escalations = escalations;
+        st.slot_pool = e->dtd->a.S / 64u;
+        st.kernel_ms = kms;
+        st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+        *stats = st;
+    }
+    return MCS_OK;
+}
+
+int dtrade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n) {
+    std::vector<DtCluster> cl;
+    if (int s = dt_clusters(e, cl)) return s;
+    for (uint32_t k = 0; k < n; ++k) {
+        mcs_cluster_stats s{};
+        s.t_end = e->dtd->h_ctl->T;
+        s.placed = cl[k].decided;
+        s.waited = cl[k].moved;
+        s.peak_running = cl[k].peak;
+        s.flags = cl[k].flags;
+        s.pool = e->dtd->a.S / 64u;
+        s.iterations = e->dtd->h_ctl->ticks;
+        s.release_scans = 0;
+        out[k] = s;
+    }
+    return MCS_OK;
+}
+
+int dtrade_delay_stats(mcs_engine* e, mcs_delay_cluster_stats* out, uint32_t n) {
+    std::vector<DtCluster> cl;
+    if (int s = dt_clusters(e, cl)) return s;
+    for (uint32_t k = 0; k < n; ++k) {
+        mcs_delay_cluster_stats d{};
+        d.total_wait_ms = cl[k].total;
+        d.jobs_count = cl[k].count;
+        d.moved_l1 = cl[k].moved;
+        d.placed_l1 = cl[k].placed_l1;
+        d.peak_l1 = 0;
+        d.l1_left = cl[k].l1n;
+        out[k] = d;
+    }
+    return MCS_OK;
+}
+
+int dtrade_trade_stats(mcs_engine* e, mcs_trade_stats* out) {
+    std::vector<DtCluster> cl;
+    if (int s = dt_clusters(e, cl)) return s;
+    const DtCtl& c = *e->dtd->h_ctl;
+    mcs_trade_stats s{};
+    uint32_t flags = c.flags;
+    for (uint32_t k = 0; k < e->C; ++k) {
+        const uint64_t J = e->job_off[k + 1] - e->job_off[k];
+        s.placed += cl[k].decided;
+        s.waited += cl[k].moved;
+        s.undecided += J - cl[k].decided;
+        flags |= cl[k].flags;
+    }
+    if (c.n_trades > e->dtd->a.trade_cap || c.n_foreign > e->dtd->a.foreign_cap) flags |= MCS_FLAG_LOG_OVERFLOW;
+    s.trades = c.n_trades;
+    s.trades_won = c.n_won;
+    s.ticks = c.ticks;
+    s.t_final = c.T;
+    s.flags = flags;
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) ms = 0.0f;
+    s.kernel_ms = ms;
+    *out = s;
+    return MCS_OK;
+}
+
+int dtrade_read_trades(mcs_engine* e, mcs_trade_rec* out, uint64_t cap, uint64_t* n) {
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(e->dtd->h_ctl, e->dtd->ctl, sizeof(DtCtl), hipMemcpyDeviceToHost));
+    const uint64_t total = e->dtd->h_ctl->n_trades;
+    const uint64_t k = std::min<uint64_t>(std::min<uint64_t>(total, e->dtd->a.trade_cap), cap);
+    if (k) {
+        std::vector<mcs_contract_rec> v(k);
+        HIPCHK(e, hipMemcpy(v.data(), e->dtd->trades, k * sizeof(mcs_contract_rec), hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < k; ++i) out[i] = mcs_trade_rec{v[i].t_s, v[i].requester, v[i].winner, v[i].approvals};
+    }
+    *n = total;
+    return MCS_OK;
+}
+
+int dtrade_read_vnode_counts(mcs_engine* e, uint32_t* out, uint32_t n) {
+    std::vector<DtCluster> cl;
+    if (int s = dt_clusters(e, cl)) return s;
+    for (uint32_t k = 0; k < n; ++k) out[k] = cl[k].nv;
+    return MCS_OK;
+}
+
+}  // namespace mcs
+
+extern "C" {
+
+int mcs_read_contracts(mcs_engine* e, mcs_contract_rec* out, uint64_t cap, uint64_t* n) {
+    if (int st = check_engine(e)) return st;
+    if (!n || (cap && !out)) return fail(e, MCS_E_INVALID, "bad output");
+    if (!e->dtrade_run || !e->dtd) return fail(e, MCS_E_STATE, "no DELAY trading run");
+    mcs::DtradeDev* d = e->dtd;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(d->h_ctl, d->ctl, sizeof(mcs::DtCtl), hipMemcpyDeviceToHost));
+    const uint64_t total = d->h_ctl->n_trades;
+    const uint64_t k = std::min<uint64_t>(std::min<uint64_t>(total, d->a.trade_cap), cap);
+    if (k) HIPCHK(e, hipMemcpy(out, d->trades, k * sizeof(mcs_contract_rec), hipMemcpyDeviceToHost));
+    *n = total;
+    return MCS_OK;
+}
+
+int mcs_read_foreign(mcs_engine* e, mcs_foreign_rec* out, uint64_t cap, uint64_t* n) {
+    if (int st = check_engine(e)) return st;
+    if (!n || (cap && !out)) return fail(e, MCS_E_INVALID, "bad output");
+    if (!e->dtrade_run || !e->dtd) return fail(e, MCS_E_STATE, "no DELAY trading run");
+    mcs::DtradeDev* d = e->dtd;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(d->h_ctl, d->ctl, sizeof(mcs::DtCtl), hipMemcpyDeviceToHost));
+    const uint64_t total = d->h_ctl->n_foreign;
+    const uint64_t k = std::min<uint64_t>(std::min<uint64_t>(total, d->a.foreign_cap), cap);
+    if (k) HIPCHK(e, hipMemcpy(out, d->foreign, k * sizeof(mcs_foreign_rec), hipMemcpyDeviceToHost));
+    *n = total;
+    return MCS_OK;
+}
+
+int mcs_read_virtual_node_caps(mcs_engine* e, uint32_t cluster, uint32_t* cores, uint32_t* mem,
+                               uint32_t cap, uint32_t* n) {
+    if (int st = check_engine(e)) return st;
+    if (!n || (cap && (!cores || !mem))) return fail(e, MCS_E_INVALID, "bad output");
+    if (!e->dtrade_run || !e->dtd) return fail(e, MCS_E_STATE, "no DELAY trading run");
+    if (cluster >= e->C) return fail(e, MCS_E_INVALID, "cluster index out of range");
+    mcs::DtradeDev* d = e->dtd;
+    mcs::DtCluster k{};
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(&k, d->cl + cluster, sizeof(k), hipMemcpyDeviceToHost));
+    const uint32_t m = std::min<uint32_t>(std::min<uint32_t>(k.nv, d->a.V), cap);
+    if (m) {
+        std::vector<uint2> v(m);
+        HIPCHK(e, hipMemcpy(v.data(), d->vcap + (size_t)cluster * d->a.V, m * sizeof(uint2), hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < m; ++i) {
+            cores[i] = v[i].x;
+            mem[i] = v[i].y;
+        }
+    }
+    *n = k.nv;
+    return MCS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,695 @@
+// mcs_dtrade.hip — gfx950 kernels of the lock-step trading system with DELAY schedulers
+// (semantics restated in oracle/mcs_oracle_dtrade.c, header of mcs_dtrade_internal.h).
+//
+// One tick T is three launches on the engine stream (each a grid-wide barrier), replayed from a
+// captured hipGraph 64 ticks at a time:
+//   A dt_step_kernel    one wave per cluster: one Delay iteration (pkg/scheduler/scheduler.go:
+//                       298-369): releases, "/delay" arrivals, the Level1 pass with its skip (D6)
+//                       through an exact fit filter, the Level0 head and its MaxWaitTime move,
+//                       and the WaitTime statistics (scheduler.go:309-312,338-341)
+//   C dt_sample_kernel  one wave per cluster at T % 5 == 0: GetResourceUtilization over physical
+//                       and virtual nodes (cluster.go:46-63, float32 in node order) and
+//                       WaitTime.GetAverage (scheduler.go:56-63)
+//   D dt_trader_kernel  one wave for the system: trader rounds in cluster order
+//                       (trader.go:280-325): contract sizing over the requester's Level1
+//                       (scheduler_client.go:126-289), RequestResource/ApproveTrade with locks
+//                       across lanes (pkg/trader/server.go:31-61, trader.go:141-167), heap order,
+//                       ApproveContract -> AllocateVirtualNodeResources on the responder
+//                       (Foreign jobs into its running slots, cluster.go:87-125) and
+//                       AddVirtualNode on the requester (cluster.go:65-85); then the next tick.
+// Per-cluster state a wave writes and re-reads inside a kernel is staged in LDS, or read back with
+// sc1 loads (L2) after an atomic write, never through this CU's non-coherent vector L1.
+#include "mcs_dtrade_internal.h"
+#include "mcs_wave.h"
+
+namespace mcs {
+namespace {
+
+__device__ __forceinline__ uint32_t dt_wave_sum_u32(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+
+__device__ __forceinline__ long long dt_wave_sum_i64(long long v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)(unsigned long long)v, o);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)((unsigned long long)v >> 32), o);
+        v += (long long)((unsigned long long)lo | ((unsigned long long)hi << 32));
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t dt_wave_max_u32(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t w = (uint32_t)__shfl_xor((int)v, o);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+
+// Go uint64 value of a device free counter (sign extension of the u32, see the header)
+__device__ __forceinline__ unsigned long long go_u64(uint32_t x) {
+    return (unsigned long long)(long long)(int32_t)x;
+}
+__device__ __forceinline__ float go_f32(uint32_t x) { return (float)go_u64(x); }
+__device__ __forceinline__ double go_f64(uint32_t x) { return (double)go_u64(x); }
+
+// Go's float64 -> uint conversion on amd64 (mcs_oracle_dtrade.c: go_f64_to_u64)
+__device__ __forceinline__ unsigned long long go_f64_to_u64(double x) {
+    const double two63 = 9223372036854775808.0;
+    if (x < two63) return (unsigned long long)(long long)x;
+    const double y = x - two63;
+    if (y >= two63) return 0ull;
+    return (unsigned long long)(long long)y ^ 0x8000000000000000ull;
+}
+
+__device__ __forceinline__ uint32_t ld32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld64(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void dt_init_kernel(DtArgs a) {
+    const uint32_t c = blockIdx.x, lane = threadIdx.x;
+    const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
+    uint32_t sc = 0, sm = 0;
+    for (uint32_t i = lane; i < N; i += kWave) {
+        const uint2 f = a.free0[n0 + i];
+        a.tn[n0 + i] = (unsigned long long)f.x | ((unsigned long long)f.y << 32);
+        const uint2 cp = a.cap[n0 + i];
+        sc += cp.x;  // SetTotalResources: uint32 sums (cluster.go:34-37)
+        sm += cp.y;
+    }
+    sc = dt_wave_sum_u32(sc);
+    sm = dt_wave_sum_u32(sm);
+    for (uint32_t s = lane; s < a.S; s += kWave) a.sfin[(size_t)c * a.S + s] = kEmpty;
+    const uint64_t j0 = a.job_off[c], j1 = a.job_off[c + 1];
+    for (uint64_t j = j0 + lane; j < j1; j += kWave) {
+        a.out_node[j] = MCS_NODE_UNPLACED;
+        a.out_start[j] = MCS_TIME_NONE;
+        a.out_finish[j] = MCS_TIME_NONE;
+        a.jmap[j] = 0;
+    }
+    if (lane == 0) {
+        DtCluster z{};
+        z.minf = kEmpty;
+        z.total_c = sc;
+        z.total_m = sm;
+        a.cl[c] = z;
+        DtTrader t{};
+        t.next_id = 1u;  // s.id = rand.Uint32() (pkg/trader/server.go:26), seeded: 1
+        a.tr[c] = t;
+    }
+    if (c == 0 && lane == 0) {
+        DtCtl z{};
+        *a.ctl = z;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Phase A: one Delay iteration of cluster c at tick T.
+__global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
+    __shared__ unsigned long long nodes[kDtMaxNodes + kDtMaxVnodes];
+    __shared__ uint32_t sfin[kDtMaxSlots];
+    __shared__ uint32_t hist[kWave];
+    if (a.ctl->done) return;
+    const uint32_t T = a.ctl->T;
+    const uint32_t c = blockIdx.x, lane = threadIdx.x;
+    const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
+    const uint64_t j0 = a.job_off[c];
+    const uint32_t J = (uint32_t)(a.job_off[c + 1] - j0);
+    const uint4* __restrict__ jobs = a.jobs + j0;
+    uint32_t* __restrict__ l1 = a.l1 + j0;
+    long long* __restrict__ jmap = a.jmap + j0;
+    const size_t sb = (size_t)c * a.S;
+    const uint32_t S = a.S;
+    DtCluster st = a.cl[c];
+    const uint32_t NN = N + st.nv;
+
+    for (uint32_t i = lane; i < NN; i += kWave)
+        nodes[i] = i < N ? a.tn[n0 + i] : a.vn[(size_t)c * a.V + (i - N)];
+    for (uint32_t s = lane; s < S; s += kWave) sfin[s] = a.sfin[sb + s];
+    __syncthreads();
+
+    // releases due at T (cluster.go:153-157), Foreign jobs included
+    if (st.minf <= T) {
+        uint32_t lm = kEmpty, nrel = 0;
+        for (uint32_t s = lane; s < S; s += kWave) {
+            const uint32_t f = sfin[s];
+            if (f <= T) {
+                // per u32 half: a wrapped counter's low half may carry (Go's uint64 wraps back)
+                const unsigned long long cm = a.scm[sb + s];
+                uint32_t* h = reinterpret_cast<uint32_t*>(&nodes[a.snode[sb + s]]);
+                atomicAdd(h, (uint32_t)cm);
+                atomicAdd(h + 1, (uint32_t)(cm >> 32));
+                sfin[s] = kEmpty;
+                ++nrel;
+            } else {
+                lm = f < lm ? f : lm;
+            }
+        }
+        st.nrun -= dt_wave_sum_u32(nrel);
+        st.minf = wave_min_u32(lm);
+        __syncthreads();
+    }
+    // "/delay" arrivals up to T join Level0 (server.go:67-74): JobsMap[id] = 0, JobsCount++
+    {
+        const uint32_t before = st.next_arr;
+        while (st.next_arr < J) {
+            const uint32_t i = st.next_arr + lane;
+            const bool ok = i < J && jobs[i].x <= T;
+            const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(ok));
+            st.next_arr += n;
+            if (n < (uint32_t)kWave) break;
+        }
+        st.count += (long long)(st.next_arr - before);
+    }
+
+    // ScheduleJob (scheduler.go:127-139) over Cluster.Nodes: physical, then virtual
+    auto first_fit = [&](uint32_t jc, uint32_t jm) -> uint32_t {
+        uint32_t best = kEmpty;
+        for (uint32_t b = 0; b < NN; b += kWave) {
+            const uint32_t i = b + lane;
+            if (i < NN) {
+                const unsigned long long v = nodes[i];
+                if ((uint32_t)v >= jc && (uint32_t)(v >> 32) >= jm) best = i;
+            }
+            if (__ballot(best != kEmpty)) break;
+        }
+        return wave_min_u32(best);
+    };
+    // Node.RunJob commit (cluster.go:144-148) + running slot; false on slot overflow
+    auto commit = [&](uint32_t k, uint32_t jc, uint32_t jm, uint32_t fin) -> bool {
+        const unsigned long long need = (unsigned long long)jc | ((unsigned long long)jm << 32);
+        uint32_t slot = kEmpty;
+        for (uint32_t b = 0; b < S; b += kWave) {
+            const unsigned long long fr = __ballot(sfin[b + lane] == kEmpty);
+            if (fr) {
+                slot = b + (uint32_t)__builtin_ctzll(fr);
+                break;
+            }
+        }
+        if (slot == kEmpty) return false;
+        if (lane == 0) {
+            // u32 halves: a wrapped node may borrow across them (Go's uint64 counters would
+            // wrap the same way), so update each half on its own
+            nodes[k] = (unsigned long long)((uint32_t)nodes[k] - jc) |
+                       ((unsigned long long)((uint32_t)(nodes[k] >> 32) - jm) << 32);
+            sfin[slot] = fin;
+            a.snode[sb + slot] = k;
+            a.scm[sb + slot] = need;
+        }
+        __syncthreads();
+        ++st.nrun;
+        st.peak = st.nrun > st.peak ? st.nrun : st.peak;
+        st.minf = fin < st.minf ? fin : st.minf;
+        return true;
+    };
+
+    // ---- Level1 pass (scheduler.go:302-329) ----
+    if (st.l1n != 0u) {
+        // exact fit filter (see mcs_delay.hip): lane l holds the max free memory over nodes with
+        // min(free cores, 63) >= l; conservative for wrapped counters (huge u32 values)
+        hist[lane] = 0u;
+        __syncthreads();
+        uint32_t mc = 0u;
+        for (uint32_t i = lane; i < NN; i += kWave) {
+            const unsigned long long v = nodes[i];
+            const uint32_t fc = (uint32_t)v;
+            atomicMax(&hist[fc < 63u ? fc : 63u], (uint32_t)(v >> 32));
+            mc = fc > mc ? fc : mc;
+        }
+        __syncthreads();
+        const uint32_t max_c = dt_wave_max_u32(mc);
+        uint32_t best = hist[lane];
+        for (int o = 1; o < kWave; o <<= 1) {
+            const uint32_t w = (uint32_t)__shfl_down((int)best, o);
+            best = (lane + (uint32_t)o < (uint32_t)kWave && w > best) ? w : best;
+        }
+        uint32_t wr = 0;
+        bool carry_skip = false;  // the last entry of the previous row was placed
+        const uint32_t n1 = st.l1n;
+        for (uint32_t base = 0; base < n1; base += kWave) {
+            const uint32_t pos = base + lane;
+            const bool live = pos < n1;
+            const uint32_t j = live ? l1[pos] : 0u;
+            const uint4 jb = live ? jobs[j] : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t bm = (uint32_t)__shfl((int)best, (int)(jb.z < 63u ? jb.z : 63u));
+            unsigned long long cand = __ballot(live && jb.z <= max_c && bm >= jb.w);
+            unsigned long long placedm = 0ull, skipm = carry_skip ? 1ull : 0ull;
+            bool overflow = false;
+            while (cand) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(cand);
+                cand &= cand - 1ull;
+                if ((skipm >> b) & 1ull) continue;  // slid into slot i: not examined (D6)
+                const uint32_t jc = readlane(jb.z, b), jm = readlane(jb.w, b);
+                const uint32_t k = first_fit(jc, jm);
+                if (k == kEmpty) continue;
+                const uint32_t jd = readlane(jb.y, b), jj = readlane(j, b);
+                const uint32_t fin = T + jd;
+                if (jd != 0u && !commit(k, jc, jm, fin)) {
+                    overflow = true;
+                    break;
+                }
+                if (lane == 0) {
+                    a.out_node[j0 + jj] = (int32_t)k;
+                    a.out_start[j0 + jj] = T;
+                    a.out_finish[j0 + jj] = fin;
+                }
+                placedm |= 1ull << b;
+                if (b < 63u) skipm |= 1ull << (b + 1u);
+                ++st.decided;
+                ++st.placed_l1;
+            }
+            if (overflow) {
+                st.flags |= MCS_FLAG_OVERFLOW;
+                wr = n1;  // state is abandoned (the engine re-runs with more slots)
+                break;
+            }
+            const unsigned long long livem = __ballot(live);
+            const uint32_t last = 63u - (uint32_t)__builtin_clzll(livem);
+            carry_skip = ((placedm >> last) & 1ull) != 0ull && last == 63u;
+            // WaitTime update of every examined job (the skipped one is not examined)
+            long long delta = 0;
+            const bool examined = live && !((skipm >> lane) & 1ull);
+            const bool placed = ((placedm >> lane) & 1ull) != 0ull;
+            if (examined) {
+                const long long nv = (long long)(T - jb.x) * 1000ll;
+                delta = nv - jmap[j];
+                jmap[j] = placed ? 0ll : nv;  // delete(JobsMap, id) on success (:316)
+            }
+            st.total += dt_wave_sum_i64(delta);
+            // compaction in the same sweep (append(Level1[:i], Level1[i+1:]...), :319)
+            const unsigned long long kept = livem & ~placedm;
+            if (live && !placed) {
+                const uint32_t np = wr + (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                                             (uint32_t)(kept >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((uint32_t)kept, 0u));
+                if (np != pos) l1[np] = j;
+            }
+            wr += (uint32_t)__builtin_popcountll(kept);
+        }
+        st.l1n = wr;
+    }
+
+    // ---- Level0 head (scheduler.go:332-366) ----
+    if (!(st.flags & MCS_FLAG_OVERFLOW) && st.l0_head < st.next_arr) {
+        const uint32_t j = st.l0_head;
+        const uint4 jb = jobs[j];
+        const uint32_t k = first_fit(jb.z, jb.w);
+        const long long nv = (long long)(T - jb.x) * 1000ll;
+        const long long old = jmap[j];
+        st.total += nv - old;
+        if (k != kEmpty) {
+            const uint32_t fin = T + jb.y;
+            if (jb.y != 0u && !commit(k, jb.z, jb.w, fin)) {
+                st.flags |= MCS_FLAG_OVERFLOW;
+            } else {
+                if (lane == 0) {
+                    a.out_node[j0 + j] = (int32_t)k;
+                    a.out_start[j0 + j] = T;
+                    a.out_finish[j0 + j] = fin;
+                    jmap[j] = 0;
+                }
+                ++st.l0_head;
+                ++st.decided;
+            }
+        } else {
+            if (lane == 0) jmap[j] = nv;
+            if (T - jb.x >= a.max_wait) {  // MaxWaitTime (:353): Level1 append (:357)
+                if (lane == 0) l1[st.l1n] = j;
+                ++st.l1n;
+                ++st.l0_head;
+                ++st.moved;
+            }
+        }
+    }
+
+    __syncthreads();
+    for (uint32_t i = lane; i < NN; i += kWave) {
+        if (i < N)
+            a.tn[n0 + i] = nodes[i];
+        else
+            a.vn[(size_t)c * a.V + (i - N)] = nodes[i];
+    }
+    for (uint32_t s = lane; s < S; s += kWave) a.sfin[sb + s] = sfin[s];
+    if (lane == 0) a.cl[c] = st;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Phase C: the state stream sample (trader_server.go:24-47) every sample_period seconds.
+__global__ __launch_bounds__(64) void dt_sample_kernel(DtArgs a) {
+    __shared__ float dc[kDtMaxNodes + kDtMaxVnodes], dm[kDtMaxNodes + kDtMaxVnodes];
+    if (a.ctl->done) return;
+    const uint32_t T = a.ctl->T;
+    if (T % a.sample_period != 0u) return;
+    const uint32_t c = blockIdx.x, lane = threadIdx.x;
+    const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
+    DtCluster st = a.cl[c];
+    const uint32_t NN = N + st.nv;
+    for (uint32_t i = lane; i < NN; i += kWave) {
+        unsigned long long v;
+        uint2 cp;
+        if (i < N) {
+            v = a.tn[n0 + i];
+            cp = a.cap[n0 + i];
+        } else {
+            v = a.vn[(size_t)c * a.V + (i - N)];
+            cp = a.vcap[(size_t)c * a.V + (i - N)];
+        }
+        // float32(node.Cores) - float32(node.CoresAvailable) (cluster.go:55-56), uint64 -> float32
+        dc[i] = __fsub_rn((float)cp.x, go_f32((uint32_t)v));
+        dm[i] = __fsub_rn((float)cp.y, go_f32((uint32_t)(v >> 32)));
+    }
+    __syncthreads();
+    if (lane == 0) {
+        float sc = 0.0f, sm = 0.0f;
+        for (uint32_t i = 0; i < NN; ++i) {  // node order, float32 like Go
+            sc = __fadd_rn(sc, dc[i]);
+            sm = __fadd_rn(sm, dm[i]);
+        }
+        a.cl[c].cu = __fdiv_rn(sc, (float)st.total_c);
+        a.cl[c].mu = __fdiv_rn(sm, (float)st.total_m);
+        // WaitTime.GetAverage (scheduler.go:56-63)
+        a.cl[c].avgw = st.count != 0 ? __ddiv_rn((double)st.total, (double)st.count) : 0.0;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// ApproveTrade (trader.go:141-167) with approvePolicy{0.8, 0.8, -1, -1}, like or_approve_trade
+__device__ __forceinline__ bool dt_approve(uint32_t tc, uint32_t tm, float cu, float mu, uint32_t kc,
+                                           uint32_t km, uint32_t ksec) {
+    if (!(cu < 0.8f && mu < 0.8f)) return false;
+    const float ftm = (float)tm, ftc = (float)tc;
+    const float avail_mem = __fsub_rn(ftm, __fmul_rn(ftm, mu));
+    const float avail_core = __fsub_rn(ftc, __fmul_rn(ftc, cu));
+    if (!(avail_core >= (float)kc && avail_mem >= (float)km)) return false;
+    const double secs = (double)ksec;  // Duration.Seconds() of whole seconds
+    const double b = __dmul_rn(__dmul_rn(-1.0, (double)kc), secs);
+    const double d = __dmul_rn(__dmul_rn(-1.0, (double)km), secs);
+    const double incentive = __dadd_rn(b, d);
+    return 0.0 >= incentive;  // float64(price 0) >= incentive (:155)
+}
+
+// Phase D: trader rounds in cluster order, then the next tick.
+__global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
+    __shared__ DtTrader trs[kDtMaxClusters];
+    __shared__ uint32_t appr[kDtMaxClusters];
+    __shared__ uint32_t nvs[kDtMaxClusters];  // virtual nodes per cluster (written here)
+    if (a.ctl->done) return;
+    const uint32_t T = a.ctl->T;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t C = a.C;
+    for (uint32_t q = lane; q < C; q += kWave) {
+        trs[q] = a.tr[q];
+        nvs[q] = a.cl[q].nv;
+    }
+    __syncthreads();
+    unsigned long long n_trades = a.ctl->n_trades, n_won = a.ctl->n_won, n_for = a.ctl->n_foreign;
+    uint32_t lflags = 0;
+
+    for (uint32_t q0 = 0; q0 < C && a.period; q0 += kWave) {
+        const uint32_t ql = q0 + lane;
+        unsigned long long due = __ballot(ql < C && trs[ql].next_due <= T);
+        while (due) {
+            const uint32_t q = q0 + (uint32_t)__builtin_ctzll(due);
+            due &= due - 1ull;
+            // RequestPolicyMonitor of requester q (trader.go:282-324): two-stage machine
+            while (trs[q].next_due <= T) {
+                DtTrader tq = trs[q];
+                if (tq.stage == 0u) {  // cs := t.State.getState() (:284)
+                    tq.cs_cu = a.cl[q].cu;
+                    tq.cs_mu = a.cl[q].mu;
+                    tq.cs_avgw = a.cl[q].avgw;
+                }
+                const uint32_t pol = tq.stage;
+                const bool broken = pol == 0u ? (tq.cs_avgw > 600000.0)                     // :137-139
+                                              : (tq.cs_cu > 0.8f || tq.cs_mu > 0.8f);       // :127-130
+                tq.stage = pol == 0u ? 1u : 0u;
+                if (!broken) {
+                    if (pol == 1u) tq.next_due = T + a.period;  // time.Sleep(10 s) (:323)
+                    __syncthreads();
+                    if (lane == 0) trs[q] = tq;
+                    __syncthreads();
+                    continue;
+                }
+                // ---- calculateContractRequest over GetLevel1() (ProvideJobs, D9 padding) ----
+                const uint32_t ln = a.cl[q].l1n;
+                const uint64_t qj0 = a.job_off[q];
+                uint32_t sc = 0, sm = 0, md = 0;
+                for (uint32_t i = lane; i < ln; i += kWave) {
+                    const uint4 jb = a.jobs[qj0 + a.l1[qj0 + i]];
+                    if (pol == 0u) {  // fast node: sums and the longest duration (:138-155)
+                        sc += jb.z;
+                        sm += jb.w;
+                        md = jb.y > md ? jb.y : md;
+                    } else {          // small node: int32 arithmetic (:232-259)
+                        sc += (int32_t)(0u - jb.z) < 0 ? jb.z : 0u;
+                        sm += (int32_t)(0u - jb.w) < 0 ? jb.w : 0u;
+                    }
+                }
+                const uint32_t kc = dt_wave_sum_u32(sc), km = dt_wave_sum_u32(sm);
+                uint32_t ksec = dt_wave_max_u32(md);
+                if (pol == 1u) {
+                    // contract.Time per job: endTime if the previous time < endTime, else 0
+                    // (:263-265); a padded last batch (len % 20 != 0) ends with zero jobs -> 0
+                    uint32_t t = 0;
+                    if (lane == 0) {
+                        if (ln % 20u == 0u) {
+                            for (uint32_t i = 0; i < ln; ++i) {
+                                const uint32_t d = a.jobs[qj0 + a.l1[qj0 + i]].y;
+                                t = t < d ? d : 0u;
+                            }
+                        }
+                    }
+                    ksec = (uint32_t)__shfl((int)t, 0);
+                }
+                // ---- Trade (trader.go:193-278): RequestResource to every other trader ----
+                uint32_t napp = 0;
+                for (uint32_t r0 = 0; r0 < C; r0 += kWave) {
+                    const uint32_t r = r0 + lane;
+                    bool app = false;
+                    if (r < C && r != q) {
+                        DtTrader t = trs[r];
+                        if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
+                        if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
+                            const DtCluster& rc = a.cl[r];
+                            app = dt_approve(rc.total_c, rc.total_m, rc.cu, rc.mu, kc, km, ksec);
+                            t.lock_id = t.next_id++;  // set even when not approving (:44-46)
+                            t.lock_until = T + a.lock_s;
+                        }
+                        trs[r] = t;
+                    }
+                    const unsigned long long ab = __ballot(app);
+                    if (app) {
+                        const uint32_t at = napp + (uint32_t)__builtin_amdgcn_mbcnt_hi(
+                                                       (uint32_t)(ab >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)ab, 0u));
+                        appr[at] = r;
+                    }
+                    napp += (uint32_t)__builtin_popcountll(ab);
+                }
+                __syncthreads();
+                // container/heap of equal prices (every response echoes the request's price,
+                // server.go:44) pops pushes a0, a1, ..., a(n-1) as a0, a(n-1), ..., a1
+                int32_t winner = -1;
+                uint32_t failed = 0;
+                for (uint32_t i = 0; i < napp && winner < 0; ++i) {
+                    const uint32_t r = appr[i == 0u ? 0u : napp - i];
+                    // ApproveContract (server.go:63-85): the lock set in this round still
+                    // matches; AllocateVirtualNodeResources on the responder (cluster.go:87-125)
+                    uint32_t rc_ = kc, rm_ = km;
+                    const uint32_t rn0 = a.node_off[r], rN = a.node_off[r + 1] - rn0;
+                    const uint32_t rNN = rN + nvs[r];
+                    bool ovf = false;
+                    for (uint32_t nd = 0; nd < rNN; ++nd) {
+                        if (rm_ == 0u && rc_ == 0u) break;  // :90-92
+                        unsigned long long* np_ = nd < rN ? &a.tn[rn0 + nd]
+                                                          : &a.vn[(size_t)r * a.V + (nd - rN)];
+                        const unsigned long long v = ld64(np_);
+                        double mem_diff = 0.0, core_diff = 0.0;
+                        if (rm_ > 0u) mem_diff = fabs(__dsub_rn((double)rm_, go_f64((uint32_t)(v >> 32))));
+                        if (rc_ > 0u) core_diff = fabs(__dsub_rn((double)rc_, go_f64((uint32_t)v)));
+                        if (mem_diff > (double)rm_)
+                            rm_ = 0u;
+                        else
+                            rm_ -= (uint32_t)mem_diff;
+                        if (core_diff > (double)rc_)
+                            rc_ = 0u;
+                        else
+                            rc_ -= (uint32_t)core_diff;
+                        const unsigned long long fc = go_f64_to_u64(core_diff), fm = go_f64_to_u64(mem_diff);
+                        if (lane == 0) {
+                            if (n_for < a.foreign_cap) {
+                                mcs_foreign_rec fr;
+                                fr.requester = q;
+                                fr.responder = r;
+                                fr.node = nd;
+                                fr.start_s = T;
+                                fr.finish_s = T + ksec;
+                                fr.pad = 0u;
+                                fr.c = fc;
+                                fr.m = fm;
+                                a.foreign_log[n_for] = fr;
+                            } else {
+                                lflags |= MCS_FLAG_LOG_OVERFLOW;
+                            }
+                        }
+                        ++n_for;
+                        if (ksec == 0u) continue;  // RunJob sleeps 0: commit and release at once
+                        // go node.RunJob(Foreign) (:116): commit now, release at T + time
+                        uint32_t slot = kEmpty;
+                        const size_t rsb = (size_t)r * a.S;
+                        for (uint32_t b = 0; b < a.S; b += kWave) {
+                            const unsigned long long fr = __ballot(ld32(&a.sfin[rsb + b + lane]) == kEmpty);
+                            if (fr) {
+                                slot = b + (uint32_t)__builtin_ctzll(fr);
+                                break;
+                            }
+                        }
+                        if (slot == kEmpty) {
+                            ovf = true;
+                            break;
+                        }
+                        if (lane == 0) {
+                            const uint32_t lo = (uint32_t)v - (uint32_t)fc;
+                            const uint32_t hi = (uint32_t)(v >> 32) - (uint32_t)fm;
+                            __hip_atomic_store(np_, (unsigned long long)lo | ((unsigned long long)hi << 32),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store(&a.sfin[rsb + slot], T + ksec, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                            a.snode[rsb + slot] = nd;
+                            a.scm[rsb + slot] = (unsigned long long)(uint32_t)fc |
+                                                ((unsigned long long)(uint32_t)fm << 32);
+                            atomicAdd(&a.cl[r].nrun, 1u);  // atomics: never read back in here
+                            atomicMin(&a.cl[r].minf, T + ksec);
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __syncthreads();
+                    }
+                    if (ovf) {
+                        lflags |= MCS_FLAG_OVERFLOW;
+                        break;
+                    }
+                    if (lane == 0) trs[r].lock_id = 0u;  // currentContract reset (:83)
+                    __syncthreads();
+                    if (rc_ > 0u || rm_ > 0u) {  // "couldn't schedule enough resources" (:119-121)
+                        ++failed;
+                        continue;
+                    }
+                    winner = (int32_t)r;
+                    // AddVirtualNode on the requester (cluster.go:65-85)
+                    if (lane == 0) {
+                        const uint32_t nv = nvs[q];
+                        if (nv < a.V) {
+                            __hip_atomic_store(&a.vn[(size_t)q * a.V + nv],
+                                               (unsigned long long)kc | ((unsigned long long)km << 32),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            a.vcap[(size_t)q * a.V + nv] = make_uint2(kc, km);
+                            nvs[q] = nv + 1u;
+                            atomicAdd(&a.cl[q].nv, 1u);
+                        } else {
+                            atomicOr(&a.cl[q].flags, (uint32_t)MCS_FLAG_VNODE_OVERFLOW);
+                        }
+                    }
+                    __syncthreads();
+                }
+                if (lane == 0) {
+                    if (winner >= 0) ++n_won;
+                    if (n_trades < a.trade_cap) {
+                        mcs_contract_rec rec;
+                        rec.t_s = T;
+                        rec.requester = q;
+                        rec.winner = winner;
+                        rec.approvals = napp;
+                        rec.policy = pol;
+                        rec.cores = kc;
+                        rec.mem = km;
+                        rec.time_s = ksec;
+                        rec.failed = failed;
+                        rec.pad = 0u;
+                        a.trade_log[n_trades] = rec;
+                    } else {
+                        lflags |= MCS_FLAG_LOG_OVERFLOW;
+                    }
+                    tq.next_due = T + (winner >= 0 ? a.ok_sleep : a.fail_sleep) + (pol == 1u ? a.period : 0u);
+                    tq.lock_id = trs[q].lock_id;  // q's own lock may have been set as a responder
+                    tq.lock_until = trs[q].lock_until;
+                    tq.next_id = trs[q].next_id;
+                    trs[q] = tq;
+                }
+                ++n_trades;
+                __syncthreads();
+                if (lflags & MCS_FLAG_OVERFLOW) break;
+            }
+            if (lflags & MCS_FLAG_OVERFLOW) break;
+        }
+        if (lflags & MCS_FLAG_OVERFLOW) break;
+    }
+
+    // the next tick: T+1 while any cluster has a queued job, else the next arrival, sample tick
+    // or trader round (oracle/mcs_oracle_dtrade.c)
+    bool all_done = true, queued = false;
+    uint32_t nxt = T + a.sample_period - T % a.sample_period, fl = 0;
+    for (uint32_t q = lane; q < C; q += kWave) {
+        const DtCluster k = a.cl[q];
+        const uint32_t J = (uint32_t)(a.job_off[q + 1] - a.job_off[q]);
+        all_done = all_done && k.decided == J;
+        queued = queued || k.l1n > 0u || k.next_arr > k.l0_head;
+        if (k.next_arr < J) {
+            const uint32_t at = a.jobs[a.job_off[q] + k.next_arr].x;
+            nxt = at < nxt ? at : nxt;
+        }
+        if (a.period) nxt = trs[q].next_due < nxt ? trs[q].next_due : nxt;
+        fl |= k.flags;
+    }
+    const bool done_all = !__ballot(!all_done);
+    const bool queued_any = __ballot(queued) != 0ull;
+    nxt = wave_min_u32(nxt);
+    for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o);
+    __syncthreads();
+    for (uint32_t q = lane; q < C; q += kWave) a.tr[q] = trs[q];
+    if (lane == 0) {
+        DtCtl* ctl = a.ctl;
+        uint32_t flags = ctl->flags | fl | lflags;
+        uint32_t done = 0, Tn = T;
+        if (done_all || (flags & MCS_FLAG_OVERFLOW)) {
+            done = 1u;
+        } else if (T >= a.t_max) {
+            done = 1u;
+            flags |= MCS_FLAG_T_MAX;
+        } else {
+            Tn = (queued_any || nxt <= T + 1u) ? T + 1u : nxt;
+        }
+        ctl->T = Tn;
+        ctl->done = done;
+        ctl->ticks += 1u;
+        ctl->flags = flags;
+        ctl->n_trades = n_trades;
+        ctl->n_won = n_won;
+        ctl->n_foreign = n_for;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_dtrade_init(const DtArgs& a, hipStream_t s) {
+    if (a.C == 0) return hipSuccess;
+    hipLaunchKernelGGL(dt_init_kernel, dim3(a.C), dim3(kWave), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_dtrade_tick(const DtArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(dt_step_kernel, dim3(a.C), dim3(kWave), 0, s, a);
+    hipError_t st = hipGetLastError();
+    if (st != hipSuccess) return st;
+    hipLaunchKernelGGL(dt_sample_kernel, dim3(a.C), dim3(kWave), 0, s, a);
+    st = hipGetLastError();
+    if (st != hipSuccess) return st;
+    hipLaunchKernelGGL(dt_trader_kernel, dim3(1), dim3(kWave), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace mcs

@@ -1,0 +1,95 @@
+// mcs_dtrade_internal.h — device layout of the lock-step trading system with DELAY schedulers
+// (mcs_trade.h; oracle/mcs_oracle_dtrade.c).  One engine holds the whole system.
+//
+// HBM, per cluster c (C of them):
+//   tn     u64 {free_c | free_m << 32} per physical node (CSR node_off), live across ticks
+//   vn     u64 free vector of virtual node v at [c * V + v]; vcap uint2 its capacity
+//   sfin/snode/scm  running slots (finish, node, {c | m << 32}); Foreign jobs included
+//   l1     u32 Level1 list (local job indices), capacity = the cluster's job count (at job_off)
+//   jmap   i64 WaitTime.JobsMap per job (at job_off)
+//   cl     DtCluster queue cursors, counters, WaitTime sums, last sample
+//   tr     DtTrader trader state (two-stage RequestPolicyMonitor, responder lock)
+//   ctl    DtCtl the lock-step clock and log counters
+// Free counters are u32 halves read as Go uint64 values by sign extension: a Foreign job can take
+// more than a node has (cluster.go:116), and the wrapped uint64 is 2^64 - x for small x, which
+// the device keeps as the u32 2^32 - x (same comparisons against needs < 2^31; conversions to
+// float32/float64 go through the sign-extended uint64 like Go's).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mcs_trade.h"
+#include "mcs_internal.h"
+
+namespace mcs {
+
+constexpr uint32_t kDtMaxNodes = 1024;  // physical nodes per cluster
+constexpr uint32_t kDtMaxVnodes = 256;  // virtual nodes a cluster can receive
+constexpr uint32_t kDtMaxSlots = 4096;  // running slots per cluster (LDS staging, 16 KB)
+constexpr uint32_t kDtMaxClusters = 1024;
+
+struct DtCluster {
+    uint32_t next_arr;  // jobs [0, next_arr) have arrived
+    uint32_t l0_head;   // Level0 = [l0_head, next_arr)
+    uint32_t l1n;       // len(Level1)
+    uint32_t nv;        // virtual nodes received
+    uint32_t decided;
+    uint32_t moved;
+    uint32_t placed_l1;
+    uint32_t minf;      // earliest running finish (kEmpty = none)
+    uint32_t nrun;
+    uint32_t peak;
+    uint32_t flags;
+    uint32_t total_c;   // SetTotalResources at Run (cluster.go:26-40), physical nodes only
+    uint32_t total_m;
+    float cu, mu;       // last sample
+    uint32_t pad;
+    double avgw;        // last WaitTime.GetAverage()
+    long long total;    // WaitTime.TotalTime (ms)
+    long long count;    // WaitTime.JobsCount
+};
+
+struct DtTrader {
+    uint32_t lock_id, lock_until, next_id, next_due;
+    uint32_t stage;     // 0: WaitTime next (a fresh cs), 1: Utilization (stale cs)
+    float cs_cu, cs_mu;
+    uint32_t pad;
+    double cs_avgw;
+};
+
+struct DtCtl {
+    uint32_t T, done, ticks, flags;
+    unsigned long long n_trades, n_won, n_foreign;
+};
+
+struct DtArgs {
+    uint32_t C, V, S;
+    uint32_t period, ok_sleep, fail_sleep, lock_s, sample_period, max_wait, t_max;
+    unsigned long long trade_cap, foreign_cap;
+    const uint32_t* node_off;
+    const uint2* cap;
+    const uint2* free0;
+    unsigned long long* tn;
+    unsigned long long* vn;
+    uint2* vcap;
+    const uint4* jobs;
+    const uint64_t* job_off;
+    int32_t* out_node;
+    uint32_t* out_start;
+    uint32_t* out_finish;
+    uint32_t* sfin;
+    uint32_t* snode;
+    unsigned long long* scm;
+    uint32_t* l1;
+    long long* jmap;
+    DtCluster* cl;
+    DtTrader* tr;
+    DtCtl* ctl;
+    mcs_contract_rec* trade_log;
+    mcs_foreign_rec* foreign_log;
+};
+
+hipError_t launch_dtrade_init(const DtArgs& a, hipStream_t s);
+hipError_t launch_dtrade_tick(const DtArgs& a, hipStream_t s);  // phases A, C, D of one tick
+
+}  // namespace mcs

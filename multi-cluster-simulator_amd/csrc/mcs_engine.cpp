@@ -130,8 +130,9 @@ int mcs_engine_create(const mcs_config* cfg, int device, mcs_engine** out) {
     if (c.policy > MCS_POLICY_DELAY || c.borrow > 1 || c.trader > 1 || c.wait_sleep_s != 1 ||
         c.idle_sleep_s != 1)
         return MCS_E_INVALID; /* FIFO or DELAY with the reference sleeps */
-    if (c.policy == MCS_POLICY_DELAY && (c.borrow || c.trader))
-        return MCS_E_INVALID; /* Delay never borrows (scheduler.go:298-369); DELAY trading: mcs_trade.h */
+    if (c.policy == MCS_POLICY_DELAY && c.borrow)
+        return MCS_E_INVALID; /* Delay never borrows (scheduler.go:298-369) */
+    if (c.policy == MCS_POLICY_DELAY && c.max_wait_s == 0) return MCS_E_INVALID;
     if (c.borrow || c.trader) {
         if (c.trader && (c.trader_period_s == 0 || c.sample_period_s == 0 || c.lock_s == 0))
             return MCS_E_INVALID;
@@ -167,6 +168,7 @@ int mcs_engine_destroy(mcs_engine* e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     mcs::trade_free(e);
+    mcs::dtrade_free(e);
     mcs::comm_free(e);
     free_clusters(e);
     free_jobs(e);
@@ -207,6 +209,7 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
     free_clusters(e);
     free_jobs(e);
     mcs::trade_free(e);
+    mcs::dtrade_free(e);
     e->has_clusters = e->has_jobs = e->has_run = false;
     e->C = n_clusters;
     e->max_n = max_n;
@@ -258,6 +261,7 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
 static int alloc_jobs(mcs_engine* e, const uint64_t* job_offsets) {
     free_jobs(e);
     mcs::trade_free(e);
+    mcs::dtrade_free(e);
     e->has_jobs = e->has_run = false;
     e->job_off.assign(job_offsets, job_offsets + e->C + 1);
     e->total_jobs = job_offsets[e->C];
@@ -381,8 +385,10 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     if (int st = check_engine(e)) return st;
     if (!e->has_clusters || !e->has_jobs) return fail(e, MCS_E_STATE, "load clusters and jobs first");
     if (t_end_s != MCS_TIME_NONE) return fail(e, MCS_E_INVALID, "finite horizons are reserved");
+    if (e->cfg.policy == MCS_POLICY_DELAY && e->cfg.trader) return mcs::dtrade_run(e, stats);
     if (e->cfg.borrow || e->cfg.trader) return mcs::trade_run(e, stats);
     e->trade_run = false;
+    e->dtrade_run = false;
     const bool delay = e->cfg.policy == MCS_POLICY_DELAY;
     e->delay_run = delay;
     if (delay && !e->d_l1_cm) { /* Level1 can hold every job of its cluster: never overflows */
@@ -494,6 +500,7 @@ int mcs_read_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n_clu
     if (!e->has_run) return fail(e, MCS_E_STATE, "mcs_run first");
     if (!out || n_clusters > e->C) return fail(e, MCS_E_INVALID, "bad output");
     if (e->trade_run) return mcs::trade_cluster_stats(e, out, n_clusters);
+    if (e->dtrade_run) return mcs::dtrade_cluster_stats(e, out, n_clusters);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipMemcpy(out, e->d_cstats, n_clusters * sizeof(mcs_cluster_stats),
                         hipMemcpyDeviceToHost));
@@ -504,6 +511,7 @@ int mcs_read_delay_stats(mcs_engine* e, mcs_delay_cluster_stats* out, uint32_t n
     if (int st = check_engine(e)) return st;
     if (!e->has_run || !e->delay_run) return fail(e, MCS_E_STATE, "no DELAY run");
     if (!out || n_clusters > e->C) return fail(e, MCS_E_INVALID, "bad output");
+    if (e->dtrade_run) return mcs::dtrade_delay_stats(e, out, n_clusters);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipMemcpy(out, e->d_dstats, n_clusters * sizeof(mcs_delay_cluster_stats),
                         hipMemcpyDeviceToHost));

@@ -15,6 +15,14 @@ void trade_free(mcs_engine* e);
 void comm_free(mcs_engine* e);
 int trade_run(mcs_engine* e, mcs_stats* stats);
 int trade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n_clusters);
+struct DtradeDev;  // mcs_dtrade.cpp: lock-step trading with DELAY schedulers
+void dtrade_free(mcs_engine* e);
+int dtrade_run(mcs_engine* e, mcs_stats* stats);
+int dtrade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n);
+int dtrade_delay_stats(mcs_engine* e, mcs_delay_cluster_stats* out, uint32_t n);
+int dtrade_trade_stats(mcs_engine* e, mcs_trade_stats* out);
+int dtrade_read_trades(mcs_engine* e, mcs_trade_rec* out, uint64_t cap, uint64_t* n);
+int dtrade_read_vnode_counts(mcs_engine* e, uint32_t* out, uint32_t n);
 }  // namespace mcs
 
 struct mcs_engine {
@@ -58,6 +66,9 @@ struct mcs_engine {
     mcs::TradeDev* td = nullptr;
     bool trade_run = false;  // results of the last run come from the lock-step path
     uint32_t tr_lq = 0, tr_slots = 0;  // capacity escalation of the lock-step path (0 = auto)
+    mcs::DtradeDev* dtd = nullptr;     // DELAY trading state (mcs_dtrade.cpp)
+    bool dtrade_run = false;           // results of the last run come from DELAY trading
+    uint32_t dt_vnodes = 0;            // virtual-node capacity per cluster (0 = auto)
 };
 
 inline int fail(mcs_engine* e, int code, const std::string& msg) {

@@ -455,6 +455,7 @@ int mcs_trade_end(mcs_engine* e, mcs_stats* stats) {
     e->has_run = true;
     e->trade_run = true;
     e->delay_run = false;
+    e->dtrade_run = false;
     mcs_trade_stats ts{};
     mcs_stats st{};
     if (int s = mcs::fill_stats(e, &ts, &st)) return s;
@@ -473,6 +474,7 @@ int mcs_trade_end(mcs_engine* e, mcs_stats* stats) {
 int mcs_read_trade_stats(mcs_engine* e, mcs_trade_stats* out) {
     if (int st = check_engine(e)) return st;
     if (!out) return fail(e, MCS_E_INVALID, "null output");
+    if (e->dtrade_run && e->dtd) return mcs::dtrade_trade_stats(e, out);
     if (!e->trade_run || !e->td) return fail(e, MCS_E_STATE, "no lock-step run");
     mcs_stats st{};
     if (int s = mcs::fill_stats(e, out, &st)) return s;
@@ -486,6 +488,10 @@ int mcs_read_trade_stats(mcs_engine* e, mcs_trade_stats* out) {
 int mcs_read_lent(mcs_engine* e, mcs_lent_rec* out, uint64_t cap, uint64_t* n) {
     if (int st = check_engine(e)) return st;
     if (!n || (cap && !out)) return fail(e, MCS_E_INVALID, "bad output");
+    if (e->dtrade_run && e->dtd) {  // Delay never borrows: no lent runs
+        *n = 0;
+        return MCS_OK;
+    }
     if (!e->trade_run || !e->td) return fail(e, MCS_E_STATE, "no lock-step run");
     mcs::TradeDev* td = e->td;
     HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -509,6 +515,7 @@ int mcs_read_lent(mcs_engine* e, mcs_lent_rec* out, uint64_t cap, uint64_t* n) {
 int mcs_read_trades(mcs_engine* e, mcs_trade_rec* out, uint64_t cap, uint64_t* n) {
     if (int st = check_engine(e)) return st;
     if (!n || (cap && !out)) return fail(e, MCS_E_INVALID, "bad output");
+    if (e->dtrade_run && e->dtd) return mcs::dtrade_read_trades(e, out, cap, n);
     if (!e->trade_run || !e->td) return fail(e, MCS_E_STATE, "no lock-step run");
     mcs::TradeDev* td = e->td;
     HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -522,6 +529,10 @@ int mcs_read_trades(mcs_engine* e, mcs_trade_rec* out, uint64_t cap, uint64_t* n
 
 int mcs_read_virtual_nodes(mcs_engine* e, uint32_t* out, uint32_t n_total) {
     if (int st = check_engine(e)) return st;
+    if (e->dtrade_run && e->dtd) {
+        if (!out || n_total > e->C) return fail(e, MCS_E_INVALID, "bad output");
+        return mcs::dtrade_read_vnode_counts(e, out, n_total);
+    }
     if (!e->trade_run || !e->td) return fail(e, MCS_E_STATE, "no lock-step run");
     const uint32_t Ct = e->C * e->world;
     if (!out || n_total > Ct) return fail(e, MCS_E_INVALID, "bad output");

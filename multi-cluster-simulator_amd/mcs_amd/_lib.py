@@ -31,6 +31,7 @@ MCS_FLAG_CLOCK_OVERFLOW = 0x4
 MCS_FLAG_LENT_OVERFLOW = 0x8
 MCS_FLAG_LOG_OVERFLOW = 0x10
 MCS_FLAG_T_MAX = 0x20
+MCS_FLAG_VNODE_OVERFLOW = 0x40
 
 MCS_POLICY_FIFO = 0
 MCS_POLICY_DELAY = 1
@@ -135,6 +136,16 @@ class mcs_trade_rec(C.Structure):
     _fields_ = [("t_s", C.c_uint32), ("requester", C.c_uint32), ("winner", C.c_int32), ("approvals", C.c_uint32)]
 
 
+class mcs_contract_rec(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("t_s", "requester")] + [("winner", C.c_int32)] + \
+               [(n, C.c_uint32) for n in ("approvals", "policy", "cores", "mem", "time_s", "failed", "pad")]
+
+
+class mcs_foreign_rec(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("requester", "responder", "node", "start_s", "finish_s", "pad")] + \
+               [("c", C.c_uint64), ("m", C.c_uint64)]
+
+
 class mcs_trade_stats(C.Structure):
     _fields_ = [
         ("placed", C.c_uint64),
@@ -202,6 +213,9 @@ SIGNATURES = [
     ("mcs_read_lent", C.c_int, [vp, C.POINTER(mcs_lent_rec), C.c_uint64, u64p]),
     ("mcs_read_trades", C.c_int, [vp, C.POINTER(mcs_trade_rec), C.c_uint64, u64p]),
     ("mcs_read_virtual_nodes", C.c_int, [vp, u32p, C.c_uint32]),
+    ("mcs_read_contracts", C.c_int, [vp, C.POINTER(mcs_contract_rec), C.c_uint64, u64p]),
+    ("mcs_read_foreign", C.c_int, [vp, C.POINTER(mcs_foreign_rec), C.c_uint64, u64p]),
+    ("mcs_read_virtual_node_caps", C.c_int, [vp, C.c_uint32, u32p, u32p, C.c_uint32, u32p]),
 ]
 
 _lib = None

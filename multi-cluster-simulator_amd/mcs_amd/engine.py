@@ -123,6 +123,12 @@ CLUSTER_STATS_DTYPE = np.dtype([("t_end", "<u4"), ("placed", "<u4"), ("waited", 
 DELAY_STATS_DTYPE = np.dtype([("total_wait_ms", "<i8"), ("jobs_count", "<i8"), ("moved_l1", "<u4"),
                               ("placed_l1", "<u4"), ("peak_l1", "<u4"), ("l1_left", "<u4")])
 
+CONTRACT_DTYPE = np.dtype([("t", "<u4"), ("requester", "<u4"), ("winner", "<i4"), ("approvals", "<u4"),
+                           ("policy", "<u4"), ("cores", "<u4"), ("mem", "<u4"), ("time_s", "<u4"), ("failed", "<u4"),
+                           ("pad", "<u4")])
+FOREIGN_DTYPE = np.dtype([("requester", "<u4"), ("responder", "<u4"), ("node", "<u4"), ("start", "<u4"),
+                          ("finish", "<u4"), ("pad", "<u4"), ("c", "<u8"), ("m", "<u8")])
+
 LENT_DTYPE = np.dtype([("lender", "<u4"), ("borrower", "<u4"), ("job", "<u8"), ("node", "<u4"),
                        ("start", "<u4"), ("finish", "<u4"), ("pad", "<u4")])
 TRADE_DTYPE = np.dtype([("t", "<u4"), ("requester", "<u4"), ("winner", "<i4"), ("approvals", "<u4")])
@@ -287,6 +293,36 @@ class Engine:
             self._c(L.lib().mcs_read_trades(self._h, out.ctypes.data_as(C.POINTER(L.mcs_trade_rec)), n.value,
                                             C.byref(n)))
         return out
+
+    def contracts(self) -> np.ndarray:
+        """Trader rounds with their contracts (DELAY trading, CONTRACT_DTYPE)."""
+        n = C.c_uint64()
+        self._c(L.lib().mcs_read_contracts(self._h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, CONTRACT_DTYPE)
+        if n.value:
+            self._c(L.lib().mcs_read_contracts(self._h, out.ctypes.data_as(C.POINTER(L.mcs_contract_rec)), n.value,
+                                               C.byref(n)))
+        return out
+
+    def foreign(self) -> np.ndarray:
+        """Foreign jobs launched by AllocateVirtualNodeResources (DELAY trading, FOREIGN_DTYPE)."""
+        n = C.c_uint64()
+        self._c(L.lib().mcs_read_foreign(self._h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, FOREIGN_DTYPE)
+        if n.value:
+            self._c(L.lib().mcs_read_foreign(self._h, out.ctypes.data_as(C.POINTER(L.mcs_foreign_rec)), n.value,
+                                             C.byref(n)))
+        return out
+
+    def virtual_node_caps(self, cluster: int):
+        """[(cores, memory)] of the virtual nodes `cluster` received (DELAY trading)."""
+        n = C.c_uint32()
+        self._c(L.lib().mcs_read_virtual_node_caps(self._h, cluster, None, None, 0, C.byref(n)))
+        c = np.zeros(max(n.value, 1), np.uint32)
+        m = np.zeros(max(n.value, 1), np.uint32)
+        self._c(L.lib().mcs_read_virtual_node_caps(self._h, cluster, L.ptr(c, C.c_uint32), L.ptr(m, C.c_uint32),
+                                                   n.value, C.byref(n)))
+        return [(int(c[i]), int(m[i])) for i in range(n.value)]
 
     def virtual_nodes(self, n_total: Optional[int] = None) -> np.ndarray:
         n_total = n_total if n_total is not None else self.num_clusters * getattr(self, "world", 1)

@@ -16,7 +16,8 @@ PY
 cp "$PKG"/csrc/*.h "$PKG/build/v_$NAME/"
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wall -Wno-unused-result -I$ROOT/include -mllvm -amdgpu-atomic-optimizer-strategy=None"
 /opt/rocm/bin/hipcc $FLAGS -I"$PKG/csrc" -c -o "$PKG/build/v_$NAME/k.o" "$PKG/build/v_$NAME/mcs_kernels.hip"
+OTHERS=$(ls "$PKG"/build/*.o | grep -v '/mcs_kernels.o$')
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$ROOT/variants/libmcs_$NAME.so" "$PKG/build/v_$NAME/k.o" \
-    "$PKG/build/mcs_engine.o" "$PKG/build/mcs_trade_k.o" "$PKG/build/mcs_trade.o" -L/opt/rocm/lib -lrccl \
+    $OTHERS -L/opt/rocm/lib -lrccl \
     -Wl,-rpath,/opt/rocm/lib
 echo "variants/libmcs_$NAME.so"
