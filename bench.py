@@ -53,7 +53,16 @@ def parse():
     if a.traffic_json is None:
         a.traffic_json = os.path.join(REPO, "profiles", "traffic_latest_delay.json" if a.policy == "delay"
                                       else "traffic_latest.json")
-    if a.config == "c5":  # BASELINE.json configs[4]: 64 trading clusters, 10M jobs
+    if a.config == "c5" and a.policy == "delay":
+        # DELAY schedulers trading real contracts: cluster_small replicas at the
+        # reference client's rate, where Level1 fills and the WaitTime policy breaks
+        if a.clusters == 4096:
+            a.clusters = 64
+        if a.jobs_per_cluster == 16384:
+            a.jobs_per_cluster = 2000
+        if a.cpu_sample_clusters == 512:
+            a.cpu_sample_clusters = 16
+    elif a.config == "c5":  # BASELINE.json configs[4]: 64 trading clusters, 10M jobs
         if a.clusters == 4096:
             a.clusters = 64
         if a.jobs_per_cluster == 16384:
@@ -88,6 +97,112 @@ def cpu_baseline_c5(args, lam, sample_jobs):
                   f"{dt:.2f} s wall",
         "seconds": dt,
     }
+
+
+def main_c5_delay(args, world, rank, local_rank):
+    """C5 with DELAY schedulers: args.clusters cluster_small replicas with the
+    reference client's arrivals, Delay loops + traders with real contracts in lock-step on ONE engine
+    (the whole system on one GPU; with N ranks every rank runs its own independent system)."""
+    import torch
+    import torch.distributed as dist
+
+    from mcs_amd import Cluster, Engine, GenParams, replicate
+    from mcs_amd.shard import aggregate, rank_seed
+
+    dist_on = world > 1
+    if dist_on:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend="nccl")
+    dev = torch.device("cuda", local_rank)
+    spec = Cluster.load(os.path.join(REPO, "assets", "cluster_small.json"))
+    eng = Engine(local_rank, policy="DELAY", trader=True)
+    eng.load_clusters(replicate(spec, args.clusters))
+    eng.generate_jobs(GenParams(seed=rank_seed(args.seed, rank)), args.jobs_per_cluster)
+    n_jobs = eng.num_jobs
+
+    def barrier():
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        eng.run()
+    barrier()
+    t0 = time.perf_counter()
+    kernel_ms, decided = [], 0
+    for _ in range(args.steps):
+        st = eng.run()
+        kernel_ms.append(st.kernel_ms)
+        decided += st.placed
+    barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed_max, decided_all = aggregate(elapsed, decided, device=dev)
+    ts = eng.trade_stats()
+    tr = eng.contracts()
+    if rank == 0:
+        avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+        achieved = decided / args.steps * BYTES_PER_PLACEMENT / avg_kernel_s / 1e9
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            import oracle_ref as O
+            from mcs_amd.engine import gen_streams_host
+
+            k = min(args.cpu_sample_clusters, args.clusters)
+            jk = min(args.jobs_per_cluster, 1000)
+            arrays = replicate(spec, k)
+            streams = gen_streams_host(GenParams(seed=rank_seed(args.seed, 0)), arrays, jk)
+            O.lib()
+            c0 = time.perf_counter()
+            r = O.dtrade_run(arrays, streams, trade_cap=1, foreign_cap=1)
+            dt = time.perf_counter() - c0
+            cpu = {"value": float((r["node"] >= 0).sum()) / dt, "unit": "job placements/s", "cores": 1,
+                   "kind": "port",
+                   "sample": f"{k} cluster_small x {jk} jobs ({streams.n_jobs} jobs, {r['n_trades']} trader rounds, "
+                             f"{r['t_final']} ticks), oracle/mcs_oracle_dtrade.c -O3, 1 thread, {dt:.2f} s wall",
+                   "seconds": dt}
+        out = {
+            "metric": "trading-system job placements/sec with DELAY schedulers (real contracts)",
+            "value": decided_all / elapsed_max,
+            "unit": "placements/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded device generator restating pkg/client/client.go, Poisson(10)/min arrivals)",
+            "config": {
+                "workload": f"C5-DELAY: {args.clusters} cluster_small clusters, Delay + traders in lock-step, "
+                            f"{args.jobs_per_cluster} jobs/cluster ({n_jobs} jobs), reference client arrivals",
+                "clusters_total": args.clusters,
+                "nodes": 5,
+                "jobs_per_cluster": args.jobs_per_cluster,
+                "parallelism": f"{world} independent system(s), one per GPU",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel": "lock-step tick (dt_step/dt_sample/dt_trader), launch/latency-bound",
+                "kernel_ms_avg": avg_kernel_s * 1e3,
+                "bytes_per_placement": BYTES_PER_PLACEMENT,
+            },
+            "cpu_baseline": cpu,
+            "trading": {"ticks": ts["ticks"], "t_final": ts["t_final"],
+                        "us_per_tick": avg_kernel_s * 1e6 / max(ts["ticks"], 1), "trades": ts["trades"],
+                        "trades_won": ts["trades_won"], "wait_time_rounds": int((tr["policy"] == 0).sum()),
+                        "foreign_jobs": int(len(eng.foreign())), "flags": ts["flags"]},
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist_on:
+        dist.destroy_process_group()
 
 
 def main_c5(args, world, rank, local_rank):
@@ -231,6 +346,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     if args.config == "c5":
+        if args.policy == "delay":
+            return main_c5_delay(args, world, rank, local_rank)
         return main_c5(args, world, rank, local_rank)
 
     import torch

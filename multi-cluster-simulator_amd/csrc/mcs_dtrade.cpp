@@ -24,8 +24,9 @@ struct DtradeDev {
     uint32_t* sfin = nullptr;
     uint32_t* snode = nullptr;
     unsigned long long* scm = nullptr;
-    uint32_t* l1 = nullptr;
-    long long* jmap = nullptr;
+    unsigned long long* l1cm = nullptr;
+    unsigned long long* l1jd = nullptr;
+    unsigned long long* l1al = nullptr;
     DtCluster* cl = nullptr;
     DtTrader* tr = nullptr;
     DtCtl* ctl = nullptr;
@@ -56,7 +57,7 @@ int dtrade_alloc(mcs_engine* e) {
     if (e->max_n > kDtMaxNodes) return fail(e, MCS_E_INVALID, "more than 1024 nodes in a cluster");
     const uint32_t S = e->cfg.slot_pool ? 64u * e->cfg.slot_pool : (e->tr_slots ? e->tr_slots : dt_auto_slots(e->max_n));
     if (S > kDtMaxSlots) return fail(e, MCS_E_INVALID, "slot pool above 4096");
-    const uint32_t V = e->dt_vnodes ? e->dt_vnodes : 16u;
+    const uint32_t V = e->dt_vnodes ? e->dt_vnodes : 64u;
     DtradeDev* d = new (std::nothrow) DtradeDev();
     if (!d) return fail(e, MCS_E_NOMEM, "DELAY trading state");
     e->dtd = d;
@@ -68,8 +69,9 @@ int dtrade_alloc(mcs_engine* e) {
     HIPCHK(e, hipMalloc(&d->sfin, (size_t)C * S * 4));
     HIPCHK(e, hipMalloc(&d->snode, (size_t)C * S * 4));
     HIPCHK(e, hipMalloc(&d->scm, (size_t)C * S * 8));
-    HIPCHK(e, hipMalloc(&d->l1, nj * 4));
-    HIPCHK(e, hipMalloc(&d->jmap, nj * 8));
+    HIPCHK(e, hipMalloc(&d->l1cm, nj * 8));
+    HIPCHK(e, hipMalloc(&d->l1jd, nj * 8));
+    HIPCHK(e, hipMalloc(&d->l1al, nj * 8));
     HIPCHK(e, hipMalloc(&d->cl, C * sizeof(DtCluster)));
     HIPCHK(e, hipMalloc(&d->tr, C * sizeof(DtTrader)));
     HIPCHK(e, hipMalloc(&d->ctl, sizeof(DtCtl)));
@@ -103,8 +105,9 @@ int dtrade_alloc(mcs_engine* e) {
     a.sfin = d->sfin;
     a.snode = d->snode;
     a.scm = d->scm;
-    a.l1 = d->l1;
-    a.jmap = d->jmap;
+    a.l1cm = d->l1cm;
+    a.l1jd = d->l1jd;
+    a.l1al = d->l1al;
     a.cl = d->cl;
     a.tr = d->tr;
     a.ctl = d->ctl;
@@ -174,8 +177,9 @@ void dtrade_free(mcs_engine* e) {
     dfree(d->sfin);
     dfree(d->snode);
     dfree(d->scm);
-    dfree(d->l1);
-    dfree(d->jmap);
+    dfree(d->l1cm);
+    dfree(d->l1jd);
+    dfree(d->l1al);
     dfree(d->cl);
     dfree(d->tr);
     dfree(d->ctl);

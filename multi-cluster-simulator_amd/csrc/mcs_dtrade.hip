@@ -90,11 +90,11 @@ __global__ __launch_bounds__(64) void dt_init_kernel(DtArgs a) {
         a.out_node[j] = MCS_NODE_UNPLACED;
         a.out_start[j] = MCS_TIME_NONE;
         a.out_finish[j] = MCS_TIME_NONE;
-        a.jmap[j] = 0;
     }
     if (lane == 0) {
         DtCluster z{};
         z.minf = kEmpty;
+        z.head_last = kEmpty;
         z.total_c = sc;
         z.total_m = sm;
         a.cl[c] = z;
@@ -121,8 +121,9 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
     const uint64_t j0 = a.job_off[c];
     const uint32_t J = (uint32_t)(a.job_off[c + 1] - j0);
     const uint4* __restrict__ jobs = a.jobs + j0;
-    uint32_t* __restrict__ l1 = a.l1 + j0;
-    long long* __restrict__ jmap = a.jmap + j0;
+    unsigned long long* __restrict__ l1cm = a.l1cm + j0;
+    unsigned long long* __restrict__ l1jd = a.l1jd + j0;
+    unsigned long long* __restrict__ l1al = a.l1al + j0;
     const size_t sb = (size_t)c * a.S;
     const uint32_t S = a.S;
     DtCluster st = a.cl[c];
@@ -150,7 +151,9 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
                 lm = f < lm ? f : lm;
             }
         }
-        st.nrun -= dt_wave_sum_u32(nrel);
+        const uint32_t nr = dt_wave_sum_u32(nrel);
+        st.nrun -= nr;
+        st.l1_dirty |= nr != 0u ? 1u : 0u;
         st.minf = wave_min_u32(lm);
         __syncthreads();
     }
@@ -209,59 +212,121 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
     };
 
     // ---- Level1 pass (scheduler.go:302-329) ----
-    if (st.l1n != 0u) {
-        // exact fit filter (see mcs_delay.hip): lane l holds the max free memory over nodes with
-        // min(free cores, 63) >= l; conservative for wrapped counters (huge u32 values)
-        hist[lane] = 0u;
-        __syncthreads();
-        uint32_t mc = 0u;
-        for (uint32_t i = lane; i < NN; i += kWave) {
-            const unsigned long long v = nodes[i];
-            const uint32_t fc = (uint32_t)v;
-            atomicMax(&hist[fc < 63u ? fc : 63u], (uint32_t)(v >> 32));
-            mc = fc > mc ? fc : mc;
+    if (st.l1n != 0u && !st.l1_dirty) {
+        // nothing raised a free counter since the last pass and it placed nothing: every entry
+        // fails again; each JobsMap entry becomes 1000 * (T - arrival)
+        st.total += 1000ll * (long long)((unsigned long long)st.l1n * T - st.s_last);
+        st.s_last = (unsigned long long)st.l1n * T;
+        st.t_all = T;
+    } else if (st.l1n != 0u) {
+        const bool exact = NN <= (uint32_t)kWave;  // small clusters: per-lane exact first fit
+        // bigger clusters: exact fit filter (see mcs_delay.hip): lane l holds the max free memory
+        // over nodes with min(free cores, 63) >= l; conservative for wrapped counters
+        uint32_t best = 0u, max_c = 0u;
+        if (!exact) {
+            hist[lane] = 0u;
+            __syncthreads();
+            uint32_t mc = 0u;
+            for (uint32_t i = lane; i < NN; i += kWave) {
+                const unsigned long long v = nodes[i];
+                const uint32_t fc = (uint32_t)v;
+                atomicMax(&hist[fc < 63u ? fc : 63u], (uint32_t)(v >> 32));
+                mc = fc > mc ? fc : mc;
+            }
+            __syncthreads();
+            max_c = dt_wave_max_u32(mc);
+            best = hist[lane];
+            for (int o = 1; o < kWave; o <<= 1) {
+                const uint32_t w = (uint32_t)__shfl_down((int)best, o);
+                best = (lane + (uint32_t)o < (uint32_t)kWave && w > best) ? w : best;
+            }
         }
-        __syncthreads();
-        const uint32_t max_c = dt_wave_max_u32(mc);
-        uint32_t best = hist[lane];
-        for (int o = 1; o < kWave; o <<= 1) {
-            const uint32_t w = (uint32_t)__shfl_down((int)best, o);
-            best = (lane + (uint32_t)o < (uint32_t)kWave && w > best) ? w : best;
-        }
+        // per lane: the lowest node (physical, then virtual) that fits this lane's entry
+        auto lane_fit = [&](uint32_t c_l, uint32_t m_l) -> uint32_t {
+            uint32_t kl = kEmpty;
+            for (uint32_t i = NN; i-- > 0u;) {
+                const unsigned long long v = nodes[i];
+                kl = ((uint32_t)v >= c_l && (uint32_t)(v >> 32) >= m_l) ? i : kl;
+            }
+            return kl;
+        };
         uint32_t wr = 0;
         bool carry_skip = false;  // the last entry of the previous row was placed
-        const uint32_t n1 = st.l1n;
+        const uint32_t n1 = st.l1n, t_all = st.t_all;
+        unsigned long long s_new = 0ull;
+        // rows of 64 entries, each row's three coalesced loads issued one row ahead
+        unsigned long long ncm = 0, njd = 0, nal = 0;
+        if (lane < n1) {
+            ncm = l1cm[lane];
+            njd = l1jd[lane];
+            nal = l1al[lane];
+        }
         for (uint32_t base = 0; base < n1; base += kWave) {
             const uint32_t pos = base + lane;
             const bool live = pos < n1;
-            const uint32_t j = live ? l1[pos] : 0u;
-            const uint4 jb = live ? jobs[j] : make_uint4(0u, 0u, 0u, 0u);
-            const uint32_t bm = (uint32_t)__shfl((int)best, (int)(jb.z < 63u ? jb.z : 63u));
-            unsigned long long cand = __ballot(live && jb.z <= max_c && bm >= jb.w);
+            const unsigned long long cm = ncm, jdv = njd, al = nal;
+            if (pos + kWave < n1) {
+                ncm = l1cm[pos + kWave];
+                njd = l1jd[pos + kWave];
+                nal = l1al[pos + kWave];
+            }
+            const uint32_t jc_l = (uint32_t)cm, jm_l = (uint32_t)(cm >> 32);
             unsigned long long placedm = 0ull, skipm = carry_skip ? 1ull : 0ull;
             bool overflow = false;
-            while (cand) {
-                const uint32_t b = (uint32_t)__builtin_ctzll(cand);
-                cand &= cand - 1ull;
-                if ((skipm >> b) & 1ull) continue;  // slid into slot i: not examined (D6)
-                const uint32_t jc = readlane(jb.z, b), jm = readlane(jb.w, b);
-                const uint32_t k = first_fit(jc, jm);
-                if (k == kEmpty) continue;
-                const uint32_t jd = readlane(jb.y, b), jj = readlane(j, b);
-                const uint32_t fin = T + jd;
-                if (jd != 0u && !commit(k, jc, jm, fin)) {
-                    overflow = true;
-                    break;
+            if (exact) {
+                uint32_t from = 0;
+                for (;;) {  // the next entry in list order that fits now and is not skipped
+                    __syncthreads();
+                    const uint32_t kl = live ? lane_fit(jc_l, jm_l) : kEmpty;
+                    const unsigned long long fitm = __ballot(kl != kEmpty) & ~skipm &
+                                                    (from < 64u ? (~0ull << from) : 0ull);
+                    if (!fitm) break;
+                    const uint32_t b = (uint32_t)__builtin_ctzll(fitm);
+                    const uint32_t k = readlane(kl, b);
+                    const uint32_t jc = readlane(jc_l, b), jm = readlane(jm_l, b);
+                    const uint32_t jd = readlane((uint32_t)(jdv >> 32), b), jj = readlane((uint32_t)jdv, b);
+                    const uint32_t fin = T + jd;
+                    if (jd != 0u && !commit(k, jc, jm, fin)) {
+                        overflow = true;
+                        break;
+                    }
+                    if (lane == 0) {
+                        a.out_node[j0 + jj] = (int32_t)k;
+                        a.out_start[j0 + jj] = T;
+                        a.out_finish[j0 + jj] = fin;
+                    }
+                    placedm |= 1ull << b;
+                    if (b < 63u) skipm |= 1ull << (b + 1u);
+                    from = b + 2u;
+                    ++st.decided;
+                    ++st.placed_l1;
                 }
-                if (lane == 0) {
-                    a.out_node[j0 + jj] = (int32_t)k;
-                    a.out_start[j0 + jj] = T;
-                    a.out_finish[j0 + jj] = fin;
+            } else {
+                const uint32_t bm = (uint32_t)__shfl((int)best, (int)(jc_l < 63u ? jc_l : 63u));
+                unsigned long long cand = __ballot(live && jc_l <= max_c && bm >= jm_l);
+                while (cand) {
+                    const uint32_t b = (uint32_t)__builtin_ctzll(cand);
+                    cand &= cand - 1ull;
+                    if ((skipm >> b) & 1ull) continue;  // slid into slot i: not examined (D6)
+                    const uint32_t jc = readlane(jc_l, b), jm = readlane(jm_l, b);
+                    const uint32_t k = first_fit(jc, jm);
+                    if (k == kEmpty) continue;
+                    const uint32_t jd = readlane((uint32_t)(jdv >> 32), b), jj = readlane((uint32_t)jdv, b);
+                    const uint32_t fin = T + jd;
+                    if (jd != 0u && !commit(k, jc, jm, fin)) {
+                        overflow = true;
+                        break;
+                    }
+                    if (lane == 0) {
+                        a.out_node[j0 + jj] = (int32_t)k;
+                        a.out_start[j0 + jj] = T;
+                        a.out_finish[j0 + jj] = fin;
+                    }
+                    placedm |= 1ull << b;
+                    if (b < 63u) skipm |= 1ull << (b + 1u);
+                    ++st.decided;
+                    ++st.placed_l1;
                 }
-                placedm |= 1ull << b;
-                if (b < 63u) skipm |= 1ull << (b + 1u);
-                ++st.decided;
-                ++st.placed_l1;
             }
             if (overflow) {
                 st.flags |= MCS_FLAG_OVERFLOW;
@@ -271,27 +336,33 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             const unsigned long long livem = __ballot(live);
             const uint32_t last = 63u - (uint32_t)__builtin_clzll(livem);
             carry_skip = ((placedm >> last) & 1ull) != 0ull && last == 63u;
-            // WaitTime update of every examined job (the skipped one is not examined)
-            long long delta = 0;
+            // WaitTime update of every examined job (the skipped one is not examined): its
+            // JobsMap entry goes from 1000 * (last - arrival) to 1000 * (T - arrival)
             const bool examined = live && !((skipm >> lane) & 1ull);
             const bool placed = ((placedm >> lane) & 1ull) != 0ull;
-            if (examined) {
-                const long long nv = (long long)(T - jb.x) * 1000ll;
-                delta = nv - jmap[j];
-                jmap[j] = placed ? 0ll : nv;  // delete(JobsMap, id) on success (:316)
-            }
+            const uint32_t sl = (uint32_t)(al >> 32);
+            const uint32_t eff = sl > t_all ? sl : t_all;
+            const long long delta = examined ? (long long)(T - eff) * 1000ll : 0ll;
             st.total += dt_wave_sum_i64(delta);
             // compaction in the same sweep (append(Level1[:i], Level1[i+1:]...), :319)
             const unsigned long long kept = livem & ~placedm;
+            const uint32_t nl = examined ? T : eff;  // the kept entry's last examination
             if (live && !placed) {
                 const uint32_t np = wr + (uint32_t)__builtin_amdgcn_mbcnt_hi(
                                              (uint32_t)(kept >> 32),
                                              __builtin_amdgcn_mbcnt_lo((uint32_t)kept, 0u));
-                if (np != pos) l1[np] = j;
+                if (np != pos) {
+                    l1cm[np] = cm;
+                    l1jd[np] = jdv;
+                }
+                if (np != pos || nl != sl) l1al[np] = (al & 0xFFFFFFFFull) | ((unsigned long long)nl << 32);
             }
+            s_new += (unsigned long long)dt_wave_sum_i64(live && !placed ? (long long)nl : 0ll);
             wr += (uint32_t)__builtin_popcountll(kept);
         }
         st.l1n = wr;
+        st.s_last = s_new;
+        st.l1_dirty = wr != n1 ? 1u : 0u;  // a pass that placed: its skipped entries come next
     }
 
     // ---- Level0 head (scheduler.go:332-366) ----
@@ -299,9 +370,10 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         const uint32_t j = st.l0_head;
         const uint4 jb = jobs[j];
         const uint32_t k = first_fit(jb.z, jb.w);
-        const long long nv = (long long)(T - jb.x) * 1000ll;
-        const long long old = jmap[j];
-        st.total += nv - old;
+        // JobsMap: 0 until the head is first examined, then 1000 * (last - arrival)
+        const long long old = st.head_last == kEmpty ? 0ll : (long long)(st.head_last - jb.x) * 1000ll;
+        st.total += (long long)(T - jb.x) * 1000ll - old;
+        st.head_last = T;
         if (k != kEmpty) {
             const uint32_t fin = T + jb.y;
             if (jb.y != 0u && !commit(k, jb.z, jb.w, fin)) {
@@ -311,19 +383,22 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
                     a.out_node[j0 + j] = (int32_t)k;
                     a.out_start[j0 + j] = T;
                     a.out_finish[j0 + j] = fin;
-                    jmap[j] = 0;
                 }
                 ++st.l0_head;
                 ++st.decided;
+                st.head_last = kEmpty;
             }
-        } else {
-            if (lane == 0) jmap[j] = nv;
-            if (T - jb.x >= a.max_wait) {  // MaxWaitTime (:353): Level1 append (:357)
-                if (lane == 0) l1[st.l1n] = j;
-                ++st.l1n;
-                ++st.l0_head;
-                ++st.moved;
+        } else if (T - jb.x >= a.max_wait) {  // MaxWaitTime (:353): Level1 append (:357)
+            if (lane == 0) {
+                l1cm[st.l1n] = (unsigned long long)jb.z | ((unsigned long long)jb.w << 32);
+                l1jd[st.l1n] = (unsigned long long)j | ((unsigned long long)jb.y << 32);
+                l1al[st.l1n] = (unsigned long long)jb.x | ((unsigned long long)T << 32);
             }
+            ++st.l1n;
+            st.s_last += T;
+            ++st.l0_head;
+            ++st.moved;
+            st.head_last = kEmpty;
         }
     }
 
@@ -438,31 +513,40 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
                 // ---- calculateContractRequest over GetLevel1() (ProvideJobs, D9 padding) ----
                 const uint32_t ln = a.cl[q].l1n;
                 const uint64_t qj0 = a.job_off[q];
+                const unsigned long long* qcm = a.l1cm + qj0;
+                const unsigned long long* qjd = a.l1jd + qj0;
                 uint32_t sc = 0, sm = 0, md = 0;
                 for (uint32_t i = lane; i < ln; i += kWave) {
-                    const uint4 jb = a.jobs[qj0 + a.l1[qj0 + i]];
+                    const unsigned long long cm = qcm[i];
+                    const uint32_t jc = (uint32_t)cm, jm = (uint32_t)(cm >> 32);
                     if (pol == 0u) {  // fast node: sums and the longest duration (:138-155)
-                        sc += jb.z;
-                        sm += jb.w;
-                        md = jb.y > md ? jb.y : md;
+                        const uint32_t d = (uint32_t)(qjd[i] >> 32);
+                        sc += jc;
+                        sm += jm;
+                        md = d > md ? d : md;
                     } else {          // small node: int32 arithmetic (:232-259)
-                        sc += (int32_t)(0u - jb.z) < 0 ? jb.z : 0u;
-                        sm += (int32_t)(0u - jb.w) < 0 ? jb.w : 0u;
+                        sc += (int32_t)(0u - jc) < 0 ? jc : 0u;
+                        sm += (int32_t)(0u - jm) < 0 ? jm : 0u;
                     }
                 }
                 const uint32_t kc = dt_wave_sum_u32(sc), km = dt_wave_sum_u32(sm);
                 uint32_t ksec = dt_wave_max_u32(md);
                 if (pol == 1u) {
                     // contract.Time per job: endTime if the previous time < endTime, else 0
-                    // (:263-265); a padded last batch (len % 20 != 0) ends with zero jobs -> 0
+                    // (:263-265); a padded last batch (len % 20 != 0) ends with zero jobs -> 0.
+                    // Durations are staged 64 at a time in LDS, then scanned by one lane.
                     uint32_t t = 0;
-                    if (lane == 0) {
-                        if (ln % 20u == 0u) {
-                            for (uint32_t i = 0; i < ln; ++i) {
-                                const uint32_t d = a.jobs[qj0 + a.l1[qj0 + i]].y;
-                                t = t < d ? d : 0u;
+                    if (ln % 20u == 0u) {
+                        for (uint32_t b = 0; b < ln; b += kWave) {
+                            __syncthreads();
+                            if (b + lane < ln) appr[lane] = (uint32_t)(qjd[b + lane] >> 32);
+                            __syncthreads();
+                            if (lane == 0) {
+                                const uint32_t m = ln - b < (uint32_t)kWave ? ln - b : (uint32_t)kWave;
+                                for (uint32_t i = 0; i < m; ++i) t = t < appr[i] ? appr[i] : 0u;
                             }
                         }
+                        __syncthreads();
                     }
                     ksec = (uint32_t)__shfl((int)t, 0);
                 }
@@ -565,6 +649,7 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
                                                 ((unsigned long long)(uint32_t)fm << 32);
                             atomicAdd(&a.cl[r].nrun, 1u);  // atomics: never read back in here
                             atomicMin(&a.cl[r].minf, T + ksec);
+                            atomicOr(&a.cl[r].l1_dirty, 1u);  // the commit may wrap a counter
                         }
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                         __syncthreads();
@@ -590,6 +675,7 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
                             a.vcap[(size_t)q * a.V + nv] = make_uint2(kc, km);
                             nvs[q] = nv + 1u;
                             atomicAdd(&a.cl[q].nv, 1u);
+                            atomicOr(&a.cl[q].l1_dirty, 1u);
                         } else {
                             atomicOr(&a.cl[q].flags, (uint32_t)MCS_FLAG_VNODE_OVERFLOW);
                         }

@@ -5,8 +5,9 @@
 //   tn     u64 {free_c | free_m << 32} per physical node (CSR node_off), live across ticks
 //   vn     u64 free vector of virtual node v at [c * V + v]; vcap uint2 its capacity
 //   sfin/snode/scm  running slots (finish, node, {c | m << 32}); Foreign jobs included
-//   l1     u32 Level1 list (local job indices), capacity = the cluster's job count (at job_off)
-//   jmap   i64 WaitTime.JobsMap per job (at job_off)
+//   l1cm/l1jd/l1al  the Level1 list, capacity = the cluster's job count (at job_off), one u64 each:
+//          {cores | mem << 32}, {job | dur << 32}, {arrival | last examined << 32}; the JobsMap
+//          entry of a Level1 job is 1000 * (last - arrival), so no per-job map is kept
 //   cl     DtCluster queue cursors, counters, WaitTime sums, last sample
 //   tr     DtTrader trader state (two-stage RequestPolicyMonitor, responder lock)
 //   ctl    DtCtl the lock-step clock and log counters
@@ -43,10 +44,17 @@ struct DtCluster {
     uint32_t total_c;   // SetTotalResources at Run (cluster.go:26-40), physical nodes only
     uint32_t total_m;
     float cu, mu;       // last sample
-    uint32_t pad;
+    uint32_t head_last; // last tick the Level0 head was examined (kEmpty: not yet)
     double avgw;        // last WaitTime.GetAverage()
     long long total;    // WaitTime.TotalTime (ms)
     long long count;    // WaitTime.JobsCount
+    // Level1 pass elision: a pass can only place a job after something raised a free counter
+    // (a release, a new virtual node, a Foreign job wrapping a counter) or after a pass that
+    // placed (its skipped entries).  Otherwise every entry fails again and only its JobsMap entry
+    // moves to T: entries' effective last = max(stored last, t_all), s_last = their sum.
+    uint32_t l1_dirty;
+    uint32_t t_all;
+    unsigned long long s_last;
 };
 
 struct DtTrader {
@@ -80,8 +88,9 @@ struct DtArgs {
     uint32_t* sfin;
     uint32_t* snode;
     unsigned long long* scm;
-    uint32_t* l1;
-    long long* jmap;
+    unsigned long long* l1cm;
+    unsigned long long* l1jd;
+    unsigned long long* l1al;
     DtCluster* cl;
     DtTrader* tr;
     DtCtl* ctl;
