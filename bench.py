@@ -26,6 +26,7 @@ sys.path.insert(0, os.path.join(REPO, "multi-cluster-simulator_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 BYTES_PER_PLACEMENT = 28  # 16 B job record read + 12 B result write
+BYTES_PER_PLACEMENT_FUSED = 12  # --gen fused: the record is synthesised in registers, only results move
 
 
 def parse():
@@ -46,13 +47,17 @@ def parse():
     ap.add_argument("--policy", choices=["fifo", "delay"], default="fifo",
                     help="c4 policy: fifo (the headline, Scheduler.Fifo) or delay (Scheduler.Delay, "
                          "the reference's default policy, scheduler.go:116)")
+    ap.add_argument("--gen", choices=["stream", "fused"], default="stream",
+                    help="c4 job stream: 'stream' = records generated before the timed region and read "
+                         "from HBM (SURVEY §8d, 28 B/placement); 'fused' = synthesised inside the "
+                         "placement kernel (SURVEY §8f row 3, 12 B/placement)")
     ap.add_argument("--config", choices=["c4", "c5"], default="c4",
                     help="c4: the headline FIFO benchmark; c5: the lock-step borrow + trader system "
                          "(--clusters = clusters of the WHOLE system, sharded over the ranks)")
     a = ap.parse_args()
     if a.traffic_json is None:
-        a.traffic_json = os.path.join(REPO, "profiles", "traffic_latest_delay.json" if a.policy == "delay"
-                                      else "traffic_latest.json")
+        a.traffic_json = os.path.join(REPO, "profiles", "traffic_latest" + ("_delay" if a.policy == "delay" else "")
+                                      + ("_fused" if a.gen == "fused" else "") + ".json")
     if a.config == "c5" and a.policy == "delay":
         # DELAY schedulers trading real contracts: cluster_small replicas at the
         # reference client's rate, where Level1 fills and the WaitTime policy breaks
@@ -368,7 +373,9 @@ def main():
     eng = Engine(local_rank, policy="DELAY" if delay else "FIFO")
     arrays = replicate(uniform_cluster(args.nodes), args.clusters)
     eng.load_clusters(arrays)
-    gp = GenParams(seed=rank_seed(args.seed, rank), arrival_mode=1, lam=lam)
+    fused = args.gen == "fused"
+    bpp = BYTES_PER_PLACEMENT_FUSED if fused else BYTES_PER_PLACEMENT
+    gp = GenParams(seed=rank_seed(args.seed, rank), arrival_mode=1, lam=lam, fused=fused)
     eng.generate_jobs(gp, args.jobs_per_cluster)
     n_jobs = eng.num_jobs
 
@@ -415,13 +422,13 @@ def main():
     if rank == 0:
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
         placements_per_launch = placed / args.steps  # this rank
-        achieved = placements_per_launch * BYTES_PER_PLACEMENT / avg_kernel_s / 1e9
+        achieved = placements_per_launch * bpp / avg_kernel_s / 1e9
         traffic = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if (tj.get("clusters"), tj.get("nodes"), tj.get("jobs_per_cluster"), tj.get("policy", "fifo")) == \
-                    (args.clusters, args.nodes, args.jobs_per_cluster, args.policy):
+            if (tj.get("clusters"), tj.get("nodes"), tj.get("jobs_per_cluster"), tj.get("policy", "fifo"),
+                    tj.get("gen", "stream")) == (args.clusters, args.nodes, args.jobs_per_cluster, args.policy, args.gen):
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -448,11 +455,13 @@ def main():
             "config": {
                 "workload": f"C4: {args.clusters} clusters x {args.nodes} nodes per GPU, "
                             f"{'DELAY' if delay else 'FIFO'}, no trading, "
+                            + ("job stream synthesised inside the kernel (fused), " if fused else "") +
                             f"{args.jobs_per_cluster} jobs/cluster, scaled arrivals at {args.load:.0%} memory load "
                             f"(lambda={lam:.4f}/s)",
                 "clusters_per_gpu": args.clusters,
                 "nodes": args.nodes,
                 "jobs_per_cluster": args.jobs_per_cluster,
+                "gen": args.gen,
                 "placements_per_step_per_gpu": placements_per_launch,
                 "parallelism": f"dp{world} (independent cluster shards, no collective on the data path)",
             },
@@ -465,7 +474,7 @@ def main():
                 "traffic": traffic,
                 "kernel": "mcs::delay_kernel" if delay else "mcs::fifo_kernel",
                 "kernel_ms_avg": avg_kernel_s * 1e3,
-                "bytes_per_placement": BYTES_PER_PLACEMENT,
+                "bytes_per_placement": bpp,
             },
             "cpu_baseline": cpu,
             "slot_pool_escalations": escalations,

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MCS_ABI_VERSION 3
+#define MCS_ABI_VERSION 4
 
 /* ---- status codes --------------------------------------------------------------------------- */
 typedef enum mcs_status {
@@ -103,7 +103,10 @@ typedef struct mcs_gen_params {
     double lambda;        /* Poisson mean per minute (REF, 10 in client.go:108) or per second (SCALED) */
     uint32_t max_cores;   /* 0 = per-cluster max node Cores (setMaxCluster, client.go:68-83)          */
     uint32_t max_mem;     /* 0 = per-cluster max node Memory                                          */
-    uint32_t reserved[4];
+    uint32_t fused;       /* 1: no job records in HBM; the FIFO/DELAY kernels synthesise each 64-job
+                             batch in registers, bit-identical to the records;
+                             mcs_read_jobs and the trading paths materialise them on demand      */
+    uint32_t reserved[3];
 } mcs_gen_params;
 
 void mcs_gen_params_default(mcs_gen_params* p);
@@ -179,7 +182,8 @@ int mcs_submit_jobs(mcs_engine* eng, const uint32_t* arrival_s, const uint32_t* 
                     const uint32_t* cores, const uint32_t* mem, const uint64_t* job_offsets);
 
 /* Same as mcs_submit_jobs but synthesises n_jobs per cluster on the device (bit-identical to
- * mcs_gen_cluster_host for every cluster). */
+ * mcs_gen_cluster_host for every cluster).  With p->fused the records are never stored: every
+ * FIFO/DELAY run regenerates them inside the placement kernels. */
 int mcs_generate_jobs(mcs_engine* eng, const mcs_gen_params* p, uint64_t jobs_per_cluster);
 
 /* Copies the (submitted or generated) job streams back to the host (sizes from the offsets). */

@@ -14,7 +14,8 @@
 //   * node free vectors, running slots and releases are fifo_kernel's (LDS packed u64 nodes,
 //     first fit = per-lane select + DPP wave minimum, commit = one ds_sub_u64);
 //   * Level0 is a cursor h into the arrival-sorted SoA stream (jobs leave Level0 in stream order,
-//     either placed or moved), streamed 64 records at a time like fifo_kernel's ready queue;
+//     either placed or moved), streamed 64 records at a time like fifo_kernel's ready queue, or
+//     synthesised in registers with fused generation (GEN, mcs_gen_dev.h);
 //   * Level1 is a dense list in HBM scratch (capacity = the cluster's job count, so it never
 //     overflows): {cores | mem << 32} and {job | dur << 32}, 16 B per entry.  A pass reads it 64
 //     entries per coalesced load (sc1: served by L2, never a stale L1 line of this CU) and
@@ -32,6 +33,7 @@
 // change anything is the next release, the Level0 head's MaxWaitTime move, or (empty Level0) the
 // next arrival — the skipped iterations repeat the same failures (exact, oracle-tested).
 #define MCS_GEN_FN __host__ __device__ static inline
+#include "mcs_gen_dev.h"
 #include "mcs_internal.h"
 #include "mcs_wave.h"
 
@@ -59,7 +61,7 @@ __device__ __forceinline__ uint64_t ld_l2(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int NPL, int P>
+template <int NPL, int P, bool GEN>
 __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     static_assert(P <= 32, "free-row mask is one u32 per lane");
     constexpr bool kHist = NPL <= 2;  // exact Level1 fit histogram (256 B of LDS)
@@ -86,7 +88,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
 
     const uint64_t j0 = a.job_off[ci];
     const uint32_t J = (uint32_t)(a.job_off[ci + 1] - j0);
-    const uint4* __restrict__ jobs = a.jobs + j0;
+    const uint4* __restrict__ jobs = GEN ? nullptr : a.jobs + j0;
     int32_t* __restrict__ o_node = a.out_node + j0;
     uint32_t* __restrict__ o_start = a.out_start + j0;
     uint32_t* __restrict__ o_finish = a.out_finish + j0;
@@ -99,9 +101,18 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
 #pragma unroll
     for (int p = 0; p < P; ++p) pay_nf[p * kWave + lane] = (uint64_t)kEmpty << 32;
 
+    // Level0 batches: streamed from HBM, or synthesised in registers (GEN, mcs_gen_dev.h)
+    GenStream gs;
+    if constexpr (GEN) gs.init(a.gen, ci, lane);
+    auto load_batch = [&](uint32_t base) __attribute__((always_inline)) -> uint4 {
+        if constexpr (GEN)
+            return gs.next(base, lane);
+        else
+            return jobs[base + lane];
+    };
     uint32_t cb = 0;
-    uint4 cur = jobs[lane];
-    uint4 nxt = jobs[kWave + lane];
+    uint4 cur = load_batch(0);
+    uint4 nxt = load_batch(kWave);
 
     uint32_t t = 0, h = 0, l1n = 0, minf = kEmpty, flags = 0;
     // Counters and the WaitTime sums live in VGPRs (the asm hides their uniformity): the CU's scalar
@@ -302,7 +313,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         if (h - cb >= (uint32_t)kWave) {
             cur = nxt;
             cb += kWave;
-            nxt = jobs[cb + kWave + lane];
+            nxt = load_batch(cb + kWave);
         }
         const uint32_t l = (h - cb) & 63u;
         const uint32_t arr = readlane(cur.x, l);
@@ -430,34 +441,39 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     }
 }
 
-template <int NPL, int P>
+template <int NPL, int P, bool GEN>
 static hipError_t launch_delay_one(const DelayArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((delay_kernel<NPL, P>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL((delay_kernel<NPL, P, GEN>), dim3(a.n_items), dim3(kWave), 0, s, a);
     return hipGetLastError();
 }
 
-template <int NPL>
+template <int NPL, bool GEN>
 static hipError_t launch_delay_npl(const DelayArgs& a, int pool, hipStream_t s) {
     switch (pool) {
-        case 2: return launch_delay_one<NPL, 2>(a, s);
-        case 4: return launch_delay_one<NPL, 4>(a, s);
-        case 8: return launch_delay_one<NPL, 8>(a, s);
-        case 16: return launch_delay_one<NPL, 16>(a, s);
-        case 32: return launch_delay_one<NPL, 32>(a, s);
+        case 2: return launch_delay_one<NPL, 2, GEN>(a, s);
+        case 4: return launch_delay_one<NPL, 4, GEN>(a, s);
+        case 8: return launch_delay_one<NPL, 8, GEN>(a, s);
+        case 16: return launch_delay_one<NPL, 16, GEN>(a, s);
+        case 32: return launch_delay_one<NPL, 32, GEN>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <bool GEN>
+static hipError_t launch_delay_gen(const DelayArgs& a, int npl, int pool, hipStream_t s) {
+    switch (npl) {
+        case 1: return launch_delay_npl<1, GEN>(a, pool, s);
+        case 2: return launch_delay_npl<2, GEN>(a, pool, s);
+        case 4: return launch_delay_npl<4, GEN>(a, pool, s);
+        case 8: return launch_delay_npl<8, GEN>(a, pool, s);
+        case 16: return launch_delay_npl<16, GEN>(a, pool, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 hipError_t launch_delay(const DelayArgs& a, int npl, int pool, hipStream_t s) {
     if (a.n_items == 0) return hipSuccess;
-    switch (npl) {
-        case 1: return launch_delay_npl<1>(a, pool, s);
-        case 2: return launch_delay_npl<2>(a, pool, s);
-        case 4: return launch_delay_npl<4>(a, pool, s);
-        case 8: return launch_delay_npl<8>(a, pool, s);
-        case 16: return launch_delay_npl<16>(a, pool, s);
-        default: return hipErrorInvalidValue;
-    }
+    return a.gen.on ? launch_delay_gen<true>(a, npl, pool, s) : launch_delay_gen<false>(a, npl, pool, s);
 }
 
 }  // namespace mcs

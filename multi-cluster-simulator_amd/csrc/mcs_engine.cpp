@@ -36,6 +36,8 @@ void free_clusters(mcs_engine* e) {
 
 void free_jobs(mcs_engine* e) {
     dfree(e->d_jobs);
+    dfree(e->d_gen_max);
+    e->gen = mcs::GenArgs{};
     dfree(e->d_job_off);
     dfree(e->d_out_node);
     dfree(e->d_out_start);
@@ -63,6 +65,24 @@ int auto_pool(uint32_t max_n) {
 
 
 }  // namespace
+
+namespace mcs {
+int ensure_job_records(mcs_engine* e) {
+    if (e->d_jobs) return MCS_OK;
+    const size_t nj = e->total_jobs ? e->total_jobs : 1;
+    HIPCHK(e, hipMalloc(&e->d_jobs, (nj + kJobPad) * sizeof(uint4)));
+    HIPCHK(e, hipMemsetAsync(e->d_jobs + nj, 0, kJobPad * sizeof(uint4), e->stream));
+    hipError_t st = launch_gen_attrs(e->d_jobs, e->d_job_off, e->gen.max_c, e->gen.max_m, e->C,
+                                     e->gen.seed, e->gen.max_dur, e->gen.base, e->stream);
+    if (st == hipSuccess)
+        st = launch_gen_arrivals(e->d_jobs, e->d_job_off, e->C, e->gen.seed, e->gen.mode, e->gen.enl,
+                                 e->gen.base, e->stream);
+    if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+    if (st != hipSuccess)
+        return fail(e, MCS_E_HIP, std::string("job generation: ") + hipGetErrorString(st));
+    return MCS_OK;
+}
+}  // namespace mcs
 
 extern "C" {
 
@@ -258,7 +278,7 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
     return MCS_OK;
 }
 
-static int alloc_jobs(mcs_engine* e, const uint64_t* job_offsets) {
+static int alloc_jobs(mcs_engine* e, const uint64_t* job_offsets, bool records) {
     free_jobs(e);
     mcs::trade_free(e);
     mcs::dtrade_free(e);
@@ -268,8 +288,10 @@ static int alloc_jobs(mcs_engine* e, const uint64_t* job_offsets) {
     const size_t nj = e->total_jobs ? e->total_jobs : 1;
     /* kJobPad records of slack after the last cluster: the FIFO kernel streams 64-record batches
      * one ahead without bounds masks (records past a cluster's end are read, never used) */
-    HIPCHK(e, hipMalloc(&e->d_jobs, (nj + mcs::kJobPad) * sizeof(uint4)));
-    HIPCHK(e, hipMemset(e->d_jobs + nj, 0, mcs::kJobPad * sizeof(uint4)));
+    if (records) {
+        HIPCHK(e, hipMalloc(&e->d_jobs, (nj + mcs::kJobPad) * sizeof(uint4)));
+        HIPCHK(e, hipMemset(e->d_jobs + nj, 0, mcs::kJobPad * sizeof(uint4)));
+    }
     HIPCHK(e, hipMalloc(&e->d_job_off, (e->C + 1) * sizeof(uint64_t)));
     HIPCHK(e, hipMalloc(&e->d_out_node, nj * sizeof(int32_t)));
     HIPCHK(e, hipMalloc(&e->d_out_start, nj * sizeof(uint32_t)));
@@ -310,7 +332,7 @@ int mcs_submit_jobs(mcs_engine* e, const uint32_t* arrival_s, const uint32_t* du
             return fail(e, MCS_E_INVALID, "simulated clock could exceed 2^32-1 seconds");
     }
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    if (int st = alloc_jobs(e, job_offsets)) return st;
+    if (int st = alloc_jobs(e, job_offsets, true)) return st;
     std::vector<uint4> h(nj ? nj : 1);
     for (uint64_t i = 0; i < nj; ++i) h[i] = make_uint4(arrival_s[i], dur_s[i], cores[i], mem[i]);
     HIPCHK(e, hipMemcpy(e->d_jobs, h.data(), (nj ? nj : 1) * sizeof(uint4), hipMemcpyHostToDevice));
@@ -321,17 +343,16 @@ int mcs_submit_jobs(mcs_engine* e, const uint32_t* arrival_s, const uint32_t* du
 int mcs_generate_jobs(mcs_engine* e, const mcs_gen_params* p, uint64_t jobs_per_cluster) {
     if (int st = check_engine(e)) return st;
     if (!e->has_clusters) return fail(e, MCS_E_STATE, "mcs_load_clusters first");
-    if (!p || !(p->lambda > 0.0) || p->lambda > 128.0 || p->arrival_mode > 1u || p->max_dur_s == 0)
+    if (!p || !(p->lambda > 0.0) || p->lambda > 128.0 || p->arrival_mode > 1u || p->max_dur_s == 0 ||
+        p->fused > 1u)
         return fail(e, MCS_E_INVALID, "bad generator parameters");
     if (jobs_per_cluster > 0xFFFFFFFFull) return fail(e, MCS_E_INVALID, "too many jobs per cluster");
     std::vector<uint64_t> off(e->C + 1);
     for (uint32_t c = 0; c <= e->C; ++c) off[c] = (uint64_t)c * jobs_per_cluster;
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    if (int st = alloc_jobs(e, off.data())) return st;
+    if (int st = alloc_jobs(e, off.data(), false)) return st;
     const uint32_t* mc = e->d_max_c;
     const uint32_t* mm = e->d_max_m;
-    std::vector<uint32_t> fixc, fixm;
-    uint32_t* tmp = nullptr;
     if (p->max_cores || p->max_mem) { /* explicit maxima override setMaxCluster */
         std::vector<uint32_t> hc(e->C), hm(e->C);
         HIPCHK(e, hipMemcpy(hc.data(), e->d_max_c, e->C * 4, hipMemcpyDeviceToHost));
@@ -340,24 +361,25 @@ int mcs_generate_jobs(mcs_engine* e, const mcs_gen_params* p, uint64_t jobs_per_
             if (p->max_cores) hc[c] = p->max_cores;
             if (p->max_mem) hm[c] = p->max_mem;
         }
-        HIPCHK(e, hipMalloc(&tmp, 2 * e->C * sizeof(uint32_t)));
-        HIPCHK(e, hipMemcpy(tmp, hc.data(), e->C * 4, hipMemcpyHostToDevice));
-        HIPCHK(e, hipMemcpy(tmp + e->C, hm.data(), e->C * 4, hipMemcpyHostToDevice));
-        mc = tmp;
-        mm = tmp + e->C;
+        HIPCHK(e, hipMalloc(&e->d_gen_max, 2 * (size_t)e->C * sizeof(uint32_t)));
+        HIPCHK(e, hipMemcpy(e->d_gen_max, hc.data(), e->C * 4, hipMemcpyHostToDevice));
+        HIPCHK(e, hipMemcpy(e->d_gen_max + e->C, hm.data(), e->C * 4, hipMemcpyHostToDevice));
+        mc = e->d_gen_max;
+        mm = e->d_gen_max + e->C;
     }
     /* clusters are keyed by their global index rank*C + c (mcs_set_shard), so a sharded system
      * generates exactly the streams of the same system on one engine */
-    const uint32_t base = e->rank * e->C;
-    hipError_t st = mcs::launch_gen_attrs(e->d_jobs, e->d_job_off, mc, mm, e->C, p->seed,
-                                          p->max_dur_s, base, e->stream);
-    if (st == hipSuccess)
-        st = mcs::launch_gen_arrivals(e->d_jobs, e->d_job_off, e->C, p->seed, p->arrival_mode,
-                                      std::exp(-p->lambda), base, e->stream);
-    if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
-    if (tmp) (void)hipFree(tmp);
-    if (st != hipSuccess)
-        return fail(e, MCS_E_HIP, std::string("job generation: ") + hipGetErrorString(st));
+    e->gen.seed = p->seed;
+    e->gen.enl = std::exp(-p->lambda);
+    e->gen.max_c = mc;
+    e->gen.max_m = mm;
+    e->gen.mode = p->arrival_mode;
+    e->gen.max_dur = p->max_dur_s;
+    e->gen.base = e->rank * e->C;
+    e->gen.on = p->fused;
+    /* fused: no records in HBM; the FIFO/DELAY kernels synthesise each batch (mcs_gen_dev.h) */
+    if (!p->fused)
+        if (int st = mcs::ensure_job_records(e)) return st;
     e->has_jobs = true;
     return MCS_OK;
 }
@@ -369,6 +391,7 @@ int mcs_read_jobs(mcs_engine* e, uint32_t* arrival_s, uint32_t* dur_s, uint32_t*
     const uint64_t nj = e->total_jobs;
     if (!nj) return MCS_OK;
     if (!arrival_s || !dur_s || !cores || !mem) return fail(e, MCS_E_INVALID, "null output");
+    if (int st = mcs::ensure_job_records(e)) return st;
     std::vector<uint4> h(nj);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipMemcpy(h.data(), e->d_jobs, nj * sizeof(uint4), hipMemcpyDeviceToHost));
@@ -385,6 +408,8 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     if (int st = check_engine(e)) return st;
     if (!e->has_clusters || !e->has_jobs) return fail(e, MCS_E_STATE, "load clusters and jobs first");
     if (t_end_s != MCS_TIME_NONE) return fail(e, MCS_E_INVALID, "finite horizons are reserved");
+    if (e->cfg.borrow || e->cfg.trader) /* the trading paths read the job records */
+        if (int st = mcs::ensure_job_records(e)) return st;
     if (e->cfg.policy == MCS_POLICY_DELAY && e->cfg.trader) return mcs::dtrade_run(e, stats);
     if (e->cfg.borrow || e->cfg.trader) return mcs::trade_run(e, stats);
     e->trade_run = false;
@@ -412,6 +437,7 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     a.out_finish = e->d_out_finish;
     a.cstats = e->d_cstats;
     a.totals = e->d_totals;
+    a.gen = e->gen;
     a.n_items = e->C;
     mcs::DelayArgs da{};
     da.node_free0 = e->d_free0;
@@ -427,6 +453,7 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     da.cstats = e->d_cstats;
     da.dstats = e->d_dstats;
     da.totals = e->d_totals;
+    da.gen = e->gen;
     da.max_wait_s = e->cfg.max_wait_s;
     da.n_items = e->C;
 

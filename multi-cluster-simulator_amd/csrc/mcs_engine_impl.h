@@ -21,6 +21,9 @@ int dtrade_run(mcs_engine* e, mcs_stats* stats);
 int dtrade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n);
 int dtrade_delay_stats(mcs_engine* e, mcs_delay_cluster_stats* out, uint32_t n);
 int dtrade_trade_stats(mcs_engine* e, mcs_trade_stats* out);
+// job records in HBM for the paths that read them (trading, mcs_read_jobs): a fused synthetic
+// stream is materialised by the generator kernels (mcs_engine.cpp)
+int ensure_job_records(mcs_engine* e);
 int dtrade_read_trades(mcs_engine* e, mcs_trade_rec* out, uint64_t cap, uint64_t* n);
 int dtrade_read_vnode_counts(mcs_engine* e, uint32_t* out, uint32_t n);
 }  // namespace mcs
@@ -45,7 +48,9 @@ struct mcs_engine {
     uint32_t* d_live_m = nullptr;
     uint32_t* d_max_c = nullptr;
     uint32_t* d_max_m = nullptr;
-    uint4* d_jobs = nullptr;
+    uint4* d_jobs = nullptr;        // null while a fused synthetic stream is not materialised
+    mcs::GenArgs gen{};             // the synthetic stream of mcs_generate_jobs (gen.on: fused)
+    uint32_t* d_gen_max = nullptr;  // its explicit maxima: [C] cores, then [C] memory
     uint64_t* d_job_off = nullptr;
     int32_t* d_out_node = nullptr;
     uint32_t* d_out_start = nullptr;

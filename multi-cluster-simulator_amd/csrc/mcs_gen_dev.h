@@ -1,0 +1,104 @@
+// mcs_gen_dev.h — the job stream synthesised inside the placement kernels.
+//
+// With mcs_gen_params.fused the FIFO and DELAY kernels never read job records from HBM: each
+// 64-job batch is generated in registers when the kernel reaches it.  Job j of cluster k gets
+// exactly the record mcs_gen_job_attrs + mcs_gen_arrivals (mcs_gen.h) give it, so a fused run
+// equals the materialised run bit for bit (tests/test_gpu_fused.py).
+//
+//   * Attributes are counter-based (key, j): one job per lane.
+//   * Arrivals are mcs_gen_arrivals' sequential scan over Poisson periods.  Here a wave draws the
+//     counts of 64 periods at once (lane l = period pw + l), prefix-sums the counts and the period
+//     lengths (REF: n * floor(60 / n) s, or 60 s for an empty minute; SCALED: 1 s), and each lane
+//     finds its job's period with a 6-step binary search over the inclusive counts.  A window of
+//     64 periods holds ~64 * lambda jobs, so at the C4 rate the scan costs about one window per
+//     two batches.
+// The host resolves exp(-lambda) once (like mcs_generate_jobs), so device and host draws match.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef MCS_GEN_FN
+#define MCS_GEN_FN __host__ __device__ static inline
+#endif
+#include "mcs_gen.h"
+#include "mcs_internal.h"
+#include "mcs_wave.h"
+
+namespace mcs {
+
+__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t w = (uint32_t)__shfl_up((int)v, o);
+        v += lane >= (uint32_t)o ? w : 0u;
+    }
+    return v;
+}
+
+struct GenStream {
+    uint64_t ckey, akey;
+    double enl;
+    uint32_t mode, mc, mm, md;
+    uint32_t pw, jw, tw;   // window: first period, its first job, its start second
+    uint32_t n, cum, tex;  // lane l: jobs of period pw + l, inclusive job count, start offset
+    uint32_t tot, span;    // jobs and seconds of the whole window
+
+    __device__ __forceinline__ void fill(uint32_t lane) {
+        n = mcs_poisson(akey, (uint64_t)pw + lane, enl);
+        const uint32_t d = mode == 0u ? (n == 0u ? 60u : n * (60u / n)) : 1u;  // client.go:116-125, D5
+        cum = wave_incl_sum_u32(n, lane);
+        const uint32_t dinc = wave_incl_sum_u32(d, lane);
+        tex = dinc - d;
+        tot = readlane(cum, 63);
+        span = readlane(dinc, 63);
+    }
+
+    __device__ __forceinline__ void init(const GenArgs& g, uint32_t cluster, uint32_t lane) {
+        ckey = mcs_cluster_key(g.seed, g.base + cluster);
+        akey = mcs_arrival_key(ckey);
+        enl = g.enl;
+        mode = g.mode;
+        mc = g.max_c[cluster];
+        mm = g.max_m[cluster];
+        md = g.max_dur;
+        pw = 0u;
+        jw = 0u;
+        tw = 0u;
+        fill(lane);
+    }
+
+    // the records {arrival, dur, cores, mem} of jobs [base, base + 64); bases must increase
+    __device__ __forceinline__ uint4 next(uint32_t base, uint32_t lane) {
+        const uint32_t j = base + lane;
+        uint32_t arr = 0u, done = 0u;
+        for (;;) {
+            // every lane searches (the shuffles need all lanes); lanes outside the window discard
+            const uint32_t rel = j - jw;
+            uint32_t lo = 0u;
+#pragma unroll
+            for (uint32_t s = 32u; s != 0u; s >>= 1) {
+                const uint32_t c = (uint32_t)__shfl((int)cum, (int)(lo + s - 1u));
+                lo += c <= rel ? s : 0u;
+            }
+            const uint32_t np = (uint32_t)__shfl((int)n, (int)lo);
+            const uint32_t cp = (uint32_t)__shfl((int)cum, (int)lo);
+            const uint32_t te = (uint32_t)__shfl((int)tex, (int)lo);
+            const uint32_t a = mode == 0u ? tw + te + (rel - (cp - np)) * (60u / (np != 0u ? np : 1u))
+                                          : pw + lo;
+            if (!done && rel < tot) {
+                arr = a;
+                done = 1u;
+            }
+            if (base + 63u - jw < tot) break;  // the batch's last job lies in this window
+            jw += tot;
+            tw += span;
+            pw += (uint32_t)kWave;
+            fill(lane);
+        }
+        uint32_t d, c, m;
+        mcs_gen_job_attrs(ckey, j, mc, mm, md, &d, &c, &m);
+        return make_uint4(arr, d, c, m);
+    }
+};
+
+}  // namespace mcs

@@ -27,6 +27,19 @@ struct Totals {  // device-side accumulation of mcs_stats (only clusters that di
     unsigned int overflowed;
 };
 
+// In-kernel synthesis of the job stream (mcs_gen_dev.h): with `on` the FIFO and
+// DELAY kernels generate each 64-job batch in registers and `jobs` is not read (may be null).
+struct GenArgs {
+    unsigned long long seed;
+    double enl;             // exp(-lambda), resolved once on the host like mcs_generate_jobs
+    const uint32_t* max_c;  // per-cluster maxima: setMaxCluster (client.go:68-83) or explicit
+    const uint32_t* max_m;
+    uint32_t mode;          // mcs_arrival_mode
+    uint32_t max_dur;
+    uint32_t base;          // global index of the engine's cluster 0 (mcs_set_shard)
+    uint32_t on;
+};
+
 struct FifoArgs {
     const uint2* node_free0;
     const uint32_t* node_off;
@@ -38,6 +51,7 @@ struct FifoArgs {
     uint32_t* out_finish;
     mcs_cluster_stats* cstats;
     Totals* totals;
+    GenArgs gen;
     uint32_t n_items;
 };
 
@@ -55,6 +69,7 @@ struct DelayArgs {
     mcs_cluster_stats* cstats;
     mcs_delay_cluster_stats* dstats;
     Totals* totals;
+    GenArgs gen;
     uint32_t max_wait_s;
     uint32_t n_items;
 };

@@ -20,7 +20,8 @@
 //     next completion time is a DPP wave minimum;
 //   * job records are streamed from HBM 64 at a time with one coalesced 16 B/lane load (uint4
 //     {arrival, dur, cores, mem}), double-buffered one batch ahead, and broadcast to the scalar
-//     unit with v_readlane;
+//     unit with v_readlane; with fused generation (GEN) each batch is synthesised in registers
+//     instead and no record is read (mcs_gen_dev.h);
 //   * results are gathered 64 jobs per register batch (placements happen in job order because
 //     FIFO head-of-line blocking is strict) and written with three coalesced 256 B stores.
 //
@@ -32,12 +33,13 @@
 // float32 and must round like Go).
 #define MCS_GEN_FN __host__ __device__ static inline
 #include "mcs_gen.h"
+#include "mcs_gen_dev.h"
 #include "mcs_internal.h"
 #include "mcs_wave.h"
 
 namespace mcs {
 
-template <int NPL, int P>
+template <int NPL, int P, bool GEN>
 __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     static_assert(P <= 32, "free-row mask is one u32 per lane");
     const uint32_t item = blockIdx.x;
@@ -68,7 +70,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     // ---- job stream ----
     const uint64_t j0 = a.job_off[ci];
     const uint32_t J = (uint32_t)(a.job_off[ci + 1] - j0);
-    const uint4* __restrict__ jobs = a.jobs + j0;
+    const uint4* __restrict__ jobs = GEN ? nullptr : a.jobs + j0;
     int32_t* __restrict__ o_node = a.out_node + j0;
     uint32_t* __restrict__ o_start = a.out_start + j0;
     uint32_t* __restrict__ o_finish = a.out_finish + j0;
@@ -77,8 +79,14 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     // (the next cluster's, or the pad) are read but never used, because r < J guards every use.
     // An unmasked load can land straight in the loop-carried batch registers, so the prefetch one
     // batch ahead is not waited for until that batch is needed.
+    // GEN: the batch is synthesised in registers instead (mcs_gen_dev.h; bases come in order)
+    GenStream gs;
+    if constexpr (GEN) gs.init(a.gen, ci, lane);
     auto load_batch = [&](uint32_t base) __attribute__((always_inline)) -> uint4 {
-        return jobs[base + lane];
+        if constexpr (GEN)
+            return gs.next(base, lane);
+        else
+            return jobs[base + lane];
     };
 
     // running slots: frm = this lane's free rows (bit p), lmin = earliest finish among its
@@ -284,20 +292,32 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
 }
 
 // ---- variant table ------------------------------------------------------------------------------
-template <int NPL, int P>
+template <int NPL, int P, bool GEN>
 static hipError_t launch_one(const FifoArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((fifo_kernel<NPL, P>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL((fifo_kernel<NPL, P, GEN>), dim3(a.n_items), dim3(kWave), 0, s, a);
     return hipGetLastError();
 }
 
-template <int NPL>
+template <int NPL, bool GEN>
 static hipError_t launch_npl(const FifoArgs& a, int pool, hipStream_t s) {
     switch (pool) {
-        case 2: return launch_one<NPL, 2>(a, s);
-        case 4: return launch_one<NPL, 4>(a, s);
-        case 8: return launch_one<NPL, 8>(a, s);
-        case 16: return launch_one<NPL, 16>(a, s);
-        case 32: return launch_one<NPL, 32>(a, s);
+        case 2: return launch_one<NPL, 2, GEN>(a, s);
+        case 4: return launch_one<NPL, 4, GEN>(a, s);
+        case 8: return launch_one<NPL, 8, GEN>(a, s);
+        case 16: return launch_one<NPL, 16, GEN>(a, s);
+        case 32: return launch_one<NPL, 32, GEN>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <bool GEN>
+static hipError_t launch_fifo_gen(const FifoArgs& a, int npl, int pool, hipStream_t s) {
+    switch (npl) {
+        case 1: return launch_npl<1, GEN>(a, pool, s);
+        case 2: return launch_npl<2, GEN>(a, pool, s);
+        case 4: return launch_npl<4, GEN>(a, pool, s);
+        case 8: return launch_npl<8, GEN>(a, pool, s);
+        case 16: return launch_npl<16, GEN>(a, pool, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -310,14 +330,7 @@ bool fifo_variant_exists(int npl, int pool) {
 
 hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, hipStream_t s) {
     if (a.n_items == 0) return hipSuccess;
-    switch (npl) {
-        case 1: return launch_npl<1>(a, pool, s);
-        case 2: return launch_npl<2>(a, pool, s);
-        case 4: return launch_npl<4>(a, pool, s);
-        case 8: return launch_npl<8>(a, pool, s);
-        case 16: return launch_npl<16>(a, pool, s);
-        default: return hipErrorInvalidValue;
-    }
+    return a.gen.on ? launch_fifo_gen<true>(a, npl, pool, s) : launch_fifo_gen<false>(a, npl, pool, s);
 }
 
 // ---- device job-stream synthesis (mcs_gen.h; bit-identical to the host generator) -------------

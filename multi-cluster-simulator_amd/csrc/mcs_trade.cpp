@@ -72,6 +72,7 @@ uint32_t auto_lq(const mcs_engine* e) {
 int trade_alloc(mcs_engine* e) {
     if (e->td) return MCS_OK;
     if (!e->has_clusters || !e->has_jobs) return fail(e, MCS_E_STATE, "load clusters and jobs first");
+    if (int st = ensure_job_records(e)) return st;
     const uint32_t Cl = e->C, Ct = e->C * e->world;
     if (Ct > kTrMaxClusters) return fail(e, MCS_E_INVALID, "more than 1024 clusters in a trading system");
     if (e->max_n > kTrMaxNodes) return fail(e, MCS_E_INVALID, "more than 1024 nodes in a cluster");

@@ -84,7 +84,8 @@ class mcs_gen_params(C.Structure):
         ("lambda_", C.c_double),
         ("max_cores", C.c_uint32),
         ("max_mem", C.c_uint32),
-        ("reserved", C.c_uint32 * 4),
+        ("fused", C.c_uint32),
+        ("reserved", C.c_uint32 * 3),
     ]
 
 

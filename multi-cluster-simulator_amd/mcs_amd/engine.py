@@ -35,6 +35,7 @@ class GenParams:
     lam: float = 10.0
     max_cores: int = 0
     max_mem: int = 0
+    fused: bool = False  # synthesise the stream inside the placement kernels (no records in HBM)
 
     def to_c(self) -> L.mcs_gen_params:
         p = L.mcs_gen_params()
@@ -45,6 +46,7 @@ class GenParams:
         p.lambda_ = float(self.lam)
         p.max_cores = self.max_cores
         p.max_mem = self.max_mem
+        p.fused = int(bool(self.fused))
         return p
 
 

@@ -36,7 +36,7 @@ def test_library_loads_and_exports_header_symbols():
     # every declared function has a ctypes signature in the binding
     bound = {name for name, _, _ in L.SIGNATURES}
     assert set(declared) == bound
-    assert lib.mcs_abi_version() == 3
+    assert lib.mcs_abi_version() == 4
 
 
 def test_library_is_gfx950_code_object():
@@ -113,7 +113,8 @@ def test_struct_layouts_match_headers(tmp_path):
     import ctypes as C
 
     structs = [L.mcs_config, L.mcs_gen_params, L.mcs_stats, L.mcs_cluster_stats, L.mcs_lent_rec,
-               L.mcs_trade_rec, L.mcs_trade_stats, L.mcs_comm_id]
+               L.mcs_trade_rec, L.mcs_trade_stats, L.mcs_comm_id, L.mcs_delay_cluster_stats,
+               L.mcs_contract_rec, L.mcs_foreign_rec]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mcs_trade.h"', "int main(void) {"]
     for s in structs:
         n = s.__name__

@@ -1,0 +1,115 @@
+"""GPU parity of on-device job generation fused into the placement kernels.
+
+With GenParams(fused=True) no job record is stored: fifo_kernel / delay_kernel synthesise each
+64-job batch in registers (csrc/mcs_gen_dev.h).  The runs must equal, bit for bit, the same runs
+over the materialised records and the CPU oracle over the host generator's streams (the host
+generator mcs_gen_cluster_host is the reference for the stream itself, test_abi.py).  Covered:
+both arrival modes (REF per-minute spacing with empty minutes, SCALED per-second), FIFO and DELAY,
+mixed cluster sizes in one launch (5, 10 and 256 nodes), explicit maxima, slot-pool escalation,
+mcs_read_jobs and the trading path materialising a fused stream on demand."""
+import numpy as np
+import pytest
+
+import oracle_ref as O
+from mcs_amd import (Engine, GenParams, gen_streams_host, pack_clusters, replicate, scaled_lambda,
+                     uniform_cluster)
+from mcs_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def mixed_arrays():
+    return pack_clusters([uniform_cluster(5)] * 6 + [uniform_cluster(10)] * 4 + [uniform_cluster(256)] * 6)
+
+
+def run(policy, arrays, gp, jobs, **kw):
+    with Engine(0, policy=policy, **kw) as eng:
+        eng.load_clusters(arrays)
+        eng.generate_jobs(gp, jobs)
+        st = eng.run()
+        node, start, fin = eng.placements()
+        cs = eng.cluster_stats()
+        ds = eng.delay_stats() if policy == "DELAY" else None
+    return node, start, fin, cs, ds, st
+
+
+CASES = [
+    ("FIFO", L.MCS_ARRIVAL_REF, 10.0, 2500),
+    ("FIFO", L.MCS_ARRIVAL_SCALED, None, 2500),
+    ("DELAY", L.MCS_ARRIVAL_REF, 10.0, 2000),
+    ("DELAY", L.MCS_ARRIVAL_SCALED, 0.8, 1000),
+]
+
+
+@pytest.mark.parametrize("policy,mode,lam,jobs", CASES, ids=[f"{c[0]}-{'REF' if c[1] == 0 else 'SCALED'}" for c in CASES])
+def test_fused_equals_records_and_oracle(policy, mode, lam, jobs):
+    arrays = mixed_arrays()
+    lam = lam if lam is not None else scaled_lambda(256, load=0.9)
+    gp = GenParams(seed=0x5EED + jobs, arrival_mode=mode, lam=lam)
+    ref = run(policy, arrays, gp, jobs)
+    gp.fused = True
+    fz = run(policy, arrays, gp, jobs)
+    for a, b, name in zip(ref[:3], fz[:3], ("node", "start", "finish")):
+        np.testing.assert_array_equal(a, b, err_msg=name)
+    for key in ("t_end", "placed", "waited", "peak_running", "flags"):
+        np.testing.assert_array_equal(ref[3][key], fz[3][key], err_msg=key)
+    if policy == "DELAY":
+        np.testing.assert_array_equal(ref[4], fz[4])
+    # and the oracle over the host generator's streams (bit-identical to the device generator)
+    gp.fused = False
+    streams = gen_streams_host(gp, arrays, jobs)
+    if policy == "FIFO":
+        on, os_, of, _ = O.fifo_run_batch(arrays, streams, n_threads=8)
+    else:
+        on, os_, of, _ = O.delay_run_batch(arrays, streams, n_threads=8)
+    np.testing.assert_array_equal(fz[0], on)
+    np.testing.assert_array_equal(fz[1], os_)
+    np.testing.assert_array_equal(fz[2], of)
+
+
+def test_fused_read_jobs_materialises_the_stream():
+    arrays = mixed_arrays()
+    gp = GenParams(seed=77, arrival_mode=L.MCS_ARRIVAL_REF, lam=10.0, max_cores=20, max_mem=9000, fused=True)
+    with Engine(0) as eng:
+        eng.load_clusters(arrays)
+        eng.generate_jobs(gp, 1500)
+        got = eng.read_jobs()
+        eng.run()  # a fused run after the records exist still synthesises and matches
+        node = eng.placements()[0]
+    gp.fused = False
+    want = gen_streams_host(gp, arrays, 1500)
+    for f in ("arrival", "dur", "cores", "mem"):
+        np.testing.assert_array_equal(getattr(got, f), getattr(want, f), err_msg=f)
+    on, _, _, _ = O.fifo_run_batch(arrays, want, n_threads=8)
+    np.testing.assert_array_equal(node, on)
+
+
+def test_fused_slot_pool_escalation():
+    arrays = replicate(uniform_cluster(256), 8)
+    gp = GenParams(seed=5, arrival_mode=L.MCS_ARRIVAL_SCALED, lam=scaled_lambda(256, load=0.9), fused=True)
+    node, start, fin, cs, _, st = run("FIFO", arrays, gp, 4000, slot_pool=2)
+    assert st.escalations >= 1
+    gp.fused = False
+    on, os_, of, _ = O.fifo_run_batch(arrays, gen_streams_host(gp, arrays, 4000), n_threads=8)
+    np.testing.assert_array_equal(node, on)
+    np.testing.assert_array_equal(start, os_)
+
+
+def test_fused_stream_drives_delay_trading():
+    """The trading path reads job records: a fused stream is materialised for it on demand."""
+    from mcs_amd import Cluster
+    import os
+    spec = Cluster.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets",
+                                     "cluster_small.json"))
+    arrays = replicate(spec, 6)
+    res = []
+    for fused in (False, True):
+        gp = GenParams(seed=11, fused=fused)
+        with Engine(0, policy="DELAY", trader=True) as eng:
+            eng.load_clusters(arrays)
+            eng.generate_jobs(gp, 600)
+            eng.run()
+            res.append((eng.placements(), eng.contracts()))
+    for a, b in zip(res[0][0], res[1][0]):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(res[0][1], res[1][1])

@@ -60,10 +60,11 @@ if bench and "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
         "nodes": bench["config"]["nodes"],
         "jobs_per_cluster": bench["config"]["jobs_per_cluster"],
         "policy": "delay" if "DELAY" in bench["metric"] else "fifo",
+        "gen": bench["config"].get("gen", "stream"),
         "hbm_bytes_per_launch": fetch + write,
         "fetch_bytes_corrected": fetch,
         "write_bytes": write,
-        "algorithmic_bytes_per_launch": 28.0 * jobs,
+        "algorithmic_bytes_per_launch": float(bench["roofline"]["bytes_per_placement"]) * jobs,
         "bytes_per_placement": (fetch + write) / jobs,
         "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), FETCH doubled per "
                   "MI355X_MICROARCH.md gfx950 correction",
@@ -71,8 +72,8 @@ if bench and "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
     summary["traffic"] = traffic
     with open(f"{out}/traffic.json", "w") as f:
         json.dump(traffic, f, indent=1)
-    with open("profiles/traffic_latest.json" if traffic["policy"] == "fifo" else
-              "profiles/traffic_latest_delay.json", "w") as f:
+    with open("profiles/traffic_latest" + ("_delay" if traffic["policy"] == "delay" else "")
+              + ("_fused" if traffic["gen"] == "fused" else "") + ".json", "w") as f:
         json.dump(traffic, f, indent=1)
 if "SQ_INSTS_SALU" in counters and bench:
     jobs = bench["config"]["placements_per_step_per_gpu"]
