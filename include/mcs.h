@@ -230,6 +230,27 @@ int mcs_read_live_state(mcs_engine* eng, uint32_t cluster, uint32_t* free_c, uin
 int mcs_resource_utilization(mcs_engine* eng, uint32_t cluster, float* core_util,
                              float* mem_util);
 
+/* ---- the ClusterState record as a batched reduction ---------------------- */
+/* pb.ClusterState (resource-channel.proto:27-34) that each cluster's Start stream
+ * (trader_server.go:24-47) would send at simulated second t_s, rebuilt from the last FIFO/DELAY
+ * run's placements: the counters after second t_s (jobs with start <= t_s < finish hold their
+ * node), GetResourceUtilization over them (cluster.go:46-63, float32 in node order) and the Run
+ * totals (cluster.go:26-40).  average_wait_time is not part of it (host side: mcs_read_delay_stats
+ * at the end of a DELAY run, 0 under FIFO where "/delay" never feeds WaitTime). */
+typedef struct mcs_cluster_state {
+    float cores_utilization;
+    float memory_utilization;
+    uint32_t total_cpu;
+    uint32_t total_memory;
+    uint32_t running;   /* jobs holding resources at t_s */
+    uint32_t t_s;
+} mcs_cluster_state;
+
+/* One gfx950 launch over every cluster (MCS_E_STATE after a trading run).  kernel_ms (may be
+ * NULL) receives the launch's device time from HIP events on the engine stream. */
+int mcs_cluster_states(mcs_engine* eng, uint32_t t_s, mcs_cluster_state* out, uint32_t n_clusters,
+                       double* kernel_ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -631,4 +631,40 @@ int mcs_resource_utilization(mcs_engine* e, uint32_t cluster, float* core_util,
     return MCS_OK;
 }
 
+int mcs_cluster_states(mcs_engine* e, uint32_t t_s, mcs_cluster_state* out, uint32_t n_clusters,
+                       double* kernel_ms) {
+    if (int st = check_engine(e)) return st;
+    if (!e->has_run) return fail(e, MCS_E_STATE, "mcs_run first");
+    if (e->trade_run || e->dtrade_run)
+        return fail(e, MCS_E_STATE, "cluster states are rebuilt from a FIFO/DELAY run without trading");
+    if (!out || n_clusters > e->C) return fail(e, MCS_E_INVALID, "bad output");
+    if (int st = mcs::ensure_job_records(e)) return st;
+    mcs_cluster_state* d_out = nullptr;
+    HIPCHK(e, hipMalloc(&d_out, (e->C ? e->C : 1) * sizeof(mcs_cluster_state)));
+    mcs::StateArgs a{};
+    a.node_off = e->d_node_off;
+    a.cap = e->d_cap;
+    a.free0 = e->d_free0;
+    a.jobs = e->d_jobs;
+    a.job_off = e->d_job_off;
+    a.out_node = e->d_out_node;
+    a.out_start = e->d_out_start;
+    a.out_finish = e->d_out_finish;
+    a.out = d_out;
+    a.t = t_s;
+    a.n_clusters = e->C;
+    hipError_t st = hipEventRecord(e->ev0, e->stream);
+    if (st == hipSuccess) st = mcs::launch_state(a, e->max_n ? e->max_n : 1, e->stream);
+    if (st == hipSuccess) st = hipEventRecord(e->ev1, e->stream);
+    if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+    float ms = 0.0f;
+    if (st == hipSuccess) st = hipEventElapsedTime(&ms, e->ev0, e->ev1);
+    if (st == hipSuccess && n_clusters)
+        st = hipMemcpy(out, d_out, n_clusters * sizeof(mcs_cluster_state), hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    if (st != hipSuccess) return fail(e, MCS_E_HIP, std::string("cluster states: ") + hipGetErrorString(st));
+    if (kernel_ms) *kernel_ms = ms;
+    return MCS_OK;
+}
+
 }  // extern "C"

@@ -76,6 +76,21 @@ struct DelayArgs {
 
 hipError_t launch_delay(const DelayArgs& a, int npl, int pool, hipStream_t s);  // mcs_delay.hip
 
+struct StateArgs {  // the ClusterState reduction over a run's placements (mcs_state.hip)
+    const uint32_t* node_off;
+    const uint2* cap;
+    const uint2* free0;
+    const uint4* jobs;
+    const uint64_t* job_off;
+    const int32_t* out_node;
+    const uint32_t* out_start;
+    const uint32_t* out_finish;
+    mcs_cluster_state* out;
+    uint32_t t;
+    uint32_t n_clusters;
+};
+hipError_t launch_state(const StateArgs& a, uint32_t max_n, hipStream_t s);  // mcs_state.hip
+
 // Launchers (mcs_kernels.hip).  Return hipSuccess or the launch error.
 hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, hipStream_t s);
 bool fifo_variant_exists(int npl, int pool);

@@ -117,6 +117,17 @@ class mcs_cluster_stats(C.Structure):
     ]
 
 
+class mcs_cluster_state(C.Structure):
+    _fields_ = [
+        ("cores_utilization", C.c_float),
+        ("memory_utilization", C.c_float),
+        ("total_cpu", C.c_uint32),
+        ("total_memory", C.c_uint32),
+        ("running", C.c_uint32),
+        ("t_s", C.c_uint32),
+    ]
+
+
 class mcs_delay_cluster_stats(C.Structure):
     _fields_ = [
         ("total_wait_ms", C.c_int64),
@@ -202,6 +213,8 @@ SIGNATURES = [
     ("mcs_lend_check", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32, i32p]),
     ("mcs_read_live_state", C.c_int, [vp, C.c_uint32, u32p, u32p, C.c_uint32]),
     ("mcs_resource_utilization", C.c_int, [vp, C.c_uint32, f32p, f32p]),
+    ("mcs_cluster_states", C.c_int, [vp, C.c_uint32, C.POINTER(mcs_cluster_state), C.c_uint32,
+                                     C.POINTER(C.c_double)]),
     # include/mcs_trade.h
     ("mcs_set_shard", C.c_int, [vp, C.c_uint32, C.c_uint32]),
     ("mcs_comm_unique_id", C.c_int, [C.POINTER(mcs_comm_id)]),

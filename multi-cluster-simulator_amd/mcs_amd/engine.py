@@ -125,6 +125,9 @@ CLUSTER_STATS_DTYPE = np.dtype([("t_end", "<u4"), ("placed", "<u4"), ("waited", 
 DELAY_STATS_DTYPE = np.dtype([("total_wait_ms", "<i8"), ("jobs_count", "<i8"), ("moved_l1", "<u4"),
                               ("placed_l1", "<u4"), ("peak_l1", "<u4"), ("l1_left", "<u4")])
 
+CLUSTER_STATE_DTYPE = np.dtype([("cores_utilization", "<f4"), ("memory_utilization", "<f4"), ("total_cpu", "<u4"),
+                                ("total_memory", "<u4"), ("running", "<u4"), ("t_s", "<u4")])
+
 CONTRACT_DTYPE = np.dtype([("t", "<u4"), ("requester", "<u4"), ("winner", "<i4"), ("approvals", "<u4"),
                            ("policy", "<u4"), ("cores", "<u4"), ("mem", "<u4"), ("time_s", "<u4"), ("failed", "<u4"),
                            ("pad", "<u4")])
@@ -361,6 +364,16 @@ class Engine:
         self._c(L.lib().mcs_read_delay_stats(self._h, out.ctypes.data_as(C.POINTER(L.mcs_delay_cluster_stats)),
                                              n))
         return out
+
+    def cluster_states(self, t_s: int, with_time: bool = False):
+        """ClusterState of every cluster at simulated second t_s, rebuilt on the GPU from the last
+        FIFO/DELAY run (mcs_cluster_states; CLUSTER_STATE_DTYPE).  with_time: also the kernel ms."""
+        n = self.num_clusters
+        out = np.zeros(n, CLUSTER_STATE_DTYPE)
+        ms = C.c_double(0.0)
+        self._c(L.lib().mcs_cluster_states(self._h, int(t_s), out.ctypes.data_as(C.POINTER(L.mcs_cluster_state)),
+                                           n, C.byref(ms)))
+        return (out, ms.value) if with_time else out
 
     # -- single-job mirrors (live state) --------------------------------------------------------
     def schedule_one(self, cluster: int, cores: int, mem: int) -> int:
