@@ -9,7 +9,7 @@ mkdir -p "$ROOT/variants" "$PKG/build/v_$NAME"
 python3 - "$PKG/csrc/mcs_kernels.hip" "$BODY" "$PKG/build/v_$NAME/mcs_kernels.hip" <<'PY'
 import sys
 s = open(sys.argv[1]).read()
-i = s.index('template <int NPL, int P>\n__global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {')
+i = s.index('template <int NPL, int P, bool GEN>\n__global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {')
 j = s.index('// ---- variant table')
 open(sys.argv[3], 'w').write(s[:i] + open(sys.argv[2]).read() + s[j:])
 PY
