@@ -194,7 +194,7 @@ def main_c5_delay(args, world, rank, local_rank):
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": "lock-step tick (dt_step/dt_sample/dt_trader), launch/latency-bound",
+                "kernel": "lock-step tick (dt_step with the sample, dt_trader), launch/latency-bound",
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "bytes_per_placement": BYTES_PER_PLACEMENT,
             },

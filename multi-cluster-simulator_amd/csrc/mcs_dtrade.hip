@@ -1,15 +1,16 @@
 // mcs_dtrade.hip — gfx950 kernels of the lock-step trading system with DELAY schedulers
 // (semantics restated in oracle/mcs_oracle_dtrade.c, header of mcs_dtrade_internal.h).
 //
-// One tick T is three launches on the engine stream (each a grid-wide barrier), replayed from a
+// One tick T is two launches on the engine stream (each a grid-wide barrier), replayed from a
 // captured hipGraph 64 ticks at a time:
 //   A dt_step_kernel    one wave per cluster: one Delay iteration (pkg/scheduler/scheduler.go:
 //                       298-369): releases, "/delay" arrivals, the Level1 pass with its skip (D6)
 //                       through an exact fit filter, the Level0 head and its MaxWaitTime move,
-//                       and the WaitTime statistics (scheduler.go:309-312,338-341)
-//   C dt_sample_kernel  one wave per cluster at T % 5 == 0: GetResourceUtilization over physical
-//                       and virtual nodes (cluster.go:46-63, float32 in node order) and
-//                       WaitTime.GetAverage (scheduler.go:56-63)
+//                       and the WaitTime statistics (scheduler.go:309-312,338-341); then phase C,
+//                       the state sample at T % 5 == 0, on the same wave (it reads only its own
+//                       cluster): GetResourceUtilization over physical and virtual nodes
+//                       (cluster.go:46-63, float32 in node order) and WaitTime.GetAverage
+//                       (scheduler.go:56-63)
 //   D dt_trader_kernel  one wave for the system: trader rounds in cluster order
 //                       (trader.go:280-325): contract sizing over the requester's Level1
 //                       (scheduler_client.go:126-289), RequestResource/ApproveTrade with locks
@@ -410,46 +411,32 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             a.vn[(size_t)c * a.V + (i - N)] = nodes[i];
     }
     for (uint32_t s = lane; s < S; s += kWave) a.sfin[sb + s] = sfin[s];
+    // ---- phase C: the state stream sample (trader_server.go:24-47) every sample_period seconds ----
+    if (T % a.sample_period == 0u) {
+        __syncthreads();  // sfin's LDS is reused for the per-node differences
+        float* dc = reinterpret_cast<float*>(sfin);
+        float* dm = dc + (kDtMaxNodes + kDtMaxVnodes);
+        for (uint32_t i = lane; i < NN; i += kWave) {
+            const unsigned long long v = nodes[i];
+            const uint2 cp = i < N ? a.cap[n0 + i] : a.vcap[(size_t)c * a.V + (i - N)];
+            // float32(node.Cores) - float32(node.CoresAvailable) (cluster.go:55-56), uint64 -> float32
+            dc[i] = __fsub_rn((float)cp.x, go_f32((uint32_t)v));
+            dm[i] = __fsub_rn((float)cp.y, go_f32((uint32_t)(v >> 32)));
+        }
+        __syncthreads();
+        if (lane == 0) {
+            float sc = 0.0f, sm = 0.0f;
+            for (uint32_t i = 0; i < NN; ++i) {  // node order, float32 like Go
+                sc = __fadd_rn(sc, dc[i]);
+                sm = __fadd_rn(sm, dm[i]);
+            }
+            st.cu = __fdiv_rn(sc, (float)st.total_c);
+            st.mu = __fdiv_rn(sm, (float)st.total_m);
+            // WaitTime.GetAverage (scheduler.go:56-63)
+            st.avgw = st.count != 0 ? __ddiv_rn((double)st.total, (double)st.count) : 0.0;
+        }
+    }
     if (lane == 0) a.cl[c] = st;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Phase C: the state stream sample (trader_server.go:24-47) every sample_period seconds.
-__global__ __launch_bounds__(64) void dt_sample_kernel(DtArgs a) {
-    __shared__ float dc[kDtMaxNodes + kDtMaxVnodes], dm[kDtMaxNodes + kDtMaxVnodes];
-    if (a.ctl->done) return;
-    const uint32_t T = a.ctl->T;
-    if (T % a.sample_period != 0u) return;
-    const uint32_t c = blockIdx.x, lane = threadIdx.x;
-    const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
-    DtCluster st = a.cl[c];
-    const uint32_t NN = N + st.nv;
-    for (uint32_t i = lane; i < NN; i += kWave) {
-        unsigned long long v;
-        uint2 cp;
-        if (i < N) {
-            v = a.tn[n0 + i];
-            cp = a.cap[n0 + i];
-        } else {
-            v = a.vn[(size_t)c * a.V + (i - N)];
-            cp = a.vcap[(size_t)c * a.V + (i - N)];
-        }
-        // float32(node.Cores) - float32(node.CoresAvailable) (cluster.go:55-56), uint64 -> float32
-        dc[i] = __fsub_rn((float)cp.x, go_f32((uint32_t)v));
-        dm[i] = __fsub_rn((float)cp.y, go_f32((uint32_t)(v >> 32)));
-    }
-    __syncthreads();
-    if (lane == 0) {
-        float sc = 0.0f, sm = 0.0f;
-        for (uint32_t i = 0; i < NN; ++i) {  // node order, float32 like Go
-            sc = __fadd_rn(sc, dc[i]);
-            sm = __fadd_rn(sm, dm[i]);
-        }
-        a.cl[c].cu = __fdiv_rn(sc, (float)st.total_c);
-        a.cl[c].mu = __fdiv_rn(sm, (float)st.total_m);
-        // WaitTime.GetAverage (scheduler.go:56-63)
-        a.cl[c].avgw = st.count != 0 ? __ddiv_rn((double)st.total, (double)st.count) : 0.0;
-    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -770,9 +757,6 @@ hipError_t launch_dtrade_init(const DtArgs& a, hipStream_t s) {
 hipError_t launch_dtrade_tick(const DtArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(dt_step_kernel, dim3(a.C), dim3(kWave), 0, s, a);
     hipError_t st = hipGetLastError();
-    if (st != hipSuccess) return st;
-    hipLaunchKernelGGL(dt_sample_kernel, dim3(a.C), dim3(kWave), 0, s, a);
-    st = hipGetLastError();
     if (st != hipSuccess) return st;
     hipLaunchKernelGGL(dt_trader_kernel, dim3(1), dim3(kWave), 0, s, a);
     return hipGetLastError();
