@@ -254,7 +254,10 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         uint32_t wr = 0;
         bool carry_skip = false;  // the last entry of the previous row was placed
         const uint32_t n1 = st.l1n, t_all = st.t_all;
-        unsigned long long s_new = 0ull;
+        // per-lane partial sums of the JobsMap moves and of the kept entries' last examinations,
+        // reduced once after the sweep (a wave reduction per row would serialise the pass)
+        long long tot_l = 0ll;
+        unsigned long long snew_l = 0ull;
         // rows of 64 entries, each row's three coalesced loads issued one row ahead
         unsigned long long ncm = 0, njd = 0, nal = 0;
         if (lane < n1) {
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             const uint32_t sl = (uint32_t)(al >> 32);
             const uint32_t eff = sl > t_all ? sl : t_all;
             const long long delta = examined ? (long long)(T - eff) * 1000ll : 0ll;
-            st.total += dt_wave_sum_i64(delta);
+            tot_l += delta;
             // compaction in the same sweep (append(Level1[:i], Level1[i+1:]...), :319)
             const unsigned long long kept = livem & ~placedm;
             const uint32_t nl = examined ? T : eff;  // the kept entry's last examination
@@ -358,11 +361,12 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
                 }
                 if (np != pos || nl != sl) l1al[np] = (al & 0xFFFFFFFFull) | ((unsigned long long)nl << 32);
             }
-            s_new += (unsigned long long)dt_wave_sum_i64(live && !placed ? (long long)nl : 0ll);
+            snew_l += live && !placed ? (unsigned long long)nl : 0ull;
             wr += (uint32_t)__builtin_popcountll(kept);
         }
         st.l1n = wr;
-        st.s_last = s_new;
+        st.total += dt_wave_sum_i64(tot_l);
+        st.s_last = (unsigned long long)dt_wave_sum_i64((long long)snew_l);
         st.l1_dirty = wr != n1 ? 1u : 0u;  // a pass that placed: its skipped entries come next
     }
 
