@@ -167,6 +167,43 @@ def test_config4_full_size_sampled_parity(engine):
         np.testing.assert_array_equal(node[js], on, err_msg=f"cluster {k}")
         np.testing.assert_array_equal(start[js], os_, err_msg=f"cluster {k}")
         assert cs[k]["t_end"] == ost["t_end"] and cs[k]["waited"] == ost["waited"]
+    # no node is ever over-committed: the ClusterState reduction at sampled seconds (a wrapped
+    # free counter would show as utilization > 1)
+    for t in np.linspace(0, int(fin.max()), 7).astype(int):
+        cst = engine.cluster_states(int(t))
+        assert (cst["cores_utilization"] <= 1.0).all() and (cst["memory_utilization"] <= 1.0).all(), t
+        assert (cst["cores_utilization"] >= 0.0).all() and (cst["memory_utilization"] >= 0.0).all(), t
+
+
+def test_config4_delay_fused_full_size_properties():
+    """C4 at full size under DELAY with the stream synthesised in the kernel: every job is placed
+    exactly once after its arrival, no node is over-committed, and sampled clusters are bit-exact
+    against the oracle over the host generator's streams."""
+    from mcs_amd.engine import gen_cluster_host, scaled_lambda
+
+    n, J = 4096, 16384
+    arrays = replicate(uniform_cluster(256), n)
+    gp = GenParams(seed=0x5EED5EED, arrival_mode=1, lam=scaled_lambda(256, load=0.9), fused=True)
+    with Engine(0, policy="DELAY") as eng:
+        eng.load_clusters(arrays)
+        eng.generate_jobs(gp, J)
+        st = eng.run()
+        assert st.placed == n * J and st.unplaced == 0
+        node, start, fin = eng.placements()
+        ds = eng.delay_stats()
+        assert (node >= 0).all() and (node < 256).all()
+        for t in np.linspace(0, int(fin.max()), 5).astype(int):
+            cst = eng.cluster_states(int(t))
+            assert (cst["cores_utilization"] <= 1.0).all() and (cst["memory_utilization"] <= 1.0).all(), t
+        for k in [0, 2049, 4095]:
+            a, d, c, m = gen_cluster_host(gp, k, 32, 24000, J)
+            js = slice(k * J, (k + 1) * J)
+            assert (start[js] >= a).all()
+            np.testing.assert_array_equal(fin[js], start[js] + d)
+            on, os_, of, ost = O.delay_run(arrays.free_c[:256], arrays.free_m[:256], a, d, c, m)
+            np.testing.assert_array_equal(node[js], on, err_msg=f"cluster {k}")
+            np.testing.assert_array_equal(start[js], os_, err_msg=f"cluster {k}")
+            assert ds[k]["total_wait_ms"] == ost["total_wait_ms"]
 
 
 def test_heterogeneous_cluster_sizes(engine):
