@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--jobs-per-cluster", type=int, default=16384)
     ap.add_argument("--load", type=float, default=0.9, help="offered memory load of the scaled arrivals")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x4D43535F53494D31)
-    ap.add_argument("--cpu-sample-clusters", type=int, default=512)
+    ap.add_argument("--cpu-sample-clusters", type=int, default=2048,
+                    help="C4 CPU baseline sample: that many clusters with full streams (~20 thread-s of oracle work)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None,
@@ -65,14 +66,14 @@ def parse():
             a.clusters = 64
         if a.jobs_per_cluster == 16384:
             a.jobs_per_cluster = 2000
-        if a.cpu_sample_clusters == 512:
+        if a.cpu_sample_clusters == 2048:
             a.cpu_sample_clusters = 16
     elif a.config == "c5":  # BASELINE.json configs[4]: 64 trading clusters, 10M jobs
         if a.clusters == 4096:
             a.clusters = 64
         if a.jobs_per_cluster == 16384:
             a.jobs_per_cluster = 156250
-        if a.cpu_sample_clusters == 512:
+        if a.cpu_sample_clusters == 2048:
             a.cpu_sample_clusters = 64
     return a
 
