@@ -2,6 +2,7 @@
 alternating variants round-robin so box-to-box and thermal drift cancel.
 
 usage: python tools/ab_bench.py lib_a.so lib_b.so [...] [--rounds 3] [--steps 5]
+(env AB_POLICY=FIFO|DELAY, AB_NODES, AB_LOAD select the workload; default C4 FIFO)
 Each variant runs in its own subprocess (MCS_LIB=<path>) per round; prints median kernel ms."""
 import json
 import os
@@ -17,9 +18,10 @@ sys.path.insert(0, os.path.join(os.environ["REPO"], "multi-cluster-simulator_amd
 from mcs_amd import Engine, GenParams, replicate, uniform_cluster
 from mcs_amd.engine import scaled_lambda
 steps = int(os.environ["STEPS"])
-eng = Engine(0)
-eng.load_clusters(replicate(uniform_cluster(256), 4096))
-eng.generate_jobs(GenParams(arrival_mode=1, lam=scaled_lambda(256, load=0.9)), 16384)
+nn, load = int(os.environ.get("AB_NODES", "256")), float(os.environ.get("AB_LOAD", "0.9"))
+eng = Engine(0, policy=os.environ.get("AB_POLICY", "FIFO"))
+eng.load_clusters(replicate(uniform_cluster(nn), 4096))
+eng.generate_jobs(GenParams(arrival_mode=1, lam=scaled_lambda(nn, load=load)), 16384)
 eng.run()
 ms = [eng.run().kernel_ms for _ in range(steps)]
 print(json.dumps({"ms": ms}))
