@@ -18,10 +18,13 @@
  * exchange, state samples, trader rounds), bit-identical to oracle/mcs_oracle_trade.c.  With
  * MCS_POLICY_DELAY the schedulers run Scheduler.Delay and the traders size real contracts from
  * Level1 (oracle/mcs_oracle_dtrade.c): Foreign jobs on responders, virtual nodes
- * with capacity on requesters.  DELAY trading runs on one engine (world == 1).
+ * with capacity on requesters.  DELAY trading shards too: its tick exchanges one block per rank
+ * (per-cluster records + node snapshots) and runs the trader rounds replicated on every rank.
  *
  * Sharding: the clusters are split in equal contiguous blocks over `world` engines (one per GPU,
- * usually one process each).  Every tick needs three all-gathers of small fixed-size records.
+ * usually one process each).  Every FIFO tick needs three all-gathers of small fixed-size records;
+ * a DELAY tick needs one (phase 0 -> 1; phases 2 and 3 move no bytes), and every rank must hold
+ * the same number of clusters and the same largest cluster (the block layout).
  * Two transports:
  *   - RCCL (mcs_comm_unique_id on rank 0, shared out of band, then mcs_comm_init on every rank):
  *     mcs_run drives the whole lock-step loop with ncclAllGather over xGMI;
@@ -127,12 +130,13 @@ int mcs_read_trades(mcs_engine* eng, mcs_trade_rec* out, uint64_t cap, uint64_t*
  * zero-capacity under FIFO, the contract's capacity under DELAY. */
 int mcs_read_virtual_nodes(mcs_engine* eng, uint32_t* out, uint32_t n_total);
 
-/* ---- DELAY trading (MCS_POLICY_DELAY with cfg.trader; one engine holds the system) ---------- */
-/* Trader rounds with their contracts, in (t_s, requester) order; *n = total count. */
+/* ---- DELAY trading (MCS_POLICY_DELAY with cfg.trader) ----------------------------------------- */
+/* Trader rounds of ALL clusters with their contracts, in (t_s, requester) order, identical on
+ * every rank; *n = total count. */
 int mcs_read_contracts(mcs_engine* eng, mcs_contract_rec* out, uint64_t cap, uint64_t* n);
-/* Foreign jobs in launch order; *n = total count. */
+/* Foreign jobs of ALL clusters in launch order (global indices, identical on every rank). */
 int mcs_read_foreign(mcs_engine* eng, mcs_foreign_rec* out, uint64_t cap, uint64_t* n);
-/* Capacities {cores, memory} of the virtual nodes cluster `cluster` received, in order (node
+/* Capacities {cores, memory} of the virtual nodes local cluster `cluster` received, in order (node
  * index n_physical + i); *n = their count. */
 int mcs_read_virtual_node_caps(mcs_engine* eng, uint32_t cluster, uint32_t* cores, uint32_t* mem,
                                uint32_t cap, uint32_t* n);

@@ -1,8 +1,10 @@
 // mcs_dtrade.cpp — host side of the lock-step trading system with DELAY schedulers (DESIGN.md
-// §11): device state, the tick loop (three kernels per tick, 64 ticks per captured hipGraph,
-// one host poll per replay), capacity escalation and the result readers of mcs_trade.h.
-// Every decision is made by the gfx950 kernels of mcs_dtrade.hip; there is no CPU path.
+// §11): device state, the tick loop (two kernels per tick; world 1: 64 ticks per captured
+// hipGraph, one host poll per replay; world > 1: an ncclAllGather of the exchange blocks between
+// the kernels, or the caller-driven phases), capacity escalation and the result readers of
+// mcs_trade.h.  Every decision is made by the gfx950 kernels of mcs_dtrade.hip; there is no CPU path.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -32,8 +34,12 @@ struct DtradeDev {
     DtCtl* ctl = nullptr;
     mcs_contract_rec* trades = nullptr;
     mcs_foreign_rec* foreign = nullptr;
+    unsigned char* xb = nullptr;  // world exchange blocks
+    uint32_t* nv_all = nullptr;
     DtCtl* h_ctl = nullptr;
     hipGraphExec_t graph = nullptr;
+    bool begun = false;  // caller-driven lock-step in progress
+    std::chrono::steady_clock::time_point w0{};
 };
 
 namespace {
@@ -52,12 +58,14 @@ uint32_t dt_auto_slots(uint32_t max_n) {
 
 int dtrade_alloc(mcs_engine* e) {
     if (e->dtd) return MCS_OK;
-    const uint32_t C = e->C;
-    if (C > kDtMaxClusters) return fail(e, MCS_E_INVALID, "more than 1024 clusters in a trading system");
+    const uint32_t C = e->C, Ct = e->C * e->world;
+    if (Ct > kDtMaxClusters) return fail(e, MCS_E_INVALID, "more than 1024 clusters in a trading system");
     if (e->max_n > kDtMaxNodes) return fail(e, MCS_E_INVALID, "more than 1024 nodes in a cluster");
     const uint32_t S = e->cfg.slot_pool ? 64u * e->cfg.slot_pool : (e->tr_slots ? e->tr_slots : dt_auto_slots(e->max_n));
     if (S > kDtMaxSlots) return fail(e, MCS_E_INVALID, "slot pool above 4096");
     const uint32_t V = e->dt_vnodes ? e->dt_vnodes : 64u;
+    const uint32_t NS = std::max<uint32_t>(e->dt_ns ? e->dt_ns : e->max_n, 1u), W = NS + V;
+    const unsigned long long blk = (unsigned long long)C * sizeof(DtRec) + (unsigned long long)C * W * 8ull;
     DtradeDev* d = new (std::nothrow) DtradeDev();
     if (!d) return fail(e, MCS_E_NOMEM, "DELAY trading state");
     e->dtd = d;
@@ -73,7 +81,10 @@ int dtrade_alloc(mcs_engine* e) {
     HIPCHK(e, hipMalloc(&d->l1jd, nj * 8));
     HIPCHK(e, hipMalloc(&d->l1al, nj * 8));
     HIPCHK(e, hipMalloc(&d->cl, C * sizeof(DtCluster)));
-    HIPCHK(e, hipMalloc(&d->tr, C * sizeof(DtTrader)));
+    HIPCHK(e, hipMalloc(&d->tr, Ct * sizeof(DtTrader)));
+    HIPCHK(e, hipMalloc(&d->xb, std::max<unsigned long long>(blk * e->world, 8ull)));
+    HIPCHK(e, hipMemset(d->xb, 0, blk * e->world));
+    HIPCHK(e, hipMalloc(&d->nv_all, Ct * 4));
     HIPCHK(e, hipMalloc(&d->ctl, sizeof(DtCtl)));
     HIPCHK(e, hipMalloc(&d->trades, trade_cap * sizeof(mcs_contract_rec)));
     HIPCHK(e, hipMalloc(&d->foreign, foreign_cap * sizeof(mcs_foreign_rec)));
@@ -82,6 +93,14 @@ int dtrade_alloc(mcs_engine* e) {
     a.C = C;
     a.V = V;
     a.S = S;
+    a.base = e->rank * C;
+    a.Ct = Ct;
+    a.NS = NS;
+    a.W = W;
+    a.rank = e->rank;
+    a.blk = blk;
+    a.xb = d->xb;
+    a.nv_all = d->nv_all;
     a.period = e->cfg.trader_period_s;
     a.ok_sleep = e->cfg.trade_ok_sleep_s;
     a.fail_sleep = e->cfg.trade_fail_sleep_s;
@@ -156,6 +175,56 @@ int dt_run_once(mcs_engine* e, double* kernel_ms) {
     return MCS_OK;
 }
 
+// N engines (one per GPU): the exchange blocks are all-gathered in place over xGMI between the two
+// kernels of every tick; one host poll per kDtGraphTicks ticks (the kernels of finished ticks
+// return at once on ctl->done, identically on every rank)
+int dt_run_rccl(mcs_engine* e, double* kernel_ms) {
+    DtradeDev* d = e->dtd;
+    ncclComm_t comm = (ncclComm_t)e->comm;
+    hipError_t st = launch_dtrade_init(d->a, e->stream);
+    if (st != hipSuccess) return dt_hip_fail(e, "DELAY trading init", st);
+    HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+    for (;;) {
+        for (uint32_t t = 0; t < kDtGraphTicks; ++t) {
+            st = launch_dtrade_step(d->a, e->stream);
+            if (st != hipSuccess) return dt_hip_fail(e, "dt_step_kernel", st);
+            const ncclResult_t r = ncclAllGather(d->xb + (size_t)e->rank * d->a.blk, d->xb, d->a.blk, ncclUint8,
+                                                 comm, e->stream);
+            if (r != ncclSuccess)
+                return fail(e, MCS_E_RCCL, std::string("ncclAllGather(exchange blocks): ") + ncclGetErrorString(r));
+            st = launch_dtrade_trader(d->a, e->stream);
+            if (st != hipSuccess) return dt_hip_fail(e, "dt_trader_kernel", st);
+        }
+        if (int s = dt_poll(e)) return s;
+        if (d->h_ctl->done) break;
+    }
+    HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    float ms = 0.0f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+    *kernel_ms = ms;
+    return MCS_OK;
+}
+
+// every rank must lay its exchange block out alike: the snapshot stride is the largest cluster of
+// the whole system, and the cluster count per rank must match
+int dt_agree_shape(mcs_engine* e) {
+    uint32_t* buf = nullptr;
+    HIPCHK(e, hipMalloc(&buf, 2 * sizeof(uint32_t)));
+    const uint32_t h[2] = {e->max_n, e->C};
+    uint32_t mx[2] = {0, 0};
+    HIPCHK(e, hipMemcpy(buf, h, sizeof(h), hipMemcpyHostToDevice));
+    ncclResult_t r = ncclAllReduce(buf, buf, 2, ncclUint32, ncclMax, (ncclComm_t)e->comm, e->stream);
+    hipError_t st = hipStreamSynchronize(e->stream);
+    if (r == ncclSuccess && st == hipSuccess) st = hipMemcpy(mx, buf, sizeof(mx), hipMemcpyDeviceToHost);
+    (void)hipFree(buf);
+    if (r != ncclSuccess) return fail(e, MCS_E_RCCL, std::string("ncclAllReduce(shape): ") + ncclGetErrorString(r));
+    if (st != hipSuccess) return dt_hip_fail(e, "shape exchange", st);
+    if (mx[1] != e->C) return fail(e, MCS_E_INVALID, "sharded DELAY trading needs the same cluster count on every rank");
+    e->dt_ns = mx[0];
+    return MCS_OK;
+}
+
 int dt_clusters(mcs_engine* e, std::vector<DtCluster>& cl) {
     cl.resize(e->C);
     HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -185,6 +254,8 @@ void dtrade_free(mcs_engine* e) {
     dfree(d->ctl);
     dfree(d->trades);
     dfree(d->foreign);
+    dfree(d->xb);
+    dfree(d->nv_all);
     if (d->h_ctl) (void)hipHostFree(d->h_ctl);
     delete d;
     e->dtd = nullptr;
@@ -192,22 +263,29 @@ void dtrade_free(mcs_engine* e) {
 }
 
 int dtrade_run(mcs_engine* e, mcs_stats* stats) {
-    if (e->world > 1)
-        return fail(e, MCS_E_INVALID, "DELAY trading runs on one engine holding the whole system (world 1)");
+    if (e->world > 1 && !e->comm)
+        return fail(e, MCS_E_STATE, "sharded DELAY trading run needs mcs_comm_init (or mcs_trade_phase)");
     const auto w0 = std::chrono::steady_clock::now();
     e->tr_slots = 0;
     e->dt_vnodes = 0;
+    // a communicator selects the RCCL loop (world 1 included: one rank's all-gather is a copy)
+    const bool rccl = e->comm != nullptr;
+    if (rccl) {
+        dtrade_free(e);
+        if (int s = dt_agree_shape(e)) return s;
+    } else {
+        e->dt_ns = 0;
+    }
     uint32_t escalations = 0;
     double kms = 0.0;
     for (;;) {
         if (int s = dtrade_alloc(e)) return s;
         double ms = 0.0;
-        if (int s = dt_run_once(e, &ms)) return s;
+        if (int s = rccl ? dt_run_rccl(e, &ms) : dt_run_once(e, &ms)) return s;
         kms += ms;
-        std::vector<DtCluster> cl;
-        if (int s = dt_clusters(e, cl)) return s;
-        uint32_t flags = e->dtd->h_ctl->flags;
-        for (const auto& k : cl) flags |= k.flags;
+        if (int s = dt_poll(e)) return s;
+        // ctl->flags is replicated (it ORs every cluster's record), so every rank escalates alike
+        const uint32_t flags = e->dtd->h_ctl->flags;
         const uint32_t S = e->dtd->a.S, V = e->dtd->a.V;
         bool grow_s = (flags & MCS_FLAG_OVERFLOW) != 0, grow_v = (flags & MCS_FLAG_VNODE_OVERFLOW) != 0;
         if (!grow_s && !grow_v) break;
@@ -240,6 +318,101 @@ int dtrade_run(mcs_engine* e, mcs_stats* stats) {
         st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
         *stats = st;
     }
+    return MCS_OK;
+}
+
+// ---- caller-driven lock-step (mcs_trade_begin/xfer_bytes/phase/end with MCS_POLICY_DELAY) ----
+// A tick is phase 0 (dt_step_kernel; out = this rank's exchange block) and phase 1 (in = every
+// rank's block in rank order; dt_trader_kernel).  Phases 2 and 3 move no bytes; phase 3 reports
+// done.  Every rank must hold the same cluster count and the same largest cluster (block layout).
+int dtrade_begin(mcs_engine* e) {
+    if (int s = dtrade_alloc(e)) return s;
+    DtradeDev* d = e->dtd;
+    d->w0 = std::chrono::steady_clock::now();
+    const hipError_t st = launch_dtrade_init(d->a, e->stream);
+    if (st != hipSuccess) return dt_hip_fail(e, "DELAY trading init", st);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+    d->begun = true;
+    e->has_run = false;
+    e->dtrade_run = false;
+    return MCS_OK;
+}
+
+int dtrade_xfer_bytes(mcs_engine* e, uint32_t phase, uint64_t* in_bytes, uint64_t* out_bytes) {
+    if (int s = dtrade_alloc(e)) return s;
+    const uint64_t blk = e->dtd->a.blk;
+    switch (phase) {
+        case 0: *in_bytes = 0; *out_bytes = blk; break;
+        case 1: *in_bytes = blk * e->world; *out_bytes = 0; break;
+        default: *in_bytes = 0; *out_bytes = 0; break;
+    }
+    return MCS_OK;
+}
+
+int dtrade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_bytes, void* out,
+                 uint64_t out_bytes, uint32_t* done) {
+    DtradeDev* d = e->dtd;
+    if (!d || !d->begun) return fail(e, MCS_E_STATE, "mcs_trade_begin first");
+    uint64_t ib = 0, ob = 0;
+    if (int s = dtrade_xfer_bytes(e, phase, &ib, &ob)) return s;
+    if (in_bytes != ib || out_bytes != ob || (ib && !in) || (ob && !out))
+        return fail(e, MCS_E_INVALID, "exchange buffer sizes do not match mcs_trade_xfer_bytes");
+    hipError_t st = hipSuccess;
+    switch (phase) {
+        case 0:
+            st = launch_dtrade_step(d->a, e->stream);
+            if (st != hipSuccess) return dt_hip_fail(e, "dt_step_kernel", st);
+            HIPCHK(e, hipMemcpyAsync(out, d->xb + (size_t)e->rank * d->a.blk, ob, hipMemcpyDeviceToHost, e->stream));
+            break;
+        case 1:
+            HIPCHK(e, hipMemcpyAsync(d->xb, in, ib, hipMemcpyHostToDevice, e->stream));
+            st = launch_dtrade_trader(d->a, e->stream);
+            if (st != hipSuccess) return dt_hip_fail(e, "dt_trader_kernel", st);
+            HIPCHK(e, hipMemcpyAsync(d->h_ctl, d->ctl, sizeof(DtCtl), hipMemcpyDeviceToHost, e->stream));
+            break;
+        default:
+            break;
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (done) *done = phase == 3 ? d->h_ctl->done : 0u;
+    return MCS_OK;
+}
+
+int dtrade_end(mcs_engine* e, mcs_stats* stats) {
+    DtradeDev* d = e->dtd;
+    if (!d || !d->begun) return fail(e, MCS_E_STATE, "mcs_trade_begin first");
+    HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    d->begun = false;
+    e->has_run = true;
+    e->dtrade_run = true;
+    e->trade_run = false;
+    e->delay_run = true;
+    if (int s = dt_poll(e)) return s;
+    const uint32_t flags = d->h_ctl->flags;
+    if (stats) {
+        std::vector<DtCluster> cl;
+        if (int s = dt_clusters(e, cl)) return s;
+        mcs_stats st{};
+        st.jobs = e->total_jobs;
+        for (uint32_t k = 0; k < e->C; ++k) {
+            st.placed += cl[k].decided;
+            st.waited += cl[k].moved;
+        }
+        st.unplaced = e->total_jobs - st.placed;
+        st.clusters = e->C;
+        st.slot_pool = d->a.S / 64u;
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) ms = 0.0f;
+        st.kernel_ms = ms;
+        st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d->w0).count();
+        *stats = st;
+    }
+    if (flags & MCS_FLAG_OVERFLOW)
+        return fail(e, MCS_E_CAPACITY, "running-slot pool overflow (raise mcs_config.slot_pool)");
+    if (flags & MCS_FLAG_VNODE_OVERFLOW)
+        return fail(e, MCS_E_CAPACITY, "virtual-node capacity overflow");
     return MCS_OK;
 }
 
@@ -318,9 +491,8 @@ int dtrade_read_trades(mcs_engine* e, mcs_trade_rec* out, uint64_t cap, uint64_t
 }
 
 int dtrade_read_vnode_counts(mcs_engine* e, uint32_t* out, uint32_t n) {
-    std::vector<DtCluster> cl;
-    if (int s = dt_clusters(e, cl)) return s;
-    for (uint32_t k = 0; k < n; ++k) out[k] = cl[k].nv;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (n) HIPCHK(e, hipMemcpy(out, e->dtd->nv_all, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return MCS_OK;
 }
 

@@ -1,23 +1,26 @@
 // mcs_dtrade.hip — gfx950 kernels of the lock-step trading system with DELAY schedulers
 // (semantics restated in oracle/mcs_oracle_dtrade.c, header of mcs_dtrade_internal.h).
 //
-// One tick T is two launches on the engine stream (each a grid-wide barrier), replayed from a
-// captured hipGraph 64 ticks at a time:
-//   A dt_step_kernel    one wave per cluster: one Delay iteration (pkg/scheduler/scheduler.go:
+// One tick T is two launches on the engine stream (each a grid-wide barrier); with world 1 they are
+// replayed from a captured hipGraph 64 ticks at a time, with world > 1 an all-gather of the
+// exchange blocks (RCCL over xGMI, or the caller's transport) sits between them:
+//   A dt_step_kernel    one wave per local cluster: one Delay iteration (pkg/scheduler/scheduler.go:
 //                       298-369): releases, "/delay" arrivals, the Level1 pass with its skip (D6)
 //                       through an exact fit filter, the Level0 head and its MaxWaitTime move,
 //                       and the WaitTime statistics (scheduler.go:309-312,338-341); then phase C,
 //                       the state sample at T % 5 == 0, on the same wave (it reads only its own
 //                       cluster): GetResourceUtilization over physical and virtual nodes
 //                       (cluster.go:46-63, float32 in node order) and WaitTime.GetAverage
-//                       (scheduler.go:56-63)
-//   D dt_trader_kernel  one wave for the system: trader rounds in cluster order
-//                       (trader.go:280-325): contract sizing over the requester's Level1
-//                       (scheduler_client.go:126-289), RequestResource/ApproveTrade with locks
+//                       (scheduler.go:56-63); then the cluster's exchange record (DtRec) and, when
+//                       a trader round is due, its node snapshot and the contract sizes over its
+//                       Level1 (scheduler_client.go:126-289)
+//   D dt_trader_kernel  one wave for the whole system, replicated on every rank: trader rounds in
+//                       cluster order (trader.go:280-325), RequestResource/ApproveTrade with locks
 //                       across lanes (pkg/trader/server.go:31-61, trader.go:141-167), heap order,
-//                       ApproveContract -> AllocateVirtualNodeResources on the responder
-//                       (Foreign jobs into its running slots, cluster.go:87-125) and
-//                       AddVirtualNode on the requester (cluster.go:65-85); then the next tick.
+//                       ApproveContract -> AllocateVirtualNodeResources on the responder's snapshot
+//                       (Foreign jobs, cluster.go:87-125; the owner rank also commits them to its
+//                       live nodes and running slots) and AddVirtualNode on the requester
+//                       (cluster.go:65-85); then the next tick.
 // Per-cluster state a wave writes and re-reads inside a kernel is staged in LDS, or read back with
 // sc1 loads (L2) after an atomic write, never through this CU's non-coherent vector L1.
 #include "mcs_dtrade_internal.h"
@@ -71,6 +74,17 @@ __device__ __forceinline__ unsigned long long ld64(const unsigned long long* p) 
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// rank block of global cluster g: its exchange record and node snapshot
+__device__ __forceinline__ const DtRec* dt_rec(const DtArgs& a, uint32_t g) {
+    const uint32_t r = g / a.C, c = g - r * a.C;
+    return reinterpret_cast<const DtRec*>(a.xb + (size_t)r * a.blk) + c;
+}
+__device__ __forceinline__ unsigned long long* dt_snap(const DtArgs& a, uint32_t g) {
+    const uint32_t r = g / a.C, c = g - r * a.C;
+    return reinterpret_cast<unsigned long long*>(a.xb + (size_t)r * a.blk + (size_t)a.C * sizeof(DtRec)) +
+           (size_t)c * a.W;
+}
+
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void dt_init_kernel(DtArgs a) {
     const uint32_t c = blockIdx.x, lane = threadIdx.x;
@@ -99,12 +113,17 @@ __global__ __launch_bounds__(64) void dt_init_kernel(DtArgs a) {
         z.total_c = sc;
         z.total_m = sm;
         a.cl[c] = z;
+    }
+    // the replicated trader state of every cluster of the system: block c takes c, c + C, ...
+    for (uint32_t g = c + lane * a.C; g < a.Ct; g += kWave * a.C) {
         DtTrader t{};
         t.next_id = 1u;  // s.id = rand.Uint32() (pkg/trader/server.go:26), seeded: 1
-        a.tr[c] = t;
+        a.tr[g] = t;
+        a.nv_all[g] = 0u;
     }
     if (c == 0 && lane == 0) {
         DtCtl z{};
+        z.any_due = 1u;
         *a.ctl = z;
     }
 }
@@ -441,6 +460,75 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         }
     }
     if (lane == 0) a.cl[c] = st;
+
+    // ---- this cluster's exchange record and, when a trader round is due at T, its node
+    // snapshot and both contract sizes over GetLevel1() (ProvideJobs, trader_server.go:69-94) ----
+    const uint32_t g = a.base + c;
+    unsigned char* blk = a.xb + (size_t)a.rank * a.blk;
+    unsigned long long* snap =
+        reinterpret_cast<unsigned long long*>(blk + (size_t)a.C * sizeof(DtRec)) + (size_t)c * a.W;
+    const bool any_due = a.period != 0u && a.ctl->any_due != 0u;
+    if (any_due)
+        for (uint32_t i = lane; i < NN; i += kWave) snap[i < N ? i : a.NS + (i - N)] = nodes[i];
+    uint32_t fsc = 0, fsm = 0, fmd = 0, ssc = 0, ssm = 0, sst = 0;
+    if (any_due && a.tr[g].next_due <= T) {
+        // Level1 rows were compacted by other lanes in this kernel: read them back through L2
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        const uint32_t ln = st.l1n;
+        for (uint32_t i = lane; i < ln; i += kWave) {
+            const unsigned long long cm = ld64(&l1cm[i]);
+            const uint32_t jc = (uint32_t)cm, jm = (uint32_t)(cm >> 32);
+            const uint32_t d = (uint32_t)(ld64(&l1jd[i]) >> 32);
+            fsc += jc;  // fast node: uint32 sums and the longest duration (:138-155)
+            fsm += jm;
+            fmd = d > fmd ? d : fmd;
+            ssc += (int32_t)(0u - jc) < 0 ? jc : 0u;  // small node: int32 arithmetic (:232-259)
+            ssm += (int32_t)(0u - jm) < 0 ? jm : 0u;
+        }
+        fsc = dt_wave_sum_u32(fsc);
+        fsm = dt_wave_sum_u32(fsm);
+        fmd = dt_wave_max_u32(fmd);
+        ssc = dt_wave_sum_u32(ssc);
+        ssm = dt_wave_sum_u32(ssm);
+        // small node contract.Time per job: endTime if the previous time < endTime, else 0
+        // (:263-265); a padded last batch (len % 20 != 0) ends with zero jobs -> 0.  Durations are
+        // staged 64 at a time in LDS, then scanned by one lane.
+        if (ln % 20u == 0u) {
+            for (uint32_t b = 0; b < ln; b += kWave) {
+                __syncthreads();
+                if (b + lane < ln) hist[lane] = (uint32_t)(ld64(&l1jd[b + lane]) >> 32);
+                __syncthreads();
+                if (lane == 0) {
+                    const uint32_t m = ln - b < (uint32_t)kWave ? ln - b : (uint32_t)kWave;
+                    for (uint32_t i = 0; i < m; ++i) sst = sst < hist[i] ? hist[i] : 0u;
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        DtRec r;
+        r.cu = st.cu;
+        r.mu = st.mu;
+        r.avgw = st.avgw;
+        r.total_c = st.total_c;
+        r.total_m = st.total_m;
+        r.nv = st.nv;
+        r.N = N;
+        r.nfree = S - st.nrun;
+        r.flags = st.flags;
+        r.done = st.decided == J ? 1u : 0u;
+        r.queued = (st.l1n > 0u || st.next_arr > st.l0_head) ? 1u : 0u;
+        r.nxt = st.next_arr < J ? jobs[st.next_arr].x : kEmpty;
+        r.fc = fsc;
+        r.fm = fsm;
+        r.ft = fmd;
+        r.sc = ssc;
+        r.sm = ssm;
+        r.st = sst;
+        r.pad = 0u;
+        reinterpret_cast<DtRec*>(blk)[c] = r;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -459,36 +547,46 @@ __device__ __forceinline__ bool dt_approve(uint32_t tc, uint32_t tm, float cu, f
     return 0.0 >= incentive;  // float64(price 0) >= incentive (:155)
 }
 
-// Phase D: trader rounds in cluster order, then the next tick.
+// Phase D: trader rounds in cluster order over the whole system, then the next tick.  Every rank
+// runs it on the same gathered records and replicated trader state, so every decision is identical
+// on every rank; a rank applies the side effects on its own clusters (Foreign jobs, virtual nodes)
+// to its live state as well as to the snapshot the later rounds of this tick read.
 __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
     __shared__ DtTrader trs[kDtMaxClusters];
     __shared__ uint32_t appr[kDtMaxClusters];
     __shared__ uint32_t nvs[kDtMaxClusters];  // virtual nodes per cluster (written here)
+    __shared__ uint32_t nfr[kDtMaxClusters];  // free running slots per cluster (taken here)
     if (a.ctl->done) return;
     const uint32_t T = a.ctl->T;
+    const bool any_due = a.ctl->any_due != 0u;
     const uint32_t lane = threadIdx.x;
-    const uint32_t C = a.C;
-    for (uint32_t q = lane; q < C; q += kWave) {
+    const uint32_t Ct = a.Ct;
+    for (uint32_t q = lane; q < Ct; q += kWave) {
         trs[q] = a.tr[q];
-        nvs[q] = a.cl[q].nv;
+        const DtRec* rq = dt_rec(a, q);
+        nvs[q] = rq->nv;
+        nfr[q] = rq->nfree;
     }
     __syncthreads();
     unsigned long long n_trades = a.ctl->n_trades, n_won = a.ctl->n_won, n_for = a.ctl->n_foreign;
     uint32_t lflags = 0;
 
-    for (uint32_t q0 = 0; q0 < C && a.period; q0 += kWave) {
+    for (uint32_t q0 = 0; q0 < Ct && a.period && any_due; q0 += kWave) {
         const uint32_t ql = q0 + lane;
-        unsigned long long due = __ballot(ql < C && trs[ql].next_due <= T);
+        unsigned long long due = __ballot(ql < Ct && trs[ql].next_due <= T);
         while (due) {
             const uint32_t q = q0 + (uint32_t)__builtin_ctzll(due);
             due &= due - 1ull;
+            const DtRec* rq = dt_rec(a, q);
+            const uint32_t ql_ = q - a.base;  // local index when q is on this rank
+            const bool qloc = ql_ < a.C;
             // RequestPolicyMonitor of requester q (trader.go:282-324): two-stage machine
             while (trs[q].next_due <= T) {
                 DtTrader tq = trs[q];
                 if (tq.stage == 0u) {  // cs := t.State.getState() (:284)
-                    tq.cs_cu = a.cl[q].cu;
-                    tq.cs_mu = a.cl[q].mu;
-                    tq.cs_avgw = a.cl[q].avgw;
+                    tq.cs_cu = rq->cu;
+                    tq.cs_mu = rq->mu;
+                    tq.cs_avgw = rq->avgw;
                 }
                 const uint32_t pol = tq.stage;
                 const bool broken = pol == 0u ? (tq.cs_avgw > 600000.0)                     // :137-139
@@ -501,57 +599,22 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
                     __syncthreads();
                     continue;
                 }
-                // ---- calculateContractRequest over GetLevel1() (ProvideJobs, D9 padding) ----
-                const uint32_t ln = a.cl[q].l1n;
-                const uint64_t qj0 = a.job_off[q];
-                const unsigned long long* qcm = a.l1cm + qj0;
-                const unsigned long long* qjd = a.l1jd + qj0;
-                uint32_t sc = 0, sm = 0, md = 0;
-                for (uint32_t i = lane; i < ln; i += kWave) {
-                    const unsigned long long cm = qcm[i];
-                    const uint32_t jc = (uint32_t)cm, jm = (uint32_t)(cm >> 32);
-                    if (pol == 0u) {  // fast node: sums and the longest duration (:138-155)
-                        const uint32_t d = (uint32_t)(qjd[i] >> 32);
-                        sc += jc;
-                        sm += jm;
-                        md = d > md ? d : md;
-                    } else {          // small node: int32 arithmetic (:232-259)
-                        sc += (int32_t)(0u - jc) < 0 ? jc : 0u;
-                        sm += (int32_t)(0u - jm) < 0 ? jm : 0u;
-                    }
-                }
-                const uint32_t kc = dt_wave_sum_u32(sc), km = dt_wave_sum_u32(sm);
-                uint32_t ksec = dt_wave_max_u32(md);
-                if (pol == 1u) {
-                    // contract.Time per job: endTime if the previous time < endTime, else 0
-                    // (:263-265); a padded last batch (len % 20 != 0) ends with zero jobs -> 0.
-                    // Durations are staged 64 at a time in LDS, then scanned by one lane.
-                    uint32_t t = 0;
-                    if (ln % 20u == 0u) {
-                        for (uint32_t b = 0; b < ln; b += kWave) {
-                            __syncthreads();
-                            if (b + lane < ln) appr[lane] = (uint32_t)(qjd[b + lane] >> 32);
-                            __syncthreads();
-                            if (lane == 0) {
-                                const uint32_t m = ln - b < (uint32_t)kWave ? ln - b : (uint32_t)kWave;
-                                for (uint32_t i = 0; i < m; ++i) t = t < appr[i] ? appr[i] : 0u;
-                            }
-                        }
-                        __syncthreads();
-                    }
-                    ksec = (uint32_t)__shfl((int)t, 0);
-                }
+                // calculateContractRequest over GetLevel1() (scheduler_client.go:126-289), sized
+                // by the owner's step kernel after phase A: Level1 does not change in phase D
+                const uint32_t kc = pol == 0u ? rq->fc : rq->sc;
+                const uint32_t km = pol == 0u ? rq->fm : rq->sm;
+                const uint32_t ksec = pol == 0u ? rq->ft : rq->st;
                 // ---- Trade (trader.go:193-278): RequestResource to every other trader ----
                 uint32_t napp = 0;
-                for (uint32_t r0 = 0; r0 < C; r0 += kWave) {
+                for (uint32_t r0 = 0; r0 < Ct; r0 += kWave) {
                     const uint32_t r = r0 + lane;
                     bool app = false;
-                    if (r < C && r != q) {
+                    if (r < Ct && r != q) {
                         DtTrader t = trs[r];
                         if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
                         if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
-                            const DtCluster& rc = a.cl[r];
-                            app = dt_approve(rc.total_c, rc.total_m, rc.cu, rc.mu, kc, km, ksec);
+                            const DtRec* rr = dt_rec(a, r);
+                            app = dt_approve(rr->total_c, rr->total_m, rr->cu, rr->mu, kc, km, ksec);
                             t.lock_id = t.next_id++;  // set even when not approving (:44-46)
                             t.lock_until = T + a.lock_s;
                         }
@@ -576,14 +639,16 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
                     // ApproveContract (server.go:63-85): the lock set in this round still
                     // matches; AllocateVirtualNodeResources on the responder (cluster.go:87-125)
                     uint32_t rc_ = kc, rm_ = km;
-                    const uint32_t rn0 = a.node_off[r], rN = a.node_off[r + 1] - rn0;
+                    const uint32_t rN = dt_rec(a, r)->N;
                     const uint32_t rNN = rN + nvs[r];
+                    unsigned long long* rs = dt_snap(a, r);
+                    const uint32_t rl = r - a.base;  // local index when r is on this rank
+                    const bool rloc = rl < a.C;
                     bool ovf = false;
                     for (uint32_t nd = 0; nd < rNN; ++nd) {
                         if (rm_ == 0u && rc_ == 0u) break;  // :90-92
-                        unsigned long long* np_ = nd < rN ? &a.tn[rn0 + nd]
-                                                          : &a.vn[(size_t)r * a.V + (nd - rN)];
-                        const unsigned long long v = ld64(np_);
+                        unsigned long long* sp = nd < rN ? &rs[nd] : &rs[a.NS + (nd - rN)];
+                        const unsigned long long v = ld64(sp);
                         double mem_diff = 0.0, core_diff = 0.0;
                         if (rm_ > 0u) mem_diff = fabs(__dsub_rn((double)rm_, go_f64((uint32_t)(v >> 32))));
                         if (rc_ > 0u) core_diff = fabs(__dsub_rn((double)rc_, go_f64((uint32_t)v)));
@@ -614,33 +679,41 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
                         }
                         ++n_for;
                         if (ksec == 0u) continue;  // RunJob sleeps 0: commit and release at once
-                        // go node.RunJob(Foreign) (:116): commit now, release at T + time
-                        uint32_t slot = kEmpty;
-                        const size_t rsb = (size_t)r * a.S;
-                        for (uint32_t b = 0; b < a.S; b += kWave) {
-                            const unsigned long long fr = __ballot(ld32(&a.sfin[rsb + b + lane]) == kEmpty);
-                            if (fr) {
-                                slot = b + (uint32_t)__builtin_ctzll(fr);
-                                break;
-                            }
-                        }
-                        if (slot == kEmpty) {
+                        // go node.RunJob(Foreign) (:116): commit now, release at T + time.  The
+                        // free-slot count is replicated, so every rank sees the same overflow.
+                        if (nfr[r] == 0u) {
                             ovf = true;
                             break;
                         }
+                        const unsigned long long nv_ = (unsigned long long)((uint32_t)v - (uint32_t)fc) |
+                                                       ((unsigned long long)((uint32_t)(v >> 32) - (uint32_t)fm) << 32);
                         if (lane == 0) {
-                            const uint32_t lo = (uint32_t)v - (uint32_t)fc;
-                            const uint32_t hi = (uint32_t)(v >> 32) - (uint32_t)fm;
-                            __hip_atomic_store(np_, (unsigned long long)lo | ((unsigned long long)hi << 32),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            __hip_atomic_store(&a.sfin[rsb + slot], T + ksec, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                            a.snode[rsb + slot] = nd;
-                            a.scm[rsb + slot] = (unsigned long long)(uint32_t)fc |
-                                                ((unsigned long long)(uint32_t)fm << 32);
-                            atomicAdd(&a.cl[r].nrun, 1u);  // atomics: never read back in here
-                            atomicMin(&a.cl[r].minf, T + ksec);
-                            atomicOr(&a.cl[r].l1_dirty, 1u);  // the commit may wrap a counter
+                            __hip_atomic_store(sp, nv_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            nfr[r] -= 1u;
+                        }
+                        if (rloc) {  // the owner: live node counter and a running slot
+                            uint32_t slot = kEmpty;
+                            const size_t rsb = (size_t)rl * a.S;
+                            for (uint32_t b = 0; b < a.S; b += kWave) {
+                                const unsigned long long fr = __ballot(ld32(&a.sfin[rsb + b + lane]) == kEmpty);
+                                if (fr) {
+                                    slot = b + (uint32_t)__builtin_ctzll(fr);
+                                    break;
+                                }
+                            }
+                            if (lane == 0 && slot != kEmpty) {
+                                unsigned long long* np_ = nd < rN ? &a.tn[a.node_off[rl] + nd]
+                                                                  : &a.vn[(size_t)rl * a.V + (nd - rN)];
+                                __hip_atomic_store(np_, nv_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                __hip_atomic_store(&a.sfin[rsb + slot], T + ksec, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                                a.snode[rsb + slot] = nd;
+                                a.scm[rsb + slot] = (unsigned long long)(uint32_t)fc |
+                                                    ((unsigned long long)(uint32_t)fm << 32);
+                                atomicAdd(&a.cl[rl].nrun, 1u);  // atomics: never read back in here
+                                atomicMin(&a.cl[rl].minf, T + ksec);
+                                atomicOr(&a.cl[rl].l1_dirty, 1u);  // the commit may wrap a counter
+                            }
                         }
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                         __syncthreads();
@@ -659,16 +732,21 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
                     // AddVirtualNode on the requester (cluster.go:65-85)
                     if (lane == 0) {
                         const uint32_t nv = nvs[q];
+                        const unsigned long long cap = (unsigned long long)kc | ((unsigned long long)km << 32);
                         if (nv < a.V) {
-                            __hip_atomic_store(&a.vn[(size_t)q * a.V + nv],
-                                               (unsigned long long)kc | ((unsigned long long)km << 32),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            a.vcap[(size_t)q * a.V + nv] = make_uint2(kc, km);
+                            __hip_atomic_store(&dt_snap(a, q)[a.NS + nv], cap, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
                             nvs[q] = nv + 1u;
-                            atomicAdd(&a.cl[q].nv, 1u);
-                            atomicOr(&a.cl[q].l1_dirty, 1u);
+                            if (qloc) {
+                                __hip_atomic_store(&a.vn[(size_t)ql_ * a.V + nv], cap, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                                a.vcap[(size_t)ql_ * a.V + nv] = make_uint2(kc, km);
+                                atomicAdd(&a.cl[ql_].nv, 1u);
+                                atomicOr(&a.cl[ql_].l1_dirty, 1u);
+                            }
                         } else {
-                            atomicOr(&a.cl[q].flags, (uint32_t)MCS_FLAG_VNODE_OVERFLOW);
+                            lflags |= MCS_FLAG_VNODE_OVERFLOW;
+                            if (qloc) atomicOr(&a.cl[ql_].flags, (uint32_t)MCS_FLAG_VNODE_OVERFLOW);
                         }
                     }
                     __syncthreads();
@@ -709,25 +787,26 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
     // the next tick: T+1 while any cluster has a queued job, else the next arrival, sample tick
     // or trader round (oracle/mcs_oracle_dtrade.c)
     bool all_done = true, queued = false;
-    uint32_t nxt = T + a.sample_period - T % a.sample_period, fl = 0;
-    for (uint32_t q = lane; q < C; q += kWave) {
-        const DtCluster k = a.cl[q];
-        const uint32_t J = (uint32_t)(a.job_off[q + 1] - a.job_off[q]);
-        all_done = all_done && k.decided == J;
-        queued = queued || k.l1n > 0u || k.next_arr > k.l0_head;
-        if (k.next_arr < J) {
-            const uint32_t at = a.jobs[a.job_off[q] + k.next_arr].x;
-            nxt = at < nxt ? at : nxt;
-        }
-        if (a.period) nxt = trs[q].next_due < nxt ? trs[q].next_due : nxt;
-        fl |= k.flags;
+    uint32_t nxt = T + a.sample_period - T % a.sample_period, fl = 0, ndue = kEmpty;
+    for (uint32_t q = lane; q < Ct; q += kWave) {
+        const DtRec* rq = dt_rec(a, q);
+        all_done = all_done && rq->done != 0u;
+        queued = queued || rq->queued != 0u;
+        nxt = rq->nxt < nxt ? rq->nxt : nxt;
+        if (a.period) ndue = trs[q].next_due < ndue ? trs[q].next_due : ndue;
+        fl |= rq->flags;
     }
     const bool done_all = !__ballot(!all_done);
     const bool queued_any = __ballot(queued) != 0ull;
+    ndue = wave_min_u32(ndue);
     nxt = wave_min_u32(nxt);
+    nxt = ndue < nxt ? ndue : nxt;
     for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o);
     __syncthreads();
-    for (uint32_t q = lane; q < C; q += kWave) a.tr[q] = trs[q];
+    for (uint32_t q = lane; q < Ct; q += kWave) {
+        a.tr[q] = trs[q];
+        a.nv_all[q] = nvs[q];
+    }
     if (lane == 0) {
         DtCtl* ctl = a.ctl;
         uint32_t flags = ctl->flags | fl | lflags;
@@ -742,6 +821,7 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
         }
         ctl->T = Tn;
         ctl->done = done;
+        ctl->any_due = ndue <= Tn ? 1u : 0u;
         ctl->ticks += 1u;
         ctl->flags = flags;
         ctl->n_trades = n_trades;
@@ -758,12 +838,20 @@ hipError_t launch_dtrade_init(const DtArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_dtrade_tick(const DtArgs& a, hipStream_t s) {
+hipError_t launch_dtrade_step(const DtArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(dt_step_kernel, dim3(a.C), dim3(kWave), 0, s, a);
-    hipError_t st = hipGetLastError();
-    if (st != hipSuccess) return st;
+    return hipGetLastError();
+}
+
+hipError_t launch_dtrade_trader(const DtArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(dt_trader_kernel, dim3(1), dim3(kWave), 0, s, a);
     return hipGetLastError();
+}
+
+hipError_t launch_dtrade_tick(const DtArgs& a, hipStream_t s) {
+    const hipError_t st = launch_dtrade_step(a, s);
+    if (st != hipSuccess) return st;
+    return launch_dtrade_trader(a, s);
 }
 
 }  // namespace mcs

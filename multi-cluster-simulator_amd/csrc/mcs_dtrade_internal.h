@@ -1,7 +1,8 @@
 // mcs_dtrade_internal.h — device layout of the lock-step trading system with DELAY schedulers
-// (mcs_trade.h; oracle/mcs_oracle_dtrade.c).  One engine holds the whole system.
+// (mcs_trade.h; oracle/mcs_oracle_dtrade.c).  The system of Ct = world * C clusters
+// is sharded over `world` engines in contiguous blocks of C; the trader rounds run replicated.
 //
-// HBM, per cluster c (C of them):
+// HBM, per local cluster c (C of them):
 //   tn     u64 {free_c | free_m << 32} per physical node (CSR node_off), live across ticks
 //   vn     u64 free vector of virtual node v at [c * V + v]; vcap uint2 its capacity
 //   sfin/snode/scm  running slots (finish, node, {c | m << 32}); Foreign jobs included
@@ -10,7 +11,11 @@
 //          entry of a Level1 job is 1000 * (last - arrival), so no per-job map is kept
 //   cl     DtCluster queue cursors, counters, WaitTime sums, last sample
 //   tr     DtTrader trader state (two-stage RequestPolicyMonitor, responder lock)
-//   ctl    DtCtl the lock-step clock and log counters
+//   ctl    DtCtl the lock-step clock and log counters (replicated: identical on every rank)
+//   xb     the exchange blocks, one per rank (world * blk bytes): rank r's block holds DtRec[C] and
+//          the node snapshots u64[C * W] of clusters [r*C, r*C + C) after phase A (physical nodes
+//          at [0, N), virtual node v at [NS + v]).  Phase D reads every block (gathered by RCCL or
+//          the caller; with world 1 the step kernel writes the only block in place).
 // Free counters are u32 halves read as Go uint64 values by sign extension: a Foreign job can take
 // more than a node has (cluster.go:116), and the wrapped uint64 is 2^64 - x for small x, which
 // the device keeps as the u32 2^32 - x (same comparisons against needs < 2^31; conversions to
@@ -27,7 +32,7 @@ namespace mcs {
 constexpr uint32_t kDtMaxNodes = 1024;  // physical nodes per cluster
 constexpr uint32_t kDtMaxVnodes = 256;  // virtual nodes a cluster can receive
 constexpr uint32_t kDtMaxSlots = 4096;  // running slots per cluster (LDS staging, 16 KB)
-constexpr uint32_t kDtMaxClusters = 1024;
+constexpr uint32_t kDtMaxClusters = 1024;  // in the whole system (all ranks)
 
 struct DtCluster {
     uint32_t next_arr;  // jobs [0, next_arr) have arrived
@@ -57,6 +62,22 @@ struct DtCluster {
     unsigned long long s_last;
 };
 
+// What the replicated trader rounds need of a cluster after phase A (one per cluster, in xb).
+struct DtRec {
+    float cu, mu;       // last sample
+    double avgw;
+    uint32_t total_c, total_m, nv, N;
+    uint32_t nfree;     // free running slots (Foreign jobs need one each)
+    uint32_t flags;
+    uint32_t done;      // every job decided
+    uint32_t queued;    // Level0 or Level1 non-empty
+    uint32_t nxt;       // next arrival (kEmpty: none)
+    uint32_t fc, fm, ft;  // the fast-node contract over Level1 (computed when the trader is due)
+    uint32_t sc, sm, st;  // the small-node contract
+    uint32_t pad;
+};
+static_assert(sizeof(DtRec) == 80, "DtRec layout");
+
 struct DtTrader {
     uint32_t lock_id, lock_until, next_id, next_due;
     uint32_t stage;     // 0: WaitTime next (a fresh cs), 1: Utilization (stale cs)
@@ -67,11 +88,18 @@ struct DtTrader {
 
 struct DtCtl {
     uint32_t T, done, ticks, flags;
+    uint32_t any_due, pad0;  // a trader round is due at T (phase A then sizes contracts)
     unsigned long long n_trades, n_won, n_foreign;
 };
 
 struct DtArgs {
     uint32_t C, V, S;
+    uint32_t base, Ct;   // global index of local cluster 0; clusters in the system (world * C)
+    uint32_t NS, W;      // snapshot stride: physical nodes, physical + virtual
+    uint32_t rank;
+    unsigned long long blk;  // bytes of one rank's exchange block
+    unsigned char* xb;       // world exchange blocks
+    uint32_t* nv_all;        // virtual nodes of every cluster (replicated)
     uint32_t period, ok_sleep, fail_sleep, lock_s, sample_period, max_wait, t_max;
     unsigned long long trade_cap, foreign_cap;
     const uint32_t* node_off;
@@ -92,13 +120,16 @@ struct DtArgs {
     unsigned long long* l1jd;
     unsigned long long* l1al;
     DtCluster* cl;
-    DtTrader* tr;
+    DtTrader* tr;  // Ct entries, replicated
     DtCtl* ctl;
     mcs_contract_rec* trade_log;
     mcs_foreign_rec* foreign_log;
 };
 
 hipError_t launch_dtrade_init(const DtArgs& a, hipStream_t s);
-hipError_t launch_dtrade_tick(const DtArgs& a, hipStream_t s);  // phases A, C, D of one tick
+// one tick: phases A and C (dt_step_kernel, writes this rank's exchange block), then phase D
+hipError_t launch_dtrade_step(const DtArgs& a, hipStream_t s);
+hipError_t launch_dtrade_trader(const DtArgs& a, hipStream_t s);
+hipError_t launch_dtrade_tick(const DtArgs& a, hipStream_t s);  // world 1: both
 
 }  // namespace mcs

@@ -26,6 +26,13 @@ int dtrade_trade_stats(mcs_engine* e, mcs_trade_stats* out);
 int ensure_job_records(mcs_engine* e);
 int dtrade_read_trades(mcs_engine* e, mcs_trade_rec* out, uint64_t cap, uint64_t* n);
 int dtrade_read_vnode_counts(mcs_engine* e, uint32_t* out, uint32_t n);
+// caller-driven lock-step of a sharded DELAY trading system (mcs_trade_begin/xfer/phase/end)
+int dtrade_begin(mcs_engine* e);
+int dtrade_xfer_bytes(mcs_engine* e, uint32_t phase, uint64_t* in_bytes, uint64_t* out_bytes);
+int dtrade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_bytes, void* out,
+                 uint64_t out_bytes, uint32_t* done);
+int dtrade_end(mcs_engine* e, mcs_stats* stats);
+inline bool is_dtrade(const mcs_engine* e);
 }  // namespace mcs
 
 struct mcs_engine {
@@ -74,7 +81,10 @@ struct mcs_engine {
     mcs::DtradeDev* dtd = nullptr;     // DELAY trading state (mcs_dtrade.cpp)
     bool dtrade_run = false;           // results of the last run come from DELAY trading
     uint32_t dt_vnodes = 0;            // virtual-node capacity per cluster (0 = auto)
+    uint32_t dt_ns = 0;                // node-snapshot stride over all ranks (0 = max_n)
 };
+
+inline bool mcs::is_dtrade(const mcs_engine* e) { return e->cfg.policy == MCS_POLICY_DELAY && e->cfg.trader; }
 
 inline int fail(mcs_engine* e, int code, const std::string& msg) {
     if (e) e->err = msg;

@@ -315,7 +315,8 @@ int trade_run(mcs_engine* e, mcs_stats* stats) {
     uint32_t escalations = 0;
     for (;;) {
         if (int s = mcs_trade_begin(e)) return s;
-        if (int s = e->world == 1 ? run_local(e) : run_rccl(e)) return s;
+        // a communicator selects the RCCL loop (world 1 included: one rank's all-gather is a copy)
+        if (int s = e->comm ? run_rccl(e) : run_local(e)) return s;
         const int s = mcs_trade_end(e, stats);
         if (s != MCS_E_CAPACITY) {
             if (stats) stats->escalations = escalations;
@@ -351,6 +352,8 @@ int mcs_set_shard(mcs_engine* e, uint32_t rank, uint32_t world) {
     if (world == 0 || rank >= world) return fail(e, MCS_E_INVALID, "rank must be < world");
     if ((uint64_t)world * e->C > 0xFFFFFFFFull) return fail(e, MCS_E_INVALID, "too many clusters");
     mcs::trade_free(e);
+    mcs::dtrade_free(e);
+    e->dt_ns = 0;
     e->rank = rank;
     e->world = world;
     return MCS_OK;
@@ -383,6 +386,11 @@ int mcs_comm_init(mcs_engine* e, const mcs_comm_id* id) {
 
 int mcs_trade_begin(mcs_engine* e) {
     if (int st = check_engine(e)) return st;
+    if (mcs::is_dtrade(e)) {
+        if (!e->has_jobs) return fail(e, MCS_E_STATE, "mcs_submit_jobs first");
+        if (int st = mcs::ensure_job_records(e)) return st;
+        return mcs::dtrade_begin(e);
+    }
     if (!(e->cfg.borrow || e->cfg.trader)) return fail(e, MCS_E_STATE, "engine config has no borrow/trader");
     if (int st = mcs::trade_alloc(e)) return st;
     mcs::TradeDev* td = e->td;
@@ -399,6 +407,7 @@ int mcs_trade_begin(mcs_engine* e) {
 
 int mcs_trade_xfer_bytes(mcs_engine* e, uint32_t phase, uint64_t* in_bytes, uint64_t* out_bytes) {
     if (!e || !in_bytes || !out_bytes || phase > 3) return MCS_E_INVALID;
+    if (mcs::is_dtrade(e)) return mcs::dtrade_xfer_bytes(e, phase, in_bytes, out_bytes);
     const uint64_t Cl = e->C, Ct = (uint64_t)e->C * e->world;
     switch (phase) {
         case 0: *in_bytes = 0; *out_bytes = Cl * sizeof(mcs::TrRecA); break;
@@ -412,6 +421,7 @@ int mcs_trade_xfer_bytes(mcs_engine* e, uint32_t phase, uint64_t* in_bytes, uint
 int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_bytes, void* out,
                     uint64_t out_bytes, uint32_t* done) {
     if (int st = check_engine(e)) return st;
+    if (mcs::is_dtrade(e)) return mcs::dtrade_phase(e, phase, in, in_bytes, out, out_bytes, done);
     mcs::TradeDev* td = e->td;
     if (!td || !td->begun) return fail(e, MCS_E_STATE, "mcs_trade_begin first");
     uint64_t ib = 0, ob = 0;
@@ -449,6 +459,7 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
 
 int mcs_trade_end(mcs_engine* e, mcs_stats* stats) {
     if (int st = check_engine(e)) return st;
+    if (mcs::is_dtrade(e)) return mcs::dtrade_end(e, stats);
     mcs::TradeDev* td = e->td;
     if (!td || !td->begun) return fail(e, MCS_E_STATE, "mcs_trade_begin first");
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
@@ -531,7 +542,7 @@ int mcs_read_trades(mcs_engine* e, mcs_trade_rec* out, uint64_t cap, uint64_t* n
 int mcs_read_virtual_nodes(mcs_engine* e, uint32_t* out, uint32_t n_total) {
     if (int st = check_engine(e)) return st;
     if (e->dtrade_run && e->dtd) {
-        if (!out || n_total > e->C) return fail(e, MCS_E_INVALID, "bad output");
+        if (!out || n_total > e->C * e->world) return fail(e, MCS_E_INVALID, "bad output");
         return mcs::dtrade_read_vnode_counts(e, out, n_total);
     }
     if (!e->trade_run || !e->td) return fail(e, MCS_E_STATE, "no lock-step run");

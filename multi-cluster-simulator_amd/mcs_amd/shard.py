@@ -50,13 +50,17 @@ def run_lockstep(engine, allgather):
     `allgather(buf: np.ndarray[uint8]) -> np.ndarray[uint8]` must return the concatenation, in
     rank order, of every rank's `buf` (all ranks call it the same number of times).  Every tick
     is phases 0..3 with an all-gather between consecutive phases; phase 3 reports `done`
-    identically on every rank.  Returns the engine's RunStats."""
+    identically on every rank.  A phase whose output is empty on every rank (the DELAY system moves
+    bytes only from phase 0 to phase 1) is not gathered.  Returns the engine's RunStats."""
+    def xfer(out):
+        return allgather(out) if out.size else out
+
     engine.trade_begin()
     while True:
         out, _ = engine.trade_phase(0, None)
-        out, _ = engine.trade_phase(1, allgather(out))
-        out, _ = engine.trade_phase(2, allgather(out))
-        _, done = engine.trade_phase(3, allgather(out))
+        out, _ = engine.trade_phase(1, xfer(out))
+        out, _ = engine.trade_phase(2, xfer(out))
+        _, done = engine.trade_phase(3, xfer(out))
         if done:
             return engine.trade_end()
 

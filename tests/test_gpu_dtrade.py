@@ -73,3 +73,63 @@ def test_gpu_dtrade_without_traders_equals_delay():
         node, start, fin = eng.placements()
     np.testing.assert_array_equal(g["node"], node)
     np.testing.assert_array_equal(g["start"], start)
+
+
+def test_gpu_dtrade_caller_driven_world1_equals_run():
+    """The caller-driven phase API at world 1 (phase 0 -> 1 carries this rank's exchange block back
+    in unchanged) == mcs_run's graph-replayed loop, bit for bit."""
+    from mcs_amd.shard import run_lockstep
+
+    arrays, streams, _ = seeded_workload("n64_hot", 8, 2000)
+    g = run(arrays, streams)
+    with Engine(0, policy="DELAY", trader=True) as eng:
+        eng.load_clusters(arrays)
+        eng.submit_jobs(streams)
+        run_lockstep(eng, lambda buf: buf)
+        node, start, fin = eng.placements()
+        trades, foreign = eng.contracts(), eng.foreign()
+        t_final = eng.trade_stats()["t_final"]
+    np.testing.assert_array_equal(node, g["node"])
+    np.testing.assert_array_equal(start, g["start"])
+    np.testing.assert_array_equal(fin, g["finish"])
+    assert trades.tobytes() == g["trades"].tobytes()
+    assert foreign.tobytes() == g["foreign"].tobytes()
+    assert t_final == g["ts"]["t_final"]
+
+
+def test_gpu_dtrade_two_ranks_gloo():
+    """world = 2 shards (two processes, two engines on device 0) exchanging one block per rank per
+    tick over gloo via the caller-driven phase API == the oracle of the whole system."""
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29583")
+    r = subprocess.run([sys.executable, os.path.join(here, "dtrade_2rank.py")], env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "DTRADE-2RANK OK" in r.stdout
+
+
+def test_gpu_dtrade_rccl_loop_world1():
+    """The RCCL tick loop (shape all-reduce, one in-place ncclAllGather of the exchange blocks per
+    tick, mcs_dtrade.cpp dt_run_rccl) on a world-1 communicator == the graph-replayed loop."""
+    arrays, streams, _ = seeded_workload("n64_hot", 8, 2000)
+    g = run(arrays, streams)
+    with Engine(0, policy="DELAY", trader=True) as eng:
+        eng.load_clusters(arrays)
+        eng.set_shard(0, 1)
+        eng.comm_init(Engine.comm_unique_id())
+        eng.submit_jobs(streams)
+        eng.run()
+        node, start, fin = eng.placements()
+        trades, foreign = eng.contracts(), eng.foreign()
+        vn = eng.virtual_nodes()
+        t_final = eng.trade_stats()["t_final"]
+    np.testing.assert_array_equal(node, g["node"])
+    np.testing.assert_array_equal(start, g["start"])
+    np.testing.assert_array_equal(fin, g["finish"])
+    assert trades.tobytes() == g["trades"].tobytes()
+    assert foreign.tobytes() == g["foreign"].tobytes()
+    assert vn.tolist() == [len(v) for v in g["vnodes"]]
+    assert t_final == g["ts"]["t_final"]

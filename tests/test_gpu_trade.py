@@ -117,3 +117,25 @@ def test_gpu_trade_two_ranks_one_gpu():
                        text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "TRADE-2RANK OK" in r.stdout
+
+
+def test_gpu_trade_rccl_loop_world1():
+    """The RCCL tick loop (three ncclAllGather per tick, mcs_trade.cpp run_rccl) on a world-1
+    communicator == the HBM-exchange loop: exercises the RCCL transport on a one-GPU box."""
+    arrays, streams, _ = seeded_workload("n64_hot", 8, 1500)
+    want = gpu_trade(arrays, streams)
+    with Engine(0, borrow=True, trader=True, t_max_s=20_000_000) as eng:
+        eng.load_clusters(arrays)
+        eng.set_shard(0, 1)
+        eng.comm_init(Engine.comm_unique_id())
+        eng.submit_jobs(streams)
+        eng.run()
+        node, start, fin = eng.placements()
+        got = dict(lent=eng.lent(), trades=eng.trades(), vn=eng.virtual_nodes(), ts=eng.trade_stats())
+    np.testing.assert_array_equal(node, want["node"])
+    np.testing.assert_array_equal(start, want["start"])
+    np.testing.assert_array_equal(fin, want["finish"])
+    assert got["lent"].tobytes() == want["lent"].tobytes()
+    assert got["trades"].tobytes() == want["trades"].tobytes()
+    assert got["vn"].tolist() == want["virtual_nodes"].tolist()
+    assert got["ts"]["t_final"] == want["tstats"]["t_final"]

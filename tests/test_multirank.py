@@ -69,3 +69,42 @@ def test_rank_seed_and_shard_range():
     assert spans[0][0] == 0 and spans[-1][1] == 4097
     assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
     assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def test_run_lockstep_skips_empty_exchanges():
+    """The caller-driven lock-step driver gathers only non-empty phase outputs (a DELAY trading
+    tick moves bytes from phase 0 to phase 1 only; FIFO trading moves them at every phase)."""
+    from mcs_amd.shard import run_lockstep
+
+    class FakeEngine:
+        def __init__(self, sizes, ticks):
+            self.sizes, self.ticks, self.calls = sizes, ticks, []
+
+        def trade_begin(self):
+            self.calls.append("begin")
+
+        def trade_phase(self, phase, inp):
+            n_in = 0 if inp is None else len(inp)
+            self.calls.append((phase, n_in))
+            if phase == 3:
+                self.ticks -= 1
+            return np.zeros(self.sizes[phase], np.uint8), phase == 3 and self.ticks == 0
+
+        def trade_end(self):
+            self.calls.append("end")
+            return "stats"
+
+    gathered = []
+
+    def allgather(buf):
+        gathered.append(len(buf))
+        return np.concatenate([buf, buf])  # two ranks
+
+    eng = FakeEngine([96, 0, 0, 0], ticks=3)
+    assert run_lockstep(eng, allgather) == "stats"
+    assert gathered == [96] * 3
+    assert eng.calls[1:5] == [(0, 0), (1, 192), (2, 0), (3, 0)]
+    gathered.clear()
+    eng = FakeEngine([8, 4, 12, 0], ticks=2)
+    run_lockstep(eng, allgather)
+    assert gathered == [8, 4, 12] * 2
