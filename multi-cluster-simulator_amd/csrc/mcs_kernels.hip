@@ -7,8 +7,9 @@
 // of A.3.  Every decision is wave-uniform, so the wave never diverges on control flow:
 //
 //   * node free vectors are staged in LDS as packed u64 {free_c, free_m}, lane l owning nodes
-//     l, l+64, ... (NPL per lane); first fit = one ds_read_b64 per 64-node chunk, a per-lane
-//     lowest-fitting-node select and a DPP wave minimum (no LDS round trip, no SALU chain);
+//     l, l+64, ... (NPL per lane); first fit = one ds_read_b64 per 64-node chunk (issued at the
+//     end of the previous pass, after its commit and releases, so the LDS latency is off the
+//     decision chain), a per-lane lowest-fitting-node select and a DPP wave minimum;
 //     commit is one ds_sub_u64 and a release one ds_add_u64 (the packed halves never borrow or
 //     carry because a placed job fits and resources are conserved);
 //   * the running set is a pool of 64*P slots (row p, lane l): finish times in VGPRs (one
@@ -158,6 +159,11 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     // One pass = one decision; the loop has a single exit (the structurizer then needs no flow
     // copies of the loop-carried registers).
     uint32_t stop = 0u;
+    // node free vectors for the next first fit, read at the end of the previous pass (after its
+    // commit and releases) so the LDS latency overlaps the record broadcast of the next pass
+    uint64_t nvr[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) nvr[k] = nodes[k * kWave + lane];
     do {
         ++n_iter;
         // ReadyQueue head (:255-260): the next stream job, queued once its arrival has passed
@@ -182,7 +188,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
             uint32_t best = kEmpty;
 #pragma unroll
             for (int k = NPL - 1; k >= 0; --k) {
-                const uint64_t v = nodes[k * kWave + lane];
+                const uint64_t v = nvr[k];
                 const uint32_t x = (uint32_t)v >= jc ? nid[k] : kEmpty;
                 best = (uint32_t)(v >> 32) >= jm ? (x < best ? x : best) : best;
             }
@@ -249,6 +255,8 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                 if (minf <= t) release();
             }
         }
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) nvr[k] = nodes[k * kWave + lane];
     } while (!stop);
 
     if (flags & MCS_FLAG_DEADLOCK) {
