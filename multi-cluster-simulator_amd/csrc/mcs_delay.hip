@@ -167,8 +167,8 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
 #pragma unroll
         for (int k = NPL - 1; k >= 0; --k) {
             const uint64_t v = nodes[k * kWave + lane];
-            const uint32_t x = (uint32_t)v >= jc ? nid[k] : kEmpty;
-            best = (uint32_t)(v >> 32) >= jm ? (x < best ? x : best) : best;
+            // descending chunks: a fit replaces best (padding chunks sit above every real one)
+            best = ((uint32_t)v >= jc && (uint32_t)(v >> 32) >= jm) ? nid[k] : best;
         }
         return wave_min_u32(best);
     };

@@ -98,8 +98,10 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     for (int p = 0; p < P; ++p) pay_nf[p * kWave + lane] = (uint64_t)kEmpty << 32;  // free: never expires
 
     uint32_t cb = 0;
-    uint4 cur = load_batch(0);
-    uint4 nxt = load_batch(kWave);
+    uint4 nxt = load_batch(0);
+    // wait for the first batch here: the only load pending at the pass loop's entry is then the
+    // prefetch, which the loop never reads, so the waitcnt pass does not flush it at every batch
+    asm volatile("" ::"v"(nxt.x), "v"(nxt.y), "v"(nxt.z), "v"(nxt.w));
 
     uint32_t t = 0, r = 0, minf = kEmpty, flags = 0;
     // Counters that no decision reads live in VGPRs (the asm hides their uniformity): the CU's
@@ -113,36 +115,39 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     int32_t on = -1;
     uint32_t os = kEmpty, of = kEmpty;
 
-    // release every running job with finish <= t (cluster.go:153-157; A.2 step 1)
+    // release every running job with finish <= t (cluster.go:153-157; A.2 step 1).  Row by row:
+    // the expired test of row p over all lanes is one compare whose lane mask drives both the
+    // payload hand-back of that row (one pass per row with any expiry, constant LDS offsets) and
+    // the free-row bits; the lane's next finish is the min over its unexpired rows.
     auto release = [&]() __attribute__((always_inline)) {
         ++n_rel;
-        uint32_t xm = 0u;  // this lane's expired rows
-        uint32_t lm = lmin;
-        if (lmin <= t) {  // only lanes holding an expired slot scan their rows
-            lm = kEmpty;
+        uint32_t lm = kEmpty;
+        uint64_t nf[P];
+        bool ex[P];
 #pragma unroll
-            for (int p = 0; p < P; ++p) {  // free rows hold kEmpty: never expired, min-neutral
-                const uint32_t f = (uint32_t)(pay_nf[p * kWave + lane] >> 32);
-                const bool live = f > t;
-                xm |= live ? 0u : (1u << p);
-                lm = live ? (f < lm ? f : lm) : lm;
-            }
-            frm |= xm;
+        for (int p = 0; p < P; ++p) {  // free rows hold kEmpty: never expired, min-neutral
+            nf[p] = pay_nf[p * kWave + lane];
+            const uint32_t f = (uint32_t)(nf[p] >> 32);
+            ex[p] = f <= t;
+            const uint32_t fl = ex[p] ? kEmpty : f;
+            lm = fl < lm ? fl : lm;
         }
         lmin = lm;
-        // give the expired payloads back to their nodes, one expired row per lane per pass
-        for (;;) {
-            const uint64_t b = __ballot(xm != 0u);
-            if (!b) break;
-            used -= (uint32_t)__builtin_popcountll(b);
-            if (xm != 0u) {
-                const uint32_t ad = (uint32_t)(__ffs(xm) - 1) * kWave + lane;
-                xm &= xm - 1u;
-                const uint64_t nf = pay_nf[ad];
-                atomicAdd((unsigned long long*)&nodes[(uint32_t)nf], (unsigned long long)pay_cm[ad]);
-                pay_nf[ad] = nf | ((uint64_t)kEmpty << 32);  // the row is free again
+        uint32_t nexp = 0u;
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const uint64_t m = __ballot(ex[p]);
+            if (m) {
+                nexp += (uint32_t)__builtin_popcountll(m);
+                if (ex[p]) {  // give the payload back to its node; the row is free again
+                    atomicAdd((unsigned long long*)&nodes[(uint32_t)nf[p]],
+                              (unsigned long long)pay_cm[p * kWave + lane]);
+                    reinterpret_cast<uint32_t*>(pay_nf)[2 * (p * kWave + lane) + 1] = kEmpty;
+                    frm |= 1u << p;
+                }
             }
         }
+        used -= nexp;
         minf = wave_min_u32(lmin);
     };
 
@@ -164,15 +169,16 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     uint64_t nvr[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) nvr[k] = nodes[k * kWave + lane];
+    // Outer loop: one 64-record batch; inner loop: the passes whose ready cursor is in it.  The
+    // batch registers change only here, once per batch, so no pass copies them (a per-pass
+    // conditional swap made LLVM copy both buffers and wait for the prefetch on every pass).
+    do {
+    const uint4 cur = nxt;
+    nxt = load_batch(cb + kWave);  // prefetch one batch ahead
     do {
         ++n_iter;
         // ReadyQueue head (:255-260): the next stream job, queued once its arrival has passed
-        if (r - cb >= (uint32_t)kWave) {
-            cur = nxt;
-            cb += kWave;
-            nxt = load_batch(cb + kWave);
-        }
-        const uint32_t l = (r - cb) & 63u;
+        const uint32_t l = r - cb;
         const uint32_t arr = readlane(cur.x, l);
         const uint32_t jd = readlane(cur.y, l);
         const uint32_t jc = readlane(cur.z, l);
@@ -187,20 +193,30 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
             // each lane keeps its lowest fitting node, then a DPP wave minimum
             uint32_t best = kEmpty;
 #pragma unroll
+            // descending chunks: a lower chunk's node index is always lower, so a fit simply
+            // replaces best (padding chunks only sit above every real one and carry kEmpty)
             for (int k = NPL - 1; k >= 0; --k) {
                 const uint64_t v = nvr[k];
-                const uint32_t x = (uint32_t)v >= jc ? nid[k] : kEmpty;
-                best = (uint32_t)(v >> 32) >= jm ? (x < best ? x : best) : best;
+                best = ((uint32_t)v >= jc && (uint32_t)(v >> 32) >= jm) ? nid[k] : best;
             }
             const uint32_t k = wave_min_u32(best);
             if (k != kEmpty) {
                 // placement record, 64 jobs per register batch (jobs are placed in job order)
                 const uint32_t ol = r & 63u;
                 const uint32_t fin = t + jd;
-                const bool pme = lane == ol;
-                on = pme ? (int32_t)k : on;
-                os = pme ? t : os;
-                of = pme ? fin : of;
+                // lane ol of the batch takes (k, t, fin): three v_writelane (lane select in m0,
+                // the one scalar operand gfx950 allows beside the data SGPR)
+                // m0 is reserved to the compiler, which uses it nowhere in these kernels
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+                asm("s_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                    "v_writelane_b32 %0, %4, m0\n\t"
+                    "v_writelane_b32 %1, %5, m0\n\t"
+                    "v_writelane_b32 %2, %6, m0"
+                    : "+v"(on), "+v"(os), "+v"(of)
+                    : "s"(ol), "s"(k), "s"(t), "s"(fin)
+                    : "m0");
+#pragma clang diagnostic pop
                 ++placed;
                 if (ol == 63u) flush(r - 63u);
                 // A zero-duration job is committed and released before the next decision can
@@ -257,6 +273,8 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         }
 #pragma unroll
         for (int k = 0; k < NPL; ++k) nvr[k] = nodes[k * kWave + lane];
+    } while (!stop && r - cb < (uint32_t)kWave);
+    cb += kWave;
     } while (!stop);
 
     if (flags & MCS_FLAG_DEADLOCK) {
