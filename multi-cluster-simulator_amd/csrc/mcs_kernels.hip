@@ -162,8 +162,9 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
 
     // ---- Scheduler.Fifo (scheduler.go:216-296) ----
     // One pass = one decision; the loop has a single exit (the structurizer then needs no flow
-    // copies of the loop-carried registers).
-    uint32_t stop = 0u;
+    // copies of the loop-carried registers).  rend bounds the ready cursor of the inner loop: the
+    // end of the current batch, or 0 once the run stops, so one scalar compare ends both loops.
+    uint32_t rend;
     // node free vectors for the next first fit, read at the end of the previous pass (after its
     // commit and releases) so the LDS latency overlaps the record broadcast of the next pass
     uint64_t nvr[NPL];
@@ -175,6 +176,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     do {
     const uint4 cur = nxt;
     nxt = load_batch(cb + kWave);  // prefetch one batch ahead
+    rend = cb + kWave;
     do {
         ++n_iter;
         // ReadyQueue head (:255-260): the next stream job, queued once its arrival has passed
@@ -185,7 +187,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         const uint32_t jm = readlane(cur.w, l);
         uint32_t tn = t;
         if (r >= J) {  // every job decided
-            stop = 1u;
+            rend = 0u;
         } else if (arr > t) {  // all queues empty: 1 s sleeps to the arrival (:294); a wait head
             tn = arr;          // has always arrived, so this is never taken with have_w
         } else {
@@ -214,11 +216,16 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                     "v_writelane_b32 %1, %5, m0\n\t"
                     "v_writelane_b32 %2, %6, m0"
                     : "+v"(on), "+v"(os), "+v"(of)
-                    : "s"(ol), "s"(k), "s"(t), "s"(fin)
+                    : "s"(sgpr(ol)), "s"(sgpr(k)), "s"(sgpr(t)), "s"(sgpr(fin))
                     : "m0");
 #pragma clang diagnostic pop
                 ++placed;
-                if (ol == 63u) flush(r - 63u);
+                if (ol == 63u) {  // a full batch: every lane's job r - 63 + lane < J, no mask
+                    const uint32_t i = r - 63u + lane;
+                    __builtin_nontemporal_store(on, o_node + i);
+                    __builtin_nontemporal_store(os, o_start + i);
+                    __builtin_nontemporal_store(of, o_finish + i);
+                }
                 // A zero-duration job is committed and released before the next decision can
                 // read the node (RunJob sleeps 0; the release precedes the next branch, D3).
                 if (jd != 0u) {
@@ -229,7 +236,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                     const uint64_t any = __ballot(frm != 0u);
                     if (!any) {
                         flags |= MCS_FLAG_OVERFLOW;
-                        stop = 1u;
+                        rend = 0u;
                     } else {
                         if (lane == (uint32_t)__builtin_ctzll(any)) {
                             const uint32_t ad = (uint32_t)(__ffs(frm) - 1) * kWave + lane;
@@ -256,16 +263,16 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                 have_w = 1u;
                 if (minf == kEmpty) {  // nothing running: the head can never fit
                     flags |= MCS_FLAG_DEADLOCK;
-                    stop = 1u;
+                    rend = 0u;
                 } else {  // A.3: 1 s retries until the next completion (no lender, :234)
                     tn = minf > t + 1u ? minf : t + 1u;
                 }
             }
         }
-        if (!stop && tn != t) {
+        if (tn != t) {  // (after a stop only an overflowed run moves t; it is re-run anyway)
             if (tn < t) {  // the u32 seconds clock would wrap (D8 range exceeded): stop, flagged
                 flags |= MCS_FLAG_CLOCK_OVERFLOW;
-                stop = 1u;
+                rend = 0u;
             } else {
                 t = tn;
                 if (minf <= t) release();
@@ -273,9 +280,9 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         }
 #pragma unroll
         for (int k = 0; k < NPL; ++k) nvr[k] = nodes[k * kWave + lane];
-    } while (!stop && r - cb < (uint32_t)kWave);
+    } while (r < rend);
     cb += kWave;
-    } while (!stop);
+    } while (rend != 0u);
 
     if (flags & MCS_FLAG_DEADLOCK) {
         // jobs r..J-1 are never placed (the Go loop retries the head forever)

@@ -11,6 +11,12 @@ __device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 
+// a wave-uniform value pinned to an SGPR (an "s" asm operand may otherwise get a VGPR where the
+// divergence analysis cannot prove uniformity); free when the value already lives in an SGPR
+__device__ __forceinline__ uint32_t sgpr(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
 // unsigned min over the wave with DPP row shifts and row broadcasts (no LDS round trip):
 // rows of 16 lanes are scanned with row_shr 1/2/4/8, then row_bcast:15 / row_bcast:31 carry the
 // row minima upward; lane 63 ends with the wave minimum.  Lanes with no DPP source keep `old` =
