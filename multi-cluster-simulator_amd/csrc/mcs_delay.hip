@@ -129,34 +129,38 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     int32_t on = -1;
     uint32_t os = kEmpty, of = kEmpty, ov = 0u;
 
+    // release every running job with finish <= t (cluster.go:153-157), row by row as in
+    // fifo_kernel: row p's expired test over all lanes is one compare whose lane mask drives the
+    // payload hand-back of that row and its free-row bits
     auto release = [&]() __attribute__((always_inline)) {
         ++n_rel;
-        uint32_t xm = 0u;
-        uint32_t lm = lmin;
-        if (lmin <= t) {
-            lm = kEmpty;
+        uint32_t lm = kEmpty;
+        uint64_t nf[P];
+        bool ex[P];
 #pragma unroll
-            for (int p = 0; p < P; ++p) {
-                const uint32_t f = (uint32_t)(pay_nf[p * kWave + lane] >> 32);
-                const bool live = f > t;
-                xm |= live ? 0u : (1u << p);
-                lm = live ? (f < lm ? f : lm) : lm;
-            }
-            frm |= xm;
+        for (int p = 0; p < P; ++p) {  // free rows hold kEmpty: never expired, min-neutral
+            nf[p] = pay_nf[p * kWave + lane];
+            const uint32_t f = (uint32_t)(nf[p] >> 32);
+            ex[p] = f <= t;
+            const uint32_t fl = ex[p] ? kEmpty : f;
+            lm = fl < lm ? fl : lm;
         }
         lmin = lm;
-        for (;;) {
-            const uint64_t b = __ballot(xm != 0u);
-            if (!b) break;
-            used -= (uint32_t)__builtin_popcountll(b);
-            if (xm != 0u) {
-                const uint32_t ad = (uint32_t)(__ffs(xm) - 1) * kWave + lane;
-                xm &= xm - 1u;
-                const uint64_t nf = pay_nf[ad];
-                atomicAdd((unsigned long long*)&nodes[(uint32_t)nf], (unsigned long long)pay_cm[ad]);
-                pay_nf[ad] = nf | ((uint64_t)kEmpty << 32);
+        uint32_t nexp = 0u;
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const uint64_t m = __ballot(ex[p]);
+            if (m) {
+                nexp += (uint32_t)__builtin_popcountll(m);
+                if (ex[p]) {
+                    atomicAdd((unsigned long long*)&nodes[(uint32_t)nf[p]],
+                              (unsigned long long)pay_cm[p * kWave + lane]);
+                    reinterpret_cast<uint32_t*>(pay_nf)[2 * (p * kWave + lane) + 1] = kEmpty;
+                    frm |= 1u << p;
+                }
             }
         }
+        used -= nexp;
         minf = wave_min_u32(lmin);
     };
 
@@ -329,11 +333,19 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                     flags |= MCS_FLAG_OVERFLOW;
                     stop = 1u;
                 } else {
-                    const bool pme = lane == ol;
-                    on = pme ? (int32_t)k : on;
-                    os = pme ? t : os;
-                    of = pme ? fin : of;
-                    ov = pme ? 1u : ov;
+                    // lane ol of the batch takes (k, t, fin, written): v_writelane with the
+                    // lane select in m0 (m0 is used nowhere else in these kernels)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+                    asm("s_mov_b32 m0, %4\n\ts_nop 0\n\t"
+                        "v_writelane_b32 %0, %5, m0\n\t"
+                        "v_writelane_b32 %1, %6, m0\n\t"
+                        "v_writelane_b32 %2, %7, m0\n\t"
+                        "v_writelane_b32 %3, 1, m0"
+                        : "+v"(on), "+v"(os), "+v"(of), "+v"(ov)
+                        : "s"(sgpr(ol)), "s"(sgpr(k)), "s"(sgpr(t)), "s"(sgpr(fin))
+                        : "m0");
+#pragma clang diagnostic pop
                     ++placed;
                     ++h;
                     changed = 1u;
