@@ -173,8 +173,17 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     // Outer loop: one 64-record batch; inner loop: the passes whose ready cursor is in it.  The
     // batch registers change only here, once per batch, so no pass copies them (a per-pass
     // conditional swap made LLVM copy both buffers and wait for the prefetch on every pass).
+    // The previous batch's results (all 64 placed) are stored here, after the wait for this
+    // batch's records and before the next prefetch: the batch-boundary wait then covers only
+    // memory operations issued a whole batch earlier, never stores still in flight to HBM.
     do {
     const uint4 cur = nxt;
+    if (cb != 0u) {  // a full batch: every lane's job cb - 64 + lane < J, no mask
+        const uint32_t i = cb - kWave + lane;
+        __builtin_nontemporal_store(on, o_node + i);
+        __builtin_nontemporal_store(os, o_start + i);
+        __builtin_nontemporal_store(of, o_finish + i);
+    }
     nxt = load_batch(cb + kWave);  // prefetch one batch ahead
     rend = cb + kWave;
     do {
@@ -220,12 +229,6 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                     : "m0");
 #pragma clang diagnostic pop
                 ++placed;
-                if (ol == 63u) {  // a full batch: every lane's job r - 63 + lane < J, no mask
-                    const uint32_t i = r - 63u + lane;
-                    __builtin_nontemporal_store(on, o_node + i);
-                    __builtin_nontemporal_store(os, o_start + i);
-                    __builtin_nontemporal_store(of, o_finish + i);
-                }
                 // A zero-duration job is committed and released before the next decision can
                 // read the node (RunJob sleeps 0; the release precedes the next branch, D3).
                 if (jd != 0u) {
