@@ -233,16 +233,18 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                 // read the node (RunJob sleeps 0; the release precedes the next branch, D3).
                 if (jd != 0u) {
                     const uint64_t need = (uint64_t)jc | ((uint64_t)jm << 32);
-                    // commit — Node.RunJob, cluster.go:146-147 (synchronous, D2)
-                    if (lane == (k & 63u)) atomicSub((unsigned long long*)&nodes[k], (unsigned long long)need);
-                    // slot insert: the lowest lane with a free row, its lowest free row
+                    // slot insert: the lowest lane with a free row, its lowest free row.  That
+                    // lane also commits — Node.RunJob, cluster.go:146-147 (synchronous, D2) — since
+                    // any lane can reach any node in LDS; on a pool overflow the run stops and the
+                    // cluster is re-run with a bigger pool, so the skipped commit never matters.
                     const uint64_t any = __ballot(frm != 0u);
                     if (!any) {
                         flags |= MCS_FLAG_OVERFLOW;
                         rend = 0u;
                     } else {
                         if (lane == (uint32_t)__builtin_ctzll(any)) {
-                            const uint32_t ad = (uint32_t)(__ffs(frm) - 1) * kWave + lane;
+                            atomicSub((unsigned long long*)&nodes[k], (unsigned long long)need);
+                            const uint32_t ad = (uint32_t)__builtin_ctz(frm) * kWave + lane;  // frm != 0 here
                             frm &= frm - 1u;
                             pay_cm[ad] = need;
                             pay_nf[ad] = (uint64_t)k | ((uint64_t)fin << 32);
