@@ -52,8 +52,10 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     // conserved, so the low half never carries).  Node k lives at nodes[k].
     __shared__ uint64_t nodes[NPL * kWave];
     // running slots, row-major [P][64]: {cores | mem << 32} and {node | finish << 32}
-    __shared__ uint64_t pay_cm[P * kWave];
-    __shared__ uint64_t pay_nf[P * kWave];
+    // (one array, so a slot's two words share one address register and differ by an offset)
+    __shared__ uint64_t pay[2 * P * kWave];
+    uint64_t* const pay_cm = pay;
+    uint64_t* const pay_nf = pay + P * kWave;
 
     // ---- cluster spec: Run() keeps the JSON availability (scheduler.go:101-109) ----
     const uint32_t n0 = a.node_off[ci];
@@ -243,7 +245,8 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                         rend = 0u;
                     } else {
                         if (lane == (uint32_t)__builtin_ctzll(any)) {
-                            atomicSub((unsigned long long*)&nodes[k], (unsigned long long)need);
+                            __hip_atomic_fetch_sub(&nodes[k], need, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);  // ds_sub_u64
                             const uint32_t ad = (uint32_t)__builtin_ctz(frm) * kWave + lane;  // frm != 0 here
                             frm &= frm - 1u;
                             pay_cm[ad] = need;
