@@ -70,8 +70,9 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     const uint32_t lane = threadIdx.x;
 
     __shared__ uint64_t nodes[NPL * kWave];
-    __shared__ uint64_t pay_cm[P * kWave];
-    __shared__ uint64_t pay_nf[P * kWave];
+    __shared__ uint64_t pay[2 * P * kWave];  // running slots: {cores|mem} rows, then {node|finish}
+    uint64_t* const pay_cm = pay;
+    uint64_t* const pay_nf = pay + P * kWave;
 
     // ---- cluster spec: Run() keeps the JSON availability (scheduler.go:101-109) ----
     const uint32_t n0 = a.node_off[ci];
@@ -112,7 +113,10 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     };
     uint32_t cb = 0;
     uint4 cur = load_batch(0);
-    uint4 nxt = load_batch(kWave);
+    // wait for the first batch here, so the only load pending at the pass loop's entry is the
+    // prefetch, which the loop never reads (no flush of it at every pass; fifo_kernel v18)
+    asm volatile("" ::"v"(cur.x), "v"(cur.y), "v"(cur.z), "v"(cur.w));
+    uint4 nxt = make_uint4(0u, 0u, 0u, 0u);
 
     uint32_t t = 0, h = 0, l1n = 0, minf = kEmpty, flags = 0;
     // Counters and the WaitTime sums live in VGPRs (the asm hides their uniformity): the CU's scalar
@@ -184,11 +188,11 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         __attribute__((always_inline)) -> bool {
         if (jd == 0u) return true;
         const uint64_t need = (uint64_t)jc | ((uint64_t)jm << 32);
-        if (lane == (k & 63u)) atomicSub((unsigned long long*)&nodes[k], (unsigned long long)need);
         const uint64_t any = __ballot(frm != 0u);
-        if (!any) return false;
-        if (lane == (uint32_t)__builtin_ctzll(any)) {
-            const uint32_t ad = (uint32_t)(__ffs(frm) - 1) * kWave + lane;
+        if (!any) return false;  // pool overflow: the run stops and the cluster is re-run
+        if (lane == (uint32_t)__builtin_ctzll(any)) {  // the slot's lane also commits the node
+            __hip_atomic_fetch_sub(&nodes[k], need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t ad = (uint32_t)__builtin_ctz(frm) * kWave + lane;
             frm &= frm - 1u;
             pay_cm[ad] = need;
             pay_nf[ad] = (uint64_t)k | ((uint64_t)fin << 32);
@@ -212,8 +216,19 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         ov = 0u;
     };
 
-    uint32_t stop = 0u;
-    if (J != 0u) do {
+    // Outer loop: one 64-record Level0 batch (records in `cur`); inner loop: the passes whose head
+    // h is in it.  rend bounds h: the batch end, or 0 once the run stops.  A batch's results are
+    // stored at the next batch boundary, after the wait for the prefetched records.
+    uint32_t stop = 0u, rend = 0u;
+    if (J != 0u) for (;;) {
+    if (cb != 0u) {
+        const uint4 nb = nxt;  // waits for the prefetch, issued a whole batch ago
+        flush(cb - kWave);     // the previous batch (all 64 decided), with its arrivals in cur
+        cur = nb;
+    }
+    nxt = load_batch(cb + kWave);
+    rend = cb + kWave;
+    do {
         ++n_iter;
         uint32_t changed = 0u, l1w = 0u;
 
@@ -312,13 +327,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         }
 
         // ---- Level0 head (scheduler.go:332-366) ----
-        // Unmasked batch advance: the job array has kJobPad records of slack, so the prefetch one
-        // batch ahead is always in bounds and lands straight in the loop-carried registers.
-        if (h - cb >= (uint32_t)kWave) {
-            cur = nxt;
-            cb += kWave;
-            nxt = load_batch(cb + kWave);
-        }
+        // (unmasked batch loads: the job array has kJobPad records of slack)
         const uint32_t l = (h - cb) & 63u;
         const uint32_t arr = readlane(cur.x, l);
         if (!stop && h < J && arr <= t) {  // Level0 is non-empty: its head has arrived
@@ -363,7 +372,6 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                 changed = 1u;
                 l1w = 1u;
             }
-            if (changed && (h & 63u) == 0u) flush(h - 64u);
         }
         // Level1 stores must have reached L2 before the next pass's sc1 loads
         if (l1w) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -393,10 +401,14 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                 if (minf <= t) release();
             }
         }
-    } while (!stop);
+        if (stop) rend = 0u;
+    } while (h < rend);
+    if (rend == 0u) break;
+    cb += kWave;
+    }
 
     if (!(flags & (MCS_FLAG_OVERFLOW | MCS_FLAG_CLOCK_OVERFLOW))) {
-        if ((h & 63u) != 0u) flush(h & ~63u);
+        if (h > cb) flush(cb);  // the current batch's decided jobs (earlier batches are stored)
         if (flags & MCS_FLAG_DEADLOCK) {
             // the Level1 jobs left are retried forever: never placed
             for (uint32_t base = 0; base < l1n; base += kWave) {
