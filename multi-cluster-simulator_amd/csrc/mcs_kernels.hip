@@ -60,15 +60,17 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     // ---- cluster spec: Run() keeps the JSON availability (scheduler.go:101-109) ----
     const uint32_t n0 = a.node_off[ci];
     const uint32_t N = a.node_off[ci + 1] - n0;
-    uint32_t nid[NPL];
+    // Lane l holds the NPL consecutive nodes l * NPL + c (c = chunk), stored at nodes[c * 64 + l]
+    // (lane-contiguous rows, conflict-free): the lowest fitting node is then in the lowest lane
+    // with any fit, at that lane's lowest fitting chunk.
 #pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-        const uint32_t idx = k * kWave + lane;
-        uint2 v = make_uint2(0u, 0u);
-        if (idx < N) v = a.node_free0[n0 + idx];
-        nodes[idx] = (uint64_t)v.x | ((uint64_t)v.y << 32);
-        nid[k] = idx < N ? idx : kEmpty;  // node index, or never-fits for padding lanes
+    for (int c = 0; c < NPL; ++c) {
+        const uint32_t node = lane * NPL + c;
+        uint2 v = make_uint2(0u, 0u);  // padding: free 0 fits only a zero job, which node 0 takes
+        if (node < N) v = a.node_free0[n0 + node];
+        nodes[c * kWave + lane] = (uint64_t)v.x | ((uint64_t)v.y << 32);
     }
+    const uint64_t vmask = __ballot(lane * NPL < N);  // lanes holding a real node
 
     // ---- job stream ----
     const uint64_t j0 = a.job_off[ci];
@@ -202,18 +204,21 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         } else if (arr > t) {  // all queues empty: 1 s sleeps to the arrival (:294); a wait head
             tn = arr;          // has always arrived, so this is never taken with have_w
         } else {
-            // first fit — ScheduleJob, scheduler.go:129-137: lowest node index with both >=;
-            // each lane keeps its lowest fitting node, then a DPP wave minimum
-            uint32_t best = kEmpty;
+            // first fit — ScheduleJob, scheduler.go:129-137: lowest node index with both >=.
+            // Each lane finds its lowest fitting chunk (descending selects); the lowest lane with
+            // a fit (ballot + ff1) holds the node, and one readlane fetches its chunk.
+            uint32_t bc = NPL;
 #pragma unroll
-            // descending chunks: a lower chunk's node index is always lower, so a fit simply
-            // replaces best (padding chunks only sit above every real one and carry kEmpty)
-            for (int k = NPL - 1; k >= 0; --k) {
-                const uint64_t v = nvr[k];
-                best = ((uint32_t)v >= jc && (uint32_t)(v >> 32) >= jm) ? nid[k] : best;
+            for (int c = NPL - 1; c >= 0; --c) {
+                const uint64_t v = nvr[c];
+                bc = ((uint32_t)v >= jc && (uint32_t)(v >> 32) >= jm) ? (uint32_t)c : bc;
             }
-            const uint32_t k = wave_min_u32(best);
-            if (k != kEmpty) {
+            const uint64_t fit = __ballot(bc < (uint32_t)NPL) & vmask;
+            if (fit) {
+                const uint32_t fl = (uint32_t)__builtin_ctzll(fit);
+                const uint32_t fch = readlane(bc, fl);
+                const uint32_t k = fl * NPL + fch;        // the node (Go index)
+                const uint32_t kx = fch * kWave + fl;     // its place in nodes[]
                 // placement record, 64 jobs per register batch (jobs are placed in job order)
                 const uint32_t ol = r & 63u;
                 const uint32_t fin = t + jd;
@@ -245,12 +250,12 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                         rend = 0u;
                     } else {
                         if (lane == (uint32_t)__builtin_ctzll(any)) {
-                            __hip_atomic_fetch_sub(&nodes[k], need, __ATOMIC_RELAXED,
+                            __hip_atomic_fetch_sub(&nodes[kx], need, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP);  // ds_sub_u64
                             const uint32_t ad = (uint32_t)__builtin_ctz(frm) * kWave + lane;  // frm != 0 here
                             frm &= frm - 1u;
                             pay_cm[ad] = need;
-                            pay_nf[ad] = (uint64_t)k | ((uint64_t)fin << 32);
+                            pay_nf[ad] = (uint64_t)kx | ((uint64_t)fin << 32);  // release target
                             lmin = fin < lmin ? fin : lmin;
                         }
                         ++used;
