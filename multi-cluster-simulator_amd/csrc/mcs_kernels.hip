@@ -6,19 +6,20 @@
 // workgroup, under the serialized semantics SFIFO of SURVEY Appendix A with the exact fast-forward
 // of A.3.  Every decision is wave-uniform, so the wave never diverges on control flow:
 //
-//   * node free vectors are staged in LDS as packed u64 {free_c, free_m}, lane l owning nodes
-//     l, l+64, ... (NPL per lane); first fit = one ds_read_b64 per 64-node chunk (issued at the
-//     end of the previous pass, after its commit and releases, so the LDS latency is off the
-//     decision chain), a per-lane lowest-fitting-node select and a DPP wave minimum;
-//     commit is one ds_sub_u64 and a release one ds_add_u64 (the packed halves never borrow or
-//     carry because a placed job fits and resources are conserved);
+//   * node free vectors are staged in LDS as packed u64 {free_c, free_m}, lane l owning the NPL
+//     consecutive nodes l*NPL.. (chunk c at nodes[c*64 + l]); first fit = one ds_read_b64 per
+//     chunk (issued at the end of the previous pass, after its commit and releases), a per-lane
+//     lowest-fitting-chunk select, a ballot + ff1 for the lowest lane with a fit and one readlane
+//     of its chunk; commit is one ds_sub_u64 (by the slot-insert lane) and a release one
+//     ds_add_u64 (the packed halves never borrow or carry: a placed job fits and resources are
+//     conserved);
 //   * the running set is a pool of 64*P slots (row p, lane l): finish times in VGPRs (one
 //     register per row, static indices only), payload {cores|mem, node} in LDS [P][64]
 //     (lane-contiguous, bank-conflict-free); a free slot is the lowest free row of the lowest
 //     lane that has one (ballot + ffbl);
-//   * releases at a clock advance are wave-parallel: each lane tests its P rows, then scatters
-//     its expired payloads into the node array with ds_add_u64 (order-free integer adds); the
-//     next completion time is a DPP wave minimum;
+//   * releases at a clock advance go row by row: the expired test of row p over all lanes is one
+//     compare whose lane mask drives that row's payload hand-back (ds_add_u64, order-free integer
+//     adds) and its free-row bits; the next completion time is a DPP wave minimum;
 //   * job records are streamed from HBM 64 at a time with one coalesced 16 B/lane load (uint4
 //     {arrival, dur, cores, mem}), double-buffered one batch ahead, and broadcast to the scalar
 //     unit with v_readlane; with fused generation (GEN) each batch is synthesised in registers
