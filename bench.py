@@ -6,18 +6,29 @@ reference FIFO loop (pkg/scheduler/scheduler.go:216-296) for every cluster of th
 spec until every job is placed.  Inputs (job streams) are generated on the device before the timed
 region and stay resident in HBM.
 
-Multi-GPU: one process per GPU (torchrun), clusters sharded by rank with NO data-path collective
-(clusters are independent); per-GPU work is fixed (4096 clusters per rank) -> "scaling": "weak".
-torch.distributed is used only for the barrier and the max-over-ranks of the timed region.
+Configs (BASELINE.json `configs`):
+  c4 (default, the headline) — 4096 clusters x 256 nodes, FIFO, no trading.  Multi-GPU: one process
+     per GPU (torchrun); with --shard strong (default) the 4096 clusters of ONE system are split in
+     contiguous blocks over the ranks, each cluster keyed by its global index, so every rank
+     regenerates exactly the streams the 1-GPU run simulates ("scaling": "strong"); --shard weak
+     gives every rank its own 4096 clusters ("scaling": "weak").  No data-path collective: clusters
+     are independent; torch.distributed carries only the barrier and the max/sum around the timed
+     region.
+  c3 — 1024 cluster_small replicas per GPU, FIFO, the reference client's arrivals (weak).
+  c2 — one cluster_big cluster with 1M jobs (a single wave: a latency line, replicas only on N>1).
+  c5 — the lock-step trading system (64 clusters, borrow + trader; --policy delay: DELAY + real
+     contracts), sharded over the ranks with RCCL all-gathers.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with "roofline" (HBM-bound:
-28 algorithmic bytes per placement) and "cpu_baseline" (the oracle, rank 0, N=1).
+28 algorithmic bytes per placement; the kernel is latency-bound, see "limiter") and
+"cpu_baseline" (the naive CPU oracle, rank 0, N=1, with the host's core count and CPU model).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -27,6 +38,8 @@ sys.path.insert(0, os.path.join(REPO, "multi-cluster-simulator_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 BYTES_PER_PLACEMENT = 28  # 16 B job record read + 12 B result write
 BYTES_PER_PLACEMENT_FUSED = 12  # --gen fused: the record is synthesised in registers, only results move
+LIMITER = ("latency: each cluster is a serial chain of decisions (one wave per cluster); HBM bytes are "
+           "exactly the algorithmic ones, the bound is the per-decision dependency chain (DESIGN.md §7)")
 
 
 def parse():
@@ -34,48 +47,69 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--clusters", type=int, default=4096, help="clusters per GPU (weak scaling)")
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c4",
+                    help="c4: the headline FIFO benchmark; c3: 1024 cluster_small replicas per GPU; c2: one "
+                         "cluster_big with 1M jobs; c5: the lock-step borrow + trader system")
+    ap.add_argument("--shard", choices=["strong", "weak"], default="strong",
+                    help="c4 over N GPUs: strong = the 4096 clusters of one system split over the ranks "
+                         "(BASELINE configs[3]); weak = 4096 clusters per rank")
+    ap.add_argument("--clusters", type=int, default=0,
+                    help="c4: clusters of the system (strong) or per GPU (weak); c3: replicas per GPU; "
+                         "c5: clusters of the whole trading system")
     ap.add_argument("--nodes", type=int, default=256)
-    ap.add_argument("--jobs-per-cluster", type=int, default=16384)
+    ap.add_argument("--jobs-per-cluster", type=int, default=0)
     ap.add_argument("--load", type=float, default=0.9, help="offered memory load of the scaled arrivals")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x4D43535F53494D31)
-    ap.add_argument("--cpu-sample-clusters", type=int, default=2048,
-                    help="C4 CPU baseline sample: that many clusters with full streams (~20 thread-s of oracle work)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-sample-clusters", type=int, default=0,
+                    help="CPU baseline sample: that many clusters with full streams (0 = per-config default, "
+                         "about 10-30 s of oracle work)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, usable cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None,
-                    help="per-launch HBM bytes measured by a separate rocprofv3 --pmc pass")
+                    help="per-launch HBM bytes measured by a separate rocprofv3 --pmc pass (profile figure)")
     ap.add_argument("--policy", choices=["fifo", "delay"], default="fifo",
-                    help="c4 policy: fifo (the headline, Scheduler.Fifo) or delay (Scheduler.Delay, "
-                         "the reference's default policy, scheduler.go:116)")
+                    help="fifo (the headline, Scheduler.Fifo) or delay (Scheduler.Delay, the reference's "
+                         "default policy, scheduler.go:116)")
     ap.add_argument("--gen", choices=["stream", "fused"], default="stream",
-                    help="c4 job stream: 'stream' = records generated before the timed region and read "
-                         "from HBM (SURVEY §8d, 28 B/placement); 'fused' = synthesised inside the "
-                         "placement kernel (SURVEY §8f row 3, 12 B/placement)")
-    ap.add_argument("--config", choices=["c4", "c5"], default="c4",
-                    help="c4: the headline FIFO benchmark; c5: the lock-step borrow + trader system "
-                         "(--clusters = clusters of the WHOLE system, sharded over the ranks)")
+                    help="job stream: 'stream' = records generated before the timed region and read from HBM "
+                         "(SURVEY §8d, 28 B/placement); 'fused' = synthesised inside the placement kernel "
+                         "(SURVEY §8f row 3, 12 B/placement)")
     a = ap.parse_args()
+    defaults = {  # (clusters, jobs per cluster, cpu sample clusters)
+        "c4": (4096, 16384, 2048),
+        "c3": (1024, 65536, 1024),
+        "c2": (1, 1_000_000, 1),
+        "c5": (64, 2000 if a.policy == "delay" else 156250, 16 if a.policy == "delay" else 64),
+    }[a.config]
+    a.clusters = a.clusters or defaults[0]
+    a.jobs_per_cluster = a.jobs_per_cluster or defaults[1]
+    a.cpu_sample_clusters = a.cpu_sample_clusters or defaults[2]
     if a.traffic_json is None:
         a.traffic_json = os.path.join(REPO, "profiles", "traffic_latest" + ("_delay" if a.policy == "delay" else "")
                                       + ("_fused" if a.gen == "fused" else "") + ".json")
-    if a.config == "c5" and a.policy == "delay":
-        # DELAY schedulers trading real contracts: cluster_small replicas at the
-        # reference client's rate, where Level1 fills and the WaitTime policy breaks
-        if a.clusters == 4096:
-            a.clusters = 64
-        if a.jobs_per_cluster == 16384:
-            a.jobs_per_cluster = 2000
-        if a.cpu_sample_clusters == 2048:
-            a.cpu_sample_clusters = 16
-    elif a.config == "c5":  # BASELINE.json configs[4]: 64 trading clusters, 10M jobs
-        if a.clusters == 4096:
-            a.clusters = 64
-        if a.jobs_per_cluster == 16384:
-            a.jobs_per_cluster = 156250
-        if a.cpu_sample_clusters == 2048:
-            a.cpu_sample_clusters = 64
     return a
+
+
+def host_info(n_threads):
+    """What the CPU baseline ran on: usable cores, the machine's cpus and the CPU model."""
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count() or 1
+    return {"threads": n_threads, "host_nproc": os.cpu_count(), "host_usable_cpus": usable, "cpu_model": model}
+
+
+NAIVE = ("the CPU oracle is the deliberately naive restatement of the Go loop (it rescans the running "
+         "list on every pass); it is a reported baseline, not the target")
 
 
 def cpu_baseline_c5(args, lam, sample_jobs):
@@ -100,8 +134,9 @@ def cpu_baseline_c5(args, lam, sample_jobs):
         "kind": "port",
         "sample": f"{args.clusters} clusters x {args.nodes} nodes x {sample_jobs} jobs ({streams.n_jobs} jobs, "
                   f"{r['n_lent']} lent runs, {r['t_final']} ticks), oracle/mcs_oracle_trade.c -O3, 1 thread, "
-                  f"{dt:.2f} s wall",
+                  f"{dt:.2f} s wall; {NAIVE}",
         "seconds": dt,
+        "host": host_info(1),
     }
 
 
@@ -174,8 +209,9 @@ def main_c5_delay(args, world, rank, local_rank):
             cpu = {"value": float((r["node"] >= 0).sum()) / dt, "unit": "job placements/s", "cores": 1,
                    "kind": "port",
                    "sample": f"{k} cluster_small x {jk} jobs ({streams.n_jobs} jobs, {r['n_trades']} trader rounds, "
-                             f"{r['t_final']} ticks), oracle/mcs_oracle_dtrade.c -O3, 1 thread, {dt:.2f} s wall",
-                   "seconds": dt}
+                             f"{r['t_final']} ticks), oracle/mcs_oracle_dtrade.c -O3, 1 thread, {dt:.2f} s wall; "
+                             f"{NAIVE}",
+                   "seconds": dt, "host": host_info(1)}
         out = {
             "metric": "trading-system job placements/sec with DELAY schedulers (real contracts)",
             "value": decided_all / elapsed_max,
@@ -201,6 +237,7 @@ def main_c5_delay(args, world, rank, local_rank):
             },
             "roofline": {
                 "bound": "hbm",
+                "limiter": "launch/latency: a tick is dependent launches of a few us (DESIGN.md §11)",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -224,7 +261,7 @@ def main_c5_delay(args, world, rank, local_rank):
 
 def main_c5(args, world, rank, local_rank):
     """C5: the whole trading system (args.clusters clusters) split in equal blocks over the ranks,
-    one lock-step run per step; the three per-tick record exchanges are RCCL all-gathers over xGMI
+    one lock-step run per step; the per-tick record exchanges are RCCL all-gathers over xGMI
     when world > 1 (mcs_trade.h)."""
     import torch
     import torch.distributed as dist
@@ -298,10 +335,11 @@ def main_c5(args, world, rank, local_rank):
                 "clusters_total": args.clusters,
                 "nodes": args.nodes,
                 "jobs_per_cluster": args.jobs_per_cluster,
-                "parallelism": f"{world} shard(s); per-tick RCCL all-gathers" if dist_on else "1 GPU, exchange in HBM",
+                "parallelism": f"{world} shard(s); per-tick RCCL all-gather" if dist_on else "1 GPU, exchange in HBM",
             },
             "roofline": {
                 "bound": "hbm",
+                "limiter": "launch/latency: a tick is dependent launches of a few us (DESIGN.md §9)",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -322,20 +360,90 @@ def main_c5(args, world, rank, local_rank):
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, lam, n_threads):
+# ---- C2 / C3 / C4: independent clusters, no trading --------------------------------------------
+class Workload:
+    """One rank's share of a FIFO/DELAY batch config."""
+
+    def __init__(self, args, world, rank):
+        from mcs_amd import Cluster, GenParams, replicate, uniform_cluster
+        from mcs_amd.engine import scaled_lambda
+        from mcs_amd.shard import rank_seed
+
+        self.cfg = args.config
+        self.J = args.jobs_per_cluster
+        fused = args.gen == "fused"
+        if args.config == "c4":
+            self.spec_name = f"{args.nodes} nodes x {{32 cores, 24000 memory}}"
+            spec = uniform_cluster(args.nodes)
+            lam = scaled_lambda(args.nodes, load=args.load)
+            self.lam = lam
+            self.arrival = f"scaled per-second Poisson arrivals at {args.load:.0%} memory load (lambda={lam:.4f}/s)"
+            gp = GenParams(seed=args.seed, arrival_mode=1, lam=lam, fused=fused)
+            if args.shard == "strong":
+                if args.clusters % world:
+                    raise SystemExit(f"--clusters {args.clusters} must divide over {world} ranks (strong sharding)")
+                self.total = args.clusters
+                self.per = args.clusters // world
+                self.base = rank * self.per  # global index of this rank's first cluster
+                self.shard = (rank, world)
+                self.scaling = "strong"
+            else:
+                self.total = args.clusters * world
+                self.per = args.clusters
+                self.base = 0
+                self.shard = None
+                gp.seed = rank_seed(args.seed, rank)
+                self.scaling = "weak"
+        else:
+            name = "cluster_small" if args.config == "c3" else "cluster_big"
+            self.spec_name = f"assets/{name}.json"
+            spec = Cluster.load(os.path.join(REPO, "assets", name + ".json"))
+            self.lam = 10.0
+            self.arrival = "reference client arrivals (Poisson(10) per minute, 60/n s spacing; client.go:107-125)"
+            gp = GenParams(seed=rank_seed(args.seed, rank), fused=fused)
+            self.per = args.clusters
+            self.total = args.clusters * world
+            self.base = 0
+            self.shard = None
+            self.scaling = "weak"
+        self.spec = spec
+        self.arrays = replicate(spec, self.per)
+        self.gp = gp
+
+    def describe(self, args, world):
+        pol = "DELAY" if args.policy == "delay" else "FIFO"
+        fused = "job stream synthesised inside the kernel (fused), " if args.gen == "fused" else ""
+        if self.cfg == "c4":
+            if self.scaling == "strong":
+                head = (f"C4: {self.total} clusters total x {args.nodes} nodes, split {self.per} per GPU over "
+                        f"{world} GPU(s) (strong sharding, clusters keyed by global index)")
+            else:
+                head = f"C4 weak: {self.per} clusters x {args.nodes} nodes per GPU ({self.total} in total)"
+        elif self.cfg == "c3":
+            head = f"C3: {self.per} cluster_small replicas per GPU ({self.total} in total)"
+        else:
+            head = f"C2: one cluster_big cluster per GPU ({world} independent replica(s))"
+        return (f"{head}, {pol}, no trading, {fused}{self.J} jobs/cluster, {self.arrival}")
+
+    def cpu_sample(self, args):
+        from mcs_amd.engine import gen_streams_host
+
+        k = min(args.cpu_sample_clusters, self.per)
+        from mcs_amd import replicate
+
+        arrays = replicate(self.spec, k)
+        gp = type(self.gp)(**{**self.gp.__dict__, "fused": False})
+        return arrays, gen_streams_host(gp, arrays, self.J, base=self.base), k
+
+
+def cpu_baseline(args, wl, n_threads):
     """The oracle (CPU restatement, deliberately naive, -O3) on a bounded sample of the same
     workload: the first cpu_sample_clusters clusters of rank 0, full job streams, OpenMP over
     clusters.  Test infrastructure used as the reported baseline only."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_ref as O
-    from mcs_amd import GenParams, replicate, uniform_cluster
-    from mcs_amd.engine import gen_streams_host
-    from mcs_amd.shard import rank_seed
 
-    k = min(args.cpu_sample_clusters, args.clusters)
-    arrays = replicate(uniform_cluster(args.nodes), k)
-    gp = GenParams(seed=rank_seed(args.seed, 0), arrival_mode=1, lam=lam)
-    streams = gen_streams_host(gp, arrays, args.jobs_per_cluster)
+    arrays, streams, k = wl.cpu_sample(args)
     O.lib()
     t0 = time.perf_counter()
     if args.policy == "delay":
@@ -349,24 +457,14 @@ def cpu_baseline(args, lam, n_threads):
         "unit": "placements/s",
         "cores": n_threads,
         "kind": "port",
-        "sample": f"{k} of {args.clusters} clusters x {args.nodes} nodes x {args.jobs_per_cluster} jobs "
-                  f"({streams.n_jobs} placements), {src} -O3, OpenMP over clusters, "
-                  f"{dt:.2f} s wall",
+        "sample": f"{k} of {wl.per} clusters ({wl.spec_name}) x {wl.J} jobs ({streams.n_jobs} placements), "
+                  f"{src} -O3, OpenMP over clusters on {n_threads} thread(s), {dt:.2f} s wall; {NAIVE}",
         "seconds": dt,
+        "host": host_info(n_threads),
     }
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-
-    if args.config == "c5":
-        if args.policy == "delay":
-            return main_c5_delay(args, world, rank, local_rank)
-        return main_c5(args, world, rank, local_rank)
-
+def main_batch(args, world, rank, local_rank):
     import torch
     import torch.distributed as dist
 
@@ -376,19 +474,18 @@ def main():
         dist.init_process_group(backend="nccl")
     dev = torch.device("cuda", local_rank)
 
-    from mcs_amd import Engine, GenParams, replicate, uniform_cluster
-    from mcs_amd.engine import scaled_lambda
-    from mcs_amd.shard import aggregate, rank_seed
+    from mcs_amd import Engine
+    from mcs_amd.shard import aggregate
 
-    lam = scaled_lambda(args.nodes, load=args.load)
+    wl = Workload(args, world, rank)
     delay = args.policy == "delay"
     eng = Engine(local_rank, policy="DELAY" if delay else "FIFO")
-    arrays = replicate(uniform_cluster(args.nodes), args.clusters)
-    eng.load_clusters(arrays)
+    eng.load_clusters(wl.arrays)
+    if wl.shard is not None:
+        eng.set_shard(*wl.shard)  # generation keyed by the global cluster index rank * per + k
     fused = args.gen == "fused"
     bpp = BYTES_PER_PLACEMENT_FUSED if fused else BYTES_PER_PLACEMENT
-    gp = GenParams(seed=rank_seed(args.seed, rank), arrival_mode=1, lam=lam, fused=fused)
-    eng.generate_jobs(gp, args.jobs_per_cluster)
+    eng.generate_jobs(wl.gp, wl.J)
     n_jobs = eng.num_jobs
 
     def barrier():
@@ -422,6 +519,7 @@ def main():
         "waited_frac": float(cs["waited"].sum()) / max(n_jobs, 1),
         "peak_running_max": int(cs["peak_running"].max()),
         "slot_pool": int(cs["pool"].max()),
+        "clusters_per_gpu": wl.per,
     }
     if delay:
         ds = eng.delay_stats()
@@ -440,18 +538,23 @@ def main():
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if (tj.get("clusters"), tj.get("nodes"), tj.get("jobs_per_cluster"), tj.get("policy", "fifo"),
-                    tj.get("gen", "stream")) == (args.clusters, args.nodes, args.jobs_per_cluster, args.policy, args.gen):
+                    tj.get("gen", "stream"), tj.get("config", "c4")) == \
+                    (wl.per, args.nodes, wl.J, args.policy, args.gen, args.config):
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            n_thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(args, lam, n_thr)
+            n_thr = args.cpu_threads or min(16, host_info(0)["host_usable_cpus"] or 1)
+            if args.config == "c2":
+                n_thr = 1  # one cluster: the oracle is one serial loop
+            cpu = cpu_baseline(args, wl, n_thr)
         value = placed_all / elapsed_max
+        metric = {"c4": "job placements/sec (whole node) at 4096 clusters x 256 nodes",
+                  "c3": "job placements/sec at 1024 cluster_small replicas per GPU",
+                  "c2": "job placements/sec, one cluster_big cluster with 1M jobs"}[args.config]
         out = {
-            "metric": "job placements/sec (whole node) at 4096 clusters x 256 nodes"
-                      + (", DELAY policy" if delay else ""),
+            "metric": metric + (", DELAY policy" if delay else ""),
             "value": value,
             "unit": "placements/s",
             "n_gpus": world,
@@ -459,34 +562,36 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": wl.scaling,
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (seeded device generator restating pkg/client/client.go distributions; "
-                    "scaled Poisson arrivals)",
+            "data": "synthetic (seeded device generator restating pkg/client/client.go distributions)",
             "config": {
-                "workload": f"C4: {args.clusters} clusters x {args.nodes} nodes per GPU, "
-                            f"{'DELAY' if delay else 'FIFO'}, no trading, "
-                            + ("job stream synthesised inside the kernel (fused), " if fused else "") +
-                            f"{args.jobs_per_cluster} jobs/cluster, scaled arrivals at {args.load:.0%} memory load "
-                            f"(lambda={lam:.4f}/s)",
-                "clusters_per_gpu": args.clusters,
-                "nodes": args.nodes,
-                "jobs_per_cluster": args.jobs_per_cluster,
+                "workload": wl.describe(args, world),
+                "clusters_total": wl.total,
+                "clusters_per_gpu": wl.per,
+                "nodes": int(wl.arrays.node_off[1] - wl.arrays.node_off[0]),
+                "jobs_per_cluster": wl.J,
                 "gen": args.gen,
                 "placements_per_step_per_gpu": placements_per_launch,
-                "parallelism": f"dp{world} (independent cluster shards, no collective on the data path)",
+                "parallelism": (f"dp{world}: " + ("one system's clusters split over the GPUs" if wl.scaling == "strong"
+                                                  else "independent replicas per GPU")
+                                + ", no collective on the data path"),
             },
             "roofline": {
                 "bound": "hbm",
+                "limiter": LIMITER,
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": "profiles/ rocprofv3 --pmc pass of the same command (not measured in this run)"
+                if traffic is not None else None,
                 "kernel": "mcs::delay_kernel" if delay else "mcs::fifo_kernel",
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "bytes_per_placement": bpp,
+                "placements_per_launch": placements_per_launch,
             },
             "cpu_baseline": cpu,
             "slot_pool_escalations": escalations,
@@ -497,6 +602,18 @@ def main():
     eng.close()
     if dist_on:
         dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config == "c5":
+        if args.policy == "delay":
+            return main_c5_delay(args, world, rank, local_rank)
+        return main_c5(args, world, rank, local_rank)
+    return main_batch(args, world, rank, local_rank)
 
 
 if __name__ == "__main__":

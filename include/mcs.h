@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MCS_ABI_VERSION 4
+#define MCS_ABI_VERSION 5
 
 /* ---- status codes --------------------------------------------------------------------------- */
 typedef enum mcs_status {
@@ -38,7 +38,10 @@ typedef enum mcs_status {
     MCS_E_HIP = -3,      /* a HIP runtime call failed                                             */
     MCS_E_RCCL = -4,     /* an RCCL call failed                                                   */
     MCS_E_STATE = -5,    /* call out of order (e.g. mcs_run before mcs_load_clusters)             */
-    MCS_E_NOMEM = -6     /* host or device allocation failed                                      */
+    MCS_E_NOMEM = -6,    /* host or device allocation failed                                      */
+    MCS_E_RANGE = -7     /* a cluster's simulated clock left the uint32 seconds range (D8): the run
+                            stopped there; MCS_FLAG_CLOCK_OVERFLOW marks it and its undecided jobs
+                            read MCS_NODE_UNPLACED / MCS_TIME_NONE                                 */
 } mcs_status;
 
 /* Node index written for a job that is never placed (head-of-line deadlock: the wait-queue head
@@ -83,7 +86,13 @@ typedef struct mcs_config {
     uint32_t lent_queue_cap;     /* LentQueue entries per cluster (0 = 4096)                        */
     uint32_t t_max_s;            /* stop the lock-step clock after this tick (0 = 0xFFFFFFFE)       */
     uint32_t max_wait_s;         /* DELAY: Policy.MaxWaitTime, 10 s (scheduler.go:115,353)          */
-    uint32_t reserved[2];
+    uint32_t unchecked_horizon;  /* 0 (default): mcs_submit_jobs / mcs_generate_jobs / mcs_append_jobs
+                                    reject streams whose clock bound (last arrival + sum of (dur + 1
+                                    [+ max_wait_s under DELAY])) leaves the uint32 range.  1: skip that
+                                    check (tests of the device-side guard: the kernels then stop the
+                                    cluster with MCS_FLAG_CLOCK_OVERFLOW and mcs_run returns
+                                    MCS_E_RANGE)                                                     */
+    uint32_t reserved[1];
 } mcs_config;
 
 /* Fills the reference defaults (FIFO, no borrow, no trader, 1 s sleeps, trader cadences above). */
@@ -136,6 +145,9 @@ typedef struct mcs_stats {
     uint32_t slot_pool;     /* largest slot pool used (x64)                                      */
     double kernel_ms;       /* device time of the placement kernel(s), HIP events on the engine stream */
     double wall_ms;         /* host wall time of the whole mcs_run call                           */
+    uint64_t pending;       /* online runs: jobs not decided yet (queued, or arriving later)       */
+    uint32_t t_horizon;     /* online runs: the horizon reached (MCS_TIME_NONE after a drain)      */
+    uint32_t online;        /* 1 if this run continued an online session (finite horizons)         */
 } mcs_stats;
 
 typedef struct mcs_cluster_stats {
@@ -190,17 +202,47 @@ int mcs_generate_jobs(mcs_engine* eng, const mcs_gen_params* p, uint64_t jobs_pe
 int mcs_read_jobs(mcs_engine* eng, uint32_t* arrival_s, uint32_t* dur_s, uint32_t* cores,
                   uint32_t* mem);
 
-/* Runs the configured policy loop for every cluster from its loaded spec until every job is
- * placed (t_end_s = MCS_TIME_NONE; other horizons are reserved), over ScheduleJob
- * (scheduler.go:127-139) and Node.RunJob (cluster.go:141-161):
+/* Runs the configured policy loop for every cluster over ScheduleJob (scheduler.go:127-139) and
+ * Node.RunJob (cluster.go:141-161):
  *   MCS_POLICY_FIFO  — Scheduler.Fifo (scheduler.go:216-296), serialized semantics SFIFO
  *                      (SURVEY Appendix A); with cfg.borrow or cfg.trader set the clusters instead
  *                      advance in lock-step with the borrow and trade exchanges (mcs_trade.h);
  *   MCS_POLICY_DELAY — Scheduler.Delay (scheduler.go:298-369) with jobs ingested by the "/delay"
  *                      handler (server.go:53-78), serialized semantics SDELAY.
  *                      MCS_FLAG_DEADLOCK marks clusters whose Level1 keeps jobs that can never
- *                      fit; those jobs get MCS_NODE_UNPLACED and every other job is placed. */
+ *                      fit; those jobs get MCS_NODE_UNPLACED and every other job is placed.
+ *
+ * Batch mode (the default after mcs_submit_jobs / mcs_generate_jobs): t_end_s = MCS_TIME_NONE runs
+ * every cluster from its loaded spec until every job is decided; repeated calls repeat the run.
+ *
+ * Online mode (FIFO / DELAY without trading) replaces the reference's infinite loop
+ * fed by HTTP POSTs (scheduler.go:216-296, 298-369; server.go:23-78): a finite t_end_s, or any
+ * mcs_append_jobs, starts a session that keeps each cluster's state (clock, queues, node counters,
+ * running jobs) on the device between calls.  mcs_run(t_end_s) then makes every decision the Go
+ * loop makes at simulated seconds t < t_end_s and stops there; mcs_run(MCS_TIME_NONE) continues
+ * until every job appended so far is decided (a drain).  Horizons are non-decreasing.  Jobs
+ * appended after mcs_run(h) must arrive at or after h (they are POSTed after that moment).  Splitting
+ * a run into horizons, with the jobs appended between them, gives bit-for-bit the placements of
+ * the batch run over all the jobs.  Between horizons the placements of undecided jobs read
+ * MCS_NODE_UNPLACED / MCS_TIME_NONE; the cluster and DELAY statistics are final after a drain.
+ * Returns MCS_E_RANGE (results readable) when a cluster's clock leaves the uint32 range. */
 int mcs_run(mcs_engine* eng, uint32_t t_end_s, mcs_stats* stats);
+
+/* Online mode: append jobs to the clusters' streams (the "/" or "/delay" handler appending to the
+ * ReadyQueue / Level0, server.go:38-41,67-69).  Jobs of cluster c are [job_offsets[c],
+ * job_offsets[c+1]) of the given arrays, arrival-sorted, each arrival >= the cluster's last one and
+ * >= the last horizon run.  Their ids continue the cluster's stream (dense order of
+ * mcs_read_placements: per cluster, submitted then appended jobs in order).  Starts an online
+ * session (state at t = 0) if none is active.  Not available with borrow/trader. */
+int mcs_append_jobs(mcs_engine* eng, const uint32_t* arrival_s, const uint32_t* dur_s,
+                    const uint32_t* cores, const uint32_t* mem, const uint64_t* job_offsets);
+
+/* Online mode: restart the session at t = 0 with every job submitted and appended so far. */
+int mcs_rewind(mcs_engine* eng);
+
+/* Dense CSR of the current streams (n_clusters + 1 entries): jobs of cluster c are rows
+ * [off[c], off[c+1]) of mcs_read_placements / mcs_read_jobs. */
+int mcs_read_job_offsets(mcs_engine* eng, uint64_t* off);
 
 /* Per-job results of the last mcs_run, indexed like the submitted jobs. */
 int mcs_read_placements(mcs_engine* eng, int32_t* node, uint32_t* start_s, uint32_t* finish_s);

@@ -61,9 +61,15 @@ __device__ __forceinline__ uint64_t ld_l2(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int NPL, int P, bool GEN>
+// HOR: the online variant, as fifo_kernel's: resume from the previous horizon's
+// OnlineState / node image / slot image (Level1 stays in its HBM list), run every iteration at
+// t < a.on.t_hor, save.  A cluster with nothing queued parks without advancing its clock (the
+// iteration is idempotent when re-run); only a drain (t_hor = kEmpty) ends a run the way the
+// one-shot kernel does.
+template <int NPL, int P, bool GEN, bool HOR>
 __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     static_assert(P <= 32, "free-row mask is one u32 per lane");
+    static_assert(!(HOR && GEN), "online runs stream records");
     constexpr bool kHist = NPL <= 2;  // exact Level1 fit histogram (256 B of LDS)
     const uint32_t item = blockIdx.x;
     const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
@@ -88,7 +94,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     }
 
     const uint64_t j0 = a.job_off[ci];
-    const uint32_t J = (uint32_t)(a.job_off[ci + 1] - j0);
+    const uint32_t J = HOR ? a.on.job_cnt[ci] : (uint32_t)(a.job_off[ci + 1] - j0);
     const uint4* __restrict__ jobs = GEN ? nullptr : a.jobs + j0;
     int32_t* __restrict__ o_node = a.out_node + j0;
     uint32_t* __restrict__ o_start = a.out_start + j0;
@@ -111,13 +117,6 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         else
             return jobs[base + lane];
     };
-    uint32_t cb = 0;
-    uint4 cur = load_batch(0);
-    // wait for the first batch here, so the only load pending at the pass loop's entry is the
-    // prefetch, which the loop never reads (no flush of it at every pass; fifo_kernel v18)
-    asm volatile("" ::"v"(cur.x), "v"(cur.y), "v"(cur.z), "v"(cur.w));
-    uint4 nxt = make_uint4(0u, 0u, 0u, 0u);
-
     uint32_t t = 0, h = 0, l1n = 0, minf = kEmpty, flags = 0;
     // Counters and the WaitTime sums live in VGPRs (the asm hides their uniformity): the CU's scalar
     // unit is the scarcer issue resource (fifo_kernel's measurements).
@@ -127,8 +126,59 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     //   wacc  per lane: Level0 placements of that lane's batch slots, added at each batch flush;
     //   l1_t  t of every Level1 placement;  mv_a  arrival of every job moved to Level1
     uint64_t wacc = 0, l1_t = 0, mv_a = 0;
+    bool live = true;
+    if constexpr (HOR) {  // resume from the previous horizon
+        const OnlineState st = a.on.st_in[ci];
+        if (st.valid) {
+            const unsigned long long* img = a.on.img_in + (size_t)ci * a.on.img_stride;
+#pragma unroll
+            for (int k = 0; k < NPL; ++k) nodes[k * kWave + lane] = img[k * kWave + lane];
+            const unsigned long long* sl = a.on.slot_in + (size_t)ci * kSlotImg;
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                if ((uint32_t)p < st.pool) {
+                    const uint64_t nf = sl[(kMaxPool + p) * kWave + lane];
+                    pay_cm[p * kWave + lane] = sl[p * kWave + lane];
+                    pay_nf[p * kWave + lane] = nf;
+                    const uint32_t f = (uint32_t)(nf >> 32);
+                    if (f != kEmpty) {
+                        frm &= ~(1u << p);
+                        lmin = f < lmin ? f : lmin;
+                    }
+                }
+            }
+            minf = wave_min_u32(lmin);
+            t = st.t;
+            h = st.cursor;
+            l1n = st.aux;
+            // a drained deadlock is not final online: later arrivals still reach Level0
+            flags = st.flags & ~MCS_FLAG_DEADLOCK;
+            placed = st.placed;
+            moved = st.waited;
+            peak = st.peak;
+            used = st.used;
+            n_iter = st.n_iter;
+            n_rel = st.n_rel;
+            placed_l1 = st.placed_l1;
+            peak_l1 = st.peak_l1;
+            l1_t = st.l1_t;
+            mv_a = st.mv_a;
+            if (lane == 0) wacc = st.wsum;
+        }
+        // nothing to do: a clock overflow is final, the horizon may be reached, and a cluster
+        // with nothing queued keeps its clock (a drain does not advance it again)
+        live = !(flags & MCS_FLAG_CLOCK_OVERFLOW) && t < a.on.t_hor && (h < J || l1n != 0u);
+    }
     asm volatile("" : "+v"(used), "+v"(peak), "+v"(n_iter), "+v"(n_rel), "+v"(placed), "+v"(moved),
                  "+v"(placed_l1), "+v"(peak_l1), "+v"(l1_t), "+v"(mv_a));
+
+    const uint32_t cb0 = HOR ? (h & ~63u) : 0u;
+    uint32_t cb = cb0;
+    uint4 cur = load_batch(cb0);
+    // wait for the first batch here, so the only load pending at the pass loop's entry is the
+    // prefetch, which the loop never reads (no flush of it at every pass; fifo_kernel v18)
+    asm volatile("" ::"v"(cur.x), "v"(cur.y), "v"(cur.z), "v"(cur.w));
+    uint4 nxt = make_uint4(0u, 0u, 0u, 0u);
     // Level0 result batch: lane (job & 63) holds its record; ov = written by Level0
     int32_t on = -1;
     uint32_t os = kEmpty, of = kEmpty, ov = 0u;
@@ -220,8 +270,8 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     // h is in it.  rend bounds h: the batch end, or 0 once the run stops.  A batch's results are
     // stored at the next batch boundary, after the wait for the prefetched records.
     uint32_t stop = 0u, rend = 0u;
-    if (J != 0u) for (;;) {
-    if (cb != 0u) {
+    if (live && (HOR || J != 0u)) for (;;) {
+    if (cb != cb0) {
         const uint4 nb = nxt;  // waits for the prefetch, issued a whole batch ago
         flush(cb - kWave);     // the previous batch (all 64 decided), with its arrivals in cur
         cur = nb;
@@ -292,6 +342,11 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                     const uint32_t jw = readlane((uint32_t)jdv, b);
                     const uint32_t jd = readlane((uint32_t)(jdv >> 32), b);
                     const uint32_t fin = t + jd;
+                    if (fin + 1u <= t) {  // finish leaves the u32 clock (D8): stop, flagged
+                        flags |= MCS_FLAG_CLOCK_OVERFLOW;
+                        stop = 1u;
+                        break;
+                    }
                     if (!commit(k, jc, jm, fin, jd)) {
                         flags |= MCS_FLAG_OVERFLOW;
                         stop = 1u;
@@ -338,7 +393,10 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
             const uint32_t ol = h & 63u;
             if (k != kEmpty) {
                 const uint32_t fin = t + jd;
-                if (!commit(k, jc, jm, fin, jd)) {
+                if (fin + 1u <= t) {  // finish leaves the u32 clock (D8): stop, flagged
+                    flags |= MCS_FLAG_CLOCK_OVERFLOW;
+                    stop = 1u;
+                } else if (!commit(k, jc, jm, fin, jd)) {
                     flags |= MCS_FLAG_OVERFLOW;
                     stop = 1u;
                 } else {
@@ -388,10 +446,12 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         }
         if (!stop) {
             if (h >= J && l1n == 0u) {  // every job placed: the run ends at the next iteration
-                t = t + 1u;
+                // (online: parked; the next horizon re-runs this iteration, which is idempotent
+                // with nothing queued, unless this is a drain)
+                if (!HOR || a.on.t_hor == kEmpty) t = t + 1u;
                 stop = 1u;
             } else if (!changed && tn == kEmpty) {  // nothing runs or arrives: Level1 never fits
-                flags |= MCS_FLAG_DEADLOCK;
+                if (!HOR || a.on.t_hor == kEmpty) flags |= MCS_FLAG_DEADLOCK;  // (online: parked)
                 stop = 1u;
             } else if (tn <= t) {
                 flags |= MCS_FLAG_CLOCK_OVERFLOW;
@@ -399,6 +459,9 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
             } else {
                 t = tn;
                 if (minf <= t) release();
+                if constexpr (HOR) {
+                    if (t >= a.on.t_hor) stop = 1u;  // the horizon: resume here next time
+                }
             }
         }
         if (stop) rend = 0u;
@@ -407,10 +470,11 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     cb += kWave;
     }
 
-    if (!(flags & (MCS_FLAG_OVERFLOW | MCS_FLAG_CLOCK_OVERFLOW))) {
+    if (!(flags & MCS_FLAG_OVERFLOW)) {
         if (h > cb) flush(cb);  // the current batch's decided jobs (earlier batches are stored)
-        if (flags & MCS_FLAG_DEADLOCK) {
-            // the Level1 jobs left are retried forever: never placed
+        if (flags & (MCS_FLAG_DEADLOCK | MCS_FLAG_CLOCK_OVERFLOW)) {
+            // the Level1 jobs left are retried forever (deadlock) or were not decided before the
+            // clock left the u32 range (the run fails with MCS_E_RANGE): never placed
             for (uint32_t base = 0; base < l1n; base += kWave) {
                 const uint32_t pos = base + lane;
                 if (pos < l1n) {
@@ -421,11 +485,19 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                 }
             }
         }
+        if (flags & MCS_FLAG_CLOCK_OVERFLOW) {  // and so were the Level0 jobs h..J-1
+            for (uint32_t i = h + lane; i < J; i += kWave) {
+                o_node[i] = MCS_NODE_UNPLACED;
+                o_start[i] = MCS_TIME_NONE;
+                o_finish[i] = MCS_TIME_NONE;
+            }
+        }
     }
     // WaitTime.TotalTime (scheduler.go:309-312,338-341): a placed job keeps 1000 * (start -
     // arrival); a job left in Level1 holds 1000 * (t - arrival) from the last pass.  Every moved
     // job's arrival is in mv_a, so Level1 contributes l1_t + left * t - mv_a.
-    const uint32_t left = (flags & MCS_FLAG_DEADLOCK) ? l1n : 0u;
+    // (online: the Level1 jobs still queued count at t as well; the values are final after a drain)
+    const uint32_t left = (HOR || (flags & MCS_FLAG_DEADLOCK)) ? l1n : 0u;
     uint64_t wsum = wacc;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -434,6 +506,54 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         wsum += (uint64_t)lo | ((uint64_t)hi << 32);
     }
     const uint64_t wait_s = wsum + l1_t + (uint64_t)left * t - mv_a;
+    // WaitTime.JobsCount counts the jobs POSTed to "/delay" (server.go:72): all of them at the
+    // end of a run; online, those that arrived before the horizon
+    int64_t jobs_count = (int64_t)J;
+    if constexpr (HOR) {
+        if (a.on.t_hor != kEmpty) {
+            uint32_t n = h;
+            for (uint32_t b = h; b < J; b += kWave) {
+                const uint32_t i = b + lane;
+                const uint64_t got = __ballot(i < J && jobs[i].x < a.on.t_hor);
+                n += (uint32_t)__builtin_popcountll(got);
+                if (got != ~0ull) break;  // arrivals are sorted: the first late one ends the count
+            }
+            jobs_count = (int64_t)n;
+        }
+        if (!(flags & MCS_FLAG_OVERFLOW)) {  // save the state the next horizon resumes from
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // other lanes' LDS atomics
+            unsigned long long* img = a.on.img_out + (size_t)ci * a.on.img_stride;
+#pragma unroll
+            for (int k = 0; k < NPL; ++k) img[k * kWave + lane] = nodes[k * kWave + lane];
+            unsigned long long* sl = a.on.slot_out + (size_t)ci * kSlotImg;
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                sl[p * kWave + lane] = pay_cm[p * kWave + lane];
+                sl[(kMaxPool + p) * kWave + lane] = pay_nf[p * kWave + lane];
+            }
+            if (lane == 0) {
+                OnlineState st{};
+                st.valid = 1u;
+                st.t = t;
+                st.cursor = h;
+                st.aux = l1n;
+                st.flags = flags;
+                st.pool = (uint32_t)P;
+                st.placed = placed;
+                st.waited = moved;
+                st.peak = peak;
+                st.used = used;
+                st.n_iter = n_iter;
+                st.n_rel = n_rel;
+                st.placed_l1 = placed_l1;
+                st.peak_l1 = peak_l1;
+                st.l1_t = l1_t;
+                st.mv_a = mv_a;
+                st.wsum = wsum;
+                a.on.st_out[ci] = st;
+            }
+        }
+    }
 
     if (lane == 0) {
         mcs_cluster_stats st;
@@ -448,7 +568,9 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         a.cstats[ci] = st;
         mcs_delay_cluster_stats ds;
         ds.total_wait_ms = (int64_t)(wait_s * 1000ull);
-        ds.jobs_count = (int64_t)J;  // every job has arrived when the run ends
+        // every job has arrived when the run ends; a run stopped by the clock range is an error
+        // (MCS_E_RANGE) whose wait statistics mean nothing: marked -1
+        ds.jobs_count = (flags & MCS_FLAG_CLOCK_OVERFLOW) ? -1 : jobs_count;
         ds.moved_l1 = moved;
         ds.placed_l1 = placed_l1;
         ds.peak_l1 = peak_l1;
@@ -459,45 +581,50 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         } else {
             atomicAdd(&a.totals->placed, (unsigned long long)placed);
             atomicAdd(&a.totals->waited, (unsigned long long)moved);
-            atomicAdd(&a.totals->unplaced, (unsigned long long)(J - placed));
+            // online: jobs not decided yet are pending, not unplaced (a drain decides them)
+            const bool final_ = !HOR || a.on.t_hor == kEmpty || (flags & MCS_FLAG_CLOCK_OVERFLOW);
+            if (final_) atomicAdd(&a.totals->unplaced, (unsigned long long)(J - placed));
             if (flags & MCS_FLAG_DEADLOCK) atomicAdd(&a.totals->deadlocked, 1u);
+            if (flags & MCS_FLAG_CLOCK_OVERFLOW) atomicAdd(&a.totals->clock_overflowed, 1u);
         }
     }
 }
 
-template <int NPL, int P, bool GEN>
+template <int NPL, int P, bool GEN, bool HOR>
 static hipError_t launch_delay_one(const DelayArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((delay_kernel<NPL, P, GEN>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL((delay_kernel<NPL, P, GEN, HOR>), dim3(a.n_items), dim3(kWave), 0, s, a);
     return hipGetLastError();
 }
 
-template <int NPL, bool GEN>
+template <int NPL, bool GEN, bool HOR>
 static hipError_t launch_delay_npl(const DelayArgs& a, int pool, hipStream_t s) {
     switch (pool) {
-        case 2: return launch_delay_one<NPL, 2, GEN>(a, s);
-        case 4: return launch_delay_one<NPL, 4, GEN>(a, s);
-        case 8: return launch_delay_one<NPL, 8, GEN>(a, s);
-        case 16: return launch_delay_one<NPL, 16, GEN>(a, s);
-        case 32: return launch_delay_one<NPL, 32, GEN>(a, s);
+        case 2: return launch_delay_one<NPL, 2, GEN, HOR>(a, s);
+        case 4: return launch_delay_one<NPL, 4, GEN, HOR>(a, s);
+        case 8: return launch_delay_one<NPL, 8, GEN, HOR>(a, s);
+        case 16: return launch_delay_one<NPL, 16, GEN, HOR>(a, s);
+        case 32: return launch_delay_one<NPL, 32, GEN, HOR>(a, s);
         default: return hipErrorInvalidValue;
     }
 }
 
-template <bool GEN>
+template <bool GEN, bool HOR>
 static hipError_t launch_delay_gen(const DelayArgs& a, int npl, int pool, hipStream_t s) {
     switch (npl) {
-        case 1: return launch_delay_npl<1, GEN>(a, pool, s);
-        case 2: return launch_delay_npl<2, GEN>(a, pool, s);
-        case 4: return launch_delay_npl<4, GEN>(a, pool, s);
-        case 8: return launch_delay_npl<8, GEN>(a, pool, s);
-        case 16: return launch_delay_npl<16, GEN>(a, pool, s);
+        case 1: return launch_delay_npl<1, GEN, HOR>(a, pool, s);
+        case 2: return launch_delay_npl<2, GEN, HOR>(a, pool, s);
+        case 4: return launch_delay_npl<4, GEN, HOR>(a, pool, s);
+        case 8: return launch_delay_npl<8, GEN, HOR>(a, pool, s);
+        case 16: return launch_delay_npl<16, GEN, HOR>(a, pool, s);
         default: return hipErrorInvalidValue;
     }
 }
 
-hipError_t launch_delay(const DelayArgs& a, int npl, int pool, hipStream_t s) {
+hipError_t launch_delay(const DelayArgs& a, int npl, int pool, bool hor, hipStream_t s) {
     if (a.n_items == 0) return hipSuccess;
-    return a.gen.on ? launch_delay_gen<true>(a, npl, pool, s) : launch_delay_gen<false>(a, npl, pool, s);
+    if (hor) return a.gen.on ? hipErrorInvalidValue : launch_delay_gen<false, true>(a, npl, pool, s);
+    return a.gen.on ? launch_delay_gen<true, false>(a, npl, pool, s)
+                    : launch_delay_gen<false, false>(a, npl, pool, s);
 }
 
 }  // namespace mcs

@@ -35,6 +35,8 @@ void free_clusters(mcs_engine* e) {
 }
 
 void free_jobs(mcs_engine* e) {
+    mcs::online_free(e);  // a new stream ends any online session
+    e->bounds_known = false;
     dfree(e->d_jobs);
     dfree(e->d_gen_max);
     e->gen = mcs::GenArgs{};
@@ -46,10 +48,13 @@ void free_jobs(mcs_engine* e) {
     dfree(e->d_l1_jd);
 }
 
+}  // namespace
+
+namespace mcs {
 int npl_for(uint32_t max_n) {
     const int opts[] = {1, 2, 4, 8, 16};
     for (int o : opts)
-        if ((uint32_t)(o * mcs::kWave) >= max_n) return o;
+        if ((uint32_t)(o * kWave) >= max_n) return o;
     return -1;
 }
 
@@ -59,14 +64,10 @@ int npl_for(uint32_t max_n) {
 int auto_pool(uint32_t max_n) {
     const uint32_t want = (2u * max_n + 63u) / 64u;
     int p = 2;
-    while ((uint32_t)p < want && p < mcs::kMaxPool) p *= 2;
+    while ((uint32_t)p < want && p < kMaxPool) p *= 2;
     return p;
 }
 
-
-}  // namespace
-
-namespace mcs {
 int ensure_job_records(mcs_engine* e) {
     if (e->d_jobs) return MCS_OK;
     const size_t nj = e->total_jobs ? e->total_jobs : 1;
@@ -190,6 +191,7 @@ int mcs_engine_destroy(mcs_engine* e) {
     mcs::trade_free(e);
     mcs::dtrade_free(e);
     mcs::comm_free(e);
+    mcs::online_free(e);
     free_clusters(e);
     free_jobs(e);
     dfree(e->d_totals);
@@ -320,19 +322,26 @@ int mcs_submit_jobs(mcs_engine* e, const uint32_t* arrival_s, const uint32_t* du
     if (int st = check_job_offsets(e, job_offsets)) return st;
     const uint64_t nj = job_offsets[e->C];
     if (nj && (!arrival_s || !dur_s || !cores || !mem)) return fail(e, MCS_E_INVALID, "null job array");
+    /* the clock never passes the last arrival + sum(dur + 1) under FIFO, + max_wait_s per job under
+     * DELAY (a Level0 head may wait that long before it moves): keep that inside uint32 (D8) */
+    const uint32_t extra = mcs::horizon_extra(e);
+    std::vector<uint32_t> last(e->C, 0u);
+    std::vector<uint64_t> sum(e->C, 0ull);
     for (uint32_t c = 0; c < e->C; ++c) { /* the ReadyQueue is filled in arrival order (server.go:41) */
-        /* the clock never passes the last arrival + sum(dur + 1): keep that inside uint32 (D8) */
-        uint64_t horizon = job_offsets[c + 1] > job_offsets[c] ? arrival_s[job_offsets[c + 1] - 1] : 0;
         for (uint64_t i = job_offsets[c]; i < job_offsets[c + 1]; ++i) {
             if (i > job_offsets[c] && arrival_s[i] < arrival_s[i - 1])
                 return fail(e, MCS_E_INVALID, "arrivals must be non-decreasing within a cluster");
-            horizon += (uint64_t)dur_s[i] + 1u;
+            sum[c] += (uint64_t)dur_s[i] + 1u + extra;
         }
-        if (horizon >= 0xFFFFFFFFull)
+        last[c] = job_offsets[c + 1] > job_offsets[c] ? arrival_s[job_offsets[c + 1] - 1] : 0u;
+        if (!e->cfg.unchecked_horizon && (uint64_t)last[c] + sum[c] >= 0xFFFFFFFFull)
             return fail(e, MCS_E_INVALID, "simulated clock could exceed 2^32-1 seconds");
     }
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (int st = alloc_jobs(e, job_offsets, true)) return st;
+    e->last_arr.swap(last);
+    e->sum_dur.swap(sum);
+    e->bounds_known = true;
     std::vector<uint4> h(nj ? nj : 1);
     for (uint64_t i = 0; i < nj; ++i) h[i] = make_uint4(arrival_s[i], dur_s[i], cores[i], mem[i]);
     HIPCHK(e, hipMemcpy(e->d_jobs, h.data(), (nj ? nj : 1) * sizeof(uint4), hipMemcpyHostToDevice));
@@ -380,6 +389,33 @@ int mcs_generate_jobs(mcs_engine* e, const mcs_gen_params* p, uint64_t jobs_per_
     /* fused: no records in HBM; the FIFO/DELAY kernels synthesise each batch (mcs_gen_dev.h) */
     if (!p->fused)
         if (int st = mcs::ensure_job_records(e)) return st;
+    /* the clock range (D8), as mcs_submit_jobs checks it: exact over the records, or for a fused
+     * stream its last arrival (the arrival scan, nothing stored) + jobs * (max_dur + extra) */
+    if (!e->cfg.unchecked_horizon && e->C) {
+        const uint32_t extra = mcs::horizon_extra(e);
+        if (!p->fused) {
+            if (int st = mcs::stream_bounds(e, e->last_arr, e->sum_dur)) return st;
+            e->bounds_known = true;
+            for (uint32_t c = 0; c < e->C; ++c)
+                if ((uint64_t)e->last_arr[c] + e->sum_dur[c] >= 0xFFFFFFFFull)
+                    return fail(e, MCS_E_INVALID, "simulated clock could exceed 2^32-1 seconds");
+        } else {
+            unsigned long long* d_last = nullptr;
+            std::vector<unsigned long long> last(e->C);
+            HIPCHK(e, hipMalloc(&d_last, e->C * sizeof(unsigned long long)));
+            hipError_t st = mcs::launch_gen_bound(e->d_job_off, e->C, e->gen.seed, e->gen.mode, e->gen.enl,
+                                                  e->gen.base, d_last, e->stream);
+            if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+            if (st == hipSuccess)
+                st = hipMemcpy(last.data(), d_last, e->C * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+            (void)hipFree(d_last);
+            if (st != hipSuccess) return fail(e, MCS_E_HIP, std::string("clock bound: ") + hipGetErrorString(st));
+            const uint64_t dur_bound = jobs_per_cluster * ((uint64_t)p->max_dur_s + extra);
+            for (uint32_t c = 0; c < e->C; ++c)
+                if (last[c] + dur_bound >= 0xFFFFFFFFull)
+                    return fail(e, MCS_E_INVALID, "simulated clock could exceed 2^32-1 seconds");
+        }
+    }
     e->has_jobs = true;
     return MCS_OK;
 }
@@ -394,7 +430,11 @@ int mcs_read_jobs(mcs_engine* e, uint32_t* arrival_s, uint32_t* dur_s, uint32_t*
     if (int st = mcs::ensure_job_records(e)) return st;
     std::vector<uint4> h(nj);
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, hipMemcpy(h.data(), e->d_jobs, nj * sizeof(uint4), hipMemcpyDeviceToHost));
+    if (e->segmented) {
+        if (int st = mcs::online_read_jobs(e, h.data())) return st;
+    } else {
+        HIPCHK(e, hipMemcpy(h.data(), e->d_jobs, nj * sizeof(uint4), hipMemcpyDeviceToHost));
+    }
     for (uint64_t i = 0; i < nj; ++i) {
         arrival_s[i] = h[i].x;
         dur_s[i] = h[i].y;
@@ -407,7 +447,11 @@ int mcs_read_jobs(mcs_engine* e, uint32_t* arrival_s, uint32_t* dur_s, uint32_t*
 int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     if (int st = check_engine(e)) return st;
     if (!e->has_clusters || !e->has_jobs) return fail(e, MCS_E_STATE, "load clusters and jobs first");
-    if (t_end_s != MCS_TIME_NONE) return fail(e, MCS_E_INVALID, "finite horizons are reserved");
+    if (e->online || t_end_s != MCS_TIME_NONE) { /* online mode (mcs_online.cpp) */
+        if (e->cfg.borrow || e->cfg.trader)
+            return fail(e, MCS_E_INVALID, "finite horizons are implemented for FIFO/DELAY without trading");
+        return mcs::online_run(e, t_end_s, stats);
+    }
     if (e->cfg.borrow || e->cfg.trader) /* the trading paths read the job records */
         if (int st = mcs::ensure_job_records(e)) return st;
     if (e->cfg.policy == MCS_POLICY_DELAY && e->cfg.trader) return mcs::dtrade_run(e, stats);
@@ -422,8 +466,8 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
         HIPCHK(e, hipMalloc(&e->d_l1_jd, nj * sizeof(uint64_t)));
     }
     const auto w0 = std::chrono::steady_clock::now();
-    const int npl = npl_for(e->max_n ? e->max_n : 1);
-    int pool = e->cfg.slot_pool ? (int)e->cfg.slot_pool : auto_pool(e->max_n);
+    const int npl = mcs::npl_for(e->max_n ? e->max_n : 1);
+    int pool = e->cfg.slot_pool ? (int)e->cfg.slot_pool : mcs::auto_pool(e->max_n);
     if (npl < 0) return fail(e, MCS_E_INVALID, "cluster too large");
 
     mcs::FifoArgs a{};
@@ -465,9 +509,9 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     for (;;) {
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));
         if (delay)
-            HIPCHK(e, mcs::launch_delay(da, npl, pool, e->stream));
+            HIPCHK(e, mcs::launch_delay(da, npl, pool, false, e->stream));
         else
-            HIPCHK(e, mcs::launch_fifo(a, npl, pool, e->stream));
+            HIPCHK(e, mcs::launch_fifo(a, npl, pool, false, e->stream));
         HIPCHK(e, hipEventRecord(e->ev1, e->stream));
         HIPCHK(e, hipMemcpyAsync(&tot, e->d_totals, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -506,7 +550,13 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
         stats->kernel_ms = kms;
         stats->wall_ms =
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+        stats->pending = 0;
+        stats->t_horizon = MCS_TIME_NONE;
+        stats->online = 0;
     }
+    if (tot.clock_overflowed)
+        return fail(e, MCS_E_RANGE, std::to_string(tot.clock_overflowed) +
+                                        " cluster(s) stopped: the simulated clock left the uint32 seconds range");
     return MCS_OK;
 }
 
@@ -516,6 +566,7 @@ int mcs_read_placements(mcs_engine* e, int32_t* node, uint32_t* start_s, uint32_
     const uint64_t nj = e->total_jobs;
     if (!nj) return MCS_OK;
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->segmented) return mcs::online_read_rows(e, node, start_s, finish_s);
     if (node) HIPCHK(e, hipMemcpy(node, e->d_out_node, nj * 4, hipMemcpyDeviceToHost));
     if (start_s) HIPCHK(e, hipMemcpy(start_s, e->d_out_start, nj * 4, hipMemcpyDeviceToHost));
     if (finish_s) HIPCHK(e, hipMemcpy(finish_s, e->d_out_finish, nj * 4, hipMemcpyDeviceToHost));
@@ -637,6 +688,8 @@ int mcs_cluster_states(mcs_engine* e, uint32_t t_s, mcs_cluster_state* out, uint
     if (!e->has_run) return fail(e, MCS_E_STATE, "mcs_run first");
     if (e->trade_run || e->dtrade_run)
         return fail(e, MCS_E_STATE, "cluster states are rebuilt from a FIFO/DELAY run without trading");
+    if (e->segmented)
+        return fail(e, MCS_E_STATE, "cluster states are rebuilt from batch runs (not after mcs_append_jobs)");
     if (!out || n_clusters > e->C) return fail(e, MCS_E_INVALID, "bad output");
     if (int st = mcs::ensure_job_records(e)) return st;
     mcs_cluster_state* d_out = nullptr;

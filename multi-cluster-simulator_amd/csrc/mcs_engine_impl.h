@@ -33,6 +33,16 @@ int dtrade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_byte
                  uint64_t out_bytes, uint32_t* done);
 int dtrade_end(mcs_engine* e, mcs_stats* stats);
 inline bool is_dtrade(const mcs_engine* e);
+// online mode (mcs_online.cpp)
+void online_free(mcs_engine* e);
+int online_run(mcs_engine* e, uint32_t t_hor, mcs_stats* stats);
+int online_read_rows(mcs_engine* e, int32_t* node, uint32_t* start_s, uint32_t* finish_s);
+int online_read_jobs(mcs_engine* e, uint4* out);
+int npl_for(uint32_t max_n);
+int auto_pool(uint32_t max_n);
+// per-cluster clock bound of the streams in HBM: last arrival and sum of (dur + 1 + extra)
+int stream_bounds(mcs_engine* e, std::vector<uint32_t>& last, std::vector<uint64_t>& sum);
+uint32_t horizon_extra(const mcs_engine* e);  // max_wait_s under DELAY, else 0
 }  // namespace mcs
 
 struct mcs_engine {
@@ -82,6 +92,22 @@ struct mcs_engine {
     bool dtrade_run = false;           // results of the last run come from DELAY trading
     uint32_t dt_vnodes = 0;            // virtual-node capacity per cluster (0 = auto)
     uint32_t dt_ns = 0;                // node-snapshot stride over all ranks (0 = max_n)
+    // online mode (mcs_online.cpp): per-cluster state kept on the device between horizons
+    bool online = false;               // a session is active
+    bool segmented = false;            // job_off holds segment starts with slack (appends)
+    uint32_t on_t_done = 0;            // the last horizon run (appended arrivals must be >= it)
+    int on_pool = 0;                   // slot rows that every saved state fits in
+    int on_cur = 0;                    // which of the double-buffered states is current
+    mcs::OnlineState* d_ost[2] = {nullptr, nullptr};
+    unsigned long long* d_oimg[2] = {nullptr, nullptr};
+    unsigned long long* d_oslot[2] = {nullptr, nullptr};
+    unsigned long long* d_l1_bak = nullptr;  // DELAY: Level1 lists at the start of a horizon
+    size_t l1_bak_words = 0;
+    uint32_t* d_job_cnt = nullptr;
+    std::vector<uint32_t> job_cnt;     // jobs per cluster (online; job_off = segment starts)
+    std::vector<uint32_t> last_arr;    // last arrival per cluster (append checks)
+    std::vector<uint64_t> sum_dur;     // sum of (dur + 1 [+ max_wait]) per cluster (clock bound)
+    bool bounds_known = false;         // last_arr / sum_dur filled
 };
 
 inline bool mcs::is_dtrade(const mcs_engine* e) { return e->cfg.policy == MCS_POLICY_DELAY && e->cfg.trader; }

@@ -25,6 +25,8 @@ struct Totals {  // device-side accumulation of mcs_stats (only clusters that di
     unsigned long long unplaced;
     unsigned int deadlocked;
     unsigned int overflowed;
+    unsigned int clock_overflowed;  // clusters stopped by MCS_FLAG_CLOCK_OVERFLOW (run fails, MCS_E_RANGE)
+    unsigned int pad;
 };
 
 // In-kernel synthesis of the job stream (mcs_gen_dev.h): with `on` the FIFO and
@@ -40,6 +42,33 @@ struct GenArgs {
     uint32_t on;
 };
 
+// Online mode (mcs_run with a finite horizon, mcs_append_jobs): one record per
+// cluster carried between horizons, plus the node image (the LDS layout of nodes[]) and the running
+// slots.  valid == 0 starts the cluster from its spec at t = 0.
+struct OnlineState {
+    uint32_t valid;
+    uint32_t t;       // the next loop iteration's time (not yet executed)
+    uint32_t cursor;  // FIFO: ready cursor r; DELAY: Level0 head h
+    uint32_t aux;     // FIFO: have_w (job r is the WaitQueue head); DELAY: len(Level1)
+    uint32_t flags;
+    uint32_t pool;    // slot rows saved in the slot image (rows >= pool are free)
+    uint32_t placed, waited, peak, used, n_iter, n_rel, placed_l1, peak_l1;  // DELAY: waited = moved
+    unsigned long long l1_t, mv_a, wsum;  // DELAY WaitTime sums (mcs_delay.hip)
+};
+constexpr uint32_t kSlotImg = 2u * kMaxPool * kWave;  // u64 words of one cluster's slot image
+
+struct OnlineArgs {  // read only by the HOR kernel variants
+    const uint32_t* job_cnt;   // jobs in each cluster's segment (job_off = segment starts)
+    const OnlineState* st_in;  // state at the start of this horizon (read only: reruns reuse it)
+    OnlineState* st_out;
+    const unsigned long long* img_in;  // node image, img_stride words per cluster
+    unsigned long long* img_out;
+    const unsigned long long* slot_in;  // slot image: kSlotImg words per cluster ([cm rows][nf rows])
+    unsigned long long* slot_out;
+    uint32_t img_stride;
+    uint32_t t_hor;  // stop before any iteration at t >= t_hor; kEmpty = drain
+};
+
 struct FifoArgs {
     const uint2* node_free0;
     const uint32_t* node_off;
@@ -52,6 +81,7 @@ struct FifoArgs {
     mcs_cluster_stats* cstats;
     Totals* totals;
     GenArgs gen;
+    OnlineArgs on;
     uint32_t n_items;
 };
 
@@ -70,11 +100,13 @@ struct DelayArgs {
     mcs_delay_cluster_stats* dstats;
     Totals* totals;
     GenArgs gen;
+    OnlineArgs on;
     uint32_t max_wait_s;
     uint32_t n_items;
 };
 
-hipError_t launch_delay(const DelayArgs& a, int npl, int pool, hipStream_t s);  // mcs_delay.hip
+// hor: the online variant (OnlineArgs; records streamed, never fused)
+hipError_t launch_delay(const DelayArgs& a, int npl, int pool, bool hor, hipStream_t s);  // mcs_delay.hip
 
 struct StateArgs {  // the ClusterState reduction over a run's placements (mcs_state.hip)
     const uint32_t* node_off;
@@ -92,7 +124,7 @@ struct StateArgs {  // the ClusterState reduction over a run's placements (mcs_s
 hipError_t launch_state(const StateArgs& a, uint32_t max_n, hipStream_t s);  // mcs_state.hip
 
 // Launchers (mcs_kernels.hip).  Return hipSuccess or the launch error.
-hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, hipStream_t s);
+hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, bool hor, hipStream_t s);
 bool fifo_variant_exists(int npl, int pool);
 hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t* max_c,
                             const uint32_t* max_m, uint32_t n_clusters, uint64_t seed,
@@ -100,6 +132,9 @@ hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t
 hipError_t launch_gen_arrivals(uint4* jobs, const uint64_t* job_off, uint32_t n_clusters,
                                uint64_t seed, uint32_t mode, double exp_neg_lambda,
                                uint32_t cluster_base, hipStream_t s);
+hipError_t launch_gen_bound(const uint64_t* job_off, uint32_t n_clusters, uint64_t seed, uint32_t mode,
+                            double exp_neg_lambda, uint32_t cluster_base, unsigned long long* last,
+                            hipStream_t s);
 hipError_t launch_schedule_one(uint32_t* live_c, uint32_t* live_m, uint32_t n, uint32_t c,
                                uint32_t m, int32_t* out_node, hipStream_t s);
 hipError_t launch_lend_check(const uint32_t* live_c, const uint32_t* live_m, uint32_t n,

@@ -41,9 +41,14 @@
 
 namespace mcs {
 
-template <int NPL, int P, bool GEN>
+// HOR: the online variant.  The cluster resumes from the OnlineState, node image
+// and slot image of the previous horizon (or its spec when the state is not valid), runs every
+// iteration at t < a.on.t_hor, and saves them again; job counts come from a.on.job_cnt.  The
+// one-shot variant (HOR = false) is the batch hot path and does none of this.
+template <int NPL, int P, bool GEN, bool HOR>
 __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     static_assert(P <= 32, "free-row mask is one u32 per lane");
+    static_assert(!(HOR && GEN), "online runs stream records");
     const uint32_t item = blockIdx.x;
     const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
     const uint32_t lane = threadIdx.x;
@@ -75,7 +80,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
 
     // ---- job stream ----
     const uint64_t j0 = a.job_off[ci];
-    const uint32_t J = (uint32_t)(a.job_off[ci + 1] - j0);
+    const uint32_t J = HOR ? a.on.job_cnt[ci] : (uint32_t)(a.job_off[ci + 1] - j0);
     const uint4* __restrict__ jobs = GEN ? nullptr : a.jobs + j0;
     int32_t* __restrict__ o_node = a.out_node + j0;
     uint32_t* __restrict__ o_start = a.out_start + j0;
@@ -102,23 +107,68 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
 #pragma unroll
     for (int p = 0; p < P; ++p) pay_nf[p * kWave + lane] = (uint64_t)kEmpty << 32;  // free: never expires
 
-    uint32_t cb = 0;
-    uint4 nxt = load_batch(0);
-    // wait for the first batch here: the only load pending at the pass loop's entry is then the
-    // prefetch, which the loop never reads, so the waitcnt pass does not flush it at every batch
-    asm volatile("" ::"v"(nxt.x), "v"(nxt.y), "v"(nxt.z), "v"(nxt.w));
-
     uint32_t t = 0, r = 0, minf = kEmpty, flags = 0;
     // Counters that no decision reads live in VGPRs (the asm hides their uniformity): the CU's
     // one scalar unit is shared by 16 cluster waves and is the scarcer issue resource.
     uint32_t used = 0, peak = 0, waited = 0, placed = 0;
     uint32_t n_iter = 0, n_rel = 0;  // diagnostics: loop passes, release scans
-    asm volatile("" : "+v"(used), "+v"(peak), "+v"(waited), "+v"(placed), "+v"(n_iter), "+v"(n_rel));
     // have_w: the job at the ready cursor r already failed once and is the WaitQueue head
     // (|WaitQueue| <= 1, scheduler.go:264-268), so the candidate is always job r
     uint32_t have_w = 0u;
     int32_t on = -1;
     uint32_t os = kEmpty, of = kEmpty;
+    bool live = true;  // the loop runs (online: not parked, not stopped for good)
+    uint32_t r_in = 0;
+    if constexpr (HOR) {  // resume from the previous horizon
+        const OnlineState st = a.on.st_in[ci];
+        if (st.valid) {
+            const unsigned long long* img = a.on.img_in + (size_t)ci * a.on.img_stride;
+#pragma unroll
+            for (int c = 0; c < NPL; ++c) nodes[c * kWave + lane] = img[c * kWave + lane];
+            const unsigned long long* sl = a.on.slot_in + (size_t)ci * kSlotImg;
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                if ((uint32_t)p < st.pool) {
+                    const uint64_t nf = sl[(kMaxPool + p) * kWave + lane];
+                    pay_cm[p * kWave + lane] = sl[p * kWave + lane];
+                    pay_nf[p * kWave + lane] = nf;
+                    const uint32_t f = (uint32_t)(nf >> 32);
+                    if (f != kEmpty) {
+                        frm &= ~(1u << p);
+                        lmin = f < lmin ? f : lmin;
+                    }
+                }
+            }
+            minf = wave_min_u32(lmin);
+            t = st.t;
+            r = st.cursor;
+            have_w = st.aux;
+            flags = st.flags;
+            placed = st.placed;
+            waited = st.waited;
+            peak = st.peak;
+            used = st.used;
+            n_iter = st.n_iter;
+            n_rel = st.n_rel;
+        }
+        r_in = r;
+        // a deadlocked head blocks the cluster for good (nothing runs, nothing can overtake it);
+        // a clock overflow is final; a parked cluster waits for jobs; the horizon may be reached
+        live = !(flags & (MCS_FLAG_DEADLOCK | MCS_FLAG_CLOCK_OVERFLOW)) && r < J && t < a.on.t_hor;
+        // the register result batch holds the rows already decided in the current batch
+        const uint32_t i = (r & ~63u) + lane;
+        on = o_node[i];
+        os = o_start[i];
+        of = o_finish[i];
+    }
+    asm volatile("" : "+v"(used), "+v"(peak), "+v"(waited), "+v"(placed), "+v"(n_iter), "+v"(n_rel));
+
+    const uint32_t cb0 = HOR ? (r & ~63u) : 0u;
+    uint32_t cb = cb0;
+    uint4 nxt = load_batch(cb0);
+    // wait for the first batch here: the only load pending at the pass loop's entry is then the
+    // prefetch, which the loop never reads, so the waitcnt pass does not flush it at every batch
+    asm volatile("" ::"v"(nxt.x), "v"(nxt.y), "v"(nxt.z), "v"(nxt.w));
 
     // release every running job with finish <= t (cluster.go:153-157; A.2 step 1).  Row by row:
     // the expired test of row p over all lanes is one compare whose lane mask drives both the
@@ -169,12 +219,13 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     // One pass = one decision; the loop has a single exit (the structurizer then needs no flow
     // copies of the loop-carried registers).  rend bounds the ready cursor of the inner loop: the
     // end of the current batch, or 0 once the run stops, so one scalar compare ends both loops.
-    uint32_t rend;
+    uint32_t rend = 0u;
     // node free vectors for the next first fit, read at the end of the previous pass (after its
     // commit and releases) so the LDS latency overlaps the record broadcast of the next pass
     uint64_t nvr[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) nvr[k] = nodes[k * kWave + lane];
+    if (live) {
     // Outer loop: one 64-record batch; inner loop: the passes whose ready cursor is in it.  The
     // batch registers change only here, once per batch, so no pass copies them (a per-pass
     // conditional swap made LLVM copy both buffers and wait for the prefetch on every pass).
@@ -183,7 +234,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     // memory operations issued a whole batch earlier, never stores still in flight to HBM.
     do {
     const uint4 cur = nxt;
-    if (cb != 0u) {  // a full batch: every lane's job cb - 64 + lane < J, no mask
+    if (cb != cb0) {  // a full batch: every lane's job cb - 64 + lane < J, no mask
         const uint32_t i = cb - kWave + lane;
         __builtin_nontemporal_store(on, o_node + i);
         __builtin_nontemporal_store(os, o_start + i);
@@ -215,14 +266,20 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                 bc = ((uint32_t)v >= jc && (uint32_t)(v >> 32) >= jm) ? (uint32_t)c : bc;
             }
             const uint64_t fit = __ballot(bc < (uint32_t)NPL) & vmask;
-            if (fit) {
+            const uint32_t fin = t + jd;
+            if (fit && fin + 1u <= t) {
+                // the finish time wraps the u32 seconds clock or hits the kEmpty sentinel (D8
+                // range exceeded; the host bound of mcs_submit_jobs / mcs_generate_jobs keeps
+                // checked inputs away from it): stop, flagged; job r stays undecided
+                flags |= MCS_FLAG_CLOCK_OVERFLOW;
+                rend = 0u;
+            } else if (fit) {
                 const uint32_t fl = (uint32_t)__builtin_ctzll(fit);
                 const uint32_t fch = readlane(bc, fl);
                 const uint32_t k = fl * NPL + fch;        // the node (Go index)
                 const uint32_t kx = fch * kWave + fl;     // its place in nodes[]
                 // placement record, 64 jobs per register batch (jobs are placed in job order)
                 const uint32_t ol = r & 63u;
-                const uint32_t fin = t + jd;
                 // lane ol of the batch takes (k, t, fin): three v_writelane (lane select in m0,
                 // the one scalar operand gfx950 allows beside the data SGPR)
                 // m0 is reserved to the compiler, which uses it nowhere in these kernels
@@ -290,6 +347,9 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
             } else {
                 t = tn;
                 if (minf <= t) release();
+                if constexpr (HOR) {
+                    if (t >= a.on.t_hor) rend = 0u;  // the horizon: resume here next time
+                }
             }
         }
 #pragma unroll
@@ -297,9 +357,11 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     } while (r < rend);
     cb += kWave;
     } while (rend != 0u);
+    }  // live
 
-    if (flags & MCS_FLAG_DEADLOCK) {
-        // jobs r..J-1 are never placed (the Go loop retries the head forever)
+    if (flags & (MCS_FLAG_DEADLOCK | MCS_FLAG_CLOCK_OVERFLOW)) {
+        // jobs r..J-1 are never placed (deadlock: the Go loop retries the head forever) or were
+        // not decided before the clock left the u32 range (the run fails with MCS_E_RANGE)
         const uint32_t b0 = r & ~63u;
         if (lane >= (r & 63u)) {
             on = MCS_NODE_UNPLACED;
@@ -311,9 +373,51 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         os = MCS_TIME_NONE;
         of = MCS_TIME_NONE;
         for (uint32_t b = b0 + kWave; b < J; b += kWave) flush(b);
-    } else if (!(flags & (MCS_FLAG_OVERFLOW | MCS_FLAG_CLOCK_OVERFLOW)) && J > 0u &&
+    } else if (HOR) {
+        // online: the batch holding the last decision of this horizon, lanes decided so far (a
+        // batch boundary reached in the same pass is rewritten with the same values)
+        if (!(flags & MCS_FLAG_OVERFLOW) && r > r_in) {
+            const uint32_t i = ((r - 1u) & ~63u) + lane;
+            if (i < r) {
+                __builtin_nontemporal_store(on, o_node + i);
+                __builtin_nontemporal_store(os, o_start + i);
+                __builtin_nontemporal_store(of, o_finish + i);
+            }
+        }
+    } else if (!(flags & MCS_FLAG_OVERFLOW) && J > 0u &&
                ((J - 1u) & 63u) != 63u) {
         flush((J - 1u) & ~63u);
+    }
+
+    if constexpr (HOR) {  // save the state the next horizon resumes from (rerun on overflow)
+        if (!(flags & MCS_FLAG_OVERFLOW)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // other lanes' LDS atomics
+            unsigned long long* img = a.on.img_out + (size_t)ci * a.on.img_stride;
+#pragma unroll
+            for (int c = 0; c < NPL; ++c) img[c * kWave + lane] = nodes[c * kWave + lane];
+            unsigned long long* sl = a.on.slot_out + (size_t)ci * kSlotImg;
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                sl[p * kWave + lane] = pay_cm[p * kWave + lane];
+                sl[(kMaxPool + p) * kWave + lane] = pay_nf[p * kWave + lane];
+            }
+            if (lane == 0) {
+                OnlineState st{};
+                st.valid = 1u;
+                st.t = t;
+                st.cursor = r;
+                st.aux = have_w;
+                st.flags = flags;
+                st.pool = (uint32_t)P;
+                st.placed = placed;
+                st.waited = waited;
+                st.peak = peak;
+                st.used = used;
+                st.n_iter = n_iter;
+                st.n_rel = n_rel;
+                a.on.st_out[ci] = st;
+            }
+        }
     }
 
     if (lane == 0) {
@@ -332,39 +436,42 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         } else {
             atomicAdd(&a.totals->placed, (unsigned long long)placed);
             atomicAdd(&a.totals->waited, (unsigned long long)waited);
-            atomicAdd(&a.totals->unplaced, (unsigned long long)(J - placed));
+            // online: jobs not decided yet are pending, not unplaced
+            const bool final_ = !HOR || (flags & (MCS_FLAG_DEADLOCK | MCS_FLAG_CLOCK_OVERFLOW));
+            if (final_) atomicAdd(&a.totals->unplaced, (unsigned long long)(J - placed));
             if (flags & MCS_FLAG_DEADLOCK) atomicAdd(&a.totals->deadlocked, 1u);
+            if (flags & MCS_FLAG_CLOCK_OVERFLOW) atomicAdd(&a.totals->clock_overflowed, 1u);
         }
     }
 }
 
 // ---- variant table ------------------------------------------------------------------------------
-template <int NPL, int P, bool GEN>
+template <int NPL, int P, bool GEN, bool HOR>
 static hipError_t launch_one(const FifoArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((fifo_kernel<NPL, P, GEN>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL((fifo_kernel<NPL, P, GEN, HOR>), dim3(a.n_items), dim3(kWave), 0, s, a);
     return hipGetLastError();
 }
 
-template <int NPL, bool GEN>
+template <int NPL, bool GEN, bool HOR>
 static hipError_t launch_npl(const FifoArgs& a, int pool, hipStream_t s) {
     switch (pool) {
-        case 2: return launch_one<NPL, 2, GEN>(a, s);
-        case 4: return launch_one<NPL, 4, GEN>(a, s);
-        case 8: return launch_one<NPL, 8, GEN>(a, s);
-        case 16: return launch_one<NPL, 16, GEN>(a, s);
-        case 32: return launch_one<NPL, 32, GEN>(a, s);
+        case 2: return launch_one<NPL, 2, GEN, HOR>(a, s);
+        case 4: return launch_one<NPL, 4, GEN, HOR>(a, s);
+        case 8: return launch_one<NPL, 8, GEN, HOR>(a, s);
+        case 16: return launch_one<NPL, 16, GEN, HOR>(a, s);
+        case 32: return launch_one<NPL, 32, GEN, HOR>(a, s);
         default: return hipErrorInvalidValue;
     }
 }
 
-template <bool GEN>
+template <bool GEN, bool HOR>
 static hipError_t launch_fifo_gen(const FifoArgs& a, int npl, int pool, hipStream_t s) {
     switch (npl) {
-        case 1: return launch_npl<1, GEN>(a, pool, s);
-        case 2: return launch_npl<2, GEN>(a, pool, s);
-        case 4: return launch_npl<4, GEN>(a, pool, s);
-        case 8: return launch_npl<8, GEN>(a, pool, s);
-        case 16: return launch_npl<16, GEN>(a, pool, s);
+        case 1: return launch_npl<1, GEN, HOR>(a, pool, s);
+        case 2: return launch_npl<2, GEN, HOR>(a, pool, s);
+        case 4: return launch_npl<4, GEN, HOR>(a, pool, s);
+        case 8: return launch_npl<8, GEN, HOR>(a, pool, s);
+        case 16: return launch_npl<16, GEN, HOR>(a, pool, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -375,9 +482,11 @@ bool fifo_variant_exists(int npl, int pool) {
     return np && pp;
 }
 
-hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, hipStream_t s) {
+hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, bool hor, hipStream_t s) {
     if (a.n_items == 0) return hipSuccess;
-    return a.gen.on ? launch_fifo_gen<true>(a, npl, pool, s) : launch_fifo_gen<false>(a, npl, pool, s);
+    if (hor) return a.gen.on ? hipErrorInvalidValue : launch_fifo_gen<false, true>(a, npl, pool, s);
+    return a.gen.on ? launch_fifo_gen<true, false>(a, npl, pool, s)
+                    : launch_fifo_gen<false, false>(a, npl, pool, s);
 }
 
 // ---- device job-stream synthesis (mcs_gen.h; bit-identical to the host generator) -------------
@@ -428,6 +537,44 @@ __global__ __launch_bounds__(64) void gen_arrivals_kernel(uint4* jobs, const uin
             T += 1u;
         }
     }
+}
+
+// last arrival of every cluster's synthetic stream (the scan of mcs_gen_arrivals in 64-bit time,
+// nothing stored): the clock-range check of a fused stream in mcs_generate_jobs
+__global__ __launch_bounds__(64) void gen_bound_kernel(const uint64_t* job_off, uint32_t n_clusters,
+                                                      uint64_t seed, uint32_t mode, double enl,
+                                                      uint32_t base, unsigned long long* last) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_clusters) return;
+    const uint64_t J = job_off[c + 1] - job_off[c];
+    const uint64_t akey = mcs_arrival_key(mcs_cluster_key(seed, base + c));
+    uint64_t j = 0, period = 0, T = 0, lastT = 0;
+    while (j < J) {
+        const uint32_t n = mcs_poisson(akey, period++, enl);
+        if (mode == 0u) {
+            if (n == 0u) {
+                T += 60u;
+                continue;
+            }
+            const uint64_t take = (J - j) < n ? (J - j) : n;
+            lastT = T + (take - 1u) * (60u / n);
+            T += (uint64_t)n * (60u / n);
+            j += take;
+        } else {
+            if (n) lastT = T;
+            j += n;
+            T += 1u;
+        }
+    }
+    last[c] = lastT;
+}
+
+hipError_t launch_gen_bound(const uint64_t* job_off, uint32_t n_clusters, uint64_t seed, uint32_t mode,
+                            double exp_neg_lambda, uint32_t base, unsigned long long* last, hipStream_t s) {
+    if (n_clusters == 0) return hipSuccess;
+    hipLaunchKernelGGL(gen_bound_kernel, dim3((n_clusters + 63) / 64), dim3(64), 0, s, job_off, n_clusters,
+                       seed, mode, exp_neg_lambda, base, last);
+    return hipGetLastError();
 }
 
 hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t* max_c,

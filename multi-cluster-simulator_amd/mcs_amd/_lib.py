@@ -21,6 +21,7 @@ MCS_E_HIP = -3
 MCS_E_RCCL = -4
 MCS_E_STATE = -5
 MCS_E_NOMEM = -6
+MCS_E_RANGE = -7
 
 MCS_NODE_UNPLACED = -1
 MCS_NODE_BORROWED = -2
@@ -47,6 +48,7 @@ STATUS_NAMES = {
     MCS_E_RCCL: "MCS_E_RCCL",
     MCS_E_STATE: "MCS_E_STATE",
     MCS_E_NOMEM: "MCS_E_NOMEM",
+    MCS_E_RANGE: "MCS_E_RANGE",
 }
 
 
@@ -72,7 +74,8 @@ class mcs_config(C.Structure):
         ("lent_queue_cap", C.c_uint32),
         ("t_max_s", C.c_uint32),
         ("max_wait_s", C.c_uint32),
-        ("reserved", C.c_uint32 * 2),
+        ("unchecked_horizon", C.c_uint32),
+        ("reserved", C.c_uint32 * 1),
     ]
 
 
@@ -101,6 +104,9 @@ class mcs_stats(C.Structure):
         ("slot_pool", C.c_uint32),
         ("kernel_ms", C.c_double),
         ("wall_ms", C.c_double),
+        ("pending", C.c_uint64),
+        ("t_horizon", C.c_uint32),
+        ("online", C.c_uint32),
     ]
 
 
@@ -203,6 +209,9 @@ SIGNATURES = [
     ("mcs_generate_jobs", C.c_int, [vp, C.POINTER(mcs_gen_params), C.c_uint64]),
     ("mcs_read_jobs", C.c_int, [vp, u32p, u32p, u32p, u32p]),
     ("mcs_run", C.c_int, [vp, C.c_uint32, C.POINTER(mcs_stats)]),
+    ("mcs_append_jobs", C.c_int, [vp, u32p, u32p, u32p, u32p, u64p]),
+    ("mcs_rewind", C.c_int, [vp]),
+    ("mcs_read_job_offsets", C.c_int, [vp, u64p]),
     ("mcs_read_placements", C.c_int, [vp, i32p, u32p, u32p]),
     ("mcs_read_cluster_stats", C.c_int, [vp, C.POINTER(mcs_cluster_stats), C.c_uint32]),
     ("mcs_read_delay_stats", C.c_int, [vp, C.POINTER(mcs_delay_cluster_stats), C.c_uint32]),

@@ -88,7 +88,10 @@ class JobStreams:
         return slice(int(self.job_off[k]), int(self.job_off[k + 1]))
 
 
-def gen_streams_host(params: GenParams, arrays: ClusterArrays, jobs_per_cluster: int) -> JobStreams:
+def gen_streams_host(params: GenParams, arrays: ClusterArrays, jobs_per_cluster: int, base: int = 0) -> JobStreams:
+    """Host streams of clusters base .. base + n - 1 of a (possibly sharded) system: cluster k of
+    `arrays` is keyed by its global index base + k, as the device generator keys it after
+    mcs_set_shard (gen.base = rank * C)."""
     n = arrays.n_clusters
     tot = n * jobs_per_cluster
     out = [np.empty(tot, np.uint32) for _ in range(4)]
@@ -96,7 +99,7 @@ def gen_streams_host(params: GenParams, arrays: ClusterArrays, jobs_per_cluster:
         sl = arrays.nodes_of(k)
         mc = params.max_cores or int(arrays.cap_c[sl].max(initial=0))
         mm = params.max_mem or int(arrays.cap_m[sl].max(initial=0))
-        a, d, c, m = gen_cluster_host(params, k, mc, mm, jobs_per_cluster)
+        a, d, c, m = gen_cluster_host(params, base + k, mc, mm, jobs_per_cluster)
         s = slice(k * jobs_per_cluster, (k + 1) * jobs_per_cluster)
         out[0][s], out[1][s], out[2][s], out[3][s] = a, d, c, m
     off = np.arange(n + 1, dtype=np.uint64) * jobs_per_cluster
@@ -115,6 +118,14 @@ class RunStats:
     slot_pool: int
     kernel_ms: float
     wall_ms: float
+    pending: int = 0      # online: jobs not decided yet
+    t_horizon: int = L.MCS_TIME_NONE
+    online: bool = False
+
+    @classmethod
+    def from_c(cls, st: "L.mcs_stats") -> "RunStats":
+        return cls(st.jobs, st.placed, st.waited, st.unplaced, st.clusters, st.deadlocked, st.escalations,
+                   st.slot_pool, st.kernel_ms, st.wall_ms, st.pending, st.t_horizon, bool(st.online))
 
 
 CLUSTER_STATS_DTYPE = np.dtype([("t_end", "<u4"), ("placed", "<u4"), ("waited", "<u4"),
@@ -272,8 +283,7 @@ class Engine:
     def trade_end(self) -> RunStats:
         st = L.mcs_stats()
         self._c(L.lib().mcs_trade_end(self._h, C.byref(st)))
-        return RunStats(st.jobs, st.placed, st.waited, st.unplaced, st.clusters, st.deadlocked,
-                        st.escalations, st.slot_pool, st.kernel_ms, st.wall_ms)
+        return RunStats.from_c(st)
 
     def trade_stats(self) -> dict:
         ts = L.mcs_trade_stats()
@@ -336,11 +346,36 @@ class Engine:
         return out
 
     # -- the hot path ---------------------------------------------------------------------------
-    def run(self) -> RunStats:
+    def run(self, t_end: Optional[int] = None) -> RunStats:
+        """mcs_run: a batch run (t_end None, no online session), or online mode:
+        every decision at simulated seconds < t_end, or with t_end None a drain of every job
+        appended so far."""
         st = L.mcs_stats()
-        self._c(L.lib().mcs_run(self._h, L.MCS_TIME_NONE, C.byref(st)))
-        return RunStats(st.jobs, st.placed, st.waited, st.unplaced, st.clusters, st.deadlocked,
-                        st.escalations, st.slot_pool, st.kernel_ms, st.wall_ms)
+        self._c(L.lib().mcs_run(self._h, L.MCS_TIME_NONE if t_end is None else int(t_end), C.byref(st)))
+        return RunStats.from_c(st)
+
+    def run_status(self, t_end: Optional[int] = None) -> Tuple[int, RunStats]:
+        """mcs_run returning (status, stats) without raising (e.g. MCS_E_RANGE, results readable)."""
+        st = L.mcs_stats()
+        rc = L.lib().mcs_run(self._h, L.MCS_TIME_NONE if t_end is None else int(t_end), C.byref(st))
+        return rc, RunStats.from_c(st)
+
+    def append_jobs(self, s: JobStreams):
+        """mcs_append_jobs: s.job_off is the CSR of the APPENDED jobs per cluster (online mode)."""
+        a = [np.ascontiguousarray(x, dtype=np.uint32) for x in (s.arrival, s.dur, s.cores, s.mem)]
+        off = np.ascontiguousarray(s.job_off, dtype=np.uint64)
+        self._c(L.lib().mcs_append_jobs(self._h, *[L.ptr(x, C.c_uint32) for x in a], L.ptr(off, C.c_uint64)))
+        self.job_off = self.job_offsets()
+
+    def rewind(self):
+        """mcs_rewind: restart the online session at t = 0 with every job so far."""
+        self._c(L.lib().mcs_rewind(self._h))
+
+    def job_offsets(self) -> np.ndarray:
+        """mcs_read_job_offsets: dense CSR of the current streams."""
+        off = np.zeros(self.num_clusters + 1, np.uint64)
+        self._c(L.lib().mcs_read_job_offsets(self._h, L.ptr(off, C.c_uint64)))
+        return off
 
     def placements(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         n = self.num_jobs

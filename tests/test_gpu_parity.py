@@ -135,10 +135,10 @@ def test_config4_shape_reduced(engine, kind):
     assert_parity(arrays, streams, node, start, fin, cs)
 
 
-def test_config4_full_size_sampled_parity(engine):
+def test_config4_full_size_parity(engine):
     """BASELINE config 4 at full size on one GPU: 4096 clusters x 256 nodes x 16384 jobs (64M
-    placements).  Clusters are independent, so bit-exact parity is checked on a sample of clusters
-    against the oracle, and size-independent properties on all of them."""
+    placements), EVERY cluster bit-exact against the oracle (OpenMP over clusters, a few seconds of
+    host time), plus size-independent properties."""
     from mcs_amd.engine import scaled_lambda
 
     n, J = 4096, 16384
@@ -158,15 +158,8 @@ def test_config4_full_size_sampled_parity(engine):
     s2 = start.reshape(n, J).astype(np.int64)
     assert (np.diff(s2, axis=1) >= 0).all()  # strict FIFO: starts non-decreasing in job order
     assert (cs["placed"] == J).all()
-    # bit-exact on a sample of clusters
-    sample = [0, 1, 7, 513, 2047, 3000, 4095]
-    for k in sample:
-        js = jobs.of(k)
-        on, os_, of, ost = O.fifo_run(arrays.free_c[:256], arrays.free_m[:256], jobs.arrival[js], jobs.dur[js],
-                                      jobs.cores[js], jobs.mem[js])
-        np.testing.assert_array_equal(node[js], on, err_msg=f"cluster {k}")
-        np.testing.assert_array_equal(start[js], os_, err_msg=f"cluster {k}")
-        assert cs[k]["t_end"] == ost["t_end"] and cs[k]["waited"] == ost["waited"]
+    # bit-exact on every cluster
+    assert_parity(arrays, jobs, node, start, fin, cs, n_threads=16)
     # no node is ever over-committed: the ClusterState reduction at sampled seconds (a wrapped
     # free counter would show as utilization > 1)
     for t in np.linspace(0, int(fin.max()), 7).astype(int):
@@ -175,10 +168,26 @@ def test_config4_full_size_sampled_parity(engine):
         assert (cst["cores_utilization"] >= 0.0).all() and (cst["memory_utilization"] >= 0.0).all(), t
 
 
-def test_config4_delay_fused_full_size_properties():
-    """C4 at full size under DELAY with the stream synthesised in the kernel: every job is placed
-    exactly once after its arrival, no node is over-committed, and sampled clusters are bit-exact
-    against the oracle over the host generator's streams."""
+def test_config4_strong_shards_two_ranks_one_gpu():
+    """bench.py --shard strong on two ranks (two processes, two engines on device 0): each holds a
+    contiguous half of one system, generation keyed by the global cluster index; the concatenated
+    outputs equal one engine holding every cluster and the oracle of the whole system."""
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29587")
+    r = subprocess.run([sys.executable, os.path.join(here, "c4_strong_2rank.py")], env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "C4-STRONG-2RANK OK" in r.stdout
+
+
+def test_config4_delay_fused_full_size_parity():
+    """C4 at full size under DELAY with the stream synthesised in the kernel: every cluster
+    bit-exact against the DELAY oracle over the same streams (materialised on demand by
+    mcs_read_jobs, which equals the host generator), every job placed exactly once after its
+    arrival, and no node over-committed."""
     from mcs_amd.engine import gen_cluster_host, scaled_lambda
 
     n, J = 4096, 16384
@@ -191,19 +200,25 @@ def test_config4_delay_fused_full_size_properties():
         assert st.placed == n * J and st.unplaced == 0
         node, start, fin = eng.placements()
         ds = eng.delay_stats()
+        cs = eng.cluster_stats()
         assert (node >= 0).all() and (node < 256).all()
         for t in np.linspace(0, int(fin.max()), 5).astype(int):
             cst = eng.cluster_states(int(t))
             assert (cst["cores_utilization"] <= 1.0).all() and (cst["memory_utilization"] <= 1.0).all(), t
-        for k in [0, 2049, 4095]:
-            a, d, c, m = gen_cluster_host(gp, k, 32, 24000, J)
-            js = slice(k * J, (k + 1) * J)
-            assert (start[js] >= a).all()
-            np.testing.assert_array_equal(fin[js], start[js] + d)
-            on, os_, of, ost = O.delay_run(arrays.free_c[:256], arrays.free_m[:256], a, d, c, m)
-            np.testing.assert_array_equal(node[js], on, err_msg=f"cluster {k}")
-            np.testing.assert_array_equal(start[js], os_, err_msg=f"cluster {k}")
-            assert ds[k]["total_wait_ms"] == ost["total_wait_ms"]
+        jobs = eng.read_jobs()
+    for k in (0, 2049, 4095):  # the materialised stream is the host generator's
+        a, d, c, m = gen_cluster_host(gp, k, 32, 24000, J)
+        js = jobs.of(k)
+        assert np.array_equal(jobs.arrival[js], a) and np.array_equal(jobs.dur[js], d)
+        assert np.array_equal(jobs.cores[js], c) and np.array_equal(jobs.mem[js], m)
+    assert (start >= jobs.arrival).all()
+    np.testing.assert_array_equal(fin, start + jobs.dur)
+    on, os_, of, osd = O.delay_run_batch(arrays, jobs, n_threads=16)
+    bad = np.flatnonzero((node != on) | (start != os_) | (fin != of))
+    assert bad.size == 0, f"{bad.size} mismatches, first jobs {bad[:5]}"
+    np.testing.assert_array_equal(ds["total_wait_ms"], osd["total_wait_ms"])
+    np.testing.assert_array_equal(ds["moved_l1"], osd["moved_l1"])
+    np.testing.assert_array_equal(cs["t_end"], osd["t_end"])
 
 
 def test_heterogeneous_cluster_sizes(engine):
@@ -265,3 +280,31 @@ def test_extreme_values(engine):
                    np.array([0, len(jobs)], np.uint64))
     node, start, fin, st, cs = run_engine(engine, arrays, s)
     assert_parity(arrays, s, node, start, fin, cs, n_threads=1)
+
+
+@pytest.mark.parametrize("policy", ["FIFO", "DELAY"])
+def test_every_kernel_variant(policy):
+    """Every compiled variant of the placement kernel — nodes per lane NPL 1..16 (the largest
+    cluster: 64..1024 nodes) x slot rows 2..32 (cfg.slot_pool) x streamed / fused records — against
+    the oracle (the library's kernels are built with LLVM's iterative ILP scheduler: each variant is
+    its own schedule)."""
+    from mcs_amd.engine import scaled_lambda
+
+    for nn in (64, 128, 256, 512, 1024):
+        arrays = pack_clusters([uniform_cluster(nn), uniform_cluster(max(1, nn // 3)), uniform_cluster(5)])
+        lam = scaled_lambda(nn, load=1.1)
+        gp = GenParams(seed=nn, arrival_mode=1, lam=lam, max_cores=32, max_mem=24000)
+        streams = gen_streams_host(gp, arrays, 1200)
+        oracle = (O.delay_run_batch if policy == "DELAY" else O.fifo_run_batch)(arrays, streams, n_threads=8)
+        for pool in (2, 4, 8, 16, 32):
+            for fused in (False, True):
+                with Engine(0, slot_pool=pool, policy=policy) as eng:
+                    eng.load_clusters(arrays)
+                    gp.fused = fused
+                    eng.generate_jobs(gp, 1200)
+                    eng.run()
+                    node, start, fin = eng.placements()
+                tag = f"nodes {nn} pool {pool} fused {fused}"
+                np.testing.assert_array_equal(node, oracle[0], err_msg=tag)
+                np.testing.assert_array_equal(start, oracle[1], err_msg=tag)
+                np.testing.assert_array_equal(fin, oracle[2], err_msg=tag)

@@ -139,3 +139,43 @@ def test_gpu_trade_rccl_loop_world1():
     assert got["trades"].tobytes() == want["trades"].tobytes()
     assert got["vn"].tolist() == want["virtual_nodes"].tolist()
     assert got["ts"]["t_final"] == want["tstats"]["t_final"]
+
+
+def test_gpu_trade_config5_full_size():
+    """BASELINE config 5 at its stated size: 64 clusters x 256 nodes x 156,250 jobs (10M jobs),
+    FIFO + borrow + trader in lock-step, against the trading oracle of the whole system (about a
+    minute of host time).  Every own placement, every lent run, every trade and the final tick."""
+    from mcs_amd import GenParams, replicate, uniform_cluster
+    from mcs_amd.engine import scaled_lambda
+
+    C, J = 64, 156_250
+    arrays = replicate(uniform_cluster(256), C)
+    gp = GenParams(seed=0x4D43535F53494D31, arrival_mode=1, lam=scaled_lambda(256, load=0.9))
+    with Engine(0, borrow=True, trader=True) as eng:
+        eng.load_clusters(arrays)
+        eng.generate_jobs(gp, J)
+        eng.run()
+        node, start, fin = eng.placements()
+        lent = eng.lent()
+        trades = eng.trades()
+        vn = eng.virtual_nodes()
+        ts = eng.trade_stats()
+        streams = eng.read_jobs()
+    assert ts["flags"] == 0, ts["flags"]
+    o = O.trade_run(arrays, streams, lent_cap=len(lent) + 1, trade_cap=len(trades) + 1)
+    assert o["n_lent"] == len(lent) and o["n_trades"] == len(trades)
+    for k, g in (("node", node), ("start", start), ("finish", fin)):
+        bad = np.flatnonzero(g != o[k])
+        assert bad.size == 0, f"{k}: {bad.size} mismatches, first jobs {bad[:5]}"
+    ol = o["lent"].copy()
+    ol["job"] -= streams.job_off[ol["borrower"]]  # the ABI's job index is within the borrower's stream
+
+    def canon(x):
+        x = x[np.lexsort((x["job"], x["borrower"], x["lender"], x["start"]))]
+        return [x[f] for f in ("lender", "borrower", "job", "node", "start", "finish")]
+
+    for a, b in zip(canon(lent), canon(ol)):
+        np.testing.assert_array_equal(a, b)
+    assert trade_rows(trades) == trade_rows(o["trades"])
+    np.testing.assert_array_equal(vn, o["virtual_nodes"])
+    assert ts["t_final"] == o["t_final"]

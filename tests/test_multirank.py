@@ -62,6 +62,56 @@ def test_two_rank_gloo_shards_and_aggregation():
     assert h0 != h1  # the two ranks simulated different streams
 
 
+def _strong_worker(rank, world, port, q):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "multi-cluster-simulator_amd"), here]
+    import torch.distributed as dist
+
+    import oracle_ref as O
+    from mcs_amd import GenParams, replicate, uniform_cluster
+    from mcs_amd.engine import gen_streams_host
+    from mcs_amd.shard import shard_range
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    total, J = 10, 400
+    gp = GenParams(seed=99, arrival_mode=1, lam=0.5)
+    lo, hi = shard_range(total, world, rank)
+    arrays = replicate(uniform_cluster(64), hi - lo)
+    streams = gen_streams_host(gp, arrays, J, base=lo)  # keyed by the global cluster index
+    node, st, fi, _ = O.fifo_run_batch(arrays, streams)
+    parts = [None] * world
+    dist.all_gather_object(parts, (node, st, fi))
+    if rank == 0:
+        full = replicate(uniform_cluster(64), total)
+        fs = gen_streams_host(gp, full, J)
+        on, os_, of, _ = O.fifo_run_batch(full, fs)
+        ok = all(np.array_equal(np.concatenate([p[i] for p in parts]), w) for i, w in enumerate((on, os_, of)))
+        q.put(ok)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_strong_shards_concatenate_to_one_system(world):
+    """C4 strong sharding (bench.py --shard strong) on CPU over gloo: every rank simulates the
+    contiguous block shard_range gives it, with streams keyed by the GLOBAL cluster index; the
+    concatenated shard outputs equal the whole system run in one process."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_strong_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert ok
+
+
 def test_rank_seed_and_shard_range():
     assert rank_seed(5, 0) == 5
     assert len({rank_seed(5, r) for r in range(8)}) == 8
