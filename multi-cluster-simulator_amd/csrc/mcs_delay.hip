@@ -126,6 +126,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     //   wacc  per lane: Level0 placements of that lane's batch slots, added at each batch flush;
     //   l1_t  t of every Level1 placement;  mv_a  arrival of every job moved to Level1
     uint64_t wacc = 0, l1_t = 0, mv_a = 0;
+    uint32_t ovf = 0u;  // a finish time left the u32 clock range (recorded in VALU)
     bool live = true;
     if constexpr (HOR) {  // resume from the previous horizon
         const OnlineState st = a.on.st_in[ci];
@@ -170,7 +171,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         live = !(flags & MCS_FLAG_CLOCK_OVERFLOW) && t < a.on.t_hor && (h < J || l1n != 0u);
     }
     asm volatile("" : "+v"(used), "+v"(peak), "+v"(n_iter), "+v"(n_rel), "+v"(placed), "+v"(moved),
-                 "+v"(placed_l1), "+v"(peak_l1), "+v"(l1_t), "+v"(mv_a));
+                 "+v"(placed_l1), "+v"(peak_l1), "+v"(l1_t), "+v"(mv_a), "+v"(ovf));
 
     const uint32_t cb0 = HOR ? (h & ~63u) : 0u;
     uint32_t cb = cb0;
@@ -342,11 +343,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                     const uint32_t jw = readlane((uint32_t)jdv, b);
                     const uint32_t jd = readlane((uint32_t)(jdv >> 32), b);
                     const uint32_t fin = t + jd;
-                    if (fin + 1u <= t) {  // finish leaves the u32 clock (D8): stop, flagged
-                        flags |= MCS_FLAG_CLOCK_OVERFLOW;
-                        stop = 1u;
-                        break;
-                    }
+                    ovf |= (fin + 1u <= t) ? 1u : 0u;  // finish leaves the u32 clock (D8), off the chain
                     if (!commit(k, jc, jm, fin, jd)) {
                         flags |= MCS_FLAG_OVERFLOW;
                         stop = 1u;
@@ -393,10 +390,8 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
             const uint32_t ol = h & 63u;
             if (k != kEmpty) {
                 const uint32_t fin = t + jd;
-                if (fin + 1u <= t) {  // finish leaves the u32 clock (D8): stop, flagged
-                    flags |= MCS_FLAG_CLOCK_OVERFLOW;
-                    stop = 1u;
-                } else if (!commit(k, jc, jm, fin, jd)) {
+                ovf |= (fin + 1u <= t) ? 1u : 0u;  // finish leaves the u32 clock (D8), off the chain
+                if (!commit(k, jc, jm, fin, jd)) {
                     flags |= MCS_FLAG_OVERFLOW;
                     stop = 1u;
                 } else {
@@ -470,6 +465,9 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     cb += kWave;
     }
 
+    // a finish past the u32 clock released its job early: every result of the cluster is void
+    const bool ovf_fin = sgpr(ovf) != 0u;
+    if (ovf_fin) flags |= MCS_FLAG_CLOCK_OVERFLOW;
     if (!(flags & MCS_FLAG_OVERFLOW)) {
         if (h > cb) flush(cb);  // the current batch's decided jobs (earlier batches are stored)
         if (flags & (MCS_FLAG_DEADLOCK | MCS_FLAG_CLOCK_OVERFLOW)) {
@@ -486,7 +484,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
             }
         }
         if (flags & MCS_FLAG_CLOCK_OVERFLOW) {  // and so were the Level0 jobs h..J-1
-            for (uint32_t i = h + lane; i < J; i += kWave) {
+            for (uint32_t i = (ovf_fin ? 0u : h) + lane; i < J; i += kWave) {
                 o_node[i] = MCS_NODE_UNPLACED;
                 o_start[i] = MCS_TIME_NONE;
                 o_finish[i] = MCS_TIME_NONE;

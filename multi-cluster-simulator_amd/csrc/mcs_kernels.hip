@@ -112,6 +112,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     // one scalar unit is shared by 16 cluster waves and is the scarcer issue resource.
     uint32_t used = 0, peak = 0, waited = 0, placed = 0;
     uint32_t n_iter = 0, n_rel = 0;  // diagnostics: loop passes, release scans
+    uint32_t ovf_r = kEmpty;         // first job whose finish left the u32 clock range
     // have_w: the job at the ready cursor r already failed once and is the WaitQueue head
     // (|WaitQueue| <= 1, scheduler.go:264-268), so the candidate is always job r
     uint32_t have_w = 0u;
@@ -161,7 +162,8 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         os = o_start[i];
         of = o_finish[i];
     }
-    asm volatile("" : "+v"(used), "+v"(peak), "+v"(waited), "+v"(placed), "+v"(n_iter), "+v"(n_rel));
+    asm volatile("" : "+v"(used), "+v"(peak), "+v"(waited), "+v"(placed), "+v"(n_iter), "+v"(n_rel),
+                 "+v"(ovf_r));
 
     const uint32_t cb0 = HOR ? (r & ~63u) : 0u;
     uint32_t cb = cb0;
@@ -206,14 +208,6 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         minf = wave_min_u32(lmin);
     };
 
-    auto flush = [&](uint32_t base) __attribute__((always_inline)) {
-        const uint32_t i = base + lane;
-        if (i < J) {
-            __builtin_nontemporal_store(on, o_node + i);
-            __builtin_nontemporal_store(os, o_start + i);
-            __builtin_nontemporal_store(of, o_finish + i);
-        }
-    };
 
     // ---- Scheduler.Fifo (scheduler.go:216-296) ----
     // One pass = one decision; the loop has a single exit (the structurizer then needs no flow
@@ -266,20 +260,14 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                 bc = ((uint32_t)v >= jc && (uint32_t)(v >> 32) >= jm) ? (uint32_t)c : bc;
             }
             const uint64_t fit = __ballot(bc < (uint32_t)NPL) & vmask;
-            const uint32_t fin = t + jd;
-            if (fit && fin + 1u <= t) {
-                // the finish time wraps the u32 seconds clock or hits the kEmpty sentinel (D8
-                // range exceeded; the host bound of mcs_submit_jobs / mcs_generate_jobs keeps
-                // checked inputs away from it): stop, flagged; job r stays undecided
-                flags |= MCS_FLAG_CLOCK_OVERFLOW;
-                rend = 0u;
-            } else if (fit) {
+            if (fit) {
                 const uint32_t fl = (uint32_t)__builtin_ctzll(fit);
                 const uint32_t fch = readlane(bc, fl);
                 const uint32_t k = fl * NPL + fch;        // the node (Go index)
                 const uint32_t kx = fch * kWave + fl;     // its place in nodes[]
                 // placement record, 64 jobs per register batch (jobs are placed in job order)
                 const uint32_t ol = r & 63u;
+                const uint32_t fin = t + jd;
                 // lane ol of the batch takes (k, t, fin): three v_writelane (lane select in m0,
                 // the one scalar operand gfx950 allows beside the data SGPR)
                 // m0 is reserved to the compiler, which uses it nowhere in these kernels
@@ -297,6 +285,16 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                 // A zero-duration job is committed and released before the next decision can
                 // read the node (RunJob sleeps 0; the release precedes the next branch, D3).
                 if (jd != 0u) {
+                    // a finish that wraps the u32 clock or hits the kEmpty sentinel (D8 range;
+                    // the host bound keeps checked inputs away from it) is recorded off the
+                    // decision chain, in VALU: the first such job ends the valid results
+                    {
+                        uint32_t tv = t, jv = jd;  // VGPR copies: the check stays in VALU
+                        asm volatile("" : "+v"(tv), "+v"(jv));
+                        const uint32_t fv = tv + jv;
+                        const uint32_t cand = (fv + 1u <= tv) ? r : kEmpty;
+                        ovf_r = cand < ovf_r ? cand : ovf_r;
+                    }
                     const uint64_t need = (uint64_t)jc | ((uint64_t)jm << 32);
                     // slot insert: the lowest lane with a free row, its lowest free row.  That
                     // lane also commits — Node.RunJob, cluster.go:146-147 (synchronous, D2) — since
@@ -359,35 +357,32 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     } while (rend != 0u);
     }  // live
 
-    if (flags & (MCS_FLAG_DEADLOCK | MCS_FLAG_CLOCK_OVERFLOW)) {
-        // jobs r..J-1 are never placed (deadlock: the Go loop retries the head forever) or were
-        // not decided before the clock left the u32 range (the run fails with MCS_E_RANGE)
-        const uint32_t b0 = r & ~63u;
-        if (lane >= (r & 63u)) {
-            on = MCS_NODE_UNPLACED;
-            os = MCS_TIME_NONE;
-            of = MCS_TIME_NONE;
-        }
-        flush(b0);
-        on = MCS_NODE_UNPLACED;
-        os = MCS_TIME_NONE;
-        of = MCS_TIME_NONE;
-        for (uint32_t b = b0 + kWave; b < J; b += kWave) flush(b);
-    } else if (HOR) {
-        // online: the batch holding the last decision of this horizon, lanes decided so far (a
-        // batch boundary reached in the same pass is rewritten with the same values)
-        if (!(flags & MCS_FLAG_OVERFLOW) && r > r_in) {
+    // [rs, J) is undecided: a deadlocked head and everything behind it (the Go loop retries the
+    // head forever), or every job from the first one whose clock left the u32 range (the run
+    // fails with MCS_E_RANGE)
+    const uint32_t ovf_job = sgpr(ovf_r);
+    if (ovf_job != kEmpty) flags |= MCS_FLAG_CLOCK_OVERFLOW;
+    const uint32_t rs = ovf_job < r ? ovf_job : r;
+    if (!(flags & MCS_FLAG_OVERFLOW)) {
+        // the batch holding the last decision, lanes decided (a batch boundary reached in the
+        // same pass is rewritten with the same values); earlier batches are stored
+        if (r > r_in) {
             const uint32_t i = ((r - 1u) & ~63u) + lane;
-            if (i < r) {
+            if (i < rs) {
                 __builtin_nontemporal_store(on, o_node + i);
                 __builtin_nontemporal_store(os, o_start + i);
                 __builtin_nontemporal_store(of, o_finish + i);
             }
         }
-    } else if (!(flags & MCS_FLAG_OVERFLOW) && J > 0u &&
-               ((J - 1u) & 63u) != 63u) {
-        flush((J - 1u) & ~63u);
+        if (flags & (MCS_FLAG_DEADLOCK | MCS_FLAG_CLOCK_OVERFLOW)) {
+            for (uint32_t i = rs + lane; i < J; i += kWave) {
+                o_node[i] = MCS_NODE_UNPLACED;
+                o_start[i] = MCS_TIME_NONE;
+                o_finish[i] = MCS_TIME_NONE;
+            }
+        }
     }
+    if (flags & MCS_FLAG_CLOCK_OVERFLOW) placed = rs < placed ? rs : placed;
 
     if constexpr (HOR) {  // save the state the next horizon resumes from (rerun on overflow)
         if (!(flags & MCS_FLAG_OVERFLOW)) {
@@ -405,7 +400,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                 OnlineState st{};
                 st.valid = 1u;
                 st.t = t;
-                st.cursor = r;
+                st.cursor = rs;
                 st.aux = have_w;
                 st.flags = flags;
                 st.pool = (uint32_t)P;

@@ -62,11 +62,15 @@ def horizons_for(streams, k):
     return sorted({int(x) for x in np.linspace(0, top, k + 2)[1:-1]})
 
 
-def make_prefix_check(final):
-    fnode, fstart, ffin = final
-
+def make_prefix_check(final, full_off):
     def check(eng, h, st):
         node, start, fin = eng.placements()
+        # the engine holds, per cluster, the first jobs of its stream (appended so far): map them
+        # to the rows of the final run
+        off = eng.job_offsets()
+        idx = np.concatenate([np.arange(int(full_off[k]), int(full_off[k]) + int(off[k + 1] - off[k]))
+                              for k in range(len(off) - 1)]).astype(np.int64)
+        fnode, fstart, ffin = (x[idx] for x in final)
         decided = (fstart < h) & (fnode >= 0)
         assert np.array_equal(node[decided], fnode[decided]), h
         assert np.array_equal(start[decided], fstart[decided]), h
@@ -85,7 +89,7 @@ def test_online_fifo_slices_equal_batch_and_oracle(kind, C, J, k):
     on, os_, of, osd = O.fifo_run_batch(arrays, streams, n_threads=8)
     assert np.array_equal(b[0], on) and np.array_equal(b[1], os_) and np.array_equal(b[2], of)
     hs = horizons_for(streams, k)
-    g = run_online(arrays, streams, hs, check_prefix=make_prefix_check(b[:3]))
+    g = run_online(arrays, streams, hs, check_prefix=make_prefix_check(b[:3], streams.job_off))
     for i in range(3):
         np.testing.assert_array_equal(g[i], b[i])
     for f in ("t_end", "placed", "waited", "peak_running", "flags"):
@@ -100,7 +104,7 @@ def test_online_delay_slices_equal_batch_and_oracle(kind, C, J, k):
     on, os_, of, osd = O.delay_run_batch(arrays, streams, n_threads=8)
     assert np.array_equal(b[0], on) and np.array_equal(b[1], os_) and np.array_equal(b[2], of)
     hs = horizons_for(streams, k)
-    g = run_online(arrays, streams, hs, policy="DELAY", check_prefix=make_prefix_check(b[:3]))
+    g = run_online(arrays, streams, hs, policy="DELAY", check_prefix=make_prefix_check(b[:3], streams.job_off))
     for i in range(3):
         np.testing.assert_array_equal(g[i], b[i])
     for f in ("t_end", "placed", "flags"):
@@ -116,7 +120,7 @@ def test_online_many_small_slices_grow_segments():
     b = batch(arrays, streams)
     top = int(streams.arrival.max()) + 1
     hs = list(range(7, top, max(1, top // 90)))
-    g = run_online(arrays, streams, hs, check_prefix=make_prefix_check(b[:3]))
+    g = run_online(arrays, streams, hs, check_prefix=make_prefix_check(b[:3], streams.job_off))
     for i in range(3):
         np.testing.assert_array_equal(g[i], b[i])
     gd = run_online(arrays, streams, hs, policy="DELAY")
