@@ -141,6 +141,21 @@ int mcs_read_foreign(mcs_engine* eng, mcs_foreign_rec* out, uint64_t cap, uint64
 int mcs_read_virtual_node_caps(mcs_engine* eng, uint32_t cluster, uint32_t* cores, uint32_t* mem,
                                uint32_t cap, uint32_t* n);
 
+/* ---- single-call mirror of the approval rule ---------------------------------------------------- */
+/* Trader.ApproveTrade (pkg/trader/trader.go:141-167) with the reference's approvePolicy{0.8, 0.8, -1,
+ * -1} (trader.go:47-52): a responder whose sample is {core_util, mem_util} and whose totals are
+ * {total_cores, total_memory} (SetTotalResources, uint32) asked for the contract {cores, memory,
+ * time_s, price 0}.  Evaluated on the GPU by the same device function both trader kernels call
+ * (float32 availability T - T*u and float64 incentive in Go's order, no FMA contraction). */
+typedef struct mcs_approve_query {
+    uint32_t total_cores, total_memory;
+    float core_util, mem_util;
+    uint32_t cores, memory, time_s, pad;
+} mcs_approve_query;
+
+/* out[i] = 1 (approve) or 0 for each of the n queries. */
+int mcs_approve_trade(mcs_engine* eng, const mcs_approve_query* q, uint32_t n, int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

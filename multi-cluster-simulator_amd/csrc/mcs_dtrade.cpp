@@ -551,4 +551,22 @@ int mcs_read_virtual_node_caps(mcs_engine* e, uint32_t cluster, uint32_t* cores,
     return MCS_OK;
 }
 
+int mcs_approve_trade(mcs_engine* e, const mcs_approve_query* q, uint32_t n, int32_t* out) {
+    if (int st = check_engine(e)) return st;
+    if (n && (!q || !out)) return fail(e, MCS_E_INVALID, "null query or output");
+    if (!n) return MCS_OK;
+    mcs_approve_query* dq = nullptr;
+    int32_t* dout = nullptr;
+    hipError_t st = hipMalloc(&dq, n * sizeof(mcs_approve_query));
+    if (st == hipSuccess) st = hipMalloc(&dout, n * sizeof(int32_t));
+    if (st == hipSuccess) st = hipMemcpy(dq, q, n * sizeof(mcs_approve_query), hipMemcpyHostToDevice);
+    if (st == hipSuccess) st = mcs::launch_approve(dq, n, dout, e->stream);
+    if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+    if (st == hipSuccess) st = hipMemcpy(out, dout, n * sizeof(int32_t), hipMemcpyDeviceToHost);
+    if (dq) (void)hipFree(dq);
+    if (dout) (void)hipFree(dout);
+    if (st != hipSuccess) return fail(e, MCS_E_HIP, std::string("approve_trade: ") + hipGetErrorString(st));
+    return MCS_OK;
+}
+
 }  // extern "C"

@@ -24,6 +24,7 @@
 // Per-cluster state a wave writes and re-reads inside a kernel is staged in LDS, or read back with
 // sc1 loads (L2) after an atomic write, never through this CU's non-coherent vector L1.
 #include "mcs_dtrade_internal.h"
+#include "mcs_trader_dev.h"
 #include "mcs_wave.h"
 
 namespace mcs {
@@ -532,21 +533,6 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// ApproveTrade (trader.go:141-167) with approvePolicy{0.8, 0.8, -1, -1}, like or_approve_trade
-__device__ __forceinline__ bool dt_approve(uint32_t tc, uint32_t tm, float cu, float mu, uint32_t kc,
-                                           uint32_t km, uint32_t ksec) {
-    if (!(cu < 0.8f && mu < 0.8f)) return false;
-    const float ftm = (float)tm, ftc = (float)tc;
-    const float avail_mem = __fsub_rn(ftm, __fmul_rn(ftm, mu));
-    const float avail_core = __fsub_rn(ftc, __fmul_rn(ftc, cu));
-    if (!(avail_core >= (float)kc && avail_mem >= (float)km)) return false;
-    const double secs = (double)ksec;  // Duration.Seconds() of whole seconds
-    const double b = __dmul_rn(__dmul_rn(-1.0, (double)kc), secs);
-    const double d = __dmul_rn(__dmul_rn(-1.0, (double)km), secs);
-    const double incentive = __dadd_rn(b, d);
-    return 0.0 >= incentive;  // float64(price 0) >= incentive (:155)
-}
-
 // Phase D: trader rounds in cluster order over the whole system, then the next tick.  Every rank
 // runs it on the same gathered records and replicated trader state, so every decision is identical
 // on every rank; a rank applies the side effects on its own clusters (Foreign jobs, virtual nodes)
@@ -614,7 +600,7 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
                         if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
                         if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
                             const DtRec* rr = dt_rec(a, r);
-                            app = dt_approve(rr->total_c, rr->total_m, rr->cu, rr->mu, kc, km, ksec);
+                            app = approve_trade_dev(rr->total_c, rr->total_m, rr->cu, rr->mu, kc, km, ksec);
                             t.lock_id = t.next_id++;  // set even when not approving (:44-46)
                             t.lock_until = T + a.lock_s;
                         }
@@ -830,7 +816,23 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
     }
 }
 
+// The single-call mirror of ApproveTrade (mcs_approve_trade): the kernels' own device function on
+// caller-given samples and contracts, one query per thread.
+__global__ __launch_bounds__(256) void approve_kernel(const mcs_approve_query* q, uint32_t n, int32_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const mcs_approve_query x = q[i];
+    out[i] = approve_trade_dev(x.total_cores, x.total_memory, x.core_util, x.mem_util, x.cores, x.memory,
+                               x.time_s) ? 1 : 0;
+}
+
 }  // namespace
+
+hipError_t launch_approve(const mcs_approve_query* q, uint32_t n, int32_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(approve_kernel, dim3((n + 255) / 256), dim3(256), 0, s, q, n, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_dtrade_init(const DtArgs& a, hipStream_t s) {
     if (a.C == 0) return hipSuccess;

@@ -127,6 +127,7 @@ struct DtArgs {
 };
 
 hipError_t launch_dtrade_init(const DtArgs& a, hipStream_t s);
+hipError_t launch_approve(const mcs_approve_query* q, uint32_t n, int32_t* out, hipStream_t s);  // the mirror
 // one tick: phases A and C (dt_step_kernel, writes this rank's exchange block), then phase D
 hipError_t launch_dtrade_step(const DtArgs& a, hipStream_t s);
 hipError_t launch_dtrade_trader(const DtArgs& a, hipStream_t s);

@@ -19,6 +19,7 @@
 // staged in LDS: an L2 atomic or store followed by a plain global load of the same line from the
 // same wave could be served stale by the non-coherent vector L1.
 #include "mcs_trade_internal.h"
+#include "mcs_trader_dev.h"
 #include "mcs_wave.h"
 
 namespace mcs {
@@ -369,16 +370,11 @@ __global__ __launch_bounds__(64) void tr_post_kernel(TradeArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// ApproveTrade (trader.go:141-167) of the contract {cores, mem, time 0 s, price 0} that every
-// FIFO trade carries (the small-node contract over an empty Level1), on the responder's sample.
+// ApproveTrade (trader.go:141-167) of the contract {cores 0, mem 0, time 0 s, price 0} that every
+// FIFO trade carries (the small-node contract over an empty Level1), on the responder's sample:
+// mcs_trader_dev.h's function, shared with the DELAY trader and the mcs_approve_trade mirror.
 __device__ __forceinline__ bool approve_zero_contract(uint32_t tc, uint32_t tm, float cu, float mu) {
-    if (!(cu < 0.8f && mu < 0.8f)) return false;  // :147
-    const float ftm = (float)tm, ftc = (float)tc;
-    const float avail_mem = __fsub_rn(ftm, __fmul_rn(ftm, mu));   // :148
-    const float avail_core = __fsub_rn(ftc, __fmul_rn(ftc, cu));  // :149
-    if (!(avail_core >= 0.0f && avail_mem >= 0.0f)) return false;  // :151
-    // incentive = -1*0*0 + -1*0*0 = -0.0 (float64); price 0 >= -0.0 (:154-155)
-    return true;
+    return approve_trade_dev(tc, tm, cu, mu, 0u, 0u, 0u);
 }
 
 // Phase D: trader rounds (replicated) and the next tick.

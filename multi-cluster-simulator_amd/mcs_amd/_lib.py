@@ -183,6 +183,12 @@ class mcs_trade_stats(C.Structure):
     ]
 
 
+class mcs_approve_query(C.Structure):
+    _fields_ = [("total_cores", C.c_uint32), ("total_memory", C.c_uint32), ("core_util", C.c_float),
+                ("mem_util", C.c_float), ("cores", C.c_uint32), ("memory", C.c_uint32), ("time_s", C.c_uint32),
+                ("pad", C.c_uint32)]
+
+
 class mcs_comm_id(C.Structure):
     _fields_ = [("bytes", C.c_char * 128)]
 
@@ -239,6 +245,7 @@ SIGNATURES = [
     ("mcs_read_contracts", C.c_int, [vp, C.POINTER(mcs_contract_rec), C.c_uint64, u64p]),
     ("mcs_read_foreign", C.c_int, [vp, C.POINTER(mcs_foreign_rec), C.c_uint64, u64p]),
     ("mcs_read_virtual_node_caps", C.c_int, [vp, C.c_uint32, u32p, u32p, C.c_uint32, u32p]),
+    ("mcs_approve_trade", C.c_int, [vp, C.POINTER(mcs_approve_query), C.c_uint32, i32p]),
 ]
 
 _lib = None

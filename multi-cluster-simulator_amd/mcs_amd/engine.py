@@ -410,6 +410,22 @@ class Engine:
                                            n, C.byref(ms)))
         return (out, ms.value) if with_time else out
 
+    def approve_trade(self, total_cores, total_memory, core_util, mem_util, cores, memory, time_s) -> np.ndarray:
+        """mcs_approve_trade: Trader.ApproveTrade (trader.go:141-167) on the GPU for arrays of
+        (responder totals + sample, contract) queries; returns 0/1 per query."""
+        arrs = np.broadcast_arrays(*(np.asarray(x) for x in (total_cores, total_memory, core_util, mem_util, cores,
+                                                              memory, time_s)))
+        n = arrs[0].size
+        q = np.zeros(n, dtype=[("total_cores", "<u4"), ("total_memory", "<u4"), ("core_util", "<f4"),
+                               ("mem_util", "<f4"), ("cores", "<u4"), ("memory", "<u4"), ("time_s", "<u4"),
+                               ("pad", "<u4")])
+        for f, a in zip(("total_cores", "total_memory", "core_util", "mem_util", "cores", "memory", "time_s"), arrs):
+            q[f] = a.ravel()
+        out = np.zeros(max(n, 1), np.int32)
+        self._c(L.lib().mcs_approve_trade(self._h, q.ctypes.data_as(C.POINTER(L.mcs_approve_query)), n,
+                                          L.ptr(out, C.c_int32)))
+        return out[:n]
+
     # -- single-job mirrors (live state) --------------------------------------------------------
     def schedule_one(self, cluster: int, cores: int, mem: int) -> int:
         node = C.c_int32(-1)

@@ -114,7 +114,7 @@ def test_struct_layouts_match_headers(tmp_path):
 
     structs = [L.mcs_config, L.mcs_gen_params, L.mcs_stats, L.mcs_cluster_stats, L.mcs_lent_rec,
                L.mcs_trade_rec, L.mcs_trade_stats, L.mcs_comm_id, L.mcs_delay_cluster_stats,
-               L.mcs_contract_rec, L.mcs_foreign_rec, L.mcs_cluster_state]
+               L.mcs_contract_rec, L.mcs_foreign_rec, L.mcs_cluster_state, L.mcs_approve_query]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mcs_trade.h"', "int main(void) {"]
     for s in structs:
         n = s.__name__

@@ -23,17 +23,26 @@ def dt_system(k):
             cl.Nodes[int(node)].CoresAvailable = fc
             cl.Nodes[int(node)].MemoryAvailable = fm
         cls.append(cl)
-    jobs = k["jobs"]
-    n = len(jobs)
-    off = np.array([0, n] + [n] * (len(cls) - 1), np.uint64)
+    per = [sorted(k["jobs"], key=lambda j: j[0]) if c == 0 else
+           sorted(k.get("jobs_by_cluster", {}).get(str(c), []), key=lambda j: j[0]) for c in range(len(cls))]
+    jobs = [j for p in per for j in p]
+    off = np.concatenate([[0], np.cumsum([len(p) for p in per])]).astype(np.uint64)
     s = JobStreams(np.array([j[1] for j in jobs], np.uint32), np.array([j[4] for j in jobs], np.uint32),
                    np.array([j[2] for j in jobs], np.uint32), np.array([j[3] for j in jobs], np.uint32), off)
     return pack_clusters(cls), s
 
 
+def kat_expectations(k):
+    """[(global job index, (node, start, finish))] of cluster 0 ("expect") and the others"""
+    per = {"0": k["expect"], **k.get("expect_by_cluster", {})}
+    sizes = [len(k["jobs"])] + [len(k.get("jobs_by_cluster", {}).get(str(c), [])) for c in range(1, len(k["clusters"]))]
+    base = np.concatenate([[0], np.cumsum(sizes)])
+    return [(int(base[int(c)]) + int(j), tuple(v)) for c, e in per.items() for j, v in e.items()]
+
+
 def check_kat(k, node, start, fin, trades, foreign, n_foreign, vnodes, t_final):
-    for jid, (nd, s, f) in k["expect"].items():
-        assert (int(node[int(jid)]), int(start[int(jid)]), int(fin[int(jid)])) == (nd, s, f)
+    for g, (nd, s, f) in kat_expectations(k):
+        assert (int(node[g]), int(start[g]), int(fin[g])) == (nd, s, f), (k["name"], g)
     got = [[int(r[f]) for f in ("t", "requester", "winner", "approvals", "policy", "cores", "mem", "time_s",
                                 "failed")] for r in trades]
     assert got == k["trades"]

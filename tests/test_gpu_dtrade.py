@@ -36,6 +36,8 @@ def test_gpu_dtrade_kats(k):
     r = run(arrays, s, t_max_s=k["t_max"])
     check_kat(k, r["node"], r["start"], r["finish"], r["trades"], r["foreign"], len(r["foreign"]), r["vnodes"],
               r["ts"]["t_final"])
+    for key, v in k.get("stats0", {}).items():  # WaitTime statistics of cluster 0
+        assert r["ds"][key][0] == v, key
 
 
 @pytest.mark.parametrize("kind,C,J", [("small", 8, 300), ("small", 16, 600), ("big", 8, 800), ("n64_hot", 8, 2000)])
@@ -133,3 +135,59 @@ def test_gpu_dtrade_rccl_loop_world1():
     assert foreign.tobytes() == g["foreign"].tobytes()
     assert vn.tolist() == [len(v) for v in g["vnodes"]]
     assert t_final == g["ts"]["t_final"]
+
+
+F32 = np.float32
+
+
+def test_gpu_approve_trade_kat6_boundaries(engine):
+    """KAT6 and neighbouring float32 boundaries of ApproveTrade (trader.go:141-167),
+    evaluated by the device function both trader kernels call (mcs_approve_trade), against the
+    hand-derived answers and the oracle.  TotalCore 160 / TotalMemory 120000 = cluster_small."""
+    u7 = float(np.nextafter(F32(0.8), F32(0)))  # 0.79999995f
+    cases = [  # (tc, tm, cu, mu, cores, mem, time_s) -> approve
+        ((160, 120000, 0.5, 0.0, 80, 0, 50), 1),      # availability exactly 80.0 >= 80
+        ((160, 120000, 0.5, 0.0, 81, 0, 50), 0),      # 80.0 < 81
+        ((160, 120000, 0.8, 0.0, 0, 0, 0), 0),        # 0.8f < 0.8f is false
+        ((160, 120000, u7, 0.0, 32, 0, 10), 1),       # 160 - 160*0.79999995f = 32.000008f >= 32
+        ((160, 120000, u7, 0.0, 33, 0, 10), 0),       # 32.000008f < 33
+        ((160, 120000, 0.0, 0.5, 0, 60000, 7), 1),    # memory availability exactly 60000
+        ((160, 120000, 0.0, 0.5, 0, 60001, 7), 0),
+        ((160, 120000, 0.0, u7, 0, 24000, 0), 1),     # 120000 - 120000*0.79999995f = 24000.006f
+        ((160, 120000, 0.0, u7, 0, 24001, 0), 0),
+        ((160, 120000, 0.3, 0.7, 0, 0, 0), 1),        # the zero contract: incentive -0.0 <= price 0
+        ((160, 120000, float("nan"), 0.0, 0, 0, 0), 0),   # a NaN sample never passes cu < 0.8
+        ((16777217, 1, 0.0, 0.0, 16777217, 0, 1), 1),  # float32(16777217) == float32(16777217): >= holds
+        ((16777216, 1, 0.0, 0.0, 16777218, 0, 1), 0),  # 16777216.0 < 16777218.0
+        ((0, 0, 0.0, 0.0, 0, 0, 0), 1),               # empty cluster, zero contract
+    ]
+    q = np.array([c for c, _ in cases], dtype=object)
+    cols = [np.array([c[i] for c, _ in cases], dtype=(np.float32 if i in (2, 3) else np.uint32)) for i in range(7)]
+    got = engine.approve_trade(*cols)
+    want = np.array([w for _, w in cases])
+    np.testing.assert_array_equal(got, want)
+    orc = np.array([O.approve_trade(int(c[0]), int(c[1]), F32(c[2]), F32(c[3]), int(c[4]), int(c[5]),
+                                    int(c[6]) * 1_000_000_000, 0.0) for c, _ in cases])
+    np.testing.assert_array_equal(orc, want)
+
+
+def test_gpu_approve_trade_sweep_vs_oracle(engine):
+    """200k queries at and around the integer utilizations a cluster can sample (used/total in
+    float32) with requests at the float32 availability +-1: GPU == oracle, bit for bit."""
+    rng = np.random.default_rng(6)
+    n = 200_000
+    tc = rng.choice([160, 320, 2560, 8192, 24000, 99991, 16777215], n).astype(np.uint32)
+    tm = rng.choice([120000, 240000, 6144000, 1 << 24, 3], n).astype(np.uint32)
+    cu = (rng.integers(0, tc.astype(np.int64) + 1) .astype(np.float32) / tc.astype(np.float32)).astype(np.float32)
+    mu = (rng.integers(0, tm.astype(np.int64) + 1).astype(np.float32) / tm.astype(np.float32)).astype(np.float32)
+    av_c = (tc.astype(np.float32) - tc.astype(np.float32) * cu).astype(np.float32)
+    av_m = (tm.astype(np.float32) - tm.astype(np.float32) * mu).astype(np.float32)
+    kc = np.clip(np.floor(av_c).astype(np.int64) + rng.integers(-1, 2, n), 0, None).astype(np.uint32)
+    km = np.clip(np.floor(av_m).astype(np.int64) + rng.integers(-1, 2, n), 0, None).astype(np.uint32)
+    ks = rng.integers(0, 600, n).astype(np.uint32)
+    got = engine.approve_trade(tc, tm, cu, mu, kc, km, ks)
+    orc = np.array([O.approve_trade(int(tc[i]), int(tm[i]), cu[i], mu[i], int(kc[i]), int(km[i]),
+                                    int(ks[i]) * 1_000_000_000, 0.0) for i in range(n)], np.int32)
+    bad = np.flatnonzero(got != orc)
+    assert bad.size == 0, f"{bad.size} mismatches, first {bad[:5]}"
+    assert 0.2 < got.mean() < 0.8  # both outcomes are exercised
