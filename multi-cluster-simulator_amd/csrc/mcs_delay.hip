@@ -343,7 +343,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                     const uint32_t jw = readlane((uint32_t)jdv, b);
                     const uint32_t jd = readlane((uint32_t)(jdv >> 32), b);
                     const uint32_t fin = t + jd;
-                    ovf |= (fin + 1u <= t) ? 1u : 0u;  // finish leaves the u32 clock (D8), off the chain
+                    if constexpr (HOR) ovf |= (fin + 1u <= t) ? 1u : 0u;  // D8 guard, online variant only
                     if (!commit(k, jc, jm, fin, jd)) {
                         flags |= MCS_FLAG_OVERFLOW;
                         stop = 1u;
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
             const uint32_t ol = h & 63u;
             if (k != kEmpty) {
                 const uint32_t fin = t + jd;
-                ovf |= (fin + 1u <= t) ? 1u : 0u;  // finish leaves the u32 clock (D8), off the chain
+                if constexpr (HOR) ovf |= (fin + 1u <= t) ? 1u : 0u;  // D8 guard, online variant only
                 if (!commit(k, jc, jm, fin, jd)) {
                     flags |= MCS_FLAG_OVERFLOW;
                     stop = 1u;

@@ -452,6 +452,15 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
             return fail(e, MCS_E_INVALID, "finite horizons are implemented for FIFO/DELAY without trading");
         return mcs::online_run(e, t_end_s, stats);
     }
+    if (e->cfg.unchecked_horizon && !(e->cfg.borrow || e->cfg.trader)) {
+        /* streams that skipped the host clock bound run through the online kernel variant, the one
+         * with the device-side finish-time guard: a drain from t = 0, the batch result */
+        if (int st = mcs::online_begin(e)) return st;
+        const int st = mcs::online_run(e, MCS_TIME_NONE, stats);
+        e->online = false; /* the next batch run starts again from t = 0 */
+        if (stats) stats->online = 0;
+        return st;
+    }
     if (e->cfg.borrow || e->cfg.trader) /* the trading paths read the job records */
         if (int st = mcs::ensure_job_records(e)) return st;
     if (e->cfg.policy == MCS_POLICY_DELAY && e->cfg.trader) return mcs::dtrade_run(e, stats);

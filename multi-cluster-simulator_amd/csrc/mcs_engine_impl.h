@@ -35,6 +35,7 @@ int dtrade_end(mcs_engine* e, mcs_stats* stats);
 inline bool is_dtrade(const mcs_engine* e);
 // online mode (mcs_online.cpp)
 void online_free(mcs_engine* e);
+int online_begin(mcs_engine* e);
 int online_run(mcs_engine* e, uint32_t t_hor, mcs_stats* stats);
 int online_read_rows(mcs_engine* e, int32_t* node, uint32_t* start_s, uint32_t* finish_s);
 int online_read_jobs(mcs_engine* e, uint4* out);

@@ -285,10 +285,12 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                 // A zero-duration job is committed and released before the next decision can
                 // read the node (RunJob sleeps 0; the release precedes the next branch, D3).
                 if (jd != 0u) {
-                    // a finish that wraps the u32 clock or hits the kEmpty sentinel (D8 range;
-                    // the host bound keeps checked inputs away from it) is recorded off the
-                    // decision chain, in VALU: the first such job ends the valid results
-                    {
+                    // a finish that wraps the u32 clock or hits the kEmpty sentinel (D8 range)
+                    // is recorded off the decision chain, in VALU: the first such job ends the
+                    // valid results.  Only the online variant carries this guard: the host bound
+                    // keeps checked streams away from it, and the engine runs batch runs of
+                    // unchecked streams (cfg.unchecked_horizon) through the online variant
+                    if constexpr (HOR) {
                         uint32_t tv = t, jv = jd;  // VGPR copies: the check stays in VALU
                         asm volatile("" : "+v"(tv), "+v"(jv));
                         const uint32_t fv = tv + jv;

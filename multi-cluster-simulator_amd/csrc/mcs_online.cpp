@@ -156,6 +156,8 @@ int ensure_l1(mcs_engine* e) {
     return MCS_OK;
 }
 
+}  // namespace
+
 // a session at t = 0 over the streams in HBM
 int online_begin(mcs_engine* e) {
     if (e->cfg.borrow || e->cfg.trader)
@@ -183,8 +185,6 @@ int online_begin(mcs_engine* e) {
     e->has_run = false;
     return MCS_OK;
 }
-
-}  // namespace
 
 uint32_t horizon_extra(const mcs_engine* e) { return e->cfg.policy == MCS_POLICY_DELAY ? e->cfg.max_wait_s : 0u; }
 
