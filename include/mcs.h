@@ -102,20 +102,25 @@ void mcs_config_default(mcs_config* cfg);
 typedef enum mcs_arrival_mode {
     MCS_ARRIVAL_REF = 0,    /* per minute n ~ Poisson(lambda), spacing floor(60/n) s (client.go:107-125);
                                n == 0 is an idle minute of 60 s (D5)                                 */
-    MCS_ARRIVAL_SCALED = 1  /* per second n ~ Poisson(lambda) arrivals at that second               */
+    MCS_ARRIVAL_SCALED = 1, /* per second n ~ Poisson(lambda) arrivals at that second               */
+    MCS_ARRIVAL_WEIBULL = 2 /* the client's "weibull" mode (client.go:131-145): after each job a sleep of
+                               floor(X) s, X ~ Weibull(scale lambda, shape weibull_k); the reference
+                               uses Lambda 10, K 3 (gonum distuv.Weibull)                          */
 } mcs_arrival_mode;
 
 typedef struct mcs_gen_params {
     uint64_t seed;        /* base seed; cluster k uses key = mix(seed ^ k)                           */
     uint32_t arrival_mode;/* mcs_arrival_mode                                                        */
     uint32_t max_dur_s;   /* durations U{0..max_dur_s-1}; 600 = rand.Intn(600) (client.go:98)        */
-    double lambda;        /* Poisson mean per minute (REF, 10 in client.go:108) or per second (SCALED) */
+    double lambda;        /* Poisson mean per minute (REF, 10 in client.go:108) or per second (SCALED);
+                             WEIBULL: the scale (Lambda: 10, client.go:133)                          */
     uint32_t max_cores;   /* 0 = per-cluster max node Cores (setMaxCluster, client.go:68-83)          */
     uint32_t max_mem;     /* 0 = per-cluster max node Memory                                          */
     uint32_t fused;       /* 1: no job records in HBM; the FIFO/DELAY kernels synthesise each 64-job
                              batch in registers, bit-identical to the records;
                              mcs_read_jobs and the trading paths materialise them on demand      */
-    uint32_t reserved[3];
+    float weibull_k;      /* WEIBULL: the shape (K: 3, client.go:134); 0 = 3                          */
+    uint32_t reserved[2];
 } mcs_gen_params;
 
 void mcs_gen_params_default(mcs_gen_params* p);

@@ -39,6 +39,7 @@ void free_jobs(mcs_engine* e) {
     e->bounds_known = false;
     dfree(e->d_jobs);
     dfree(e->d_gen_max);
+    dfree(e->d_wthr);
     e->gen = mcs::GenArgs{};
     dfree(e->d_job_off);
     dfree(e->d_out_node);
@@ -75,9 +76,7 @@ int ensure_job_records(mcs_engine* e) {
     HIPCHK(e, hipMemsetAsync(e->d_jobs + nj, 0, kJobPad * sizeof(uint4), e->stream));
     hipError_t st = launch_gen_attrs(e->d_jobs, e->d_job_off, e->gen.max_c, e->gen.max_m, e->C,
                                      e->gen.seed, e->gen.max_dur, e->gen.base, e->stream);
-    if (st == hipSuccess)
-        st = launch_gen_arrivals(e->d_jobs, e->d_job_off, e->C, e->gen.seed, e->gen.mode, e->gen.enl,
-                                 e->gen.base, e->stream);
+    if (st == hipSuccess) st = launch_gen_arrivals(e->d_jobs, e->d_job_off, e->C, e->gen, e->stream);
     if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
     if (st != hipSuccess)
         return fail(e, MCS_E_HIP, std::string("job generation: ") + hipGetErrorString(st));
@@ -108,6 +107,28 @@ void mcs_config_default(mcs_config* cfg) {
     cfg->max_wait_s = 10; /* sched.Policy.MaxWaitTime = 10 * time.Second, scheduler.go:115 */
 }
 
+/* the Weibull gap table of mcs_gen.h: thr[n-1] = floor(2^64 exp(-(n/scale)^k)) while nonzero.
+ * Returns its length, or -1 if it does not vanish within MCS_GEN_WEIBULL_MAX entries. */
+static int weibull_table(double scale, double k, uint64_t* thr) {
+    if (!(scale > 0.0) || !(k > 0.0)) return -1;
+    for (uint32_t n = 1; n <= MCS_GEN_WEIBULL_MAX; ++n) {
+        const double p = std::exp(-std::pow((double)n / scale, k));
+        const double v = std::ldexp(p, 64);
+        if (v < 1.0) return (int)n - 1;
+        thr[n - 1] = v >= 18446744073709551615.0 ? 0xFFFFFFFFFFFFFFFFull : (uint64_t)v;
+    }
+    return -1;
+}
+
+static bool gen_params_ok(const mcs_gen_params* p) {
+    if (!p || p->arrival_mode > 2u || p->max_dur_s == 0 || p->fused > 1u) return false;
+    if (p->arrival_mode == 2u) {
+        uint64_t thr[MCS_GEN_WEIBULL_MAX];
+        return weibull_table(p->lambda, p->weibull_k > 0.0f ? p->weibull_k : 3.0, thr) >= 0;
+    }
+    return p->lambda > 0.0 && p->lambda <= 128.0;
+}
+
 void mcs_gen_params_default(mcs_gen_params* p) {
     if (!p) return;
     std::memset(p, 0, sizeof(*p));
@@ -123,12 +144,14 @@ int mcs_gen_cluster_host(const mcs_gen_params* p, uint32_t cluster, uint32_t max
                          uint32_t max_mem, uint64_t n_jobs, uint32_t* arrival_s, uint32_t* dur_s,
                          uint32_t* cores, uint32_t* mem) {
     if (!p || (n_jobs && (!arrival_s || !dur_s || !cores || !mem))) return MCS_E_INVALID;
-    if (!(p->lambda > 0.0) || p->lambda > 128.0 || p->arrival_mode > 1u || p->max_dur_s == 0)
-        return MCS_E_INVALID;
+    if (!gen_params_ok(p)) return MCS_E_INVALID;
     const uint64_t key = mcs_cluster_key(p->seed, cluster);
     for (uint64_t i = 0; i < n_jobs; ++i)
         mcs_gen_job_attrs(key, i, max_cores, max_mem, p->max_dur_s, &dur_s[i], &cores[i], &mem[i]);
-    mcs_gen_arrivals(key, p->arrival_mode, std::exp(-p->lambda), n_jobs, arrival_s);
+    uint64_t thr[MCS_GEN_WEIBULL_MAX];
+    int wn = 0;
+    if (p->arrival_mode == 2u) wn = weibull_table(p->lambda, p->weibull_k > 0.0f ? p->weibull_k : 3.0, thr);
+    mcs_gen_arrivals(key, p->arrival_mode, std::exp(-p->lambda), thr, (uint32_t)wn, n_jobs, arrival_s);
     return MCS_OK;
 }
 
@@ -352,9 +375,7 @@ int mcs_submit_jobs(mcs_engine* e, const uint32_t* arrival_s, const uint32_t* du
 int mcs_generate_jobs(mcs_engine* e, const mcs_gen_params* p, uint64_t jobs_per_cluster) {
     if (int st = check_engine(e)) return st;
     if (!e->has_clusters) return fail(e, MCS_E_STATE, "mcs_load_clusters first");
-    if (!p || !(p->lambda > 0.0) || p->lambda > 128.0 || p->arrival_mode > 1u || p->max_dur_s == 0 ||
-        p->fused > 1u)
-        return fail(e, MCS_E_INVALID, "bad generator parameters");
+    if (!gen_params_ok(p)) return fail(e, MCS_E_INVALID, "bad generator parameters");
     if (jobs_per_cluster > 0xFFFFFFFFull) return fail(e, MCS_E_INVALID, "too many jobs per cluster");
     std::vector<uint64_t> off(e->C + 1);
     for (uint32_t c = 0; c <= e->C; ++c) off[c] = (uint64_t)c * jobs_per_cluster;
@@ -386,6 +407,16 @@ int mcs_generate_jobs(mcs_engine* e, const mcs_gen_params* p, uint64_t jobs_per_
     e->gen.max_dur = p->max_dur_s;
     e->gen.base = e->rank * e->C;
     e->gen.on = p->fused;
+    e->gen.wthr = nullptr;
+    e->gen.wn = 0;
+    if (p->arrival_mode == 2u) { /* the Weibull gap table, resolved once on the host (mcs_gen.h) */
+        uint64_t thr[MCS_GEN_WEIBULL_MAX];
+        const int wn = weibull_table(p->lambda, p->weibull_k > 0.0f ? p->weibull_k : 3.0, thr);
+        HIPCHK(e, hipMalloc(&e->d_wthr, MCS_GEN_WEIBULL_MAX * sizeof(uint64_t)));
+        HIPCHK(e, hipMemcpy(e->d_wthr, thr, (size_t)wn * sizeof(uint64_t), hipMemcpyHostToDevice));
+        e->gen.wthr = e->d_wthr;
+        e->gen.wn = (uint32_t)wn;
+    }
     /* fused: no records in HBM; the FIFO/DELAY kernels synthesise each batch (mcs_gen_dev.h) */
     if (!p->fused)
         if (int st = mcs::ensure_job_records(e)) return st;
@@ -403,8 +434,7 @@ int mcs_generate_jobs(mcs_engine* e, const mcs_gen_params* p, uint64_t jobs_per_
             unsigned long long* d_last = nullptr;
             std::vector<unsigned long long> last(e->C);
             HIPCHK(e, hipMalloc(&d_last, e->C * sizeof(unsigned long long)));
-            hipError_t st = mcs::launch_gen_bound(e->d_job_off, e->C, e->gen.seed, e->gen.mode, e->gen.enl,
-                                                  e->gen.base, d_last, e->stream);
+            hipError_t st = mcs::launch_gen_bound(e->d_job_off, e->C, e->gen, d_last, e->stream);
             if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
             if (st == hipSuccess)
                 st = hipMemcpy(last.data(), d_last, e->C * sizeof(unsigned long long), hipMemcpyDeviceToHost);

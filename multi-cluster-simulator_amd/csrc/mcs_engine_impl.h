@@ -69,6 +69,7 @@ struct mcs_engine {
     uint4* d_jobs = nullptr;        // null while a fused synthetic stream is not materialised
     mcs::GenArgs gen{};             // the synthetic stream of mcs_generate_jobs (gen.on: fused)
     uint32_t* d_gen_max = nullptr;  // its explicit maxima: [C] cores, then [C] memory
+    unsigned long long* d_wthr = nullptr;  // its Weibull gap table (MCS_ARRIVAL_WEIBULL)
     uint64_t* d_job_off = nullptr;
     int32_t* d_out_node = nullptr;
     uint32_t* d_out_start = nullptr;

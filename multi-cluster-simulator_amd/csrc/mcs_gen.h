@@ -9,6 +9,9 @@
  *                          floor(60/n) s apart, the loop sleeping after every send (116-125), so a
  *                          minute lasts n*floor(60/n) s; n == 0 panics in Go (60/0) -> idle 60 s (D5)
  *   arrivals, SCALED mode: per second n ~ Poisson(lambda_s), all n arrive at that second
+ *   arrivals, WEIBULL mode: the client's "weibull" time_dist (client.go:131-145): after each job it
+ *                          sleeps time.Duration(X) * time.Second with X ~ Weibull(Lambda 10, K 3),
+ *                          i.e. floor(X) whole seconds (the float64 -> Duration conversion truncates)
  *
  * Beta(2,2) is drawn as the median of three U(0,1) (the median of 3 iid uniforms is exactly
  * Beta(2,2)); floor(B*max) is computed on 32-bit fixed point: (median_u32 * max) >> 32.  Poisson is
@@ -97,12 +100,38 @@ MCS_GEN_FN uint32_t mcs_poisson(uint64_t akey, uint64_t idx, double exp_neg_lamb
     return k;
 }
 
-/* Sequential arrival scan of one cluster: arrival[j] for j < n_jobs.  mode 0 = REF, 1 = SCALED. */
+/* Weibull gaps: floor(X), X ~ Weibull(lambda, k), from the 64-bit draw u by inverse CDF on the
+ * integer grid: floor(X) >= n  <=>  X >= n  <=>  U <= exp(-(n/lambda)^k).  thr[n-1] =
+ * floor(2^64 * exp(-(n/lambda)^k)) is resolved ONCE on the host (like exp(-lambda) for Poisson) and
+ * decreases to 0 within MCS_GEN_WEIBULL_MAX entries; the gap is the number of leading entries with
+ * u < thr (binary search), so host and device gaps are identical integers. */
+#define MCS_GEN_WEIBULL_MAX 256u
+MCS_GEN_FN uint32_t mcs_weibull_gap(uint64_t u, const uint64_t* thr, uint32_t nthr) {
+    uint32_t lo = 0, hi = nthr;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (u < thr[mid])
+            lo = mid + 1u;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+/* Sequential arrival scan of one cluster: arrival[j] for j < n_jobs.  mode 0 = REF, 1 = SCALED,
+ * 2 = WEIBULL (thr / nthr: the gap table above; unused by the Poisson modes). */
 MCS_GEN_FN void mcs_gen_arrivals(uint64_t ckey, uint32_t mode, double exp_neg_lambda,
-                                 uint64_t n_jobs, uint32_t* arrival) {
+                                 const uint64_t* thr, uint32_t nthr, uint64_t n_jobs, uint32_t* arrival) {
     const uint64_t akey = mcs_arrival_key(ckey);
     uint64_t j = 0, period = 0;
     uint32_t T = 0;
+    if (mode == 2u) { /* SendJob, then Sleep(floor(X)) (client.go:136-145): job 0 at t = 0 */
+        for (j = 0; j < n_jobs; ++j) {
+            arrival[j] = T;
+            T += mcs_weibull_gap(mcs_draw(akey, j), thr, nthr);
+        }
+        return;
+    }
     while (j < n_jobs) {
         const uint32_t n = mcs_poisson(akey, period++, exp_neg_lambda);
         if (mode == 0u) {

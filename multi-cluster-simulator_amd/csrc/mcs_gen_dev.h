@@ -12,7 +12,11 @@
 //     finds its job's period with a 6-step binary search over the inclusive counts.  A window of
 //     64 periods holds ~64 * lambda jobs, so at the C4 rate the scan costs about one window per
 //     two batches.
-// The host resolves exp(-lambda) once (like mcs_generate_jobs), so device and host draws match.
+//   * WEIBULL arrivals (client.go:131-145) are a running sum of per-job gaps: each lane draws its
+//     job's gap from the host-resolved table (mcs_weibull_gap), the wave prefix-sums them and the
+//     batch total carries to the next batch.
+// The host resolves exp(-lambda) and the Weibull gap table once (like mcs_generate_jobs), so device
+// and host draws match.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -42,6 +46,8 @@ struct GenStream {
     uint32_t pw, jw, tw;   // window: first period, its first job, its start second
     uint32_t n, cum, tex;  // lane l: jobs of period pw + l, inclusive job count, start offset
     uint32_t tot, span;    // jobs and seconds of the whole window
+    const uint64_t* wthr;  // WEIBULL: gap table; wcarry = arrival of the next batch's first job
+    uint32_t wn, wcarry;
 
     __device__ __forceinline__ void fill(uint32_t lane) {
         n = mcs_poisson(akey, (uint64_t)pw + lane, enl);
@@ -64,14 +70,23 @@ struct GenStream {
         pw = 0u;
         jw = 0u;
         tw = 0u;
-        fill(lane);
+        wthr = (const uint64_t*)g.wthr;
+        wn = g.wn;
+        wcarry = 0u;
+        if (mode != 2u) fill(lane);
     }
 
     // the records {arrival, dur, cores, mem} of jobs [base, base + 64); bases must increase
     __device__ __forceinline__ uint4 next(uint32_t base, uint32_t lane) {
         const uint32_t j = base + lane;
         uint32_t arr = 0u, done = 0u;
-        for (;;) {
+        if (mode == 2u) {  // job j arrives after the gaps of jobs 0..j-1 (consecutive batches)
+            const uint32_t g = mcs_weibull_gap(mcs_draw(akey, j), wthr, wn);
+            const uint32_t inc = wave_incl_sum_u32(g, lane);
+            arr = wcarry + inc - g;
+            wcarry += readlane(inc, 63);
+        }
+        if (mode != 2u) for (;;) {  // (a wave-uniform loop: every lane takes part in the shuffles)
             // every lane searches (the shuffles need all lanes); lanes outside the window discard
             const uint32_t rel = j - jw;
             uint32_t lo = 0u;

@@ -40,6 +40,9 @@ struct GenArgs {
     uint32_t max_dur;
     uint32_t base;          // global index of the engine's cluster 0 (mcs_set_shard)
     uint32_t on;
+    const unsigned long long* wthr;  // WEIBULL gap table (mcs_gen.h), resolved on the host
+    uint32_t wn;
+    uint32_t pad;
 };
 
 // Online mode (mcs_run with a finite horizon, mcs_append_jobs): one record per
@@ -129,12 +132,10 @@ bool fifo_variant_exists(int npl, int pool);
 hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t* max_c,
                             const uint32_t* max_m, uint32_t n_clusters, uint64_t seed,
                             uint32_t max_dur, uint32_t cluster_base, hipStream_t s);
-hipError_t launch_gen_arrivals(uint4* jobs, const uint64_t* job_off, uint32_t n_clusters,
-                               uint64_t seed, uint32_t mode, double exp_neg_lambda,
-                               uint32_t cluster_base, hipStream_t s);
-hipError_t launch_gen_bound(const uint64_t* job_off, uint32_t n_clusters, uint64_t seed, uint32_t mode,
-                            double exp_neg_lambda, uint32_t cluster_base, unsigned long long* last,
-                            hipStream_t s);
+hipError_t launch_gen_arrivals(uint4* jobs, const uint64_t* job_off, uint32_t n_clusters, const GenArgs& g,
+                               hipStream_t s);
+hipError_t launch_gen_bound(const uint64_t* job_off, uint32_t n_clusters, const GenArgs& g,
+                            unsigned long long* last, hipStream_t s);
 hipError_t launch_schedule_one(uint32_t* live_c, uint32_t* live_m, uint32_t n, uint32_t c,
                                uint32_t m, int32_t* out_node, hipStream_t s);
 hipError_t launch_lend_check(const uint32_t* live_c, const uint32_t* live_m, uint32_t n,

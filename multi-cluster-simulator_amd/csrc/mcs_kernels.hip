@@ -504,18 +504,24 @@ __global__ __launch_bounds__(256) void gen_attrs_kernel(uint4* jobs, const uint6
 }
 
 __global__ __launch_bounds__(64) void gen_arrivals_kernel(uint4* jobs, const uint64_t* job_off,
-                                                         uint32_t n_clusters, uint64_t seed,
-                                                         uint32_t mode, double enl, uint32_t base) {
+                                                         uint32_t n_clusters, GenArgs g) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_clusters) return;
     const uint64_t j0 = job_off[c], J = job_off[c + 1] - j0;
-    const uint64_t akey = mcs_arrival_key(mcs_cluster_key(seed, base + c));
+    const uint64_t akey = mcs_arrival_key(mcs_cluster_key(g.seed, g.base + c));
     uint64_t j = 0, period = 0;
     uint32_t T = 0;
     // same scan as mcs_gen_arrivals (mcs_gen.h), writing into the .x lane of the records
+    if (g.mode == 2u) {
+        for (; j < J; ++j) {
+            jobs[j0 + j].x = T;
+            T += mcs_weibull_gap(mcs_draw(akey, j), (const uint64_t*)g.wthr, g.wn);
+        }
+        return;
+    }
     while (j < J) {
-        const uint32_t n = mcs_poisson(akey, period++, enl);
-        if (mode == 0u) {
+        const uint32_t n = mcs_poisson(akey, period++, g.enl);
+        if (g.mode == 0u) {
             if (n == 0u) {
                 T += 60u;
                 continue;
@@ -538,17 +544,21 @@ __global__ __launch_bounds__(64) void gen_arrivals_kernel(uint4* jobs, const uin
 
 // last arrival of every cluster's synthetic stream (the scan of mcs_gen_arrivals in 64-bit time,
 // nothing stored): the clock-range check of a fused stream in mcs_generate_jobs
-__global__ __launch_bounds__(64) void gen_bound_kernel(const uint64_t* job_off, uint32_t n_clusters,
-                                                      uint64_t seed, uint32_t mode, double enl,
-                                                      uint32_t base, unsigned long long* last) {
+__global__ __launch_bounds__(64) void gen_bound_kernel(const uint64_t* job_off, uint32_t n_clusters, GenArgs g,
+                                                      unsigned long long* last) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_clusters) return;
     const uint64_t J = job_off[c + 1] - job_off[c];
-    const uint64_t akey = mcs_arrival_key(mcs_cluster_key(seed, base + c));
+    const uint64_t akey = mcs_arrival_key(mcs_cluster_key(g.seed, g.base + c));
     uint64_t j = 0, period = 0, T = 0, lastT = 0;
+    if (g.mode == 2u) {
+        for (; j + 1u < J; ++j) T += mcs_weibull_gap(mcs_draw(akey, j), (const uint64_t*)g.wthr, g.wn);
+        last[c] = T;
+        return;
+    }
     while (j < J) {
-        const uint32_t n = mcs_poisson(akey, period++, enl);
-        if (mode == 0u) {
+        const uint32_t n = mcs_poisson(akey, period++, g.enl);
+        if (g.mode == 0u) {
             if (n == 0u) {
                 T += 60u;
                 continue;
@@ -566,11 +576,11 @@ __global__ __launch_bounds__(64) void gen_bound_kernel(const uint64_t* job_off, 
     last[c] = lastT;
 }
 
-hipError_t launch_gen_bound(const uint64_t* job_off, uint32_t n_clusters, uint64_t seed, uint32_t mode,
-                            double exp_neg_lambda, uint32_t base, unsigned long long* last, hipStream_t s) {
+hipError_t launch_gen_bound(const uint64_t* job_off, uint32_t n_clusters, const GenArgs& g,
+                            unsigned long long* last, hipStream_t s) {
     if (n_clusters == 0) return hipSuccess;
-    hipLaunchKernelGGL(gen_bound_kernel, dim3((n_clusters + 63) / 64), dim3(64), 0, s, job_off, n_clusters,
-                       seed, mode, exp_neg_lambda, base, last);
+    hipLaunchKernelGGL(gen_bound_kernel, dim3((n_clusters + 63) / 64), dim3(64), 0, s, job_off, n_clusters, g,
+                       last);
     return hipGetLastError();
 }
 
@@ -583,12 +593,11 @@ hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t
     return hipGetLastError();
 }
 
-hipError_t launch_gen_arrivals(uint4* jobs, const uint64_t* job_off, uint32_t n_clusters,
-                               uint64_t seed, uint32_t mode, double exp_neg_lambda,
-                               uint32_t base, hipStream_t s) {
+hipError_t launch_gen_arrivals(uint4* jobs, const uint64_t* job_off, uint32_t n_clusters, const GenArgs& g,
+                               hipStream_t s) {
     if (n_clusters == 0) return hipSuccess;
-    hipLaunchKernelGGL(gen_arrivals_kernel, dim3((n_clusters + 63) / 64), dim3(64), 0, s, jobs,
-                       job_off, n_clusters, seed, mode, exp_neg_lambda, base);
+    hipLaunchKernelGGL(gen_arrivals_kernel, dim3((n_clusters + 63) / 64), dim3(64), 0, s, jobs, job_off,
+                       n_clusters, g);
     return hipGetLastError();
 }
 

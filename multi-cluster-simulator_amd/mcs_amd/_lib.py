@@ -38,6 +38,7 @@ MCS_POLICY_FIFO = 0
 MCS_POLICY_DELAY = 1
 MCS_ARRIVAL_REF = 0
 MCS_ARRIVAL_SCALED = 1
+MCS_ARRIVAL_WEIBULL = 2
 
 STATUS_NAMES = {
     MCS_OK: "MCS_OK",
@@ -88,7 +89,8 @@ class mcs_gen_params(C.Structure):
         ("max_cores", C.c_uint32),
         ("max_mem", C.c_uint32),
         ("fused", C.c_uint32),
-        ("reserved", C.c_uint32 * 3),
+        ("weibull_k", C.c_float),
+        ("reserved", C.c_uint32 * 2),
     ]
 
 

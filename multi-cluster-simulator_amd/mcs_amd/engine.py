@@ -36,6 +36,7 @@ class GenParams:
     max_cores: int = 0
     max_mem: int = 0
     fused: bool = False  # synthesise the stream inside the placement kernels (no records in HBM)
+    weibull_k: float = 0.0  # MCS_ARRIVAL_WEIBULL shape (0 = 3, client.go:134); lam is then the scale
 
     def to_c(self) -> L.mcs_gen_params:
         p = L.mcs_gen_params()
@@ -47,6 +48,7 @@ class GenParams:
         p.max_cores = self.max_cores
         p.max_mem = self.max_mem
         p.fused = int(bool(self.fused))
+        p.weibull_k = float(self.weibull_k)
         return p
 
 

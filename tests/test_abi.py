@@ -92,6 +92,25 @@ def test_generator_scaled_mode_rate():
     assert abs(rate - lam) / lam < 0.02
 
 
+def test_generator_weibull_mode_gaps():
+    """MCS_ARRIVAL_WEIBULL (client.go:131-145): gaps are floor(X), X ~ Weibull(scale 10, shape 3):
+    P(gap = n) = exp(-(n/10)^3) - exp(-((n+1)/10)^3); job 0 arrives at t = 0."""
+    a, d, c, m = gen_cluster_host(GenParams(seed=21, arrival_mode=2, lam=10.0), 0, 32, 24000, 300_000)
+    assert a[0] == 0 and (np.diff(a.astype(np.int64)) >= 0).all()
+    g = np.diff(a.astype(np.int64))
+    n = np.arange(0, 40)
+    pmf = np.exp(-(n / 10.0) ** 3) - np.exp(-((n + 1) / 10.0) ** 3)
+    emp = np.bincount(g, minlength=40)[:40] / len(g)
+    assert np.abs(emp - pmf).max() < 0.003
+    assert abs(g.mean() - (pmf * n).sum()) < 0.03
+    # the shape parameter is honoured, and a scale whose gap table would not vanish is refused
+    a2 = gen_cluster_host(GenParams(seed=21, arrival_mode=2, lam=10.0, weibull_k=1.5), 0, 32, 24000, 100_000)[0]
+    n2 = np.arange(1, 200)
+    assert abs(np.diff(a2.astype(np.int64)).mean() - np.exp(-(n2 / 10.0) ** 1.5).sum()) < 0.1  # E[floor X]
+    with pytest.raises(mcs_amd.MCSError):
+        gen_cluster_host(GenParams(arrival_mode=2, lam=1000.0), 0, 32, 24000, 10)
+
+
 def test_generator_rejects_bad_params():
     with pytest.raises(mcs_amd.MCSError):
         gen_cluster_host(GenParams(lam=0.0), 0, 32, 24000, 10)

@@ -38,10 +38,13 @@ CASES = [
     ("FIFO", L.MCS_ARRIVAL_SCALED, None, 2500),
     ("DELAY", L.MCS_ARRIVAL_REF, 10.0, 2000),
     ("DELAY", L.MCS_ARRIVAL_SCALED, 0.8, 1000),
+    ("FIFO", L.MCS_ARRIVAL_WEIBULL, 10.0, 2500),   # the client's "weibull" mode (client.go:131-145)
+    ("DELAY", L.MCS_ARRIVAL_WEIBULL, 6.0, 1500),
 ]
+MODE_NAMES = {L.MCS_ARRIVAL_REF: "REF", L.MCS_ARRIVAL_SCALED: "SCALED", L.MCS_ARRIVAL_WEIBULL: "WEIBULL"}
 
 
-@pytest.mark.parametrize("policy,mode,lam,jobs", CASES, ids=[f"{c[0]}-{'REF' if c[1] == 0 else 'SCALED'}" for c in CASES])
+@pytest.mark.parametrize("policy,mode,lam,jobs", CASES, ids=[f"{c[0]}-{MODE_NAMES[c[1]]}" for c in CASES])
 def test_fused_equals_records_and_oracle(policy, mode, lam, jobs):
     arrays = mixed_arrays()
     lam = lam if lam is not None else scaled_lambda(256, load=0.9)
@@ -113,3 +116,23 @@ def test_fused_stream_drives_delay_trading():
     for a, b in zip(res[0][0], res[1][0]):
         np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("lam,k", [(10.0, 3.0), (2.5, 1.5), (40.0, 6.0)])
+def test_weibull_device_records_equal_host(lam, k):
+    """WEIBULL arrivals materialised by the device generator (gen_arrivals_kernel) and synthesised
+    in the kernel both equal the host generator, for the reference's (Lambda 10, K 3) and others."""
+    arrays = mixed_arrays()
+    gp = GenParams(seed=99, arrival_mode=L.MCS_ARRIVAL_WEIBULL, lam=lam, weibull_k=k)
+    with Engine(0) as eng:
+        eng.load_clusters(arrays)
+        eng.generate_jobs(gp, 3001)
+        dev = eng.read_jobs()
+    host = gen_streams_host(gp, arrays, 3001)
+    for f in ("arrival", "dur", "cores", "mem"):
+        np.testing.assert_array_equal(getattr(dev, f), getattr(host, f), err_msg=f)
+    gp.fused = True
+    fz = run("FIFO", arrays, gp, 3001)
+    on, os_, of, _ = O.fifo_run_batch(arrays, host, n_threads=8)
+    np.testing.assert_array_equal(fz[0], on)
+    np.testing.assert_array_equal(fz[1], os_)
