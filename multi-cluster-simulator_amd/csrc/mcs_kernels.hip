@@ -39,7 +39,58 @@
 #include "mcs_internal.h"
 #include "mcs_wave.h"
 
+#ifdef MCS_STAMPS
+// diagnostic build only (tools/stamp_probe.py): per-segment cycle sums of the pass loop
+#define MCS_STAMP(v)                                                                    \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");       \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+    } while (0)
+__device__ unsigned long long g_stamps[8];
+#else
+#define MCS_STAMP(v) \
+    do {             \
+    } while (0)
+#endif
+
 namespace mcs {
+
+// nvr[c] = nodes[c * 64 + lane] for every chunk, and one wait, in one asm statement (LLVM then
+// tracks no LDS load of its own, and no copy of a register still being loaded can slip between
+// the reads and the wait; base = this lane's byte address of chunk 0)
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+#define MCS_RD2(i) "ds_read2st64_b64 %" #i ", %[b] offset0:" #i "*2 offset1:" #i "*2+1\n\t"
+template <int NPL>
+__device__ __forceinline__ void reload_nodes(uint64_t (&nvr)[NPL], uint32_t base) {
+    if constexpr (NPL == 1) {
+        asm volatile("ds_read_b64 %0, %[b]\n\ts_waitcnt lgkmcnt(0)" : "=v"(nvr[0]) : [b] "v"(base) : "memory");
+    } else {
+        u64x2 q[8];
+        if constexpr (NPL == 2) {
+            asm volatile(MCS_RD2(0) "s_waitcnt lgkmcnt(0)" : "=v"(q[0]) : [b] "v"(base) : "memory");
+        } else if constexpr (NPL == 4) {
+            asm volatile(MCS_RD2(0) MCS_RD2(1) "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(q[0]), "=&v"(q[1]) : [b] "v"(base) : "memory");
+        } else if constexpr (NPL == 8) {
+            asm volatile(MCS_RD2(0) MCS_RD2(1) MCS_RD2(2) MCS_RD2(3) "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]) : [b] "v"(base) : "memory");
+        } else {
+            static_assert(NPL == 16, "chunks per lane");
+            asm volatile(MCS_RD2(0) MCS_RD2(1) MCS_RD2(2) MCS_RD2(3) MCS_RD2(4) MCS_RD2(5) MCS_RD2(6)
+                             MCS_RD2(7) "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5]),
+                           "=&v"(q[6]), "=&v"(q[7])
+                         : [b] "v"(base) : "memory");
+        }
+#pragma unroll
+        for (int c = 0; c < NPL / 2; ++c) {
+            nvr[2 * c] = q[c].x;
+            nvr[2 * c + 1] = q[c].y;
+        }
+    }
+}
+#undef MCS_RD2
 
 // HOR: the online variant.  The cluster resumes from the OnlineState, node image
 // and slot image of the previous horizon (or its spec when the state is not valid), runs every
@@ -107,7 +158,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
 #pragma unroll
     for (int p = 0; p < P; ++p) pay_nf[p * kWave + lane] = (uint64_t)kEmpty << 32;  // free: never expires
 
-    uint32_t t = 0, r = 0, minf = kEmpty, flags = 0;
+    uint32_t t = 0, r = 0, flags = 0;
     // Counters that no decision reads live in VGPRs (the asm hides their uniformity): the CU's
     // one scalar unit is shared by 16 cluster waves and is the scarcer issue resource.
     uint32_t used = 0, peak = 0, waited = 0, placed = 0;
@@ -140,7 +191,6 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                     }
                 }
             }
-            minf = wave_min_u32(lmin);
             t = st.t;
             r = st.cursor;
             have_w = st.aux;
@@ -172,60 +222,191 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     // prefetch, which the loop never reads, so the waitcnt pass does not flush it at every batch
     asm volatile("" ::"v"(nxt.x), "v"(nxt.y), "v"(nxt.z), "v"(nxt.w));
 
+    // LDS byte addresses of the node vector and of this lane's slot column
+    const uint32_t nodes_lds = lds_addr(nodes);
+    const uint32_t pay_lds = lds_addr(pay) + lane * 8u;
+
+    // Node free vectors in registers (nvr[c]: node lane * NPL + c), the state every decision
+    // reads: a commit updates them in place, so a decision never waits on LDS.  The LDS copy
+    // nodes[] is written only for a release, whose hand-backs are LDS atomics, and read back
+    // inside it.
+    uint64_t nvr[NPL];
+#pragma unroll
+    for (int c = 0; c < NPL; ++c) {
+        nvr[c] = nodes[c * kWave + lane];
+        asm volatile("" ::"v"(nvr[c]));  // waited for here, not at the loop's first compare
+    }
+
     // release every running job with finish <= t (cluster.go:153-157; A.2 step 1).  Row by row:
-    // the expired test of row p over all lanes is one compare whose lane mask drives both the
-    // payload hand-back of that row (one pass per row with any expiry, constant LDS offsets) and
-    // the free-row bits; the lane's next finish is the min over its unexpired rows.
+    // the expired test of row p over all lanes is one compare straight into a lane mask, which
+    // drives the payload hand-back of that row (only rows with an expiry branch off the straight
+    // line) and the free-row bits; the lane's next finish is the min over its unexpired rows.
     auto release = [&]() __attribute__((always_inline)) {
         ++n_rel;
-        uint32_t lm = kEmpty;
-        uint64_t nf[P];
-        bool ex[P];
 #pragma unroll
-        for (int p = 0; p < P; ++p) {  // free rows hold kEmpty: never expired, min-neutral
+        for (int c = 0; c < NPL; ++c) nodes[c * kWave + lane] = nvr[c];  // publish (LDS in order)
+        const uint32_t t1 = t + 1u;  // t < kEmpty here (a wrap stops the run first)
+        uint64_t nf[P], cm[P];
+        uint64_t m[P];
+        // lane's next finish: min over unexpired rows, as min(f - (t + 1)) + (t + 1) in u32: an
+        // expired row (f <= t) wraps above every unexpired and free one, and the bound ~t1 caps
+        // the result at kEmpty when the lane has none left
+        uint32_t lm = ~t1;
+#pragma unroll
+        for (int p = 0; p < P; ++p) {  // free rows hold kEmpty: never expired
             nf[p] = pay_nf[p * kWave + lane];
+            cm[p] = pay_cm[p * kWave + lane];  // (read with the finish words: one wait)
             const uint32_t f = (uint32_t)(nf[p] >> 32);
-            ex[p] = f <= t;
-            const uint32_t fl = ex[p] ? kEmpty : f;
-            lm = fl < lm ? fl : lm;
+            m[p] = lanes_ge(t, f);
+            const uint32_t d = f - t1;
+            lm = d < lm ? d : lm;
         }
-        lmin = lm;
         uint32_t nexp = 0u;
 #pragma unroll
         for (int p = 0; p < P; ++p) {
-            const uint64_t m = __ballot(ex[p]);
-            if (m) {
-                nexp += (uint32_t)__builtin_popcountll(m);
-                if (ex[p]) {  // give the payload back to its node; the row is free again
-                    atomicAdd((unsigned long long*)&nodes[(uint32_t)nf[p]],
-                              (unsigned long long)pay_cm[p * kWave + lane]);
-                    reinterpret_cast<uint32_t*>(pay_nf)[2 * (p * kWave + lane) + 1] = kEmpty;
-                    frm |= 1u << p;
-                }
+            if (__builtin_expect(m[p] != 0ull, 0)) {
+                nexp += (uint32_t)__builtin_popcountll(m[p]);
+                // the expired lanes (exec = m[p]) give their payloads back to their nodes and
+                // free the row: ds_add_u64 on the node, finish word := kEmpty (no wait: the
+                // node reload below is ordered after them by LDS)
+                const uint32_t na = nodes_lds + (uint32_t)nf[p] * 8u;
+                uint64_t sv;
+                asm volatile(
+                    "s_mov_b64 %[sv], exec\n\t"
+                    "s_mov_b64 exec, %[m]\n\t"
+                    "ds_add_u64 %[na], %[cm]\n\t"
+                    "ds_write_b32 %[pa], %[emp] offset:%[of]\n\t"
+                    "v_or_b32 %[frm], %[bit], %[frm]\n\t"
+                    "s_mov_b64 exec, %[sv]"
+                    : [sv] "=&s"(sv), [frm] "+v"(frm)
+                    : [m] "s"(m[p]), [pa] "v"(pay_lds), [na] "v"(na), [cm] "v"(cm[p]), [emp] "v"(kEmpty),
+                      [bit] "i"(1u << p), [of] "i"((P + p) * kWave * 8 + 4)
+                    : "memory");
             }
         }
         used -= nexp;
-        minf = wave_min_u32(lmin);
+        // read the node vectors back and wait here, in one statement: LLVM then has no LDS load
+        // of its own in flight, and no decision path carries a wait
+        reload_nodes(nvr, nodes_lds + lane * 8u);
+        lmin = lm + t1;
     };
 
+    // rend bounds the ready cursor of the inner pass loop: the end of the current batch, or 0 once
+    // the run stops, so one scalar compare ends both loops
+    uint32_t rend = 0u;
+    // a placement of job ri on node k = fl * NPL + fch at t: the result record (lane ri & 63 of
+    // the register batch) and, for a job that runs, Node.RunJob's commit (cluster.go:146-147,
+    // synchronous D2) with the running-slot insert.  fr: lanes with a free slot row.
+    auto place = [&](uint32_t ri, uint32_t jd, uint32_t jc, uint32_t jm, uint32_t fl, uint32_t fch,
+                     uint64_t fr) __attribute__((always_inline)) {
+        const uint32_t k = fl * NPL + fch;     // the node (Go index)
+        const uint32_t kx = fch * kWave + fl;  // its place in nodes[]
+        const uint32_t ol = ri & 63u;
+        const uint32_t fin = t + jd;
+        // lane ol of the batch takes (k, t, fin): three v_writelane (lane select in m0, the one
+        // scalar operand gfx950 allows beside the data SGPR); m0 is reserved to the compiler,
+        // which uses it nowhere in these kernels
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+        asm("s_mov_b32 m0, %3\n\ts_nop 0\n\t"
+            "v_writelane_b32 %0, %4, m0\n\t"
+            "v_writelane_b32 %1, %5, m0\n\t"
+            "v_writelane_b32 %2, %6, m0"
+            : "+v"(on), "+v"(os), "+v"(of)
+            : "s"(sgpr(ol)), "s"(sgpr(k)), "s"(sgpr(t)), "s"(sgpr(fin))
+            : "m0");
+#pragma clang diagnostic pop
+        // A zero-duration job is committed and released before the next decision can read the
+        // node (RunJob sleeps 0; the release precedes the next branch, D3).
+        if (jd != 0u) {
+            // a finish that wraps the u32 clock or hits the kEmpty sentinel (D8 range) is
+            // recorded off the decision chain, in VALU: the first such job ends the valid
+            // results.  Only the online variant carries this guard: the host bound keeps checked
+            // streams away from it, and the engine runs batch runs of unchecked streams
+            // (cfg.unchecked_horizon) through the online variant
+            if constexpr (HOR) {
+                uint32_t tv = t, jv = jd;  // VGPR copies: the check stays in VALU
+                asm volatile("" : "+v"(tv), "+v"(jv));
+                const uint32_t fv = tv + jv;
+                const uint32_t cand = (fv + 1u <= tv) ? ri : kEmpty;
+                ovf_r = cand < ovf_r ? cand : ovf_r;
+            }
+            // slot insert: the lowest lane with a free row, its lowest free row.  On a pool
+            // overflow the run stops and the cluster is re-run with a bigger pool.
+            if (!fr) {
+                flags |= MCS_FLAG_OVERFLOW;
+                rend = 0u;
+            } else {
+                // commit in registers: lane fl, chunk fch (packed halves: the job fits, so the
+                // low half never borrows)
+                const bool me = lane == fl;
+                const uint32_t dc = me ? jc : 0u, dm = me ? jm : 0u;
+#pragma unroll
+                for (int c = 0; c < NPL; ++c)
+                    if ((uint32_t)c == fch)
+                        nvr[c] = (uint64_t)((uint32_t)nvr[c] - dc) |
+                                 ((uint64_t)((uint32_t)(nvr[c] >> 32) - dm) << 32);
+                // That one lane (exec = its bit) writes the slot {need, node | fin << 32}; its
+                // free rows and earliest finish follow.  One asm block: exec is restored before
+                // anything else issues.
+                const uint64_t need = (uint64_t)jc | ((uint64_t)jm << 32);
+                const uint64_t nfw = (uint64_t)kx | ((uint64_t)fin << 32);  // release target
+                // (under that exec: slot row = lowest free bit, address = row * 512 + lane * 8)
+                uint64_t sv;
+                uint32_t ta, tf;
+                asm volatile(
+                    "s_mov_b64 %[sv], exec\n\t"
+                    "s_mov_b64 exec, %[m]\n\t"
+                    "v_ffbl_b32 %[ta], %[frm]\n\t"
+                    "v_lshl_add_u32 %[ta], %[ta], 9, %[pl]\n\t"
+                    "ds_write2st64_b64 %[ta], %[nd], %[nf] offset1:%[off]\n\t"
+                    "v_add_u32 %[tf], -1, %[frm]\n\t"
+                    "v_and_b32 %[frm], %[tf], %[frm]\n\t"
+                    "v_min_u32 %[lmin], %[fin], %[lmin]\n\t"
+                    "s_mov_b64 exec, %[sv]"
+                    : [sv] "=&s"(sv), [ta] "=&v"(ta), [tf] "=&v"(tf), [frm] "+v"(frm), [lmin] "+v"(lmin)
+                    : [m] "s"(1ull << __builtin_ctzll(fr)), [nd] "v"(need), [pl] "v"(pay_lds),
+                      [nf] "v"(nfw), [fin] "s"(sgpr(fin)), [off] "i"(P)
+                    : "memory");
+                ++used;
+                peak = used > peak ? used : peak;
+            }
+        }
+    };
 
     // ---- Scheduler.Fifo (scheduler.go:216-296) ----
     // One pass = one decision; the loop has a single exit (the structurizer then needs no flow
-    // copies of the loop-carried registers).  rend bounds the ready cursor of the inner loop: the
-    // end of the current batch, or 0 once the run stops, so one scalar compare ends both loops.
-    uint32_t rend = 0u;
-    // node free vectors for the next first fit, read at the end of the previous pass (after its
-    // commit and releases) so the LDS latency overlaps the record broadcast of the next pass
-    uint64_t nvr[NPL];
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) nvr[k] = nodes[k * kWave + lane];
+    // copies of the loop-carried registers).  rend (declared above) bounds the ready cursor of
+    // the inner loop.
+#ifdef MCS_STAMPS
+    unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+    unsigned long long ss[7] = {};
+#endif
+    // advance the clock to tn (> t): releases at the new instant (A.2 step 1), then the online
+    // horizon; a tn below t means the u32 seconds clock wrapped (D8 range exceeded): stop, flagged
+    auto advance = [&](uint32_t tn) __attribute__((always_inline)) {
+        if (tn < t) {
+            flags |= MCS_FLAG_CLOCK_OVERFLOW;
+            rend = 0u;
+        } else {
+            t = tn;
+            if (lanes_ge(t, lmin) != 0ull) {  // a running job finishes by t
+                release();
+                MCS_STAMP(t3);
+            }
+            if constexpr (HOR) {
+                if (t >= a.on.t_hor) rend = 0u;  // the horizon: resume here next time
+            }
+        }
+    };
+
+    // The ReadyQueue head's record {arrival, dur, cores, mem} (jr, job r) in scalar registers,
+    // broadcast from the batch registers (v_readlane) when the cursor moves.
+    uint4 jr = make_uint4(0u, 0u, 0u, 0u);
     if (live) {
-    // Outer loop: one 64-record batch; inner loop: the passes whose ready cursor is in it.  The
-    // batch registers change only here, once per batch, so no pass copies them (a per-pass
-    // conditional swap made LLVM copy both buffers and wait for the prefetch on every pass).
-    // The previous batch's results (all 64 placed) are stored here, after the wait for this
-    // batch's records and before the next prefetch: the batch-boundary wait then covers only
-    // memory operations issued a whole batch earlier, never stores still in flight to HBM.
+    // Outer loop: one 64-job result batch (and, fused, one 64-record batch); inner loop: the
+    // passes whose ready cursor is in it.  The previous batch's results (all 64 placed) are
+    // stored here.
     do {
     const uint4 cur = nxt;
     if (cb != cb0) {  // a full batch: every lane's job cb - 64 + lane < J, no mask
@@ -234,131 +415,105 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         __builtin_nontemporal_store(os, o_start + i);
         __builtin_nontemporal_store(of, o_finish + i);
     }
-    nxt = load_batch(cb + kWave);  // prefetch one batch ahead
+    nxt = load_batch(cb + kWave);  // prefetch (or generate) one batch ahead
+    {
+        const uint32_t l = r - cb;
+        jr = make_uint4(readlane(cur.x, l), readlane(cur.y, l), readlane(cur.z, l), readlane(cur.w, l));
+    }
     rend = cb + kWave;
     do {
+        MCS_STAMP(t0);
+#ifdef MCS_STAMPS
+        t1 = t0;
+        t3 = 0;
+#endif
         ++n_iter;
-        // ReadyQueue head (:255-260): the next stream job, queued once its arrival has passed
-        const uint32_t l = r - cb;
-        const uint32_t arr = readlane(cur.x, l);
-        const uint32_t jd = readlane(cur.y, l);
-        const uint32_t jc = readlane(cur.z, l);
-        const uint32_t jm = readlane(cur.w, l);
-        uint32_t tn = t;
-        if (r >= J) {  // every job decided
+        // ReadyQueue head (:255-260): the next stream job, queued once its arrival has passed.
+        // Streamed: one scalar load per pass, a value of this pass only (a loop-carried record
+        // made LLVM copy it at the latch, waiting for the load there)
+        const uint32_t arr = jr.x, jd = jr.y, jc = jr.z, jm = jr.w;
+        if (__builtin_expect(r >= J, 0)) {  // every job decided
+            MCS_STAMP(t2);
             rend = 0u;
-        } else if (arr > t) {  // all queues empty: 1 s sleeps to the arrival (:294); a wait head
-            tn = arr;          // has always arrived, so this is never taken with have_w
+        } else if (__builtin_expect(arr > t, 0)) {  // all queues empty: 1 s sleeps to the arrival
+            MCS_STAMP(t2);                           // (:294); a wait head has always arrived,
+            advance(arr);                            // so this is never taken with have_w
         } else {
             // first fit — ScheduleJob, scheduler.go:129-137: lowest node index with both >=.
-            // Each lane finds its lowest fitting chunk (descending selects); the lowest lane with
-            // a fit (ballot + ff1) holds the node, and one readlane fetches its chunk.
-            uint32_t bc = NPL;
+            // One lane mask per chunk (two compares straight into scalar registers); the lowest
+            // lane with any fit holds the node, at the lowest chunk whose mask has that lane.
+            uint64_t F[NPL];
+            uint64_t fit = 0ull;
 #pragma unroll
-            for (int c = NPL - 1; c >= 0; --c) {
+            for (int c = 0; c < NPL; ++c) {
                 const uint64_t v = nvr[c];
-                bc = ((uint32_t)v >= jc && (uint32_t)(v >> 32) >= jm) ? (uint32_t)c : bc;
+                F[c] = lanes_ge((uint32_t)v, jc) & lanes_ge((uint32_t)(v >> 32), jm);
+                fit |= F[c];
             }
-            const uint64_t fit = __ballot(bc < (uint32_t)NPL) & vmask;
-            if (fit) {
+            fit &= vmask;
+            // each lane's lowest fitting chunk, selected in VALU by the chunk masks (the scalar
+            // unit is shared by the CU's waves; the vector unit is per SIMD)
+            uint32_t bc = NPL - 1;
+#pragma unroll
+            for (int c = NPL - 2; c >= 0; --c)  // bc = F[c] has this lane ? c : bc (mask operand)
+                asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(bc) : "v"(bc), "i"(c), "s"(F[c]));
+#ifdef MCS_STAMPS
+            asm volatile("" ::"s"(fit));
+#endif
+            MCS_STAMP(t1);
+            if (__builtin_expect(fit != 0ull, 1)) {
                 const uint32_t fl = (uint32_t)__builtin_ctzll(fit);
-                const uint32_t fch = readlane(bc, fl);
-                const uint32_t k = fl * NPL + fch;        // the node (Go index)
-                const uint32_t kx = fch * kWave + fl;     // its place in nodes[]
-                // placement record, 64 jobs per register batch (jobs are placed in job order)
-                const uint32_t ol = r & 63u;
-                const uint32_t fin = t + jd;
-                // lane ol of the batch takes (k, t, fin): three v_writelane (lane select in m0,
-                // the one scalar operand gfx950 allows beside the data SGPR)
-                // m0 is reserved to the compiler, which uses it nowhere in these kernels
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-                asm("s_mov_b32 m0, %3\n\ts_nop 0\n\t"
-                    "v_writelane_b32 %0, %4, m0\n\t"
-                    "v_writelane_b32 %1, %5, m0\n\t"
-                    "v_writelane_b32 %2, %6, m0"
-                    : "+v"(on), "+v"(os), "+v"(of)
-                    : "s"(sgpr(ol)), "s"(sgpr(k)), "s"(sgpr(t)), "s"(sgpr(fin))
-                    : "m0");
-#pragma clang diagnostic pop
-                ++placed;
-                // A zero-duration job is committed and released before the next decision can
-                // read the node (RunJob sleeps 0; the release precedes the next branch, D3).
-                if (jd != 0u) {
-                    // a finish that wraps the u32 clock or hits the kEmpty sentinel (D8 range)
-                    // is recorded off the decision chain, in VALU: the first such job ends the
-                    // valid results.  Only the online variant carries this guard: the host bound
-                    // keeps checked streams away from it, and the engine runs batch runs of
-                    // unchecked streams (cfg.unchecked_horizon) through the online variant
-                    if constexpr (HOR) {
-                        uint32_t tv = t, jv = jd;  // VGPR copies: the check stays in VALU
-                        asm volatile("" : "+v"(tv), "+v"(jv));
-                        const uint32_t fv = tv + jv;
-                        const uint32_t cand = (fv + 1u <= tv) ? r : kEmpty;
-                        ovf_r = cand < ovf_r ? cand : ovf_r;
-                    }
-                    const uint64_t need = (uint64_t)jc | ((uint64_t)jm << 32);
-                    // slot insert: the lowest lane with a free row, its lowest free row.  That
-                    // lane also commits — Node.RunJob, cluster.go:146-147 (synchronous, D2) — since
-                    // any lane can reach any node in LDS; on a pool overflow the run stops and the
-                    // cluster is re-run with a bigger pool, so the skipped commit never matters.
-                    const uint64_t any = __ballot(frm != 0u);
-                    if (!any) {
-                        flags |= MCS_FLAG_OVERFLOW;
-                        rend = 0u;
-                    } else {
-                        if (lane == (uint32_t)__builtin_ctzll(any)) {
-                            __hip_atomic_fetch_sub(&nodes[kx], need, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);  // ds_sub_u64
-                            const uint32_t ad = (uint32_t)__builtin_ctz(frm) * kWave + lane;  // frm != 0 here
-                            frm &= frm - 1u;
-                            pay_cm[ad] = need;
-                            pay_nf[ad] = (uint64_t)kx | ((uint64_t)fin << 32);  // release target
-                            lmin = fin < lmin ? fin : lmin;
-                        }
-                        ++used;
-                        peak = used > peak ? used : peak;
-                        minf = fin < minf ? fin : minf;
-                    }
+                const uint32_t fch = NPL > 1 ? readlane(bc, fl) : 0u;
+                place(r, jd, jc, jm, fl, fch, lanes_ne(frm, 0u));
+                ++r;
+                {
+                    const uint32_t l = (r - cb) & 63u;  // (a batch boundary reloads it above)
+                    jr = make_uint4(readlane(cur.x, l), readlane(cur.y, l), readlane(cur.z, l),
+                                    readlane(cur.w, l));
                 }
+                MCS_STAMP(t2);
                 // wait head: WaitQueue = WaitQueue[1:] (:226; D1) and time.Sleep(1 s) (:250);
                 // ready head: next job, no sleep (:272)
-                tn = t + have_w;
-                ++r;
-                have_w = 0u;
+                if (__builtin_expect(have_w != 0u, 0)) {
+                    have_w = 0u;
+                    advance(t + 1u);
+                }
             } else {
                 // State = WAITING; WaitQueue append (:264-268).  The Go loop's next pass retries
                 // the new head at this same instant on an unchanged cluster (certain to fail),
-                // then sleeps: folded into the fast-forward below.
+                // then sleeps: folded into the fast-forward.
                 waited += 1u - have_w;
                 have_w = 1u;
+                MCS_STAMP(t2);
+                // the next completion, over every lane's earliest finish (only waits need it)
+                const uint32_t minf = wave_min_u32(lmin);
                 if (minf == kEmpty) {  // nothing running: the head can never fit
                     flags |= MCS_FLAG_DEADLOCK;
                     rend = 0u;
                 } else {  // A.3: 1 s retries until the next completion (no lender, :234)
-                    tn = minf > t + 1u ? minf : t + 1u;
+                    advance(minf > t + 1u ? minf : t + 1u);
                 }
             }
         }
-        if (tn != t) {  // (after a stop only an overflowed run moves t; it is re-run anyway)
-            if (tn < t) {  // the u32 seconds clock would wrap (D8 range exceeded): stop, flagged
-                flags |= MCS_FLAG_CLOCK_OVERFLOW;
-                rend = 0u;
-            } else {
-                t = tn;
-                if (minf <= t) release();
-                if constexpr (HOR) {
-                    if (t >= a.on.t_hor) rend = 0u;  // the horizon: resume here next time
-                }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NPL; ++k) nvr[k] = nodes[k * kWave + lane];
+#ifdef MCS_STAMPS
+        if (t3 == 0) t3 = t2;
+#endif
+        MCS_STAMP(t4);
+#ifdef MCS_STAMPS
+        ss[0] += t1 - t0;
+        ss[1] += t2 - t1;
+        ss[2] += t3 - t2;
+        ss[3] += t4 - t3;
+        ss[4] += 1u;
+        ss[5] += t3 != t2 ? 1u : 0u;
+        ss[6] += t1 != t0 ? 1u : 0u;
+#endif
     } while (r < rend);
     cb += kWave;
     } while (rend != 0u);
     }  // live
 
+    placed = r;  // FIFO places every job it decides, in order
     // [rs, J) is undecided: a deadlocked head and everything behind it (the Go loop retries the
     // head forever), or every job from the first one whose clock left the u32 range (the run
     // fails with MCS_E_RANGE)
@@ -388,10 +543,9 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
 
     if constexpr (HOR) {  // save the state the next horizon resumes from (rerun on overflow)
         if (!(flags & MCS_FLAG_OVERFLOW)) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // other lanes' LDS atomics
             unsigned long long* img = a.on.img_out + (size_t)ci * a.on.img_stride;
 #pragma unroll
-            for (int c = 0; c < NPL; ++c) img[c * kWave + lane] = nodes[c * kWave + lane];
+            for (int c = 0; c < NPL; ++c) img[c * kWave + lane] = nvr[c];  // the register truth
             unsigned long long* sl = a.on.slot_out + (size_t)ci * kSlotImg;
 #pragma unroll
             for (int p = 0; p < P; ++p) {
@@ -417,6 +571,10 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         }
     }
 
+#ifdef MCS_STAMPS
+    if (lane == 0)
+        for (int q = 0; q < 7; ++q) atomicAdd(&g_stamps[q], ss[q]);
+#endif
     if (lane == 0) {
         mcs_cluster_stats st;
         st.t_end = t;
@@ -677,3 +835,13 @@ hipError_t launch_utilization(const uint2* cap, const uint32_t* live_c, const ui
 }
 
 }  // namespace mcs
+
+#ifdef MCS_STAMPS
+// sums [decide, place, release, reload, passes, releasing passes, deciding passes, -]; reset after read
+extern "C" int mcs_debug_stamps(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) != hipSuccess) return -1;
+    unsigned long long z[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

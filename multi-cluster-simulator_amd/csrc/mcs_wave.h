@@ -7,6 +7,22 @@
 
 namespace mcs {
 
+// lane mask of a >= b (unsigned): one v_cmp into a scalar register pair (a __ballot of a
+// combined bool re-materialises the mask through a VGPR)
+__device__ __forceinline__ uint64_t lanes_ge(uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_uicmp(a, b, 35 /* ICMP_UGE */);
+}
+
+__device__ __forceinline__ uint64_t lanes_ne(uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_uicmp(a, b, 33 /* ICMP_NE */);
+}
+
+// the byte offset of a __shared__ object in LDS (for inline-asm ds_* operands)
+template <typename T>
+__device__ __forceinline__ uint32_t lds_addr(T* p) {
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)p;
+}
+
 __device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
