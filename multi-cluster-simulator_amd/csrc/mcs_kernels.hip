@@ -56,41 +56,67 @@ __device__ unsigned long long g_stamps[8];
 
 namespace mcs {
 
+// LDS costs on gfx950 (tools/micro/ldsbw.hip, 16 waves per CU): the LDS pipe spends about 2 CU
+// cycles on a ds_read_b64 or _b32, 4 on a read2 / read_b128, 8 on a read2st64_b64, 6 on a
+// ds_write_b64 or ds_add_u64 and 13.5 on a write2st64_b64 — per instruction, whatever the number
+// of active lanes.  At 16 cluster waves per CU the LDS pipe is the shared resource, so every LDS
+// access below is a single-address b64 instruction (LLVM would pair neighbouring loads into
+// read2st64, so they are written in asm).
+//
 // nvr[c] = nodes[c * 64 + lane] for every chunk, and one wait, in one asm statement (LLVM then
 // tracks no LDS load of its own, and no copy of a register still being loaded can slip between
 // the reads and the wait; base = this lane's byte address of chunk 0)
-typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-#define MCS_RD2(i) "ds_read2st64_b64 %" #i ", %[b] offset0:" #i "*2 offset1:" #i "*2+1\n\t"
+#define MCS_R1(i) "ds_read_b64 %" #i ", %[b] offset:" #i "*512\n\t"
+#define MCS_R4(i0, i1, i2, i3) MCS_R1(i0) MCS_R1(i1) MCS_R1(i2) MCS_R1(i3)
+#define MCS_O4(a, i) "=&v"(a[i]), "=&v"(a[i + 1]), "=&v"(a[i + 2]), "=&v"(a[i + 3])
 template <int NPL>
 __device__ __forceinline__ void reload_nodes(uint64_t (&nvr)[NPL], uint32_t base) {
     if constexpr (NPL == 1) {
-        asm volatile("ds_read_b64 %0, %[b]\n\ts_waitcnt lgkmcnt(0)" : "=v"(nvr[0]) : [b] "v"(base) : "memory");
+        asm volatile(MCS_R1(0) "s_waitcnt lgkmcnt(0)" : "=&v"(nvr[0]) : [b] "v"(base) : "memory");
+    } else if constexpr (NPL == 2) {
+        asm volatile(MCS_R1(0) MCS_R1(1) "s_waitcnt lgkmcnt(0)" : "=&v"(nvr[0]), "=&v"(nvr[1]) : [b] "v"(base) : "memory");
+    } else if constexpr (NPL == 4) {
+        asm volatile(MCS_R4(0, 1, 2, 3) "s_waitcnt lgkmcnt(0)" : MCS_O4(nvr, 0) : [b] "v"(base) : "memory");
+    } else if constexpr (NPL == 8) {
+        asm volatile(MCS_R4(0, 1, 2, 3) MCS_R4(4, 5, 6, 7) "s_waitcnt lgkmcnt(0)"
+                     : MCS_O4(nvr, 0), MCS_O4(nvr, 4) : [b] "v"(base) : "memory");
     } else {
-        u64x2 q[8];
-        if constexpr (NPL == 2) {
-            asm volatile(MCS_RD2(0) "s_waitcnt lgkmcnt(0)" : "=v"(q[0]) : [b] "v"(base) : "memory");
-        } else if constexpr (NPL == 4) {
-            asm volatile(MCS_RD2(0) MCS_RD2(1) "s_waitcnt lgkmcnt(0)"
-                         : "=&v"(q[0]), "=&v"(q[1]) : [b] "v"(base) : "memory");
-        } else if constexpr (NPL == 8) {
-            asm volatile(MCS_RD2(0) MCS_RD2(1) MCS_RD2(2) MCS_RD2(3) "s_waitcnt lgkmcnt(0)"
-                         : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]) : [b] "v"(base) : "memory");
-        } else {
-            static_assert(NPL == 16, "chunks per lane");
-            asm volatile(MCS_RD2(0) MCS_RD2(1) MCS_RD2(2) MCS_RD2(3) MCS_RD2(4) MCS_RD2(5) MCS_RD2(6)
-                             MCS_RD2(7) "s_waitcnt lgkmcnt(0)"
-                         : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5]),
-                           "=&v"(q[6]), "=&v"(q[7])
-                         : [b] "v"(base) : "memory");
-        }
+        static_assert(NPL == 16, "chunks per lane");
+        asm volatile(MCS_R4(0, 1, 2, 3) MCS_R4(4, 5, 6, 7) MCS_R4(8, 9, 10, 11) MCS_R4(12, 13, 14, 15)
+                     "s_waitcnt lgkmcnt(0)"
+                     : MCS_O4(nvr, 0), MCS_O4(nvr, 4), MCS_O4(nvr, 8), MCS_O4(nvr, 12) : [b] "v"(base) : "memory");
+    }
+}
+
+// nf[p] = row p of the {node | finish << 32} slot words (base: this lane's address of row 0),
+// 16 rows per asm statement with its wait
+template <int P>
+__device__ __forceinline__ void read_finish_rows(uint64_t (&nf)[P], uint32_t base) {
+    if constexpr (P == 2) {
+        asm volatile(MCS_R1(0) MCS_R1(1) "s_waitcnt lgkmcnt(0)" : "=&v"(nf[0]), "=&v"(nf[1]) : [b] "v"(base) : "memory");
+    } else if constexpr (P == 4) {
+        asm volatile(MCS_R4(0, 1, 2, 3) "s_waitcnt lgkmcnt(0)" : MCS_O4(nf, 0) : [b] "v"(base) : "memory");
+    } else if constexpr (P == 8) {
+        asm volatile(MCS_R4(0, 1, 2, 3) MCS_R4(4, 5, 6, 7) "s_waitcnt lgkmcnt(0)"
+                     : MCS_O4(nf, 0), MCS_O4(nf, 4) : [b] "v"(base) : "memory");
+    } else {
+        static_assert(P % 16 == 0, "slot rows");
 #pragma unroll
-        for (int c = 0; c < NPL / 2; ++c) {
-            nvr[2 * c] = q[c].x;
-            nvr[2 * c + 1] = q[c].y;
+        for (int h = 0; h < P; h += 16) {
+            uint64_t* q = nf + h;
+            asm volatile(MCS_R4(0, 1, 2, 3) MCS_R4(4, 5, 6, 7) MCS_R4(8, 9, 10, 11) MCS_R4(12, 13, 14, 15)
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5]),
+                           "=&v"(q[6]), "=&v"(q[7]), "=&v"(q[8]), "=&v"(q[9]), "=&v"(q[10]), "=&v"(q[11]),
+                           "=&v"(q[12]), "=&v"(q[13]), "=&v"(q[14]), "=&v"(q[15])
+                         : [b] "v"(base + (uint32_t)h * 512u)
+                         : "memory");
         }
     }
 }
-#undef MCS_RD2
+#undef MCS_R1
+#undef MCS_R4
+#undef MCS_O4
 
 // HOR: the online variant.  The cluster resumes from the OnlineState, node image
 // and slot image of the previous horizon (or its spec when the state is not valid), runs every
@@ -228,8 +254,8 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
 
     // Node free vectors in registers (nvr[c]: node lane * NPL + c), the state every decision
     // reads: a commit updates them in place, so a decision never waits on LDS.  The LDS copy
-    // nodes[] is written only for a release, whose hand-backs are LDS atomics, and read back
-    // inside it.
+    // nodes[] follows every change (ds_sub_u64 at a commit, ds_add_u64 at a release hand-back)
+    // and is read back only after a release.
     uint64_t nvr[NPL];
 #pragma unroll
     for (int c = 0; c < NPL; ++c) {
@@ -243,50 +269,43 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     // line) and the free-row bits; the lane's next finish is the min over its unexpired rows.
     auto release = [&]() __attribute__((always_inline)) {
         ++n_rel;
-#pragma unroll
-        for (int c = 0; c < NPL; ++c) nodes[c * kWave + lane] = nvr[c];  // publish (LDS in order)
         const uint32_t t1 = t + 1u;  // t < kEmpty here (a wrap stops the run first)
-        uint64_t nf[P], cm[P];
-        uint64_t m[P];
+        uint64_t nf[P];
+        read_finish_rows<P>(nf, pay_lds + P * kWave * 8u);
         // lane's next finish: min over unexpired rows, as min(f - (t + 1)) + (t + 1) in u32: an
         // expired row (f <= t) wraps above every unexpired and free one, and the bound ~t1 caps
         // the result at kEmpty when the lane has none left
         uint32_t lm = ~t1;
-#pragma unroll
-        for (int p = 0; p < P; ++p) {  // free rows hold kEmpty: never expired
-            nf[p] = pay_nf[p * kWave + lane];
-            cm[p] = pay_cm[p * kWave + lane];  // (read with the finish words: one wait)
-            const uint32_t f = (uint32_t)(nf[p] >> 32);
-            m[p] = lanes_ge(t, f);
-            const uint32_t d = f - t1;
-            lm = d < lm ? d : lm;
-        }
         uint32_t nexp = 0u;
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-            if (__builtin_expect(m[p] != 0ull, 0)) {
-                nexp += (uint32_t)__builtin_popcountll(m[p]);
-                // the expired lanes (exec = m[p]) give their payloads back to their nodes and
-                // free the row: ds_add_u64 on the node, finish word := kEmpty (no wait: the
-                // node reload below is ordered after them by LDS)
+        for (int p = 0; p < P; ++p) {  // free rows hold kEmpty: never expired
+            const uint32_t f = (uint32_t)(nf[p] >> 32);
+            const uint64_t m = lanes_ge(t, f);
+            const uint32_t d = f - t1;
+            lm = d < lm ? d : lm;
+            if (__builtin_expect(m != 0ull, 0)) {
+                nexp += (uint32_t)__builtin_popcountll(m);
+                // the expired lanes (exec = m) give their payloads back to their nodes and free
+                // the row: read payload, ds_add_u64 on the node, finish word := kEmpty
                 const uint32_t na = nodes_lds + (uint32_t)nf[p] * 8u;
-                uint64_t sv;
+                uint64_t sv, cm;
                 asm volatile(
                     "s_mov_b64 %[sv], exec\n\t"
                     "s_mov_b64 exec, %[m]\n\t"
+                    "ds_read_b64 %[cm], %[pa] offset:%[oc]\n\t"
+                    "s_waitcnt lgkmcnt(0)\n\t"
                     "ds_add_u64 %[na], %[cm]\n\t"
                     "ds_write_b32 %[pa], %[emp] offset:%[of]\n\t"
                     "v_or_b32 %[frm], %[bit], %[frm]\n\t"
                     "s_mov_b64 exec, %[sv]"
-                    : [sv] "=&s"(sv), [frm] "+v"(frm)
-                    : [m] "s"(m[p]), [pa] "v"(pay_lds), [na] "v"(na), [cm] "v"(cm[p]), [emp] "v"(kEmpty),
-                      [bit] "i"(1u << p), [of] "i"((P + p) * kWave * 8 + 4)
+                    : [sv] "=&s"(sv), [cm] "=&v"(cm), [frm] "+v"(frm)
+                    : [m] "s"(m), [pa] "v"(pay_lds), [na] "v"(na), [emp] "v"(kEmpty), [bit] "i"(1u << p),
+                      [oc] "i"(p * kWave * 8), [of] "i"((P + p) * kWave * 8 + 4)
                     : "memory");
             }
         }
         used -= nexp;
-        // read the node vectors back and wait here, in one statement: LLVM then has no LDS load
-        // of its own in flight, and no decision path carries a wait
+        // read the node vectors back (the hand-backs are ahead of the reads in LDS order)
         reload_nodes(nvr, nodes_lds + lane * 8u);
         lmin = lm + t1;
     };
@@ -359,14 +378,17 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
                     "s_mov_b64 exec, %[m]\n\t"
                     "v_ffbl_b32 %[ta], %[frm]\n\t"
                     "v_lshl_add_u32 %[ta], %[ta], 9, %[pl]\n\t"
-                    "ds_write2st64_b64 %[ta], %[nd], %[nf] offset1:%[off]\n\t"
+                    "ds_sub_u64 %[na], %[nd]\n\t"
+                    "ds_write_b64 %[ta], %[nd]\n\t"
+                    "ds_write_b64 %[ta], %[nf] offset:%[off]\n\t"
                     "v_add_u32 %[tf], -1, %[frm]\n\t"
                     "v_and_b32 %[frm], %[tf], %[frm]\n\t"
                     "v_min_u32 %[lmin], %[fin], %[lmin]\n\t"
                     "s_mov_b64 exec, %[sv]"
                     : [sv] "=&s"(sv), [ta] "=&v"(ta), [tf] "=&v"(tf), [frm] "+v"(frm), [lmin] "+v"(lmin)
                     : [m] "s"(1ull << __builtin_ctzll(fr)), [nd] "v"(need), [pl] "v"(pay_lds),
-                      [nf] "v"(nfw), [fin] "s"(sgpr(fin)), [off] "i"(P)
+                      [nf] "v"(nfw), [fin] "s"(sgpr(fin)), [off] "i"(P * kWave * 8),
+                      [na] "v"(nodes_lds + kx * 8u)
                     : "memory");
                 ++used;
                 peak = used > peak ? used : peak;
