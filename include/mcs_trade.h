@@ -22,9 +22,10 @@
  * (per-cluster records + node snapshots) and runs the trader rounds replicated on every rank.
  *
  * Sharding: the clusters are split in equal contiguous blocks over `world` engines (one per GPU,
- * usually one process each).  Every FIFO tick needs three all-gathers of small fixed-size records;
- * a DELAY tick needs one (phase 0 -> 1; phases 2 and 3 move no bytes), and every rank must hold
- * the same number of clusters and the same largest cluster (the block layout).
+ * usually one process each).  A tick of either policy needs one all-gather of one block per rank
+ * (per-cluster records + node snapshots; phase 0 -> 1; phases 2 and 3 move no bytes): the
+ * remaining phases run replicated over the whole system on every rank.  Every rank must hold the
+ * same number of clusters and the same largest cluster (the block layout).
  * Two transports:
  *   - RCCL (mcs_comm_unique_id on rank 0, shared out of band, then mcs_comm_init on every rank):
  *     mcs_run drives the whole lock-step loop with ncclAllGather over xGMI;
@@ -109,8 +110,9 @@ int mcs_comm_init(mcs_engine* eng, const mcs_comm_id* id);
 /* ---- caller-driven lock-step ---------------------------------------------------------------- */
 /* One tick is phases 0..3.  Phase p reads `in` (the all-gather, in rank order, of every rank's
  * `out` of phase p-1; phase 0 takes no input) and writes this rank's slice for the next
- * exchange.  Phase 3's input is the gathered phase-2 output; its `out` is empty.  Sizes per
- * phase from mcs_trade_xfer_bytes.  *done becomes 1 (identically on every rank) after the phase 3
+ * exchange.  Sizes per phase from mcs_trade_xfer_bytes: today only phase 0 writes (this rank's
+ * block) and only phase 1 reads (every rank's blocks); the other sizes are 0 and an empty output
+ * need not be gathered.  *done becomes 1 (identically on every rank) after the phase 3
  * that ends the run; keep calling phase 0..3 until then.  mcs_trade_begin resets the lock-step
  * state; mcs_trade_end fills the stats and makes the results readable. */
 int mcs_trade_begin(mcs_engine* eng);

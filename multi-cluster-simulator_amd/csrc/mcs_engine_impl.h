@@ -94,6 +94,7 @@ struct mcs_engine {
     bool dtrade_run = false;           // results of the last run come from DELAY trading
     uint32_t dt_vnodes = 0;            // virtual-node capacity per cluster (0 = auto)
     uint32_t dt_ns = 0;                // node-snapshot stride over all ranks (0 = max_n)
+    uint32_t tr_ns = 0;                // the same for FIFO lock-step trading
     // online mode (mcs_online.cpp): per-cluster state kept on the device between horizons
     bool online = false;               // a session is active
     bool segmented = false;            // job_off holds segment starts with slack (appends)

@@ -1,6 +1,7 @@
 // mcs_trade.cpp — C ABI of the lock-step trading path (include/mcs_trade.h): device state,
-// the tick loop (hipGraph replay on one GPU, RCCL all-gathers over xGMI across GPUs, or the
-// caller-driven phase API), and the result readers.  Host code; compiled by hipcc.
+// the tick loop (hipGraph replay on one GPU, one RCCL all-gather of the exchange blocks per tick
+// over xGMI across GPUs, or the caller-driven phase API), and the result readers.  Host code;
+// compiled by hipcc.
 //
 // Every decision is made by the gfx950 kernels of mcs_trade.hip; there is no CPU path.
 #include <hip/hip_runtime.h>
@@ -19,17 +20,17 @@
 namespace mcs {
 
 struct TradeDev {
-    TradeArgs a_local{};  // exchange in HBM (one engine holds the whole system)
-    TradeArgs a_xfer{};   // exchange through acc_all (RCCL or caller-driven)
+    TradeArgs a{};  // (the exchange blocks of every rank live in xb)
     unsigned long long* tn = nullptr;
     TrCluster* cl = nullptr;
     uint32_t* sfin = nullptr;
     uint32_t* snode = nullptr;
     unsigned long long* scm = nullptr;
     TrLq* lq = nullptr;
-    TrRecA* recA = nullptr;
-    uint32_t* acc_l = nullptr;
-    uint32_t* acc_all = nullptr;
+    unsigned char* xb = nullptr;
+    uint32_t* acc = nullptr;
+    uint32_t* lqp = nullptr;
+    uint32_t* fb = nullptr;
     TrRecC* recC = nullptr;
     TrTrader* tr = nullptr;
     TrCtl* ctl = nullptr;
@@ -91,9 +92,12 @@ int trade_alloc(mcs_engine* e) {
     HIPCHK(e, hipMalloc(&td->snode, (size_t)Cl * S * 4));
     HIPCHK(e, hipMalloc(&td->scm, (size_t)Cl * S * 8));
     HIPCHK(e, hipMalloc(&td->lq, (size_t)Cl * LQ * sizeof(TrLq)));
-    HIPCHK(e, hipMalloc(&td->recA, Ct * sizeof(TrRecA)));
-    HIPCHK(e, hipMalloc(&td->acc_l, Ct * 4));
-    HIPCHK(e, hipMalloc(&td->acc_all, (size_t)e->world * Ct * 4));
+    const uint32_t ns = std::max<uint32_t>(e->tr_ns ? e->tr_ns : e->max_n, 1u);
+    const uint64_t blk = (uint64_t)Cl * sizeof(TrXRec) + (uint64_t)Cl * ns * 8u;
+    HIPCHK(e, hipMalloc(&td->xb, (size_t)e->world * blk));
+    HIPCHK(e, hipMalloc(&td->acc, Ct * 4));
+    HIPCHK(e, hipMalloc(&td->lqp, Ct * 4));
+    HIPCHK(e, hipMalloc(&td->fb, Ct * 4));
     HIPCHK(e, hipMalloc(&td->recC, Ct * sizeof(TrRecC)));
     HIPCHK(e, hipMalloc(&td->tr, Ct * sizeof(TrTrader)));
     HIPCHK(e, hipMalloc(&td->ctl, sizeof(TrCtl)));
@@ -101,7 +105,7 @@ int trade_alloc(mcs_engine* e) {
     HIPCHK(e, hipMalloc(&td->trades, trade_cap * sizeof(mcs_trade_rec)));
     HIPCHK(e, hipHostMalloc(&td->h_ctl, sizeof(TrCtl), hipHostMallocDefault));
 
-    TradeArgs& a = td->a_local;
+    TradeArgs& a = td->a;
     a.Cl = Cl;
     a.Ct = Ct;
     a.base = e->rank * Cl;
@@ -132,16 +136,18 @@ int trade_alloc(mcs_engine* e) {
     a.snode = td->snode;
     a.scm = td->scm;
     a.lq = td->lq;
-    a.recA = td->recA;
-    a.acc_l = td->acc_l;
-    a.acc_all = td->acc_l;  // world 1: the local acceptances are the gathered ones
+    a.xb = td->xb;
+    a.blk = blk;
+    a.ns = ns;
+    a.rank = e->rank;
+    a.acc = td->acc;
+    a.lqp = td->lqp;
+    a.fb = td->fb;
     a.recC = td->recC;
     a.tr = td->tr;
     a.ctl = td->ctl;
     a.lent_log = td->lent;
     a.trade_log = td->trades;
-    td->a_xfer = a;
-    td->a_xfer.acc_all = td->acc_all;
     return MCS_OK;
 }
 
@@ -165,7 +171,7 @@ int run_local(mcs_engine* e) {
         HIPCHK(e, hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
         for (uint32_t t = 0; t < kGraphTicks; ++t)
             for (int p = 0; p < 4; ++p) {
-                const hipError_t st = launch_trade_phase(td->a_local, p, e->stream);
+                const hipError_t st = launch_trade_phase(td->a, p, e->stream);
                 if (st != hipSuccess) {
                     (void)hipStreamEndCapture(e->stream, &g);
                     if (g) (void)hipGraphDestroy(g);
@@ -189,26 +195,20 @@ int nccl_fail(mcs_engine* e, const char* what, ncclResult_t r) {
     return fail(e, MCS_E_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
-// N engines (one per GPU): the three record exchanges of a tick are ncclAllGather over xGMI
+// N engines (one per GPU): a tick's one exchange is the in-place ncclAllGather of the ranks'
+// blocks over xGMI between phase A and the replicated phases B-D
 int run_rccl(mcs_engine* e) {
     TradeDev* td = e->td;
-    const TradeArgs& a = td->a_xfer;
+    const TradeArgs& a = td->a;
     ncclComm_t comm = (ncclComm_t)e->comm;
-    const size_t base = (size_t)e->rank * e->C;
     for (;;) {
         for (uint32_t t = 0; t < kGraphTicks; ++t) {
             if (int s = launch_phase(e, a, 0)) return s;
-            ncclResult_t r = ncclAllGather(td->recA + base, td->recA, e->C * (sizeof(TrRecA) / 4),
-                                           ncclUint32, comm, e->stream);
-            if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(borrow requests)", r);
-            if (int s = launch_phase(e, a, 1)) return s;
-            r = ncclAllGather(td->acc_l, td->acc_all, a.Ct, ncclUint32, comm, e->stream);
-            if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(acceptances)", r);
-            if (int s = launch_phase(e, a, 2)) return s;
-            r = ncclAllGather(td->recC + base, td->recC, e->C * (sizeof(TrRecC) / 4), ncclUint32,
-                              comm, e->stream);
-            if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(state samples)", r);
-            if (int s = launch_phase(e, a, 3)) return s;
+            const ncclResult_t r = ncclAllGather(td->xb + (size_t)e->rank * a.blk, td->xb, a.blk, ncclUint8,
+                                                 comm, e->stream);
+            if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(exchange blocks)", r);
+            for (int p = 1; p < 4; ++p)
+                if (int s = launch_phase(e, a, p)) return s;
         }
         if (int s = poll_ctl(e)) return s;
         if (td->h_ctl->done) return MCS_OK;
@@ -234,7 +234,7 @@ int fill_stats(mcs_engine* e, mcs_trade_stats* ts, mcs_stats* st) {
         s.lent_pending += cl[k].lq_len;
         flags |= cl[k].flags;
     }
-    if (c.n_lent > td->a_local.lent_cap || c.n_trades > td->a_local.trade_cap) flags |= MCS_FLAG_LOG_OVERFLOW;
+    if (c.n_lent > td->a.lent_cap || c.n_trades > td->a.trade_cap) flags |= MCS_FLAG_LOG_OVERFLOW;
     s.trades = c.n_trades;
     s.trades_won = c.n_won;
     s.ticks = c.ticks;
@@ -249,7 +249,7 @@ int fill_stats(mcs_engine* e, mcs_trade_stats* ts, mcs_stats* st) {
         st->clusters = e->C;
         st->deadlocked = 0;
         st->escalations = 0;
-        st->slot_pool = td->a_local.S / 64u;
+        st->slot_pool = td->a.S / 64u;
     }
     return MCS_OK;
 }
@@ -272,9 +272,10 @@ void trade_free(mcs_engine* e) {
     dfree(td->snode);
     dfree(td->scm);
     dfree(td->lq);
-    dfree(td->recA);
-    dfree(td->acc_l);
-    dfree(td->acc_all);
+    dfree(td->xb);
+    dfree(td->acc);
+    dfree(td->lqp);
+    dfree(td->fb);
     dfree(td->recC);
     dfree(td->tr);
     dfree(td->ctl);
@@ -300,7 +301,7 @@ int trade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n) {
         s.waited = cl[k].waited;
         s.peak_running = cl[k].peak;
         s.flags = cl[k].flags;
-        s.pool = td->a_local.S / 64u;
+        s.pool = td->a.S / 64u;
         s.iterations = td->h_ctl->ticks;
         s.release_scans = 0;
         out[k] = s;
@@ -308,9 +309,30 @@ int trade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n) {
     return MCS_OK;
 }
 
+// every rank must lay its exchange block out alike: the snapshot stride is the largest cluster of
+// the whole system, and the cluster count per rank must match (one all-reduce before the run)
+int tr_agree_shape(mcs_engine* e) {
+    uint32_t* buf = nullptr;
+    HIPCHK(e, hipMalloc(&buf, 2 * sizeof(uint32_t)));
+    const uint32_t h[2] = {e->max_n, e->C};
+    uint32_t mx[2] = {0, 0};
+    HIPCHK(e, hipMemcpy(buf, h, sizeof(h), hipMemcpyHostToDevice));
+    ncclResult_t r = ncclAllReduce(buf, buf, 2, ncclUint32, ncclMax, (ncclComm_t)e->comm, e->stream);
+    hipError_t st = hipStreamSynchronize(e->stream);
+    if (r == ncclSuccess && st == hipSuccess) st = hipMemcpy(mx, buf, sizeof(mx), hipMemcpyDeviceToHost);
+    (void)hipFree(buf);
+    if (r != ncclSuccess) return nccl_fail(e, "ncclAllReduce(shape)", r);
+    if (st != hipSuccess) return hip_fail(e, "shape exchange", st);
+    if (mx[1] != e->C) return fail(e, MCS_E_INVALID, "sharded lock-step trading needs the same cluster count on every rank");
+    e->tr_ns = mx[0];
+    return MCS_OK;
+}
+
 int trade_run(mcs_engine* e, mcs_stats* stats) {
     if (e->world > 1 && !e->comm)
         return fail(e, MCS_E_STATE, "sharded lock-step run needs mcs_comm_init (or mcs_trade_phase)");
+    if (e->comm && !e->td)
+        if (int s = tr_agree_shape(e)) return s;
     e->tr_lq = e->tr_slots = 0;
     uint32_t escalations = 0;
     for (;;) {
@@ -323,7 +345,7 @@ int trade_run(mcs_engine* e, mcs_stats* stats) {
             return s;
         }
         // capacity escalation: the flags are replicated on every rank, so all ranks re-run alike
-        const uint32_t flags = e->td->h_ctl->flags, LQ = e->td->a_local.LQ, S = e->td->a_local.S;
+        const uint32_t flags = e->td->h_ctl->flags, LQ = e->td->a.LQ, S = e->td->a.S;
         bool grew = false;
         if ((flags & MCS_FLAG_LENT_OVERFLOW) && !e->cfg.lent_queue_cap && LQ < kMaxLq) {
             e->tr_lq = std::min<uint32_t>(LQ * 4u, kMaxLq);
@@ -334,10 +356,11 @@ int trade_run(mcs_engine* e, mcs_stats* stats) {
             grew = true;
         }
         if (!grew) return s;
-        const uint32_t lq = e->tr_lq, sl = e->tr_slots;
+        const uint32_t lq = e->tr_lq, sl = e->tr_slots, ns = e->tr_ns;
         trade_free(e);
         e->tr_lq = lq;
         e->tr_slots = sl;
+        e->tr_ns = ns;
         ++escalations;
     }
 }
@@ -354,6 +377,7 @@ int mcs_set_shard(mcs_engine* e, uint32_t rank, uint32_t world) {
     mcs::trade_free(e);
     mcs::dtrade_free(e);
     e->dt_ns = 0;
+    e->tr_ns = 0;
     e->rank = rank;
     e->world = world;
     return MCS_OK;
@@ -395,7 +419,7 @@ int mcs_trade_begin(mcs_engine* e) {
     if (int st = mcs::trade_alloc(e)) return st;
     mcs::TradeDev* td = e->td;
     td->w0 = std::chrono::steady_clock::now();
-    const hipError_t st = mcs::launch_trade_init(td->a_local, e->stream);
+    const hipError_t st = mcs::launch_trade_init(td->a, e->stream);
     if (st != hipSuccess) return mcs::hip_fail(e, "trade init", st);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));  // kernel_ms: the lock-step loop only
@@ -408,12 +432,17 @@ int mcs_trade_begin(mcs_engine* e) {
 int mcs_trade_xfer_bytes(mcs_engine* e, uint32_t phase, uint64_t* in_bytes, uint64_t* out_bytes) {
     if (!e || !in_bytes || !out_bytes || phase > 3) return MCS_E_INVALID;
     if (mcs::is_dtrade(e)) return mcs::dtrade_xfer_bytes(e, phase, in_bytes, out_bytes);
-    const uint64_t Cl = e->C, Ct = (uint64_t)e->C * e->world;
+    // one exchange per tick: phase 0 writes this rank's block, phase 1 takes every rank's blocks;
+    // phases 2 and 3 move no bytes.  (Block size: the engine's own largest cluster sets the
+    // snapshot stride on the caller-driven path, so every rank must hold clusters of one largest
+    // size, as the shard helpers do.)
+    const uint64_t Cl = e->C;
+    const uint64_t ns = std::max<uint32_t>(e->tr_ns ? e->tr_ns : e->max_n, 1u);
+    const uint64_t blk = Cl * sizeof(mcs::TrXRec) + Cl * ns * 8u;
     switch (phase) {
-        case 0: *in_bytes = 0; *out_bytes = Cl * sizeof(mcs::TrRecA); break;
-        case 1: *in_bytes = Ct * sizeof(mcs::TrRecA); *out_bytes = Ct * 4; break;
-        case 2: *in_bytes = (uint64_t)e->world * Ct * 4; *out_bytes = Cl * sizeof(mcs::TrRecC); break;
-        default: *in_bytes = Ct * sizeof(mcs::TrRecC); *out_bytes = 0; break;
+        case 0: *in_bytes = 0; *out_bytes = blk; break;
+        case 1: *in_bytes = (uint64_t)e->world * blk; *out_bytes = 0; break;
+        default: *in_bytes = 0; *out_bytes = 0; break;
     }
     return MCS_OK;
 }
@@ -428,25 +457,20 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
     if (int st = mcs_trade_xfer_bytes(e, phase, &ib, &ob)) return fail(e, st, "bad phase");
     if (in_bytes != ib || out_bytes != ob || (ib && !in) || (ob && !out))
         return fail(e, MCS_E_INVALID, "exchange buffer sizes do not match mcs_trade_xfer_bytes");
-    const mcs::TradeArgs& a = td->a_xfer;
-    const size_t base = (size_t)e->rank * e->C;
+    const mcs::TradeArgs& a = td->a;
     switch (phase) {
         case 0:
             if (int s = mcs::launch_phase(e, a, 0)) return s;
-            HIPCHK(e, hipMemcpyAsync(out, td->recA + base, ob, hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(e, hipMemcpyAsync(out, td->xb + (size_t)e->rank * a.blk, ob, hipMemcpyDeviceToHost, e->stream));
             break;
         case 1:
-            HIPCHK(e, hipMemcpyAsync(td->recA, in, ib, hipMemcpyHostToDevice, e->stream));
+            HIPCHK(e, hipMemcpyAsync(td->xb, in, ib, hipMemcpyHostToDevice, e->stream));
             if (int s = mcs::launch_phase(e, a, 1)) return s;
-            HIPCHK(e, hipMemcpyAsync(out, td->acc_l, ob, hipMemcpyDeviceToHost, e->stream));
             break;
         case 2:
-            HIPCHK(e, hipMemcpyAsync(td->acc_all, in, ib, hipMemcpyHostToDevice, e->stream));
             if (int s = mcs::launch_phase(e, a, 2)) return s;
-            HIPCHK(e, hipMemcpyAsync(out, td->recC + base, ob, hipMemcpyDeviceToHost, e->stream));
             break;
         default:
-            HIPCHK(e, hipMemcpyAsync(td->recC, in, ib, hipMemcpyHostToDevice, e->stream));
             if (int s = mcs::launch_phase(e, a, 3)) return s;
             HIPCHK(e, hipMemcpyAsync(td->h_ctl, td->ctl, sizeof(mcs::TrCtl), hipMemcpyDeviceToHost,
                                      e->stream));
@@ -509,7 +533,7 @@ int mcs_read_lent(mcs_engine* e, mcs_lent_rec* out, uint64_t cap, uint64_t* n) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipMemcpy(td->h_ctl, td->ctl, sizeof(mcs::TrCtl), hipMemcpyDeviceToHost));
     const uint64_t total = td->h_ctl->n_lent;
-    const uint64_t have = std::min<uint64_t>(total, td->a_local.lent_cap);
+    const uint64_t have = std::min<uint64_t>(total, td->a.lent_cap);
     std::vector<mcs_lent_rec> v(have);
     if (have) HIPCHK(e, hipMemcpy(v.data(), td->lent, have * sizeof(mcs_lent_rec), hipMemcpyDeviceToHost));
     std::sort(v.begin(), v.end(), [](const mcs_lent_rec& x, const mcs_lent_rec& y) {
@@ -533,7 +557,7 @@ int mcs_read_trades(mcs_engine* e, mcs_trade_rec* out, uint64_t cap, uint64_t* n
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipMemcpy(td->h_ctl, td->ctl, sizeof(mcs::TrCtl), hipMemcpyDeviceToHost));
     const uint64_t total = td->h_ctl->n_trades;
-    const uint64_t k = std::min<uint64_t>(std::min<uint64_t>(total, td->a_local.trade_cap), cap);
+    const uint64_t k = std::min<uint64_t>(std::min<uint64_t>(total, td->a.trade_cap), cap);
     if (k) HIPCHK(e, hipMemcpy(out, td->trades, k * sizeof(mcs_trade_rec), hipMemcpyDeviceToHost));
     *n = total;
     return MCS_OK;

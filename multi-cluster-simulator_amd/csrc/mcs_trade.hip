@@ -1,18 +1,21 @@
 // mcs_trade.hip — gfx950 kernels of the lock-step trading path (mcs_trade.h).
 //
 // One tick of the lock-step semantics is four launches on the engine stream, each a kernel
-// boundary (= grid-wide barrier) and, on N GPUs, an RCCL all-gather of fixed-size records between
-// them:
-//   A tr_step_kernel    one wave per cluster: releases, arrivals, the Fifo decisions of the tick
-//                       (scheduler.go:216-296) and the tick's borrow request (server.go:160-248)
-//   B tr_lend_kernel    one wave per cluster as lender: Lend (strict '>', scheduler.go:194-202)
-//                       against every request of the tick, in borrower order; LentQueue appends
-//   C tr_post_kernel    one wave per cluster as borrower: BorrowedQueue move when some lender
-//                       accepted (scheduler.go:237-242); float32 utilization sample
-//                       (cluster.go:46-63) on trader ticks; clock hints
-//   D tr_trader_kernel  one wave for the whole system, replicated on every rank: trader rounds
-//                       in cluster order (trader.go:280-325, 193-278; server.go:31-85) with the
-//                       responders evaluated across lanes, then the next tick (fast-forward)
+// boundary (= grid-wide barrier), with ONE exchange: on N GPUs an RCCL all-gather of the ranks'
+// blocks (post-A records + node snapshots) between A and B; B, C and D then run replicated on
+// every rank over the whole system, so they need nothing more from the other ranks:
+//   A tr_step_kernel    one wave per local cluster: releases, arrivals, the Fifo decisions of the
+//                       tick (scheduler.go:216-296), the tick's borrow request (server.go:160-248),
+//                       the float32 utilization sample (cluster.go:46-63) on trader ticks; then
+//                       the cluster's exchange record and node snapshot
+//   B tr_lend_kernel    one wave per cluster of the system as lender: Lend (strict '>',
+//                       scheduler.go:194-202) on its snapshot against every request of the tick,
+//                       in borrower order; the owner rank appends to its LentQueue
+//   C tr_post_kernel    one wave per cluster of the system as borrower: BorrowedQueue move when
+//                       some lender accepted (scheduler.go:237-242, owner rank); clock hints
+//   D tr_trader_kernel  one wave for the whole system: trader rounds in cluster order
+//                       (trader.go:280-325, 193-278; server.go:31-85) with the responders
+//                       evaluated across lanes, then the next tick (fast-forward)
 // Work per tick is a handful of decisions per cluster: the path is launch/latency-bound, so the
 // engine replays the four launches from a captured hipGraph.  Within a kernel the per-cluster
 // state a wave both writes and re-reads (node free vectors, slot finish times, trader locks) is
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(64) void tr_init_kernel(TradeArgs a) {
             TrTrader t{};
             t.next_id = 1u;  // s.id = rand.Uint32() (pkg/trader/server.go:26), seeded: 1
             a.tr[g] = t;
-            a.acc_l[g] = 0u;
+            a.acc[g] = 0u;
         }
         if (lane == 0) {
             TrCtl z{};
@@ -240,31 +243,83 @@ __global__ __launch_bounds__(64) void tr_step_kernel(TradeArgs a) {
     }
 
     __syncthreads();
-    for (uint32_t i = lane; i < N; i += kWave) a.tn[n0 + i] = nodes[i];
+    // GetResourceUtilization (cluster.go:46-63) when a trader reads it at this tick: the state
+    // stream samples every sample_period_s (trader_server.go:24-47) and trader rounds fall on
+    // multiples of the period, so the sample a round reads is the one taken at its own tick
+    // (phases B-C do not change node counters)
+    if (a.trader && T % a.sample_period == 0u) {
+        bool due = false;
+        for (uint32_t q = lane; q < a.Ct; q += kWave) due = due || a.tr[q].next_due <= T;
+        if (__ballot(due)) {
+            __shared__ float dcs[kTrMaxNodes], dms[kTrMaxNodes];
+            for (uint32_t i = lane; i < N; i += kWave) {
+                const unsigned long long v = nodes[i];
+                const uint2 cp = a.cap[n0 + i];
+                dcs[i] = __fsub_rn((float)cp.x, (float)(uint32_t)v);
+                dms[i] = __fsub_rn((float)cp.y, (float)(uint32_t)(v >> 32));
+            }
+            __syncthreads();
+            if (lane == 0) {
+                float sc = 0.0f, sm = 0.0f;
+                for (uint32_t i = 0; i < N; ++i) {  // node order, float32 (Go)
+                    sc = __fadd_rn(sc, dcs[i]);
+                    sm = __fadd_rn(sm, dms[i]);
+                }
+                st.cu = __fdiv_rn(sc, (float)st.total_c);
+                st.mu = __fdiv_rn(sm, (float)st.total_m);
+            }
+            st.cu = __shfl(st.cu, 0);
+            st.mu = __shfl(st.mu, 0);
+        }
+    }
+    unsigned long long* snap = tr_snap(a, g);
+    for (uint32_t i = lane; i < N; i += kWave) {
+        a.tn[n0 + i] = nodes[i];
+        snap[i] = nodes[i];
+    }
     for (uint32_t s = lane; s < S; s += kWave) a.sfin[sb + s] = sfin[s];
     if (lane == 0) {
         a.cl[c] = st;
-        a.recA[g] = req;
+        TrXRec x;
+        x.req = req;
+        x.n = N;
+        x.has_w = st.has_w;
+        x.lq_len = st.lq_len;
+        x.rq_busy = st.rq_head < st.next_arr ? 1u : 0u;
+        x.decided = st.decided;
+        x.J = J;
+        x.next_arr_t = st.next_arr < J ? jobs[st.next_arr].x : kEmpty;
+        x.flags = st.flags;
+        x.cu = st.cu;
+        x.mu = st.mu;
+        x.total_c = st.total_c;
+        x.total_m = st.total_m;
+        *tr_xrec(a, g) = x;
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-// Phase B: the cluster as lender, requests in borrower order ("/borrow", server.go:80-113).
+// Phase B: cluster L of the system as lender, requests in borrower order ("/borrow",
+// server.go:80-113), on L's post-A snapshot.  Every rank runs it for every lender, so the
+// acceptances (acc) and LentQueue lengths (lqp) are replicated; only L's owner appends.
 __global__ __launch_bounds__(64) void tr_lend_kernel(TradeArgs a) {
     if (a.ctl->done) return;
-    const uint32_t c = blockIdx.x, lane = lane_id(), g = a.base + c;
-    const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
-    const unsigned long long* __restrict__ tn = a.tn + n0;
-    uint32_t lq_len = a.cl[c].lq_len, lq_head = a.cl[c].lq_head, flags = a.cl[c].flags;
+    const uint32_t L = blockIdx.x, lane = lane_id();
+    const bool own = L / a.Cl == a.rank;
+    const uint32_t c = L - a.rank * a.Cl;  // (own only)
+    const TrXRec xl = *tr_xrec(a, L);
+    const uint32_t N = xl.n;
+    const unsigned long long* __restrict__ tn = tr_snap(a, L);
+    uint32_t lq_len = xl.lq_len, lq_head = own ? a.cl[c].lq_head : 0u, fb = 0;
     const uint32_t LQ = a.LQ;
     for (uint32_t b0 = 0; b0 < a.Ct; b0 += kWave) {
         const uint32_t bl = b0 + lane;
-        const bool has = bl < a.Ct && bl != g && a.recA[bl].job != kEmpty;  // self skipped (:176)
+        const bool has = bl < a.Ct && bl != L && tr_xrec(a, bl)->req.job != kEmpty;  // self skipped (:176)
         unsigned long long pend = __ballot(has);
         while (pend) {
             const uint32_t b = b0 + (uint32_t)__builtin_ctzll(pend);
             pend &= pend - 1ull;
-            const TrRecA r = a.recA[b];
+            const TrRecA r = tr_xrec(a, b)->req;
             bool ok = false;
             for (uint32_t i0 = 0; i0 < N; i0 += kWave) {
                 const uint32_t i = i0 + lane;
@@ -276,97 +331,75 @@ __global__ __launch_bounds__(64) void tr_lend_kernel(TradeArgs a) {
             }
             if (!__ballot(ok)) continue;  // "can't lend" (scheduler.go:201)
             if (lq_len >= LQ) {
-                flags |= MCS_FLAG_LENT_OVERFLOW;
+                fb |= MCS_FLAG_LENT_OVERFLOW;
                 continue;
             }
             if (lane == 0) {
-                uint32_t at = lq_head + lq_len;
-                at = at >= LQ ? at - LQ : at;
-                TrLq e{};
-                e.borrower = b;
-                e.job = r.job;
-                e.c = r.c;
-                e.m = r.m;
-                e.dur = r.dur;
-                a.lq[(size_t)c * LQ + at] = e;
-                a.acc_l[b] = 1u;
+                if (own) {
+                    uint32_t at = lq_head + lq_len;
+                    at = at >= LQ ? at - LQ : at;
+                    TrLq e{};
+                    e.borrower = b;
+                    e.job = r.job;
+                    e.c = r.c;
+                    e.m = r.m;
+                    e.dur = r.dur;
+                    a.lq[(size_t)c * LQ + at] = e;
+                }
+                a.acc[b] = 1u;  // (every accepting lender writes the same value)
             }
             ++lq_len;
         }
     }
     if (lane == 0) {
-        a.cl[c].lq_len = lq_len;
-        a.cl[c].flags = flags;
+        a.lqp[L] = lq_len;
+        a.fb[L] = fb;
+        if (own) {
+            a.cl[c].lq_len = lq_len;
+            a.cl[c].flags |= fb;
+        }
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-// Phase C: the cluster as borrower, utilization sample, clock hints.
+// Phase C: cluster g of the system as borrower (the owner rank moves the job) and its clock
+// hints for the trader phase, replicated.
 __global__ __launch_bounds__(64) void tr_post_kernel(TradeArgs a) {
-    __shared__ float dc[kTrMaxNodes], dm[kTrMaxNodes];
     if (a.ctl->done) return;
     const uint32_t T = a.ctl->T;
-    const uint32_t c = blockIdx.x, lane = lane_id(), g = a.base + c;
-    const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
-    const uint64_t j0 = a.job_off[c];
-    const uint32_t J = (uint32_t)(a.job_off[c + 1] - j0);
-    TrCluster st = a.cl[c];
-
-    const TrRecA r = a.recA[g];
-    if (r.job != kEmpty) {
-        uint32_t acc = 0;
-        for (uint32_t w = 0; w < a.world; ++w) acc |= a.acc_all[(size_t)w * a.Ct + g];
-        if (acc) {  // BorrowedQueue append, WaitQueue pop (scheduler.go:237-242)
-            if (lane == 0) {
-                a.out_node[j0 + r.job] = MCS_NODE_BORROWED;
-                a.out_start[j0 + r.job] = T;
-                a.out_finish[j0 + r.job] = MCS_TIME_NONE;
-            }
+    const uint32_t g = blockIdx.x, lane = lane_id();
+    if (lane != 0) return;
+    const TrXRec x = *tr_xrec(a, g);
+    const bool own = g / a.Cl == a.rank;
+    uint32_t has_w = x.has_w, decided = x.decided;
+    if (x.req.job != kEmpty && a.acc[g]) {  // BorrowedQueue append, WaitQueue pop (scheduler.go:237-242)
+        has_w = 0u;
+        ++decided;
+        if (own) {
+            const uint32_t c = g - a.rank * a.Cl;
+            const uint64_t j0 = a.job_off[c];
+            a.out_node[j0 + x.req.job] = MCS_NODE_BORROWED;
+            a.out_start[j0 + x.req.job] = T;
+            a.out_finish[j0 + x.req.job] = MCS_TIME_NONE;
+            TrCluster st = a.cl[c];
             st.has_w = 0u;
             ++st.decided;
             ++st.borrowed;
+            a.cl[c] = st;
         }
     }
-    // GetResourceUtilization (cluster.go:46-63) when a trader reads it at this tick: the state
-    // stream samples every sample_period_s (trader_server.go:24-47) and trader rounds fall on
-    // multiples of the period, so the sample a round reads is the one taken at its own tick
-    if (a.trader && T % a.sample_period == 0u) {
-        bool due = false;
-        for (uint32_t q = lane; q < a.Ct; q += kWave) due = due || a.tr[q].next_due <= T;
-        if (__ballot(due)) {
-            for (uint32_t i = lane; i < N; i += kWave) {
-                const unsigned long long v = a.tn[n0 + i];
-                const uint2 cp = a.cap[n0 + i];
-                dc[i] = __fsub_rn((float)cp.x, (float)(uint32_t)v);
-                dm[i] = __fsub_rn((float)cp.y, (float)(uint32_t)(v >> 32));
-            }
-            __syncthreads();
-            if (lane == 0) {
-                float sc = 0.0f, sm = 0.0f;
-                for (uint32_t i = 0; i < N; ++i) {  // node order, float32 (Go)
-                    sc = __fadd_rn(sc, dc[i]);
-                    sm = __fadd_rn(sm, dm[i]);
-                }
-                st.cu = __fdiv_rn(sc, (float)st.total_c);
-                st.mu = __fdiv_rn(sm, (float)st.total_m);
-            }
-            st.cu = __shfl(st.cu, 0);
-            st.mu = __shfl(st.mu, 0);
-        }
-    }
-    if (lane == 0) {
-        TrRecC o;
-        o.cu = st.cu;
-        o.mu = st.mu;
-        o.total_c = st.total_c;
-        o.total_m = st.total_m;
-        o.busy = (st.has_w || st.lq_len > 0u || st.rq_head < st.next_arr) ? 1u : 0u;
-        o.next_arr_t = st.next_arr < J ? a.jobs[j0 + st.next_arr].x : kEmpty;
-        o.done = (st.decided == J && st.lq_len == 0u) ? 1u : 0u;
-        o.flags = st.flags;
-        a.recC[g] = o;
-        a.cl[c] = st;
-    }
+    a.acc[g] = 0u;  // (only this wave reads it; cleared for the next tick)
+    const uint32_t lq = a.lqp[g];
+    TrRecC o;
+    o.cu = x.cu;
+    o.mu = x.mu;
+    o.total_c = x.total_c;
+    o.total_m = x.total_m;
+    o.busy = (has_w || lq > 0u || x.rq_busy) ? 1u : 0u;
+    o.next_arr_t = x.next_arr_t;
+    o.done = (decided == x.J && lq == 0u) ? 1u : 0u;
+    o.flags = x.flags | a.fb[g];
+    a.recC[g] = o;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -463,7 +496,6 @@ __global__ __launch_bounds__(64) void tr_trader_kernel(TradeArgs a) {
         nxt = rc.next_arr_t < nxt ? rc.next_arr_t : nxt;
         if (a.trader) nxt = trs[q].next_due < nxt ? trs[q].next_due : nxt;
         fl |= rc.flags;
-        a.acc_l[q] = 0u;
     }
     const bool done_all = !__ballot(!all_done);
     const bool busy_any = __ballot(busy) != 0ull;
@@ -507,10 +539,10 @@ hipError_t launch_trade_phase(const TradeArgs& a, int phase, hipStream_t s) {
             hipLaunchKernelGGL(tr_step_kernel, dim3(a.Cl), dim3(kWave), 0, s, a);
             break;
         case 1:
-            hipLaunchKernelGGL(tr_lend_kernel, dim3(a.Cl), dim3(kWave), 0, s, a);
+            hipLaunchKernelGGL(tr_lend_kernel, dim3(a.Ct), dim3(kWave), 0, s, a);
             break;
         case 2:
-            hipLaunchKernelGGL(tr_post_kernel, dim3(a.Cl), dim3(kWave), 0, s, a);
+            hipLaunchKernelGGL(tr_post_kernel, dim3(a.Ct), dim3(kWave), 0, s, a);
             break;
         case 3:
             hipLaunchKernelGGL(tr_trader_kernel, dim3(1), dim3(kWave), 0, s, a);

@@ -5,14 +5,17 @@
 //   cl      TrCluster: queue cursors, counters, last utilization sample
 //   sfin    u32 [S] running-slot finish times (kEmpty = free); snode u32 [S]; scm u64 [S]
 //   lq      TrLq [LQ] LentQueue ring
-// Exchange records, indexed by GLOBAL cluster (C_t = world * C_l), all-gathered every tick:
-//   recA    TrRecA   borrow request of the tick (phase A -> B)
-//   acc_l   u32 [C_t] "some lender of this rank accepted borrower b" (phase B -> C);
-//   acc_all u32 [world][C_t] its gather
+// Exchange blocks, one per rank (world * blk bytes), the tick's only exchange (all-gathered once):
+//   rank r's block holds TrXRec[C_l] (the post-A record of its clusters: borrow request, queue
+//   state, utilization sample) followed by the node snapshots u64 [C_l][ns] (post-A free vectors,
+//   which every rank's lender scan reads)
+// Replicated per global cluster (C_t = world * C_l); every rank computes them alike from the
+// gathered blocks:
+//   acc     u32 [C_t] "some lender accepted borrower b this tick" (phase B -> C)
+//   lqp     u32 [C_t] LentQueue length after phase B; fb u32 [C_t] flags raised in phase B
 //   recC    TrRecC   utilization sample + clock hints (phase C -> D)
-//   tr      TrTrader [C_t] trader/lock state, REPLICATED: every rank runs the identical trader
-//           rounds on identical gathered inputs
-//   ctl     TrCtl    the lock-step clock and log counters (replicated)
+//   tr      TrTrader [C_t] trader/lock state: every rank runs the identical trader rounds
+//   ctl     TrCtl    the lock-step clock and log counters
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -51,6 +54,16 @@ struct TrCluster {
 struct TrRecA {  // phase A -> B: the tick's borrow request (job == kEmpty: none)
     uint32_t job, c, m, dur;
 };
+
+struct TrXRec {  // a cluster's post-A exchange record (64 B)
+    TrRecA req;           // the tick's borrow request (req.job == kEmpty: none)
+    uint32_t n;           // nodes (of the snapshot)
+    uint32_t has_w, lq_len, rq_busy;  // wait head, LentQueue length, ready jobs queued
+    uint32_t decided, J, next_arr_t, flags;
+    float cu, mu;         // latest utilization sample (taken in phase A on sample ticks)
+    uint32_t total_c, total_m;
+};
+static_assert(sizeof(TrXRec) == 64, "exchange record");
 
 struct TrRecC {  // phase C -> D
     float cu, mu;
@@ -94,15 +107,29 @@ struct TradeArgs {
     uint32_t* snode;
     unsigned long long* scm;
     TrLq* lq;
-    TrRecA* recA;
-    uint32_t* acc_l;
-    const uint32_t* acc_all;
+    unsigned char* xb;       // world exchange blocks
+    unsigned long long blk;  // bytes of one rank's block
+    uint32_t ns, rank;       // snapshot stride (nodes), this rank
+    uint32_t* acc;
+    uint32_t* lqp;
+    uint32_t* fb;
     TrRecC* recC;
     TrTrader* tr;
     TrCtl* ctl;
     mcs_lent_rec* lent_log;
     mcs_trade_rec* trade_log;
 };
+
+// the exchange record and node snapshot of global cluster g
+__device__ __forceinline__ TrXRec* tr_xrec(const TradeArgs& a, uint32_t g) {
+    const uint32_t r = g / a.Cl, c = g - r * a.Cl;
+    return reinterpret_cast<TrXRec*>(a.xb + (size_t)r * a.blk) + c;
+}
+__device__ __forceinline__ unsigned long long* tr_snap(const TradeArgs& a, uint32_t g) {
+    const uint32_t r = g / a.Cl, c = g - r * a.Cl;
+    return reinterpret_cast<unsigned long long*>(a.xb + (size_t)r * a.blk + (size_t)a.Cl * sizeof(TrXRec)) +
+           (size_t)c * a.ns;
+}
 
 hipError_t launch_trade_init(const TradeArgs& a, hipStream_t s);
 hipError_t launch_trade_phase(const TradeArgs& a, int phase, hipStream_t s);

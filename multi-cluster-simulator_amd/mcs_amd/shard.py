@@ -50,8 +50,8 @@ def run_lockstep(engine, allgather):
     `allgather(buf: np.ndarray[uint8]) -> np.ndarray[uint8]` must return the concatenation, in
     rank order, of every rank's `buf` (all ranks call it the same number of times).  Every tick
     is phases 0..3 with an all-gather between consecutive phases; phase 3 reports `done`
-    identically on every rank.  A phase whose output is empty on every rank (the DELAY system moves
-    bytes only from phase 0 to phase 1) is not gathered.  Returns the engine's RunStats."""
+    identically on every rank.  A phase whose output is empty on every rank is not gathered (both
+    trading systems move bytes only from phase 0 to phase 1).  Returns the engine's RunStats."""
     def xfer(out):
         return allgather(out) if out.size else out
 

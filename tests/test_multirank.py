@@ -122,8 +122,9 @@ def test_rank_seed_and_shard_range():
 
 
 def test_run_lockstep_skips_empty_exchanges():
-    """The caller-driven lock-step driver gathers only non-empty phase outputs (a DELAY trading
-    tick moves bytes from phase 0 to phase 1 only; FIFO trading moves them at every phase)."""
+    """The caller-driven lock-step driver gathers only non-empty phase outputs (a trading tick
+    moves bytes from phase 0 to phase 1 only; the driver also copes with an engine whose every
+    phase moves bytes)."""
     from mcs_amd.shard import run_lockstep
 
     class FakeEngine:
