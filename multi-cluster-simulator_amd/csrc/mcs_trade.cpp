@@ -31,7 +31,6 @@ struct TradeDev {
     uint32_t* acc = nullptr;
     uint32_t* lqp = nullptr;
     uint32_t* fb = nullptr;
-    TrRecC* recC = nullptr;
     TrTrader* tr = nullptr;
     TrCtl* ctl = nullptr;
     mcs_lent_rec* lent = nullptr;
@@ -98,7 +97,6 @@ int trade_alloc(mcs_engine* e) {
     HIPCHK(e, hipMalloc(&td->acc, Ct * 4));
     HIPCHK(e, hipMalloc(&td->lqp, Ct * 4));
     HIPCHK(e, hipMalloc(&td->fb, Ct * 4));
-    HIPCHK(e, hipMalloc(&td->recC, Ct * sizeof(TrRecC)));
     HIPCHK(e, hipMalloc(&td->tr, Ct * sizeof(TrTrader)));
     HIPCHK(e, hipMalloc(&td->ctl, sizeof(TrCtl)));
     HIPCHK(e, hipMalloc(&td->lent, lent_cap * sizeof(mcs_lent_rec)));
@@ -143,7 +141,6 @@ int trade_alloc(mcs_engine* e) {
     a.acc = td->acc;
     a.lqp = td->lqp;
     a.fb = td->fb;
-    a.recC = td->recC;
     a.tr = td->tr;
     a.ctl = td->ctl;
     a.lent_log = td->lent;
@@ -276,7 +273,6 @@ void trade_free(mcs_engine* e) {
     dfree(td->acc);
     dfree(td->lqp);
     dfree(td->fb);
-    dfree(td->recC);
     dfree(td->tr);
     dfree(td->ctl);
     dfree(td->lent);

@@ -1,6 +1,6 @@
 // mcs_trade.hip — gfx950 kernels of the lock-step trading path (mcs_trade.h).
 //
-// One tick of the lock-step semantics is four launches on the engine stream, each a kernel
+// One tick of the lock-step semantics is three launches on the engine stream, each a kernel
 // boundary (= grid-wide barrier), with ONE exchange: on N GPUs an RCCL all-gather of the ranks'
 // blocks (post-A records + node snapshots) between A and B; B, C and D then run replicated on
 // every rank over the whole system, so they need nothing more from the other ranks:
@@ -11,8 +11,8 @@
 //   B tr_lend_kernel    one wave per cluster of the system as lender: Lend (strict '>',
 //                       scheduler.go:194-202) on its snapshot against every request of the tick,
 //                       in borrower order; the owner rank appends to its LentQueue
-//   C tr_post_kernel    one wave per cluster of the system as borrower: BorrowedQueue move when
-//                       some lender accepted (scheduler.go:237-242, owner rank); clock hints
+//   C (in the trader kernel) one lane per cluster of the system as borrower: BorrowedQueue move
+//                       when some lender accepted (scheduler.go:237-242, owner rank); clock hints
 //   D tr_trader_kernel  one wave for the whole system: trader rounds in cluster order
 //                       (trader.go:280-325, 193-278; server.go:31-85) with the responders
 //                       evaluated across lanes, then the next tick (fast-forward)
@@ -363,12 +363,8 @@ __global__ __launch_bounds__(64) void tr_lend_kernel(TradeArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // Phase C: cluster g of the system as borrower (the owner rank moves the job) and its clock
-// hints for the trader phase, replicated.
-__global__ __launch_bounds__(64) void tr_post_kernel(TradeArgs a) {
-    if (a.ctl->done) return;
-    const uint32_t T = a.ctl->T;
-    const uint32_t g = blockIdx.x, lane = lane_id();
-    if (lane != 0) return;
+// hints for the trader phase; run by one lane of the trader wave per cluster (replicated).
+__device__ __forceinline__ TrRecC post_cluster(const TradeArgs& a, uint32_t g, uint32_t T) {
     const TrXRec x = *tr_xrec(a, g);
     const bool own = g / a.Cl == a.rank;
     uint32_t has_w = x.has_w, decided = x.decided;
@@ -388,7 +384,7 @@ __global__ __launch_bounds__(64) void tr_post_kernel(TradeArgs a) {
             a.cl[c] = st;
         }
     }
-    a.acc[g] = 0u;  // (only this wave reads it; cleared for the next tick)
+    a.acc[g] = 0u;  // (only this lane reads it; cleared for the next tick)
     const uint32_t lq = a.lqp[g];
     TrRecC o;
     o.cu = x.cu;
@@ -399,7 +395,7 @@ __global__ __launch_bounds__(64) void tr_post_kernel(TradeArgs a) {
     o.next_arr_t = x.next_arr_t;
     o.done = (decided == x.J && lq == 0u) ? 1u : 0u;
     o.flags = x.flags | a.fb[g];
-    a.recC[g] = o;
+    return o;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -410,14 +406,19 @@ __device__ __forceinline__ bool approve_zero_contract(uint32_t tc, uint32_t tm, 
     return approve_trade_dev(tc, tm, cu, mu, 0u, 0u, 0u);
 }
 
-// Phase D: trader rounds (replicated) and the next tick.
+// Phases C and D: every cluster's borrower step and sample record (one lane each), then the
+// trader rounds (replicated) and the next tick.
 __global__ __launch_bounds__(64) void tr_trader_kernel(TradeArgs a) {
     __shared__ TrTrader trs[kTrMaxClusters];
+    __shared__ TrRecC rcs[kTrMaxClusters];
     if (a.ctl->done) return;
     const uint32_t T = a.ctl->T;
     const uint32_t lane = lane_id();
     const uint32_t Ct = a.Ct;
-    for (uint32_t q = lane; q < Ct; q += kWave) trs[q] = a.tr[q];
+    for (uint32_t q = lane; q < Ct; q += kWave) {
+        trs[q] = a.tr[q];
+        rcs[q] = post_cluster(a, q, T);
+    }
     __syncthreads();
     unsigned long long n_trades = a.ctl->n_trades, n_won = a.ctl->n_won;
     uint32_t lflags = 0;
@@ -429,7 +430,7 @@ __global__ __launch_bounds__(64) void tr_trader_kernel(TradeArgs a) {
             while (due) {  // RequestPolicyMonitor of requester q (trader.go:282-324), index order
                 const uint32_t q = q0 + (uint32_t)__builtin_ctzll(due);
                 due &= due - 1ull;
-                const TrRecC rq = a.recC[q];
+                const TrRecC rq = rcs[q];
                 // policies [WaitTime, Utilization] (trader.go:55-62): WaitTime never breaks under
                 // FIFO (its average is only fed by /delay); Utilization (trader.go:127-130)
                 const bool broken = rq.cu > 0.8f || rq.mu > 0.8f;
@@ -447,7 +448,7 @@ __global__ __launch_bounds__(64) void tr_trader_kernel(TradeArgs a) {
                         TrTrader t = trs[r];
                         if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
                         if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
-                            const TrRecC rr = a.recC[r];
+                            const TrRecC rr = rcs[r];
                             app = approve_zero_contract(rr.total_c, rr.total_m, rr.cu, rr.mu);
                             t.lock_id = t.next_id++;  // set even when not approving (:44-46)
                             t.lock_until = T + a.lock_s;
@@ -490,7 +491,7 @@ __global__ __launch_bounds__(64) void tr_trader_kernel(TradeArgs a) {
     bool all_done = true, busy = false;
     uint32_t nxt = kEmpty, fl = 0;
     for (uint32_t q = lane; q < Ct; q += kWave) {
-        const TrRecC rc = a.recC[q];
+        const TrRecC rc = rcs[q];
         all_done = all_done && rc.done;
         busy = busy || rc.busy;
         nxt = rc.next_arr_t < nxt ? rc.next_arr_t : nxt;
@@ -541,9 +542,8 @@ hipError_t launch_trade_phase(const TradeArgs& a, int phase, hipStream_t s) {
         case 1:
             hipLaunchKernelGGL(tr_lend_kernel, dim3(a.Ct), dim3(kWave), 0, s, a);
             break;
-        case 2:
-            hipLaunchKernelGGL(tr_post_kernel, dim3(a.Ct), dim3(kWave), 0, s, a);
-            break;
+        case 2:  // (phase C runs inside the trader kernel)
+            return hipSuccess;
         case 3:
             hipLaunchKernelGGL(tr_trader_kernel, dim3(1), dim3(kWave), 0, s, a);
             break;

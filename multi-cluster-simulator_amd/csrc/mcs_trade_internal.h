@@ -13,7 +13,7 @@
 // gathered blocks:
 //   acc     u32 [C_t] "some lender accepted borrower b this tick" (phase B -> C)
 //   lqp     u32 [C_t] LentQueue length after phase B; fb u32 [C_t] flags raised in phase B
-//   recC    TrRecC   utilization sample + clock hints (phase C -> D)
+//   (TrRecC, the sample + clock hints of phase C, lives in the trader kernel's LDS)
 //   tr      TrTrader [C_t] trader/lock state: every rank runs the identical trader rounds
 //   ctl     TrCtl    the lock-step clock and log counters
 #pragma once
@@ -113,7 +113,6 @@ struct TradeArgs {
     uint32_t* acc;
     uint32_t* lqp;
     uint32_t* fb;
-    TrRecC* recC;
     TrTrader* tr;
     TrCtl* ctl;
     mcs_lent_rec* lent_log;
