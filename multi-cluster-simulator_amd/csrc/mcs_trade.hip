@@ -303,28 +303,36 @@ __global__ __launch_bounds__(64) void tr_step_kernel(TradeArgs a) {
 // server.go:80-113), on L's post-A snapshot.  Every rank runs it for every lender, so the
 // acceptances (acc) and LentQueue lengths (lqp) are replicated; only L's owner appends.
 __global__ __launch_bounds__(64) void tr_lend_kernel(TradeArgs a) {
+    __shared__ unsigned long long sn[kTrMaxNodes];
     if (a.ctl->done) return;
     const uint32_t L = blockIdx.x, lane = lane_id();
     const bool own = L / a.Cl == a.rank;
     const uint32_t c = L - a.rank * a.Cl;  // (own only)
     const TrXRec xl = *tr_xrec(a, L);
     const uint32_t N = xl.n;
-    const unsigned long long* __restrict__ tn = tr_snap(a, L);
+    {  // the lender's snapshot, staged once for every request of the tick
+        const unsigned long long* __restrict__ tn = tr_snap(a, L);
+        for (uint32_t i = lane; i < N; i += kWave) sn[i] = tn[i];
+        __syncthreads();
+    }
     uint32_t lq_len = xl.lq_len, lq_head = own ? a.cl[c].lq_head : 0u, fb = 0;
     const uint32_t LQ = a.LQ;
     for (uint32_t b0 = 0; b0 < a.Ct; b0 += kWave) {
         const uint32_t bl = b0 + lane;
-        const bool has = bl < a.Ct && bl != L && tr_xrec(a, bl)->req.job != kEmpty;  // self skipped (:176)
-        unsigned long long pend = __ballot(has);
+        // this block of 64 borrowers' requests, one per lane, broadcast per pending request
+        TrRecA rl{kEmpty, 0u, 0u, 0u};
+        if (bl < a.Ct && bl != L) rl = tr_xrec(a, bl)->req;  // self skipped (:176)
+        unsigned long long pend = __ballot(rl.job != kEmpty);
         while (pend) {
-            const uint32_t b = b0 + (uint32_t)__builtin_ctzll(pend);
+            const uint32_t bi = (uint32_t)__builtin_ctzll(pend);
+            const uint32_t b = b0 + bi;
             pend &= pend - 1ull;
-            const TrRecA r = tr_xrec(a, b)->req;
+            const TrRecA r{readlane(rl.job, bi), readlane(rl.c, bi), readlane(rl.m, bi), readlane(rl.dur, bi)};
             bool ok = false;
             for (uint32_t i0 = 0; i0 < N; i0 += kWave) {
                 const uint32_t i = i0 + lane;
                 if (i < N) {
-                    const unsigned long long v = tn[i];
+                    const unsigned long long v = sn[i];
                     ok = ok || ((uint32_t)v > r.c && (uint32_t)(v >> 32) > r.m);
                 }
                 if (__ballot(ok)) break;
