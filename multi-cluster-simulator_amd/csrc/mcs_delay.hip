@@ -35,6 +35,7 @@
 #define MCS_GEN_FN __host__ __device__ static inline
 #include "mcs_gen_dev.h"
 #include "mcs_internal.h"
+#include "mcs_lds.h"
 #include "mcs_wave.h"
 
 namespace mcs {
@@ -187,14 +188,16 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     // release every running job with finish <= t (cluster.go:153-157), row by row as in
     // fifo_kernel: row p's expired test over all lanes is one compare whose lane mask drives the
     // payload hand-back of that row and its free-row bits
+    // LDS byte addresses (single-address b64 accesses: mcs_lds.h)
+    const uint32_t pay_lds = lds_addr(pay);
     auto release = [&]() __attribute__((always_inline)) {
         ++n_rel;
         uint32_t lm = kEmpty;
         uint64_t nf[P];
         bool ex[P];
+        read_finish_rows<P>(nf, pay_lds + lane * 8u + P * kWave * 8u);
 #pragma unroll
         for (int p = 0; p < P; ++p) {  // free rows hold kEmpty: never expired, min-neutral
-            nf[p] = pay_nf[p * kWave + lane];
             const uint32_t f = (uint32_t)(nf[p] >> 32);
             ex[p] = f <= t;
             const uint32_t fl = ex[p] ? kEmpty : f;
@@ -245,8 +248,10 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
             __hip_atomic_fetch_sub(&nodes[k], need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             const uint32_t ad = (uint32_t)__builtin_ctz(frm) * kWave + lane;
             frm &= frm - 1u;
-            pay_cm[ad] = need;
-            pay_nf[ad] = (uint64_t)k | ((uint64_t)fin << 32);
+            // two single-address writes (LLVM pairs them into one write2st64, 2x the LDS time)
+            const uint64_t nfw = (uint64_t)k | ((uint64_t)fin << 32);
+            asm volatile("ds_write_b64 %0, %1\n\tds_write_b64 %0, %2 offset:%3"
+                         :: "v"(pay_lds + ad * 8u), "v"(need), "v"(nfw), "i"(P * kWave * 8) : "memory");
             lmin = fin < lmin ? fin : lmin;
         }
         ++used;
