@@ -62,7 +62,11 @@ namespace mcs {
 // and slot image of the previous horizon (or its spec when the state is not valid), runs every
 // iteration at t < a.on.t_hor, and saves them again; job counts come from a.on.job_cnt.  The
 // one-shot variant (HOR = false) is the batch hot path and does none of this.
-template <int NPL, int P, bool GEN, bool HOR>
+// LAT: the low-occupancy form (a few cluster waves per CU, e.g. one system sharded over several
+// GPUs): the fitting chunk is picked by scalar bit tests and a release reads every slot payload
+// with the finish words (one wait), which shortens one decision's chain at the price of scalar
+// work and LDS time, the shared resources at 16 waves per CU.
+template <int NPL, int P, bool GEN, bool HOR, bool LAT>
 __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
     static_assert(P <= 32, "free-row mask is one u32 per lane");
     static_assert(!(HOR && GEN), "online runs stream records");
@@ -211,7 +215,18 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
         ++n_rel;
         const uint32_t t1 = t + 1u;  // t < kEmpty here (a wrap stops the run first)
         uint64_t nf[P];
-        read_finish_rows<P>(nf, pay_lds + P * kWave * 8u);
+        uint64_t cm[LAT ? P : 1];
+        if constexpr (LAT) {  // payload rows 0..P-1 and finish rows P..2P-1, one wait
+            uint64_t rows[2 * P];
+            read_finish_rows<2 * P>(rows, pay_lds);
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                cm[p] = rows[p];
+                nf[p] = rows[P + p];
+            }
+        } else {
+            read_finish_rows<P>(nf, pay_lds + P * kWave * 8u);
+        }
         // lane's next finish: min over unexpired rows, as min(f - (t + 1)) + (t + 1) in u32: an
         // expired row (f <= t) wraps above every unexpired and free one, and the bound ~t1 caps
         // the result at kEmpty when the lane has none left
@@ -226,22 +241,37 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
             if (__builtin_expect(m != 0ull, 0)) {
                 nexp += (uint32_t)__builtin_popcountll(m);
                 // the expired lanes (exec = m) give their payloads back to their nodes and free
-                // the row: read payload, ds_add_u64 on the node, finish word := kEmpty
+                // the row: (read payload,) ds_add_u64 on the node, finish word := kEmpty
                 const uint32_t na = nodes_lds + (uint32_t)nf[p] * 8u;
-                uint64_t sv, cm;
-                asm volatile(
-                    "s_mov_b64 %[sv], exec\n\t"
-                    "s_mov_b64 exec, %[m]\n\t"
-                    "ds_read_b64 %[cm], %[pa] offset:%[oc]\n\t"
-                    "s_waitcnt lgkmcnt(0)\n\t"
-                    "ds_add_u64 %[na], %[cm]\n\t"
-                    "ds_write_b32 %[pa], %[emp] offset:%[of]\n\t"
-                    "v_or_b32 %[frm], %[bit], %[frm]\n\t"
-                    "s_mov_b64 exec, %[sv]"
-                    : [sv] "=&s"(sv), [cm] "=&v"(cm), [frm] "+v"(frm)
-                    : [m] "s"(m), [pa] "v"(pay_lds), [na] "v"(na), [emp] "v"(kEmpty), [bit] "i"(1u << p),
-                      [oc] "i"(p * kWave * 8), [of] "i"((P + p) * kWave * 8 + 4)
-                    : "memory");
+                uint64_t sv;
+                if constexpr (LAT) {
+                    asm volatile(
+                        "s_mov_b64 %[sv], exec\n\t"
+                        "s_mov_b64 exec, %[m]\n\t"
+                        "ds_add_u64 %[na], %[cm]\n\t"
+                        "ds_write_b32 %[pa], %[emp] offset:%[of]\n\t"
+                        "v_or_b32 %[frm], %[bit], %[frm]\n\t"
+                        "s_mov_b64 exec, %[sv]"
+                        : [sv] "=&s"(sv), [frm] "+v"(frm)
+                        : [m] "s"(m), [pa] "v"(pay_lds), [na] "v"(na), [cm] "v"(cm[p]), [emp] "v"(kEmpty),
+                          [bit] "i"(1u << p), [of] "i"((P + p) * kWave * 8 + 4)
+                        : "memory");
+                } else {
+                    uint64_t cmr;
+                    asm volatile(
+                        "s_mov_b64 %[sv], exec\n\t"
+                        "s_mov_b64 exec, %[m]\n\t"
+                        "ds_read_b64 %[cm], %[pa] offset:%[oc]\n\t"
+                        "s_waitcnt lgkmcnt(0)\n\t"
+                        "ds_add_u64 %[na], %[cm]\n\t"
+                        "ds_write_b32 %[pa], %[emp] offset:%[of]\n\t"
+                        "v_or_b32 %[frm], %[bit], %[frm]\n\t"
+                        "s_mov_b64 exec, %[sv]"
+                        : [sv] "=&s"(sv), [cm] "=&v"(cmr), [frm] "+v"(frm)
+                        : [m] "s"(m), [pa] "v"(pay_lds), [na] "v"(na), [emp] "v"(kEmpty), [bit] "i"(1u << p),
+                          [oc] "i"(p * kWave * 8), [of] "i"((P + p) * kWave * 8 + 4)
+                        : "memory");
+                }
             }
         }
         used -= nexp;
@@ -416,16 +446,25 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
             // each lane's lowest fitting chunk, selected in VALU by the chunk masks (the scalar
             // unit is shared by the CU's waves; the vector unit is per SIMD)
             uint32_t bc = NPL - 1;
+            if constexpr (!LAT) {
 #pragma unroll
-            for (int c = NPL - 2; c >= 0; --c)  // bc = F[c] has this lane ? c : bc (mask operand)
-                asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(bc) : "v"(bc), "i"(c), "s"(F[c]));
+                for (int c = NPL - 2; c >= 0; --c)  // bc = F[c] has this lane ? c : bc (mask operand)
+                    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(bc) : "v"(bc), "i"(c), "s"(F[c]));
+            }
 #ifdef MCS_STAMPS
             asm volatile("" ::"s"(fit));
 #endif
             MCS_STAMP(t1);
             if (__builtin_expect(fit != 0ull, 1)) {
                 const uint32_t fl = (uint32_t)__builtin_ctzll(fit);
-                const uint32_t fch = NPL > 1 ? readlane(bc, fl) : 0u;
+                uint32_t fch = 0u;
+                if constexpr (LAT) {  // lowest chunk whose mask has lane fl: scalar bit tests
+                    fch = NPL - 1;
+#pragma unroll
+                    for (int c = NPL - 2; c >= 0; --c) fch = ((F[c] >> fl) & 1ull) ? (uint32_t)c : fch;
+                } else if constexpr (NPL > 1) {
+                    fch = readlane(bc, fl);
+                }
                 place(r, jd, jc, jm, fl, fch, lanes_ne(frm, 0u));
                 ++r;
                 {
@@ -563,32 +602,37 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
 }
 
 // ---- variant table ------------------------------------------------------------------------------
-template <int NPL, int P, bool GEN, bool HOR>
+template <int NPL, int P, bool GEN, bool HOR, bool LAT>
 static hipError_t launch_one(const FifoArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((fifo_kernel<NPL, P, GEN, HOR>), dim3(a.n_items), dim3(kWave), 0, s, a);
+    hipLaunchKernelGGL((fifo_kernel<NPL, P, GEN, HOR, LAT>), dim3(a.n_items), dim3(kWave), 0, s, a);
     return hipGetLastError();
 }
 
 template <int NPL, bool GEN, bool HOR>
-static hipError_t launch_npl(const FifoArgs& a, int pool, hipStream_t s) {
+static hipError_t launch_npl(const FifoArgs& a, int pool, bool lat, hipStream_t s) {
     switch (pool) {
-        case 2: return launch_one<NPL, 2, GEN, HOR>(a, s);
-        case 4: return launch_one<NPL, 4, GEN, HOR>(a, s);
-        case 8: return launch_one<NPL, 8, GEN, HOR>(a, s);
-        case 16: return launch_one<NPL, 16, GEN, HOR>(a, s);
-        case 32: return launch_one<NPL, 32, GEN, HOR>(a, s);
+        case 2: return lat ? launch_one<NPL, 2, GEN, HOR, !GEN && !HOR>(a, s)
+                             : launch_one<NPL, 2, GEN, HOR, false>(a, s);
+        case 4: return lat ? launch_one<NPL, 4, GEN, HOR, !GEN && !HOR>(a, s)
+                             : launch_one<NPL, 4, GEN, HOR, false>(a, s);
+        case 8: return lat ? launch_one<NPL, 8, GEN, HOR, !GEN && !HOR>(a, s)
+                             : launch_one<NPL, 8, GEN, HOR, false>(a, s);
+        case 16: return lat ? launch_one<NPL, 16, GEN, HOR, !GEN && !HOR>(a, s)
+                             : launch_one<NPL, 16, GEN, HOR, false>(a, s);
+        case 32: return lat ? launch_one<NPL, 32, GEN, HOR, !GEN && !HOR>(a, s)
+                             : launch_one<NPL, 32, GEN, HOR, false>(a, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 template <bool GEN, bool HOR>
-static hipError_t launch_fifo_gen(const FifoArgs& a, int npl, int pool, hipStream_t s) {
+static hipError_t launch_fifo_gen(const FifoArgs& a, int npl, int pool, bool lat, hipStream_t s) {
     switch (npl) {
-        case 1: return launch_npl<1, GEN, HOR>(a, pool, s);
-        case 2: return launch_npl<2, GEN, HOR>(a, pool, s);
-        case 4: return launch_npl<4, GEN, HOR>(a, pool, s);
-        case 8: return launch_npl<8, GEN, HOR>(a, pool, s);
-        case 16: return launch_npl<16, GEN, HOR>(a, pool, s);
+        case 1: return launch_npl<1, GEN, HOR>(a, pool, lat, s);
+        case 2: return launch_npl<2, GEN, HOR>(a, pool, lat, s);
+        case 4: return launch_npl<4, GEN, HOR>(a, pool, lat, s);
+        case 8: return launch_npl<8, GEN, HOR>(a, pool, lat, s);
+        case 16: return launch_npl<16, GEN, HOR>(a, pool, lat, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -599,11 +643,24 @@ bool fifo_variant_exists(int npl, int pool) {
     return np && pp;
 }
 
+// The low-occupancy form for grids of at most kLatWavesPerCu cluster waves per CU (the streamed
+// batch path only): measured on C4 shards, 2.3-2.4 % faster at 1-4 waves per CU, 1.5 % slower at 8
+// (DESIGN.md §4).  MCS_FIFO_LAT=0/1 forces it off/on (A/B timing, the variant test).
+constexpr uint32_t kLatWavesPerCu = 4;
 hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, bool hor, hipStream_t s) {
-    if (a.n_items == 0) return hipSuccess;
-    if (hor) return a.gen.on ? hipErrorInvalidValue : launch_fifo_gen<false, true>(a, npl, pool, s);
-    return a.gen.on ? launch_fifo_gen<true, false>(a, npl, pool, s)
-                    : launch_fifo_gen<false, false>(a, npl, pool, s);
+    const char* env = getenv("MCS_FIFO_LAT");
+    const int g_lat_env = env ? atoi(env) : -1;
+    static int n_cu = 0;
+    if (n_cu == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+            n_cu = 256;
+    }
+    const bool lat = g_lat_env >= 0 ? g_lat_env != 0 : a.n_items <= kLatWavesPerCu * (uint32_t)n_cu;
+    if (hor) return a.gen.on ? hipErrorInvalidValue : launch_fifo_gen<false, true>(a, npl, pool, false, s);
+    return a.gen.on ? launch_fifo_gen<true, false>(a, npl, pool, false, s)
+                    : launch_fifo_gen<false, false>(a, npl, pool, lat, s);
 }
 
 // ---- device job-stream synthesis (mcs_gen.h; bit-identical to the host generator) -------------

@@ -297,14 +297,27 @@ def test_every_kernel_variant(policy):
         streams = gen_streams_host(gp, arrays, 1200)
         oracle = (O.delay_run_batch if policy == "DELAY" else O.fifo_run_batch)(arrays, streams, n_threads=8)
         for pool in (2, 4, 8, 16, 32):
-            for fused in (False, True):
-                with Engine(0, slot_pool=pool, policy=policy) as eng:
-                    eng.load_clusters(arrays)
-                    gp.fused = fused
-                    eng.generate_jobs(gp, 1200)
-                    eng.run()
-                    node, start, fin = eng.placements()
-                tag = f"nodes {nn} pool {pool} fused {fused}"
+            # streamed FIFO has two forms (the low-occupancy one is picked for small grids;
+            # MCS_FIFO_LAT forces either): both are checked
+            for fused, lat in ((False, "1"), (False, "0"), (True, None)):
+                if policy == "DELAY" and lat == "0":
+                    continue
+                old = os.environ.get("MCS_FIFO_LAT")
+                if lat is not None:
+                    os.environ["MCS_FIFO_LAT"] = lat
+                try:
+                    with Engine(0, slot_pool=pool, policy=policy) as eng:
+                        eng.load_clusters(arrays)
+                        gp.fused = fused
+                        eng.generate_jobs(gp, 1200)
+                        eng.run()
+                        node, start, fin = eng.placements()
+                finally:
+                    if old is None:
+                        os.environ.pop("MCS_FIFO_LAT", None)
+                    else:
+                        os.environ["MCS_FIFO_LAT"] = old
+                tag = f"nodes {nn} pool {pool} fused {fused} lat {lat}"
                 np.testing.assert_array_equal(node, oracle[0], err_msg=tag)
                 np.testing.assert_array_equal(start, oracle[1], err_msg=tag)
                 np.testing.assert_array_equal(fin, oracle[2], err_msg=tag)
