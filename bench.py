@@ -345,7 +345,7 @@ def main_c5(args, world, rank, local_rank):
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": "lock-step tick (tr_step/tr_lend/tr_post/tr_trader), launch/latency-bound",
+                "kernel": "lock-step tick (tr_step/tr_lend/tr_trader, one exchange), launch/latency-bound",
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "bytes_per_placement": BYTES_PER_PLACEMENT,
             },
