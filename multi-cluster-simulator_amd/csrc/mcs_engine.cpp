@@ -265,8 +265,10 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
 
     std::vector<uint2> free0(nn ? nn : 1), cap(nn ? nn : 1);
     std::vector<uint32_t> lc(nn ? nn : 1), lm(nn ? nn : 1), mxc(n_clusters), mxm(n_clusters);
+    e->free_lt31 = true;
     for (uint64_t i = 0; i < nn; ++i) {
         free0[i] = make_uint2(free_c[i], free_m[i]);
+        if (free_c[i] >= 0x7FFFFFFFu || free_m[i] >= 0x7FFFFFFFu) e->free_lt31 = false;
         cap[i] = make_uint2(cap_c[i], cap_m[i]);
         lc[i] = free_c[i];
         lm[i] = free_m[i];
@@ -522,6 +524,7 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     a.totals = e->d_totals;
     a.gen = e->gen;
     a.n_items = e->C;
+    a.guard_ok = e->free_lt31 ? 1u : 0u;
     mcs::DelayArgs da{};
     da.node_free0 = e->d_free0;
     da.node_off = e->d_node_off;

@@ -55,6 +55,7 @@ struct mcs_engine {
 
     uint32_t C = 0;
     uint32_t max_n = 0;
+    bool free_lt31 = false;  // every node free value < 2^31 - 1 (fifo_asm_kernel guard bits)
     uint64_t total_nodes = 0, total_jobs = 0;
     std::vector<uint32_t> node_off;
     std::vector<uint64_t> job_off;

@@ -86,6 +86,7 @@ struct FifoArgs {
     GenArgs gen;
     OnlineArgs on;
     uint32_t n_items;
+    uint32_t guard_ok;  // every node's free values < 2^31 - 1: the hand-scheduled loop may run
 };
 
 struct DelayArgs {
@@ -129,6 +130,10 @@ hipError_t launch_state(const StateArgs& a, uint32_t max_n, hipStream_t s);  // 
 // Launchers (mcs_kernels.hip).  Return hipSuccess or the launch error.
 hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, bool hor, hipStream_t s);
 bool fifo_variant_exists(int npl, int pool);
+// the hand-scheduled decision loop (mcs_fifo_asm.hip): NPL <= 4, P <= 8 (run as 8), streamed
+// batch runs; MCS_FIFO_ASM=0 turns it off
+bool fifo_asm_eligible(const FifoArgs& a, int npl, int pool, bool hor);
+hipError_t launch_fifo_asm(const FifoArgs& a, hipStream_t s);
 hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t* max_c,
                             const uint32_t* max_m, uint32_t n_clusters, uint64_t seed,
                             uint32_t max_dur, uint32_t cluster_base, hipStream_t s);

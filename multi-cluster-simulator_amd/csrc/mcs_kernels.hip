@@ -658,6 +658,7 @@ hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, bool hor, hipStream
             n_cu = 256;
     }
     const bool lat = g_lat_env >= 0 ? g_lat_env != 0 : a.n_items <= kLatWavesPerCu * (uint32_t)n_cu;
+    if (fifo_asm_eligible(a, npl, pool, hor)) return launch_fifo_asm(a, s);
     if (hor) return a.gen.on ? hipErrorInvalidValue : launch_fifo_gen<false, true>(a, npl, pool, false, s);
     return a.gen.on ? launch_fifo_gen<true, false>(a, npl, pool, false, s)
                     : launch_fifo_gen<false, false>(a, npl, pool, lat, s);

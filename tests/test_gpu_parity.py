@@ -297,14 +297,19 @@ def test_every_kernel_variant(policy):
         streams = gen_streams_host(gp, arrays, 1200)
         oracle = (O.delay_run_batch if policy == "DELAY" else O.fifo_run_batch)(arrays, streams, n_threads=8)
         for pool in (2, 4, 8, 16, 32):
-            # streamed FIFO has two forms (the low-occupancy one is picked for small grids;
-            # MCS_FIFO_LAT forces either): both are checked
-            for fused, lat in ((False, "1"), (False, "0"), (True, None)):
+            # streamed FIFO has three forms: the hand-scheduled loop (mcs_fifo_asm.hip, up to 256
+            # nodes and 8 slot rows; MCS_FIFO_ASM=0 turns it off) and the compiled kernel's two
+            # (the low-occupancy one is picked for small grids; MCS_FIFO_LAT forces either)
+            for fused, lat, asm in ((False, "1", "0"), (False, "0", "0"), (False, None, "1"), (True, None, None)):
                 if policy == "DELAY" and lat == "0":
                     continue
-                old = os.environ.get("MCS_FIFO_LAT")
-                if lat is not None:
-                    os.environ["MCS_FIFO_LAT"] = lat
+                if policy == "DELAY" and asm == "1":
+                    continue
+                env = {"MCS_FIFO_LAT": lat, "MCS_FIFO_ASM": asm}
+                old = {k: os.environ.get(k) for k in env}
+                for k, v in env.items():
+                    if v is not None:
+                        os.environ[k] = v
                 try:
                     with Engine(0, slot_pool=pool, policy=policy) as eng:
                         eng.load_clusters(arrays)
@@ -313,11 +318,12 @@ def test_every_kernel_variant(policy):
                         eng.run()
                         node, start, fin = eng.placements()
                 finally:
-                    if old is None:
-                        os.environ.pop("MCS_FIFO_LAT", None)
-                    else:
-                        os.environ["MCS_FIFO_LAT"] = old
-                tag = f"nodes {nn} pool {pool} fused {fused} lat {lat}"
+                    for k, v in old.items():
+                        if v is None:
+                            os.environ.pop(k, None)
+                        else:
+                            os.environ[k] = v
+                tag = f"nodes {nn} pool {pool} fused {fused} lat {lat} asm {asm}"
                 np.testing.assert_array_equal(node, oracle[0], err_msg=tag)
                 np.testing.assert_array_equal(start, oracle[1], err_msg=tag)
                 np.testing.assert_array_equal(fin, oracle[2], err_msg=tag)

@@ -9,6 +9,6 @@ jobs = float(sys.argv[2]) if len(sys.argv) > 2 else 67108864.0
 for g in sorted(glob.glob(f"{run}/pmc*_g*/pmc_counter_collection.csv")):
     agg = collections.defaultdict(float)
     for row in csv.DictReader(open(g)):
-        if "fifo_kernel" in row["Kernel_Name"]:
+        if any(k in row["Kernel_Name"] for k in ("fifo_kernel", "fifo_asm_kernel")):
             agg[row["Counter_Name"]] += float(row["Counter_Value"])
     print(g.split("/")[-2], {k: round(v / jobs, 3) for k, v in agg.items()})
