@@ -512,6 +512,7 @@ def main_batch(args, world, rank, local_rank):
     elapsed = time.perf_counter() - t0
 
     elapsed_max, placed_all = aggregate(elapsed, placed, device=dev)
+    kernel_name = eng.last_kernel  # the placement kernel these timings belong to
     cs = eng.cluster_stats()  # outside the timed region: per-cluster decision-loop diagnostics
     diag = {
         "loop_passes_per_job": float(cs["iterations"].sum()) / max(n_jobs, 1),
@@ -588,7 +589,7 @@ def main_batch(args, world, rank, local_rank):
                 "traffic": traffic,
                 "traffic_source": "profiles/ rocprofv3 --pmc pass of the same command (not measured in this run)"
                 if traffic is not None else None,
-                "kernel": "mcs::delay_kernel" if delay else "mcs::fifo_kernel",
+                "kernel": kernel_name,
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "bytes_per_placement": bpp,
                 "placements_per_launch": placements_per_launch,

@@ -184,6 +184,10 @@ int mcs_engine_create(const mcs_config* cfg, int device, mcs_engine** out);
 int mcs_engine_destroy(mcs_engine* eng);
 const char* mcs_last_error(const mcs_engine* eng);
 int mcs_abi_version(void);
+/* Name of the placement kernel the last mcs_run launched first ("mcs::fifo_asm_kernel",
+ * "mcs::fifo_kernel", "mcs::delay_kernel"; "" before any run): lets a caller match its timings
+ * to a rocprofv3 kernel trace.  Owned by the engine. */
+const char* mcs_last_kernel(const mcs_engine* eng);
 
 /* Cluster specs (assets/cluster_*.json, Cluster/Node in pkg/scheduler/cluster.go:14-24,127-138):
  * nodes of cluster c are [node_offsets[c], node_offsets[c+1]) in JSON array order; free_* are the

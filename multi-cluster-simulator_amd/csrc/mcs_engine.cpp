@@ -228,6 +228,7 @@ int mcs_engine_destroy(mcs_engine* e) {
 }
 
 const char* mcs_last_error(const mcs_engine* e) { return e ? e->err.c_str() : "null engine"; }
+const char* mcs_last_kernel(const mcs_engine* e) { return e ? e->last_kernel : ""; }
 
 uint32_t mcs_num_clusters(const mcs_engine* e) { return e ? e->C : 0; }
 uint64_t mcs_num_jobs(const mcs_engine* e) { return e ? e->total_jobs : 0; }
@@ -265,10 +266,11 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
 
     std::vector<uint2> free0(nn ? nn : 1), cap(nn ? nn : 1);
     std::vector<uint32_t> lc(nn ? nn : 1), lm(nn ? nn : 1), mxc(n_clusters), mxm(n_clusters);
-    e->free_lt31 = true;
+    e->free_lt31 = e->free_lt15 = true;
     for (uint64_t i = 0; i < nn; ++i) {
         free0[i] = make_uint2(free_c[i], free_m[i]);
         if (free_c[i] >= 0x7FFFFFFFu || free_m[i] >= 0x7FFFFFFFu) e->free_lt31 = false;
+        if (free_c[i] >= 0x7FFFu || free_m[i] >= 0x7FFFu) e->free_lt15 = false;
         cap[i] = make_uint2(cap_c[i], cap_m[i]);
         lc[i] = free_c[i];
         lm[i] = free_m[i];
@@ -524,7 +526,7 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     a.totals = e->d_totals;
     a.gen = e->gen;
     a.n_items = e->C;
-    a.guard_ok = e->free_lt31 ? 1u : 0u;
+    a.guard_ok = (e->free_lt31 ? 1u : 0u) | (e->free_lt15 ? 2u : 0u);
     mcs::DelayArgs da{};
     da.node_free0 = e->d_free0;
     da.node_off = e->d_node_off;
@@ -547,6 +549,13 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     uint32_t escalations = 0;
     int pool_used = pool;
     HIPCHK(e, hipMemsetAsync(e->d_totals, 0, sizeof(mcs::Totals), e->stream));
+    switch (delay ? -1 : mcs::fifo_asm_form(a, npl, pool, false)) {
+        case -1: e->last_kernel = "mcs::delay_kernel"; break;
+        case 17: e->last_kernel = "mcs::fifo_asm_kernel<16, true>"; break;
+        case 16: e->last_kernel = "mcs::fifo_asm_kernel<16, false>"; break;
+        case 32: e->last_kernel = "mcs::fifo_asm_kernel<32, false>"; break;
+        default: e->last_kernel = "mcs::fifo_kernel"; break;
+    }
     mcs::Totals tot{};
     for (;;) {
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));

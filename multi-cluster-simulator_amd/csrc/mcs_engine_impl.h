@@ -52,10 +52,12 @@ struct mcs_engine {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::string err;
+    const char* last_kernel = "";  // mcs_last_kernel: the first placement launch of the last run
 
     uint32_t C = 0;
     uint32_t max_n = 0;
-    bool free_lt31 = false;  // every node free value < 2^31 - 1 (fifo_asm_kernel guard bits)
+    bool free_lt31 = false;  // every node free value < 2^31 - 1 (fifo_asm_kernel<32> guard bits)
+    bool free_lt15 = false;  // every node free value < 2^15 - 1 (fifo_asm_kernel<16>)
     uint64_t total_nodes = 0, total_jobs = 0;
     std::vector<uint32_t> node_off;
     std::vector<uint64_t> job_off;

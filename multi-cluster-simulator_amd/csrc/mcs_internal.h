@@ -86,7 +86,8 @@ struct FifoArgs {
     GenArgs gen;
     OnlineArgs on;
     uint32_t n_items;
-    uint32_t guard_ok;  // every node's free values < 2^31 - 1: the hand-scheduled loop may run
+    uint32_t guard_ok;  // bit 0: every node's free values < 2^31 - 1 (the hand-scheduled loop
+                        // may run, W32 node format); bit 1: < 2^15 - 1 (W16 node format)
 };
 
 struct DelayArgs {
@@ -129,10 +130,14 @@ hipError_t launch_state(const StateArgs& a, uint32_t max_n, hipStream_t s);  // 
 
 // Launchers (mcs_kernels.hip).  Return hipSuccess or the launch error.
 hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, bool hor, hipStream_t s);
+uint32_t cu_count();  // CUs of the current device (256 on MI355X)
+// the low-occupancy forms are picked for grids of at most this many cluster waves per CU
+constexpr uint32_t kLatWavesPerCu = 4;
 bool fifo_variant_exists(int npl, int pool);
-// the hand-scheduled decision loop (mcs_fifo_asm.hip): NPL <= 4, P <= 8 (run as 8), streamed
+// the hand-scheduled decision loop (mcs_fifo_asm.hip): NPL == 4, P == 8, streamed
 // batch runs; MCS_FIFO_ASM=0 turns it off
 bool fifo_asm_eligible(const FifoArgs& a, int npl, int pool, bool hor);
+int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor);  // 17 (W16R), 16, 32 or 0
 hipError_t launch_fifo_asm(const FifoArgs& a, hipStream_t s);
 hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t* max_c,
                             const uint32_t* max_m, uint32_t n_clusters, uint64_t seed,

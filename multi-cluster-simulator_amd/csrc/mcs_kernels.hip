@@ -646,10 +646,7 @@ bool fifo_variant_exists(int npl, int pool) {
 // The low-occupancy form for grids of at most kLatWavesPerCu cluster waves per CU (the streamed
 // batch path only): measured on C4 shards, 2.3-2.4 % faster at 1-4 waves per CU, 1.5 % slower at 8
 // (DESIGN.md §4).  MCS_FIFO_LAT=0/1 forces it off/on (A/B timing, the variant test).
-constexpr uint32_t kLatWavesPerCu = 4;
-hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, bool hor, hipStream_t s) {
-    const char* env = getenv("MCS_FIFO_LAT");
-    const int g_lat_env = env ? atoi(env) : -1;
+uint32_t cu_count() {
     static int n_cu = 0;
     if (n_cu == 0) {
         int dev = 0;
@@ -657,7 +654,13 @@ hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, bool hor, hipStream
             hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
             n_cu = 256;
     }
-    const bool lat = g_lat_env >= 0 ? g_lat_env != 0 : a.n_items <= kLatWavesPerCu * (uint32_t)n_cu;
+    return (uint32_t)n_cu;
+}
+
+hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, bool hor, hipStream_t s) {
+    const char* env = getenv("MCS_FIFO_LAT");
+    const int g_lat_env = env ? atoi(env) : -1;
+    const bool lat = g_lat_env >= 0 ? g_lat_env != 0 : a.n_items <= kLatWavesPerCu * cu_count();
     if (fifo_asm_eligible(a, npl, pool, hor)) return launch_fifo_asm(a, s);
     if (hor) return a.gen.on ? hipErrorInvalidValue : launch_fifo_gen<false, true>(a, npl, pool, false, s);
     return a.gen.on ? launch_fifo_gen<true, false>(a, npl, pool, false, s)

@@ -290,6 +290,7 @@ int online_run(mcs_engine* e, uint32_t t_hor, mcs_stats* stats) {
     double kms = 0.0;
     uint32_t escalations = 0;
     HIPCHK(e, hipMemsetAsync(e->d_totals, 0, sizeof(Totals), e->stream));
+    e->last_kernel = delay ? "mcs::delay_kernel" : "mcs::fifo_kernel";  // the HOR variants
     Totals tot{};
     for (;;) {
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));

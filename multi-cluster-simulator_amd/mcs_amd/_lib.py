@@ -212,6 +212,7 @@ SIGNATURES = [
     ("mcs_engine_create", C.c_int, [C.POINTER(mcs_config), C.c_int, C.POINTER(vp)]),
     ("mcs_engine_destroy", C.c_int, [vp]),
     ("mcs_last_error", C.c_char_p, [vp]),
+    ("mcs_last_kernel", C.c_char_p, [vp]),
     ("mcs_load_clusters", C.c_int, [vp, u32p, u32p, u32p, u32p, u32p, C.c_uint32]),
     ("mcs_submit_jobs", C.c_int, [vp, u32p, u32p, u32p, u32p, u64p]),
     ("mcs_generate_jobs", C.c_int, [vp, C.POINTER(mcs_gen_params), C.c_uint64]),

@@ -356,6 +356,11 @@ class Engine:
         self._c(L.lib().mcs_run(self._h, L.MCS_TIME_NONE if t_end is None else int(t_end), C.byref(st)))
         return RunStats.from_c(st)
 
+    @property
+    def last_kernel(self) -> str:
+        """mcs_last_kernel: the placement kernel the last run launched first (its rocprofv3 name)."""
+        return L.lib().mcs_last_kernel(self._h).decode()
+
     def run_status(self, t_end: Optional[int] = None) -> Tuple[int, RunStats]:
         """mcs_run returning (status, stats) without raising (e.g. MCS_E_RANGE, results readable)."""
         st = L.mcs_stats()

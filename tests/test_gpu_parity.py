@@ -282,6 +282,50 @@ def test_extreme_values(engine):
     assert_parity(arrays, s, node, start, fin, cs, n_threads=1)
 
 
+@pytest.mark.parametrize("free", [0x7FFE, 0x7FFF])
+def test_hand_scheduled_loop_field_bounds(engine, free):
+    """The hand-scheduled loop's node formats at their bounds: free values up to 2^15 - 2 pick the
+    16-bit format, 2^15 - 1 the 32-bit one (mcs_last_kernel says which ran).  Requests equal to a
+    node's free value fit it exactly; each cluster's last job asks for one of the values around
+    2^15, 2^16 and 2^31 that a truncated or unclamped request would fit, and must deadlock."""
+    from mcs_amd.cluster import Node
+
+    rng = np.random.default_rng(free)
+    over = [free + 1, 0x8000, 0xFFFF, 0x10000, 0x10000 + 5, 0x17FFE, 0x7FFFFFFF, 0x80000000, 0x80000005,
+            0xFFFFFFFF]
+    clusters, parts = [], []
+    J = 3000
+    for k in range(2 * len(over)):
+        cl = Cluster(Id=k + 1, Nodes=[])
+        for i in range(200):
+            c = free if i % 7 == 0 else int(rng.integers(0, free + 1))
+            m = free if i % 5 == 0 else int(rng.integers(0, free + 1))
+            cl.Nodes.append(Node(Id=i + 1, Cores=free, Memory=free, CoresAvailable=c, MemoryAvailable=m))
+        clusters.append(cl)
+        arr = np.cumsum(rng.poisson(0.3, J)).astype(np.uint32)
+        dur = rng.integers(0, 40, J).astype(np.uint32)
+        cores = rng.integers(0, free // 3, J).astype(np.uint32)
+        mem = rng.integers(0, free // 3, J).astype(np.uint32)
+        exact = rng.random(J) < 0.02
+        cores[exact] = free
+        mem[exact] = free
+        o = over[k % len(over)]
+        if k < len(over):
+            cores[-1], mem[-1] = o, 1  # the oversize field is cores, then memory
+        else:
+            cores[-1], mem[-1] = 1, o
+        parts.append((arr, dur, cores, mem))
+    arrays = pack_clusters(clusters)
+    off = np.arange(len(parts) + 1, dtype=np.uint64) * J
+    s = JobStreams(*(np.concatenate([p[f] for p in parts]) for f in range(4)), off)
+    node, start, fin, st, cs = run_engine(engine, arrays, s)
+    assert engine.last_kernel == ("mcs::fifo_asm_kernel<16, true>" if free < 0x7FFF
+                                  else "mcs::fifo_asm_kernel<32, false>")
+    assert_parity(arrays, s, node, start, fin, cs)
+    assert (cs["flags"] & L.MCS_FLAG_DEADLOCK).all()  # every cluster's last request fits nowhere
+    assert (node.reshape(-1, J)[:, -1] == -1).all()
+
+
 @pytest.mark.parametrize("policy", ["FIFO", "DELAY"])
 def test_every_kernel_variant(policy):
     """Every compiled variant of the placement kernel — nodes per lane NPL 1..16 (the largest
@@ -297,13 +341,16 @@ def test_every_kernel_variant(policy):
         streams = gen_streams_host(gp, arrays, 1200)
         oracle = (O.delay_run_batch if policy == "DELAY" else O.fifo_run_batch)(arrays, streams, n_threads=8)
         for pool in (2, 4, 8, 16, 32):
-            # streamed FIFO has three forms: the hand-scheduled loop (mcs_fifo_asm.hip, up to 256
-            # nodes and 8 slot rows; MCS_FIFO_ASM=0 turns it off) and the compiled kernel's two
-            # (the low-occupancy one is picked for small grids; MCS_FIFO_LAT forces either)
-            for fused, lat, asm in ((False, "1", "0"), (False, "0", "0"), (False, None, "1"), (True, None, None)):
+            # streamed FIFO has five forms: the hand-scheduled loop (mcs_fifo_asm.hip, 129-256
+            # nodes and 8 slot rows) in its 16-bit node format with register slots (picked for these
+            # clusters), with LDS slots (MCS_FIFO_ASM=16) and its 32-bit one (=32; =0 turns the loop
+            # off), and the compiled kernel's two (the low-occupancy one is picked for small grids;
+            # MCS_FIFO_LAT forces either)
+            for fused, lat, asm in ((False, "1", "0"), (False, "0", "0"), (False, None, "1"),
+                                    (False, None, "16"), (False, None, "32"), (True, None, None)):
                 if policy == "DELAY" and lat == "0":
                     continue
-                if policy == "DELAY" and asm == "1":
+                if policy == "DELAY" and asm in ("1", "16", "32"):
                     continue
                 env = {"MCS_FIFO_LAT": lat, "MCS_FIFO_ASM": asm}
                 old = {k: os.environ.get(k) for k in env}

@@ -1,8 +1,8 @@
 """A/B timing of libmcs.so kernel variants on the C4 workload in ONE process per variant,
 alternating variants round-robin so box-to-box and thermal drift cancel.
 
-usage: python tools/ab_bench.py lib_a.so lib_b.so [...] [--rounds 3] [--steps 5]
-(env AB_POLICY=FIFO|DELAY, AB_NODES, AB_LOAD select the workload; default C4 FIFO)
+usage: python tools/ab_bench.py lib_a.so lib_b.so[@VAR=value] [...] [--rounds 3] [--steps 5]
+(env AB_POLICY=FIFO|DELAY, AB_NODES, AB_LOAD, AB_CLUSTERS select the workload; default C4 FIFO)
 Each variant runs in its own subprocess (MCS_LIB=<path>) per round; prints median kernel ms."""
 import json
 import os
@@ -20,7 +20,8 @@ from mcs_amd.engine import scaled_lambda
 steps = int(os.environ["STEPS"])
 nn, load = int(os.environ.get("AB_NODES", "256")), float(os.environ.get("AB_LOAD", "0.9"))
 eng = Engine(0, policy=os.environ.get("AB_POLICY", "FIFO"))
-eng.load_clusters(replicate(uniform_cluster(nn), 4096))
+nc = int(os.environ.get("AB_CLUSTERS", "4096"))
+eng.load_clusters(replicate(uniform_cluster(nn), nc))
 eng.generate_jobs(GenParams(arrival_mode=1, lam=scaled_lambda(nn, load=load)), 16384)
 eng.run()
 ms = [eng.run().kernel_ms for _ in range(steps)]
@@ -38,7 +39,11 @@ def main():
     res = {a: [] for a in args}
     for _ in range(rounds):
         for lib in args:
-            env = dict(os.environ, MCS_LIB=os.path.abspath(lib), REPO=REPO, STEPS=str(steps))
+            path, _, extra = lib.partition("@")  # lib.so@VAR=value: a per-variant environment
+            env = dict(os.environ, MCS_LIB=os.path.abspath(path), REPO=REPO, STEPS=str(steps))
+            if extra:
+                k, _, v = extra.partition("=")
+                env[k] = v
             out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True,
                                  timeout=300)
             if out.returncode != 0:
@@ -47,7 +52,7 @@ def main():
             res[lib] += json.loads(out.stdout.strip().splitlines()[-1])["ms"]
     for lib, ms in res.items():
         print(f"{os.path.basename(lib):28s} median {statistics.median(ms):8.3f} ms  min {min(ms):8.3f}  "
-              f"max {max(ms):8.3f}  ({67108864 / statistics.median(ms) / 1e6:.3f}e9 placements/s)")
+              f"max {max(ms):8.3f}  ({int(os.environ.get('AB_CLUSTERS', '4096')) * 16384 / statistics.median(ms) / 1e6:.3f}e9 placements/s)")
 
 
 if __name__ == "__main__":
