@@ -5,7 +5,7 @@ set -u
 mkdir -p gpurun_out/ab16
 timeout -k 10 240 python tools/asm_debug.py > gpurun_out/ab16/debug.txt 2>&1
 rc=$?; echo "debug rc=$rc"; [ $rc -ne 0 ] && exit $rc
-MCS_LIB="$PWD/variants/libmcs_a17.so" timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 \
+MCS_LIB="$PWD/${PARITY_LIB:-variants/libmcs_a17.so}" timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 \
     --timeout-method thread -p no:cacheprovider > gpurun_out/ab16/parity.log 2>&1
 rc=$?; tail -3 gpurun_out/ab16/parity.log; echo "parity rc=$rc"; [ $rc -ne 0 ] && exit $rc
 LIBS=${LIBS:-"variants/libmcs_a17.so@MCS_FIFO_ASM=16 variants/libmcs_a17.so@MCS_FIFO_ASM=17"}
