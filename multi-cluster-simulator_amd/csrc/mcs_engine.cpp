@@ -551,9 +551,10 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     HIPCHK(e, hipMemsetAsync(e->d_totals, 0, sizeof(mcs::Totals), e->stream));
     switch (delay ? -1 : mcs::fifo_asm_form(a, npl, pool, false)) {
         case -1: e->last_kernel = "mcs::delay_kernel"; break;
-        case 17: e->last_kernel = "mcs::fifo_asm_kernel<16, true>"; break;
-        case 16: e->last_kernel = "mcs::fifo_asm_kernel<16, false>"; break;
-        case 32: e->last_kernel = "mcs::fifo_asm_kernel<32, false>"; break;
+        case 18: e->last_kernel = "mcs::fifo_asm_kernel<16, true, 1, 2>"; break;
+        case 17: e->last_kernel = "mcs::fifo_asm_kernel<16, true, 4, 8>"; break;
+        case 16: e->last_kernel = "mcs::fifo_asm_kernel<16, false, 4, 8>"; break;
+        case 32: e->last_kernel = "mcs::fifo_asm_kernel<32, false, 4, 8>"; break;
         default: e->last_kernel = "mcs::fifo_kernel"; break;
     }
     mcs::Totals tot{};

@@ -48,8 +48,6 @@ namespace mcs {
 
 namespace {
 
-constexpr int kAsmNpl = 4;
-constexpr int kAsmPool = 8;
 
 // Register map of the loop (all fixed; listed as clobbers).
 //   s40 t     s41 min(64, J - cb)  s42 J   s43 have_w  s44 flags  s45 arr   s46 dur
@@ -64,7 +62,8 @@ constexpr int kAsmPool = 8;
 //   release: row expiry masks in s[50:55], s[60:63], s[86:91]
 //   v[64:71] nodes (W32: pairs {C, M} per chunk; W16: v64-v67)   v[72:79] fit-test differences
 //   v80-v86 fit bits / byte mask   (release: finish rows in v[72:87])
-//   v89 free rows  v90 earliest finish  v91-93 result batch (kx, start, finish)
+//   v89 free rows  v90 earliest finish  v91-92 result batch (kx, start; finish = start + dur at
+//   the store)
 //   v[94:97] records  v[98:101] next records   v107 slot column  v108 node column  v109 node base
 //   v110 lane  v111 -1   v[112:113] payload  v[114:115] {node address, fin}  v117 slot address
 //   v118 frm - 1  v120 DPP min / scan temp  v121 address  v[122:123] payload  v124 lane minimum
@@ -135,7 +134,6 @@ constexpr int kAsmPool = 8;
 #define MCS_FA_COMMIT16                                                                           \
     "s_lshr_b32 s53, s52, 3\n\t"                                                                  \
     "s_lshl3_add_u32 s54, s52, s50\n\t"                                                           \
-    "s_add_u32 s55, s40, s46\n\t"                                                                 \
     "s_mov_b64 exec, s[62:63]\n\t"                                                                \
     "s_set_gpr_idx_on s53, gpr_idx(SRC0,DST)\n\t"                                                 \
     "v_mov_b32 v64, v72\n\t"                                                                      \
@@ -151,7 +149,8 @@ constexpr int kAsmPool = 8;
     "v_add_u32 v118, -1, v89\n\t"                                                                 \
     "ds_sub_u64 v114, v[112:113]\n\t"                                                             \
     "ds_write_b64 v117, v[112:113]\n\t"                                                           \
-    "ds_write_b64 v117, v[114:115] offset:4096\n\t"
+    "ds_write_b64 v117, v[114:115] offset:4096\n\t"                                               \
+    "v_and_b32 v89, v118, v89\n\t"
 #define MCS_FA_INSERT16                                                                           \
     "v_mov_b32 v112, s48\n\t"                                                                     \
     "v_lshl_add_u32 v114, s54, 2, v109\n\t"                                                       \
@@ -160,7 +159,8 @@ constexpr int kAsmPool = 8;
     "v_add_u32 v118, -1, v89\n\t"                                                                 \
     "ds_sub_u32 v114, v112\n\t"                                                                   \
     "ds_write_b32 v117, v112\n\t"                                                                 \
-    "ds_write_b64 v117, v[114:115] offset:4096\n\t"
+    "ds_write_b64 v117, v[114:115] offset:4096\n\t"                                               \
+    "v_and_b32 v89, v118, v89\n\t"
 
 // the record at the cursor (s47) to the scalar unit
 #define MCS_FA_REC32                                                                              \
@@ -257,17 +257,15 @@ constexpr int kAsmPool = 8;
     "v_mov_b32 v39, -1\n\t"
 // (exec = the insert lane, or empty when the pool is full; s73 = the node array's LDS base)
 #define MCS_FA_INSERT16R                                                                          \
-    "v_mov_b32 v112, s48\n\t"                                                                    \
     "v_readlane_b32 s86, v117, s85\n\t" /* 0-7, or 8 with exec empty: in range either way */   \
     "s_lshl2_add_u32 s87, s54, s73\n\t"                                                          \
-    "v_add_u32 v118, -1, v89\n\t"                                                                \
-    "v_mov_b32 v114, s87\n\t"                                                                    \
-    "ds_sub_u32 v114, v112\n\t"                                                                  \
+    "s_lshl_b32 s76, 1, s86\n\t"                                                                 \
     "s_set_gpr_idx_on s86, gpr_idx(DST)\n\t"                                                     \
     "v_mov_b32 v32, s55\n\t"                                                                     \
     "v_mov_b32 v40, s48\n\t"                                                                     \
     "v_mov_b32 v48, s87\n\t"                                                                     \
-    "s_set_gpr_idx_off\n\t"
+    "s_set_gpr_idx_off\n\t"                                                                      \
+    "v_xor_b32 v89, s76, v89\n\t" /* the row is taken */
 #define MCS_FR_ROW(p, MASK, F, P, A)                                                                       \
     "s_cmp_lg_u64 " MASK ", 0\n\t"                                                               \
     "s_cbranch_scc0 mcsfa_r" #p "_%=\n\t"                                                        \
@@ -280,8 +278,11 @@ constexpr int kAsmPool = 8;
     "s_mov_b64 exec, -1\n"                                                                       \
     "mcsfa_r" #p "_%=:\n\t"
 #define MCS_FA_SCAN16R                                                                            \
-    "s_not_b32 s76, s74\n\t"                                                                     \
-    "v_mov_b32 v124, s76\n\t"                                                                    \
+    /* the LDS node copy is refreshed from the registers first (commits do not touch it) */       \
+    "ds_write_b32 v108, v64 offset:0\n\t"                                                        \
+    "ds_write_b32 v108, v65 offset:256\n\t"                                                      \
+    "ds_write_b32 v108, v66 offset:512\n\t"                                                      \
+    "ds_write_b32 v108, v67 offset:768\n\t"                                                      \
     "s_mov_b32 s75, 0\n\t"                                                                       \
     "v_cmp_ge_u32_e64 s[50:51], s40, v32\n\t"                                                    \
     "v_cmp_ge_u32_e64 s[52:53], s40, v33\n\t"                                                    \
@@ -296,20 +297,11 @@ constexpr int kAsmPool = 8;
     MCS_FR_ROW(4, "s[62:63]", "v36", "v44", "v52") MCS_FR_ROW(5, "s[86:87]", "v37", "v45", "v53")  \
     MCS_FR_ROW(6, "s[88:89]", "v38", "v46", "v54") MCS_FR_ROW(7, "s[90:91]", "v39", "v47", "v55")  \
     "s_sub_u32 s80, s80, s75\n\t" MCS_FA_RELOAD16                                               \
-    /* earliest remaining finish (released rows now hold -1) under the reload's latency */       \
-    "v_subrev_u32 v72, s74, v32\n\t"                                                             \
-    "v_subrev_u32 v73, s74, v33\n\t"                                                             \
-    "v_subrev_u32 v74, s74, v34\n\t"                                                             \
-    "v_subrev_u32 v75, s74, v35\n\t"                                                             \
-    "v_subrev_u32 v76, s74, v36\n\t"                                                             \
-    "v_subrev_u32 v77, s74, v37\n\t"                                                             \
-    "v_subrev_u32 v78, s74, v38\n\t"                                                             \
-    "v_subrev_u32 v79, s74, v39\n\t"                                                             \
-    "v_min3_u32 v124, v124, v72, v73\n\t"                                                        \
-    "v_min3_u32 v120, v74, v75, v76\n\t"                                                         \
-    "v_min3_u32 v124, v124, v77, v78\n\t"                                                        \
-    "v_min3_u32 v124, v124, v79, v120\n\t"                                                       \
-    "v_add_u32 v90, s74, v124\n\t"
+    /* the lane's earliest remaining finish (released rows now hold -1) */                     \
+    "v_min3_u32 v90, v32, v33, v34\n\t"                                                          \
+    "v_min3_u32 v90, v90, v35, v36\n\t"                                                          \
+    "v_min3_u32 v90, v90, v37, v38\n\t"                                                          \
+    "v_min_u32 v90, v90, v39\n\t"
 
 // node registers back from the LDS copy
 #define MCS_FA_RELOAD32                                                                           \
@@ -336,6 +328,81 @@ constexpr int kAsmPool = 8;
     "v_min_u32 v97, 0x7fff, v101\n\t"                                                             \
     "v_lshl_or_b32 v96, v97, 16, v96\n\t"
 
+// ---- per-form hooks of the loop -----------------------------------------------------------------
+// lanes with a fit into vcc
+#define MCS_FA_ANYFIT "v_cmp_ne_u32_e32 vcc, 0, v86\n\t"
+#define MCS_FA_ANYFIT32 MCS_FA_ANYFIT
+#define MCS_FA_ANYFIT16 MCS_FA_ANYFIT
+#define MCS_FA_ANYFIT16R MCS_FA_ANYFIT
+// the fitting lane's byte mask (PICK1, a broadcast) and its lowest fitting chunk (PICK2)
+#define MCS_FA_PICK1 "v_readlane_b32 s51, v86, s50\n\t"
+#define MCS_FA_PICK2 "s_ff1_i32_b32 s52, s51\n\t" /* 8 * the lane's first fitting chunk */
+#define MCS_FA_PICK132 MCS_FA_PICK1
+#define MCS_FA_PICK116 MCS_FA_PICK1
+#define MCS_FA_PICK116R MCS_FA_PICK1
+#define MCS_FA_PICK232 MCS_FA_PICK2
+#define MCS_FA_PICK216 MCS_FA_PICK2
+#define MCS_FA_PICK216R MCS_FA_PICK2
+// a zero-duration job's node (kx into s54; m0 = the cursor for the result writes)
+#define MCS_FA_ZEROKX                                                                             \
+    "v_readlane_b32 s51, v86, s50\n\t"                                                           \
+    "s_mov_b32 m0, s47\n\t"                                                                      \
+    "s_ff1_i32_b32 s52, s51\n\t"                                                                 \
+    "s_lshl3_add_u32 s54, s52, s50\n\t"
+#define MCS_FA_ZEROKX32 MCS_FA_ZEROKX
+#define MCS_FA_ZEROKX16 MCS_FA_ZEROKX
+#define MCS_FA_ZEROKX16R MCS_FA_ZEROKX
+// slots of the pool (64 lanes x P rows)
+#define MCS_FA_POOLMAX32 "64*8"
+#define MCS_FA_POOLMAX16 "64*8"
+#define MCS_FA_POOLMAX16R "64*8"
+// the result batch's node index from kx = chunk * 64 + lane
+#define MCS_FA_NODEIDX                                                                            \
+    "v_and_b32 v126, 63, v91\n\t"                                                                \
+    "v_lshrrev_b32 v127, 6, v91\n\t"                                                             \
+    "v_lshl_add_u32 v126, v126, 2, v127\n\t" /* node = lane * 4 + chunk */
+#define MCS_FA_NODEIDX32 MCS_FA_NODEIDX
+#define MCS_FA_NODEIDX16 MCS_FA_NODEIDX
+#define MCS_FA_NODEIDX16R MCS_FA_NODEIDX
+
+// ---- W16S: W16R for clusters of at most 64 nodes (one chunk, node = lane) and 2 slot rows --------
+// (cluster_small / cluster_big: C1-C3).  The fit bit is bit 15 of one SDWA AND; no chunk pick, and
+// the commit is a plain move under exec = the fitting lane.  s72 = 0x7fff.
+#define MCS_FA_FIT16S                                                                             \
+    "v_pk_sub_u16 v72, v64, s48\n\t"                                                             \
+    "v_and_b32_sdwa v80, v72, v72 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_cmp_lt_u32_e64 s[60:61], s49, v89\n\t"                                                    \
+    "v_ffbl_b32 v117, v89\n\t"
+#define MCS_FA_ANYFIT16S "v_cmp_lt_u32_e32 vcc, s72, v80\n\t"
+#define MCS_FA_PICK116S ""
+#define MCS_FA_PICK216S ""
+#define MCS_FA_FREELANES16S ""
+#define MCS_FA_COMMIT16S                                                                          \
+    "s_mov_b32 s54, s50\n\t"                                                                     \
+    "s_mov_b64 exec, s[62:63]\n\t"                                                               \
+    "v_mov_b32 v64, v72\n\t"
+#define MCS_FA_ZEROKX16S                                                                          \
+    "s_mov_b32 m0, s47\n\t"                                                                      \
+    "s_mov_b32 s54, s50\n\t"
+#define MCS_FA_POOLMAX16S "64*2"
+#define MCS_FA_NODEIDX16S "v_mov_b32 v126, v91\n\t"
+#define MCS_FA_REC16S MCS_FA_REC16
+#define MCS_FA_TAKE16S MCS_FA_TAKE16
+#define MCS_FA_RELOAD16S "ds_read_b32 v64, v108 offset:0\n\t"
+#define MCS_FA_INIT16S                                                                            \
+    "s_mov_b32 s49, 0x100\n\t"                                                                   \
+    "v_mov_b32 v32, -1\n\t"                                                                      \
+    "v_mov_b32 v33, -1\n\t"
+#define MCS_FA_INSERT16S MCS_FA_INSERT16R
+#define MCS_FA_SCAN16S                                                                            \
+    "ds_write_b32 v108, v64 offset:0\n\t"                                                        \
+    "s_mov_b32 s75, 0\n\t"                                                                       \
+    "v_cmp_ge_u32_e64 s[50:51], s40, v32\n\t"                                                    \
+    "v_cmp_ge_u32_e64 s[52:53], s40, v33\n\t"                                                    \
+    MCS_FR_ROW(0, "s[50:51]", "v32", "v40", "v48") MCS_FR_ROW(1, "s[52:53]", "v33", "v41", "v49")  \
+    "s_sub_u32 s80, s80, s75\n\t" MCS_FA_RELOAD16S                                              \
+    "v_min_u32 v90, v32, v33\n\t"
+
 // ---- the decision loop ------------------------------------------------------------------------
 #define MCS_FA_LOOP(W)                                                                            \
     /* ---- entry: state into the fixed registers ---- */                                        \
@@ -352,6 +419,7 @@ constexpr int kAsmPool = 8;
     "s_mov_b32 s82, 0\n\t"                                                                        \
     "s_mov_b32 s83, 0\n\t"                                                                        \
     "s_mov_b32 s84, 0\n\t"                                                                        \
+    "s_mov_b32 s77, -1\n\t" /* nothing running */                                                \
     "s_mov_b64 s[64:65], %[jobs]\n\t"                                                             \
     "s_mov_b64 s[66:67], %[onp]\n\t"                                                              \
     "s_mov_b64 s[68:69], %[osp]\n\t"                                                              \
@@ -380,29 +448,26 @@ constexpr int kAsmPool = 8;
     /* ---- one pass = one decision (scheduler.go:216-296) ---- */                               \
     "mcsfa_inner_%=:\n\t"                                                                         \
     "s_cmp_gt_u32 s45, s40\n\t" /* ready head not arrived: sleep to it */                         \
-    "s_cbranch_scc1 mcsfa_arrive_%=\n\t" MCS_FA_FIT##W                                            \
-    "v_cmp_ne_u32_e32 vcc, 0, v86\n\t"                                                            \
+    "s_cbranch_scc1 mcsfa_arrive_%=\n\t" MCS_FA_FIT##W MCS_FA_ANYFIT##W                           \
+    "s_add_u32 s55, s40, s46\n\t"                                                                 \
     "s_cbranch_vccz mcsfa_nofit_%=\n\t"                                                           \
     "s_ff1_i32_b64 s50, vcc\n\t" /* lowest lane with a fit */                                     \
     "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
     "s_cbranch_scc1 mcsfa_zero_%=\n\t"                                                            \
-    "v_readlane_b32 s51, v86, s50\n\t" MCS_FA_FREELANES##W                                       \
-    "s_lshl_b64 s[62:63], 1, s50\n\t"                                                             \
-    "s_ff1_i32_b32 s52, s51\n\t" /* 8 * its first fitting chunk */                                \
+    MCS_FA_PICK1##W MCS_FA_FREELANES##W                                                           \
+    "s_lshl_b64 s[62:63], 1, s50\n\t" MCS_FA_PICK2##W                                             \
     MCS_FA_COMMIT##W                                                                              \
     /* running-slot insert: lowest lane with a free row (none: exec empty), its lowest row */     \
     "s_ff1_i32_b64 s85, s[60:61]\n\t"                                                             \
     "s_lshl_b64 s[62:63], 1, s85\n\t"                                                             \
     "s_and_b64 exec, s[62:63], s[60:61]\n\t" MCS_FA_INSERT##W                                     \
-    "v_and_b32 v89, v118, v89\n\t"                                                                \
-    "v_min_u32 v90, s55, v90\n\t"                                                                 \
+    "s_min_u32 s77, s77, s55\n\t" /* the wave's earliest finish */                                \
     "s_mov_b64 exec, -1\n\t"                                                                      \
     "s_mov_b32 m0, s47\n\t"                                                                       \
     "s_add_u32 s80, s80, 1\n\t"                                                                   \
     "s_max_u32 s81, s81, s80\n\t"                                                                 \
     "v_writelane_b32 v91, s54, m0\n\t"                                                            \
-    "v_writelane_b32 v92, s40, m0\n\t"                                                            \
-    "v_writelane_b32 v93, s55, m0\n"                                                              \
+    "v_writelane_b32 v92, s40, m0\n"                                                              \
     /* next ready job; a WaitQueue head placed sleeps 1 s (:250) */                               \
     "mcsfa_placed_%=:\n\t"                                                                        \
     "s_add_u32 s47, s47, 1\n\t"                                                                   \
@@ -414,14 +479,9 @@ constexpr int kAsmPool = 8;
     "s_branch mcsfa_bend_%=\n"                                                                    \
                                                                                                   \
     /* zero-duration job: committed and released before the next decision (D3) */               \
-    "mcsfa_zero_%=:\n\t"                                                                          \
-    "v_readlane_b32 s51, v86, s50\n\t"                                                            \
-    "s_mov_b32 m0, s47\n\t"                                                                       \
-    "s_ff1_i32_b32 s52, s51\n\t"                                                                  \
-    "s_lshl3_add_u32 s54, s52, s50\n\t"                                                           \
+    "mcsfa_zero_%=:\n\t" MCS_FA_ZEROKX##W                                                        \
     "v_writelane_b32 v91, s54, m0\n\t"                                                            \
     "v_writelane_b32 v92, s40, m0\n\t"                                                            \
-    "v_writelane_b32 v93, s40, m0\n\t"                                                            \
     "s_branch mcsfa_placed_%=\n"                                                                  \
                                                                                                   \
     "mcsfa_hwadv_%=:\n\t"                                                                         \
@@ -435,21 +495,6 @@ constexpr int kAsmPool = 8;
     "s_add_u32 s82, s82, s76\n\t"                                                                 \
     "s_mov_b32 s43, 1\n\t"                                                                        \
     "s_add_u32 s83, s83, 1\n\t"                                                                   \
-    "v_mov_b32 v120, v90\n\t"                                                                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_min_u32_dpp v120, v120, v120 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_min_u32_dpp v120, v120, v120 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_min_u32_dpp v120, v120, v120 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_min_u32_dpp v120, v120, v120 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_min_u32_dpp v120, v120, v120 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"                  \
-    "s_nop 1\n\t"                                                                                 \
-    "v_min_u32_dpp v120, v120, v120 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"                  \
-    "s_nop 1\n\t"                                                                                 \
-    "v_readlane_b32 s77, v120, 63\n\t"                                                            \
     "s_cmp_eq_u32 s77, -1\n\t"                                                                    \
     "s_cbranch_scc1 mcsfa_deadlock_%=\n\t"                                                        \
     "s_add_u32 s56, s40, 1\n\t"                                                                   \
@@ -467,11 +512,27 @@ constexpr int kAsmPool = 8;
     "s_cmp_lt_u32 s56, s40\n\t"                                                                   \
     "s_cbranch_scc1 mcsfa_clkovf_%=\n\t"                                                          \
     "s_mov_b32 s40, s56\n\t"                                                                      \
-    "v_cmp_ge_u32_e32 vcc, s40, v90\n\t"                                                          \
-    "s_cbranch_vccz mcsfa_loopend_%=\n\t"                                                         \
+    "s_cmp_lt_u32 s40, s77\n\t" /* nothing finishes by t: no release */                          \
+    "s_cbranch_scc1 mcsfa_loopend_%=\n\t"                                                         \
     /* release every running job with finish <= t (cluster.go:153-157) */                        \
     "s_add_u32 s84, s84, 1\n\t"                                                                   \
     "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN##W                                                   \
+    /* the wave's earliest remaining finish (DPP minimum of v90) under the reload's latency */   \
+    "v_mov_b32 v120, v90\n\t"                                                                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"                  \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"                  \
+    "s_nop 1\n\t"                                                                                 \
+    "v_readlane_b32 s77, v120, 63\n\t"                                                            \
     "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
     "s_branch mcsfa_loopend_%=\n"                                                                 \
                                                                                                   \
@@ -487,7 +548,7 @@ constexpr int kAsmPool = 8;
                                                                                                   \
     /* ---- batch end: store the 64 results, take the prefetched records, prefetch the next ---- */ \
     "mcsfa_bend_%=:\n\t"                                                                          \
-    "s_cmp_gt_u32 s81, 64*8\n\t"                                                                  \
+    "s_cmp_gt_u32 s81, " MCS_FA_POOLMAX##W "\n\t"                                                 \
     "s_cbranch_scc1 mcsfa_poolovf_%=\n\t"                                                         \
     "s_add_u32 s76, s57, s47\n\t"                                                                 \
     "s_cmp_ge_u32 s76, s42\n\t"                                                                   \
@@ -495,11 +556,10 @@ constexpr int kAsmPool = 8;
     "s_waitcnt vmcnt(0)\n\t"                                                                      \
     "v_add_u32 v125, s57, v110\n\t"                                                               \
     "v_lshlrev_b32 v125, 2, v125\n\t"                                                             \
-    "v_and_b32 v126, 63, v91\n\t"                                                                 \
-    "v_lshrrev_b32 v127, 6, v91\n\t"                                                              \
-    "v_lshl_add_u32 v126, v126, 2, v127\n\t" /* node = lane * 4 + chunk */                        \
+    MCS_FA_NODEIDX##W                                                                             \
     "global_store_dword v125, v126, s[66:67] nt\n\t"                                              \
     "global_store_dword v125, v92, s[68:69] nt\n\t"                                               \
+    "v_add_u32 v93, v92, v95\n\t" /* finish = start + the batch's duration column */            \
     "global_store_dword v125, v93, s[70:71] nt\n\t"                                               \
     "s_add_u32 s57, s57, 64\n\t" MCS_FA_TAKE##W                                                   \
     "v_add_u32 v121, s57, v110\n\t"                                                               \
@@ -525,7 +585,7 @@ constexpr int kAsmPool = 8;
     "s_mov_b32 %[nrel], s84\n\t"                                                                  \
     "v_mov_b32 %[on], v91\n\t"                                                                    \
     "v_mov_b32 %[os], v92\n\t"                                                                    \
-    "v_mov_b32 %[of], v93\n\t"                                                                    \
+    "v_add_u32 %[of], v92, v95\n\t"                                                              \
     "v_mov_b32 %[frm], v89\n\t"                                                                   \
     "v_mov_b32 %[lmin], v90\n\t"                                                                  \
     "s_nop 1"
@@ -534,23 +594,25 @@ constexpr int kAsmPool = 8;
 // payloads [8][64] (u64 / u32 in a u64 stride) at 2048, slot {node address | finish << 32}
 // [8][64] at 6144 (the offsets in the asm)
 // (RS: the W16R form, running slots in registers; the LDS slot arrays are then unused)
-template <int W, bool RS>
+// (NPL nodes per lane, P slot rows: 4/8 for 129-256 node clusters, 1/2 for at most 64 nodes)
+template <int W, bool RS, int NPL, int P>
 __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
     static_assert(W == 16 || !RS, "register slots: 16-bit node format only");
+    static_assert((NPL == 4 && P == 8) || (NPL == 1 && P == 2 && W == 16 && RS), "loop shapes");
     const uint32_t item = blockIdx.x;
     const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
     const uint32_t lane = threadIdx.x;
 
-    __shared__ uint64_t lds[kAsmNpl * kWave + 2 * kAsmPool * kWave];
-    uint64_t* const pay_nf = lds + kAsmNpl * kWave + kAsmPool * kWave;
+    __shared__ uint64_t lds[NPL * kWave + 2 * P * kWave];
+    uint64_t* const pay_nf = lds + NPL * kWave + P * kWave;
 
     constexpr uint32_t kGuard = W == 32 ? 0x80000000u : 0x8000u;
     constexpr uint32_t kClamp = kGuard - 1u;  // request clamp and padding value
     const uint32_t n0 = a.node_off[ci];
     const uint32_t N = a.node_off[ci + 1] - n0;
 #pragma unroll
-    for (int c = 0; c < kAsmNpl; ++c) {
-        const uint32_t node = lane * kAsmNpl + c;
+    for (int c = 0; c < NPL; ++c) {
+        const uint32_t node = lane * NPL + c;
         uint2 v = make_uint2(kClamp, kClamp);  // padding: never fits
         if (node < N) {
             v = a.node_free0[n0 + node];
@@ -564,7 +626,7 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
     }
     if constexpr (!RS) {
 #pragma unroll
-        for (int p = 0; p < kAsmPool; ++p) pay_nf[p * kWave + lane] = (uint64_t)kEmpty << 32;
+        for (int p = 0; p < P; ++p) pay_nf[p * kWave + lane] = (uint64_t)kEmpty << 32;
     }
 
     const uint64_t j0 = a.job_off[ci];
@@ -585,13 +647,13 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
     const uint32_t v_nb = base + lane * (W / 4u);
     const uint32_t v_nbase = base;
     // perm selectors: W32 gathers chunk pairs 0/1 and 2/3, W16 all four chunks at once
-    const uint32_t sel0 = W == 32 ? 0x0c0c0b09u : 0x0b0a0908u;
+    const uint32_t sel0 = W == 32 ? 0x0c0c0b09u : NPL == 1 ? 0x7fffu : 0x0b0a0908u;
     const uint32_t sel1 = W == 32 ? 0x0b090c0cu : base;  // (W16R: the node array's LDS base)
 
     uint32_t t = 0, r = 0, flags = 0, have_w = 0;
     // free slot rows of the lane (W16 forms: plus the sentinel bit 8, so the lowest free row of a
     // full lane reads as 8, a register index still in range)
-    uint32_t frm = (1u << kAsmPool) - 1u + (W == 16 ? 0x100u : 0u), lmin = kEmpty;
+    uint32_t frm = (1u << P) - 1u + (W == 16 ? 0x100u : 0u), lmin = kEmpty;
     uint32_t used = 0, peak = 0, waited = 0, n_slow = 0, n_rel = 0;
     uint32_t on = 0, os = 0, of = 0;
 
@@ -609,6 +671,8 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
     : MCS_FA_CLOBBERS
     if constexpr (W == 32)
         asm volatile(MCS_FA_LOOP(32) MCS_FA_OPERANDS);
+    else if constexpr (NPL == 1)
+        asm volatile(MCS_FA_LOOP(16S) MCS_FA_OPERANDS);
     else if constexpr (RS)
         asm volatile(MCS_FA_LOOP(16R) MCS_FA_OPERANDS);
     else
@@ -616,13 +680,13 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
 #undef MCS_FA_OPERANDS
 #pragma clang diagnostic pop
 
-    if (peak > (uint32_t)(kAsmPool * kWave)) flags |= MCS_FLAG_OVERFLOW;  // a skipped insert
+    if (peak > (uint32_t)(P * kWave)) flags |= MCS_FLAG_OVERFLOW;  // a skipped insert
     const uint32_t placed = r;  // FIFO places every job it decides, in order
     if (!(flags & MCS_FLAG_OVERFLOW)) {
         if (r > 0u) {  // the batch holding the last decision (earlier ones are stored)
             const uint32_t i = ((r - 1u) & ~63u) + lane;
             if (i < r) {
-                o_node[i] = (int32_t)((on & 63u) * kAsmNpl + (on >> 6));
+                o_node[i] = (int32_t)(NPL == 1 ? on : (on & 63u) * NPL + (on >> 6));
                 o_start[i] = os;
                 o_finish[i] = of;
             }
@@ -643,7 +707,7 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
         st.waited = waited;
         st.peak_running = peak;
         st.flags = flags;
-        st.pool = (uint32_t)kAsmPool;
+        st.pool = (uint32_t)P;
         st.iterations = n_slow + r;  // passes: one per decision, plus the clock advances
         st.release_scans = n_rel;
         a.cstats[ci] = st;
@@ -661,15 +725,17 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
 
 }  // namespace
 
-// Form codes: 17 = W16R (where the 16-bit format fits), 16 = W16 with LDS slots, 32 = W32, 0 =
-// the compiled kernel.  MCS_FIFO_ASM=0 turns the hand-scheduled loop off, =16 / =32 force a form
-// (A/B timing, the variant tests).
+// Form codes: 17 = W16R and 18 = W16S (where the 16-bit format fits), 16 = W16 with LDS slots,
+// 32 = W32, 0 = the compiled kernel.  MCS_FIFO_ASM=0 turns the hand-scheduled loop off, =16 / =32
+// force a form (A/B timing, the variant tests; neither has a small-cluster shape).
 int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor) {
     const char* env = getenv("MCS_FIFO_ASM");
     const int want = env ? atoi(env) : 1;
-    // the loop is written for 129-256 node clusters with 8 slot rows (the C4 shape); smaller
-    // clusters keep the compiled kernel's fewer chunks and rows (C2/C3 ran 1.4x slower here)
-    if (want == 0 || hor || a.gen.on || npl != kAsmNpl || pool != kAsmPool) return 0;
+    // the loop's two shapes: 129-256 node clusters with 8 slot rows (C4) and at most 64 nodes with 2
+    // rows (C1-C3); other shapes and pools keep the compiled kernel
+    if (want == 0 || hor || a.gen.on) return 0;
+    if (npl == 1 && pool == 2) return (a.guard_ok & 2u) && want != 16 && want != 32 ? 18 : 0;
+    if (npl != 4 || pool != 8) return 0;
     // register slots: one LDS round trip per release instead of 2 + rows; measured faster than LDS
     // slots at every occupancy from 1 to 16 cluster waves per CU
     if ((a.guard_ok & 2u) && want != 32) return want == 16 ? 16 : 17;
@@ -680,16 +746,14 @@ bool fifo_asm_eligible(const FifoArgs& a, int npl, int pool, bool hor) {
     return fifo_asm_form(a, npl, pool, hor) != 0;
 }
 
-hipError_t launch_fifo_asm(const FifoArgs& a, hipStream_t s) {
-    const int w = fifo_asm_form(a, kAsmNpl, kAsmPool, false);
-    if (w == 17)
-        hipLaunchKernelGGL((fifo_asm_kernel<16, true>), dim3(a.n_items), dim3(kWave), 0, s, a);
-    else if (w == 16)
-        hipLaunchKernelGGL((fifo_asm_kernel<16, false>), dim3(a.n_items), dim3(kWave), 0, s, a);
-    else if (w == 32)
-        hipLaunchKernelGGL((fifo_asm_kernel<32, false>), dim3(a.n_items), dim3(kWave), 0, s, a);
-    else
-        return hipErrorInvalidValue;
+hipError_t launch_fifo_asm(const FifoArgs& a, int npl, int pool, hipStream_t s) {
+    switch (fifo_asm_form(a, npl, pool, false)) {
+        case 18: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 1, 2>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
+        case 17: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 4, 8>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
+        case 16: hipLaunchKernelGGL((fifo_asm_kernel<16, false, 4, 8>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
+        case 32: hipLaunchKernelGGL((fifo_asm_kernel<32, false, 4, 8>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -134,11 +134,11 @@ uint32_t cu_count();  // CUs of the current device (256 on MI355X)
 // the low-occupancy forms are picked for grids of at most this many cluster waves per CU
 constexpr uint32_t kLatWavesPerCu = 4;
 bool fifo_variant_exists(int npl, int pool);
-// the hand-scheduled decision loop (mcs_fifo_asm.hip): NPL == 4, P == 8, streamed
+// the hand-scheduled decision loop (mcs_fifo_asm.hip): NPL 4 / P 8 or NPL 1 / P 2, streamed
 // batch runs; MCS_FIFO_ASM=0 turns it off
 bool fifo_asm_eligible(const FifoArgs& a, int npl, int pool, bool hor);
-int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor);  // 17 (W16R), 16, 32 or 0
-hipError_t launch_fifo_asm(const FifoArgs& a, hipStream_t s);
+int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor);  // 18, 17, 16, 32 or 0
+hipError_t launch_fifo_asm(const FifoArgs& a, int npl, int pool, hipStream_t s);
 hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t* max_c,
                             const uint32_t* max_m, uint32_t n_clusters, uint64_t seed,
                             uint32_t max_dur, uint32_t cluster_base, hipStream_t s);

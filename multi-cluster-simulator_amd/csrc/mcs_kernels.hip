@@ -661,7 +661,7 @@ hipError_t launch_fifo(const FifoArgs& a, int npl, int pool, bool hor, hipStream
     const char* env = getenv("MCS_FIFO_LAT");
     const int g_lat_env = env ? atoi(env) : -1;
     const bool lat = g_lat_env >= 0 ? g_lat_env != 0 : a.n_items <= kLatWavesPerCu * cu_count();
-    if (fifo_asm_eligible(a, npl, pool, hor)) return launch_fifo_asm(a, s);
+    if (fifo_asm_eligible(a, npl, pool, hor)) return launch_fifo_asm(a, npl, pool, s);
     if (hor) return a.gen.on ? hipErrorInvalidValue : launch_fifo_gen<false, true>(a, npl, pool, false, s);
     return a.gen.on ? launch_fifo_gen<true, false>(a, npl, pool, false, s)
                     : launch_fifo_gen<false, false>(a, npl, pool, lat, s);

@@ -319,8 +319,8 @@ def test_hand_scheduled_loop_field_bounds(engine, free):
     off = np.arange(len(parts) + 1, dtype=np.uint64) * J
     s = JobStreams(*(np.concatenate([p[f] for p in parts]) for f in range(4)), off)
     node, start, fin, st, cs = run_engine(engine, arrays, s)
-    assert engine.last_kernel == ("mcs::fifo_asm_kernel<16, true>" if free < 0x7FFF
-                                  else "mcs::fifo_asm_kernel<32, false>")
+    assert engine.last_kernel == ("mcs::fifo_asm_kernel<16, true, 4, 8>" if free < 0x7FFF
+                                  else "mcs::fifo_asm_kernel<32, false, 4, 8>")
     assert_parity(arrays, s, node, start, fin, cs)
     assert (cs["flags"] & L.MCS_FLAG_DEADLOCK).all()  # every cluster's last request fits nowhere
     assert (node.reshape(-1, J)[:, -1] == -1).all()
