@@ -126,7 +126,6 @@ namespace {
     "s_lshr_b32 s53, s52, 2\n\t"                                                                  \
     "s_lshl3_add_u32 s54, s52, s50\n\t" /* kx = chunk * 64 + fl */                                \
     "s_add_u32 s55, s40, s46\n\t"       /* finish */                                              \
-    "s_mov_b64 exec, s[62:63]\n\t"                                                                \
     "s_set_gpr_idx_on s53, gpr_idx(SRC0,DST)\n\t"                                                 \
     "v_mov_b32 v64, v72\n\t"                                                                      \
     "v_mov_b32 v65, v73\n\t"                                                                      \
@@ -134,7 +133,6 @@ namespace {
 #define MCS_FA_COMMIT16                                                                           \
     "s_lshr_b32 s53, s52, 3\n\t"                                                                  \
     "s_lshl3_add_u32 s54, s52, s50\n\t"                                                           \
-    "s_mov_b64 exec, s[62:63]\n\t"                                                                \
     "s_set_gpr_idx_on s53, gpr_idx(SRC0,DST)\n\t"                                                 \
     "v_mov_b32 v64, v72\n\t"                                                                      \
     "s_set_gpr_idx_off\n\t"
@@ -379,7 +377,6 @@ namespace {
 #define MCS_FA_FREELANES16S ""
 #define MCS_FA_COMMIT16S                                                                          \
     "s_mov_b32 s54, s50\n\t"                                                                     \
-    "s_mov_b64 exec, s[62:63]\n\t"                                                               \
     "v_mov_b32 v64, v72\n\t"
 #define MCS_FA_ZEROKX16S                                                                          \
     "s_mov_b32 m0, s47\n\t"                                                                      \
@@ -455,7 +452,7 @@ namespace {
     "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
     "s_cbranch_scc1 mcsfa_zero_%=\n\t"                                                            \
     MCS_FA_PICK1##W MCS_FA_FREELANES##W                                                           \
-    "s_lshl_b64 s[62:63], 1, s50\n\t" MCS_FA_PICK2##W                                             \
+    "s_lshl_b64 exec, 1, s50\n\t" /* the commit runs under exec = the fitting lane */ MCS_FA_PICK2##W \
     MCS_FA_COMMIT##W                                                                              \
     /* running-slot insert: lowest lane with a free row (none: exec empty), its lowest row */     \
     "s_ff1_i32_b64 s85, s[60:61]\n\t"                                                             \
@@ -465,18 +462,22 @@ namespace {
     "s_mov_b64 exec, -1\n\t"                                                                      \
     "s_mov_b32 m0, s47\n\t"                                                                       \
     "s_add_u32 s80, s80, 1\n\t"                                                                   \
-    "s_max_u32 s81, s81, s80\n\t"                                                                 \
     "v_writelane_b32 v91, s54, m0\n\t"                                                            \
     "v_writelane_b32 v92, s40, m0\n"                                                              \
     /* next ready job; a WaitQueue head placed sleeps 1 s (:250) */                               \
     "mcsfa_placed_%=:\n\t"                                                                        \
     "s_add_u32 s47, s47, 1\n\t"                                                                   \
-    "s_cmp_lg_u32 s43, 0\n\t" MCS_FA_REC##W                                                       \
-    "s_cbranch_scc1 mcsfa_hwadv_%=\n"                                                             \
+ MCS_FA_REC##W                                                                                   \
     "mcsfa_loopend_%=:\n\t"                                                                       \
     "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
     "s_cbranch_scc1 mcsfa_inner_%=\n\t"                                                           \
-    "s_branch mcsfa_bend_%=\n"                                                                    \
+    /* the pass bound ends here after a placed WaitQueue head (s41 = its cursor + 1 while one */  \
+    /* waits): it sleeps 1 s (:250) with the batch bound restored */                             \
+    "s_cmp_lg_u32 s43, 0\n\t"                                                                     \
+    "s_cbranch_scc0 mcsfa_bend_%=\n\t"                                                            \
+    "s_sub_u32 s41, s42, s57\n\t"                                                                 \
+    "s_min_u32 s41, s41, 64\n\t"                                                                  \
+    "s_branch mcsfa_hwadv_%=\n"                                                                   \
                                                                                                   \
     /* zero-duration job: committed and released before the next decision (D3) */               \
     "mcsfa_zero_%=:\n\t" MCS_FA_ZEROKX##W                                                        \
@@ -494,6 +495,7 @@ namespace {
     "s_sub_u32 s76, 1, s43\n\t"                                                                   \
     "s_add_u32 s82, s82, s76\n\t"                                                                 \
     "s_mov_b32 s43, 1\n\t"                                                                        \
+    "s_add_u32 s41, s47, 1\n\t" /* the passes stop right after this head is placed */             \
     "s_add_u32 s83, s83, 1\n\t"                                                                   \
     "s_cmp_eq_u32 s77, -1\n\t"                                                                    \
     "s_cbranch_scc1 mcsfa_deadlock_%=\n\t"                                                        \
@@ -516,6 +518,7 @@ namespace {
     "s_cbranch_scc1 mcsfa_loopend_%=\n\t"                                                         \
     /* release every running job with finish <= t (cluster.go:153-157) */                        \
     "s_add_u32 s84, s84, 1\n\t"                                                                   \
+    "s_max_u32 s81, s81, s80\n\t" /* peak: used only grows between releases */                   \
     "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN##W                                                   \
     /* the wave's earliest remaining finish (DPP minimum of v90) under the reload's latency */   \
     "v_mov_b32 v120, v90\n\t"                                                                     \
@@ -548,6 +551,7 @@ namespace {
                                                                                                   \
     /* ---- batch end: store the 64 results, take the prefetched records, prefetch the next ---- */ \
     "mcsfa_bend_%=:\n\t"                                                                          \
+    "s_max_u32 s81, s81, s80\n\t"                                                                 \
     "s_cmp_gt_u32 s81, " MCS_FA_POOLMAX##W "\n\t"                                                 \
     "s_cbranch_scc1 mcsfa_poolovf_%=\n\t"                                                         \
     "s_add_u32 s76, s57, s47\n\t"                                                                 \
@@ -579,7 +583,7 @@ namespace {
     "s_mov_b32 %[flags], s44\n\t"                                                                 \
     "s_mov_b32 %[hw], s43\n\t"                                                                    \
     "s_mov_b32 %[used], s80\n\t"                                                                  \
-    "s_mov_b32 %[peak], s81\n\t"                                                                  \
+    "s_max_u32 %[peak], s81, s80\n\t"                                                             \
     "s_mov_b32 %[waited], s82\n\t"                                                                \
     "s_mov_b32 %[nslow], s83\n\t"                                                                 \
     "s_mov_b32 %[nrel], s84\n\t"                                                                  \
