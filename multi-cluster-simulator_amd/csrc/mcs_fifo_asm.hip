@@ -327,6 +327,40 @@ namespace {
     "v_lshl_or_b32 v96, v97, 16, v96\n\t"
 
 // ---- per-form hooks of the loop -----------------------------------------------------------------
+// a decided placement: the fitting lane's chunk, the commit under exec = that lane, then the
+// running-slot insert under exec = the lowest lane with a free row (none: exec empty)
+#define MCS_FA_DECIDE_(W)                                                                         \
+    MCS_FA_PICK1##W MCS_FA_FREELANES##W                                                           \
+    "s_lshl_b64 exec, 1, s50\n\t" MCS_FA_PICK2##W MCS_FA_COMMIT##W                                \
+    "s_ff1_i32_b64 s85, s[60:61]\n\t"                                                             \
+    "s_lshl_b64 s[62:63], 1, s85\n\t"                                                             \
+    "s_and_b64 exec, s[62:63], s[60:61]\n\t" MCS_FA_INSERT##W
+#define MCS_FA_DECIDE32 MCS_FA_DECIDE_(32)
+#define MCS_FA_DECIDE16 MCS_FA_DECIDE_(16)
+#define MCS_FA_DECIDE16S MCS_FA_DECIDE_(16S)
+// W16R: ONE register-index region for both moves (the commit's chunk, then the insert's row by
+// s_set_gpr_idx_idx); the insert lane and its row are found before it (VALU reads inside the
+// region would be indexed), the row is taken after it
+#define MCS_FA_DECIDE16R                                                                          \
+    "v_readlane_b32 s51, v86, s50\n\t"                                                            \
+    "s_ff1_i32_b64 s85, s[60:61]\n\t"                                                             \
+    "s_lshl_b64 exec, 1, s50\n\t"                                                                 \
+    "v_readlane_b32 s86, v117, s85\n\t" /* 0-7, or 8 with exec empty: in range either way */    \
+    "s_ff1_i32_b32 s52, s51\n\t"                                                                  \
+    "s_lshr_b32 s53, s52, 3\n\t"                                                                  \
+    "s_lshl3_add_u32 s54, s52, s50\n\t"                                                           \
+    "s_set_gpr_idx_on s53, gpr_idx(SRC0,DST)\n\t"                                                 \
+    "v_mov_b32 v64, v72\n\t" /* the commit (cluster.go:146-147) */                                \
+    "s_lshl_b64 s[62:63], 1, s85\n\t"                                                             \
+    "s_and_b64 exec, s[62:63], s[60:61]\n\t"                                                      \
+    "s_lshl2_add_u32 s87, s54, s73\n\t"                                                           \
+    "s_set_gpr_idx_idx s86\n\t"                                                                   \
+    "v_mov_b32 v32, s55\n\t" /* the slot: finish, payload, node address (SGPR sources) */        \
+    "v_mov_b32 v40, s48\n\t"                                                                      \
+    "v_mov_b32 v48, s87\n\t"                                                                      \
+    "s_set_gpr_idx_off\n\t"                                                                       \
+    "s_lshl_b32 s76, 1, s86\n\t"                                                                  \
+    "v_xor_b32 v89, s76, v89\n\t" /* the row is taken */
 // lanes with a fit into vcc
 #define MCS_FA_ANYFIT "v_cmp_ne_u32_e32 vcc, 0, v86\n\t"
 #define MCS_FA_ANYFIT32 MCS_FA_ANYFIT
@@ -451,13 +485,7 @@ namespace {
     "s_ff1_i32_b64 s50, vcc\n\t" /* lowest lane with a fit */                                     \
     "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
     "s_cbranch_scc1 mcsfa_zero_%=\n\t"                                                            \
-    MCS_FA_PICK1##W MCS_FA_FREELANES##W                                                           \
-    "s_lshl_b64 exec, 1, s50\n\t" /* the commit runs under exec = the fitting lane */ MCS_FA_PICK2##W \
-    MCS_FA_COMMIT##W                                                                              \
-    /* running-slot insert: lowest lane with a free row (none: exec empty), its lowest row */     \
-    "s_ff1_i32_b64 s85, s[60:61]\n\t"                                                             \
-    "s_lshl_b64 s[62:63], 1, s85\n\t"                                                             \
-    "s_and_b64 exec, s[62:63], s[60:61]\n\t" MCS_FA_INSERT##W                                     \
+    MCS_FA_DECIDE##W                                                                              \
     "s_min_u32 s77, s77, s55\n\t" /* the wave's earliest finish */                                \
     "s_mov_b64 exec, -1\n\t"                                                                      \
     "s_mov_b32 m0, s47\n\t"                                                                       \
