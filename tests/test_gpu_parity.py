@@ -265,6 +265,25 @@ def test_slot_pool_escalation():
     eng.close()
 
 
+def test_slot_pool_escalation_from_hand_scheduled_loop():
+    """More than 512 jobs running at once on a 200-node cluster: the hand-scheduled loop (8 slot rows)
+    reports the overflow, the engine re-runs the cluster with a doubled pool on the compiled kernel,
+    and the result is still bit-exact."""
+    eng = Engine(0)
+    arrays = replicate(uniform_cluster(200), 2)
+    n = 1500
+    a = np.repeat(np.arange(n // 5, dtype=np.uint32), 5)[:n]
+    d = np.full(n, 700, np.uint32)
+    c = np.zeros(n, np.uint32)
+    m = np.ones(n, np.uint32)
+    s = JobStreams(np.tile(a, 2), np.tile(d, 2), np.tile(c, 2), np.tile(m, 2), np.arange(3, dtype=np.uint64) * n)
+    node, start, fin, st, cs = run_engine(eng, arrays, s)
+    assert st.escalations >= 1 and st.slot_pool > 8
+    assert (cs["peak_running"] > 512).all()
+    assert_parity(arrays, s, node, start, fin, cs)
+    eng.close()
+
+
 def test_extreme_values(engine):
     """uint32 needs and capacities near 2^32: comparisons are unsigned and exact."""
     big = 0xFFFFFFF0
