@@ -264,16 +264,16 @@ namespace {
     "v_mov_b32 v48, s87\n\t"                                                                     \
     "s_set_gpr_idx_off\n\t"                                                                      \
     "v_xor_b32 v89, s76, v89\n\t" /* the row is taken */
-#define MCS_FR_ROW(p, MASK, F, P, A)                                                                       \
-    "s_cmp_lg_u64 " MASK ", 0\n\t"                                                               \
+// (exec = the row's expiry mask, SCC = any: no separate test, and exec is restored to the full
+// wave once after the last row)
+#define MCS_FR_ROW(p, MASK, F, P, A)                                                              \
+    "s_and_b64 exec, " MASK ", -1\n\t"                                                           \
     "s_cbranch_scc0 mcsfa_r" #p "_%=\n\t"                                                        \
     "s_bcnt1_i32_b64 s76, " MASK "\n\t"                                                          \
-    "s_mov_b64 exec, " MASK "\n\t"                                                               \
     "ds_add_u32 " A ", " P "\n\t"                                                               \
     "v_mov_b32 " F ", -1\n\t"                                                                    \
     "s_add_u32 s75, s75, s76\n\t"                                                                \
-    "v_or_b32 v89, 1<<" #p ", v89\n\t"                                                          \
-    "s_mov_b64 exec, -1\n"                                                                       \
+    "v_or_b32 v89, 1<<" #p ", v89\n"                                                             \
     "mcsfa_r" #p "_%=:\n\t"
 #define MCS_FA_SCAN16R                                                                            \
     /* the LDS node copy is refreshed from the registers first (commits do not touch it) */       \
@@ -294,6 +294,7 @@ namespace {
     MCS_FR_ROW(2, "s[54:55]", "v34", "v42", "v50") MCS_FR_ROW(3, "s[60:61]", "v35", "v43", "v51")  \
     MCS_FR_ROW(4, "s[62:63]", "v36", "v44", "v52") MCS_FR_ROW(5, "s[86:87]", "v37", "v45", "v53")  \
     MCS_FR_ROW(6, "s[88:89]", "v38", "v46", "v54") MCS_FR_ROW(7, "s[90:91]", "v39", "v47", "v55")  \
+    "s_mov_b64 exec, -1\n\t"                                                                     \
     "s_sub_u32 s80, s80, s75\n\t" MCS_FA_RELOAD16                                               \
     /* the lane's earliest remaining finish (released rows now hold -1) */                     \
     "v_min3_u32 v90, v32, v33, v34\n\t"                                                          \
@@ -431,6 +432,7 @@ namespace {
     "v_cmp_ge_u32_e64 s[50:51], s40, v32\n\t"                                                    \
     "v_cmp_ge_u32_e64 s[52:53], s40, v33\n\t"                                                    \
     MCS_FR_ROW(0, "s[50:51]", "v32", "v40", "v48") MCS_FR_ROW(1, "s[52:53]", "v33", "v41", "v49")  \
+    "s_mov_b64 exec, -1\n\t"                                                                     \
     "s_sub_u32 s80, s80, s75\n\t" MCS_FA_RELOAD16S                                              \
     "v_min_u32 v90, v32, v33\n\t"
 
