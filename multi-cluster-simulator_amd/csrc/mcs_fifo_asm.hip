@@ -56,8 +56,8 @@ namespace {
 //   s[54:55] kx, finish   s56 next clock   s57 cb   s[60:61] lanes with a free row
 //   s[62:63] one-lane exec masks   s[64:65] jobs  s[66:67] out_node  s[68:69] out_start
 //   s[70:71] out_finish  s72/s73 perm selectors   s74 t + 1  s75 expired  s76 tmp
-//   s77 next completion  s78/s79 clock advances / bound 4J + 256 (a runaway loop ends as a pool
-//   overflow: the engine re-runs the cluster on the compiled kernel)   s80 used  s81 peak
+//   s77 the wave's earliest finish  s78/s79 failed fits / bound 4J + 256 (a runaway loop ends as a
+//   pool overflow: the engine re-runs the cluster on the compiled kernel)   s80 used  s81 peak
 //   s82 waited  s83 passes without a decision  s84 release scans  s85 insert lane
 //   release: row expiry masks in s[50:55], s[60:63], s[86:91]
 //   v[64:71] nodes (W32: pairs {C, M} per chunk; W16: v64-v67)   v[72:79] fit-test differences
@@ -515,9 +515,11 @@ namespace {
     "v_writelane_b32 v92, s40, m0\n\t"                                                            \
     "s_branch mcsfa_placed_%=\n"                                                                  \
                                                                                                   \
+    /* (the clock moves by t + 1 here and on a failed fit: the carry is the u32 clock's overflow) */ \
     "mcsfa_hwadv_%=:\n\t"                                                                         \
     "s_mov_b32 s43, 0\n\t"                                                                        \
-    "s_add_u32 s56, s40, 1\n\t"                                                                   \
+    "s_add_u32 s40, s40, 1\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_clkovf_%=\n\t"                                                          \
     "s_branch mcsfa_adv_%=\n"                                                                     \
                                                                                                   \
     /* no node fits: WaitQueue append (:264-268), sleep to the next completion (A.3) */          \
@@ -527,23 +529,23 @@ namespace {
     "s_mov_b32 s43, 1\n\t"                                                                        \
     "s_add_u32 s41, s47, 1\n\t" /* the passes stop right after this head is placed */             \
     "s_add_u32 s83, s83, 1\n\t"                                                                   \
+    /* runaway guard: every advance moves the clock forward and a loop without decisions goes */  \
+    /* through here; at most 2 failed fits per job (one per arrival, one per completion) */      \
+    "s_add_u32 s78, s78, 1\n\t"                                                                   \
+    "s_cmp_gt_u32 s78, s79\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_poolovf_%=\n\t"                                                         \
     "s_cmp_eq_u32 s77, -1\n\t"                                                                    \
     "s_cbranch_scc1 mcsfa_deadlock_%=\n\t"                                                        \
-    "s_add_u32 s56, s40, 1\n\t"                                                                   \
-    "s_max_u32 s56, s56, s77\n\t"                                                                 \
+    "s_add_u32 s40, s40, 1\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_clkovf_%=\n\t"                                                          \
+    "s_max_u32 s40, s40, s77\n\t" /* (every running job finishes after t: no wrap) */           \
     "s_branch mcsfa_adv_%=\n"                                                                     \
                                                                                                   \
     "mcsfa_arrive_%=:\n\t"                                                                        \
-    "s_mov_b32 s56, s45\n\t"                                                                      \
+    "s_mov_b32 s40, s45\n\t" /* (> t) */                                                         \
     "s_add_u32 s83, s83, 1\n"                                                                     \
-    /* advance the clock to s56: releases at the new instant (A.2 step 1) */                     \
+    /* the clock has advanced: releases at the new instant (A.2 step 1) */                       \
     "mcsfa_adv_%=:\n\t"                                                                           \
-    "s_add_u32 s78, s78, 1\n\t" /* runaway guard: at most 3 advances per job (arrival, */         \
-    "s_cmp_gt_u32 s78, s79\n\t" /* a completion that frees >= 1 job, a placed wait head) */       \
-    "s_cbranch_scc1 mcsfa_poolovf_%=\n\t"                                                         \
-    "s_cmp_lt_u32 s56, s40\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfa_clkovf_%=\n\t"                                                          \
-    "s_mov_b32 s40, s56\n\t"                                                                      \
     "s_cmp_lt_u32 s40, s77\n\t" /* nothing finishes by t: no release */                          \
     "s_cbranch_scc1 mcsfa_loopend_%=\n\t"                                                         \
     /* release every running job with finish <= t (cluster.go:153-157) */                        \
@@ -573,6 +575,7 @@ namespace {
     "s_or_b32 s44, s44, %[fdl]\n\t"                                                               \
     "s_branch mcsfa_exit_%=\n"                                                                    \
     "mcsfa_clkovf_%=:\n\t"                                                                        \
+    "s_mov_b32 s40, -1\n\t" /* the clock stays at the last second it reached */                   \
     "s_or_b32 s44, s44, %[fck]\n\t"                                                               \
     "s_branch mcsfa_exit_%=\n"                                                                    \
     "mcsfa_poolovf_%=:\n\t"                                                                       \
