@@ -247,6 +247,37 @@ def test_heterogeneous_cluster_sizes(engine):
     assert cs[0]["flags"] & L.MCS_FLAG_DEADLOCK  # zero nodes: the first job never fits
 
 
+@pytest.mark.parametrize("sizes", [[0, 1, 5, 63, 64, 65, 130, 200, 256], [0, 1, 2, 5, 33, 63, 64]],
+                         ids=["asm_4x8", "asm_1x2"])
+def test_heterogeneous_cluster_sizes_hand_scheduled(engine, sizes):
+    """Clusters of many sizes in one launch of each hand-scheduled loop shape (the largest picks it:
+    129-256 nodes -> 4 chunks x 8 slot rows, <= 64 nodes -> 1 chunk x 2 rows): padding nodes, an
+    empty cluster (its first job deadlocks), partial JSON availability, zero-duration jobs."""
+    from mcs_amd.engine import gen_cluster_host
+
+    rng = np.random.default_rng(len(sizes))
+    clusters, parts = [], []
+    J = 2500
+    for i, nn in enumerate(sizes):
+        cl = uniform_cluster(nn, cores=int(rng.integers(4, 64)), memory=int(rng.integers(1000, 30000)))
+        for nd in cl.Nodes:  # partial JSON availability (KAT5 rule)
+            nd.CoresAvailable = int(rng.integers(0, nd.Cores + 1))
+        clusters.append(cl)
+        mc = max([nd.Cores for nd in cl.Nodes], default=8)
+        mm = max([nd.Memory for nd in cl.Nodes], default=1000)
+        a, d, c, m = gen_cluster_host(GenParams(seed=91 + i, arrival_mode=1, lam=0.02 * max(nn, 1) + 0.2), i, mc, mm, J)
+        d = d.copy()
+        d[rng.random(J) < 0.03] = 0  # zero-duration jobs (D3)
+        parts.append((a, d, c, m))
+    arrays = pack_clusters(clusters)
+    off = np.arange(len(parts) + 1, dtype=np.uint64) * J
+    s = JobStreams(*(np.concatenate([p[f] for p in parts]) for f in range(4)), off)
+    node, start, fin, st, cs = run_engine(engine, arrays, s)
+    assert engine.last_kernel.startswith("mcs::fifo_asm_kernel<16, true")
+    assert_parity(arrays, s, node, start, fin, cs)
+    assert cs[0]["flags"] & L.MCS_FLAG_DEADLOCK  # zero nodes: the first job never fits
+
+
 def test_slot_pool_escalation():
     """Force the smallest pool (128 slots) with >128 concurrently running jobs: the engine must
     detect the overflow, re-run those clusters with a larger pool, and still be bit-exact."""
