@@ -513,7 +513,14 @@ def main_batch(args, world, rank, local_rank):
 
     elapsed_max, placed_all = aggregate(elapsed, placed, device=dev)
     kernel_name = eng.last_kernel  # the placement kernel these timings belong to
-    cs = eng.cluster_stats()  # outside the timed region: per-cluster decision-loop diagnostics
+    # outside the timed region: per-cluster decision-loop diagnostics, from one more run of the
+    # counting build (the hand-scheduled loop skips its pass / release counters otherwise)
+    os.environ["MCS_FIFO_DIAG"] = "1"
+    try:
+        eng.run()
+    finally:
+        os.environ.pop("MCS_FIFO_DIAG", None)
+    cs = eng.cluster_stats()
     diag = {
         "loop_passes_per_job": float(cs["iterations"].sum()) / max(n_jobs, 1),
         "release_scans_per_job": float(cs["release_scans"].sum()) / max(n_jobs, 1),

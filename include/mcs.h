@@ -162,8 +162,9 @@ typedef struct mcs_cluster_stats {
     uint32_t peak_running;  /* peak jobs holding resources (dur > 0)                              */
     uint32_t flags;         /* MCS_FLAG_*                                                         */
     uint32_t pool;          /* slot pool (x64) the final result was produced with                */
-    uint32_t iterations;    /* diagnostics: decision-loop passes                                  */
-    uint32_t release_scans; /* diagnostics: clock advances that released running jobs            */
+    uint32_t iterations;    /* diagnostics: decision-loop passes (the hand-scheduled loop counts the
+                               passes without a decision only with MCS_FIFO_DIAG=1 in the env)     */
+    uint32_t release_scans; /* diagnostics: clock advances that released running jobs (ditto)    */
 } mcs_cluster_stats;
 
 /* DELAY-policy statistics of one cluster (MCS_POLICY_DELAY runs; mcs_read_delay_stats). */

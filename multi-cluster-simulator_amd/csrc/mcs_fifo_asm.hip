@@ -437,7 +437,12 @@ namespace {
     "v_min_u32 v90, v32, v33\n\t"
 
 // ---- the decision loop ------------------------------------------------------------------------
-#define MCS_FA_LOOP(W)                                                                            \
+// diagnostic counters (passes without a decision, release scans): DIAG launches only
+#define MCS_FA_CNTS_D1 "s_add_u32 s83, s83, 1\n\t"
+#define MCS_FA_CNTR_D1 "s_add_u32 s84, s84, 1\n\t"
+#define MCS_FA_CNTS_D0 ""
+#define MCS_FA_CNTR_D0 ""
+#define MCS_FA_LOOP(W, D)                                                                         \
     /* ---- entry: state into the fixed registers ---- */                                        \
     "s_mov_b32 s40, %[t]\n\t"                                                                     \
     "s_mov_b32 s42, %[J]\n\t"                                                                     \
@@ -528,7 +533,7 @@ namespace {
     "s_add_u32 s82, s82, s76\n\t"                                                                 \
     "s_mov_b32 s43, 1\n\t"                                                                        \
     "s_add_u32 s41, s47, 1\n\t" /* the passes stop right after this head is placed */             \
-    "s_add_u32 s83, s83, 1\n\t"                                                                   \
+    MCS_FA_CNTS_##D                                                                               \
     /* runaway guard: every advance moves the clock forward and a loop without decisions goes */  \
     /* through here; at most 2 failed fits per job (one per arrival, one per completion) */      \
     "s_add_u32 s78, s78, 1\n\t"                                                                   \
@@ -543,13 +548,13 @@ namespace {
                                                                                                   \
     "mcsfa_arrive_%=:\n\t"                                                                        \
     "s_mov_b32 s40, s45\n\t" /* (> t) */                                                         \
-    "s_add_u32 s83, s83, 1\n"                                                                     \
+    MCS_FA_CNTS_##D "\n"                                                                          \
     /* the clock has advanced: releases at the new instant (A.2 step 1) */                       \
     "mcsfa_adv_%=:\n\t"                                                                           \
     "s_cmp_lt_u32 s40, s77\n\t" /* nothing finishes by t: no release */                          \
     "s_cbranch_scc1 mcsfa_loopend_%=\n\t"                                                         \
     /* release every running job with finish <= t (cluster.go:153-157) */                        \
-    "s_add_u32 s84, s84, 1\n\t"                                                                   \
+    MCS_FA_CNTR_##D                                                                               \
     "s_max_u32 s81, s81, s80\n\t" /* peak: used only grows between releases */                   \
     "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN##W                                                   \
     /* the wave's earliest remaining finish (DPP minimum of v90) under the reload's latency */   \
@@ -632,7 +637,9 @@ namespace {
 // [8][64] at 6144 (the offsets in the asm)
 // (RS: the W16R form, running slots in registers; the LDS slot arrays are then unused)
 // (NPL nodes per lane, P slot rows: 4/8 for 129-256 node clusters, 1/2 for at most 64 nodes)
-template <int W, bool RS, int NPL, int P>
+// (DIAG: count the passes without a decision and the release scans into mcs_cluster_stats; the
+// production launches skip them, 1.6 % of the C4 loop)
+template <int W, bool RS, int NPL, int P, bool DIAG>
 __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
     static_assert(W == 16 || !RS, "register slots: 16-bit node format only");
     static_assert((NPL == 4 && P == 8) || (NPL == 1 && P == 2 && W == 16 && RS), "loop shapes");
@@ -707,13 +714,17 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
       [fov] "i"(MCS_FLAG_OVERFLOW)                                                              \
     : MCS_FA_CLOBBERS
     if constexpr (W == 32)
-        asm volatile(MCS_FA_LOOP(32) MCS_FA_OPERANDS);
+        if constexpr (DIAG) asm volatile(MCS_FA_LOOP(32, D1) MCS_FA_OPERANDS);
+        else asm volatile(MCS_FA_LOOP(32, D0) MCS_FA_OPERANDS);
     else if constexpr (NPL == 1)
-        asm volatile(MCS_FA_LOOP(16S) MCS_FA_OPERANDS);
+        if constexpr (DIAG) asm volatile(MCS_FA_LOOP(16S, D1) MCS_FA_OPERANDS);
+        else asm volatile(MCS_FA_LOOP(16S, D0) MCS_FA_OPERANDS);
     else if constexpr (RS)
-        asm volatile(MCS_FA_LOOP(16R) MCS_FA_OPERANDS);
+        if constexpr (DIAG) asm volatile(MCS_FA_LOOP(16R, D1) MCS_FA_OPERANDS);
+        else asm volatile(MCS_FA_LOOP(16R, D0) MCS_FA_OPERANDS);
     else
-        asm volatile(MCS_FA_LOOP(16) MCS_FA_OPERANDS);
+        if constexpr (DIAG) asm volatile(MCS_FA_LOOP(16, D1) MCS_FA_OPERANDS);
+        else asm volatile(MCS_FA_LOOP(16, D0) MCS_FA_OPERANDS);
 #undef MCS_FA_OPERANDS
 #pragma clang diagnostic pop
 
@@ -783,15 +794,24 @@ bool fifo_asm_eligible(const FifoArgs& a, int npl, int pool, bool hor) {
     return fifo_asm_form(a, npl, pool, hor) != 0;
 }
 
-hipError_t launch_fifo_asm(const FifoArgs& a, int npl, int pool, hipStream_t s) {
-    switch (fifo_asm_form(a, npl, pool, false)) {
-        case 18: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 1, 2>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
-        case 17: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 4, 8>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
-        case 16: hipLaunchKernelGGL((fifo_asm_kernel<16, false, 4, 8>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
-        case 32: hipLaunchKernelGGL((fifo_asm_kernel<32, false, 4, 8>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
+template <bool DIAG>
+static hipError_t launch_form(const FifoArgs& a, int form, hipStream_t s) {
+    switch (form) {
+        case 18: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 1, 2, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
+        case 17: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
+        case 16: hipLaunchKernelGGL((fifo_asm_kernel<16, false, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
+        case 32: hipLaunchKernelGGL((fifo_asm_kernel<32, false, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+// MCS_FIFO_DIAG=1: the counting build (mcs_cluster_stats.iterations / release_scans); otherwise
+// those two fields hold the decisions and 0
+hipError_t launch_fifo_asm(const FifoArgs& a, int npl, int pool, hipStream_t s) {
+    const int form = fifo_asm_form(a, npl, pool, false);
+    const char* env = getenv("MCS_FIFO_DIAG");
+    return env && atoi(env) != 0 ? launch_form<true>(a, form, s) : launch_form<false>(a, form, s);
 }
 
 }  // namespace mcs

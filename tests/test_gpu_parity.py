@@ -278,6 +278,31 @@ def test_heterogeneous_cluster_sizes_hand_scheduled(engine, sizes):
     assert cs[0]["flags"] & L.MCS_FLAG_DEADLOCK  # zero nodes: the first job never fits
 
 
+@pytest.mark.parametrize("nodes", [256, 5])
+def test_hand_scheduled_diag_build(nodes):
+    """MCS_FIFO_DIAG=1 launches the counting build of the hand-scheduled loop: the same placements
+    and per-cluster results, plus the pass and release-scan counters (which the production build
+    leaves at the decision count and 0)."""
+    arrays, streams, _ = seeded_workload("n256" if nodes == 256 else "small", 64, 3000)
+    res = {}
+    for diag in ("0", "1"):
+        os.environ["MCS_FIFO_DIAG"] = diag
+        try:
+            with Engine(0) as eng:
+                res[diag] = run_engine(eng, arrays, streams)
+                assert eng.last_kernel.startswith("mcs::fifo_asm_kernel<16, true")
+        finally:
+            os.environ.pop("MCS_FIFO_DIAG", None)
+    for i in range(3):
+        np.testing.assert_array_equal(res["0"][i], res["1"][i])
+    c0, c1 = res["0"][4], res["1"][4]
+    for key in ("t_end", "placed", "waited", "peak_running", "flags"):
+        np.testing.assert_array_equal(c0[key], c1[key], err_msg=key)
+    assert (c0["iterations"] == c0["placed"]).all() and (c0["release_scans"] == 0).all()
+    assert (c1["iterations"] > c1["placed"]).any() and (c1["release_scans"] > 0).any()
+    assert_parity(arrays, streams, *res["1"][:3], c1)
+
+
 def test_slot_pool_escalation():
     """Force the smallest pool (128 slots) with >128 concurrently running jobs: the engine must
     detect the overflow, re-run those clusters with a larger pool, and still be bit-exact."""
