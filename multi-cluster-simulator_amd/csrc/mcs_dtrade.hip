@@ -150,9 +150,9 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
     DtCluster st = a.cl[c];
     const uint32_t NN = N + st.nv;
 
-    for (uint32_t i = lane; i < NN; i += kWave)
-        nodes[i] = i < N ? a.tn[n0 + i] : a.vn[(size_t)c * a.V + (i - N)];
-    for (uint32_t s = lane; s < S; s += kWave) sfin[s] = a.sfin[sb + s];
+    copy_rounds<4>(nodes, a.tn + n0, N, lane);
+    copy_rounds<2>(nodes + N, a.vn + (size_t)c * a.V, NN - N, lane);
+    copy_rounds<8>(sfin, a.sfin + sb, S, lane);
     __syncthreads();
 
     // releases due at T (cluster.go:153-157), Foreign jobs included
@@ -428,13 +428,9 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
     }
 
     __syncthreads();
-    for (uint32_t i = lane; i < NN; i += kWave) {
-        if (i < N)
-            a.tn[n0 + i] = nodes[i];
-        else
-            a.vn[(size_t)c * a.V + (i - N)] = nodes[i];
-    }
-    for (uint32_t s = lane; s < S; s += kWave) a.sfin[sb + s] = sfin[s];
+    copy_rounds<4>(a.tn + n0, nodes, N, lane);
+    copy_rounds<2>(a.vn + (size_t)c * a.V, nodes + N, NN - N, lane);
+    copy_rounds<8>(a.sfin + sb, sfin, S, lane);
     // ---- phase C: the state stream sample (trader_server.go:24-47) every sample_period seconds ----
     if (T % a.sample_period == 0u) {
         __syncthreads();  // sfin's LDS is reused for the per-node differences

@@ -94,8 +94,8 @@ __global__ __launch_bounds__(64) void tr_step_kernel(TradeArgs a) {
     const uint32_t vn = a.tr[g].vnodes;
     TrCluster st = a.cl[c];
 
-    for (uint32_t i = lane; i < N; i += kWave) nodes[i] = a.tn[n0 + i];
-    for (uint32_t s = lane; s < S; s += kWave) sfin[s] = a.sfin[sb + s];
+    copy_rounds<4>(nodes, a.tn + n0, N, lane);
+    copy_rounds<8>(sfin, a.sfin + sb, S, lane);
     __syncthreads();
 
     // releases due at T (cluster.go:153-157), before the tick's decisions
@@ -273,11 +273,9 @@ __global__ __launch_bounds__(64) void tr_step_kernel(TradeArgs a) {
         }
     }
     unsigned long long* snap = tr_snap(a, g);
-    for (uint32_t i = lane; i < N; i += kWave) {
-        a.tn[n0 + i] = nodes[i];
-        snap[i] = nodes[i];
-    }
-    for (uint32_t s = lane; s < S; s += kWave) a.sfin[sb + s] = sfin[s];
+    copy_rounds<4>(a.tn + n0, nodes, N, lane);
+    copy_rounds<4>(snap, nodes, N, lane);
+    copy_rounds<8>(a.sfin + sb, sfin, S, lane);
     if (lane == 0) {
         a.cl[c] = st;
         TrXRec x;
@@ -312,7 +310,7 @@ __global__ __launch_bounds__(64) void tr_lend_kernel(TradeArgs a) {
     const uint32_t N = xl.n;
     {  // the lender's snapshot, staged once for every request of the tick
         const unsigned long long* __restrict__ tn = tr_snap(a, L);
-        for (uint32_t i = lane; i < N; i += kWave) sn[i] = tn[i];
+        copy_rounds<4>(sn, tn, N, lane);
         __syncthreads();
     }
     uint32_t lq_len = xl.lq_len, lq_head = own ? a.cl[c].lq_head : 0u, fb = 0;

@@ -7,6 +7,28 @@
 
 namespace mcs {
 
+// Copies of n elements between HBM and LDS by one wave, U elements per lane per round with all
+// of a round's reads issued before its writes.  The plain `for (i = lane; i < n; i += 64)
+// dst[i] = src[i]` compiles to one read, one wait and one write per iteration: a serialized HBM
+// (or LDS) round trip per 64 elements, which dominated the lock-step tick kernels' staging.
+template <int U, typename T>
+__device__ __forceinline__ void copy_rounds(T* __restrict__ dst, const T* __restrict__ src, uint32_t n,
+                                            uint32_t lane) {
+    for (uint32_t b = 0; b < n; b += (uint32_t)U * kWave) {
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = b + (uint32_t)u * kWave + lane;
+            v[u] = i < n ? src[i] : T{};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = b + (uint32_t)u * kWave + lane;
+            if (i < n) dst[i] = v[u];
+        }
+    }
+}
+
 // lane mask of a >= b (unsigned): one v_cmp into a scalar register pair (a __ballot of a
 // combined bool re-materialises the mask through a VGPR)
 __device__ __forceinline__ uint64_t lanes_ge(uint32_t a, uint32_t b) {
