@@ -306,20 +306,25 @@ __global__ __launch_bounds__(64) void tr_lend_kernel(TradeArgs a) {
     const uint32_t L = blockIdx.x, lane = lane_id();
     const bool own = L / a.Cl == a.rank;
     const uint32_t c = L - a.rank * a.Cl;  // (own only)
+    // every read of the tick issued together (one round trip): the first 64 borrowers' requests
+    // (one per lane), the lender's snapshot — the whole stride, since its node count arrives only
+    // with its record — staged once for every request, and the record
+    TrRecA rl0{kEmpty, 0u, 0u, 0u};
+    if (lane < a.Ct && lane != L) rl0 = tr_xrec(a, lane)->req;  // self skipped (:176)
+    copy_rounds<4>(sn, tr_snap(a, L), a.ns, lane);
     const TrXRec xl = *tr_xrec(a, L);
     const uint32_t N = xl.n;
-    {  // the lender's snapshot, staged once for every request of the tick
-        const unsigned long long* __restrict__ tn = tr_snap(a, L);
-        copy_rounds<4>(sn, tn, N, lane);
-        __syncthreads();
-    }
+    __syncthreads();
     uint32_t lq_len = xl.lq_len, lq_head = own ? a.cl[c].lq_head : 0u, fb = 0;
     const uint32_t LQ = a.LQ;
     for (uint32_t b0 = 0; b0 < a.Ct; b0 += kWave) {
         const uint32_t bl = b0 + lane;
         // this block of 64 borrowers' requests, one per lane, broadcast per pending request
-        TrRecA rl{kEmpty, 0u, 0u, 0u};
-        if (bl < a.Ct && bl != L) rl = tr_xrec(a, bl)->req;  // self skipped (:176)
+        TrRecA rl = rl0;
+        if (b0 != 0u) {
+            rl = TrRecA{kEmpty, 0u, 0u, 0u};
+            if (bl < a.Ct && bl != L) rl = tr_xrec(a, bl)->req;  // self skipped (:176)
+        }
         unsigned long long pend = __ballot(rl.job != kEmpty);
         while (pend) {
             const uint32_t bi = (uint32_t)__builtin_ctzll(pend);
@@ -371,10 +376,13 @@ __global__ __launch_bounds__(64) void tr_lend_kernel(TradeArgs a) {
 // Phase C: cluster g of the system as borrower (the owner rank moves the job) and its clock
 // hints for the trader phase; run by one lane of the trader wave per cluster (replicated).
 __device__ __forceinline__ TrRecC post_cluster(const TradeArgs& a, uint32_t g, uint32_t T) {
+    // every input read first (one round trip): the record, the acceptance, the LentQueue length
+    // and the lender flags
     const TrXRec x = *tr_xrec(a, g);
+    const uint32_t accg = a.acc[g], lq = a.lqp[g], fbg = a.fb[g];
     const bool own = g / a.Cl == a.rank;
     uint32_t has_w = x.has_w, decided = x.decided;
-    if (x.req.job != kEmpty && a.acc[g]) {  // BorrowedQueue append, WaitQueue pop (scheduler.go:237-242)
+    if (x.req.job != kEmpty && accg) {  // BorrowedQueue append, WaitQueue pop (scheduler.go:237-242)
         has_w = 0u;
         ++decided;
         if (own) {
@@ -391,7 +399,6 @@ __device__ __forceinline__ TrRecC post_cluster(const TradeArgs& a, uint32_t g, u
         }
     }
     a.acc[g] = 0u;  // (only this lane reads it; cleared for the next tick)
-    const uint32_t lq = a.lqp[g];
     TrRecC o;
     o.cu = x.cu;
     o.mu = x.mu;
@@ -400,7 +407,7 @@ __device__ __forceinline__ TrRecC post_cluster(const TradeArgs& a, uint32_t g, u
     o.busy = (has_w || lq > 0u || x.rq_busy) ? 1u : 0u;
     o.next_arr_t = x.next_arr_t;
     o.done = (decided == x.J && lq == 0u) ? 1u : 0u;
-    o.flags = x.flags | a.fb[g];
+    o.flags = x.flags | fbg;
     return o;
 }
 
