@@ -627,7 +627,14 @@ namespace {
     "s_mov_b32 %[nrel], s84\n\t"                                                                  \
     "v_mov_b32 %[on], v91\n\t"                                                                    \
     "v_mov_b32 %[os], v92\n\t"                                                                    \
-    "v_add_u32 %[of], v92, v95\n\t"                                                              \
+    /* finish = start + duration of the batch the result registers hold: the current records', */ \
+    /* unless the run stopped at the first job of a new batch, whose previous batch was stored */  \
+    /* with its finishes already formed in v93 (tests/test_gpu_parity.py fuzz cases) */           \
+    "s_cmp_eq_u32 s47, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfa_xf_%=\n\t"                                                              \
+    "v_add_u32 v93, v92, v95\n"                                                                   \
+    "mcsfa_xf_%=:\n\t"                                                                            \
+    "v_mov_b32 %[of], v93\n\t"                                                                    \
     "v_mov_b32 %[frm], v89\n\t"                                                                   \
     "v_mov_b32 %[lmin], v90\n\t"                                                                  \
     "s_nop 1"

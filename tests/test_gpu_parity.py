@@ -303,6 +303,68 @@ def test_hand_scheduled_diag_build(nodes):
     assert_parity(arrays, streams, *res["1"][:3], c1)
 
 
+@pytest.mark.parametrize("shape", ["w16s", "w16r", "w32"])
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6])
+def test_hand_scheduled_fuzz(engine, shape, seed):
+    """Randomised clusters and streams through each hand-scheduled loop form, bit-exact against the
+    oracle: node counts across the shape's range (padding lanes and chunks), random JSON
+    availability, bursts of simultaneous arrivals, zero-duration and zero-resource jobs, requests
+    equal to a node's free value, and one request per cluster that fits no node (a head-of-line
+    deadlock at a random point of the stream)."""
+    from mcs_amd.cluster import Node
+
+    rng = np.random.default_rng(1000 * seed + {"w16s": 0, "w16r": 1, "w32": 2}[shape])
+    lo, hi = (1, 64) if shape == "w16s" else (129, 256)
+    clusters, parts = [], []
+    J = 2000
+    for k in range(160):
+        nn = int(rng.integers(lo, hi + 1)) if k else hi  # the largest picks the loop shape
+        cap_c = int(rng.integers(1, 64))
+        cap_m = int(rng.integers(1, 32000)) if shape != "w32" else int(rng.integers(40000, 1 << 30))
+        cl = Cluster(Id=k + 1, Nodes=[])
+        for i in range(nn):
+            fc = cap_c if rng.random() < 0.7 else int(rng.integers(0, cap_c + 1))
+            fm = cap_m if rng.random() < 0.7 else int(rng.integers(0, cap_m + 1))
+            cl.Nodes.append(Node(Id=i + 1, Cores=cap_c, Memory=cap_m, CoresAvailable=fc, MemoryAvailable=fm))
+        clusters.append(cl)
+        gaps = rng.poisson(rng.uniform(0.05, 2.0), J)
+        gaps[rng.random(J) < 0.05] += int(rng.integers(10, 500))  # idle stretches
+        arr = np.cumsum(gaps).astype(np.uint32)
+        dur = rng.integers(0, int(rng.integers(2, 300)), J).astype(np.uint32)
+        cores = rng.integers(0, cap_c + 1, J).astype(np.uint32)
+        mem = rng.integers(0, cap_m + 1, J).astype(np.uint32)
+        z = rng.random(J) < 0.02
+        cores[z] = 0
+        mem[z] = 0
+        if rng.random() < 0.5:  # one request that fits no node, somewhere in the stream
+            i = int(rng.integers(J // 4, J))
+            if rng.random() < 0.5:
+                cores[i] = cap_c + 1
+            else:
+                mem[i] = cap_m + 1
+        parts.append((arr, dur, cores, mem))
+    arrays = pack_clusters(clusters)
+    off = np.arange(len(parts) + 1, dtype=np.uint64) * J
+    s = JobStreams(*(np.concatenate([p[f] for p in parts]) for f in range(4)), off)
+    node, start, fin, st, cs = run_engine(engine, arrays, s)
+    want = {"w16s": "mcs::fifo_asm_kernel<16, true, 1, 2>", "w16r": "mcs::fifo_asm_kernel<16, true, 4, 8>",
+            "w32": "mcs::fifo_asm_kernel<32, false, 4, 8>"}[shape]
+    if st.escalations == 0:
+        assert engine.last_kernel == want
+    assert_parity(arrays, s, node, start, fin, cs)
+    # the compiled kernel on the same case (MCS_FIFO_ASM=0) agrees as well
+    os.environ["MCS_FIFO_ASM"] = "0"
+    try:
+        with Engine(0) as eng:
+            n2, s2, f2, _, _ = run_engine(eng, arrays, s)
+            assert eng.last_kernel == "mcs::fifo_kernel"
+    finally:
+        os.environ.pop("MCS_FIFO_ASM", None)
+    np.testing.assert_array_equal(n2, node)
+    np.testing.assert_array_equal(s2, start)
+    np.testing.assert_array_equal(f2, fin)
+
+
 def test_slot_pool_escalation():
     """Force the smallest pool (128 slots) with >128 concurrently running jobs: the engine must
     detect the overflow, re-run those clusters with a larger pool, and still be bit-exact."""
