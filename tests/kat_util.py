@@ -73,3 +73,45 @@ def seeded_workload(kind: str, n_clusters: int, jobs_per_cluster: int, seed: int
     arrays = replicate(spec, n_clusters)
     streams = gen_streams_host(gp, arrays, jobs_per_cluster)
     return arrays, streams, gp
+
+
+def fuzz_workload(shape: str, seed: int, n_clusters: int = 160, J: int = 2000):
+    """Randomised clusters and job streams (tests/test_gpu_parity.py, test_gpu_delay.py): node counts
+    across the shape's range ('w16s' <= 64 nodes, 'mid' 65-128, 'w16r' 129-256, 'w32' 129-256 with
+    memory values past 2^15), random JSON availability, bursts of simultaneous arrivals and idle
+    stretches, zero-duration and zero-resource jobs, requests up to a node's capacity, and in half
+    the clusters one request that fits no node at a random point of the stream."""
+    from mcs_amd import JobStreams, pack_clusters
+    from mcs_amd.cluster import Node
+
+    rng = np.random.default_rng(1000 * seed + {"w16s": 0, "w16r": 1, "w32": 2, "mid": 3}[shape])
+    lo, hi = {"w16s": (1, 64), "mid": (65, 128)}.get(shape, (129, 256))
+    clusters, parts = [], []
+    for k in range(n_clusters):
+        nn = int(rng.integers(lo, hi + 1)) if k else hi  # the largest picks the kernel shape
+        cap_c = int(rng.integers(1, 64))
+        cap_m = int(rng.integers(1, 32000)) if shape != "w32" else int(rng.integers(40000, 1 << 30))
+        cl = Cluster(Id=k + 1, Nodes=[])
+        for i in range(nn):
+            fc = cap_c if rng.random() < 0.7 else int(rng.integers(0, cap_c + 1))
+            fm = cap_m if rng.random() < 0.7 else int(rng.integers(0, cap_m + 1))
+            cl.Nodes.append(Node(Id=i + 1, Cores=cap_c, Memory=cap_m, CoresAvailable=fc, MemoryAvailable=fm))
+        clusters.append(cl)
+        gaps = rng.poisson(rng.uniform(0.05, 2.0), J)
+        gaps[rng.random(J) < 0.05] += int(rng.integers(10, 500))  # idle stretches
+        arr = np.cumsum(gaps).astype(np.uint32)
+        dur = rng.integers(0, int(rng.integers(2, 300)), J).astype(np.uint32)
+        cores = rng.integers(0, cap_c + 1, J).astype(np.uint32)
+        mem = rng.integers(0, cap_m + 1, J).astype(np.uint32)
+        z = rng.random(J) < 0.02
+        cores[z] = 0
+        mem[z] = 0
+        if rng.random() < 0.5:  # one request that fits no node, somewhere in the stream
+            i = int(rng.integers(J // 4, J))
+            if rng.random() < 0.5:
+                cores[i] = cap_c + 1
+            else:
+                mem[i] = cap_m + 1
+        parts.append((arr, dur, cores, mem))
+    off = np.arange(len(parts) + 1, dtype=np.uint64) * J
+    return pack_clusters(clusters), JobStreams(*(np.concatenate([p[f] for p in parts]) for f in range(4)), off)

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle_ref as O
-from kat_util import GOLDEN, kat_cluster, kat_expect, kat_streams, seeded_workload
+from kat_util import GOLDEN, fuzz_workload, kat_cluster, kat_expect, kat_streams, seeded_workload
 from mcs_amd import Engine, JobStreams, pack_clusters, replicate, uniform_cluster
 from mcs_amd import _lib as L
 
@@ -130,3 +130,13 @@ def test_scheduler_mirror_delay():
     pl = s.Delay([j[1] for j in k["jobs"]], jobs)
     assert [(p.Node, p.Start, p.Finish) for p in pl] == [tuple(k["expect"][str(j[0])]) for j in k["jobs"]]
     assert s.WaitTime.GetAverage() == 101000 / 8
+
+
+@pytest.mark.parametrize("shape", ["w16s", "mid", "w16r", "w32"])
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_gpu_delay_fuzz(delay_engine, shape, seed):
+    """The randomised workloads of the FIFO fuzz cases (kat_util.fuzz_workload) under DELAY: Level1
+    moves and passes, the D6 skip, WaitTime sums and never-fitting Level1 jobs, bit-exact."""
+    arrays, s = fuzz_workload(shape, seed, n_clusters=96, J=1500)
+    node, start, fin, st, cs, ds = run(delay_engine, arrays, s)
+    assert_delay_parity(arrays, s, node, start, fin, cs, ds)

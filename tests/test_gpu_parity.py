@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle_ref as O
-from kat_util import kat_cluster, kat_expect, kat_streams, load_kats, seeded_workload
+from kat_util import fuzz_workload, kat_cluster, kat_expect, kat_streams, load_kats, seeded_workload
 from mcs_amd import (CLUSTER_STATS_DTYPE, Cluster, Engine, GenParams, JobStreams, pack_clusters, replicate,
                      uniform_cluster)
 from mcs_amd import _lib as L
@@ -311,41 +311,7 @@ def test_hand_scheduled_fuzz(engine, shape, seed):
     availability, bursts of simultaneous arrivals, zero-duration and zero-resource jobs, requests
     equal to a node's free value, and one request per cluster that fits no node (a head-of-line
     deadlock at a random point of the stream)."""
-    from mcs_amd.cluster import Node
-
-    rng = np.random.default_rng(1000 * seed + {"w16s": 0, "w16r": 1, "w32": 2}[shape])
-    lo, hi = (1, 64) if shape == "w16s" else (129, 256)
-    clusters, parts = [], []
-    J = 2000
-    for k in range(160):
-        nn = int(rng.integers(lo, hi + 1)) if k else hi  # the largest picks the loop shape
-        cap_c = int(rng.integers(1, 64))
-        cap_m = int(rng.integers(1, 32000)) if shape != "w32" else int(rng.integers(40000, 1 << 30))
-        cl = Cluster(Id=k + 1, Nodes=[])
-        for i in range(nn):
-            fc = cap_c if rng.random() < 0.7 else int(rng.integers(0, cap_c + 1))
-            fm = cap_m if rng.random() < 0.7 else int(rng.integers(0, cap_m + 1))
-            cl.Nodes.append(Node(Id=i + 1, Cores=cap_c, Memory=cap_m, CoresAvailable=fc, MemoryAvailable=fm))
-        clusters.append(cl)
-        gaps = rng.poisson(rng.uniform(0.05, 2.0), J)
-        gaps[rng.random(J) < 0.05] += int(rng.integers(10, 500))  # idle stretches
-        arr = np.cumsum(gaps).astype(np.uint32)
-        dur = rng.integers(0, int(rng.integers(2, 300)), J).astype(np.uint32)
-        cores = rng.integers(0, cap_c + 1, J).astype(np.uint32)
-        mem = rng.integers(0, cap_m + 1, J).astype(np.uint32)
-        z = rng.random(J) < 0.02
-        cores[z] = 0
-        mem[z] = 0
-        if rng.random() < 0.5:  # one request that fits no node, somewhere in the stream
-            i = int(rng.integers(J // 4, J))
-            if rng.random() < 0.5:
-                cores[i] = cap_c + 1
-            else:
-                mem[i] = cap_m + 1
-        parts.append((arr, dur, cores, mem))
-    arrays = pack_clusters(clusters)
-    off = np.arange(len(parts) + 1, dtype=np.uint64) * J
-    s = JobStreams(*(np.concatenate([p[f] for p in parts]) for f in range(4)), off)
+    arrays, s = fuzz_workload(shape, seed)
     node, start, fin, st, cs = run_engine(engine, arrays, s)
     want = {"w16s": "mcs::fifo_asm_kernel<16, true, 1, 2>", "w16r": "mcs::fifo_asm_kernel<16, true, 4, 8>",
             "w32": "mcs::fifo_asm_kernel<32, false, 4, 8>"}[shape]
