@@ -67,6 +67,10 @@ __device__ __forceinline__ uint64_t ld_l2(const uint64_t* p) {
 // t < a.on.t_hor, save.  A cluster with nothing queued parks without advancing its clock (the
 // iteration is idempotent when re-run); only a drain (t_hor = kEmpty) ends a run the way the
 // one-shot kernel does.
+// online sessions: the run's final iteration (t + 1 after the last placement) has been taken; kept
+// in the saved state's flags only (a drain must take it once, whichever horizon placed the job)
+constexpr uint32_t kOnEnded = 0x80000000u;
+
 template <int NPL, int P, bool GEN, bool HOR>
 __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     static_assert(P <= 32, "free-row mask is one u32 per lane");
@@ -168,8 +172,19 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
             if (lane == 0) wacc = st.wsum;
         }
         // nothing to do: a clock overflow is final, the horizon may be reached, and a cluster
-        // with nothing queued keeps its clock (a drain does not advance it again)
+        // with nothing queued keeps its clock — except that a drain ends a run whose last job was
+        // placed in an earlier (non-drain) horizon with the batch run's final iteration (t + 1,
+        // below), once (kOnEnded in the saved flags)
+        if ((flags & kOnEnded) && h < J) {  // jobs appended after that: the run had not ended
+            t = t - 1u;
+            flags &= ~kOnEnded;
+        }
         live = !(flags & MCS_FLAG_CLOCK_OVERFLOW) && t < a.on.t_hor && (h < J || l1n != 0u);
+        if (st.valid && !live && a.on.t_hor == kEmpty && h >= J && l1n == 0u &&
+            !(flags & (kOnEnded | MCS_FLAG_CLOCK_OVERFLOW))) {
+            t = t + 1u;
+            flags |= kOnEnded;
+        }
     }
     asm volatile("" : "+v"(used), "+v"(peak), "+v"(n_iter), "+v"(n_rel), "+v"(placed), "+v"(moved),
                  "+v"(placed_l1), "+v"(peak_l1), "+v"(l1_t), "+v"(mv_a), "+v"(ovf));
@@ -443,12 +458,22 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
             const uint32_t e2 = arr <= t ? arr + max_wait : arr;
             ev = (h < J && e2 < ev) ? e2 : ev;
             tn = ev > tn ? ev : tn;
+            if constexpr (HOR) {
+                // online, an empty Level0 waits for jobs not appended yet: one arriving at or after
+                // the horizon but before the jump's target would be the head at its own second, so
+                // the jump stops at the horizon (the skipped seconds repeat the same failures either way)
+                // (nothing to come at all, kEmpty: parked below, as before)
+                if (h >= J && tn != kEmpty && tn > a.on.t_hor) tn = a.on.t_hor;
+            }
         }
         if (!stop) {
             if (h >= J && l1n == 0u) {  // every job placed: the run ends at the next iteration
                 // (online: parked; the next horizon re-runs this iteration, which is idempotent
                 // with nothing queued, unless this is a drain)
-                if (!HOR || a.on.t_hor == kEmpty) t = t + 1u;
+                if (!HOR || a.on.t_hor == kEmpty) {
+                    t = t + 1u;
+                    if constexpr (HOR) flags |= kOnEnded;
+                }
                 stop = 1u;
             } else if (!changed && tn == kEmpty) {  // nothing runs or arrives: Level1 never fits
                 if (!HOR || a.on.t_hor == kEmpty) flags |= MCS_FLAG_DEADLOCK;  // (online: parked)
@@ -564,7 +589,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         st.placed = placed;
         st.waited = moved;
         st.peak_running = peak;
-        st.flags = flags;
+        st.flags = flags & ~kOnEnded;
         st.pool = (uint32_t)P;
         st.iterations = n_iter;
         st.release_scans = n_rel;

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle_ref as O
-from kat_util import seeded_workload
+from kat_util import fuzz_workload, seeded_workload
 from mcs_amd import Engine, JobStreams, MCSError, pack_clusters, replicate, uniform_cluster
 from mcs_amd import _lib as L
 
@@ -216,3 +216,23 @@ def test_clock_overflow_is_an_error_with_unplaced_rows(policy):
         assert node[2:].tolist() == [0, 0] and start[2:].tolist() == [5, 6]
         if policy == "DELAY":
             assert eng.delay_stats()[0]["jobs_count"] == -1
+
+
+@pytest.mark.parametrize("policy", ["FIFO", "DELAY"])
+@pytest.mark.parametrize("shape,seed", [("w16s", 1), ("w16r", 2), ("w32", 3)])
+def test_online_fuzz_slices_equal_batch_and_oracle(policy, shape, seed):
+    """kat_util's randomised workloads (never-fitting requests, zero-duration jobs, idle stretches)
+    advanced in 6 horizons with the arrivals appended between them: every prefix, the drained run,
+    the batch run (the FIFO batch run goes through the hand-scheduled loop, the online one through
+    the compiled kernel) and the oracle agree."""
+    arrays, streams = fuzz_workload(shape, seed, n_clusters=48, J=1200)
+    b = batch(arrays, streams, policy=policy)
+    run_oracle = O.delay_run_batch if policy == "DELAY" else O.fifo_run_batch
+    on, os_, of, osd = run_oracle(arrays, streams, n_threads=8)
+    assert np.array_equal(b[0], on) and np.array_equal(b[1], os_) and np.array_equal(b[2], of)
+    hs = horizons_for(streams, 6)
+    g = run_online(arrays, streams, hs, policy=policy, check_prefix=make_prefix_check(b[:3], streams.job_off))
+    for i in range(3):
+        np.testing.assert_array_equal(g[i], b[i])
+    for f in ("t_end", "placed", "flags"):
+        np.testing.assert_array_equal(g[4][f], osd[f], err_msg=f)
