@@ -75,12 +75,12 @@ def seeded_workload(kind: str, n_clusters: int, jobs_per_cluster: int, seed: int
     return arrays, streams, gp
 
 
-def fuzz_workload(shape: str, seed: int, n_clusters: int = 160, J: int = 2000):
+def fuzz_workload(shape: str, seed: int, n_clusters: int = 160, J: int = 2000, blocking: bool = True):
     """Randomised clusters and job streams (tests/test_gpu_parity.py, test_gpu_delay.py): node counts
     across the shape's range ('w16s' <= 64 nodes, 'mid' 65-128, 'w16r' 129-256, 'w32' 129-256 with
     memory values past 2^15), random JSON availability, bursts of simultaneous arrivals and idle
-    stretches, zero-duration and zero-resource jobs, requests up to a node's capacity, and in half
-    the clusters one request that fits no node at a random point of the stream."""
+    stretches, zero-duration and zero-resource jobs, requests up to a node's capacity, and (blocking)
+    in half the clusters one request that fits no node at a random point of the stream."""
     from mcs_amd import JobStreams, pack_clusters
     from mcs_amd.cluster import Node
 
@@ -106,7 +106,7 @@ def fuzz_workload(shape: str, seed: int, n_clusters: int = 160, J: int = 2000):
         z = rng.random(J) < 0.02
         cores[z] = 0
         mem[z] = 0
-        if rng.random() < 0.5:  # one request that fits no node, somewhere in the stream
+        if blocking and rng.random() < 0.5:  # one request that fits no node, somewhere in the stream
             i = int(rng.integers(J // 4, J))
             if rng.random() < 0.5:
                 cores[i] = cap_c + 1

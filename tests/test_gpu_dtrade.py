@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import oracle_ref as O
-from kat_util import GOLDEN, seeded_workload
+from kat_util import GOLDEN, fuzz_workload, seeded_workload
 from mcs_amd import Engine
 from test_dtrade_oracle import check_kat, dt_system
 
@@ -191,3 +191,25 @@ def test_gpu_approve_trade_sweep_vs_oracle(engine):
     bad = np.flatnonzero(got != orc)
     assert bad.size == 0, f"{bad.size} mismatches, first {bad[:5]}"
     assert 0.2 < got.mean() < 0.8  # both outcomes are exercised
+
+
+@pytest.mark.parametrize("shape,seed", [("w16s", 1), ("w16s", 2), ("mid", 3)])
+def test_gpu_dtrade_fuzz(shape, seed):
+    """kat_util's randomised clusters and streams in a DELAY trading system (real contracts, Foreign
+    jobs, virtual nodes): every output bit-exact against the oracle."""
+    arrays, streams = fuzz_workload(shape, seed, n_clusters=8, J=300, blocking=False)
+    g = run(arrays, streams)
+    o = O.dtrade_run(arrays, streams)
+    bad = np.nonzero((g["node"] != o["node"]) | (g["start"] != o["start"]) | (g["finish"] != o["finish"]))[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first {bad[:5]}: gpu {g['node'][bad[:5]]} {g['start'][bad[:5]]} " \
+                          f"oracle {o['node'][bad[:5]]} {o['start'][bad[:5]]}"
+    fields = ("t", "requester", "winner", "approvals", "policy", "cores", "mem", "time_s", "failed")
+    assert len(g["trades"]) == len(o["trades"])
+    for f in fields:
+        np.testing.assert_array_equal(g["trades"][f], o["trades"][f], err_msg=f)
+    assert len(g["foreign"]) == o["n_foreign"]
+    for f in ("requester", "responder", "node", "start", "finish", "c", "m"):
+        np.testing.assert_array_equal(g["foreign"][f], o["foreign"][f], err_msg=f)
+    assert g["vnodes"] == o["vnodes"]
+    for f in ("total_wait_ms", "jobs_count", "moved_l1", "placed_l1"):
+        np.testing.assert_array_equal(g["ds"][f], o["stats"][f], err_msg=f)

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import oracle_ref as O
-from kat_util import seeded_workload
+from kat_util import fuzz_workload, seeded_workload
 from mcs_amd import Engine
 from mcs_amd.shard import run_lockstep
 from test_trade_oracle import kat_inputs, lent_rows, load_trade_kats, trade_rows
@@ -179,3 +179,13 @@ def test_gpu_trade_config5_full_size():
     assert trade_rows(trades) == trade_rows(o["trades"])
     np.testing.assert_array_equal(vn, o["virtual_nodes"])
     assert ts["t_final"] == o["t_final"]
+
+
+@pytest.mark.parametrize("shape,seed", [("w16s", 1), ("w16s", 2), ("mid", 3), ("w16r", 4)])
+def test_gpu_trade_fuzz(shape, seed):
+    """kat_util's randomised clusters and streams (mixed node counts and availability, bursts, idle
+    stretches, zero-duration and zero-resource jobs) in a FIFO trading system: placements, borrows,
+    lent runs, trades, virtual nodes and the final tick bit-exact against the oracle."""
+    arrays, streams = fuzz_workload(shape, seed, n_clusters=12, J=500, blocking=False)
+    g = gpu_trade(arrays, streams)
+    assert_trade_parity(arrays, streams, g)
