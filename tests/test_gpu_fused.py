@@ -136,3 +136,44 @@ def test_weibull_device_records_equal_host(lam, k):
     on, os_, of, _ = O.fifo_run_batch(arrays, host, n_threads=8)
     np.testing.assert_array_equal(fz[0], on)
     np.testing.assert_array_equal(fz[1], os_)
+
+
+@pytest.mark.parametrize("policy", ["FIFO", "DELAY"])
+@pytest.mark.parametrize("seed", [11, 12, 13, 14])
+def test_fused_fuzz(policy, seed):
+    """Random cluster shapes (1..300 nodes, random capacities and availability), arrival modes, rates,
+    duration caps and Weibull shapes: the fused run equals the materialised run and the oracle over
+    the host generator's streams."""
+    from mcs_amd import Cluster
+    from mcs_amd.cluster import Node
+
+    rng = np.random.default_rng(seed)
+    clusters = []
+    for k in range(int(rng.integers(4, 24))):
+        nn = int(rng.choice([int(rng.integers(1, 65)), int(rng.integers(65, 301))]))
+        cc, cm = int(rng.integers(1, 64)), int(rng.integers(100, 60000))
+        cl = Cluster(Id=k + 1, Nodes=[])
+        for i in range(nn):
+            cl.Nodes.append(Node(Id=i + 1, Cores=cc, Memory=cm, CoresAvailable=int(rng.integers(cc // 2, cc + 1)),
+                                 MemoryAvailable=int(rng.integers(cm // 2, cm + 1))))
+        clusters.append(cl)
+    arrays = pack_clusters(clusters)
+    mode = int(rng.choice([L.MCS_ARRIVAL_REF, L.MCS_ARRIVAL_SCALED, L.MCS_ARRIVAL_WEIBULL]))
+    lam = float(rng.uniform(0.2, 3.0)) if mode == L.MCS_ARRIVAL_SCALED else float(rng.uniform(2.0, 40.0))
+    gp = GenParams(seed=int(rng.integers(1, 1 << 62)), arrival_mode=mode, lam=lam,
+                   max_dur_s=int(rng.integers(5, 900)), weibull_k=float(rng.choice([0.0, 1.5, 4.0])))
+    jobs = int(rng.integers(300, 1500))
+    ref = run(policy, arrays, gp, jobs)
+    gp.fused = True
+    fz = run(policy, arrays, gp, jobs)
+    for a, b, name in zip(ref[:3], fz[:3], ("node", "start", "finish")):
+        np.testing.assert_array_equal(a, b, err_msg=name)
+    for key in ("t_end", "placed", "waited", "peak_running", "flags"):
+        np.testing.assert_array_equal(ref[3][key], fz[3][key], err_msg=key)
+    gp.fused = False
+    streams = gen_streams_host(gp, arrays, jobs)
+    oracle = O.fifo_run_batch if policy == "FIFO" else O.delay_run_batch
+    on, os_, of, _ = oracle(arrays, streams, n_threads=8)
+    np.testing.assert_array_equal(fz[0], on)
+    np.testing.assert_array_equal(fz[1], os_)
+    np.testing.assert_array_equal(fz[2], of)
