@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -74,9 +75,19 @@ int ensure_job_records(mcs_engine* e) {
     const size_t nj = e->total_jobs ? e->total_jobs : 1;
     HIPCHK(e, hipMalloc(&e->d_jobs, (nj + kJobPad) * sizeof(uint4)));
     HIPCHK(e, hipMemsetAsync(e->d_jobs + nj, 0, kJobPad * sizeof(uint4), e->stream));
-    hipError_t st = launch_gen_attrs(e->d_jobs, e->d_job_off, e->gen.max_c, e->gen.max_m, e->C,
-                                     e->gen.seed, e->gen.max_dur, e->gen.base, e->stream);
-    if (st == hipSuccess) st = launch_gen_arrivals(e->d_jobs, e->d_job_off, e->C, e->gen, e->stream);
+    // MCS_GEN_SERIAL=1: the per-thread scan (tests compare the two forms)
+    const char* serial = getenv("MCS_GEN_SERIAL");
+    bool wave_form = e->job_off.size() == (size_t)e->C + 1 && !(serial && atoi(serial) != 0);
+    for (uint32_t c = 0; wave_form && c < e->C; ++c)
+        wave_form = e->job_off[c + 1] - e->job_off[c] < (1ull << 32);
+    hipError_t st;
+    if (wave_form) {
+        st = launch_gen_stream(e->d_jobs, e->d_job_off, e->C, e->gen, e->stream);
+    } else {
+        st = launch_gen_attrs(e->d_jobs, e->d_job_off, e->gen.max_c, e->gen.max_m, e->C, e->gen.seed,
+                              e->gen.max_dur, e->gen.base, e->stream);
+        if (st == hipSuccess) st = launch_gen_arrivals(e->d_jobs, e->d_job_off, e->C, e->gen, e->stream);
+    }
     if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
     if (st != hipSuccess)
         return fail(e, MCS_E_HIP, std::string("job generation: ") + hipGetErrorString(st));

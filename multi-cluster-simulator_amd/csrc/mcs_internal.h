@@ -144,6 +144,9 @@ hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t
                             uint32_t max_dur, uint32_t cluster_base, hipStream_t s);
 hipError_t launch_gen_arrivals(uint4* jobs, const uint64_t* job_off, uint32_t n_clusters, const GenArgs& g,
                                hipStream_t s);
+// whole records through GenStream, one wave per cluster (every cluster below 2^32 jobs)
+hipError_t launch_gen_stream(uint4* jobs, const uint64_t* job_off, uint32_t n_clusters, const GenArgs& g,
+                             hipStream_t s);
 hipError_t launch_gen_bound(const uint64_t* job_off, uint32_t n_clusters, const GenArgs& g,
                             unsigned long long* last, hipStream_t s);
 hipError_t launch_schedule_one(uint32_t* live_c, uint32_t* live_m, uint32_t n, uint32_t c,

@@ -774,6 +774,34 @@ hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t
     return hipGetLastError();
 }
 
+// Whole records, one wave per cluster: the fused kernels' batch generator (GenStream) writing its
+// batches out.  The per-thread arrival scan above walks a cluster's stream serially (one lane per
+// cluster, 64 clusters per wave: 9.5 ms for C4); the wave form draws 64 periods and 64 jobs at a
+// time.  Its 32-bit job counters need every cluster below 2^32 jobs (the caller checks).
+__global__ __launch_bounds__(256) void gen_stream_kernel(uint4* jobs, const uint64_t* job_off,
+                                                        uint32_t n_clusters, GenArgs g) {
+    const uint32_t c = blockIdx.x * (256u / kWave) + threadIdx.x / kWave;
+    const uint32_t lane = threadIdx.x % kWave;
+    if (c >= n_clusters) return;  // wave-uniform
+    const uint64_t j0 = job_off[c];
+    const uint32_t J = (uint32_t)(job_off[c + 1] - j0);
+    GenStream gs;
+    gs.init(g, c, lane);
+    for (uint32_t b = 0; b < J; b += kWave) {
+        const uint4 rec = gs.next(b, lane);
+        if (b + lane < J) jobs[j0 + b + lane] = rec;
+    }
+}
+
+hipError_t launch_gen_stream(uint4* jobs, const uint64_t* job_off, uint32_t n_clusters, const GenArgs& g,
+                             hipStream_t s) {
+    if (n_clusters == 0) return hipSuccess;
+    const uint32_t per = 256u / kWave;
+    hipLaunchKernelGGL(gen_stream_kernel, dim3((n_clusters + per - 1) / per), dim3(256), 0, s, jobs, job_off,
+                       n_clusters, g);
+    return hipGetLastError();
+}
+
 hipError_t launch_gen_arrivals(uint4* jobs, const uint64_t* job_off, uint32_t n_clusters, const GenArgs& g,
                                hipStream_t s) {
     if (n_clusters == 0) return hipSuccess;

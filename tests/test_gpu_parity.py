@@ -103,6 +103,25 @@ def test_device_generator_matches_host(engine):
             np.testing.assert_array_equal(getattr(dev, f), getattr(host, f), err_msg=f"{kind}:{f}")
 
 
+@pytest.mark.parametrize("serial", ["0", "1"])
+def test_device_generator_forms_all_modes(engine, serial, monkeypatch):
+    """Both materialising forms (the one-wave-per-cluster GenStream writer and the per-thread scan,
+    MCS_GEN_SERIAL=1) give the host generator's records for REF, SCALED and WEIBULL arrivals,
+    including job counts that end mid-batch and clusters of 0 or 1 jobs' worth of rate."""
+    monkeypatch.setenv("MCS_GEN_SERIAL", serial)
+    arrays = replicate(uniform_cluster(64), 70)
+    engine.load_clusters(arrays)
+    for gp in (GenParams(seed=5), GenParams(seed=6, arrival_mode=1, lam=0.37),
+               GenParams(seed=7, arrival_mode=1, lam=90.0), GenParams(seed=8, arrival_mode=2, lam=10.0),
+               GenParams(seed=9, arrival_mode=2, lam=4.0, weibull_k=1.5), GenParams(seed=10, lam=0.05)):
+        for J in (1, 63, 1000):
+            engine.generate_jobs(gp, J)
+            dev = engine.read_jobs()
+            host = gen_streams_host(gp, arrays, J)
+            for f in ("arrival", "dur", "cores", "mem"):
+                np.testing.assert_array_equal(getattr(dev, f), getattr(host, f), err_msg=f"{gp}:{J}:{f}")
+
+
 def test_config1_cluster_small_10k(engine):
     """BASELINE config 1 at its own size: cluster_small, FIFO, 10k seeded jobs."""
     arrays, streams, _ = seeded_workload("small", 1, 10_000)
