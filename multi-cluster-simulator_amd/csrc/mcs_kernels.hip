@@ -757,9 +757,61 @@ __global__ __launch_bounds__(64) void gen_bound_kernel(const uint64_t* job_off, 
     last[c] = lastT;
 }
 
+// The same bound, one wave per cluster, in 64-bit time: windows of 64 periods (lane l = period
+// pw + l) are prefix-summed as in GenStream::fill until the window holding job J-1, whose lane is
+// the first with an inclusive count above J-1-jw; WEIBULL sums the gaps of jobs 0..J-2, 64 a step.
+__global__ __launch_bounds__(256) void gen_bound_wave_kernel(const uint64_t* job_off, uint32_t n_clusters,
+                                                            GenArgs g, unsigned long long* last) {
+    const uint32_t c = blockIdx.x * (256u / kWave) + threadIdx.x / kWave;
+    const uint32_t lane = threadIdx.x % kWave;
+    if (c >= n_clusters) return;  // wave-uniform
+    const uint64_t J = job_off[c + 1] - job_off[c];
+    const uint64_t akey = mcs_arrival_key(mcs_cluster_key(g.seed, g.base + c));
+    uint64_t T = 0;
+    if (g.mode == 2u) {
+        for (uint64_t b = 0; b + 1u < J; b += kWave) {
+            const uint32_t gap = b + lane + 1u < J
+                                     ? mcs_weibull_gap(mcs_draw(akey, b + lane), (const uint64_t*)g.wthr, g.wn)
+                                     : 0u;
+            T += readlane(wave_incl_sum_u32(gap, lane), 63);  // 64 gaps < 2^32 (table length bound)
+        }
+        if (lane == 0) last[c] = T;
+        return;
+    }
+    uint64_t pw = 0, jw = 0;
+    while (J != 0) {
+        const uint32_t n = mcs_poisson(akey, pw + lane, g.enl);
+        const uint32_t d = g.mode == 0u ? (n == 0u ? 60u : n * (60u / n)) : 1u;
+        const uint32_t cum = wave_incl_sum_u32(n, lane);
+        const uint32_t dinc = wave_incl_sum_u32(d, lane);
+        const uint32_t tot = readlane(cum, 63);
+        if (jw + tot >= J) {  // job J-1 lies in this window
+            const uint32_t rel = (uint32_t)(J - 1u - jw);
+            const uint32_t lo = (uint32_t)__builtin_ctzll(__ballot(cum > rel));
+            const uint32_t np = (uint32_t)__shfl((int)n, (int)lo);
+            const uint32_t cp = (uint32_t)__shfl((int)cum, (int)lo);
+            const uint32_t te = (uint32_t)__shfl((int)(dinc - d), (int)lo);
+            const uint64_t lt = g.mode == 0u ? T + te + (uint64_t)(rel - (cp - np)) * (60u / np) : T + lo;
+            if (lane == 0) last[c] = lt;
+            return;
+        }
+        jw += tot;
+        T += readlane(dinc, 63);
+        pw += kWave;
+    }
+    if (lane == 0) last[c] = 0u;
+}
+
 hipError_t launch_gen_bound(const uint64_t* job_off, uint32_t n_clusters, const GenArgs& g,
                             unsigned long long* last, hipStream_t s) {
     if (n_clusters == 0) return hipSuccess;
+    const char* serial = getenv("MCS_GEN_SERIAL");  // the per-thread scan (tests compare the forms)
+    if (!(serial && atoi(serial) != 0)) {
+        const uint32_t per = 256u / kWave;
+        hipLaunchKernelGGL(gen_bound_wave_kernel, dim3((n_clusters + per - 1) / per), dim3(256), 0, s, job_off,
+                           n_clusters, g, last);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(gen_bound_kernel, dim3((n_clusters + 63) / 64), dim3(64), 0, s, job_off, n_clusters, g,
                        last);
     return hipGetLastError();

@@ -177,3 +177,27 @@ def test_fused_fuzz(policy, seed):
     np.testing.assert_array_equal(fz[0], on)
     np.testing.assert_array_equal(fz[1], os_)
     np.testing.assert_array_equal(fz[2], of)
+
+
+@pytest.mark.parametrize("serial", ["0", "1"])
+@pytest.mark.parametrize("mode,lam,jobs", [(L.MCS_ARRIVAL_REF, 10.0, 777), (L.MCS_ARRIVAL_REF, 0.3, 130),
+                                           (L.MCS_ARRIVAL_SCALED, 2.5, 1000), (L.MCS_ARRIVAL_SCALED, 40.0, 64),
+                                           (L.MCS_ARRIVAL_WEIBULL, 10.0, 500), (L.MCS_ARRIVAL_WEIBULL, 3.0, 1)])
+def test_fused_clock_bound_is_exact(serial, mode, lam, jobs, monkeypatch):
+    """A fused stream is accepted iff every cluster's last arrival + jobs * max_dur stays below
+    2^32-1 (FIFO; mcs_generate_jobs).  The last arrivals come from the device bound scan (one wave
+    per cluster, or the per-thread scan with MCS_GEN_SERIAL=1); the host generator gives them
+    exactly, so a max_dur_s one above / at the limit must flip the verdict."""
+    monkeypatch.setenv("MCS_GEN_SERIAL", serial)
+    arrays = replicate(uniform_cluster(64), 40)
+    gp = GenParams(seed=1234, arrival_mode=mode, lam=lam, fused=True)
+    last = max(int(gen_streams_host(gp, arrays, jobs).arrival.reshape(40, jobs)[:, -1].max()), 0)
+    room = 0xFFFFFFFF - last
+    md = (room - 1) // jobs  # the largest max_dur_s still accepted
+    with Engine(0) as eng:
+        eng.load_clusters(arrays)
+        gp.max_dur_s = md
+        eng.generate_jobs(gp, jobs)
+        gp.max_dur_s = md + 1
+        with pytest.raises(L.MCSError):
+            eng.generate_jobs(gp, jobs)

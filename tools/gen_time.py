@@ -1,6 +1,7 @@
 """Materialise the C4 job stream in both device forms (GenStream wave writer, then the per-thread
 scan with MCS_GEN_SERIAL=1) and check they agree; run under rocprofv3 --kernel-trace --stats to
-time gen_stream_kernel against gen_attrs_kernel + gen_arrivals_kernel."""
+time gen_stream_kernel against gen_attrs_kernel + gen_arrivals_kernel, and the fused stream's
+clock-bound scan gen_bound_wave_kernel against gen_bound_kernel."""
 import os
 import sys
 
@@ -20,4 +21,7 @@ for serial in ("0", "1"):
 for f in ("arrival", "dur", "cores", "mem"):
     assert np.array_equal(getattr(out[0], f), getattr(out[1], f)), f
 print("forms agree:", C, "clusters x", J, "jobs")
+for serial in ("0", "1"):  # the fused stream's clock-bound scan in both forms
+    os.environ["MCS_GEN_SERIAL"] = serial
+    eng.generate_jobs(GenParams(seed=7, fused=True), J)
 eng.close()
