@@ -1,0 +1,43 @@
+"""Run the GPU fuzz parity cases over a range of fresh seeds (beyond the ones the test suite pins)
+and report every failing (test, shape/policy, seed); exit status 1 if any failed.
+
+    python tools/fuzz_sweep.py BASE COUNT
+"""
+import os
+import sys
+import time
+import traceback
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "multi-cluster-simulator_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import test_gpu_delay as TD  # noqa: E402
+import test_gpu_dtrade as TDT  # noqa: E402
+import test_gpu_fused as TF  # noqa: E402
+import test_gpu_online as TO  # noqa: E402
+import test_gpu_parity as TP  # noqa: E402
+import test_gpu_trade as TT  # noqa: E402
+from mcs_amd import Engine  # noqa: E402
+
+base, count = int(sys.argv[1]), int(sys.argv[2])
+fails, runs = [], 0
+t0 = time.time()
+with Engine(0) as eng, Engine(0, policy="DELAY") as deng:
+    for seed in range(base, base + count):
+        cases = [(f"fifo/{s}", lambda s=s: TP.test_hand_scheduled_fuzz(eng, s, seed)) for s in ("w16s", "w16r", "w32")]
+        cases += [(f"delay/{s}", lambda s=s: TD.test_gpu_delay_fuzz(deng, s, seed)) for s in ("w16s", "mid", "w16r")]
+        cases += [(f"fused/{p}", lambda p=p: TF.test_fused_fuzz(p, seed)) for p in ("FIFO", "DELAY")]
+        cases += [(f"online/{p}/{s}", lambda p=p, s=s: TO.test_online_fuzz_slices_equal_batch_and_oracle(p, s, seed))
+                  for p in ("FIFO", "DELAY") for s in ("w16s", "w16r")]
+        cases += [("trade/w16s", lambda: TT.test_gpu_trade_fuzz("w16s", seed)),
+                  ("dtrade/w16s", lambda: TDT.test_gpu_dtrade_fuzz("w16s", seed))]
+        for name, fn in cases:
+            runs += 1
+            try:
+                fn()
+            except Exception:  # noqa: BLE001 - report and continue with the next case
+                fails.append((name, seed))
+                print(f"FAIL {name} seed {seed}\n{traceback.format_exc(limit=3)}", flush=True)
+        print(f"seed {seed}: {runs} cases run, {len(fails)} failed, {time.time() - t0:.0f} s", flush=True)
+print("failures:", fails)
+sys.exit(1 if fails else 0)
