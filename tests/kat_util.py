@@ -80,7 +80,9 @@ def fuzz_workload(shape: str, seed: int, n_clusters: int = 160, J: int = 2000, b
     across the shape's range ('w16s' <= 64 nodes, 'mid' 65-128, 'w16r' 129-256, 'w32' 129-256 with
     memory values past 2^15), random JSON availability, bursts of simultaneous arrivals and idle
     stretches, zero-duration and zero-resource jobs, requests up to a node's capacity, and (blocking)
-    in half the clusters one request that fits no node at a random point of the stream."""
+    in half the clusters one request that fits no node at a random point of the stream; without
+    blocking, node 0 is fully available, so no request can wait forever (a lock-step trading run
+    would otherwise tick to its t_max)."""
     from mcs_amd import JobStreams, pack_clusters
     from mcs_amd.cluster import Node
 
@@ -96,6 +98,8 @@ def fuzz_workload(shape: str, seed: int, n_clusters: int = 160, J: int = 2000, b
             fc = cap_c if rng.random() < 0.7 else int(rng.integers(0, cap_c + 1))
             fm = cap_m if rng.random() < 0.7 else int(rng.integers(0, cap_m + 1))
             cl.Nodes.append(Node(Id=i + 1, Cores=cap_c, Memory=cap_m, CoresAvailable=fc, MemoryAvailable=fm))
+        if not blocking:  # node 0 fully available: every request fits once it drains (no stuck head)
+            cl.Nodes[0].CoresAvailable, cl.Nodes[0].MemoryAvailable = cap_c, cap_m
         clusters.append(cl)
         gaps = rng.poisson(rng.uniform(0.05, 2.0), J)
         gaps[rng.random(J) < 0.05] += int(rng.integers(10, 500))  # idle stretches

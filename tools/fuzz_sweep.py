@@ -25,14 +25,16 @@ t0 = time.time()
 with Engine(0) as eng, Engine(0, policy="DELAY") as deng:
     for seed in range(base, base + count):
         cases = [(f"fifo/{s}", lambda s=s: TP.test_hand_scheduled_fuzz(eng, s, seed)) for s in ("w16s", "w16r", "w32")]
-        cases += [(f"delay/{s}", lambda s=s: TD.test_gpu_delay_fuzz(deng, s, seed)) for s in ("w16s", "mid", "w16r")]
+        cases += [(f"delay/{s}", lambda s=s: TD.test_gpu_delay_fuzz(deng, s, seed)) for s in ("w16s", "mid", "w16r", "w32")]
         cases += [(f"fused/{p}", lambda p=p: TF.test_fused_fuzz(p, seed)) for p in ("FIFO", "DELAY")]
         cases += [(f"online/{p}/{s}", lambda p=p, s=s: TO.test_online_fuzz_slices_equal_batch_and_oracle(p, s, seed))
-                  for p in ("FIFO", "DELAY") for s in ("w16s", "w16r")]
-        cases += [("trade/w16s", lambda: TT.test_gpu_trade_fuzz("w16s", seed)),
-                  ("dtrade/w16s", lambda: TDT.test_gpu_dtrade_fuzz("w16s", seed))]
+                  for p in ("FIFO", "DELAY") for s in ("w16s", "w16r", "w32")]
+        cases += [(f"trade/{s}", lambda s=s: TT.test_gpu_trade_fuzz(s, seed)) for s in ("w16s", "mid", "w16r")]
+        cases += [(f"dtrade/{s}", lambda s=s: TDT.test_gpu_dtrade_fuzz(s, seed)) for s in ("w16s", "mid")]
         for name, fn in cases:
             runs += 1
+            if os.environ.get("SWEEP_VERBOSE"):
+                print(f"  {name} seed {seed} ...", flush=True)
             try:
                 fn()
             except Exception:  # noqa: BLE001 - report and continue with the next case
