@@ -1,7 +1,7 @@
 """Run the GPU fuzz parity cases over a range of fresh seeds (beyond the ones the test suite pins)
 and report every failing (test, shape/policy, seed); exit status 1 if any failed.
 
-    python tools/fuzz_sweep.py BASE COUNT      (SWEEP_BIG=1: larger FIFO cases only)
+    python tools/fuzz_sweep.py BASE COUNT      (SWEEP_BIG=1: larger FIFO and DELAY cases only)
 """
 import os
 import sys
@@ -31,12 +31,17 @@ with Engine(0) as eng, Engine(0, policy="DELAY") as deng:
                   for p in ("FIFO", "DELAY") for s in ("w16s", "w16r", "w32")]
         cases += [(f"trade/{s}", lambda s=s: TT.test_gpu_trade_fuzz(s, seed)) for s in ("w16s", "mid", "w16r")]
         cases += [(f"dtrade/{s}", lambda s=s: TDT.test_gpu_dtrade_fuzz(s, seed)) for s in ("w16s", "mid")]
-        if os.environ.get("SWEEP_BIG"):  # FIFO only, 600 clusters x 6000 jobs per case
+        if os.environ.get("SWEEP_BIG"):  # FIFO 600 x 6000, DELAY 400 x 5000 jobs per case
             def big(shape, seed=seed):
                 arrays, st = TP.fuzz_workload(shape, seed, n_clusters=600, J=6000)
                 node, start, fin, _, cs = TP.run_engine(eng, arrays, st)
                 TP.assert_parity(arrays, st, node, start, fin, cs)
+            def dbig(shape, seed=seed):
+                arrays, st = TP.fuzz_workload(shape, seed, n_clusters=400, J=5000)
+                node, start, fin, _, cs, ds = TD.run(deng, arrays, st)
+                TD.assert_delay_parity(arrays, st, node, start, fin, cs, ds)
             cases = [(f"fifo-big/{s}", lambda s=s: big(s)) for s in ("w16s", "mid", "w16r", "w32")]
+            cases += [(f"delay-big/{s}", lambda s=s: dbig(s)) for s in ("w16s", "mid", "w16r", "w32")]
         for name, fn in cases:
             runs += 1
             if os.environ.get("SWEEP_VERBOSE"):
