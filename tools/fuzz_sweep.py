@@ -42,6 +42,11 @@ with Engine(0) as eng, Engine(0, policy="DELAY") as deng:
                 TD.assert_delay_parity(arrays, st, node, start, fin, cs, ds)
             cases = [(f"fifo-big/{s}", lambda s=s: big(s)) for s in ("w16s", "mid", "w16r", "w32")]
             cases += [(f"delay-big/{s}", lambda s=s: dbig(s)) for s in ("w16s", "mid", "w16r", "w32")]
+            if os.environ.get("SWEEP_TRADE"):  # trading systems: 32 clusters x 2000 jobs instead
+                def tbig(shape, seed=seed):
+                    arrays, st = TP.fuzz_workload(shape, seed, n_clusters=32, J=2000, blocking=False)
+                    TT.assert_trade_parity(arrays, st, TT.gpu_trade(arrays, st))
+                cases = [(f"trade-big/{s}", lambda s=s: tbig(s)) for s in ("w16s", "mid", "w16r")]
         for name, fn in cases:
             runs += 1
             if os.environ.get("SWEEP_VERBOSE"):
