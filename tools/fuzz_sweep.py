@@ -46,7 +46,13 @@ with Engine(0) as eng, Engine(0, policy="DELAY") as deng:
                 def tbig(shape, seed=seed):
                     arrays, st = TP.fuzz_workload(shape, seed, n_clusters=32, J=2000, blocking=False)
                     TT.assert_trade_parity(arrays, st, TT.gpu_trade(arrays, st))
+                def dtbig(shape, seed=seed):  # DELAY trading: placements against the oracle
+                    arrays, st = TP.fuzz_workload(shape, seed, n_clusters=16, J=800, blocking=False)
+                    g, o = TDT.run(arrays, st), TDT.O.dtrade_run(arrays, st)
+                    for k in ("node", "start", "finish"):
+                        assert (g[k] == o[k]).all(), k
                 cases = [(f"trade-big/{s}", lambda s=s: tbig(s)) for s in ("w16s", "mid", "w16r")]
+                cases += [(f"dtrade-big/{s}", lambda s=s: dtbig(s)) for s in ("w16s", "mid")]
         for name, fn in cases:
             runs += 1
             if os.environ.get("SWEEP_VERBOSE"):
