@@ -63,7 +63,8 @@ def parse():
     ap.add_argument("--cpu-sample-clusters", type=int, default=0,
                     help="CPU baseline sample: that many clusters with full streams (0 = per-config default, "
                          "about 10-30 s of oracle work)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, usable cpus)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every usable host cpu (SURVEY §8d: OpenMP over clusters on all host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes measured by a separate rocprofv3 --pmc pass (profile figure)")
@@ -76,7 +77,7 @@ def parse():
                          "(SURVEY §8f row 3, 12 B/placement)")
     a = ap.parse_args()
     defaults = {  # (clusters, jobs per cluster, cpu sample clusters)
-        "c4": (4096, 16384, 2048),
+        "c4": (4096, 16384, 4096),
         "c3": (1024, 65536, 1024),
         "c2": (1, 1_000_000, 1),
         "c5": (64, 2000 if a.policy == "delay" else 156250, 16 if a.policy == "delay" else 64),
@@ -105,7 +106,22 @@ def host_info(n_threads):
         usable = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         usable = os.cpu_count() or 1
-    return {"threads": n_threads, "host_nproc": os.cpu_count(), "host_usable_cpus": usable, "cpu_model": model}
+    quota = None
+    try:  # cgroup v2 CPU quota ("max 100000" = none): the cores the threads can actually occupy
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            quota = None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    return {"threads": n_threads, "host_nproc": os.cpu_count(), "host_usable_cpus": usable,
+            "cgroup_cpu_quota": quota, "cpu_model": model}
+
+
+def usable_cpus():
+    try:
+        return len(os.sched_getaffinity(0)) or 1
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
 
 
 NAIVE = ("the CPU oracle is the deliberately naive restatement of the Go loop (it rescans the running "
@@ -436,13 +452,15 @@ class Workload:
         return arrays, gen_streams_host(gp, arrays, self.J, base=self.base), k
 
 
-def cpu_baseline(args, wl, n_threads):
+def cpu_baseline(args, wl, n_threads, sample_clusters=None):
     """The oracle (CPU restatement, deliberately naive, -O3) on a bounded sample of the same
     workload: the first cpu_sample_clusters clusters of rank 0, full job streams, OpenMP over
     clusters.  Test infrastructure used as the reported baseline only."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_ref as O
 
+    if sample_clusters is not None:
+        args = argparse.Namespace(**{**vars(args), "cpu_sample_clusters": sample_clusters})
     arrays, streams, k = wl.cpu_sample(args)
     O.lib()
     t0 = time.perf_counter()
@@ -553,10 +571,14 @@ def main_batch(args, world, rank, local_rank):
             pass
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            n_thr = args.cpu_threads or min(16, host_info(0)["host_usable_cpus"] or 1)
+            n_thr = args.cpu_threads or usable_cpus()
             if args.config == "c2":
                 n_thr = 1  # one cluster: the oracle is one serial loop
             cpu = cpu_baseline(args, wl, n_thr)
+            if n_thr > 16 and not args.cpu_threads:
+                # the round-1/2 figure (16 threads, a quarter of the shard) kept for comparison
+                sec = cpu_baseline(args, wl, 16, sample_clusters=max(1, min(wl.per, args.cpu_sample_clusters) // 4))
+                cpu["secondary_16_threads"] = {k: sec[k] for k in ("value", "cores", "sample", "seconds")}
         value = placed_all / elapsed_max
         metric = {"c4": "job placements/sec (whole node) at 4096 clusters x 256 nodes",
                   "c3": "job placements/sec at 1024 cluster_small replicas per GPU",

@@ -91,7 +91,9 @@ typedef struct mcs_config {
                                     [+ max_wait_s under DELAY])) leaves the uint32 range.  1: skip that
                                     check (tests of the device-side guard: the kernels then stop the
                                     cluster with MCS_FLAG_CLOCK_OVERFLOW and mcs_run returns
-                                    MCS_E_RANGE)                                                     */
+                                    MCS_E_RANGE).  Not allowed with borrow or trader (the lock-step
+                                    kernels have no such guard): mcs_engine_create returns
+                                    MCS_E_INVALID                                                    */
     uint32_t reserved[1];
 } mcs_config;
 
@@ -240,8 +242,9 @@ int mcs_run(mcs_engine* eng, uint32_t t_end_s, mcs_stats* stats);
 
 /* Online mode: append jobs to the clusters' streams (the "/" or "/delay" handler appending to the
  * ReadyQueue / Level0, server.go:38-41,67-69).  Jobs of cluster c are [job_offsets[c],
- * job_offsets[c+1]) of the given arrays, arrival-sorted, each arrival >= the cluster's last one and
- * >= the last horizon run.  Their ids continue the cluster's stream (dense order of
+ * job_offsets[c+1]) of the given arrays, arrival-sorted, each arrival >= the cluster's last one,
+ * >= the last finite horizon run, and >= the cluster's own clock after the last drain (a cluster
+ * whose drain ended earlier accepts earlier arrivals than one that ran longer).  Their ids continue the cluster's stream (dense order of
  * mcs_read_placements: per cluster, submitted then appended jobs in order).  Starts an online
  * session (state at t = 0) if none is active.  Not available with borrow/trader. */
 int mcs_append_jobs(mcs_engine* eng, const uint32_t* arrival_s, const uint32_t* dur_s,

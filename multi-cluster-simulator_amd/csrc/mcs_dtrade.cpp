@@ -210,17 +210,19 @@ int dt_run_rccl(mcs_engine* e, double* kernel_ms) {
 // the whole system, and the cluster count per rank must match
 int dt_agree_shape(mcs_engine* e) {
     uint32_t* buf = nullptr;
-    HIPCHK(e, hipMalloc(&buf, 2 * sizeof(uint32_t)));
-    const uint32_t h[2] = {e->max_n, e->C};
-    uint32_t mx[2] = {0, 0};
+    HIPCHK(e, hipMalloc(&buf, 3 * sizeof(uint32_t)));
+    /* max of C and of ~C (= ~min C): every rank sees the same verdict, so a mismatch fails on
+     * every rank instead of leaving the ranks with the largest C in the tick loop */
+    const uint32_t h[3] = {e->max_n, e->C, ~e->C};
+    uint32_t mx[3] = {0, 0, 0};
     HIPCHK(e, hipMemcpy(buf, h, sizeof(h), hipMemcpyHostToDevice));
-    ncclResult_t r = ncclAllReduce(buf, buf, 2, ncclUint32, ncclMax, (ncclComm_t)e->comm, e->stream);
+    ncclResult_t r = ncclAllReduce(buf, buf, 3, ncclUint32, ncclMax, (ncclComm_t)e->comm, e->stream);
     hipError_t st = hipStreamSynchronize(e->stream);
     if (r == ncclSuccess && st == hipSuccess) st = hipMemcpy(mx, buf, sizeof(mx), hipMemcpyDeviceToHost);
     (void)hipFree(buf);
     if (r != ncclSuccess) return fail(e, MCS_E_RCCL, std::string("ncclAllReduce(shape): ") + ncclGetErrorString(r));
     if (st != hipSuccess) return dt_hip_fail(e, "shape exchange", st);
-    if (mx[1] != e->C) return fail(e, MCS_E_INVALID, "sharded DELAY trading needs the same cluster count on every rank");
+    if (mx[1] != ~mx[2]) return fail(e, MCS_E_INVALID, "sharded DELAY trading needs the same cluster count on every rank");
     e->dt_ns = mx[0];
     return MCS_OK;
 }

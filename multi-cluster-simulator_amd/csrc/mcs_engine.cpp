@@ -194,6 +194,9 @@ int mcs_engine_create(const mcs_config* cfg, int device, mcs_engine** out) {
         if (c.trader && c.trader_period_s % c.sample_period_s != 0)
             return MCS_E_INVALID; /* rounds must fall on state samples */
         if (c.slot_pool > 64) return MCS_E_INVALID; /* lock-step slots: 64 * slot_pool <= 4096 */
+        if (c.unchecked_horizon)
+            return MCS_E_INVALID; /* the lock-step kernels carry no run-time clock guard: keep the
+                                     host bound */
     } else if (c.slot_pool != 0 && !mcs::fifo_variant_exists(1, (int)c.slot_pool)) {
         return MCS_E_INVALID;
     }
@@ -333,9 +336,15 @@ static int alloc_jobs(mcs_engine* e, const uint64_t* job_offsets, bool records) 
         HIPCHK(e, hipMemset(e->d_jobs + nj, 0, mcs::kJobPad * sizeof(uint4)));
     }
     HIPCHK(e, hipMalloc(&e->d_job_off, (e->C + 1) * sizeof(uint64_t)));
-    HIPCHK(e, hipMalloc(&e->d_out_node, nj * sizeof(int32_t)));
-    HIPCHK(e, hipMalloc(&e->d_out_start, nj * sizeof(uint32_t)));
-    HIPCHK(e, hipMalloc(&e->d_out_finish, nj * sizeof(uint32_t)));
+    /* the result arrays get the same slack: a horizon resumes by reading the 64-row result batch
+     * that holds its cursor ((r & ~63) + lane, mcs_kernels.hip / mcs_delay.hip), which reaches past
+     * the end when the last cluster's batch is partial */
+    HIPCHK(e, hipMalloc(&e->d_out_node, (nj + mcs::kJobPad) * sizeof(int32_t)));
+    HIPCHK(e, hipMalloc(&e->d_out_start, (nj + mcs::kJobPad) * sizeof(uint32_t)));
+    HIPCHK(e, hipMalloc(&e->d_out_finish, (nj + mcs::kJobPad) * sizeof(uint32_t)));
+    HIPCHK(e, hipMemset(e->d_out_node, 0xFF, (nj + mcs::kJobPad) * sizeof(int32_t)));
+    HIPCHK(e, hipMemset(e->d_out_start, 0xFF, (nj + mcs::kJobPad) * sizeof(uint32_t)));
+    HIPCHK(e, hipMemset(e->d_out_finish, 0xFF, (nj + mcs::kJobPad) * sizeof(uint32_t)));
     HIPCHK(e, hipMemcpy(e->d_job_off, job_offsets, (e->C + 1) * sizeof(uint64_t),
                         hipMemcpyHostToDevice));
     return MCS_OK;
@@ -538,6 +547,12 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     a.gen = e->gen;
     a.n_items = e->C;
     a.guard_ok = (e->free_lt31 ? 1u : 0u) | (e->free_lt15 ? 2u : 0u);
+    { /* the hand-scheduled loop addresses a cluster's records and results with 32-bit VGPR
+       * offsets from the cluster's base ((cb + lane) << 4): keep them inside 2^32 */
+        uint64_t jmax = 0;
+        for (uint32_t c = 0; c < e->C; ++c) jmax = std::max<uint64_t>(jmax, e->job_off[c + 1] - e->job_off[c]);
+        if (jmax <= mcs::kAsmMaxJobs) a.guard_ok |= 4u;
+    }
     mcs::DelayArgs da{};
     da.node_free0 = e->d_free0;
     da.node_off = e->d_node_off;

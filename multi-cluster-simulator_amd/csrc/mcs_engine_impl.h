@@ -102,6 +102,8 @@ struct mcs_engine {
     bool online = false;               // a session is active
     bool segmented = false;            // job_off holds segment starts with slack (appends)
     uint32_t on_t_done = 0;            // the last horizon run (appended arrivals must be >= it)
+    uint32_t on_t_hor = 0;             // the last finite horizon (appended arrivals must be >= it)
+    std::vector<uint32_t> on_floor;    // per cluster: its clock after the last drain (appends >= it)
     int on_pool = 0;                   // slot rows that every saved state fits in
     int on_cur = 0;                    // which of the double-buffered states is current
     mcs::OnlineState* d_ost[2] = {nullptr, nullptr};

@@ -788,7 +788,9 @@ int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor) {
     const int want = env ? atoi(env) : 1;
     // the loop's two shapes: 129-256 node clusters with 8 slot rows (C4) and at most 64 nodes with 2
     // rows (C1-C3); other shapes and pools keep the compiled kernel
-    if (want == 0 || hor || a.gen.on) return 0;
+    // (records and results are addressed by 32-bit offsets from the cluster's base: at most
+    // kAsmMaxJobs jobs per cluster, guard_ok bit 2)
+    if (want == 0 || hor || a.gen.on || !(a.guard_ok & 4u)) return 0;
     if (npl == 1 && pool == 2) return (a.guard_ok & 2u) && want != 16 && want != 32 ? 18 : 0;
     if (npl != 4 || pool != 8) return 0;
     // register slots: one LDS round trip per release instead of 2 + rows; measured faster than LDS

@@ -17,6 +17,7 @@ constexpr uint32_t kEmpty = 0xFFFFFFFFu;  // empty running slot (finish time nev
 constexpr int kWave = 64;
 constexpr int kMaxNpl = 16;   // nodes per lane -> at most 1024 nodes per cluster in ABI v1
 constexpr int kMaxPool = 32;  // running-slot registers per lane -> 2048 slots per cluster
+constexpr uint32_t kAsmMaxJobs = (1u << 28) - 128u;  // hand-scheduled loop: 32-bit record offsets
 constexpr uint32_t kJobPad = 128;  // records of slack after the job array (unmasked batch loads)
 
 struct Totals {  // device-side accumulation of mcs_stats (only clusters that did not overflow)
@@ -87,7 +88,8 @@ struct FifoArgs {
     OnlineArgs on;
     uint32_t n_items;
     uint32_t guard_ok;  // bit 0: every node's free values < 2^31 - 1 (the hand-scheduled loop
-                        // may run, W32 node format); bit 1: < 2^15 - 1 (W16 node format)
+                        // may run, W32 node format); bit 1: < 2^15 - 1 (W16 node format);
+                        // bit 2: every cluster holds at most kAsmMaxJobs jobs
 };
 
 struct DelayArgs {

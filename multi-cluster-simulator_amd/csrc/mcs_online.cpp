@@ -181,6 +181,8 @@ int online_begin(mcs_engine* e) {
     HIPCHK(e, hipMemset(e->d_ost[0], 0, (e->C ? e->C : 1) * sizeof(OnlineState)));  // valid = 0: the spec
     e->on_pool = e->cfg.slot_pool ? (int)e->cfg.slot_pool : auto_pool(e->max_n);
     e->on_t_done = 0;
+    e->on_t_hor = 0;
+    e->on_floor.assign(e->C, 0u);
     e->online = true;
     e->has_run = false;
     return MCS_OK;
@@ -223,6 +225,8 @@ void online_free(mcs_engine* e) {
     e->segmented = false;
     e->job_cnt.clear();
     e->on_t_done = 0;
+    e->on_t_hor = 0;
+    e->on_floor.clear();
 }
 
 int online_run(mcs_engine* e, uint32_t t_hor, mcs_stats* stats) {
@@ -334,10 +338,15 @@ int online_run(mcs_engine* e, uint32_t t_hor, mcs_stats* stats) {
     e->trade_run = e->dtrade_run = false;
     if (t_hor != MCS_TIME_NONE) {
         e->on_t_done = t_hor;
-    } else if (e->C) {  // a drain: later arrivals must not precede any cluster's clock
+        e->on_t_hor = t_hor;
+    } else if (e->C) {  // a drain: a cluster's later arrivals must not precede its own clock
         std::vector<mcs_cluster_stats> cs(e->C);
         HIPCHK(e, hipMemcpy(cs.data(), e->d_cstats, e->C * sizeof(mcs_cluster_stats), hipMemcpyDeviceToHost));
-        for (const auto& c : cs) e->on_t_done = std::max(e->on_t_done, c.t_end);
+        e->on_floor.resize(e->C, 0u);
+        for (uint32_t c = 0; c < e->C; ++c) {
+            e->on_floor[c] = std::max(e->on_floor[c], cs[c].t_end);
+            e->on_t_done = std::max(e->on_t_done, cs[c].t_end);  // (the next horizon's lower bound)
+        }
     }
     if (stats) {
         stats->jobs = e->total_jobs;
@@ -441,11 +450,12 @@ int mcs_append_jobs(mcs_engine* e, const uint32_t* arrival_s, const uint32_t* du
         if (a1 == a0) continue;
         if ((uint64_t)e->job_cnt[c] + (a1 - a0) > 0xFFFFFFFFull)
             return fail(e, MCS_E_INVALID, "more than 2^32-1 jobs in one cluster");
-        const uint32_t floor_ = std::max(e->job_cnt[c] ? e->last_arr[c] : 0u, e->on_t_done);
+        const uint32_t floor_ = std::max({e->job_cnt[c] ? e->last_arr[c] : 0u, e->on_t_hor,
+                                          c < e->on_floor.size() ? e->on_floor[c] : 0u});
         if (arrival_s[a0] < floor_)
             return fail(e, MCS_E_INVALID, "cluster " + std::to_string(c) + ": appended arrival " +
                                               std::to_string(arrival_s[a0]) + " precedes " + std::to_string(floor_) +
-                                              " (the last arrival or the last horizon run)");
+                                              " (the last arrival, the last horizon, or the cluster's clock after the last drain)");
         for (uint64_t i = a0; i < a1; ++i) {
             if (i > a0 && arrival_s[i] < arrival_s[i - 1])
                 return fail(e, MCS_E_INVALID, "arrivals must be non-decreasing within a cluster");

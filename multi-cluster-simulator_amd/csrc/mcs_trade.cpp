@@ -309,17 +309,19 @@ int trade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n) {
 // the whole system, and the cluster count per rank must match (one all-reduce before the run)
 int tr_agree_shape(mcs_engine* e) {
     uint32_t* buf = nullptr;
-    HIPCHK(e, hipMalloc(&buf, 2 * sizeof(uint32_t)));
-    const uint32_t h[2] = {e->max_n, e->C};
-    uint32_t mx[2] = {0, 0};
+    HIPCHK(e, hipMalloc(&buf, 3 * sizeof(uint32_t)));
+    /* max of C and of ~C (= ~min C): every rank sees the same verdict, so a mismatch fails on
+     * every rank instead of leaving the ranks with the largest C in the tick loop */
+    const uint32_t h[3] = {e->max_n, e->C, ~e->C};
+    uint32_t mx[3] = {0, 0, 0};
     HIPCHK(e, hipMemcpy(buf, h, sizeof(h), hipMemcpyHostToDevice));
-    ncclResult_t r = ncclAllReduce(buf, buf, 2, ncclUint32, ncclMax, (ncclComm_t)e->comm, e->stream);
+    ncclResult_t r = ncclAllReduce(buf, buf, 3, ncclUint32, ncclMax, (ncclComm_t)e->comm, e->stream);
     hipError_t st = hipStreamSynchronize(e->stream);
     if (r == ncclSuccess && st == hipSuccess) st = hipMemcpy(mx, buf, sizeof(mx), hipMemcpyDeviceToHost);
     (void)hipFree(buf);
     if (r != ncclSuccess) return nccl_fail(e, "ncclAllReduce(shape)", r);
     if (st != hipSuccess) return hip_fail(e, "shape exchange", st);
-    if (mx[1] != e->C) return fail(e, MCS_E_INVALID, "sharded lock-step trading needs the same cluster count on every rank");
+    if (mx[1] != ~mx[2]) return fail(e, MCS_E_INVALID, "sharded lock-step trading needs the same cluster count on every rank");
     e->tr_ns = mx[0];
     return MCS_OK;
 }
