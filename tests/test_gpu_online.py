@@ -236,3 +236,60 @@ def test_online_fuzz_slices_equal_batch_and_oracle(policy, shape, seed):
         np.testing.assert_array_equal(g[i], b[i])
     for f in ("t_end", "placed", "flags"):
         np.testing.assert_array_equal(g[4][f], osd[f], err_msg=f)
+
+
+def truncate_streams(streams, counts):
+    """the first counts[k] jobs of every cluster k (ragged clusters)"""
+    parts, off = [[], [], [], []], [0]
+    for k, n in enumerate(counts):
+        sl = streams.of(k)
+        for i, f in enumerate(("arrival", "dur", "cores", "mem")):
+            parts[i].append(getattr(streams, f)[sl][:n])
+        off.append(off[-1] + n)
+    return JobStreams(*[np.concatenate(p).astype(np.uint32) for p in parts], np.array(off, np.uint64))
+
+
+@pytest.mark.parametrize("policy", ["FIFO", "DELAY"])
+@pytest.mark.parametrize("kind", ["small", "n256"])
+def test_online_ragged_last_cluster(policy, kind):
+    """the last cluster holds fewer than 64 jobs (and one cluster none): a horizon resumes by reading
+    the 64-row result batch at its cursor, which reaches past the last job (the result
+    arrays carry kJobPad rows of slack).  Online slices and the unchecked-horizon batch path (the
+    online kernels from t = 0) equal the batch run and the oracle."""
+    arrays, full, _ = seeded_workload(kind, 4, 300)
+    streams = truncate_streams(full, [300, 0, 77, 13])
+    b = batch(arrays, streams, policy=policy)
+    ref = (O.fifo_run_batch if policy == "FIFO" else O.delay_run_batch)(arrays, streams, n_threads=4)
+    for i in range(3):
+        np.testing.assert_array_equal(b[i], ref[i])
+    g = run_online(arrays, streams, horizons_for(streams, 5), policy=policy)
+    u = batch(arrays, streams, policy=policy, unchecked_horizon=1)
+    for i in range(3):
+        np.testing.assert_array_equal(g[i], b[i])
+        np.testing.assert_array_equal(u[i], b[i])
+
+
+def test_online_append_floor_is_per_cluster_after_a_drain():
+    """after a drain each cluster accepts appended arrivals from its own clock on (mcs.h,
+    mcs_append_jobs): a cluster that finished early takes a job arriving before the clock of a
+    cluster that ran longer; an arrival before the cluster's own clock is refused."""
+    arrays = replicate(uniform_cluster(5), 2)
+    # cluster 0: one short job; cluster 1: six whole-node jobs, the sixth waits until t = 500
+    s0 = JobStreams(np.zeros(7, np.uint32), np.array([5] + [500] * 6, np.uint32),
+                    np.array([1] + [32] * 6, np.uint32), np.ones(7, np.uint32), np.array([0, 1, 7], np.uint64))
+    with Engine(0) as eng:
+        eng.load_clusters(arrays)
+        eng.append_jobs(s0)
+        eng.run()  # drain
+        t_end = eng.cluster_stats()["t_end"]
+        assert int(t_end[0]) < 100 < int(t_end[1])
+        late = JobStreams(np.array([100], np.uint32), np.array([3], np.uint32), np.array([2], np.uint32),
+                          np.array([2], np.uint32), np.array([0, 1, 1], np.uint64))
+        eng.append_jobs(late)  # cluster 0 only: 100 >= its own clock
+        eng.run()
+        node, start, fin = eng.placements()
+        assert (int(node[1]), int(start[1]), int(fin[1])) == (0, 100, 103)
+        early = JobStreams(np.array([int(t_end[1]) - 1], np.uint32), np.array([3], np.uint32),
+                           np.array([2], np.uint32), np.array([2], np.uint32), np.array([0, 0, 1], np.uint64))
+        with pytest.raises(MCSError):
+            eng.append_jobs(early)  # cluster 1: before its own clock
