@@ -64,7 +64,8 @@ def parse():
                     help="CPU baseline sample: that many clusters with full streams (0 = per-config default, "
                          "about 10-30 s of oracle work)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="0 = every usable host cpu (SURVEY §8d: OpenMP over clusters on all host cores)")
+                    help="0 = every usable host cpu: the affinity set capped by the cgroup CPU quota (SURVEY §8d: "
+                         "OpenMP over clusters on all host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes measured by a separate rocprofv3 --pmc pass (profile figure)")
@@ -118,10 +119,14 @@ def host_info(n_threads):
 
 
 def usable_cpus():
+    """cpus this process may run on: the affinity set, capped by the cgroup's CPU quota (on the GPU
+    box 256 cpus are visible but the quota is 16: 256 threads then time-slice on 16 cpus' worth)"""
     try:
-        return len(os.sched_getaffinity(0)) or 1
+        n = len(os.sched_getaffinity(0)) or 1
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q = host_info(0)["cgroup_cpu_quota"]
+    return max(1, min(n, int(q + 0.5))) if q else n
 
 
 NAIVE = ("the CPU oracle is the deliberately naive restatement of the Go loop (it rescans the running "
@@ -575,10 +580,11 @@ def main_batch(args, world, rank, local_rank):
             if args.config == "c2":
                 n_thr = 1  # one cluster: the oracle is one serial loop
             cpu = cpu_baseline(args, wl, n_thr)
-            if n_thr > 16 and not args.cpu_threads:
-                # the round-1/2 figure (16 threads, a quarter of the shard) kept for comparison
-                sec = cpu_baseline(args, wl, 16, sample_clusters=max(1, min(wl.per, args.cpu_sample_clusters) // 4))
-                cpu["secondary_16_threads"] = {k: sec[k] for k in ("value", "cores", "sample", "seconds")}
+            n_vis = host_info(0)["host_usable_cpus"] or 1
+            if args.config != "c2" and not args.cpu_threads and n_vis > n_thr:
+                # one thread per visible cpu as well (oversubscribed under the cgroup quota)
+                sec = cpu_baseline(args, wl, n_vis)
+                cpu["secondary_all_visible_cpus"] = {k: sec[k] for k in ("value", "cores", "sample", "seconds")}
         value = placed_all / elapsed_max
         metric = {"c4": "job placements/sec (whole node) at 4096 clusters x 256 nodes",
                   "c3": "job placements/sec at 1024 cluster_small replicas per GPU",

@@ -48,6 +48,9 @@ namespace mcs {
 
 namespace {
 
+#ifdef MCS_STAMPS
+__device__ unsigned long long g_fa_stamps[4];
+#endif
 
 // Register map of the loop (all fixed; listed as clobbers).
 //   s40 t     s41 min(64, J - cb)  s42 J   s43 have_w  s44 flags  s45 arr   s46 dur
@@ -79,7 +82,8 @@ namespace {
         "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v89", "v90", "v91",     \
         "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v107", "v108",        \
         "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v117", "v118", "v119", "v120",        \
-        "v121", "v122", "v123", "v124", "v125", "v126", "v127", "vcc", "scc", "m0", "exec", "memory"
+        "v121", "v122", "v123", "v124", "v125", "v126", "v127", "vcc", "scc", "m0", "exec", "memory"     \
+        MCS_FA_STAMP_CLOBBERS
 
 // ---- W-specific pieces ----------------------------------------------------------------------
 // the insert's candidate lanes: the lanes with a free slot row (computed early, off the chain)
@@ -436,6 +440,29 @@ namespace {
     "s_sub_u32 s80, s80, s75\n\t" MCS_FA_RELOAD16S                                              \
     "v_min_u32 v90, v32, v33\n\t"
 
+// ---- MCS_STAMPS probe build (tools/stamp_fa.py): s_memtime cycles per loop segment ------------------
+// s[92:93] segment start, s94 releases, s95 failed fits, s96 batch ends, s97 the whole loop; each
+// stamp waits for its own SMEM read (lgkmcnt, which also drains LDS): read the shares, not the time
+#ifdef MCS_STAMPS
+#define MCS_FA_T0 "s_memtime s[92:93]\n\ts_waitcnt lgkmcnt(0)\n\t"
+#define MCS_FA_T1(acc)                                                                            \
+    "s_memtime s[98:99]\n\ts_waitcnt lgkmcnt(0)\n\ts_sub_u32 s98, s98, s92\n\ts_add_u32 " acc ", " acc \
+    ", s98\n\t"
+#define MCS_FA_TSTART MCS_FA_T0 "s_sub_u32 s97, 0, s92\n\ts_mov_b32 s94, 0\n\ts_mov_b32 s95, 0\n\ts_mov_b32 s96, 0\n\t"
+#define MCS_FA_TEND                                                                               \
+    "s_memtime s[98:99]\n\ts_waitcnt lgkmcnt(0)\n\ts_add_u32 s97, s97, s98\n\t"                  \
+    "s_mov_b32 %[st0], s94\n\ts_mov_b32 %[st1], s95\n\ts_mov_b32 %[st2], s96\n\ts_mov_b32 %[st3], s97\n\t"
+#define MCS_FA_STAMP_CLOBBERS , "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99"
+#define MCS_FA_STAMP_OUTS , [st0] "=s"(st0), [st1] "=s"(st1), [st2] "=s"(st2), [st3] "=s"(st3)
+#else
+#define MCS_FA_T0 ""
+#define MCS_FA_T1(acc) ""
+#define MCS_FA_TSTART ""
+#define MCS_FA_TEND ""
+#define MCS_FA_STAMP_CLOBBERS
+#define MCS_FA_STAMP_OUTS
+#endif
+
 // ---- the decision loop ------------------------------------------------------------------------
 // diagnostic counters (passes without a decision, release scans): DIAG launches only
 #define MCS_FA_CNTS_D1 "s_add_u32 s83, s83, 1\n\t"
@@ -474,7 +501,7 @@ namespace {
     "v_mov_b32 v108, %[nb]\n\t"                                                                   \
     "v_mov_b32 v109, %[nbase]\n\t"                                                                \
     "v_mov_b32 v110, %[lane]\n\t"                                                                 \
-    "v_mov_b32 v111, -1\n\t" MCS_FA_INIT##W MCS_FA_RELOAD##W "s_waitcnt lgkmcnt(0)\n\t"                          \
+    "v_mov_b32 v111, -1\n\t" MCS_FA_INIT##W MCS_FA_RELOAD##W "s_waitcnt lgkmcnt(0)\n\t" MCS_FA_TSTART \
     /* prefetch batch 1 */                                                                        \
     "v_lshlrev_b32 v121, 4, v110\n\t"                                                             \
     "v_add_u32 v121, 0x400, v121\n\t"                                                             \
@@ -528,7 +555,7 @@ namespace {
     "s_branch mcsfa_adv_%=\n"                                                                     \
                                                                                                   \
     /* no node fits: WaitQueue append (:264-268), sleep to the next completion (A.3) */          \
-    "mcsfa_nofit_%=:\n\t"                                                                         \
+    "mcsfa_nofit_%=:\n\t" MCS_FA_T0                                                              \
     "s_sub_u32 s76, 1, s43\n\t"                                                                   \
     "s_add_u32 s82, s82, s76\n\t"                                                                 \
     "s_mov_b32 s43, 1\n\t"                                                                        \
@@ -544,7 +571,7 @@ namespace {
     "s_add_u32 s40, s40, 1\n\t"                                                                   \
     "s_cbranch_scc1 mcsfa_clkovf_%=\n\t"                                                          \
     "s_max_u32 s40, s40, s77\n\t" /* (every running job finishes after t: no wrap) */           \
-    "s_branch mcsfa_adv_%=\n"                                                                     \
+    MCS_FA_T1("s95") "s_branch mcsfa_adv_%=\n"                                                    \
                                                                                                   \
     "mcsfa_arrive_%=:\n\t"                                                                        \
     "s_mov_b32 s40, s45\n\t" /* (> t) */                                                         \
@@ -554,7 +581,7 @@ namespace {
     "s_cmp_lt_u32 s40, s77\n\t" /* nothing finishes by t: no release */                          \
     "s_cbranch_scc1 mcsfa_loopend_%=\n\t"                                                         \
     /* release every running job with finish <= t (cluster.go:153-157) */                        \
-    MCS_FA_CNTR_##D                                                                               \
+    MCS_FA_CNTR_##D MCS_FA_T0                                                                     \
     "s_max_u32 s81, s81, s80\n\t" /* peak: used only grows between releases */                   \
     "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN##W                                                   \
     /* the wave's earliest remaining finish (DPP minimum of v90) under the reload's latency */   \
@@ -573,7 +600,7 @@ namespace {
     "v_min_u32_dpp v120, v120, v120 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"                  \
     "s_nop 1\n\t"                                                                                 \
     "v_readlane_b32 s77, v120, 63\n\t"                                                            \
-    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
+    "s_waitcnt lgkmcnt(0)\n\t" MCS_FA_T1("s94")                                                   \
     "s_branch mcsfa_loopend_%=\n"                                                                 \
                                                                                                   \
     "mcsfa_deadlock_%=:\n\t"                                                                      \
@@ -588,7 +615,7 @@ namespace {
     "s_branch mcsfa_exit_%=\n"                                                                    \
                                                                                                   \
     /* ---- batch end: store the 64 results, take the prefetched records, prefetch the next ---- */ \
-    "mcsfa_bend_%=:\n\t"                                                                          \
+    "mcsfa_bend_%=:\n\t" MCS_FA_T0                                                               \
     "s_max_u32 s81, s81, s80\n\t"                                                                 \
     "s_cmp_gt_u32 s81, " MCS_FA_POOLMAX##W "\n\t"                                                 \
     "s_cbranch_scc1 mcsfa_poolovf_%=\n\t"                                                         \
@@ -610,12 +637,12 @@ namespace {
     "global_load_dwordx4 v[98:101], v121, s[64:65]\n\t"                                           \
     "s_sub_u32 s41, s42, s57\n\t"                                                                 \
     "s_min_u32 s41, s41, 64\n\t"                                                                  \
-    "s_mov_b32 s47, 0\n\t" MCS_FA_REC##W                                                          \
+    "s_mov_b32 s47, 0\n\t" MCS_FA_REC##W MCS_FA_T1("s96")                                         \
     "s_branch mcsfa_inner_%=\n"                                                                   \
                                                                                                   \
     /* ---- exit: state back to the compiler's registers ---- */                                 \
     "mcsfa_exit_%=:\n\t"                                                                          \
-    "s_waitcnt vmcnt(0) lgkmcnt(0)\n\t"                                                           \
+    "s_waitcnt vmcnt(0) lgkmcnt(0)\n\t" MCS_FA_TEND                                               \
     "s_mov_b32 %[t], s40\n\t"                                                                     \
     "s_add_u32 %[r], s57, s47\n\t"                                                                \
     "s_mov_b32 %[flags], s44\n\t"                                                                 \
@@ -707,6 +734,9 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
     uint32_t frm = (1u << P) - 1u + (W == 16 ? 0x100u : 0u), lmin = kEmpty;
     uint32_t used = 0, peak = 0, waited = 0, n_slow = 0, n_rel = 0;
     uint32_t on = 0, os = 0, of = 0;
+#ifdef MCS_STAMPS
+    uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;
+#endif
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
@@ -714,6 +744,7 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
     : [t] "+s"(t), [r] "+s"(r), [flags] "+s"(flags), [hw] "+s"(have_w), [used] "+s"(used),      \
       [peak] "+s"(peak), [waited] "+s"(waited), [nslow] "+s"(n_slow), [nrel] "+s"(n_rel),       \
       [on] "+v"(on), [os] "+v"(os), [of] "+v"(of), [frm] "+v"(frm), [lmin] "+v"(lmin)            \
+      MCS_FA_STAMP_OUTS                                                                           \
     : [J] "s"(J), [jobs] "s"(jobs), [onp] "s"(o_node), [osp] "s"(o_start), [ofp] "s"(o_finish), \
       [c0] "v"(cur.x), [c1] "v"(cur.y), [c2] "v"(cur.z), [c3] "v"(cur.w), [pay] "v"(v_pay),     \
       [nb] "v"(v_nb), [nbase] "v"(v_nbase), [lane] "v"(lane), [sel0] "s"(sel0),                 \
@@ -736,6 +767,14 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
 #pragma clang diagnostic pop
 
     if (peak > (uint32_t)(P * kWave)) flags |= MCS_FLAG_OVERFLOW;  // a skipped insert
+#ifdef MCS_STAMPS
+    if (lane == 0) {
+        atomicAdd(&g_fa_stamps[0], (unsigned long long)st0);
+        atomicAdd(&g_fa_stamps[1], (unsigned long long)st1);
+        atomicAdd(&g_fa_stamps[2], (unsigned long long)st2);
+        atomicAdd(&g_fa_stamps[3], (unsigned long long)st3);
+    }
+#endif
     const uint32_t placed = r;  // FIFO places every job it decides, in order
     if (!(flags & MCS_FLAG_OVERFLOW)) {
         if (r > 0u) {  // the batch holding the last decision (earlier ones are stored)
@@ -824,3 +863,13 @@ hipError_t launch_fifo_asm(const FifoArgs& a, int npl, int pool, hipStream_t s) 
 }
 
 }  // namespace mcs
+
+#ifdef MCS_STAMPS
+// the probe build's segment cycles (releases, failed fits, batch ends, whole loop), summed over the
+// clusters of the launches since the last call; read and reset
+extern "C" int mcs_debug_fa_stamps(unsigned long long* out) {
+    unsigned long long z[4] = {0, 0, 0, 0};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_fa_stamps), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_fa_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
