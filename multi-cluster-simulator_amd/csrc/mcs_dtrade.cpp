@@ -38,6 +38,9 @@ struct DtradeDev {
     uint32_t* nv_all = nullptr;
     DtCtl* h_ctl = nullptr;
     hipGraphExec_t graph = nullptr;
+    hipGraphExec_t rgraph = nullptr;  // RCCL loop: kernels + all-gathers of kDtGraphTicks ticks
+    bool rgraph_tried = false;
+    uint32_t loop_form = kLoopGraph;
     bool begun = false;  // caller-driven lock-step in progress
     std::chrono::steady_clock::time_point w0{};
 };
@@ -161,6 +164,7 @@ int dt_run_once(mcs_engine* e, double* kernel_ms) {
         (void)hipGraphDestroy(g);
         if (st != hipSuccess) return dt_hip_fail(e, "hipGraphInstantiate", st);
     }
+    d->loop_form = kLoopGraph;
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
     for (;;) {
         HIPCHK(e, hipGraphLaunch(d->graph, e->stream));
@@ -183,8 +187,25 @@ int dt_run_rccl(mcs_engine* e, double* kernel_ms) {
     ncclComm_t comm = (ncclComm_t)e->comm;
     hipError_t st = launch_dtrade_init(d->a, e->stream);
     if (st != hipSuccess) return dt_hip_fail(e, "DELAY trading init", st);
+    auto tick = [&](hipStream_t s) -> bool {
+        if (launch_dtrade_step(d->a, s) != hipSuccess) return false;
+        if (ncclAllGather(d->xb + (size_t)e->rank * d->a.blk, d->xb, d->a.blk, ncclUint8, comm, s) != ncclSuccess)
+            return false;
+        return launch_dtrade_trader(d->a, s) == hipSuccess;
+    };
+    if (!d->rgraph_tried) {  // (no host enqueue per tick when RCCL can be captured)
+        d->rgraph_tried = true;
+        d->rgraph = capture_tick_graph(e->stream, kDtGraphTicks, tick);
+    }
+    d->loop_form = d->rgraph ? kLoopRcclGraph : kLoopRcclEager;
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
     for (;;) {
+        if (d->rgraph) {
+            HIPCHK(e, hipGraphLaunch(d->rgraph, e->stream));
+            if (int s = dt_poll(e)) return s;
+            if (d->h_ctl->done) break;
+            continue;
+        }
         for (uint32_t t = 0; t < kDtGraphTicks; ++t) {
             st = launch_dtrade_step(d->a, e->stream);
             if (st != hipSuccess) return dt_hip_fail(e, "dt_step_kernel", st);
@@ -242,6 +263,7 @@ void dtrade_free(mcs_engine* e) {
     if (!d) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (d->graph) (void)hipGraphExecDestroy(d->graph);
+    if (d->rgraph) (void)hipGraphExecDestroy(d->rgraph);
     dfree(d->tn);
     dfree(d->vn);
     dfree(d->vcap);
@@ -471,6 +493,7 @@ int dtrade_trade_stats(mcs_engine* e, mcs_trade_stats* out) {
     s.ticks = c.ticks;
     s.t_final = c.T;
     s.flags = flags;
+    s.loop_form = e->dtd->loop_form;
     float ms = 0.0f;
     if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) ms = 0.0f;
     s.kernel_ms = ms;

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -44,6 +45,35 @@ int auto_pool(uint32_t max_n);
 // per-cluster clock bound of the streams in HBM: last arrival and sum of (dur + 1 + extra)
 int stream_bounds(mcs_engine* e, std::vector<uint32_t>& last, std::vector<uint64_t>& sum);
 uint32_t horizon_extra(const mcs_engine* e);  // max_wait_s under DELAY, else 0
+
+// Lock-step tick loops: mcs_trade_stats.loop_form
+constexpr uint32_t kLoopGraph = 0;      // one engine, ticks replayed from a captured hipGraph
+constexpr uint32_t kLoopRcclEager = 1;  // RCCL all-gather per tick, launches enqueued eagerly
+constexpr uint32_t kLoopRcclGraph = 2;  // RCCL all-gather per tick, captured with the kernels
+
+// Capture `ticks` ticks of `tick(stream)` (kernels and the RCCL all-gather) into one executable
+// graph.  Returns nullptr, with the stream out of capture mode and the HIP error state cleared, when
+// any step of the capture fails (the caller then keeps the eager loop); MCS_RCCL_GRAPH=0 skips it.
+template <class F>
+hipGraphExec_t capture_tick_graph(hipStream_t s, uint32_t ticks, F&& tick) {
+    if (const char* env = getenv("MCS_RCCL_GRAPH"))
+        if (atoi(env) == 0) return nullptr;
+    hipGraph_t g = nullptr;
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    bool ok = true;
+    for (uint32_t t = 0; t < ticks && ok; ++t) ok = tick(s);
+    const hipError_t ec = hipStreamEndCapture(s, &g);
+    hipGraphExec_t x = nullptr;
+    if (ok && ec == hipSuccess && g) {
+        if (hipGraphInstantiate(&x, g, nullptr, nullptr, 0) != hipSuccess) x = nullptr;
+    }
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    return x;
+}
 }  // namespace mcs
 
 struct mcs_engine {
@@ -58,6 +88,9 @@ struct mcs_engine {
     uint32_t max_n = 0;
     bool free_lt31 = false;  // every node free value < 2^31 - 1 (fifo_asm_kernel<32> guard bits)
     bool free_lt15 = false;  // every node free value < 2^15 - 1 (fifo_asm_kernel<16>)
+    uint32_t n_cus = 256;    // compute units of the device
+    uint32_t win_shift = 0xFFFFFFFFu;  // form T's window shift for the current streams
+    bool win_known = false;
     uint64_t total_nodes = 0, total_jobs = 0;
     std::vector<uint32_t> node_off;
     std::vector<uint64_t> job_off;

@@ -38,6 +38,9 @@ struct TradeDev {
     TrCtl* h_ctl = nullptr;  // pinned
     hipGraphExec_t graph = nullptr;
     uint32_t graph_ticks = 0;
+    hipGraphExec_t rgraph = nullptr;  // RCCL loop: kernels + all-gathers of kGraphTicks ticks
+    bool rgraph_tried = false;
+    uint32_t loop_form = kLoopGraph;
     bool begun = false;
     std::chrono::steady_clock::time_point w0;
 };
@@ -181,6 +184,7 @@ int run_local(mcs_engine* e) {
         if (st != hipSuccess) return hip_fail(e, "hipGraphInstantiate", st);
         td->graph_ticks = kGraphTicks;
     }
+    td->loop_form = kLoopGraph;
     for (;;) {
         HIPCHK(e, hipGraphLaunch(td->graph, e->stream));
         if (int s = poll_ctl(e)) return s;
@@ -194,18 +198,38 @@ int nccl_fail(mcs_engine* e, const char* what, ncclResult_t r) {
 
 // N engines (one per GPU): a tick's one exchange is the in-place ncclAllGather of the ranks'
 // blocks over xGMI between phase A and the replicated phases B-D
+// Captured once into a hipGraph of kGraphTicks ticks (kernels and all-gathers: no host enqueue per
+// tick); eager when the capture is refused.  Every rank captures and replays the same
+// sequence, so the collectives stay matched.
 int run_rccl(mcs_engine* e) {
     TradeDev* td = e->td;
     const TradeArgs& a = td->a;
     ncclComm_t comm = (ncclComm_t)e->comm;
+    auto tick = [&](hipStream_t s) -> bool {
+        if (launch_trade_phase(a, 0, s) != hipSuccess) return false;
+        if (ncclAllGather(td->xb + (size_t)e->rank * a.blk, td->xb, a.blk, ncclUint8, comm, s) != ncclSuccess)
+            return false;
+        for (int p = 1; p < 4; ++p)
+            if (launch_trade_phase(a, p, s) != hipSuccess) return false;
+        return true;
+    };
+    if (!td->rgraph_tried) {
+        td->rgraph_tried = true;
+        td->rgraph = capture_tick_graph(e->stream, kGraphTicks, tick);
+    }
+    td->loop_form = td->rgraph ? kLoopRcclGraph : kLoopRcclEager;
     for (;;) {
-        for (uint32_t t = 0; t < kGraphTicks; ++t) {
-            if (int s = launch_phase(e, a, 0)) return s;
-            const ncclResult_t r = ncclAllGather(td->xb + (size_t)e->rank * a.blk, td->xb, a.blk, ncclUint8,
-                                                 comm, e->stream);
-            if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(exchange blocks)", r);
-            for (int p = 1; p < 4; ++p)
-                if (int s = launch_phase(e, a, p)) return s;
+        if (td->rgraph) {
+            HIPCHK(e, hipGraphLaunch(td->rgraph, e->stream));
+        } else {
+            for (uint32_t t = 0; t < kGraphTicks; ++t) {
+                if (int s = launch_phase(e, a, 0)) return s;
+                const ncclResult_t r = ncclAllGather(td->xb + (size_t)e->rank * a.blk, td->xb, a.blk, ncclUint8,
+                                                     comm, e->stream);
+                if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(exchange blocks)", r);
+                for (int p = 1; p < 4; ++p)
+                    if (int s = launch_phase(e, a, p)) return s;
+            }
         }
         if (int s = poll_ctl(e)) return s;
         if (td->h_ctl->done) return MCS_OK;
@@ -237,6 +261,7 @@ int fill_stats(mcs_engine* e, mcs_trade_stats* ts, mcs_stats* st) {
     s.ticks = c.ticks;
     s.t_final = c.T;
     s.flags = flags;
+    s.loop_form = td->loop_form;
     if (ts) *ts = s;
     if (st) {
         st->jobs = e->total_jobs;
@@ -263,6 +288,7 @@ void trade_free(mcs_engine* e) {
     if (!td) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (td->graph) (void)hipGraphExecDestroy(td->graph);
+    if (td->rgraph) (void)hipGraphExecDestroy(td->rgraph);
     dfree(td->tn);
     dfree(td->cl);
     dfree(td->sfin);

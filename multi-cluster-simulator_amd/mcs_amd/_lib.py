@@ -179,7 +179,7 @@ class mcs_trade_stats(C.Structure):
         ("ticks", C.c_uint32),
         ("t_final", C.c_uint32),
         ("flags", C.c_uint32),
-        ("pad", C.c_uint32),
+        ("loop_form", C.c_uint32),
         ("kernel_ms", C.c_double),
         ("wall_ms", C.c_double),
     ]

@@ -1,5 +1,5 @@
-"""Two-rank lock-step DELAY trading run on ONE GPU (tests/test_gpu_dtrade.py): two processes, each an
-engine holding half of the clusters on device 0, exchanging one block per rank per tick (cluster
+"""N-rank lock-step DELAY trading run on ONE GPU (tests/test_gpu_dtrade.py): WORLD processes (env
+MCS_WORLD, default 2), each an engine holding one block of the clusters on device 0, exchanging one block per rank per tick (cluster
 records + node snapshots) over torch.distributed gloo through the caller-driven phase API
 (include/mcs_trade.h).  The trader rounds run replicated on both ranks.  Rank 0 checks the union of
 the placements, and every rank's replicated trade / Foreign logs, against the CPU oracle of the
@@ -14,8 +14,10 @@ for p in (os.path.join(REPO, "multi-cluster-simulator_amd"), REPO, HERE):
 
 import numpy as np  # noqa: E402
 
-WORLD = 2
-CASES = [("small", 16, 600), ("n64_hot", 8, 2000)]
+WORLD = int(os.environ.get("MCS_WORLD", "2"))
+# env MCS_DTRADE_CASES = "kind:clusters:jobs,..." (default: 16 cluster_small x 600, 8 n64_hot x 2000)
+CASES = [(k, int(c), int(j)) for k, c, j in
+         (x.split(":") for x in os.environ.get("MCS_DTRADE_CASES", "small:16:600,n64_hot:8:2000").split(","))]
 
 
 def one_case(rank, kind, C, J):
@@ -64,7 +66,7 @@ def one_case(rank, kind, C, J):
         won = int((o["trades"]["winner"] >= 0).sum())
         assert won > 0, kind  # the scenario exercises winning trades (Foreign jobs across ranks)
         cross = int(np.sum((o["foreign"]["requester"] // per) != (o["foreign"]["responder"] // per)))
-        print(f"DTRADE-2RANK {kind} C={C} J={J}: {len(o['trades'])} trades, {won} won, "
+        print(f"DTRADE-2RANK world {WORLD} {kind} C={C} J={J}: {len(o['trades'])} trades, {won} won, "
               f"{o['n_foreign']} Foreign jobs ({cross} across ranks)", flush=True)
     dist.barrier()
 

@@ -113,9 +113,26 @@ def test_gpu_dtrade_two_ranks_gloo():
     assert "DTRADE-2RANK OK" in r.stdout
 
 
-def test_gpu_dtrade_rccl_loop_world1():
+def test_gpu_dtrade_four_ranks_gloo():
+    """world = 4: a 64-cluster DELAY trading system (16 clusters per rank, reduced jobs) and a hot
+    32-cluster one, four processes on device 0 over gloo == the oracle of the whole system."""
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29589", MCS_WORLD="4",
+               MCS_DTRADE_CASES="small:64:300,n64_hot:32:600")
+    r = subprocess.run([sys.executable, os.path.join(here, "dtrade_2rank.py")], env=env, capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "DTRADE-2RANK OK" in r.stdout
+
+
+@pytest.mark.parametrize("graph", ["1", "0"])
+def test_gpu_dtrade_rccl_loop_world1(graph, monkeypatch):
     """The RCCL tick loop (shape all-reduce, one in-place ncclAllGather of the exchange blocks per
     tick, mcs_dtrade.cpp dt_run_rccl) on a world-1 communicator == the graph-replayed loop."""
+    monkeypatch.setenv("MCS_RCCL_GRAPH", graph)  # 1: kernels + all-gathers captured in a hipGraph; 0: eager
     arrays, streams, _ = seeded_workload("n64_hot", 8, 2000)
     g = run(arrays, streams)
     with Engine(0, policy="DELAY", trader=True) as eng:
@@ -124,6 +141,7 @@ def test_gpu_dtrade_rccl_loop_world1():
         eng.comm_init(Engine.comm_unique_id())
         eng.submit_jobs(streams)
         eng.run()
+        assert eng.trade_stats()["loop_form"] == (2 if graph == "1" else 1)
         node, start, fin = eng.placements()
         trades, foreign = eng.contracts(), eng.foreign()
         vn = eng.virtual_nodes()

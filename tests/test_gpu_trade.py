@@ -119,9 +119,23 @@ def test_gpu_trade_two_ranks_one_gpu():
     assert "TRADE-2RANK OK" in r.stdout
 
 
-def test_gpu_trade_rccl_loop_world1():
-    """The RCCL tick loop (three ncclAllGather per tick, mcs_trade.cpp run_rccl) on a world-1
+def test_gpu_trade_four_ranks_one_gpu():
+    """world = 4 shards of a 64-cluster system (the C5 shape: 64 clusters, reduced jobs), four
+    processes on device 0 exchanging blocks over gloo: rank offsets rank * blk beyond rank 1, the
+    replicated trader rounds and escalation on four ranks == the oracle of the whole system."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29585", MCS_WORLD="4",
+               MCS_TRADE_CASE="n64_hot:64:300")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "trade_2rank.py")], env=env, capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "TRADE-2RANK OK world 4" in r.stdout
+
+
+@pytest.mark.parametrize("graph", ["1", "0"])
+def test_gpu_trade_rccl_loop_world1(graph, monkeypatch):
+    """The RCCL tick loop (one ncclAllGather per tick, mcs_trade.cpp run_rccl), captured in a hipGraph or eager, on a world-1
     communicator == the HBM-exchange loop: exercises the RCCL transport on a one-GPU box."""
+    monkeypatch.setenv("MCS_RCCL_GRAPH", graph)  # 1: kernels + all-gathers captured in a hipGraph; 0: eager
     arrays, streams, _ = seeded_workload("n64_hot", 8, 1500)
     want = gpu_trade(arrays, streams)
     with Engine(0, borrow=True, trader=True, t_max_s=20_000_000) as eng:
@@ -130,6 +144,7 @@ def test_gpu_trade_rccl_loop_world1():
         eng.comm_init(Engine.comm_unique_id())
         eng.submit_jobs(streams)
         eng.run()
+        assert eng.trade_stats()["loop_form"] == (2 if graph == "1" else 1)
         node, start, fin = eng.placements()
         got = dict(lent=eng.lent(), trades=eng.trades(), vn=eng.virtual_nodes(), ts=eng.trade_stats())
     np.testing.assert_array_equal(node, want["node"])

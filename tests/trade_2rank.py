@@ -1,6 +1,6 @@
-"""Two-rank lock-step trading run on ONE GPU (tests/test_gpu_trade.py): two processes, each an
-engine holding half of the clusters on device 0, exchanging the per-tick records over
-torch.distributed gloo through the caller-driven phase API (include/mcs_trade.h).  Rank 0 checks
+"""N-rank lock-step trading run on ONE GPU (tests/test_gpu_trade.py): WORLD processes (env
+MCS_WORLD, default 2), each an engine holding one block of the clusters on device 0, exchanging
+the per-tick records over torch.distributed gloo through the caller-driven phase API (include/mcs_trade.h).  Rank 0 checks
 the union against the CPU oracle.  Prints TRADE-2RANK OK on success."""
 import os
 import sys
@@ -12,7 +12,9 @@ for p in (os.path.join(REPO, "multi-cluster-simulator_amd"), REPO, HERE):
 
 import numpy as np  # noqa: E402
 
-WORLD = 2
+WORLD = int(os.environ.get("MCS_WORLD", "2"))
+# the system: env MCS_TRADE_CASE = "kind:clusters:jobs" (default 8 n64_hot clusters x 1500 jobs)
+KIND, C_SYS, J_SYS = (lambda k, c, j: (k, int(c), int(j)))(*os.environ.get("MCS_TRADE_CASE", "n64_hot:8:1500").split(":"))
 
 
 def shard(arrays, streams, lo, hi):
@@ -37,8 +39,8 @@ def worker(rank):
     from mcs_amd.shard import run_lockstep, torch_allgather
 
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
-    C, J = 8, 1500
-    arrays, streams, gp = seeded_workload("n64_hot", C, J)
+    C, J = C_SYS, J_SYS
+    arrays, streams, gp = seeded_workload(KIND, C, J)
     per = C // WORLD
     a, s = shard(arrays, streams, rank * per, rank * per + per)
     with Engine(0, borrow=True, trader=True) as eng:
@@ -78,7 +80,8 @@ def worker(rank):
             assert trade_rows(p["trades"]) == trade_rows(o["trades"])
             assert p["vn"].tolist() == o["virtual_nodes"].tolist()
             assert p["t_final"] == o["t_final"]
-        print("TRADE-2RANK OK", len(lent), "lent runs", len(o["trades"]), "trades", flush=True)
+        print("TRADE-2RANK OK", f"world {WORLD}, {C} clusters:", len(lent), "lent runs", len(o["trades"]), "trades",
+              flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
