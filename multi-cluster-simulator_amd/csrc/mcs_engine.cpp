@@ -217,12 +217,6 @@ int mcs_engine_create(const mcs_config* cfg, int device, mcs_engine** out) {
         mcs_engine_destroy(e);
         return MCS_E_HIP;
     }
-    {
-        hipDeviceProp_t prop;
-        e->n_cus = hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0
-                       ? (uint32_t)prop.multiProcessorCount
-                       : 256u;
-    }
     *out = e;
     return MCS_OK;
 }
@@ -332,7 +326,6 @@ static int alloc_jobs(mcs_engine* e, const uint64_t* job_offsets, bool records) 
     mcs::trade_free(e);
     mcs::dtrade_free(e);
     e->has_jobs = e->has_run = false;
-    e->win_known = false;
     e->job_off.assign(job_offsets, job_offsets + e->C + 1);
     e->total_jobs = job_offsets[e->C];
     const size_t nj = e->total_jobs ? e->total_jobs : 1;
@@ -560,16 +553,6 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
         for (uint32_t c = 0; c < e->C; ++c) jmax = std::max<uint64_t>(jmax, e->job_off[c + 1] - e->job_off[c]);
         if (jmax <= mcs::kAsmMaxJobs) a.guard_ok |= 4u;
     }
-    a.n_cus = e->n_cus;
-    a.win_shift = mcs::kNoWindow;
-    if (!delay && npl == 4 && pool == 8 && e->free_lt15 && !e->gen.on && e->d_jobs) {
-        /* form T's window (once per job stream): the longest duration and the largest job rate */
-        if (!e->win_known) {
-            HIPCHK(e, mcs::fifo_window_shift(e->d_jobs, e->d_job_off, e->C, e->stream, &e->win_shift));
-            e->win_known = true;
-        }
-        a.win_shift = e->win_shift;
-    }
     mcs::DelayArgs da{};
     da.node_free0 = e->d_free0;
     da.node_off = e->d_node_off;
@@ -594,7 +577,6 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     HIPCHK(e, hipMemsetAsync(e->d_totals, 0, sizeof(mcs::Totals), e->stream));
     switch (delay ? -1 : mcs::fifo_asm_form(a, npl, pool, false)) {
         case -1: e->last_kernel = "mcs::delay_kernel"; break;
-        case 19: e->last_kernel = "mcs::fifo_asm_t_kernel"; break;
         case 18: e->last_kernel = "mcs::fifo_asm_kernel<16, true, 1, 2>"; break;
         case 17: e->last_kernel = "mcs::fifo_asm_kernel<16, true, 4, 8>"; break;
         case 16: e->last_kernel = "mcs::fifo_asm_kernel<16, false, 4, 8>"; break;

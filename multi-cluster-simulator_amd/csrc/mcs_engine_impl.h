@@ -88,9 +88,6 @@ struct mcs_engine {
     uint32_t max_n = 0;
     bool free_lt31 = false;  // every node free value < 2^31 - 1 (fifo_asm_kernel<32> guard bits)
     bool free_lt15 = false;  // every node free value < 2^15 - 1 (fifo_asm_kernel<16>)
-    uint32_t n_cus = 256;    // compute units of the device
-    uint32_t win_shift = 0xFFFFFFFFu;  // form T's window shift for the current streams
-    bool win_known = false;
     uint64_t total_nodes = 0, total_jobs = 0;
     std::vector<uint32_t> node_off;
     std::vector<uint64_t> job_off;

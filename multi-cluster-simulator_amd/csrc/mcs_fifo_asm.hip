@@ -817,553 +817,6 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
     }
 }
 
-
-// ---- form T: the finish time picks the slot row (low occupancy) ------------------
-// At one cluster wave per SIMD (<= 4 per CU: C4 strong shards of 1024 clusters or fewer per GPU)
-// the loop is a lone dependency chain and W16R's release dominates it: all 8 slot rows tested and
-// branched over at every clock advance, then a DPP minimum for the next completion.  Here a running
-// slot lives in the row of its finish's 2^k-second window (row = (finish >> k) & 63; the host picks
-// k so that 63 windows exceed the longest duration and a window holds about half a row):
-//   * finish times in v128..v191 (one row per window), {payload, node LDS address} in an LDS slot
-//     table [68][64] u64; the insert lane is the lowest free lane of the finish's row (a VALU
-//     compare issued with the fit test, off the decision chain); a row is addressed by an indexed
-//     v_mov (s_set_gpr_idx_on, VOP1: the form LLVM uses for indirect VGPR access) into v119;
-//   * a release at t visits only the window rows from the earliest finish's to t's (almost always
-//     one): a compare, the expired lanes' slot words, and ds_add of each payload to its node;
-//   * the wave's earliest finish (s77) is a lower bound (t + 1 after a release); a failed fit,
-//     which needs the exact value, takes the first non-empty row in window order (rows hold
-//     disjoint, increasing windows) and its DPP minimum;
-//   * a full row spills into rows 64..67 (v192..v195), released whenever their bound is due; no free
-//     spill slot is a pool overflow (the engine re-runs the cluster on the compiled kernel with a
-//     larger pool).
-// Same decisions, same results bit for bit as every other form (tests/test_gpu_parity.py).
-#define MCS_FT_LOOP(D) \
-    /* ---- entry: state into the fixed registers; every slot row empty ---- */ \
-    "s_mov_b32 s40, %[t]\n\t" \
-    "s_mov_b32 s42, %[J]\n\t" \
-    "s_mov_b32 s43, 0\n\t" \
-    "s_mov_b32 s44, 0\n\t" \
-    "s_mov_b32 s47, 0\n\t" \
-    "s_mov_b32 s57, 0\n\t" \
-    "s_mov_b32 s78, 0\n\t" \
-    "s_lshl2_add_u32 s79, s42, 0x100\n\t" \
-    "s_mov_b32 s80, 0\n\t" \
-    "s_mov_b32 s81, 0\n\t" \
-    "s_mov_b32 s82, 0\n\t" \
-    "s_mov_b32 s83, 0\n\t" \
-    "s_mov_b32 s84, 0\n\t" \
-    "s_mov_b32 s77, -1\n\t" /* nothing running */ \
-    "s_mov_b32 s88, 0\n\t" /* spill slots in use */ \
-    "s_mov_b32 s89, -1\n\t" /* their earliest finish (bound) */ \
-    "s_mov_b32 s49, %[kw]\n\t" /* window shift: row = (finish >> s49) & 63 */ \
-    "s_mov_b64 s[64:65], %[jobs]\n\t" \
-    "s_mov_b64 s[66:67], %[onp]\n\t" \
-    "s_mov_b64 s[68:69], %[osp]\n\t" \
-    "s_mov_b64 s[70:71], %[ofp]\n\t" \
-    "s_mov_b32 s72, %[sel0]\n\t" \
-    "s_mov_b32 s73, %[sel1]\n\t" \
-    "v_mov_b32 v94, %[c0]\n\t" \
-    "v_mov_b32 v95, %[c1]\n\t" \
-    "v_mov_b32 v96, %[c2]\n\t" \
-    "v_mov_b32 v97, %[c3]\n\t" \
-    "v_mov_b32 v107, %[pay]\n\t" \
-    "v_mov_b32 v108, %[nb]\n\t" \
-    "v_mov_b32 v110, %[lane]\n\t" \
-    "s_mov_b32 s76, 0\n\t" \
-    "mcsft_init_%=:\n\t" \
-    "s_set_gpr_idx_on s76, gpr_idx(DST)\n\t" \
-    "v_mov_b32 v128, -1\n\t" \
-    "s_set_gpr_idx_off\n\t" \
-    "s_add_u32 s76, s76, 1\n\t" \
-    "s_cmp_lt_u32 s76, 68\n\t" \
-    "s_cbranch_scc1 mcsft_init_%=\n\t" \
-    MCS_FA_RELOAD16 "s_waitcnt lgkmcnt(0)\n\t" \
-    "v_lshlrev_b32 v121, 4, v110\n\t" \
-    "v_add_u32 v121, 0x400, v121\n\t" \
-    "global_load_dwordx4 v[98:101], v121, s[64:65]\n\t" \
-    "s_min_u32 s41, s42, 64\n\t" MCS_FA_REC16 \
-    "s_cmp_lt_u32 s47, s41\n\t" \
-    "s_cbranch_scc0 mcsft_bend_%=\n\t" \
-    /* ---- one pass = one decision (scheduler.go:216-296) ---- */ \
-    "mcsft_inner_%=:\n\t" \
-    "s_cmp_gt_u32 s45, s40\n\t" \
-    "s_cbranch_scc1 mcsft_arrive_%=\n\t" \
-    "s_add_u32 s55, s40, s46\n\t" /* finish */ \
-    "s_lshr_b32 s86, s55, s49\n\t" \
-    "s_and_b32 s86, s86, 63\n\t" /* its window row */ \
-    /* first fit (scheduler.go:129-137), the row's free lanes between the last SDWA write and */ \
-    /* the v_perm that reads it (see MCS_FA_FIT16) */ \
-    "v_pk_sub_u16 v72, v64, s48\n\t" \
-    "v_pk_sub_u16 v73, v65, s48\n\t" \
-    "v_pk_sub_u16 v74, v66, s48\n\t" \
-    "v_pk_sub_u16 v75, v67, s48\n\t" \
-    "v_and_b32_sdwa v80, v72, v72 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
-    "v_and_b32_sdwa v81, v74, v74 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
-    "v_and_b32_sdwa v80, v73, v73 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
-    "v_and_b32_sdwa v81, v75, v75 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
-    "s_set_gpr_idx_on s86, gpr_idx(SRC0)\n\t" \
-    "v_mov_b32 v119, v128\n\t" \
-    "s_set_gpr_idx_off\n\t" \
-    "v_cmp_eq_u32_e64 s[60:61], v119, -1\n\t" \
-    "v_perm_b32 v86, v81, v80, s72\n\t" \
-    "v_cmp_ne_u32_e32 vcc, 0, v86\n\t" \
-    "s_cbranch_vccz mcsft_nofit_%=\n\t" \
-    "s_ff1_i32_b64 s50, vcc\n\t" /* lowest lane with a fit */ \
-    "s_cmp_eq_u32 s46, 0\n\t" \
-    "s_cbranch_scc1 mcsft_zero_%=\n\t" \
-    /* decided: the fitting lane's first chunk, the commit (cluster.go:146-147) under exec = that */ \
-    /* lane, then the slot in the finish's window row under exec = its lowest free lane */ \
-    "v_readlane_b32 s51, v86, s50\n\t" \
-    "s_ff1_i32_b64 s85, s[60:61]\n\t" /* -1: the row is full */ \
-    "s_lshl_b64 exec, 1, s50\n\t" \
-    "s_ff1_i32_b32 s52, s51\n\t" \
-    "s_lshr_b32 s53, s52, 3\n\t" \
-    "s_lshl3_add_u32 s54, s52, s50\n\t" /* kx = chunk * 64 + lane */ \
-    "s_set_gpr_idx_on s53, gpr_idx(SRC0,DST)\n\t" \
-    "v_mov_b32 v64, v72\n\t" \
-    "s_set_gpr_idx_off\n\t" \
-    "s_lshl2_add_u32 s87, s54, s73\n\t" /* the node's LDS address */ \
-    "s_cmp_eq_u32 s85, -1\n\t" \
-    "s_cbranch_scc1 mcsft_spill_%=\n\t" \
-    "s_lshl_b32 s76, s86, 9\n\t" \
-    "s_lshl_b64 exec, 1, s85\n\t" \
-    "v_add_u32 v117, s76, v107\n\t" \
-    "v_mov_b32 v112, s48\n\t" \
-    "v_mov_b32 v113, s87\n\t" \
-    "ds_write_b64 v117, v[112:113]\n\t" /* {payload, node address} */ \
-    "s_set_gpr_idx_on s86, gpr_idx(DST)\n\t" \
-    "v_mov_b32 v128, s55\n\t" /* the finish */ \
-    "s_set_gpr_idx_off\n\t" \
-    "mcsft_ins_%=:\n\t" \
-    "s_min_u32 s77, s77, s55\n\t" \
-    "s_mov_b64 exec, -1\n\t" \
-    "s_mov_b32 m0, s47\n\t" \
-    "s_add_u32 s80, s80, 1\n\t" \
-    "v_writelane_b32 v91, s54, m0\n\t" \
-    "v_writelane_b32 v92, s40, m0\n\t" \
-    /* next ready job; a WaitQueue head placed sleeps 1 s (:250) */ \
-    "mcsft_placed_%=:\n\t" \
-    "s_add_u32 s47, s47, 1\n\t" MCS_FA_REC16 \
-    "mcsft_loopend_%=:\n\t" \
-    "s_cmp_lt_u32 s47, s41\n\t" \
-    "s_cbranch_scc1 mcsft_inner_%=\n\t" \
-    "s_cmp_lg_u32 s43, 0\n\t" \
-    "s_cbranch_scc0 mcsft_bend_%=\n\t" \
-    "s_sub_u32 s41, s42, s57\n\t" \
-    "s_min_u32 s41, s41, 64\n\t" \
-    "s_branch mcsft_hwadv_%=\n\t" \
-    /* zero-duration job: committed and released before the next decision (D3) */ \
-    "mcsft_zero_%=:\n\t" MCS_FA_ZEROKX16 \
-    "v_writelane_b32 v91, s54, m0\n\t" \
-    "v_writelane_b32 v92, s40, m0\n\t" \
-    "s_branch mcsft_placed_%=\n\t" \
-    /* the finish's row is full: the spill rows (64-67), released whenever their bound is due */ \
-    "mcsft_spill_%=:\n\t" \
-    "s_mov_b64 exec, -1\n\t" \
-    "v_cmp_eq_u32_e64 s[62:63], v192, -1\n\t" \
-    "s_ff1_i32_b64 s85, s[62:63]\n\t" \
-    "s_cmp_lg_u32 s85, -1\n\t" \
-    "s_cbranch_scc1 mcsft_sp0_%=\n\t" \
-    "v_cmp_eq_u32_e64 s[62:63], v193, -1\n\t" \
-    "s_ff1_i32_b64 s85, s[62:63]\n\t" \
-    "s_cmp_lg_u32 s85, -1\n\t" \
-    "s_cbranch_scc1 mcsft_sp1_%=\n\t" \
-    "v_cmp_eq_u32_e64 s[62:63], v194, -1\n\t" \
-    "s_ff1_i32_b64 s85, s[62:63]\n\t" \
-    "s_cmp_lg_u32 s85, -1\n\t" \
-    "s_cbranch_scc1 mcsft_sp2_%=\n\t" \
-    "v_cmp_eq_u32_e64 s[62:63], v195, -1\n\t" \
-    "s_ff1_i32_b64 s85, s[62:63]\n\t" \
-    "s_cmp_lg_u32 s85, -1\n\t" \
-    "s_cbranch_scc1 mcsft_sp3_%=\n\t" \
-    "s_or_b32 s44, s44, %[fov]\n\t" /* no free slot: the engine re-runs the cluster with a larger pool */ \
-    "s_branch mcsft_exit_%=\n\t" \
-    "mcsft_sp0_%=:\n\t" \
-    "s_lshl_b64 exec, 1, s85\n\t" \
-    "v_add_u32 v117, 32768, v107\n\t" \
-    "v_mov_b32 v112, s48\n\t" \
-    "v_mov_b32 v113, s87\n\t" \
-    "ds_write_b64 v117, v[112:113]\n\t" \
-    "v_mov_b32 v192, s55\n\t" \
-    "s_add_u32 s88, s88, 1\n\t" \
-    "s_min_u32 s89, s89, s55\n\t" \
-    "s_branch mcsft_ins_%=\n\t" \
-    "mcsft_sp1_%=:\n\t" \
-    "s_lshl_b64 exec, 1, s85\n\t" \
-    "v_add_u32 v117, 33280, v107\n\t" \
-    "v_mov_b32 v112, s48\n\t" \
-    "v_mov_b32 v113, s87\n\t" \
-    "ds_write_b64 v117, v[112:113]\n\t" \
-    "v_mov_b32 v193, s55\n\t" \
-    "s_add_u32 s88, s88, 1\n\t" \
-    "s_min_u32 s89, s89, s55\n\t" \
-    "s_branch mcsft_ins_%=\n\t" \
-    "mcsft_sp2_%=:\n\t" \
-    "s_lshl_b64 exec, 1, s85\n\t" \
-    "v_add_u32 v117, 33792, v107\n\t" \
-    "v_mov_b32 v112, s48\n\t" \
-    "v_mov_b32 v113, s87\n\t" \
-    "ds_write_b64 v117, v[112:113]\n\t" \
-    "v_mov_b32 v194, s55\n\t" \
-    "s_add_u32 s88, s88, 1\n\t" \
-    "s_min_u32 s89, s89, s55\n\t" \
-    "s_branch mcsft_ins_%=\n\t" \
-    "mcsft_sp3_%=:\n\t" \
-    "s_lshl_b64 exec, 1, s85\n\t" \
-    "v_add_u32 v117, 34304, v107\n\t" \
-    "v_mov_b32 v112, s48\n\t" \
-    "v_mov_b32 v113, s87\n\t" \
-    "ds_write_b64 v117, v[112:113]\n\t" \
-    "v_mov_b32 v195, s55\n\t" \
-    "s_add_u32 s88, s88, 1\n\t" \
-    "s_min_u32 s89, s89, s55\n\t" \
-    "s_branch mcsft_ins_%=\n\t" \
-    "mcsft_hwadv_%=:\n\t" \
-    "s_mov_b32 s43, 0\n\t" \
-    "s_add_u32 s40, s40, 1\n\t" \
-    "s_cbranch_scc1 mcsft_clkovf_%=\n\t" \
-    "s_branch mcsft_adv_%=\n\t" \
-    /* no node fits: WaitQueue append (:264-268), sleep to the next completion (A.3) */ \
-    "mcsft_nofit_%=:\n\t" \
-    "s_sub_u32 s76, 1, s43\n\t" \
-    "s_add_u32 s82, s82, s76\n\t" \
-    "s_mov_b32 s43, 1\n\t" \
-    "s_add_u32 s41, s47, 1\n\t" \
-    MCS_FA_CNTS_##D \
-    "s_add_u32 s78, s78, 1\n\t" \
-    "s_cmp_gt_u32 s78, s79\n\t" \
-    "s_cbranch_scc1 mcsft_poolovf_%=\n\t" \
-    "s_cmp_eq_u32 s80, 0\n\t" /* nothing running: the head never fits */ \
-    "s_cbranch_scc1 mcsft_deadlock_%=\n\t" \
-    /* the exact earliest finish (s77 is a lower bound): the first window row from s77's that */ \
-    /* holds a slot has it (rows hold disjoint, increasing windows), then the spill rows */ \
-    "s_lshr_b32 s90, s77, s49\n\t" \
-    "s_add_u32 s91, s90, 64\n\t" \
-    "mcsft_nfrow_%=:\n\t" \
-    "s_and_b32 s86, s90, 63\n\t" \
-    "s_set_gpr_idx_on s86, gpr_idx(SRC0)\n\t" \
-    "v_mov_b32 v120, v128\n\t" \
-    "s_set_gpr_idx_off\n\t" \
-    "v_cmp_ne_u32_e32 vcc, -1, v120\n\t" \
-    "s_cbranch_vccnz mcsft_nffound_%=\n\t" \
-    "s_add_u32 s90, s90, 1\n\t" \
-    "s_cmp_lt_u32 s90, s91\n\t" \
-    "s_cbranch_scc1 mcsft_nfrow_%=\n\t" \
-    "v_mov_b32 v120, -1\n\t" /* only spill slots run */ \
-    "mcsft_nffound_%=:\n\t" \
-    "s_cmp_eq_u32 s88, 0\n\t" \
-    "s_cbranch_scc1 mcsft_nfmin_%=\n\t" \
-    "v_min3_u32 v120, v120, v192, v193\n\t" \
-    "v_min3_u32 v120, v120, v194, v195\n\t" \
-    "mcsft_nfmin_%=:\n\t" \
-    "s_nop 1\n\t" \
-    "v_min_u32_dpp v120, v120, v120 row_shr:1 row_mask:0xf bank_mask:0xf\n\t" \
-    "s_nop 1\n\t" \
-    "v_min_u32_dpp v120, v120, v120 row_shr:2 row_mask:0xf bank_mask:0xf\n\t" \
-    "s_nop 1\n\t" \
-    "v_min_u32_dpp v120, v120, v120 row_shr:4 row_mask:0xf bank_mask:0xf\n\t" \
-    "s_nop 1\n\t" \
-    "v_min_u32_dpp v120, v120, v120 row_shr:8 row_mask:0xf bank_mask:0xf\n\t" \
-    "s_nop 1\n\t" \
-    "v_min_u32_dpp v120, v120, v120 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t" \
-    "s_nop 1\n\t" \
-    "v_min_u32_dpp v120, v120, v120 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t" \
-    "s_nop 1\n\t" \
-    "v_readlane_b32 s77, v120, 63\n\t" \
-    "s_add_u32 s40, s40, 1\n\t" \
-    "s_cbranch_scc1 mcsft_clkovf_%=\n\t" \
-    "s_max_u32 s40, s40, s77\n\t" /* (every running job finishes after t: no wrap) */ \
-    "s_branch mcsft_adv_%=\n\t" \
-    "mcsft_arrive_%=:\n\t" \
-    "s_mov_b32 s40, s45\n\t" /* (> t) */ \
-    MCS_FA_CNTS_##D \
-    /* the clock has advanced: releases at the new instant (A.2 step 1, cluster.go:153-157) */ \
-    "mcsft_adv_%=:\n\t" \
-    "s_cmp_lt_u32 s40, s77\n\t" /* nothing can finish by t */ \
-    "s_cbranch_scc1 mcsft_loopend_%=\n\t" \
-    MCS_FA_CNTR_##D \
-    "s_max_u32 s81, s81, s80\n\t" /* peak: used only grows between releases */ \
-    "ds_write_b32 v108, v64 offset:0\n\t" /* the LDS node copy from the registers */ \
-    "ds_write_b32 v108, v65 offset:256\n\t" \
-    "ds_write_b32 v108, v66 offset:512\n\t" \
-    "ds_write_b32 v108, v67 offset:768\n\t" \
-    "s_mov_b32 s75, 0\n\t" \
-    /* the window rows from the earliest finish's to t's (at most all 64) */ \
-    "s_lshr_b32 s90, s77, s49\n\t" \
-    "s_lshr_b32 s91, s40, s49\n\t" \
-    "s_sub_u32 s76, s91, s90\n\t" \
-    "s_cmp_gt_u32 s76, 63\n\t" \
-    "s_cbranch_scc0 mcsft_rrow_%=\n\t" \
-    "s_sub_u32 s90, s91, 63\n\t" \
-    "mcsft_rrow_%=:\n\t" \
-    "s_and_b32 s86, s90, 63\n\t" \
-    "s_set_gpr_idx_on s86, gpr_idx(SRC0)\n\t" \
-    "v_mov_b32 v119, v128\n\t" \
-    "s_set_gpr_idx_off\n\t" \
-    "v_cmp_le_u32_e64 s[62:63], v119, s40\n\t" \
-    "s_and_b64 exec, s[62:63], -1\n\t" \
-    "s_cbranch_scc0 mcsft_rnext_%=\n\t" \
-    "s_lshl_b32 s76, s86, 9\n\t" \
-    "v_add_u32 v117, s76, v107\n\t" \
-    "ds_read_b64 v[122:123], v117\n\t" \
-    "s_bcnt1_i32_b64 s76, s[62:63]\n\t" \
-    "s_add_u32 s75, s75, s76\n\t" \
-    "s_set_gpr_idx_on s86, gpr_idx(DST)\n\t" \
-    "v_mov_b32 v128, -1\n\t" \
-    "s_set_gpr_idx_off\n\t" \
-    "s_waitcnt lgkmcnt(0)\n\t" \
-    "ds_add_u32 v123, v122\n\t" /* the payload back to its node */ \
-    "mcsft_rnext_%=:\n\t" \
-    "s_mov_b64 exec, -1\n\t" \
-    "s_add_u32 s90, s90, 1\n\t" \
-    "s_cmp_le_u32 s90, s91\n\t" \
-    "s_cbranch_scc1 mcsft_rrow_%=\n\t" \
-    "s_cmp_le_u32 s89, s40\n\t" \
-    "s_cbranch_scc0 mcsft_rspd_%=\n\t" \
-    "v_cmp_le_u32_e64 s[62:63], v192, s40\n\t" \
-    "s_and_b64 exec, s[62:63], -1\n\t" \
-    "s_cbranch_scc0 mcsft_rs0_%=\n\t" \
-    "v_add_u32 v117, 32768, v107\n\t" \
-    "ds_read_b64 v[122:123], v117\n\t" \
-    "s_bcnt1_i32_b64 s76, s[62:63]\n\t" \
-    "s_add_u32 s75, s75, s76\n\t" \
-    "s_sub_u32 s88, s88, s76\n\t" \
-    "v_mov_b32 v192, -1\n\t" \
-    "s_waitcnt lgkmcnt(0)\n\t" \
-    "ds_add_u32 v123, v122\n\t" \
-    "mcsft_rs0_%=:\n\t" \
-    "s_mov_b64 exec, -1\n\t" \
-    "v_cmp_le_u32_e64 s[62:63], v193, s40\n\t" \
-    "s_and_b64 exec, s[62:63], -1\n\t" \
-    "s_cbranch_scc0 mcsft_rs1_%=\n\t" \
-    "v_add_u32 v117, 33280, v107\n\t" \
-    "ds_read_b64 v[122:123], v117\n\t" \
-    "s_bcnt1_i32_b64 s76, s[62:63]\n\t" \
-    "s_add_u32 s75, s75, s76\n\t" \
-    "s_sub_u32 s88, s88, s76\n\t" \
-    "v_mov_b32 v193, -1\n\t" \
-    "s_waitcnt lgkmcnt(0)\n\t" \
-    "ds_add_u32 v123, v122\n\t" \
-    "mcsft_rs1_%=:\n\t" \
-    "s_mov_b64 exec, -1\n\t" \
-    "v_cmp_le_u32_e64 s[62:63], v194, s40\n\t" \
-    "s_and_b64 exec, s[62:63], -1\n\t" \
-    "s_cbranch_scc0 mcsft_rs2_%=\n\t" \
-    "v_add_u32 v117, 33792, v107\n\t" \
-    "ds_read_b64 v[122:123], v117\n\t" \
-    "s_bcnt1_i32_b64 s76, s[62:63]\n\t" \
-    "s_add_u32 s75, s75, s76\n\t" \
-    "s_sub_u32 s88, s88, s76\n\t" \
-    "v_mov_b32 v194, -1\n\t" \
-    "s_waitcnt lgkmcnt(0)\n\t" \
-    "ds_add_u32 v123, v122\n\t" \
-    "mcsft_rs2_%=:\n\t" \
-    "s_mov_b64 exec, -1\n\t" \
-    "v_cmp_le_u32_e64 s[62:63], v195, s40\n\t" \
-    "s_and_b64 exec, s[62:63], -1\n\t" \
-    "s_cbranch_scc0 mcsft_rs3_%=\n\t" \
-    "v_add_u32 v117, 34304, v107\n\t" \
-    "ds_read_b64 v[122:123], v117\n\t" \
-    "s_bcnt1_i32_b64 s76, s[62:63]\n\t" \
-    "s_add_u32 s75, s75, s76\n\t" \
-    "s_sub_u32 s88, s88, s76\n\t" \
-    "v_mov_b32 v195, -1\n\t" \
-    "s_waitcnt lgkmcnt(0)\n\t" \
-    "ds_add_u32 v123, v122\n\t" \
-    "mcsft_rs3_%=:\n\t" \
-    "s_mov_b64 exec, -1\n\t" \
-    "s_add_u32 s89, s40, 1\n\t" \
-    "s_cmp_eq_u32 s88, 0\n\t" \
-    "s_cselect_b32 s89, -1, s89\n\t" \
-    "mcsft_rspd_%=:\n\t" \
-    "s_sub_u32 s80, s80, s75\n\t" \
-    "s_cmp_eq_u32 s75, 0\n\t" \
-    "s_cbranch_scc1 mcsft_rnone_%=\n\t" \
-    MCS_FA_RELOAD16 "s_waitcnt lgkmcnt(0)\n" \
-    /* the earliest remaining finish is > t: t + 1 is a bound (none when nothing runs) */ \
-    "mcsft_rnone_%=:\n\t" \
-    "s_add_u32 s77, s40, 1\n\t" \
-    "s_cmp_eq_u32 s80, 0\n\t" \
-    "s_cselect_b32 s77, -1, s77\n\t" \
-    "s_branch mcsft_loopend_%=\n\t" \
-    "mcsft_deadlock_%=:\n\t" \
-    "s_or_b32 s44, s44, %[fdl]\n\t" \
-    "s_branch mcsft_exit_%=\n\t" \
-    "mcsft_clkovf_%=:\n\t" \
-    "s_mov_b32 s40, -1\n\t" \
-    "s_or_b32 s44, s44, %[fck]\n\t" \
-    "s_branch mcsft_exit_%=\n\t" \
-    "mcsft_poolovf_%=:\n\t" \
-    "s_or_b32 s44, s44, %[fov]\n\t" \
-    "s_branch mcsft_exit_%=\n\t" \
-    /* ---- batch end: store the 64 results, take the prefetched records, prefetch the next ---- */ \
-    "mcsft_bend_%=:\n\t" \
-    "s_max_u32 s81, s81, s80\n\t" \
-    "s_add_u32 s76, s57, s47\n\t" \
-    "s_cmp_ge_u32 s76, s42\n\t" \
-    "s_cbranch_scc1 mcsft_exit_%=\n\t" \
-    "s_waitcnt vmcnt(0)\n\t" \
-    "v_add_u32 v125, s57, v110\n\t" \
-    "v_lshlrev_b32 v125, 2, v125\n\t" \
-    MCS_FA_NODEIDX \
-    "global_store_dword v125, v126, s[66:67] nt\n\t" \
-    "global_store_dword v125, v92, s[68:69] nt\n\t" \
-    "v_add_u32 v93, v92, v95\n\t" /* finish = start + the batch's duration column */ \
-    "global_store_dword v125, v93, s[70:71] nt\n\t" \
-    "s_add_u32 s57, s57, 64\n\t" MCS_FA_TAKE16 \
-    "v_add_u32 v121, s57, v110\n\t" \
-    "v_lshlrev_b32 v121, 4, v121\n\t" \
-    "v_add_u32 v121, 0x400, v121\n\t" \
-    "global_load_dwordx4 v[98:101], v121, s[64:65]\n\t" \
-    "s_sub_u32 s41, s42, s57\n\t" \
-    "s_min_u32 s41, s41, 64\n\t" \
-    "s_mov_b32 s47, 0\n\t" MCS_FA_REC16 \
-    "s_branch mcsft_inner_%=\n\t" \
-    /* ---- exit: state back to the compiler's registers ---- */ \
-    "mcsft_exit_%=:\n\t" \
-    "s_mov_b64 exec, -1\n\t" \
-    "s_waitcnt vmcnt(0) lgkmcnt(0)\n\t" \
-    "s_mov_b32 %[t], s40\n\t" \
-    "s_add_u32 %[r], s57, s47\n\t" \
-    "s_mov_b32 %[flags], s44\n\t" \
-    "s_mov_b32 %[hw], s43\n\t" \
-    "s_mov_b32 %[used], s80\n\t" \
-    "s_max_u32 %[peak], s81, s80\n\t" \
-    "s_mov_b32 %[waited], s82\n\t" \
-    "s_mov_b32 %[nslow], s83\n\t" \
-    "s_mov_b32 %[nrel], s84\n\t" \
-    "v_mov_b32 %[on], v91\n\t" \
-    "v_mov_b32 %[os], v92\n\t" \
-    "s_cmp_eq_u32 s47, 0\n\t" \
-    "s_cbranch_scc1 mcsft_xf_%=\n\t" \
-    "v_add_u32 v93, v92, v95\n\t" \
-    "mcsft_xf_%=:\n\t" \
-    "v_mov_b32 %[of], v93\n\t" \
-    "s_nop 1"
-
-#define MCS_FT_CLOBBERS MCS_FA_CLOBBERS, "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161", "v162", "v163", "v164", "v165", "v166", "v167", "v168", "v169", "v170", "v171", "v172", "v173", "v174", "v175", "v176", "v177", "v178", "v179", "v180", "v181", "v182", "v183", "v184", "v185", "v186", "v187", "v188", "v189", "v190", "v191", "v192", "v193", "v194", "v195"
-
-template <bool DIAG>
-__global__ __launch_bounds__(64) void fifo_asm_t_kernel(FifoArgs a) {
-    const uint32_t item = blockIdx.x;
-    const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
-    const uint32_t lane = threadIdx.x;
-
-    // nodes [4][64] u32 at 0, the slot table [68][64] u64 at 1024
-    __shared__ uint32_t lds[4 * kWave + 68 * kWave * 2];
-    constexpr uint32_t kGuard = 0x8000u, kClamp = kGuard - 1u;
-    const uint32_t n0 = a.node_off[ci];
-    const uint32_t N = a.node_off[ci + 1] - n0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const uint32_t node = lane * 4 + c;
-        uint2 v = make_uint2(kClamp, kClamp);  // padding: never fits
-        if (node < N) {
-            v = a.node_free0[n0 + node];
-            v.x += kGuard;
-            v.y += kGuard;
-        }
-        lds[c * kWave + lane] = v.x | (v.y << 16);
-    }
-
-    const uint64_t j0 = a.job_off[ci];
-    const uint32_t J = (uint32_t)(a.job_off[ci + 1] - j0);
-    const uint4* jobs = a.jobs + j0;
-    int32_t* o_node = a.out_node + j0;
-    uint32_t* o_start = a.out_start + j0;
-    uint32_t* o_finish = a.out_finish + j0;
-
-    uint4 cur = jobs[lane];  // batch 0 (the array has kJobPad records of slack)
-    cur.z = cur.z < kClamp ? cur.z : kClamp;
-    cur.w = cur.w < kClamp ? cur.w : kClamp;
-    cur.z |= cur.w << 16;
-    __syncthreads();
-
-    const uint32_t base = lds_addr(lds);
-    const uint32_t v_pay = base + 1024u + lane * 8u;
-    const uint32_t v_nb = base + lane * 4u;
-    const uint32_t v_nbase = base;
-    const uint32_t sel0 = 0x0b0a0908u, sel1 = base;
-    const uint32_t kw = a.win_shift;
-
-    uint32_t t = 0, r = 0, flags = 0, have_w = 0, frm = 0, lmin = 0;
-    uint32_t used = 0, peak = 0, waited = 0, n_slow = 0, n_rel = 0;
-    uint32_t on = 0, os = 0, of = 0;
-
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-#define MCS_FT_OPERANDS                                                                           \
-    : [t] "+s"(t), [r] "+s"(r), [flags] "+s"(flags), [hw] "+s"(have_w), [used] "+s"(used),      \
-      [peak] "+s"(peak), [waited] "+s"(waited), [nslow] "+s"(n_slow), [nrel] "+s"(n_rel),       \
-      [on] "+v"(on), [os] "+v"(os), [of] "+v"(of), [frm] "+v"(frm), [lmin] "+v"(lmin)            \
-    : [J] "s"(J), [jobs] "s"(jobs), [onp] "s"(o_node), [osp] "s"(o_start), [ofp] "s"(o_finish), \
-      [c0] "v"(cur.x), [c1] "v"(cur.y), [c2] "v"(cur.z), [c3] "v"(cur.w), [pay] "v"(v_pay),     \
-      [nb] "v"(v_nb), [nbase] "v"(v_nbase), [lane] "v"(lane), [sel0] "s"(sel0),                 \
-      [sel1] "s"(sel1), [kw] "s"(kw), [fdl] "i"(MCS_FLAG_DEADLOCK),                             \
-      [fck] "i"(MCS_FLAG_CLOCK_OVERFLOW), [fov] "i"(MCS_FLAG_OVERFLOW)                          \
-    : MCS_FT_CLOBBERS
-    if constexpr (DIAG) asm volatile(MCS_FT_LOOP(D1) MCS_FT_OPERANDS);
-    else asm volatile(MCS_FT_LOOP(D0) MCS_FT_OPERANDS);
-#undef MCS_FT_OPERANDS
-#pragma clang diagnostic pop
-
-    const uint32_t placed = r;  // FIFO places every job it decides, in order
-    if (!(flags & MCS_FLAG_OVERFLOW)) {
-        if (r > 0u) {  // the batch holding the last decision (earlier ones are stored)
-            const uint32_t i = ((r - 1u) & ~63u) + lane;
-            if (i < r) {
-                o_node[i] = (int32_t)((on & 63u) * 4u + (on >> 6));
-                o_start[i] = os;
-                o_finish[i] = of;
-            }
-        }
-        if (flags & (MCS_FLAG_DEADLOCK | MCS_FLAG_CLOCK_OVERFLOW)) {
-            for (uint32_t i = r + lane; i < J; i += kWave) {
-                o_node[i] = MCS_NODE_UNPLACED;
-                o_start[i] = MCS_TIME_NONE;
-                o_finish[i] = MCS_TIME_NONE;
-            }
-        }
-    }
-    if (lane == 0) {
-        mcs_cluster_stats st;
-        st.t_end = t;
-        st.placed = placed;
-        st.waited = waited;
-        st.peak_running = peak;
-        st.flags = flags;
-        st.pool = 8u;  // (reported as the W16R pool it replaces; its capacity is 68 x 64 slots)
-        st.iterations = n_slow + r;
-        st.release_scans = n_rel;
-        a.cstats[ci] = st;
-        if (flags & MCS_FLAG_OVERFLOW) {
-            atomicAdd(&a.totals->overflowed, 1u);
-        } else {
-            atomicAdd(&a.totals->placed, (unsigned long long)placed);
-            atomicAdd(&a.totals->waited, (unsigned long long)waited);
-            atomicAdd(&a.totals->unplaced, (unsigned long long)(J - placed));
-            if (flags & MCS_FLAG_DEADLOCK) atomicAdd(&a.totals->deadlocked, 1u);
-            if (flags & MCS_FLAG_CLOCK_OVERFLOW) atomicAdd(&a.totals->clock_overflowed, 1u);
-        }
-    }
-}
-
-// the window parameters of form T: the longest duration and the largest job rate
-// (jobs * 1024 / (last arrival + 1)) over the clusters
-__global__ __launch_bounds__(256) void window_stats_kernel(const uint4* jobs, const uint64_t* job_off,
-                                                           uint32_t* out) {
-    const uint32_t c = blockIdx.x;
-    const uint64_t j0 = job_off[c], J = job_off[c + 1] - j0;
-    uint32_t mx = 0;
-    for (uint64_t i = threadIdx.x; i < J; i += 256) mx = max(mx, jobs[j0 + i].y);
-    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-    if ((threadIdx.x & 63u) == 0u) atomicMax(&out[0], mx);
-    if (threadIdx.x == 0 && J > 0) {
-        const uint64_t q = (J << 10) / ((uint64_t)jobs[j0 + J - 1].x + 1u);
-        atomicMax(&out[1], (uint32_t)(q < 0xFFFFFFFFull ? q : 0xFFFFFFFFull));
-    }
-}
-
 }  // namespace
 
 // Form codes: 17 = W16R and 18 = W16S (where the 16-bit format fits), 16 = W16 with LDS slots,
@@ -1381,16 +834,7 @@ int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor) {
     if (npl != 4 || pool != 8) return 0;
     // register slots: one LDS round trip per release instead of 2 + rows; measured faster than LDS
     // slots at every occupancy from 1 to 16 cluster waves per CU
-    if ((a.guard_ok & 2u) && want != 32) {
-        if (want == 16) return 16;
-        // form T at one cluster wave per SIMD or fewer (its LDS slot table allows 4 per CU);
-        // MCS_FIFO_T=0 never, =2 at any occupancy (tests), default 1
-        const char* te = getenv("MCS_FIFO_T");
-        const int tw = te ? atoi(te) : 1;
-        if (a.win_shift != kNoWindow && (want == 19 || (tw == 2 || (tw == 1 && a.n_items <= 4u * a.n_cus))))
-            return 19;
-        return 17;
-    }
+    if ((a.guard_ok & 2u) && want != 32) return want == 16 ? 16 : 17;
     return (a.guard_ok & 1u) ? 32 : 0;
 }
 
@@ -1401,7 +845,6 @@ bool fifo_asm_eligible(const FifoArgs& a, int npl, int pool, bool hor) {
 template <bool DIAG>
 static hipError_t launch_form(const FifoArgs& a, int form, hipStream_t s) {
     switch (form) {
-        case 19: hipLaunchKernelGGL((fifo_asm_t_kernel<DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 18: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 1, 2, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 17: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 16: hipLaunchKernelGGL((fifo_asm_kernel<16, false, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
@@ -1430,31 +873,3 @@ extern "C" int mcs_debug_fa_stamps(unsigned long long* out) {
     return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_fa_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif
-
-namespace mcs {
-hipError_t fifo_window_shift(const uint4* jobs, const uint64_t* job_off, uint32_t n_clusters, hipStream_t s,
-                             uint32_t* shift) {
-    *shift = kNoWindow;
-    if (n_clusters == 0) return hipSuccess;
-    uint32_t* d = nullptr;
-    hipError_t st = hipMalloc(&d, 2 * sizeof(uint32_t));
-    uint32_t h[2] = {0, 0};
-    if (st == hipSuccess) st = hipMemsetAsync(d, 0, 2 * sizeof(uint32_t), s);
-    if (st == hipSuccess) {
-        hipLaunchKernelGGL(window_stats_kernel, dim3(n_clusters), dim3(256), 0, s, jobs, job_off, d);
-        st = hipGetLastError();
-    }
-    if (st == hipSuccess) st = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s);
-    if (st == hipSuccess) st = hipStreamSynchronize(s);
-    if (d) (void)hipFree(d);
-    if (st != hipSuccess) return st;
-    // 63 windows of 2^k s must exceed the longest duration (live finishes then never share a row
-    // across wrap-around), and a window should expect at most half a row (32 of 64 lanes) of finishes
-    for (uint32_t k = 0; k <= 20; ++k) {
-        if ((63ull << k) < (uint64_t)h[0] + 2u) continue;
-        if (((uint64_t)h[1] << k) <= (32ull << 10)) *shift = k;
-        break;
-    }
-    return hipSuccess;
-}
-}  // namespace mcs

@@ -90,14 +90,7 @@ struct FifoArgs {
     uint32_t guard_ok;  // bit 0: every node's free values < 2^31 - 1 (the hand-scheduled loop
                         // may run, W32 node format); bit 1: < 2^15 - 1 (W16 node format);
                         // bit 2: every cluster holds at most kAsmMaxJobs jobs
-    uint32_t win_shift;  // form T's window shift k (kNoWindow: not eligible; mcs_engine.cpp)
-    uint32_t n_cus;      // compute units of the device (form T runs at <= 4 cluster waves per CU)
 };
-constexpr uint32_t kNoWindow = 0xFFFFFFFFu;
-// form T's window shift for the streams in HBM (longest duration, largest job rate), kNoWindow
-// when no shift fits (mcs_fifo_asm.hip)
-hipError_t fifo_window_shift(const uint4* jobs, const uint64_t* job_off, uint32_t n_clusters, hipStream_t s,
-                             uint32_t* shift);
 
 struct DelayArgs {
     const uint2* node_free0;

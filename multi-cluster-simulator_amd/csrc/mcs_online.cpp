@@ -428,7 +428,6 @@ int mcs_append_jobs(mcs_engine* e, const uint32_t* arrival_s, const uint32_t* du
     if (!e->has_clusters) return fail(e, MCS_E_STATE, "mcs_load_clusters first");
     if (e->cfg.borrow || e->cfg.trader)
         return fail(e, MCS_E_STATE, "online mode (finite horizons, appends) is not available with borrow/trader");
-    e->win_known = false; /* the streams change: form T's window is re-derived */
     if (!job_offsets) return fail(e, MCS_E_INVALID, "null job_offsets");
     if (job_offsets[0] != 0) return fail(e, MCS_E_INVALID, "job_offsets[0] must be 0");
     const uint32_t C = e->C;

@@ -78,8 +78,7 @@ def seeded_workload(kind: str, n_clusters: int, jobs_per_cluster: int, seed: int
 def fuzz_workload(shape: str, seed: int, n_clusters: int = 160, J: int = 2000, blocking: bool = True):
     """Randomised clusters and job streams (tests/test_gpu_parity.py, test_gpu_delay.py): node counts
     across the shape's range ('w16s' <= 64 nodes, 'mid' 65-128, 'w16r' 129-256, 'w32' 129-256 with
-    memory values past 2^15, 'w16t' 129-256 at form T's job rates with durations up to 900 s and
-    same-finish bursts that fill a window row), random JSON availability, bursts of simultaneous arrivals and idle
+    memory values past 2^15), random JSON availability, bursts of simultaneous arrivals and idle
     stretches, zero-duration and zero-resource jobs, requests up to a node's capacity, and (blocking)
     in half the clusters one request that fits no node at a random point of the stream; without
     blocking, node 0 is fully available, so no request can wait forever (a lock-step trading run
@@ -87,7 +86,7 @@ def fuzz_workload(shape: str, seed: int, n_clusters: int = 160, J: int = 2000, b
     from mcs_amd import JobStreams, pack_clusters
     from mcs_amd.cluster import Node
 
-    rng = np.random.default_rng(1000 * seed + {"w16s": 0, "w16r": 1, "w32": 2, "mid": 3, "w16t": 4}[shape])
+    rng = np.random.default_rng(1000 * seed + {"w16s": 0, "w16r": 1, "w32": 2, "mid": 3}[shape])
     lo, hi = {"w16s": (1, 64), "mid": (65, 128)}.get(shape, (129, 256))
     clusters, parts = [], []
     for k in range(n_clusters):
@@ -102,27 +101,15 @@ def fuzz_workload(shape: str, seed: int, n_clusters: int = 160, J: int = 2000, b
         if not blocking:  # node 0 fully available: every request fits once it drains (no stuck head)
             cl.Nodes[0].CoresAvailable, cl.Nodes[0].MemoryAvailable = cap_c, cap_m
         clusters.append(cl)
-        if shape == "w16t":  # form T's window: up to ~2 jobs/s, durations up to 900 s (k = 4)
-            gaps = rng.poisson(rng.uniform(0.6, 3.0), J)
-            gaps[rng.random(J) < 0.1] = 0  # simultaneous arrivals
-        else:
-            gaps = rng.poisson(rng.uniform(0.05, 2.0), J)
+        gaps = rng.poisson(rng.uniform(0.05, 2.0), J)
         gaps[rng.random(J) < 0.05] += int(rng.integers(10, 500))  # idle stretches
         arr = np.cumsum(gaps).astype(np.uint32)
-        dur = rng.integers(0, int(rng.integers(2, 900 if shape == "w16t" else 300)), J).astype(np.uint32)
+        dur = rng.integers(0, int(rng.integers(2, 300)), J).astype(np.uint32)
         cores = rng.integers(0, cap_c + 1, J).astype(np.uint32)
         mem = rng.integers(0, cap_m + 1, J).astype(np.uint32)
         z = rng.random(J) < 0.02
         cores[z] = 0
         mem[z] = 0
-        if shape == "w16t" and k % 4 == 1:  # a burst of same-finish jobs: a full window row spills
-            i = int(rng.integers(0, J - 400))
-            n = int(rng.integers(70, 380))  # (past 64 + 256 the spill rows overflow: escalation)
-            arr[i:i + n] = arr[i]
-            arr[i + n:] = np.maximum(arr[i + n:], arr[i])
-            dur[i:i + n] = int(rng.integers(1, 600))
-            cores[i:i + n] = 0
-            mem[i:i + n] = 0
         if blocking and rng.random() < 0.5:  # one request that fits no node, somewhere in the stream
             i = int(rng.integers(J // 4, J))
             if rng.random() < 0.5:

@@ -292,30 +292,26 @@ def test_heterogeneous_cluster_sizes_hand_scheduled(engine, sizes):
     off = np.arange(len(parts) + 1, dtype=np.uint64) * J
     s = JobStreams(*(np.concatenate([p[f] for p in parts]) for f in range(4)), off)
     node, start, fin, st, cs = run_engine(engine, arrays, s)
-    assert engine.last_kernel.startswith("mcs::fifo_asm")
+    assert engine.last_kernel.startswith("mcs::fifo_asm_kernel<16, true")
     assert_parity(arrays, s, node, start, fin, cs)
     assert cs[0]["flags"] & L.MCS_FLAG_DEADLOCK  # zero nodes: the first job never fits
 
 
-@pytest.mark.parametrize("nodes,form", [(256, "2"), (256, "0"), (5, "1")])
-def test_hand_scheduled_diag_build(nodes, form):
+@pytest.mark.parametrize("nodes", [256, 5])
+def test_hand_scheduled_diag_build(nodes):
     """MCS_FIFO_DIAG=1 launches the counting build of the hand-scheduled loop: the same placements
     and per-cluster results, plus the pass and release-scan counters (which the production build
-    leaves at the decision count and 0).  256 nodes: form T (MCS_FIFO_T=2) and W16R (=0)."""
+    leaves at the decision count and 0)."""
     arrays, streams, _ = seeded_workload("n256" if nodes == 256 else "small", 64, 3000)
     res = {}
-    want = {"2": "mcs::fifo_asm_t_kernel", "0": "mcs::fifo_asm_kernel<16, true, 4, 8>",
-            "1": "mcs::fifo_asm_kernel<16, true, 1, 2>"}[form]
     for diag in ("0", "1"):
         os.environ["MCS_FIFO_DIAG"] = diag
-        os.environ["MCS_FIFO_T"] = form
         try:
             with Engine(0) as eng:
                 res[diag] = run_engine(eng, arrays, streams)
-                assert eng.last_kernel == want
+                assert eng.last_kernel.startswith("mcs::fifo_asm_kernel<16, true")
         finally:
             os.environ.pop("MCS_FIFO_DIAG", None)
-            os.environ.pop("MCS_FIFO_T", None)
     for i in range(3):
         np.testing.assert_array_equal(res["0"][i], res["1"][i])
     c0, c1 = res["0"][4], res["1"][4]
@@ -326,27 +322,20 @@ def test_hand_scheduled_diag_build(nodes, form):
     assert_parity(arrays, streams, *res["1"][:3], c1)
 
 
-@pytest.mark.parametrize("shape", ["w16s", "w16r", "w16t", "w32"])
+@pytest.mark.parametrize("shape", ["w16s", "w16r", "w32"])
 @pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6])
-def test_hand_scheduled_fuzz(shape, seed):
+def test_hand_scheduled_fuzz(engine, shape, seed):
     """Randomised clusters and streams through each hand-scheduled loop form, bit-exact against the
     oracle: node counts across the shape's range (padding lanes and chunks), random JSON
     availability, bursts of simultaneous arrivals, zero-duration and zero-resource jobs, requests
     equal to a node's free value, and one request per cluster that fits no node (a head-of-line
-    deadlock at a random point of the stream).  w16t: form T (MCS_FIFO_T=2) at its job rates, with
-    same-finish bursts that spill a window row (and past the spill rows, escalate); w16r: W16R
-    (MCS_FIFO_T=0)."""
+    deadlock at a random point of the stream)."""
     arrays, s = fuzz_workload(shape, seed)
-    os.environ["MCS_FIFO_T"] = "2" if shape == "w16t" else "0"
-    try:
-        with Engine(0) as engine:
-            node, start, fin, st, cs = run_engine(engine, arrays, s)
-            last = engine.last_kernel
-    finally:
-        os.environ.pop("MCS_FIFO_T", None)
+    node, start, fin, st, cs = run_engine(engine, arrays, s)
     want = {"w16s": "mcs::fifo_asm_kernel<16, true, 1, 2>", "w16r": "mcs::fifo_asm_kernel<16, true, 4, 8>",
-            "w16t": "mcs::fifo_asm_t_kernel", "w32": "mcs::fifo_asm_kernel<32, false, 4, 8>"}[shape]
-    assert last == want  # (the first launch: escalated clusters re-run on the compiled kernel)
+            "w32": "mcs::fifo_asm_kernel<32, false, 4, 8>"}[shape]
+    if st.escalations == 0:
+        assert engine.last_kernel == want
     assert_parity(arrays, s, node, start, fin, cs)
     # the compiled kernel on the same case (MCS_FIFO_ASM=0) agrees as well
     os.environ["MCS_FIFO_ASM"] = "0"
@@ -452,8 +441,8 @@ def test_hand_scheduled_loop_field_bounds(engine, free):
     off = np.arange(len(parts) + 1, dtype=np.uint64) * J
     s = JobStreams(*(np.concatenate([p[f] for p in parts]) for f in range(4)), off)
     node, start, fin, st, cs = run_engine(engine, arrays, s)
-    assert engine.last_kernel in (("mcs::fifo_asm_t_kernel", "mcs::fifo_asm_kernel<16, true, 4, 8>") if free < 0x7FFF
-                                  else ("mcs::fifo_asm_kernel<32, false, 4, 8>",))
+    assert engine.last_kernel == ("mcs::fifo_asm_kernel<16, true, 4, 8>" if free < 0x7FFF
+                                  else "mcs::fifo_asm_kernel<32, false, 4, 8>")
     assert_parity(arrays, s, node, start, fin, cs)
     assert (cs["flags"] & L.MCS_FLAG_DEADLOCK).all()  # every cluster's last request fits nowhere
     assert (node.reshape(-1, J)[:, -1] == -1).all()
@@ -476,15 +465,14 @@ def test_every_kernel_variant(policy):
         for pool in (2, 4, 8, 16, 32):
             # streamed FIFO has five forms: the hand-scheduled loop (mcs_fifo_asm.hip, 129-256
             # nodes and 8 slot rows) in its 16-bit node format with register slots (picked for these
-            # clusters), with LDS slots (MCS_FIFO_ASM=16), form T (=19, finish-window slot rows) and
-            # the 32-bit one (=32; =0 turns the loop off), and the compiled kernel's two (the low-occupancy one is picked for small grids;
+            # clusters), with LDS slots (MCS_FIFO_ASM=16) and its 32-bit one (=32; =0 turns the loop
+            # off), and the compiled kernel's two (the low-occupancy one is picked for small grids;
             # MCS_FIFO_LAT forces either)
             for fused, lat, asm in ((False, "1", "0"), (False, "0", "0"), (False, None, "1"),
-                                    (False, None, "16"), (False, None, "19"), (False, None, "32"),
-                                    (True, None, None)):
+                                    (False, None, "16"), (False, None, "32"), (True, None, None)):
                 if policy == "DELAY" and lat == "0":
                     continue
-                if policy == "DELAY" and asm in ("1", "16", "19", "32"):
+                if policy == "DELAY" and asm in ("1", "16", "32"):
                     continue
                 env = {"MCS_FIFO_LAT": lat, "MCS_FIFO_ASM": asm}
                 old = {k: os.environ.get(k) for k in env}
