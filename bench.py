@@ -67,6 +67,9 @@ def parse():
                     help="0 = every usable host cpu: the affinity set capped by the cgroup CPU quota (SURVEY §8d: "
                          "OpenMP over clusters on all host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--comm", action="store_true",
+                    help="c5: run the RCCL tick loop (ncclAllGather per tick) even at N=1, on a world-1 "
+                         "communicator (MCS_RCCL_GRAPH=0: eager launches instead of the captured hipGraph)")
     ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes measured by a separate rocprofv3 --pmc pass (profile figure)")
     ap.add_argument("--policy", choices=["fifo", "delay"], default="fifo",
@@ -189,6 +192,8 @@ def main_c5_delay(args, world, rank, local_rank):
         box = [Engine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         eng.comm_init(box[0])
+    elif args.comm:
+        eng.comm_init(Engine.comm_unique_id())
     n_jobs = eng.num_jobs
 
     def barrier():
@@ -254,7 +259,9 @@ def main_c5_delay(args, world, rank, local_rank):
                 "jobs_per_cluster": args.jobs_per_cluster,
                 "parallelism": f"one system sharded over {world} GPU(s), {per} clusters each; "
                                + ("one RCCL all-gather of the exchange blocks per tick" if world > 1 else
-                                  "exchange in HBM"),
+                                  "exchange in HBM")
+                               + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "RCCL eager" if ts["loop_form"] == 1
+                                                    else "RCCL captured in a hipGraph") + ")",
             },
             "roofline": {
                 "bound": "hbm",
@@ -272,7 +279,7 @@ def main_c5_delay(args, world, rank, local_rank):
             "trading": {"ticks": ts["ticks"], "t_final": ts["t_final"],
                         "us_per_tick": avg_kernel_s * 1e6 / max(ts["ticks"], 1), "trades": ts["trades"],
                         "trades_won": ts["trades_won"], "wait_time_rounds": int((tr["policy"] == 0).sum()),
-                        "foreign_jobs": int(len(eng.foreign())), "flags": ts["flags"]},
+                        "foreign_jobs": int(len(eng.foreign())), "flags": ts["flags"], "loop_form": ts["loop_form"]},
         }
         print(json.dumps(out), flush=True)
     eng.close()
@@ -308,6 +315,8 @@ def main_c5(args, world, rank, local_rank):
         box = [Engine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         eng.comm_init(box[0])
+    elif args.comm:
+        eng.comm_init(Engine.comm_unique_id())
     n_jobs = eng.num_jobs
 
     def barrier():
@@ -356,7 +365,9 @@ def main_c5(args, world, rank, local_rank):
                 "clusters_total": args.clusters,
                 "nodes": args.nodes,
                 "jobs_per_cluster": args.jobs_per_cluster,
-                "parallelism": f"{world} shard(s); per-tick RCCL all-gather" if dist_on else "1 GPU, exchange in HBM",
+                "parallelism": (f"{world} shard(s); per-tick RCCL all-gather" if dist_on or args.comm else "1 GPU, exchange in HBM")
+                               + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "RCCL eager" if ts["loop_form"] == 1
+                                                    else "RCCL captured in a hipGraph") + ")",
             },
             "roofline": {
                 "bound": "hbm",
@@ -373,7 +384,7 @@ def main_c5(args, world, rank, local_rank):
             "cpu_baseline": cpu,
             "trading": {"ticks": ts["ticks"], "t_final": ts["t_final"], "us_per_tick": avg_kernel_s * 1e6 / max(ts["ticks"], 1),
                         "borrowed": ts["borrowed"], "lent_runs_all_ranks": lent_all, "trades": ts["trades"],
-                        "trades_won": ts["trades_won"], "flags": ts["flags"]},
+                        "trades_won": ts["trades_won"], "flags": ts["flags"], "loop_form": ts["loop_form"]},
         }
         print(json.dumps(out), flush=True)
     eng.close()
