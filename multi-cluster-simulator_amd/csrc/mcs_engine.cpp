@@ -575,7 +575,11 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     uint32_t escalations = 0;
     int pool_used = pool;
     HIPCHK(e, hipMemsetAsync(e->d_totals, 0, sizeof(mcs::Totals), e->stream));
-    switch (delay ? -1 : mcs::fifo_asm_form(a, npl, pool, false)) {
+    /* DELAY: the hand-scheduled loop first (mcs_delay_asm.hip); clusters that reach Level1 re-run on
+     * delay_kernel */
+    bool dasm = delay && mcs::delay_asm_eligible(npl, pool, a.guard_ok, e->gen.on);
+    switch (delay ? (dasm ? -2 : -1) : mcs::fifo_asm_form(a, npl, pool, false)) {
+        case -2: e->last_kernel = "mcs::delay_asm_kernel"; break;
         case -1: e->last_kernel = "mcs::delay_kernel"; break;
         case 18: e->last_kernel = "mcs::fifo_asm_kernel<16, true, 1, 2>"; break;
         case 17: e->last_kernel = "mcs::fifo_asm_kernel<16, true, 4, 8>"; break;
@@ -586,7 +590,9 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     mcs::Totals tot{};
     for (;;) {
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));
-        if (delay)
+        if (dasm)
+            HIPCHK(e, mcs::launch_delay_asm(da, e->stream));
+        else if (delay)
             HIPCHK(e, mcs::launch_delay(da, npl, pool, false, e->stream));
         else
             HIPCHK(e, mcs::launch_fifo(a, npl, pool, false, e->stream));
@@ -597,23 +603,31 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
         HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
         kms += ms;
         pool_used = pool;
-        if (tot.overflowed == 0) break;
-        /* capacity escalation: re-run only the overflowed clusters with a doubled pool */
-        if (pool * 2 > mcs::kMaxPool)
+        const bool bailed = dasm && tot.bailed != 0;
+        if (tot.overflowed == 0 && !bailed) break;
+        /* clusters the DELAY loop handed over re-run on delay_kernel at the same pool (with the
+         * loop's overflows, which then escalate there); capacity escalation: re-run only the
+         * overflowed clusters with a doubled pool */
+        if (!bailed && pool * 2 > mcs::kMaxPool)
             return fail(e, MCS_E_CAPACITY, "running-slot pool overflow at 2048 slots per cluster");
         std::vector<mcs_cluster_stats> cs(e->C);
         HIPCHK(e, hipMemcpy(cs.data(), e->d_cstats, e->C * sizeof(mcs_cluster_stats),
                             hipMemcpyDeviceToHost));
         std::vector<uint32_t> list;
+        const uint32_t redo = MCS_FLAG_OVERFLOW | (bailed ? mcs::kDelayBail : 0u);
         for (uint32_t c = 0; c < e->C; ++c)
-            if (cs[c].flags & MCS_FLAG_OVERFLOW) list.push_back(c);
+            if (cs[c].flags & redo) list.push_back(c);
         HIPCHK(e, hipMemcpy(e->d_list, list.data(), list.size() * sizeof(uint32_t),
                             hipMemcpyHostToDevice));
         HIPCHK(e, hipMemsetAsync(&e->d_totals->overflowed, 0, sizeof(unsigned int), e->stream));
+        HIPCHK(e, hipMemsetAsync(&e->d_totals->bailed, 0, sizeof(unsigned int), e->stream));
         a.cluster_list = da.cluster_list = e->d_list;
         a.n_items = da.n_items = (uint32_t)list.size();
-        pool *= 2;
-        ++escalations;
+        if (!bailed) {
+            pool *= 2;
+            ++escalations;
+        }
+        dasm = false;
     }
     e->has_run = true;
     if (stats) {

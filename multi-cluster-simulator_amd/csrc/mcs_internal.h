@@ -27,7 +27,7 @@ struct Totals {  // device-side accumulation of mcs_stats (only clusters that di
     unsigned int deadlocked;
     unsigned int overflowed;
     unsigned int clock_overflowed;  // clusters stopped by MCS_FLAG_CLOCK_OVERFLOW (run fails, MCS_E_RANGE)
-    unsigned int pad;
+    unsigned int bailed;            // DELAY clusters the hand-scheduled loop hands to delay_kernel
 };
 
 // In-kernel synthesis of the job stream (mcs_gen_dev.h): with `on` the FIFO and
@@ -114,6 +114,11 @@ struct DelayArgs {
 
 // hor: the online variant (OnlineArgs; records streamed, never fused)
 hipError_t launch_delay(const DelayArgs& a, int npl, int pool, bool hor, hipStream_t s);  // mcs_delay.hip
+// the hand-scheduled DELAY loop (mcs_delay_asm.hip): Level1-empty iterations; a cluster whose head
+// moves to Level1 stops with kDelayBail in its cstats flags and is re-run on delay_kernel
+constexpr uint32_t kDelayBail = 0x40000000u;
+bool delay_asm_eligible(int npl, int pool, uint32_t guard_ok, bool gen_on);
+hipError_t launch_delay_asm(const DelayArgs& a, hipStream_t s);
 
 struct StateArgs {  // the ClusterState reduction over a run's placements (mcs_state.hip)
     const uint32_t* node_off;

@@ -140,3 +140,43 @@ def test_gpu_delay_fuzz(delay_engine, shape, seed):
     arrays, s = fuzz_workload(shape, seed, n_clusters=96, J=1500)
     node, start, fin, st, cs, ds = run(delay_engine, arrays, s)
     assert_delay_parity(arrays, s, node, start, fin, cs, ds)
+
+
+@pytest.mark.parametrize("kind", [
+    "n256",        # Level0 backlog, Level1 never used: the whole run in the asm loop
+    "n256_delay",  # just under one arrival per second
+    "fuzz1",       # randomised w16r workloads (kat_util.fuzz_workload): heads wait MaxWaitTime and
+    "fuzz2",       # their clusters hand over to delay_kernel
+])
+@pytest.mark.parametrize("diag", ["0", "1"])
+def test_gpu_delay_hand_scheduled_loop(kind, diag, monkeypatch):
+    """The hand-scheduled DELAY loop (mcs_delay_asm.hip, picked for 129-256 node clusters): its
+    clusters, and those it hands to delay_kernel at their first Level1 move (re-run from t = 0),
+    equal the oracle and the compiled kernel alone (MCS_DELAY_ASM=0) on every output the oracle
+    defines; MCS_FIFO_DIAG=1 launches its counting build."""
+    if kind.startswith("fuzz"):
+        arrays, streams = fuzz_workload("w16r", int(kind[4:]), n_clusters=64, J=1500)
+    else:
+        arrays, streams, _ = seeded_workload(kind, 64, 3000)
+    monkeypatch.setenv("MCS_FIFO_DIAG", diag)
+    with Engine(0, policy="DELAY") as eng:
+        got = run(eng, arrays, streams)
+        assert eng.last_kernel == "mcs::delay_asm_kernel"
+    assert_delay_parity(arrays, streams, *got[:3], got[4], got[5])
+    monkeypatch.setenv("MCS_DELAY_ASM", "0")
+    with Engine(0, policy="DELAY") as eng:
+        ref = run(eng, arrays, streams)
+        assert eng.last_kernel == "mcs::delay_kernel"
+    for i in range(3):
+        np.testing.assert_array_equal(got[i], ref[i])
+    for f in ("t_end", "placed", "waited", "peak_running", "flags"):
+        np.testing.assert_array_equal(got[4][f], ref[4][f], err_msg=f)
+    for f in got[5].dtype.names:
+        np.testing.assert_array_equal(got[5][f], ref[5][f], err_msg=f)
+    assert got[3].placed == ref[3].placed and got[3].unplaced == ref[3].unplaced
+    if diag == "1":
+        assert (got[4]["release_scans"] > 0).any()
+    if kind == "n256":
+        assert (got[5]["moved_l1"] == 0).all()  # (no cluster needed the compiled kernel)
+    if kind.startswith("fuzz"):
+        assert (got[5]["moved_l1"] > 0).any()
