@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--nodes", type=int, default=256)
     ap.add_argument("--jobs-per-cluster", type=int, default=0)
     ap.add_argument("--load", type=float, default=0.9, help="offered memory load of the scaled arrivals")
+    ap.add_argument("--lam", type=float, default=0.0,
+                    help="c4: per-second arrival rate of the scaled arrivals (0 = from --load)")
+    ap.add_argument("--max-dur", type=int, default=600,
+                    help="c4: durations U{0..max_dur-1} s (600 = rand.Intn(600), client.go:98)")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x4D43535F53494D31)
     ap.add_argument("--cpu-sample-clusters", type=int, default=0,
                     help="CPU baseline sample: that many clusters with full streams (0 = per-config default, "
@@ -407,10 +411,13 @@ class Workload:
         if args.config == "c4":
             self.spec_name = f"{args.nodes} nodes x {{32 cores, 24000 memory}}"
             spec = uniform_cluster(args.nodes)
-            lam = scaled_lambda(args.nodes, load=args.load)
+            lam = args.lam or scaled_lambda(args.nodes, load=args.load)
             self.lam = lam
-            self.arrival = f"scaled per-second Poisson arrivals at {args.load:.0%} memory load (lambda={lam:.4f}/s)"
-            gp = GenParams(seed=args.seed, arrival_mode=1, lam=lam, fused=fused)
+            self.arrival = (f"scaled per-second Poisson arrivals at {args.load:.0%} memory load (lambda={lam:.4f}/s)"
+                            if not args.lam else f"per-second Poisson arrivals at lambda={lam:.4f}/s")
+            if args.max_dur != 600:
+                self.arrival += f", durations U{{0..{args.max_dur - 1}}} s"
+            gp = GenParams(seed=args.seed, arrival_mode=1, lam=lam, fused=fused, max_dur_s=args.max_dur)
             if args.shard == "strong":
                 if args.clusters % world:
                     raise SystemExit(f"--clusters {args.clusters} must divide over {world} ranks (strong sharding)")
