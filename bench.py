@@ -71,6 +71,8 @@ def parse():
                     help="0 = every usable host cpu: the affinity set capped by the cgroup CPU quota (SURVEY §8d: "
                          "OpenMP over clusters on all host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--slot-pool", type=int, default=0,
+                    help="c5: running slots per cluster / 64 (0 = the engine's default, 4 x nodes)")
     ap.add_argument("--comm", action="store_true",
                     help="c5: run the RCCL tick loop (ncclAllGather per tick) even at N=1, on a world-1 "
                          "communicator (MCS_RCCL_GRAPH=0: eager launches instead of the captured hipGraph)")
@@ -265,7 +267,8 @@ def main_c5_delay(args, world, rank, local_rank):
                                + ("one RCCL all-gather of the exchange blocks per tick" if world > 1 else
                                   "exchange in HBM")
                                + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "RCCL eager" if ts["loop_form"] == 1
-                                                    else "RCCL captured in a hipGraph") + ")",
+                                                    else "RCCL captured in a hipGraph" if ts["loop_form"] == 2
+                                                    else "resident in one workgroup") + ")",
             },
             "roofline": {
                 "bound": "hbm",
@@ -311,7 +314,7 @@ def main_c5(args, world, rank, local_rank):
         raise SystemExit(f"--clusters {args.clusters} must divide over {world} ranks")
     per = args.clusters // world
     lam = scaled_lambda(args.nodes, load=args.load)
-    eng = Engine(local_rank, borrow=True, trader=True)
+    eng = Engine(local_rank, borrow=True, trader=True, slot_pool=args.slot_pool)
     eng.load_clusters(replicate(uniform_cluster(args.nodes), per))
     eng.set_shard(rank, world)
     eng.generate_jobs(GenParams(seed=args.seed, arrival_mode=1, lam=lam), args.jobs_per_cluster)
@@ -371,7 +374,8 @@ def main_c5(args, world, rank, local_rank):
                 "jobs_per_cluster": args.jobs_per_cluster,
                 "parallelism": (f"{world} shard(s); per-tick RCCL all-gather" if dist_on or args.comm else "1 GPU, exchange in HBM")
                                + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "RCCL eager" if ts["loop_form"] == 1
-                                                    else "RCCL captured in a hipGraph") + ")",
+                                                    else "RCCL captured in a hipGraph" if ts["loop_form"] == 2
+                                                    else "resident in one workgroup") + ")",
             },
             "roofline": {
                 "bound": "hbm",

@@ -92,7 +92,8 @@ typedef struct mcs_trade_stats {
     uint32_t flags;        /* OR of MCS_FLAG_* over clusters and logs */
     uint32_t loop_form;    /* tick loop that ran: 0 = one engine, hipGraph-replayed ticks; 1 = RCCL
                               all-gather per tick, eager launches; 2 = RCCL, kernels and all-gathers
-                              captured in a hipGraph (MCS_RCCL_GRAPH=0 forces 1); 3 = resident */
+                              captured in a hipGraph (MCS_RCCL_GRAPH=0 forces 1); 3 = one
+                              engine, the whole system resident in one workgroup */
     double kernel_ms;      /* device time of the lock-step loop (HIP events) */
     double wall_ms;
 } mcs_trade_stats;

@@ -289,14 +289,20 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
         lc[i] = free_c[i];
         lm[i] = free_m[i];
     }
+    e->sums_lt24 = true;
     for (uint32_t c = 0; c < n_clusters; ++c) { /* setMaxCluster, client.go:68-83 */
         uint32_t a = 0, b = 0;
+        uint64_t sc = 0, sm = 0;
         for (uint32_t i = node_offsets[c]; i < node_offsets[c + 1]; ++i) {
             a = std::max(a, cap_c[i]);
             b = std::max(b, cap_m[i]);
+            sc += std::max(cap_c[i], free_c[i]);
+            sm += std::max(cap_m[i], free_m[i]);
         }
         mxc[c] = a;
         mxm[c] = b;
+        /* every partial sum of GetResourceUtilization's float32 loop is then an exact integer */
+        if (sc >= (1ull << 24) || sm >= (1ull << 24)) e->sums_lt24 = false;
     }
     const size_t nb = (nn ? nn : 1);
     HIPCHK(e, hipMalloc(&e->d_free0, nb * sizeof(uint2)));

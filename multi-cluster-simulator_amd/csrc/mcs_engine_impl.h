@@ -50,6 +50,7 @@ uint32_t horizon_extra(const mcs_engine* e);  // max_wait_s under DELAY, else 0
 constexpr uint32_t kLoopGraph = 0;      // one engine, ticks replayed from a captured hipGraph
 constexpr uint32_t kLoopRcclEager = 1;  // RCCL all-gather per tick, launches enqueued eagerly
 constexpr uint32_t kLoopRcclGraph = 2;  // RCCL all-gather per tick, captured with the kernels
+constexpr uint32_t kLoopResident = 3;   // one engine, the whole system resident in one workgroup
 
 // Capture `ticks` ticks of `tick(stream)` (kernels and the RCCL all-gather) into one executable
 // graph.  Returns nullptr, with the stream out of capture mode and the HIP error state cleared, when
@@ -88,6 +89,7 @@ struct mcs_engine {
     uint32_t max_n = 0;
     bool free_lt31 = false;  // every node free value < 2^31 - 1 (fifo_asm_kernel<32> guard bits)
     bool free_lt15 = false;  // every node free value < 2^15 - 1 (fifo_asm_kernel<16>)
+    bool sums_lt24 = false;  // every cluster's sum of max(capacity, availability) < 2^24 per resource
     uint64_t total_nodes = 0, total_jobs = 0;
     std::vector<uint32_t> node_off;
     std::vector<uint64_t> job_off;

@@ -163,9 +163,35 @@ int poll_ctl(mcs_engine* e) {
     return MCS_OK;
 }
 
-// one engine holds the whole system: the four phases of kGraphTicks ticks captured once, replayed
+// one engine holds the whole system.  When it fits one workgroup (<= 64 clusters of <= 256 nodes,
+// 1024 slots each, exact integer utilization sums) the tick loop runs resident (mcs_trade_res.hip),
+// kResTicks ticks per launch; otherwise the four phases of kGraphTicks ticks are captured once and
+// replayed.  MCS_TRADE_RESIDENT=0 forces the replayed kernels.
+constexpr uint32_t kResTicks = 1u << 16;
+
+bool resident_ok(mcs_engine* e, size_t* lds) {
+    const char* env = getenv("MCS_TRADE_RESIDENT");
+    if (env && atoi(env) == 0) return false;
+    if (!trade_resident_shape(e->td->a) || !e->sums_lt24) return false;
+    int max_lds = 0;
+    if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device) != hipSuccess)
+        return false;
+    *lds = trade_resident_lds(e->td->a.Ct, e->td->a.ns);
+    return *lds <= (size_t)max_lds;
+}
+
 int run_local(mcs_engine* e) {
     TradeDev* td = e->td;
+    size_t lds = 0;
+    if (resident_ok(e, &lds)) {
+        td->loop_form = kLoopResident;
+        for (;;) {
+            const hipError_t st = launch_trade_resident(td->a, kResTicks, lds, e->stream);
+            if (st != hipSuccess) return hip_fail(e, "resident tick kernel", st);
+            if (int s = poll_ctl(e)) return s;
+            if (td->h_ctl->done) return MCS_OK;
+        }
+    }
     if (!td->graph) {
         hipGraph_t g = nullptr;
         HIPCHK(e, hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));

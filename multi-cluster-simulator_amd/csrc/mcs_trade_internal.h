@@ -132,5 +132,10 @@ __device__ __forceinline__ unsigned long long* tr_snap(const TradeArgs& a, uint3
 
 hipError_t launch_trade_init(const TradeArgs& a, hipStream_t s);
 hipError_t launch_trade_phase(const TradeArgs& a, int phase, hipStream_t s);
+// the whole system resident in one workgroup (mcs_trade_res.hip): shape check, LDS bytes, launch
+constexpr uint32_t kTrResMaxClusters = 64;
+bool trade_resident_shape(const TradeArgs& a);
+size_t trade_resident_lds(uint32_t n_clusters, uint32_t ns);
+hipError_t launch_trade_resident(const TradeArgs& a, uint32_t tick_budget, size_t lds, hipStream_t s);
 
 }  // namespace mcs

@@ -1,0 +1,574 @@
+// mcs_trade_res.hip — the lock-step trading system (mcs_trade.h) resident in ONE
+// workgroup: the tick loop of a whole one-GPU system of up to 64 clusters x 256 nodes with 256,
+// 512 or 1024 running slots each (C5: 64 x 256) as one launch of 16 waves on one CU, its phases
+// separated by s_barrier instead of kernel boundaries.
+//
+// The three-kernel tick (mcs_trade.hip) spends its ~18 us re-staging every cluster's state: node
+// vectors and slot finish times HBM -> LDS -> HBM in tr_step, lender snapshots in tr_lend, trader
+// state in tr_trader, each a dependent memory round trip behind a kernel boundary.  Here the state
+// stays on the CU across ticks:
+//   * every cluster's node vector in LDS (u64 {free_c | free_m << 32}, 128 KiB for 64 x 256);
+//   * each wave owns up to 4 clusters; their running-slot finish times live in that wave's VGPRs
+//     (4, 8 or 16 rows of 64 lanes per cluster; the cluster being stepped is copied into a working
+//     set), the slots' {node, payload} in HBM (written at a commit, read back only when the slot
+//     expires, through L2), the clusters' queue state in LDS;
+//   * the exchange records, acceptances, LentQueue lengths, trader locks and the clock in LDS.
+// One tick (LSFIFO), each phase the body of the kernel it replaces:
+//   A  every wave, its clusters in turn: releases, arrivals, the Fifo decisions of the tick
+//      (scheduler.go:216-296), the borrow request (server.go:160-248), the utilization sample
+//      (cluster.go:46-63), the exchange record                                   [tr_step_kernel]
+//   B  every wave, its clusters as lenders: Lend (strict '>', scheduler.go:194-202) against the
+//      tick's requests in borrower order, LentQueue appends (server.go:80-113)    [tr_lend_kernel]
+//   C+D wave 0: the borrowers' BorrowedQueue moves, the trader rounds (trader.go:280-325,
+//      193-278; server.go:31-85) and the next tick                              [tr_trader_kernel]
+// The utilization sample is an integer wave sum converted once: exact against Go's float32 sum
+// in node order because the engine picks this kernel only when every cluster's sum of
+// max(capacity, JSON availability) per resource is below 2^24 (every partial sum is then an
+// integer float32 represents exactly).  Same results bit for bit as the three-kernel tick
+// (tests/test_gpu_trade.py, MCS_TRADE_RESIDENT=0 forces that path).
+#include "mcs_trade_internal.h"
+#include "mcs_trader_dev.h"
+#include "mcs_wave.h"
+
+namespace mcs {
+namespace {
+
+constexpr int kResWaves = 16;
+constexpr int kResCpw = 4;      // clusters per wave
+constexpr uint32_t kResMaxNodes = 256;
+
+__device__ __forceinline__ uint32_t rwave_sum(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+
+// HBM written by this kernel and read back later: through L2, never a stale line of the vector L1
+__device__ __forceinline__ uint64_t rld64(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t rld32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct ResShared {  // (the node vectors follow, Ct * ns u64)
+    TrXRec x[kTrResMaxClusters];
+    TrCluster st[kTrResMaxClusters];
+    TrTrader trs[kTrResMaxClusters];
+    TrRecC rcs[kTrResMaxClusters];
+    uint32_t acc[kTrResMaxClusters], lqp[kTrResMaxClusters], fb[kTrResMaxClusters];
+    uint32_t T, done, ticks, flags;
+    unsigned long long n_trades, n_won;
+};
+
+template <int kResRows>  // slot rows per cluster (64 slots each)
+__global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArgs a, uint32_t tick_budget) {
+    extern __shared__ unsigned long long res_smem[];
+    ResShared& sh = *reinterpret_cast<ResShared*>(res_smem);
+    unsigned long long* const nodes_all = res_smem + (sizeof(ResShared) + 7) / 8;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t C = a.Ct, ns = a.ns, S = a.S;
+
+    // ---- state in: the node vectors, the clusters, the traders, the clock ----
+    for (uint32_t c = 0; c < C; ++c) {
+        const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
+        for (uint32_t i = threadIdx.x; i < N; i += kResWaves * kWave) nodes_all[(size_t)c * ns + i] = a.tn[n0 + i];
+    }
+    for (uint32_t c = threadIdx.x; c < C; c += kResWaves * kWave) {
+        sh.st[c] = a.cl[c];
+        sh.trs[c] = a.tr[c];
+        sh.acc[c] = 0u;
+    }
+    if (threadIdx.x == 0) {
+        const TrCtl ctl = *a.ctl;
+        sh.T = ctl.T;
+        sh.done = ctl.done;
+        sh.ticks = ctl.ticks;
+        sh.flags = ctl.flags;
+        sh.n_trades = ctl.n_trades;
+        sh.n_won = ctl.n_won;
+    }
+    // this wave's clusters: slot finish times in registers (row r, lane l = slot r * 64 + l)
+    uint32_t fin[kResCpw][kResRows];
+    uint32_t frm[kResCpw];  // free rows of this lane
+#pragma unroll
+    for (int k = 0; k < kResCpw; ++k) {
+        const uint32_t c = wave * kResCpw + k;
+        frm[k] = 0u;
+#pragma unroll
+        for (int r = 0; r < kResRows; ++r) {
+            fin[k][r] = c < C ? a.sfin[(size_t)c * S + r * kWave + lane] : kEmpty;
+            if (fin[k][r] == kEmpty) frm[k] |= 1u << r;
+        }
+    }
+    __syncthreads();
+
+    for (uint32_t it = 0; it < tick_budget; ++it) {
+        if (sh.done) break;
+        const uint32_t T = sh.T;
+
+        // ---- phase A: each wave's clusters, in turn (tr_step_kernel) ----
+        // (one cluster's 16 slot rows are copied into a working set and back: the loop body is
+        // not unrolled over the wave's clusters, which keeps it within 128 VGPRs)
+#pragma unroll 1
+        for (int k = 0; k < kResCpw; ++k) {
+            const uint32_t c = wave * kResCpw + k;
+            if (c >= C) break;
+            uint32_t wf[kResRows];
+            uint32_t wfrm = k == 0 ? frm[0] : k == 1 ? frm[1] : k == 2 ? frm[2] : frm[3];
+#pragma unroll
+            for (int r = 0; r < kResRows; ++r)
+                wf[r] = k == 0 ? fin[0][r] : k == 1 ? fin[1][r] : k == 2 ? fin[2][r] : fin[3][r];
+            unsigned long long* const nodes = nodes_all + (size_t)c * ns;
+            const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
+            const uint64_t j0 = a.job_off[c];
+            const uint32_t J = (uint32_t)(a.job_off[c + 1] - j0);
+            const uint4* __restrict__ jobs = a.jobs + j0;
+            const size_t sb = (size_t)c * S;
+            const uint32_t vn = sh.trs[c].vnodes;
+            TrCluster& st = sh.st[c];  // (in LDS: registers hold the slot rows)
+
+            // releases due at T (cluster.go:153-157), before the tick's decisions
+            if (st.minf <= T) {
+                uint32_t lm = kEmpty, nrel = 0;
+#pragma unroll
+                for (int r = 0; r < kResRows; ++r) {
+                    const uint32_t f = wf[r];
+                    if (f <= T) {
+                        const uint32_t slot = r * kWave + lane;
+                        const uint32_t nd = rld32(a.snode + sb + slot);
+                        if (nd < N) atomicAdd(&nodes[nd], rld64(a.scm + sb + slot));
+                        wf[r] = kEmpty;
+                        wfrm |= 1u << r;
+                        ++nrel;
+                    } else {
+                        lm = f < lm ? f : lm;
+                    }
+                }
+                st.nrun -= rwave_sum(nrel);
+                st.minf = wave_min_u32(lm);
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            }
+            // arrivals up to T join the ReadyQueue (jobs are sorted by arrival)
+            while (st.next_arr < J) {
+                const uint32_t i = st.next_arr + lane;
+                const bool ok = i < J && jobs[i].x <= T;
+                const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(ok));
+                st.next_arr += n;
+                if (n < (uint32_t)kWave) break;
+            }
+
+            // ScheduleJob (scheduler.go:127-139): lowest node with both >=; zero-capacity virtual
+            // nodes (AddVirtualNode, cluster.go:79) follow the physical ones
+            auto first_fit = [&](uint32_t jc, uint32_t jm) -> uint32_t {
+                uint32_t best = kEmpty;
+                for (uint32_t b = 0; b < N; b += kWave) {
+                    const uint32_t i = b + lane;
+                    if (i < N) {
+                        const unsigned long long v = nodes[i];
+                        if ((uint32_t)v >= jc && (uint32_t)(v >> 32) >= jm) best = i;
+                    }
+                    if (__ballot(best != kEmpty)) break;
+                }
+                uint32_t kk = wave_min_u32(best);
+                if (kk == kEmpty && jc == 0u && jm == 0u && vn > 0u) kk = N;
+                return kk;
+            };
+            // Node.RunJob commit (cluster.go:144-148) + running-slot insert; false on overflow
+            auto commit = [&](uint32_t kn, uint32_t jc, uint32_t jm, uint32_t f) -> bool {
+                const unsigned long long need = (unsigned long long)jc | ((unsigned long long)jm << 32);
+                const unsigned long long any = __ballot(wfrm != 0u);
+                if (!any) return false;
+                const uint32_t sel = (uint32_t)__builtin_ctzll(any);
+                const uint32_t row = (uint32_t)__builtin_ctz(readlane(wfrm, sel));
+                if (lane == sel) {
+                    if (kn < N) atomicSub(&nodes[kn], need);
+                    a.snode[sb + row * kWave + sel] = kn;
+                    a.scm[sb + row * kWave + sel] = need;
+#pragma unroll
+                    for (int r = 0; r < kResRows; ++r)
+                        if ((uint32_t)r == row) wf[r] = f;
+                    wfrm &= ~(1u << row);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // the node commit before the next fit
+                ++st.nrun;
+                st.peak = st.nrun > st.peak ? st.nrun : st.peak;
+                st.minf = f < st.minf ? f : st.minf;
+                return true;
+            };
+            auto place_own = [&](uint32_t j, uint32_t kn, uint4 jb) -> bool {
+                const uint32_t f = T + jb.y;
+                if (jb.y != 0u && !commit(kn, jb.z, jb.w, f)) return false;
+                if (lane == 0) {
+                    a.out_node[j0 + j] = (int32_t)kn;
+                    a.out_start[j0 + j] = T;
+                    a.out_finish[j0 + j] = f;
+                }
+                ++st.placed;
+                ++st.decided;
+                return true;
+            };
+
+            TrRecA req{kEmpty, 0u, 0u, 0u};
+            for (;;) {
+                if (st.has_w) {  // WaitQueue head (scheduler.go:219-251)
+                    const uint4 jb = jobs[st.w];
+                    const uint32_t kn = first_fit(jb.z, jb.w);
+                    if (kn != kEmpty) {
+                        if (!place_own(st.w, kn, jb)) {
+                            st.flags |= MCS_FLAG_OVERFLOW;
+                            break;
+                        }
+                        st.has_w = 0u;
+                    } else if (a.borrow) {
+                        req = TrRecA{st.w, jb.z, jb.w, jb.y};  // BorrowResources (:234)
+                    }
+                    break;  // time.Sleep(1 s), :250
+                }
+                if (st.rq_head < st.next_arr) {  // ReadyQueue head (:255-272), no sleep
+                    const uint32_t j = st.rq_head++;
+                    const uint4 jb = jobs[j];
+                    const uint32_t kn = first_fit(jb.z, jb.w);
+                    if (kn != kEmpty) {
+                        if (!place_own(j, kn, jb)) {
+                            st.flags |= MCS_FLAG_OVERFLOW;
+                            break;
+                        }
+                    } else {
+                        st.has_w = 1u;
+                        st.w = j;
+                        ++st.waited;
+                    }
+                    continue;
+                }
+                if (st.lq_len > 0u) {  // LentQueue head (:277-290), written by this wave in phase B
+                    const TrLq* q = a.lq + (size_t)c * a.LQ + st.lq_head;
+                    const uint64_t w0 = rld64(reinterpret_cast<const unsigned long long*>(q));
+                    const uint64_t w1 = rld64(reinterpret_cast<const unsigned long long*>(q) + 1);
+                    const uint64_t w2 = rld64(reinterpret_cast<const unsigned long long*>(q) + 2);
+                    const uint32_t eb = (uint32_t)w0, ej = (uint32_t)(w0 >> 32);
+                    const uint32_t ec = (uint32_t)w1, em = (uint32_t)(w1 >> 32), ed = (uint32_t)w2;
+                    const uint32_t kn = first_fit(ec, em);
+                    if (kn != kEmpty) {
+                        const uint32_t f = T + ed;
+                        if (ed != 0u && !commit(kn, ec, em, f)) {
+                            st.flags |= MCS_FLAG_OVERFLOW;
+                            break;
+                        }
+                        if (lane == 0) {
+                            const unsigned long long idx = atomicAdd(&a.ctl->n_lent, 1ull);
+                            if (idx < a.lent_cap) {
+                                mcs_lent_rec rec;
+                                rec.lender = c;
+                                rec.borrower = eb;
+                                rec.job = ej;
+                                rec.node = kn;
+                                rec.start_s = T;
+                                rec.finish_s = f;
+                                rec.pad = 0u;
+                                a.lent_log[idx] = rec;
+                            }
+                        }
+                        ++st.lent_runs;
+                        st.lq_head = st.lq_head + 1u == a.LQ ? 0u : st.lq_head + 1u;
+                        --st.lq_len;
+                    }
+                    break;  // sleep 1 s (:289)
+                }
+                break;  // idle sleep (:294)
+            }
+
+            // GetResourceUtilization (cluster.go:46-63) on the ticks a trader reads it (see
+            // tr_step_kernel): an exact integer sum (the engine's eligibility check, above)
+            if (a.trader && T % a.sample_period == 0u) {
+                bool due = false;
+                for (uint32_t q = lane; q < C; q += kWave) due = due || sh.trs[q].next_due <= T;
+                if (__ballot(due)) {
+                    uint32_t uc = 0u, um = 0u;
+                    for (uint32_t i = lane; i < N; i += kWave) {
+                        const unsigned long long v = nodes[i];
+                        const uint2 cp = a.cap[n0 + i];
+                        uc += cp.x - (uint32_t)v;  // (mod 2^32: the signed sum, < 2^24 in size)
+                        um += cp.y - (uint32_t)(v >> 32);
+                    }
+                    const float sc = (float)(int32_t)rwave_sum(uc), sm = (float)(int32_t)rwave_sum(um);
+                    st.cu = __fdiv_rn(sc, (float)st.total_c);
+                    st.mu = __fdiv_rn(sm, (float)st.total_m);
+                }
+            }
+            if (lane == 0) {
+                TrXRec x;
+                x.req = req;
+                x.n = N;
+                x.has_w = st.has_w;
+                x.lq_len = st.lq_len;
+                x.rq_busy = st.rq_head < st.next_arr ? 1u : 0u;
+                x.decided = st.decided;
+                x.J = J;
+                x.next_arr_t = st.next_arr < J ? jobs[st.next_arr].x : kEmpty;
+                x.flags = st.flags;
+                x.cu = st.cu;
+                x.mu = st.mu;
+                x.total_c = st.total_c;
+                x.total_m = st.total_m;
+                sh.x[c] = x;
+            }
+#pragma unroll
+            for (int r = 0; r < kResRows; ++r) {
+                fin[0][r] = k == 0 ? wf[r] : fin[0][r];
+                fin[1][r] = k == 1 ? wf[r] : fin[1][r];
+                fin[2][r] = k == 2 ? wf[r] : fin[2][r];
+                fin[3][r] = k == 3 ? wf[r] : fin[3][r];
+            }
+            frm[0] = k == 0 ? wfrm : frm[0];
+            frm[1] = k == 1 ? wfrm : frm[1];
+            frm[2] = k == 2 ? wfrm : frm[2];
+            frm[3] = k == 3 ? wfrm : frm[3];
+        }
+        __syncthreads();
+
+        // ---- phase B: each wave's clusters as lenders, requests in borrower order (tr_lend_kernel) ----
+#pragma unroll
+        for (int k = 0; k < kResCpw; ++k) {
+            const uint32_t L = wave * kResCpw + k;
+            if (L >= C) break;
+            const unsigned long long* const nodes = nodes_all + (size_t)L * ns;
+            const uint32_t N = sh.x[L].n;
+            uint32_t lq_len = sh.x[L].lq_len, fb = 0;
+            const uint32_t lq_head = sh.st[L].lq_head;
+            const uint32_t LQ = a.LQ;
+            for (uint32_t b0 = 0; b0 < C; b0 += kWave) {
+                const uint32_t bl = b0 + lane;
+                TrRecA rl{kEmpty, 0u, 0u, 0u};
+                if (bl < C && bl != L) rl = sh.x[bl].req;  // self skipped (:176)
+                unsigned long long pend = __ballot(rl.job != kEmpty);
+                while (pend) {
+                    const uint32_t bi = (uint32_t)__builtin_ctzll(pend);
+                    const uint32_t b = b0 + bi;
+                    pend &= pend - 1ull;
+                    const TrRecA r{readlane(rl.job, bi), readlane(rl.c, bi), readlane(rl.m, bi), readlane(rl.dur, bi)};
+                    bool ok = false;
+                    for (uint32_t i0 = 0; i0 < N; i0 += kWave) {
+                        const uint32_t i = i0 + lane;
+                        if (i < N) {
+                            const unsigned long long v = nodes[i];
+                            ok = ok || ((uint32_t)v > r.c && (uint32_t)(v >> 32) > r.m);
+                        }
+                        if (__ballot(ok)) break;
+                    }
+                    if (!__ballot(ok)) continue;  // "can't lend" (scheduler.go:201)
+                    if (lq_len >= LQ) {
+                        fb |= MCS_FLAG_LENT_OVERFLOW;
+                        continue;
+                    }
+                    if (lane == 0) {
+                        uint32_t at = lq_head + lq_len;
+                        at = at >= LQ ? at - LQ : at;
+                        TrLq e{};
+                        e.borrower = b;
+                        e.job = r.job;
+                        e.c = r.c;
+                        e.m = r.m;
+                        e.dur = r.dur;
+                        a.lq[(size_t)L * LQ + at] = e;
+                        sh.acc[b] = 1u;  // (every accepting lender writes the same value)
+                    }
+                    ++lq_len;
+                }
+            }
+            if (lane == 0) {
+                sh.lqp[L] = lq_len;
+                sh.fb[L] = fb;
+                sh.st[L].lq_len = lq_len;
+                sh.st[L].flags |= fb;
+            }
+        }
+        __syncthreads();
+
+        // ---- phases C and D: wave 0 (tr_trader_kernel) ----
+        if (wave == 0) {
+            for (uint32_t g = lane; g < C; g += kWave) {  // the borrower step (post_cluster)
+                const TrXRec x = sh.x[g];
+                const uint32_t accg = sh.acc[g], lq = sh.lqp[g], fbg = sh.fb[g];
+                uint32_t has_w = x.has_w, decided = x.decided;
+                if (x.req.job != kEmpty && accg) {  // BorrowedQueue append (scheduler.go:237-242)
+                    has_w = 0u;
+                    ++decided;
+                    const uint64_t j0 = a.job_off[g];
+                    a.out_node[j0 + x.req.job] = MCS_NODE_BORROWED;
+                    a.out_start[j0 + x.req.job] = T;
+                    a.out_finish[j0 + x.req.job] = MCS_TIME_NONE;
+                    sh.st[g].has_w = 0u;
+                    ++sh.st[g].decided;
+                    ++sh.st[g].borrowed;
+                }
+                sh.acc[g] = 0u;
+                TrRecC o;
+                o.cu = x.cu;
+                o.mu = x.mu;
+                o.total_c = x.total_c;
+                o.total_m = x.total_m;
+                o.busy = (has_w || lq > 0u || x.rq_busy) ? 1u : 0u;
+                o.next_arr_t = x.next_arr_t;
+                o.done = (decided == x.J && lq == 0u) ? 1u : 0u;
+                o.flags = x.flags | fbg;
+                sh.rcs[g] = o;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            unsigned long long n_trades = sh.n_trades, n_won = sh.n_won;
+            uint32_t lflags = 0;
+            if (a.trader) {
+                for (uint32_t q0 = 0; q0 < C; q0 += kWave) {
+                    const uint32_t ql = q0 + lane;
+                    unsigned long long due = __ballot(ql < C && sh.trs[ql].next_due <= T);
+                    while (due) {  // RequestPolicyMonitor of requester q (trader.go:282-324)
+                        const uint32_t q = q0 + (uint32_t)__builtin_ctzll(due);
+                        due &= due - 1ull;
+                        const TrRecC rq = sh.rcs[q];
+                        const bool broken = rq.cu > 0.8f || rq.mu > 0.8f;  // Utilization (:127-130)
+                        if (!broken) {
+                            if (lane == 0) sh.trs[q].next_due = T + a.period;
+                            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                            continue;
+                        }
+                        uint32_t napp = 0, winner = kEmpty;
+                        for (uint32_t r0 = 0; r0 < C; r0 += kWave) {  // RequestResource, index order
+                            const uint32_t r = r0 + lane;
+                            bool app = false;
+                            if (r < C && r != q) {
+                                TrTrader t = sh.trs[r];
+                                if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
+                                if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
+                                    const TrRecC rr = sh.rcs[r];
+                                    app = approve_trade_dev(rr.total_c, rr.total_m, rr.cu, rr.mu, 0u, 0u, 0u);
+                                    t.lock_id = t.next_id++;  // set even when not approving (:44-46)
+                                    t.lock_until = T + a.lock_s;
+                                }
+                                sh.trs[r] = t;
+                            }
+                            const unsigned long long ab = __ballot(app);
+                            napp += (uint32_t)__builtin_popcountll(ab);
+                            if (winner == kEmpty && ab) winner = r0 + (uint32_t)__builtin_ctzll(ab);
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                        if (lane == 0) {
+                            if (winner != kEmpty) {
+                                sh.trs[winner].lock_id = 0u;  // ApproveContract unlocks (:83)
+                                sh.trs[q].vnodes += 1u;       // AddVirtualNode(0 cores, 0 memory)
+                                ++n_won;
+                            }
+                            if (n_trades < a.trade_cap) {
+                                mcs_trade_rec rec;
+                                rec.t_s = T;
+                                rec.requester = q;
+                                rec.winner = winner == kEmpty ? -1 : (int32_t)winner;
+                                rec.approvals = napp;
+                                a.trade_log[n_trades] = rec;
+                            } else {
+                                lflags |= MCS_FLAG_LOG_OVERFLOW;
+                            }
+                            sh.trs[q].next_due = T + (winner != kEmpty ? a.ok_sleep : a.fail_sleep) + a.period;
+                        }
+                        ++n_trades;
+                        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                    }
+                }
+            }
+            // the next tick: T+1 while any queue is busy, else the next arrival or trader round
+            bool all_done = true, busy = false;
+            uint32_t nxt = kEmpty, fl = 0;
+            for (uint32_t q = lane; q < C; q += kWave) {
+                const TrRecC rc = sh.rcs[q];
+                all_done = all_done && rc.done;
+                busy = busy || rc.busy;
+                nxt = rc.next_arr_t < nxt ? rc.next_arr_t : nxt;
+                if (a.trader) nxt = sh.trs[q].next_due < nxt ? sh.trs[q].next_due : nxt;
+                fl |= rc.flags;
+            }
+            const bool done_all = !__ballot(!all_done);
+            const bool busy_any = __ballot(busy) != 0ull;
+            nxt = wave_min_u32(nxt);
+            for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o);
+            if (lane == 0) {
+                uint32_t flags = sh.flags | fl | lflags;
+                uint32_t done = 0, Tn = T;
+                const uint32_t fatal = MCS_FLAG_OVERFLOW | MCS_FLAG_LENT_OVERFLOW;
+                if (done_all || (flags & fatal)) {
+                    done = 1u;
+                } else if (T >= a.t_max || (!busy_any && nxt == kEmpty)) {
+                    done = 1u;
+                    flags |= MCS_FLAG_T_MAX;
+                } else {
+                    Tn = (busy_any || nxt <= T + 1u) ? T + 1u : nxt;
+                }
+                sh.T = Tn;
+                sh.done = done;
+                sh.ticks += 1u;
+                sh.flags = flags;
+                sh.n_trades = n_trades;
+                sh.n_won = n_won;
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- state out (the next launch, the stats and the readers take it from HBM) ----
+    for (uint32_t c = 0; c < C; ++c) {
+        const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
+        for (uint32_t i = threadIdx.x; i < N; i += kResWaves * kWave) a.tn[n0 + i] = nodes_all[(size_t)c * ns + i];
+    }
+    for (uint32_t c = threadIdx.x; c < C; c += kResWaves * kWave) {
+        a.cl[c] = sh.st[c];
+        a.tr[c] = sh.trs[c];
+    }
+#pragma unroll
+    for (int k = 0; k < kResCpw; ++k) {
+        const uint32_t c = wave * kResCpw + k;
+        if (c < C) {
+#pragma unroll
+            for (int r = 0; r < kResRows; ++r) a.sfin[(size_t)c * S + r * kWave + lane] = fin[k][r];
+        }
+    }
+    if (threadIdx.x == 0) {
+        TrCtl ctl;
+        ctl.T = sh.T;
+        ctl.done = sh.done;
+        ctl.ticks = sh.ticks;
+        ctl.flags = sh.flags;
+        ctl.n_lent = rld64(&a.ctl->n_lent);
+        ctl.n_trades = sh.n_trades;
+        ctl.n_won = sh.n_won;
+        *a.ctl = ctl;
+    }
+}
+
+}  // namespace
+
+size_t trade_resident_lds(uint32_t n_clusters, uint32_t ns) {
+    return (sizeof(ResShared) + 7) / 8 * 8 + (size_t)n_clusters * ns * 8u;
+}
+
+// one workgroup holds the whole system: one engine (world 1), <= 64 clusters of <= 256 nodes,
+// 1024 running slots each, and the LDS to hold them (checked against the device by the caller)
+bool trade_resident_shape(const TradeArgs& a) {
+    return a.world == 1 && a.Ct <= (uint32_t)(kResWaves * kResCpw) && a.Ct <= kTrResMaxClusters &&
+           a.ns <= kResMaxNodes && (a.S == 4u * kWave || a.S == 8u * kWave || a.S == 16u * kWave);
+}
+
+hipError_t launch_trade_resident(const TradeArgs& a, uint32_t tick_budget, size_t lds, hipStream_t s) {
+    // 256 / 512 slots per cluster: 16 / 32 VGPRs of finish times per wave; 1024: 64 (that variant
+    // spills registers)
+    const void* fn = a.S == 4u * kWave   ? (const void*)tr_resident_kernel<4>
+                     : a.S == 8u * kWave ? (const void*)tr_resident_kernel<8>
+                                         : (const void*)tr_resident_kernel<16>;
+    const hipError_t st = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (st != hipSuccess) return st;
+    if (a.S == 4u * kWave)
+        hipLaunchKernelGGL(tr_resident_kernel<4>, dim3(1), dim3(kResWaves * kWave), lds, s, a, tick_budget);
+    else if (a.S == 8u * kWave)
+        hipLaunchKernelGGL(tr_resident_kernel<8>, dim3(1), dim3(kResWaves * kWave), lds, s, a, tick_budget);
+    else
+        hipLaunchKernelGGL(tr_resident_kernel<16>, dim3(1), dim3(kResWaves * kWave), lds, s, a, tick_budget);
+    return hipGetLastError();
+}
+
+}  // namespace mcs

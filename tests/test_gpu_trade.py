@@ -204,3 +204,26 @@ def test_gpu_trade_fuzz(shape, seed):
     arrays, streams = fuzz_workload(shape, seed, n_clusters=12, J=500, blocking=False)
     g = gpu_trade(arrays, streams)
     assert_trade_parity(arrays, streams, g)
+
+
+@pytest.mark.parametrize("kind,C,J,pool", [("n64_hot", 8, 1500, 0), ("n256", 16, 3000, 8), ("n256", 16, 3000, 0),
+                                           ("small", 64, 1500, 0)])
+def test_gpu_trade_resident_equals_kernels_and_oracle(kind, C, J, pool, monkeypatch):
+    """The whole system resident in one workgroup (mcs_trade_res.hip; loop_form 3, picked for one
+    engine of <= 64 clusters of <= 256 nodes with 256/512/1024 slots) == the graph-replayed tick
+    kernels (MCS_TRADE_RESIDENT=0, loop_form 0) == the oracle, on every output."""
+    arrays, streams, _ = seeded_workload(kind, C, J)
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MCS_TRADE_RESIDENT", mode)
+        res[mode] = gpu_trade(arrays, streams, slot_pool=pool)
+    assert res["1"]["tstats"]["loop_form"] == 3 and res["0"]["tstats"]["loop_form"] == 0
+    for k in ("node", "start", "finish"):
+        np.testing.assert_array_equal(res["1"][k], res["0"][k], err_msg=k)
+    assert lent_rows(res["1"]["lent"]) == lent_rows(res["0"]["lent"])
+    assert res["1"]["trades"].tobytes() == res["0"]["trades"].tobytes()
+    np.testing.assert_array_equal(res["1"]["virtual_nodes"], res["0"]["virtual_nodes"])
+    for f in ("placed", "borrowed", "waited", "undecided", "lent_runs", "lent_pending", "trades", "trades_won",
+              "ticks", "t_final", "flags"):
+        assert res["1"]["tstats"][f] == res["0"]["tstats"][f], f
+    assert_trade_parity(arrays, streams, res["1"])
