@@ -59,6 +59,15 @@ uint32_t auto_slots(uint32_t max_n) {
     return s;
 }
 
+// a one-engine system the resident tick kernel can hold (mcs_trade_res.hip; the LDS check is
+// resident_ok's).  Its slot finish times live in VGPRs, so such a system starts at 512 slots per
+// cluster (8 rows; 1024 spill): an overflow re-runs it at 1024 like any other pool overflow.
+bool resident_wanted(const mcs_engine* e) {
+    const char* env = getenv("MCS_TRADE_RESIDENT");
+    if (env && atoi(env) == 0) return false;
+    return e->world == 1 && e->C <= kTrResMaxClusters && e->max_n <= 256u && e->sums_lt24;
+}
+
 constexpr uint32_t kMaxLq = 1u << 24;  // LentQueue entries per cluster (512 MB per cluster)
 
 // Every acceptor of a borrow request keeps its own copy (server.go:232-237) and an overloaded
@@ -80,7 +89,9 @@ int trade_alloc(mcs_engine* e) {
     if (Ct > kTrMaxClusters) return fail(e, MCS_E_INVALID, "more than 1024 clusters in a trading system");
     if (e->max_n > kTrMaxNodes) return fail(e, MCS_E_INVALID, "more than 1024 nodes in a cluster");
     const uint32_t S = e->cfg.slot_pool ? 64u * e->cfg.slot_pool
-                                        : (e->tr_slots ? e->tr_slots : auto_slots(e->max_n));
+                       : e->tr_slots       ? e->tr_slots
+                       : resident_wanted(e) ? std::min<uint32_t>(512u, auto_slots(e->max_n))
+                                           : auto_slots(e->max_n);
     if (S > kTrMaxSlots) return fail(e, MCS_E_INVALID, "slot pool above 4096");
     const uint32_t LQ = e->cfg.lent_queue_cap ? e->cfg.lent_queue_cap : (e->tr_lq ? e->tr_lq : auto_lq(e));
     TradeDev* td = new (std::nothrow) TradeDev();

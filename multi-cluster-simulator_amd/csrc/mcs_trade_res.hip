@@ -56,9 +56,27 @@ struct ResShared {  // (the node vectors follow, Ct * ns u64)
     TrTrader trs[kTrResMaxClusters];
     TrRecC rcs[kTrResMaxClusters];
     uint32_t acc[kTrResMaxClusters], lqp[kTrResMaxClusters], fb[kTrResMaxClusters];
+    uint32_t capc[kTrResMaxClusters], capm[kTrResMaxClusters];  // sums of capacities (mod 2^32)
     uint32_t T, done, ticks, flags;
     unsigned long long n_trades, n_won;
 };
+
+#ifdef MCS_STAMPS
+// the probe build's per-wave segment times (s_memrealtime, 100 MHz) summed over the launches since
+// the last read: [wave][segment], segments as RS_MARK below
+constexpr int kResSeg = 10;
+__device__ unsigned long long g_res_stamps[kResWaves * kResSeg];
+#define RS_MARK(i)                                  \
+    do {                                            \
+        const uint64_t rs_now = wall_clock64();     \
+        rs_acc[i] += rs_now - rs_last;              \
+        rs_last = rs_now;                           \
+    } while (0)
+#else
+#define RS_MARK(i) \
+    do {           \
+    } while (0)
+#endif
 
 template <int kResRows>  // slot rows per cluster (64 slots each)
 __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArgs a, uint32_t tick_budget) {
@@ -87,7 +105,8 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
         sh.n_trades = ctl.n_trades;
         sh.n_won = ctl.n_won;
     }
-    // this wave's clusters: slot finish times in registers (row r, lane l = slot r * 64 + l)
+    // this wave's clusters: slot finish times in registers (row r, lane l = slot r * 64 + l), and
+    // the sums of capacities the utilization sample subtracts the free vector from
     uint32_t fin[kResCpw][kResRows];
     uint32_t frm[kResCpw];  // free rows of this lane
 #pragma unroll
@@ -99,12 +118,62 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
             fin[k][r] = c < C ? a.sfin[(size_t)c * S + r * kWave + lane] : kEmpty;
             if (fin[k][r] == kEmpty) frm[k] |= 1u << r;
         }
+        if (c < C) {
+            const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
+            uint32_t uc = 0u, um = 0u;
+            for (uint32_t i = lane; i < N; i += kWave) {
+                const uint2 cp = a.cap[n0 + i];
+                uc += cp.x;
+                um += cp.y;
+            }
+            uc = rwave_sum(uc);
+            um = rwave_sum(um);
+            if (lane == 0) {
+                sh.capc[c] = uc;
+                sh.capm[c] = um;
+            }
+        }
     }
+#ifdef MCS_STAMPS
+    uint64_t rs_acc[kResSeg];
+#pragma unroll
+    for (int i = 0; i < kResSeg; ++i) rs_acc[i] = 0u;
+    uint64_t rs_last = wall_clock64();
+#endif
     __syncthreads();
 
     for (uint32_t it = 0; it < tick_budget; ++it) {
         if (sh.done) break;
         const uint32_t T = sh.T;
+        RS_MARK(9);
+
+        // the tick's job records, all loads in flight at once: lanes 16k..16k+15 hold, for the
+        // wave's cluster k, the 16 records from its WaitQueue head (else its ReadyQueue head) and
+        // the arrival times of the 16 jobs from its first unqueued one (a tick's decisions and
+        // arrivals stay within them but for bursts, which load the records they pass directly)
+        uint4 hwin = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t awin = kEmpty, hbase = 0u;
+        {
+            const uint32_t c = wave * kResCpw + (lane >> 4), d = lane & 15u;
+            if (c < C) {
+                const uint64_t j0 = a.job_off[c];
+                const uint32_t J = (uint32_t)(a.job_off[c + 1] - j0);
+                const TrCluster& s = sh.st[c];
+                const uint32_t hb = s.has_w ? s.w : s.rq_head;
+                const uint32_t na = s.next_arr;
+                hbase = hb;
+                if (hb + d < J) hwin = a.jobs[j0 + hb + d];
+                if (na + d < J) awin = a.jobs[j0 + na + d].x;
+            }
+        }
+        // GetResourceUtilization runs on the ticks a trader reads it (see tr_step_kernel)
+        bool sample = false;
+        if (a.trader && T % a.sample_period == 0u) {
+            bool due = false;
+            for (uint32_t q = lane; q < C; q += kWave) due = due || sh.trs[q].next_due <= T;
+            sample = __ballot(due) != 0ull;
+        }
+        RS_MARK(0);
 
         // ---- phase A: each wave's clusters, in turn (tr_step_kernel) ----
         // (one cluster's 16 slot rows are copied into a working set and back: the loop body is
@@ -118,6 +187,8 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
 #pragma unroll
             for (int r = 0; r < kResRows; ++r)
                 wf[r] = k == 0 ? fin[0][r] : k == 1 ? fin[1][r] : k == 2 ? fin[2][r] : fin[3][r];
+            const uint32_t wl = (uint32_t)k * 16u;  // the cluster's window lanes
+            const uint32_t hb = readlane(hbase, wl);
             unsigned long long* const nodes = nodes_all + (size_t)c * ns;
             const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
             const uint64_t j0 = a.job_off[c];
@@ -129,33 +200,72 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
 
             // releases due at T (cluster.go:153-157), before the tick's decisions
             if (st.minf <= T) {
+                // the expired slots' {node, payload} loads of up to 8 rows issued together, then
+                // their node updates
+                constexpr int kG = kResRows < 4 ? kResRows : 4;
                 uint32_t lm = kEmpty, nrel = 0;
 #pragma unroll
-                for (int r = 0; r < kResRows; ++r) {
-                    const uint32_t f = wf[r];
-                    if (f <= T) {
-                        const uint32_t slot = r * kWave + lane;
-                        const uint32_t nd = rld32(a.snode + sb + slot);
-                        if (nd < N) atomicAdd(&nodes[nd], rld64(a.scm + sb + slot));
-                        wf[r] = kEmpty;
-                        wfrm |= 1u << r;
-                        ++nrel;
-                    } else {
-                        lm = f < lm ? f : lm;
+                for (int g = 0; g < kResRows; g += kG) {
+                    uint32_t nd[kG];
+                    unsigned long long cm[kG];
+#pragma unroll
+                    for (int r = 0; r < kG; ++r) {
+                        nd[r] = kEmpty;
+                        cm[r] = 0ull;
+                        if (wf[g + r] <= T) {
+                            const uint32_t slot = (g + r) * kWave + lane;
+                            nd[r] = rld32(a.snode + sb + slot);
+                            cm[r] = rld64(a.scm + sb + slot);
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < kG; ++r) {
+                        const uint32_t f = wf[g + r];
+                        if (f <= T) {
+                            if (nd[r] < N) atomicAdd(&nodes[nd[r]], cm[r]);
+                            wf[g + r] = kEmpty;
+                            wfrm |= 1u << (g + r);
+                            ++nrel;
+                        } else {
+                            lm = f < lm ? f : lm;
+                        }
                     }
                 }
                 st.nrun -= rwave_sum(nrel);
                 st.minf = wave_min_u32(lm);
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
             }
-            // arrivals up to T join the ReadyQueue (jobs are sorted by arrival)
-            while (st.next_arr < J) {
-                const uint32_t i = st.next_arr + lane;
-                const bool ok = i < J && jobs[i].x <= T;
-                const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(ok));
-                st.next_arr += n;
-                if (n < (uint32_t)kWave) break;
+            RS_MARK(1);
+            // arrivals up to T join the ReadyQueue (jobs are sorted by arrival): the arrival
+            // window, then direct loads past a full window
+            uint32_t nat;  // the arrival second of the first job not yet queued (kEmpty: none)
+            {
+                const uint32_t na = st.next_arr;
+                const uint32_t n = (uint32_t)__builtin_popcountll(
+                    (__ballot(awin <= T && na + (lane & 15u) < J) >> wl) & 0xffffull);
+                st.next_arr = na + n;
+                if (n < 16u) {
+                    nat = readlane(awin, wl + n);
+                } else {
+                    while (st.next_arr < J) {
+                        const uint32_t i = st.next_arr + lane;
+                        const bool ok = i < J && jobs[i].x <= T;
+                        const uint32_t m = (uint32_t)__builtin_popcountll(__ballot(ok));
+                        st.next_arr += m;
+                        if (m < (uint32_t)kWave) break;
+                    }
+                    nat = st.next_arr < J ? jobs[st.next_arr].x : kEmpty;
+                }
             }
+            // record j: from the head window when it holds it
+            auto job_at = [&](uint32_t j) -> uint4 {
+                const uint32_t d = j - hb;
+                if (d < 16u) {
+                    const uint32_t l = wl + d;
+                    return make_uint4(readlane(hwin.x, l), readlane(hwin.y, l), readlane(hwin.z, l), readlane(hwin.w, l));
+                }
+                return jobs[j];
+            };
+            RS_MARK(2);
 
             // ScheduleJob (scheduler.go:127-139): lowest node with both >=; zero-capacity virtual
             // nodes (AddVirtualNode, cluster.go:79) follow the physical ones
@@ -189,7 +299,6 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                         if ((uint32_t)r == row) wf[r] = f;
                     wfrm &= ~(1u << row);
                 }
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // the node commit before the next fit
                 ++st.nrun;
                 st.peak = st.nrun > st.peak ? st.nrun : st.peak;
                 st.minf = f < st.minf ? f : st.minf;
@@ -211,7 +320,7 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
             TrRecA req{kEmpty, 0u, 0u, 0u};
             for (;;) {
                 if (st.has_w) {  // WaitQueue head (scheduler.go:219-251)
-                    const uint4 jb = jobs[st.w];
+                    const uint4 jb = job_at(st.w);
                     const uint32_t kn = first_fit(jb.z, jb.w);
                     if (kn != kEmpty) {
                         if (!place_own(st.w, kn, jb)) {
@@ -226,7 +335,7 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                 }
                 if (st.rq_head < st.next_arr) {  // ReadyQueue head (:255-272), no sleep
                     const uint32_t j = st.rq_head++;
-                    const uint4 jb = jobs[j];
+                    const uint4 jb = job_at(j);
                     const uint32_t kn = first_fit(jb.z, jb.w);
                     if (kn != kEmpty) {
                         if (!place_own(j, kn, jb)) {
@@ -277,23 +386,21 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                 break;  // idle sleep (:294)
             }
 
-            // GetResourceUtilization (cluster.go:46-63) on the ticks a trader reads it (see
-            // tr_step_kernel): an exact integer sum (the engine's eligibility check, above)
-            if (a.trader && T % a.sample_period == 0u) {
-                bool due = false;
-                for (uint32_t q = lane; q < C; q += kWave) due = due || sh.trs[q].next_due <= T;
-                if (__ballot(due)) {
-                    uint32_t uc = 0u, um = 0u;
-                    for (uint32_t i = lane; i < N; i += kWave) {
-                        const unsigned long long v = nodes[i];
-                        const uint2 cp = a.cap[n0 + i];
-                        uc += cp.x - (uint32_t)v;  // (mod 2^32: the signed sum, < 2^24 in size)
-                        um += cp.y - (uint32_t)(v >> 32);
-                    }
-                    const float sc = (float)(int32_t)rwave_sum(uc), sm = (float)(int32_t)rwave_sum(um);
-                    st.cu = __fdiv_rn(sc, (float)st.total_c);
-                    st.mu = __fdiv_rn(sm, (float)st.total_m);
+            RS_MARK(3);
+            // GetResourceUtilization (cluster.go:46-63) on the ticks a trader reads it: an exact
+            // integer sum (the engine's eligibility check, above), capacities minus free
+            if (sample) {
+                uint32_t fc = 0u, fm = 0u;
+                for (uint32_t i = lane; i < N; i += kWave) {
+                    const unsigned long long v = nodes[i];
+                    fc += (uint32_t)v;
+                    fm += (uint32_t)(v >> 32);
                 }
+                // (mod 2^32: the signed sum, < 2^24 in size)
+                const float sc = (float)(int32_t)(sh.capc[c] - rwave_sum(fc));
+                const float sm = (float)(int32_t)(sh.capm[c] - rwave_sum(fm));
+                st.cu = __fdiv_rn(sc, (float)st.total_c);
+                st.mu = __fdiv_rn(sm, (float)st.total_m);
             }
             if (lane == 0) {
                 TrXRec x;
@@ -304,7 +411,7 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                 x.rq_busy = st.rq_head < st.next_arr ? 1u : 0u;
                 x.decided = st.decided;
                 x.J = J;
-                x.next_arr_t = st.next_arr < J ? jobs[st.next_arr].x : kEmpty;
+                x.next_arr_t = nat;
                 x.flags = st.flags;
                 x.cu = st.cu;
                 x.mu = st.mu;
@@ -323,11 +430,13 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
             frm[1] = k == 1 ? wfrm : frm[1];
             frm[2] = k == 2 ? wfrm : frm[2];
             frm[3] = k == 3 ? wfrm : frm[3];
+            RS_MARK(4);
         }
         __syncthreads();
+        RS_MARK(5);
 
         // ---- phase B: each wave's clusters as lenders, requests in borrower order (tr_lend_kernel) ----
-#pragma unroll
+#pragma unroll 1
         for (int k = 0; k < kResCpw; ++k) {
             const uint32_t L = wave * kResCpw + k;
             if (L >= C) break;
@@ -382,7 +491,9 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                 sh.st[L].flags |= fb;
             }
         }
+        RS_MARK(6);
         __syncthreads();
+        RS_MARK(7);
 
         // ---- phases C and D: wave 0 (tr_trader_kernel) ----
         if (wave == 0) {
@@ -508,8 +619,13 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                 sh.n_won = n_won;
             }
         }
+        RS_MARK(8);
         __syncthreads();
     }
+#ifdef MCS_STAMPS
+    if (lane == 0)
+        for (int i = 0; i < kResSeg; ++i) atomicAdd(&g_res_stamps[wave * kResSeg + i], (unsigned long long)rs_acc[i]);
+#endif
 
     // ---- state out (the next launch, the stats and the readers take it from HBM) ----
     for (uint32_t c = 0; c < C; ++c) {
@@ -572,3 +688,12 @@ hipError_t launch_trade_resident(const TradeArgs& a, uint32_t tick_budget, size_
 }
 
 }  // namespace mcs
+
+#ifdef MCS_STAMPS
+// the probe build's per-wave segment times (16 waves x 10 segments, 100 MHz ticks); read and reset
+extern "C" int mcs_debug_res_stamps(unsigned long long* out) {
+    unsigned long long z[mcs::kResWaves * mcs::kResSeg] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_res_stamps), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_res_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

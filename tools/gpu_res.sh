@@ -27,8 +27,14 @@ print("mismatches", bad, "flags", out["1"][1]["flags"], out["0"][1]["flags"])
 PY
 rc=$?; cat "$OUT/quick.log"; echo "quick rc=$rc"; [ $rc -ne 0 ] && exit $rc
 grep -q "mismatches \[0, 0, 0\]" "$OUT/quick.log" || exit 3
+if [ -f variants/libmcs_res_stamps.so ]; then
+    timeout -k 10 300 python -u tools/stamp_res.py variants/libmcs_res_stamps.so ${STAMP_JOBS:-20000} > "$OUT/stamps.json" 2>&1
+    rc=$?; cat "$OUT/stamps.json"; echo "stamps rc=$rc"; [ $rc -ne 0 ] && exit $rc
+fi
+[ -n "${SKIP_PYTEST:-}" ] || {
 timeout -k 10 900 python -u -m pytest tests/test_gpu_trade.py -x -v --timeout 600 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_trade.log" 2>&1
 rc=$?; tail -25 "$OUT/pytest_trade.log"; echo "pytest rc=$rc"; [ $rc -ne 0 ] && exit $rc
+}
 i=0
 while IFS= read -r line; do
     [ -z "$line" ] && continue
@@ -41,7 +47,7 @@ print('  %.4g' % d['value'], d['unit'], 'us/tick %.2f' % t['us_per_tick'], 'loop
     [ $rc -ne 0 ] && exit $rc
 done <<LIST
 ${BENCHES:-MCS_TRADE_RESIDENT=1|--config c5 --steps 1 --warmup 1 --no-cpu-baseline
-MCS_TRADE_RESIDENT=1|--config c5 --steps 1 --warmup 1 --no-cpu-baseline --slot-pool 8
+MCS_TRADE_RESIDENT=1|--config c5 --steps 1 --warmup 1 --no-cpu-baseline --slot-pool 16
 MCS_TRADE_RESIDENT=0|--config c5 --steps 1 --warmup 1 --no-cpu-baseline}
 LIST
 echo done
