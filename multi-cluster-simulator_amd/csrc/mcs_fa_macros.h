@@ -37,6 +37,19 @@
         "v121", "v122", "v123", "v124", "v125", "v126", "v127", "vcc", "scc", "m0", "exec", "memory"     \
         MCS_FA_STAMP_CLOBBERS
 
+// the fused loop's clobbers: MCS_FA_CLOBBERS less the state it keeps in register-bound operands
+// (MCS_FA_LOOP_F: s40 s43 s44 s47 s57 s59 s77 s78 s80-s84, v32-v55, v64-v67, v89-v93, v98-v101)
+#define MCS_FF_CLOBBERS \
+    "s41", "s42", "s45", "s46", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", \
+        "s58", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", \
+        "s71", "s72", "s73", "s74", "s75", "s76", "s79", "s85", "s86", "s87", "s88", "s89", \
+        "s90", "s91", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", \
+        "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v94", "v95", \
+        "v96", "v97", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", \
+        "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", \
+        "vcc", "scc", "m0", "exec", "memory" \
+        MCS_FA_STAMP_CLOBBERS
+
 // ---- W-specific pieces ----------------------------------------------------------------------
 // the insert's candidate lanes: the lanes with a free slot row (computed early, off the chain)
 #define MCS_FA_FREELANES "v_cmp_ne_u32_e64 s[60:61], 0, v89\n\t"

@@ -40,6 +40,7 @@
 // after its write (s_nop 1), v_readlane reads a VGPR at least 1 instruction after its write, m0
 // is read by v_writelane at least 1 state after an SALU write.  Loads and stores issued here are
 // waited for before the statement ends.  The loop runs with the full wave in exec.
+#include "mcs_gen_dev.h"
 #include "mcs_internal.h"
 #include "mcs_lds.h"
 #include "mcs_wave.h"
@@ -55,7 +56,7 @@ __device__ unsigned long long g_fa_stamps[4];
 #include "mcs_fa_macros.h"
 
 // ---- the decision loop ------------------------------------------------------------------------
-#define MCS_FA_LOOP(W, D)                                                                         \
+#define MCS_FA_ENTRY_S(W)                                                                         \
     /* ---- entry: state into the fixed registers ---- */                                        \
     "s_mov_b32 s40, %[t]\n\t"                                                                     \
     "s_mov_b32 s42, %[J]\n\t"                                                                     \
@@ -94,8 +95,9 @@ __device__ unsigned long long g_fa_stamps[4];
     "global_load_dwordx4 v[98:101], v121, s[64:65]\n\t"                                           \
     "s_min_u32 s41, s42, 64\n\t" MCS_FA_REC##W                                                    \
     "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
-    "s_cbranch_scc0 mcsfa_bend_%=\n"                                                              \
-                                                                                                  \
+    "s_cbranch_scc0 mcsfa_bend_%=\n"
+
+#define MCS_FA_BODY(W, D, F)                                                                      \
     /* ---- one pass = one decision (scheduler.go:216-296) ---- */                               \
     "mcsfa_inner_%=:\n\t"                                                                         \
     "s_cmp_gt_u32 s45, s40\n\t" /* ready head not arrived: sleep to it */                         \
@@ -216,7 +218,11 @@ __device__ unsigned long long g_fa_stamps[4];
     "global_store_dword v125, v92, s[68:69] nt\n\t"                                               \
     "v_add_u32 v93, v92, v95\n\t" /* finish = start + the batch's duration column */            \
     "global_store_dword v125, v93, s[70:71] nt\n\t"                                               \
-    "s_add_u32 s57, s57, 64\n\t" MCS_FA_TAKE##W                                                   \
+    "s_add_u32 s57, s57, 64\n\t" MCS_FA_BENDTAIL_##F(W)
+
+// streamed records: the prefetched batch becomes current, the next one is prefetched
+#define MCS_FA_BENDTAIL_S(W)                                                                      \
+    MCS_FA_TAKE##W                                                                                \
     "v_add_u32 v121, s57, v110\n\t"                                                               \
     "v_lshlrev_b32 v121, 4, v121\n\t"                                                             \
     "v_add_u32 v121, 0x400, v121\n\t"                                                             \
@@ -224,8 +230,14 @@ __device__ unsigned long long g_fa_stamps[4];
     "s_sub_u32 s41, s42, s57\n\t"                                                                 \
     "s_min_u32 s41, s41, 64\n\t"                                                                  \
     "s_mov_b32 s47, 0\n\t" MCS_FA_REC##W MCS_FA_T1("s96")                                         \
-    "s_branch mcsfa_inner_%=\n"                                                                   \
-                                                                                                  \
+    "s_branch mcsfa_inner_%=\n"
+// fused records: the statement ends with s59 = 1 and the kernel synthesises the next batch
+#define MCS_FA_BENDTAIL_F(W)                                                                      \
+    "s_mov_b32 s47, 0\n\t"                                                                        \
+    "s_mov_b32 s59, 1\n\t" MCS_FA_T1("s96")                                                      \
+    "s_branch mcsfa_exit_%=\n"
+
+#define MCS_FA_EXIT_S                                                                             \
     /* ---- exit: state back to the compiler's registers ---- */                                 \
     "mcsfa_exit_%=:\n\t"                                                                          \
     "s_waitcnt vmcnt(0) lgkmcnt(0)\n\t" MCS_FA_TEND                                               \
@@ -251,6 +263,56 @@ __device__ unsigned long long g_fa_stamps[4];
     "v_mov_b32 %[frm], v89\n\t"                                                                   \
     "v_mov_b32 %[lmin], v90\n\t"                                                                  \
     "s_nop 1"
+
+#define MCS_FA_LOOP(W, D) MCS_FA_ENTRY_S(W) MCS_FA_BODY(W, D, S) MCS_FA_EXIT_S
+
+// ---- the loop with the job stream synthesised in the kernel (mcs_gen_params.fused) ---------------
+// The statement runs one batch of records and ends at its batch end with s59 = 1 (or at the end of
+// the cluster with s59 = 0); the kernel then generates the next batch (GenStream, mcs_gen_dev.h)
+// into v[98:101] and enters again.  The loop state stays in its fixed registers between the
+// statements: they are the statement's register-bound operands ({s40}, {v[32:39]}, ...), so the
+// compiler keeps them there (or moves them back) across the generator's code.  Every entry sets the
+// constants again; the first (s59 = 0) also loads the nodes and takes batch 0 from the operands.
+#define MCS_FA_ENTRY_F(W)                                                                         \
+    "s_mov_b32 s42, %[J]\n\t"                                                                     \
+    "s_lshl2_add_u32 s79, s42, 0x100\n\t"                                                         \
+    "s_mov_b64 s[66:67], %[onp]\n\t"                                                              \
+    "s_mov_b64 s[68:69], %[osp]\n\t"                                                              \
+    "s_mov_b64 s[70:71], %[ofp]\n\t"                                                              \
+    "s_mov_b32 s72, %[sel0]\n\t"                                                                  \
+    "s_mov_b32 s73, %[sel1]\n\t"                                                                  \
+    "s_mov_b32 s49, 0x100\n\t"                                                                    \
+    "v_mov_b32 v107, %[pay]\n\t"                                                                  \
+    "v_mov_b32 v108, %[nb]\n\t"                                                                   \
+    "v_mov_b32 v109, %[nbase]\n\t"                                                                \
+    "v_mov_b32 v110, %[lane]\n\t"                                                                 \
+    "v_mov_b32 v111, -1\n\t"                                                                      \
+    "s_cmp_eq_u32 s59, 0\n\t"                                                                     \
+    "s_mov_b32 s59, 0\n\t" /* (no SCC write) */                                                  \
+    "s_cbranch_scc0 mcsfa_resume_%=\n\t" MCS_FA_INIT##W MCS_FA_RELOAD##W                         \
+    "v_mov_b32 v94, %[c0]\n\t"                                                                    \
+    "v_mov_b32 v95, %[c1]\n\t"                                                                    \
+    "v_mov_b32 v96, %[c2]\n\t"                                                                    \
+    "v_mov_b32 v97, %[c3]\n\t"                                                                    \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
+    "s_min_u32 s41, s42, 64\n\t"                                                                  \
+    "s_branch mcsfa_start_%=\n"                                                                   \
+    "mcsfa_resume_%=:\n\t" MCS_FA_TAKE##W                                                        \
+    "s_sub_u32 s41, s42, s57\n\t"                                                                 \
+    "s_min_u32 s41, s41, 64\n\t"                                                                  \
+    "s_mov_b32 s47, 0\n"                                                                          \
+    "mcsfa_start_%=:\n\t" MCS_FA_REC##W                                                          \
+    "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
+    "s_cbranch_scc0 mcsfa_bend_%=\n"
+#define MCS_FA_EXIT_F                                                                             \
+    "mcsfa_exit_%=:\n\t"                                                                          \
+    "s_waitcnt vmcnt(0) lgkmcnt(0)\n\t"                                                           \
+    "s_cmp_eq_u32 s47, 0\n\t" /* (as MCS_FA_EXIT_S) */                                           \
+    "s_cbranch_scc1 mcsfa_xf_%=\n\t"                                                              \
+    "v_add_u32 v93, v92, v95\n"                                                                   \
+    "mcsfa_xf_%=:\n\t"                                                                            \
+    "s_nop 1"
+#define MCS_FA_LOOP_F(W, D) MCS_FA_ENTRY_F(W) MCS_FA_BODY(W, D, F) MCS_FA_EXIT_F
 
 // Node format W (32 or 16 bits per field); LDS: nodes [4][64] (u64 / u32 words) at 0, slot
 // payloads [8][64] (u64 / u32 in a u64 stride) at 2048, slot {node address | finish << 32}
@@ -403,11 +465,143 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
     }
 }
 
+typedef uint32_t mcs_u32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t mcs_u32x4 __attribute__((ext_vector_type(4)));
+
+// The W16R / W16S loop on a fused job stream (MCS_FA_LOOP_F): the same decisions as
+// fifo_asm_kernel, batch after batch from GenStream instead of HBM records.
+template <int NPL, int P, bool DIAG>
+__global__ __launch_bounds__(64) void fifo_asm_fused_kernel(FifoArgs a) {
+    static_assert((NPL == 4 && P == 8) || (NPL == 1 && P == 2), "loop shapes");
+    const uint32_t item = blockIdx.x;
+    const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
+    const uint32_t lane = threadIdx.x;
+
+    __shared__ uint64_t lds[NPL * kWave + 2 * P * kWave];
+    constexpr uint32_t kGuard = 0x8000u, kClamp = kGuard - 1u;
+    const uint32_t n0 = a.node_off[ci];
+    const uint32_t N = a.node_off[ci + 1] - n0;
+#pragma unroll
+    for (int c = 0; c < NPL; ++c) {
+        const uint32_t node = lane * NPL + c;
+        uint2 v = make_uint2(kClamp, kClamp);  // padding: never fits
+        if (node < N) {
+            v = a.node_free0[n0 + node];
+            v.x += kGuard;
+            v.y += kGuard;
+        }
+        reinterpret_cast<uint32_t*>(lds)[c * kWave + lane] = v.x | (v.y << 16);
+    }
+
+    const uint64_t j0 = a.job_off[ci];
+    const uint32_t J = (uint32_t)(a.job_off[ci + 1] - j0);
+    int32_t* o_node = a.out_node + j0;
+    uint32_t* o_start = a.out_start + j0;
+    uint32_t* o_finish = a.out_finish + j0;
+
+    GenStream gs;
+    gs.init(a.gen, ci, lane);
+    uint4 cur = gs.next(0u, lane);  // batch 0
+    cur.z = cur.z < kClamp ? cur.z : kClamp;
+    cur.w = cur.w < kClamp ? cur.w : kClamp;
+    cur.z |= cur.w << 16;
+    __syncthreads();
+
+    const uint32_t base = lds_addr(lds);
+    const uint32_t v_pay = base + 2048u + lane * 8u;
+    const uint32_t v_nb = base + lane * 4u;
+    const uint32_t v_nbase = base;
+    const uint32_t sel0 = NPL == 1 ? 0x7fffu : 0x0b0a0908u;
+    const uint32_t sel1 = base;
+
+    // the loop state, bound to its registers (MCS_FA_LOOP_F)
+    uint32_t t = 0, have_w = 0, flags = 0, cursor = 0, cb = 0, need = 0, emin = kEmpty, fails = 0;
+    uint32_t used = 0, peak = 0, waited = 0, n_slow = 0, n_rel = 0;
+    uint32_t frm = (1u << P) - 1u + 0x100u, lmin = kEmpty, on = 0, os = 0, of = 0;
+    mcs_u32x8 sf = kEmpty, sp = 0u, sa = 0u;  // slot rows: finish, payload, node address
+    mcs_u32x4 nd = 0u;                        // node registers
+    mcs_u32x4 nx = 0u;                        // the next batch's records
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+#define MCS_FF_OPERANDS                                                                           \
+    : [t] "+{s40}"(t), [hw] "+{s43}"(have_w), [flags] "+{s44}"(flags), [cur] "+{s47}"(cursor),   \
+      [cb] "+{s57}"(cb), [need] "+{s59}"(need), [emin] "+{s77}"(emin), [fails] "+{s78}"(fails),  \
+      [used] "+{s80}"(used), [peak] "+{s81}"(peak), [waited] "+{s82}"(waited),                   \
+      [nslow] "+{s83}"(n_slow), [nrel] "+{s84}"(n_rel), [sf] "+{v[32:39]}"(sf),                   \
+      [sp] "+{v[40:47]}"(sp), [sa] "+{v[48:55]}"(sa), [nd] "+{v[64:67]}"(nd), [frm] "+{v89}"(frm), \
+      [lmin] "+{v90}"(lmin), [on] "+{v91}"(on), [os] "+{v92}"(os), [of] "+{v93}"(of)             \
+    : [nx] "{v[98:101]}"(nx), [J] "s"(J), [onp] "s"(o_node), [osp] "s"(o_start),                \
+      [ofp] "s"(o_finish), [c0] "v"(cur.x), [c1] "v"(cur.y), [c2] "v"(cur.z), [c3] "v"(cur.w),   \
+      [pay] "v"(v_pay), [nb] "v"(v_nb), [nbase] "v"(v_nbase), [lane] "v"(lane),                  \
+      [sel0] "s"(sel0), [sel1] "s"(sel1), [fdl] "i"(MCS_FLAG_DEADLOCK),                         \
+      [fck] "i"(MCS_FLAG_CLOCK_OVERFLOW), [fov] "i"(MCS_FLAG_OVERFLOW)                           \
+    : MCS_FF_CLOBBERS
+    for (;;) {
+        if constexpr (NPL == 1)
+            if constexpr (DIAG) asm volatile(MCS_FA_LOOP_F(16S, D1) MCS_FF_OPERANDS);
+            else asm volatile(MCS_FA_LOOP_F(16S, D0) MCS_FF_OPERANDS);
+        else
+            if constexpr (DIAG) asm volatile(MCS_FA_LOOP_F(16R, D1) MCS_FF_OPERANDS);
+            else asm volatile(MCS_FA_LOOP_F(16R, D0) MCS_FF_OPERANDS);
+        if (!need) break;
+        const uint4 b = gs.next(cb, lane);  // the next batch (bases increase)
+        nx = mcs_u32x4{b.x, b.y, b.z, b.w};
+    }
+#undef MCS_FF_OPERANDS
+#pragma clang diagnostic pop
+
+    const uint32_t r = cb + cursor;
+    peak = peak > used ? peak : used;
+    if (peak > (uint32_t)(P * kWave)) flags |= MCS_FLAG_OVERFLOW;  // a skipped insert
+    const uint32_t placed = r;
+    if (!(flags & MCS_FLAG_OVERFLOW)) {
+        if (r > 0u) {  // the batch holding the last decision (earlier ones are stored)
+            const uint32_t i = ((r - 1u) & ~63u) + lane;
+            if (i < r) {
+                o_node[i] = (int32_t)(NPL == 1 ? on : (on & 63u) * NPL + (on >> 6));
+                o_start[i] = os;
+                o_finish[i] = of;
+            }
+        }
+        if (flags & (MCS_FLAG_DEADLOCK | MCS_FLAG_CLOCK_OVERFLOW)) {
+            for (uint32_t i = r + lane; i < J; i += kWave) {
+                o_node[i] = MCS_NODE_UNPLACED;
+                o_start[i] = MCS_TIME_NONE;
+                o_finish[i] = MCS_TIME_NONE;
+            }
+        }
+    }
+
+    if (lane == 0) {
+        mcs_cluster_stats st;
+        st.t_end = t;
+        st.placed = placed;
+        st.waited = waited;
+        st.peak_running = peak;
+        st.flags = flags;
+        st.pool = (uint32_t)P;
+        st.iterations = n_slow + r;
+        st.release_scans = n_rel;
+        a.cstats[ci] = st;
+        if (flags & MCS_FLAG_OVERFLOW) {
+            atomicAdd(&a.totals->overflowed, 1u);
+        } else {
+            atomicAdd(&a.totals->placed, (unsigned long long)placed);
+            atomicAdd(&a.totals->waited, (unsigned long long)waited);
+            atomicAdd(&a.totals->unplaced, (unsigned long long)(J - placed));
+            if (flags & MCS_FLAG_DEADLOCK) atomicAdd(&a.totals->deadlocked, 1u);
+            if (flags & MCS_FLAG_CLOCK_OVERFLOW) atomicAdd(&a.totals->clock_overflowed, 1u);
+        }
+    }
+}
+
 }  // namespace
 
 // Form codes: 17 = W16R and 18 = W16S (where the 16-bit format fits), 16 = W16 with LDS slots,
-// 32 = W32, 0 = the compiled kernel.  MCS_FIFO_ASM=0 turns the hand-scheduled loop off, =16 / =32
-// force a form (A/B timing, the variant tests; neither has a small-cluster shape).
+// 32 = W32, 19 / 20 = W16R / W16S on a fused job stream, 0 = the compiled kernel.  MCS_FIFO_ASM=0
+// turns the hand-scheduled loop off, =16 / =32 force a form (A/B timing, the variant tests; neither
+// has a small-cluster shape nor a fused one).
 int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor) {
     const char* env = getenv("MCS_FIFO_ASM");
     const int want = env ? atoi(env) : 1;
@@ -415,7 +609,12 @@ int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor) {
     // rows (C1-C3); other shapes and pools keep the compiled kernel
     // (records and results are addressed by 32-bit offsets from the cluster's base: at most
     // kAsmMaxJobs jobs per cluster, guard_ok bit 2)
-    if (want == 0 || hor || a.gen.on || !(a.guard_ok & 4u)) return 0;
+    if (want == 0 || hor || !(a.guard_ok & 4u)) return 0;
+    // a fused job stream: the W16 register-slot shapes with GenStream at the batch ends
+    if (a.gen.on) {
+        if (want == 16 || want == 32 || !(a.guard_ok & 2u)) return 0;
+        return npl == 1 && pool == 2 ? 20 : npl == 4 && pool == 8 ? 19 : 0;
+    }
     if (npl == 1 && pool == 2) return (a.guard_ok & 2u) && want != 16 && want != 32 ? 18 : 0;
     if (npl != 4 || pool != 8) return 0;
     // register slots: one LDS round trip per release instead of 2 + rows; measured faster than LDS
@@ -431,6 +630,8 @@ bool fifo_asm_eligible(const FifoArgs& a, int npl, int pool, bool hor) {
 template <bool DIAG>
 static hipError_t launch_form(const FifoArgs& a, int form, hipStream_t s) {
     switch (form) {
+        case 20: hipLaunchKernelGGL((fifo_asm_fused_kernel<1, 2, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
+        case 19: hipLaunchKernelGGL((fifo_asm_fused_kernel<4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 18: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 1, 2, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 17: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 16: hipLaunchKernelGGL((fifo_asm_kernel<16, false, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;

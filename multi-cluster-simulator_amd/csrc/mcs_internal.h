@@ -144,7 +144,7 @@ bool fifo_variant_exists(int npl, int pool);
 // the hand-scheduled decision loop (mcs_fifo_asm.hip): NPL 4 / P 8 or NPL 1 / P 2, streamed
 // batch runs; MCS_FIFO_ASM=0 turns it off
 bool fifo_asm_eligible(const FifoArgs& a, int npl, int pool, bool hor);
-int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor);  // 18, 17, 16, 32 or 0
+int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor);  // 20, 19, 18, 17, 16, 32 or 0
 hipError_t launch_fifo_asm(const FifoArgs& a, int npl, int pool, hipStream_t s);
 hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t* max_c,
                             const uint32_t* max_m, uint32_t n_clusters, uint64_t seed,

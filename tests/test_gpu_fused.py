@@ -203,3 +203,46 @@ def test_fused_clock_bound_is_exact(serial, mode, lam, jobs, monkeypatch):
         gp.max_dur_s = md + 1
         with pytest.raises(L.MCSError):
             eng.generate_jobs(gp, jobs)
+
+
+@pytest.mark.parametrize("diag", ["0", "1"])
+@pytest.mark.parametrize("nodes,kernel", [(256, "mcs::fifo_asm_fused_kernel<4, 8>"),
+                                          (48, "mcs::fifo_asm_fused_kernel<1, 2>")], ids=["w16r", "w16s"])
+@pytest.mark.parametrize("mode", [L.MCS_ARRIVAL_REF, L.MCS_ARRIVAL_SCALED, L.MCS_ARRIVAL_WEIBULL],
+                         ids=["REF", "SCALED", "WEIBULL"])
+def test_fused_hand_scheduled_loop(mode, nodes, kernel, diag, monkeypatch):
+    """The hand-scheduled FIFO loop on a fused stream (MCS_FA_LOOP_F: GenStream between batches,
+    the loop state held in its registers across them) equals the streamed hand-scheduled loop, the
+    compiled fused kernel, and the oracle over the host generator's streams: placements, per-cluster
+    statistics (with the counting build, its pass and release-scan counts too)."""
+    monkeypatch.setenv("MCS_FIFO_DIAG", diag)
+    arrays = replicate(uniform_cluster(nodes), 24)
+    lam = {L.MCS_ARRIVAL_REF: 40.0, L.MCS_ARRIVAL_SCALED: scaled_lambda(nodes, load=0.95),
+           L.MCS_ARRIVAL_WEIBULL: 10.0}[mode]
+    gp = GenParams(seed=0xF05ED + nodes + mode, arrival_mode=mode, lam=lam)
+    jobs = 3001  # a ragged last batch
+
+    def go(fused, asm):
+        monkeypatch.setenv("MCS_FIFO_ASM", asm)
+        gp.fused = fused
+        with Engine(0, policy="FIFO") as eng:
+            eng.load_clusters(arrays)
+            eng.generate_jobs(gp, jobs)
+            eng.run()
+            return eng.placements(), eng.cluster_stats(), eng.last_kernel
+
+    fz, fcs, fk = go(True, "1")
+    assert fk == kernel
+    keys = ["t_end", "placed", "waited", "peak_running", "flags"] + (["iterations", "release_scans"] if diag == "1" else [])
+    for fused, asm in ((False, "1"), (True, "0")):
+        (pl, cs, k) = go(fused, asm)
+        assert k != kernel
+        for a, b, name in zip(pl, fz, ("node", "start", "finish")):
+            np.testing.assert_array_equal(a, b, err_msg=f"{name} vs {k}")
+        for key in keys if not (fused and asm == "0") else keys[:5]:
+            np.testing.assert_array_equal(cs[key], fcs[key], err_msg=f"{key} vs {k}")
+    gp.fused = False
+    on, os_, of, _ = O.fifo_run_batch(arrays, gen_streams_host(gp, arrays, jobs), n_threads=8)
+    np.testing.assert_array_equal(fz[0], on)
+    np.testing.assert_array_equal(fz[1], os_)
+    np.testing.assert_array_equal(fz[2], of)
