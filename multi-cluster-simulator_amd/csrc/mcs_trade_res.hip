@@ -57,6 +57,7 @@ struct ResShared {  // (the node vectors follow, Ct * ns u64)
     TrRecC rcs[kTrResMaxClusters];
     uint32_t acc[kTrResMaxClusters], lqp[kTrResMaxClusters], fb[kTrResMaxClusters];
     uint32_t capc[kTrResMaxClusters], capm[kTrResMaxClusters];  // sums of capacities (mod 2^32)
+    uint32_t gtab[kResWaves][64];  // phase B: a lender's G table, one per wave
     uint32_t T, done, ticks, flags;
     unsigned long long n_trades, n_won;
 };
@@ -269,17 +270,22 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
 
             // ScheduleJob (scheduler.go:127-139): lowest node with both >=; zero-capacity virtual
             // nodes (AddVirtualNode, cluster.go:79) follow the physical ones
+            // (every node read issued before the first compare: one LDS round trip for <= 256 nodes)
             auto first_fit = [&](uint32_t jc, uint32_t jm) -> uint32_t {
-                uint32_t best = kEmpty;
-                for (uint32_t b = 0; b < N; b += kWave) {
-                    const uint32_t i = b + lane;
-                    if (i < N) {
-                        const unsigned long long v = nodes[i];
-                        if ((uint32_t)v >= jc && (uint32_t)(v >> 32) >= jm) best = i;
-                    }
-                    if (__ballot(best != kEmpty)) break;
+                unsigned long long v[kResMaxNodes / kWave];
+#pragma unroll
+                for (uint32_t q = 0; q < kResMaxNodes / kWave; ++q) {
+                    const uint32_t i = q * kWave + lane;
+                    v[q] = i < N ? nodes[i] : 0ull;
                 }
-                uint32_t kk = wave_min_u32(best);
+                uint32_t kk = kEmpty;
+#pragma unroll
+                for (uint32_t q = 0; q < kResMaxNodes / kWave; ++q) {
+                    const uint32_t i = q * kWave + lane;
+                    const unsigned long long m =
+                        __ballot(i < N && (uint32_t)v[q] >= jc && (uint32_t)(v[q] >> 32) >= jm);
+                    if (m && kk == kEmpty) kk = q * kWave + (uint32_t)__builtin_ctzll(m);
+                }
                 if (kk == kEmpty && jc == 0u && jm == 0u && vn > 0u) kk = N;
                 return kk;
             };
@@ -436,59 +442,89 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
         RS_MARK(5);
 
         // ---- phase B: each wave's clusters as lenders, requests in borrower order (tr_lend_kernel) ----
+        // Lend (scheduler.go:194-202) accepts a request (c, m) when some node has free_c > c and
+        // free_m > m.  With every free_c of the lender at most 64 that is G[c] > m for
+        // G[x] = max free_m over the nodes with free_c > x (0 when none): the lender builds G in a
+        // 64-entry LDS table (an atomic max per node into A[free_c - 1], then a suffix maximum),
+        // and every request of the tick is tested at once, one borrower per lane (C <= 64); the
+        // accepted ones join its LentQueue in borrower order by their rank among them.  A lender
+        // with a larger free_c scans its nodes per request instead.
+        {
+            TrRecA rq{kEmpty, 0u, 0u, 0u};
+            if (lane < C) rq = sh.x[lane].req;
+            uint32_t* const tab = sh.gtab[wave];
 #pragma unroll 1
-        for (int k = 0; k < kResCpw; ++k) {
-            const uint32_t L = wave * kResCpw + k;
-            if (L >= C) break;
-            const unsigned long long* const nodes = nodes_all + (size_t)L * ns;
-            const uint32_t N = sh.x[L].n;
-            uint32_t lq_len = sh.x[L].lq_len, fb = 0;
-            const uint32_t lq_head = sh.st[L].lq_head;
-            const uint32_t LQ = a.LQ;
-            for (uint32_t b0 = 0; b0 < C; b0 += kWave) {
-                const uint32_t bl = b0 + lane;
-                TrRecA rl{kEmpty, 0u, 0u, 0u};
-                if (bl < C && bl != L) rl = sh.x[bl].req;  // self skipped (:176)
-                unsigned long long pend = __ballot(rl.job != kEmpty);
-                while (pend) {
-                    const uint32_t bi = (uint32_t)__builtin_ctzll(pend);
-                    const uint32_t b = b0 + bi;
-                    pend &= pend - 1ull;
-                    const TrRecA r{readlane(rl.job, bi), readlane(rl.c, bi), readlane(rl.m, bi), readlane(rl.dur, bi)};
-                    bool ok = false;
-                    for (uint32_t i0 = 0; i0 < N; i0 += kWave) {
-                        const uint32_t i = i0 + lane;
-                        if (i < N) {
-                            const unsigned long long v = nodes[i];
-                            ok = ok || ((uint32_t)v > r.c && (uint32_t)(v >> 32) > r.m);
+            for (int k = 0; k < kResCpw; ++k) {
+                const uint32_t L = wave * kResCpw + k;
+                if (L >= C) break;
+                const unsigned long long* const nodes = nodes_all + (size_t)L * ns;
+                const uint32_t N = sh.x[L].n;
+                uint32_t lq_len = sh.x[L].lq_len, fb = 0;
+                const uint32_t lq_head = sh.st[L].lq_head;
+                const uint32_t LQ = a.LQ;
+                const bool want = rq.job != kEmpty && lane != L;  // self skipped (:176)
+                unsigned long long okm = 0ull;
+                if (__ballot(want)) {
+                    tab[lane] = 0u;
+                    bool big = false;
+                    for (uint32_t i = lane; i < N; i += kWave) {
+                        const unsigned long long v = nodes[i];
+                        const uint32_t fc = (uint32_t)v;
+                        if (fc > 64u)
+                            big = true;
+                        else if (fc > 0u)
+                            atomicMax(&tab[fc - 1u], (uint32_t)(v >> 32));
+                    }
+                    if (!__ballot(big)) {
+                        const uint32_t g = wave_scan_max_u32(tab[63u - lane]);  // G[63 - lane]
+                        tab[63u - lane] = g;
+                        okm = __ballot(want && rq.c < 64u && tab[rq.c < 64u ? rq.c : 0u] > rq.m);
+                    } else {
+                        unsigned long long pend = __ballot(want);
+                        while (pend) {
+                            const uint32_t bi = (uint32_t)__builtin_ctzll(pend);
+                            pend &= pend - 1ull;
+                            const uint32_t rc = readlane(rq.c, bi), rm = readlane(rq.m, bi);
+                            bool ok = false;
+                            for (uint32_t i0 = 0; i0 < N; i0 += kWave) {
+                                const uint32_t i = i0 + lane;
+                                if (i < N) {
+                                    const unsigned long long v = nodes[i];
+                                    ok = ok || ((uint32_t)v > rc && (uint32_t)(v >> 32) > rm);
+                                }
+                                if (__ballot(ok)) break;
+                            }
+                            if (__ballot(ok)) okm |= 1ull << bi;
                         }
-                        if (__ballot(ok)) break;
                     }
-                    if (!__ballot(ok)) continue;  // "can't lend" (scheduler.go:201)
-                    if (lq_len >= LQ) {
-                        fb |= MCS_FLAG_LENT_OVERFLOW;
-                        continue;
-                    }
-                    if (lane == 0) {
-                        uint32_t at = lq_head + lq_len;
-                        at = at >= LQ ? at - LQ : at;
-                        TrLq e{};
-                        e.borrower = b;
-                        e.job = r.job;
-                        e.c = r.c;
-                        e.m = r.m;
-                        e.dur = r.dur;
-                        a.lq[(size_t)L * LQ + at] = e;
-                        sh.acc[b] = 1u;  // (every accepting lender writes the same value)
-                    }
-                    ++lq_len;
                 }
-            }
-            if (lane == 0) {
-                sh.lqp[L] = lq_len;
-                sh.fb[L] = fb;
-                sh.st[L].lq_len = lq_len;
-                sh.st[L].flags |= fb;
+                // appends (server.go:80-113): the first LQ - lq_len accepted, in borrower order
+                const uint32_t rank = (uint32_t)__builtin_popcountll(okm & ((1ull << lane) - 1ull));
+                if (((okm >> lane) & 1ull) && lq_len + rank < LQ) {
+                    uint32_t at = lq_head + lq_len + rank;
+                    at = at >= LQ ? at - LQ : at;
+                    TrLq e{};
+                    e.borrower = lane;
+                    e.job = rq.job;
+                    e.c = rq.c;
+                    e.m = rq.m;
+                    e.dur = rq.dur;
+                    a.lq[(size_t)L * LQ + at] = e;
+                    sh.acc[lane] = 1u;  // (every accepting lender writes the same value)
+                }
+                const uint32_t nacc = (uint32_t)__builtin_popcountll(okm);
+                if (lq_len + nacc > LQ) {
+                    fb |= MCS_FLAG_LENT_OVERFLOW;
+                    lq_len = LQ;
+                } else {
+                    lq_len += nacc;
+                }
+                if (lane == 0) {
+                    sh.lqp[L] = lq_len;
+                    sh.fb[L] = fb;
+                    sh.st[L].lq_len = lq_len;
+                    sh.st[L].flags |= fb;
+                }
             }
         }
         RS_MARK(6);

@@ -76,4 +76,30 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return readlane(v, 63);
 }
 
+// inclusive prefix scans over the wave with the same DPP steps (lane l ends with the lanes 0..l):
+// lanes with no DPP source take `old` = 0, the identity of max and of add
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_src0(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_scan_max_u32(uint32_t v) {
+    uint32_t w;
+    w = dpp_src0<0x111, 0xf>(v); v = w > v ? w : v;
+    w = dpp_src0<0x112, 0xf>(v); v = w > v ? w : v;
+    w = dpp_src0<0x114, 0xf>(v); v = w > v ? w : v;
+    w = dpp_src0<0x118, 0xf>(v); v = w > v ? w : v;
+    w = dpp_src0<0x142, 0xa>(v); v = w > v ? w : v;
+    w = dpp_src0<0x143, 0xc>(v); v = w > v ? w : v;
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_scan_add_u32(uint32_t v) {
+    v += dpp_src0<0x111, 0xf>(v);
+    v += dpp_src0<0x112, 0xf>(v);
+    v += dpp_src0<0x114, 0xf>(v);
+    v += dpp_src0<0x118, 0xf>(v);
+    v += dpp_src0<0x142, 0xa>(v);
+    v += dpp_src0<0x143, 0xc>(v);
+    return v;
+}
+
 }  // namespace mcs

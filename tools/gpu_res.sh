@@ -32,7 +32,7 @@ if [ -f variants/libmcs_res_stamps.so ]; then
     rc=$?; cat "$OUT/stamps.json"; echo "stamps rc=$rc"; [ $rc -ne 0 ] && exit $rc
 fi
 [ -n "${SKIP_PYTEST:-}" ] || {
-timeout -k 10 900 python -u -m pytest tests/test_gpu_trade.py -x -v --timeout 600 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_trade.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_trade.py -x -v -k "${PYTEST_K:-}" --timeout 600 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_trade.log" 2>&1
 rc=$?; tail -25 "$OUT/pytest_trade.log"; echo "pytest rc=$rc"; [ $rc -ne 0 ] && exit $rc
 }
 i=0
