@@ -477,7 +477,10 @@ __global__ __launch_bounds__(64) void fifo_asm_fused_kernel(FifoArgs a) {
     const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
     const uint32_t lane = threadIdx.x;
 
-    __shared__ uint64_t lds[NPL * kWave + 2 * P * kWave];
+    // LDS: the node words only (the register-slot loops keep no slot in LDS) and the generator's
+    // scratch
+    __shared__ uint32_t lds[NPL * kWave];
+    __shared__ uint32_t gscr[kGenScratch];
     constexpr uint32_t kGuard = 0x8000u, kClamp = kGuard - 1u;
     const uint32_t n0 = a.node_off[ci];
     const uint32_t N = a.node_off[ci + 1] - n0;
@@ -490,7 +493,7 @@ __global__ __launch_bounds__(64) void fifo_asm_fused_kernel(FifoArgs a) {
             v.x += kGuard;
             v.y += kGuard;
         }
-        reinterpret_cast<uint32_t*>(lds)[c * kWave + lane] = v.x | (v.y << 16);
+        lds[c * kWave + lane] = v.x | (v.y << 16);
     }
 
     const uint64_t j0 = a.job_off[ci];
@@ -500,7 +503,7 @@ __global__ __launch_bounds__(64) void fifo_asm_fused_kernel(FifoArgs a) {
     uint32_t* o_finish = a.out_finish + j0;
 
     GenStream gs;
-    gs.init(a.gen, ci, lane);
+    gs.init(a.gen, ci, lane, gscr);
     uint4 cur = gs.next(0u, lane);  // batch 0
     cur.z = cur.z < kClamp ? cur.z : kClamp;
     cur.w = cur.w < kClamp ? cur.w : kClamp;
@@ -508,7 +511,7 @@ __global__ __launch_bounds__(64) void fifo_asm_fused_kernel(FifoArgs a) {
     __syncthreads();
 
     const uint32_t base = lds_addr(lds);
-    const uint32_t v_pay = base + 2048u + lane * 8u;
+    const uint32_t v_pay = 0u;  // (no LDS slot rows)
     const uint32_t v_nb = base + lane * 4u;
     const uint32_t v_nbase = base;
     const uint32_t sel0 = NPL == 1 ? 0x7fffu : 0x0b0a0908u;

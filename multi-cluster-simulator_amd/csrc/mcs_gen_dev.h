@@ -30,14 +30,10 @@
 
 namespace mcs {
 
-__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t v, uint32_t lane) {
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t w = (uint32_t)__shfl_up((int)v, o);
-        v += lane >= (uint32_t)o ? w : 0u;
-    }
-    return v;
-}
+// (DPP row shifts and broadcasts, mcs_wave.h: no LDS round trip)
+__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t v, uint32_t) { return wave_scan_add_u32(v); }
+
+constexpr uint32_t kGenScratch = 4u * kWave;  // LDS words of GenStream's optional scratch
 
 struct GenStream {
     uint64_t ckey, akey;
@@ -48,6 +44,9 @@ struct GenStream {
     uint32_t tot, span;    // jobs and seconds of the whole window
     const uint64_t* wthr;  // WEIBULL: gap table; wcarry = arrival of the next batch's first job
     uint32_t wn, wcarry;
+    // Optional per-wave LDS scratch (kGenScratch words): the period search below runs as a scatter
+    // of period starts and a prefix maximum instead of the 6-step shuffle search
+    uint32_t* scr;
 
     __device__ __forceinline__ void fill(uint32_t lane) {
         n = mcs_poisson(akey, (uint64_t)pw + lane, enl);
@@ -59,7 +58,9 @@ struct GenStream {
         span = readlane(dinc, 63);
     }
 
-    __device__ __forceinline__ void init(const GenArgs& g, uint32_t cluster, uint32_t lane) {
+    __device__ __forceinline__ void init(const GenArgs& g, uint32_t cluster, uint32_t lane,
+                                         uint32_t* scratch = nullptr) {
+        scr = scratch;
         ckey = mcs_cluster_key(g.seed, g.base + cluster);
         akey = mcs_arrival_key(ckey);
         enl = g.enl;
@@ -89,15 +90,37 @@ struct GenStream {
         if (mode != 2u) for (;;) {  // (a wave-uniform loop: every lane takes part in the shuffles)
             // every lane searches (the shuffles need all lanes); lanes outside the window discard
             const uint32_t rel = j - jw;
-            uint32_t lo = 0u;
+            uint32_t lo = 0u, np, cp, te;
+            if (scr) {
+                // job lane l's period = the last period starting at or before it: each period with
+                // jobs marks its first job's lane (distinct lanes), the period holding the batch's
+                // first job comes from a ballot, and a prefix maximum spreads them; the period's
+                // {n, cum, tex} are then read back from its slot
+                const uint32_t off = base - jw;
+                const uint32_t st = cum - n;
+                const uint64_t cov = __ballot(n != 0u && st <= off);
+                scr[lane] = 0u;
+                if (n != 0u && st > off && st - off < (uint32_t)kWave) scr[st - off] = lane + 1u;
+                scr[kWave + lane * 3u] = n;
+                scr[kWave + lane * 3u + 1u] = cum;
+                scr[kWave + lane * 3u + 2u] = tex;
+                uint32_t mk = scr[lane];
+                if (lane == 0u && cov) mk = mk > 64u - (uint32_t)__builtin_clzll(cov) ? mk : 64u - (uint32_t)__builtin_clzll(cov);
+                const uint32_t sm = wave_scan_max_u32(mk);
+                lo = sm != 0u ? sm - 1u : 0u;
+                np = scr[kWave + lo * 3u];
+                cp = scr[kWave + lo * 3u + 1u];
+                te = scr[kWave + lo * 3u + 2u];
+            } else {
 #pragma unroll
-            for (uint32_t s = 32u; s != 0u; s >>= 1) {
-                const uint32_t c = (uint32_t)__shfl((int)cum, (int)(lo + s - 1u));
-                lo += c <= rel ? s : 0u;
+                for (uint32_t s = 32u; s != 0u; s >>= 1) {
+                    const uint32_t c = (uint32_t)__shfl((int)cum, (int)(lo + s - 1u));
+                    lo += c <= rel ? s : 0u;
+                }
+                np = (uint32_t)__shfl((int)n, (int)lo);
+                cp = (uint32_t)__shfl((int)cum, (int)lo);
+                te = (uint32_t)__shfl((int)tex, (int)lo);
             }
-            const uint32_t np = (uint32_t)__shfl((int)n, (int)lo);
-            const uint32_t cp = (uint32_t)__shfl((int)cum, (int)lo);
-            const uint32_t te = (uint32_t)__shfl((int)tex, (int)lo);
             const uint32_t a = mode == 0u ? tw + te + (rel - (cp - np)) * (60u / (np != 0u ? np : 1u))
                                           : pw + lo;
             if (!done && rel < tot) {

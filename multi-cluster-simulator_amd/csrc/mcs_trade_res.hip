@@ -50,6 +50,31 @@ __device__ __forceinline__ uint32_t rld32(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// a TrCluster field held in lane f of a VGPR (phase A's per-cluster state)
+constexpr uint32_t kStWords = sizeof(TrCluster) / 4u;
+static_assert(sizeof(TrCluster) % 4u == 0u && kStWords <= (uint32_t)kWave, "TrCluster in one VGPR");
+struct LaneField {
+    uint32_t& v;
+    uint32_t f, lane;
+    __device__ __forceinline__ operator uint32_t() const { return readlane(v, f); }
+    __device__ __forceinline__ LaneField& operator=(uint32_t x) {
+        v = lane == f ? x : v;
+        return *this;
+    }
+    __device__ __forceinline__ LaneField& operator=(const LaneField& o) { return *this = (uint32_t)o; }
+    __device__ __forceinline__ LaneField& operator+=(uint32_t x) { return *this = (uint32_t)*this + x; }
+    __device__ __forceinline__ LaneField& operator-=(uint32_t x) { return *this = (uint32_t)*this - x; }
+    __device__ __forceinline__ LaneField& operator|=(uint32_t x) { return *this = (uint32_t)*this | x; }
+    __device__ __forceinline__ LaneField& operator++() { return *this += 1u; }
+    __device__ __forceinline__ LaneField& operator--() { return *this -= 1u; }
+    __device__ __forceinline__ uint32_t operator++(int) {
+        const uint32_t o = *this;
+        *this = o + 1u;
+        return o;
+    }
+};
+#define ST(field) (LaneField{stv, (uint32_t)(offsetof(TrCluster, field) / 4u), lane})
+
 struct ResShared {  // (the node vectors follow, Ct * ns u64)
     TrXRec x[kTrResMaxClusters];
     TrCluster st[kTrResMaxClusters];
@@ -197,10 +222,13 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
             const uint4* __restrict__ jobs = a.jobs + j0;
             const size_t sb = (size_t)c * S;
             const uint32_t vn = sh.trs[c].vnodes;
-            TrCluster& st = sh.st[c];  // (in LDS: registers hold the slot rows)
+            // the cluster's queue state: word f of its TrCluster in lane f of one VGPR (uniform
+            // reads are v_readlane, writes a lane select; never written under a lane-divergent
+            // branch)
+            uint32_t stv = lane < kStWords ? reinterpret_cast<const uint32_t*>(&sh.st[c])[lane] : 0u;
 
             // releases due at T (cluster.go:153-157), before the tick's decisions
-            if (st.minf <= T) {
+            if (ST(minf) <= T) {
                 // the expired slots' {node, payload} loads of up to 8 rows issued together, then
                 // their node updates
                 constexpr int kG = kResRows < 4 ? kResRows : 4;
@@ -232,29 +260,29 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                         }
                     }
                 }
-                st.nrun -= rwave_sum(nrel);
-                st.minf = wave_min_u32(lm);
+                ST(nrun) -= rwave_sum(nrel);
+                ST(minf) = wave_min_u32(lm);
             }
             RS_MARK(1);
             // arrivals up to T join the ReadyQueue (jobs are sorted by arrival): the arrival
             // window, then direct loads past a full window
             uint32_t nat;  // the arrival second of the first job not yet queued (kEmpty: none)
             {
-                const uint32_t na = st.next_arr;
+                const uint32_t na = ST(next_arr);
                 const uint32_t n = (uint32_t)__builtin_popcountll(
                     (__ballot(awin <= T && na + (lane & 15u) < J) >> wl) & 0xffffull);
-                st.next_arr = na + n;
+                ST(next_arr) = na + n;
                 if (n < 16u) {
                     nat = readlane(awin, wl + n);
                 } else {
-                    while (st.next_arr < J) {
-                        const uint32_t i = st.next_arr + lane;
+                    while (ST(next_arr) < J) {
+                        const uint32_t i = ST(next_arr) + lane;
                         const bool ok = i < J && jobs[i].x <= T;
                         const uint32_t m = (uint32_t)__builtin_popcountll(__ballot(ok));
-                        st.next_arr += m;
+                        ST(next_arr) += m;
                         if (m < (uint32_t)kWave) break;
                     }
-                    nat = st.next_arr < J ? jobs[st.next_arr].x : kEmpty;
+                    nat = ST(next_arr) < J ? jobs[ST(next_arr)].x : kEmpty;
                 }
             }
             // record j: from the head window when it holds it
@@ -305,9 +333,9 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                         if ((uint32_t)r == row) wf[r] = f;
                     wfrm &= ~(1u << row);
                 }
-                ++st.nrun;
-                st.peak = st.nrun > st.peak ? st.nrun : st.peak;
-                st.minf = f < st.minf ? f : st.minf;
+                ++ST(nrun);
+                ST(peak) = ST(nrun) > ST(peak) ? ST(nrun) : ST(peak);
+                ST(minf) = f < ST(minf) ? f : ST(minf);
                 return true;
             };
             auto place_own = [&](uint32_t j, uint32_t kn, uint4 jb) -> bool {
@@ -318,45 +346,45 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                     a.out_start[j0 + j] = T;
                     a.out_finish[j0 + j] = f;
                 }
-                ++st.placed;
-                ++st.decided;
+                ++ST(placed);
+                ++ST(decided);
                 return true;
             };
 
             TrRecA req{kEmpty, 0u, 0u, 0u};
             for (;;) {
-                if (st.has_w) {  // WaitQueue head (scheduler.go:219-251)
-                    const uint4 jb = job_at(st.w);
+                if (ST(has_w)) {  // WaitQueue head (scheduler.go:219-251)
+                    const uint4 jb = job_at(ST(w));
                     const uint32_t kn = first_fit(jb.z, jb.w);
                     if (kn != kEmpty) {
-                        if (!place_own(st.w, kn, jb)) {
-                            st.flags |= MCS_FLAG_OVERFLOW;
+                        if (!place_own(ST(w), kn, jb)) {
+                            ST(flags) |= MCS_FLAG_OVERFLOW;
                             break;
                         }
-                        st.has_w = 0u;
+                        ST(has_w) = 0u;
                     } else if (a.borrow) {
-                        req = TrRecA{st.w, jb.z, jb.w, jb.y};  // BorrowResources (:234)
+                        req = TrRecA{ST(w), jb.z, jb.w, jb.y};  // BorrowResources (:234)
                     }
                     break;  // time.Sleep(1 s), :250
                 }
-                if (st.rq_head < st.next_arr) {  // ReadyQueue head (:255-272), no sleep
-                    const uint32_t j = st.rq_head++;
+                if (ST(rq_head) < ST(next_arr)) {  // ReadyQueue head (:255-272), no sleep
+                    const uint32_t j = ST(rq_head)++;
                     const uint4 jb = job_at(j);
                     const uint32_t kn = first_fit(jb.z, jb.w);
                     if (kn != kEmpty) {
                         if (!place_own(j, kn, jb)) {
-                            st.flags |= MCS_FLAG_OVERFLOW;
+                            ST(flags) |= MCS_FLAG_OVERFLOW;
                             break;
                         }
                     } else {
-                        st.has_w = 1u;
-                        st.w = j;
-                        ++st.waited;
+                        ST(has_w) = 1u;
+                        ST(w) = j;
+                        ++ST(waited);
                     }
                     continue;
                 }
-                if (st.lq_len > 0u) {  // LentQueue head (:277-290), written by this wave in phase B
-                    const TrLq* q = a.lq + (size_t)c * a.LQ + st.lq_head;
+                if (ST(lq_len) > 0u) {  // LentQueue head (:277-290), written by this wave in phase B
+                    const TrLq* q = a.lq + (size_t)c * a.LQ + ST(lq_head);
                     const uint64_t w0 = rld64(reinterpret_cast<const unsigned long long*>(q));
                     const uint64_t w1 = rld64(reinterpret_cast<const unsigned long long*>(q) + 1);
                     const uint64_t w2 = rld64(reinterpret_cast<const unsigned long long*>(q) + 2);
@@ -366,7 +394,7 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                     if (kn != kEmpty) {
                         const uint32_t f = T + ed;
                         if (ed != 0u && !commit(kn, ec, em, f)) {
-                            st.flags |= MCS_FLAG_OVERFLOW;
+                            ST(flags) |= MCS_FLAG_OVERFLOW;
                             break;
                         }
                         if (lane == 0) {
@@ -383,9 +411,9 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                                 a.lent_log[idx] = rec;
                             }
                         }
-                        ++st.lent_runs;
-                        st.lq_head = st.lq_head + 1u == a.LQ ? 0u : st.lq_head + 1u;
-                        --st.lq_len;
+                        ++ST(lent_runs);
+                        ST(lq_head) = ST(lq_head) + 1u == a.LQ ? 0u : ST(lq_head) + 1u;
+                        --ST(lq_len);
                     }
                     break;  // sleep 1 s (:289)
                 }
@@ -405,24 +433,24 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                 // (mod 2^32: the signed sum, < 2^24 in size)
                 const float sc = (float)(int32_t)(sh.capc[c] - rwave_sum(fc));
                 const float sm = (float)(int32_t)(sh.capm[c] - rwave_sum(fm));
-                st.cu = __fdiv_rn(sc, (float)st.total_c);
-                st.mu = __fdiv_rn(sm, (float)st.total_m);
+                ST(cu) = __float_as_uint(__fdiv_rn(sc, (float)ST(total_c)));
+                ST(mu) = __float_as_uint(__fdiv_rn(sm, (float)ST(total_m)));
             }
             if (lane == 0) {
                 TrXRec x;
                 x.req = req;
                 x.n = N;
-                x.has_w = st.has_w;
-                x.lq_len = st.lq_len;
-                x.rq_busy = st.rq_head < st.next_arr ? 1u : 0u;
-                x.decided = st.decided;
+                x.has_w = ST(has_w);
+                x.lq_len = ST(lq_len);
+                x.rq_busy = ST(rq_head) < ST(next_arr) ? 1u : 0u;
+                x.decided = ST(decided);
                 x.J = J;
                 x.next_arr_t = nat;
-                x.flags = st.flags;
-                x.cu = st.cu;
-                x.mu = st.mu;
-                x.total_c = st.total_c;
-                x.total_m = st.total_m;
+                x.flags = ST(flags);
+                x.cu = __uint_as_float(ST(cu));
+                x.mu = __uint_as_float(ST(mu));
+                x.total_c = ST(total_c);
+                x.total_m = ST(total_m);
                 sh.x[c] = x;
             }
 #pragma unroll
@@ -436,6 +464,7 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
             frm[1] = k == 1 ? wfrm : frm[1];
             frm[2] = k == 2 ? wfrm : frm[2];
             frm[3] = k == 3 ? wfrm : frm[3];
+            if (lane < kStWords) reinterpret_cast<uint32_t*>(&sh.st[c])[lane] = stv;
             RS_MARK(4);
         }
         __syncthreads();
