@@ -42,12 +42,15 @@ __device__ __forceinline__ uint32_t rwave_sum(uint32_t v) {
     return v;
 }
 
-// HBM written by this kernel and read back later: through L2, never a stale line of the vector L1
+// HBM this kernel wrote and reads back (slot payloads, LentQueue entries): all of it is written and
+// read by the one CU, whose vector L1 sees its own stores, so workgroup-scope loads (served by the
+// L1 or this XCD's L2) suffice.  (Agent-scope loads would go past the XCD's L2 to keep 8 XCDs
+// coherent: about 2 us each, measured as most of a release and of a lent run.)
 __device__ __forceinline__ uint64_t rld64(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ uint32_t rld32(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // a TrCluster field held in lane f of a VGPR (phase A's per-cluster state)
@@ -84,7 +87,7 @@ struct ResShared {  // (the node vectors follow, Ct * ns u64)
     uint32_t capc[kTrResMaxClusters], capm[kTrResMaxClusters];  // sums of capacities (mod 2^32)
     uint32_t gtab[kResWaves][64];  // phase B: a lender's G table, one per wave
     uint32_t T, done, ticks, flags;
-    unsigned long long n_trades, n_won;
+    unsigned long long n_trades, n_won, n_lent;  // (n_lent: the lent log's cursor)
 };
 
 #ifdef MCS_STAMPS
@@ -130,6 +133,7 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
         sh.flags = ctl.flags;
         sh.n_trades = ctl.n_trades;
         sh.n_won = ctl.n_won;
+        sh.n_lent = ctl.n_lent;
     }
     // this wave's clusters: slot finish times in registers (row r, lane l = slot r * 64 + l), and
     // the sums of capacities the utilization sample subtracts the free vector from
@@ -398,7 +402,7 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                             break;
                         }
                         if (lane == 0) {
-                            const unsigned long long idx = atomicAdd(&a.ctl->n_lent, 1ull);
+                            const unsigned long long idx = atomicAdd(&sh.n_lent, 1ull);
                             if (idx < a.lent_cap) {
                                 mcs_lent_rec rec;
                                 rec.lender = c;
@@ -715,7 +719,7 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
         ctl.done = sh.done;
         ctl.ticks = sh.ticks;
         ctl.flags = sh.flags;
-        ctl.n_lent = rld64(&a.ctl->n_lent);
+        ctl.n_lent = sh.n_lent;
         ctl.n_trades = sh.n_trades;
         ctl.n_won = sh.n_won;
         *a.ctl = ctl;
