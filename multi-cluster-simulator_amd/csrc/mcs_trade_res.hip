@@ -564,9 +564,17 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
         __syncthreads();
         RS_MARK(7);
 
-        // ---- phases C and D: wave 0 (tr_trader_kernel) ----
+        // ---- phases C and D: wave 0 (tr_trader_kernel), one lane per cluster (C <= 64) ----
+        // The borrower step, then the trader rounds with every trader's state in the lanes'
+        // registers: a due requester that is not over the utilization threshold only moves its own
+        // due time (all of them at once); the others run their RequestResource rounds in index
+        // order, each a ballot over the responders' lock states, with no LDS round trip.
         if (wave == 0) {
-            for (uint32_t g = lane; g < C; g += kWave) {  // the borrower step (post_cluster)
+            const uint32_t g = lane;
+            float cu = 0.0f, mu = 0.0f;
+            uint32_t tot_c = 0u, tot_m = 0u, busy = 0u, next_arr_t = kEmpty, done_g = 1u, fl = 0u;
+            TrTrader t{0u, 0u, 0u, kEmpty, 0u};
+            if (g < C) {
                 const TrXRec x = sh.x[g];
                 const uint32_t accg = sh.acc[g], lq = sh.lqp[g], fbg = sh.fb[g];
                 uint32_t has_w = x.has_w, decided = x.decided;
@@ -582,92 +590,70 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
                     ++sh.st[g].borrowed;
                 }
                 sh.acc[g] = 0u;
-                TrRecC o;
-                o.cu = x.cu;
-                o.mu = x.mu;
-                o.total_c = x.total_c;
-                o.total_m = x.total_m;
-                o.busy = (has_w || lq > 0u || x.rq_busy) ? 1u : 0u;
-                o.next_arr_t = x.next_arr_t;
-                o.done = (decided == x.J && lq == 0u) ? 1u : 0u;
-                o.flags = x.flags | fbg;
-                sh.rcs[g] = o;
+                cu = x.cu;
+                mu = x.mu;
+                tot_c = x.total_c;
+                tot_m = x.total_m;
+                busy = (has_w || lq > 0u || x.rq_busy) ? 1u : 0u;
+                next_arr_t = x.next_arr_t;
+                done_g = (decided == x.J && lq == 0u) ? 1u : 0u;
+                fl = x.flags | fbg;
+                t = sh.trs[g];
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
             unsigned long long n_trades = sh.n_trades, n_won = sh.n_won;
             uint32_t lflags = 0;
             if (a.trader) {
-                for (uint32_t q0 = 0; q0 < C; q0 += kWave) {
-                    const uint32_t ql = q0 + lane;
-                    unsigned long long due = __ballot(ql < C && sh.trs[ql].next_due <= T);
-                    while (due) {  // RequestPolicyMonitor of requester q (trader.go:282-324)
-                        const uint32_t q = q0 + (uint32_t)__builtin_ctzll(due);
-                        due &= due - 1ull;
-                        const TrRecC rq = sh.rcs[q];
-                        const bool broken = rq.cu > 0.8f || rq.mu > 0.8f;  // Utilization (:127-130)
-                        if (!broken) {
-                            if (lane == 0) sh.trs[q].next_due = T + a.period;
-                            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-                            continue;
+                const bool due = g < C && t.next_due <= T;
+                const bool broken = cu > 0.8f || mu > 0.8f;  // Utilization (trader.go:127-130)
+                if (due && !broken) t.next_due = T + a.period;
+                // ApproveTrade of this lane as a responder: its sample is fixed for the tick
+                const bool appr = g < C && approve_trade_dev(tot_c, tot_m, cu, mu, 0u, 0u, 0u);
+                unsigned long long pend = __ballot(due && broken);
+                while (pend) {  // RequestPolicyMonitor of requester q (trader.go:282-324)
+                    const uint32_t q = (uint32_t)__builtin_ctzll(pend);
+                    pend &= pend - 1ull;
+                    bool app = false;
+                    if (g < C && g != q) {  // RequestResource, index order
+                        if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
+                        if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
+                            app = appr;
+                            t.lock_id = t.next_id++;  // set even when not approving (:44-46)
+                            t.lock_until = T + a.lock_s;
                         }
-                        uint32_t napp = 0, winner = kEmpty;
-                        for (uint32_t r0 = 0; r0 < C; r0 += kWave) {  // RequestResource, index order
-                            const uint32_t r = r0 + lane;
-                            bool app = false;
-                            if (r < C && r != q) {
-                                TrTrader t = sh.trs[r];
-                                if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
-                                if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
-                                    const TrRecC rr = sh.rcs[r];
-                                    app = approve_trade_dev(rr.total_c, rr.total_m, rr.cu, rr.mu, 0u, 0u, 0u);
-                                    t.lock_id = t.next_id++;  // set even when not approving (:44-46)
-                                    t.lock_until = T + a.lock_s;
-                                }
-                                sh.trs[r] = t;
-                            }
-                            const unsigned long long ab = __ballot(app);
-                            napp += (uint32_t)__builtin_popcountll(ab);
-                            if (winner == kEmpty && ab) winner = r0 + (uint32_t)__builtin_ctzll(ab);
-                        }
-                        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-                        if (lane == 0) {
-                            if (winner != kEmpty) {
-                                sh.trs[winner].lock_id = 0u;  // ApproveContract unlocks (:83)
-                                sh.trs[q].vnodes += 1u;       // AddVirtualNode(0 cores, 0 memory)
-                                ++n_won;
-                            }
-                            if (n_trades < a.trade_cap) {
-                                mcs_trade_rec rec;
-                                rec.t_s = T;
-                                rec.requester = q;
-                                rec.winner = winner == kEmpty ? -1 : (int32_t)winner;
-                                rec.approvals = napp;
-                                a.trade_log[n_trades] = rec;
-                            } else {
-                                lflags |= MCS_FLAG_LOG_OVERFLOW;
-                            }
-                            sh.trs[q].next_due = T + (winner != kEmpty ? a.ok_sleep : a.fail_sleep) + a.period;
-                        }
-                        ++n_trades;
-                        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
                     }
+                    const unsigned long long ab = __ballot(app);
+                    const uint32_t napp = (uint32_t)__builtin_popcountll(ab);
+                    const uint32_t winner = ab ? (uint32_t)__builtin_ctzll(ab) : kEmpty;
+                    if (winner != kEmpty) {
+                        if (g == winner) t.lock_id = 0u;  // ApproveContract unlocks (:83)
+                        if (g == q) t.vnodes += 1u;       // AddVirtualNode(0 cores, 0 memory)
+                        ++n_won;
+                    }
+                    if (g == q) t.next_due = T + (winner != kEmpty ? a.ok_sleep : a.fail_sleep) + a.period;
+                    if (lane == 0) {
+                        if (n_trades < a.trade_cap) {
+                            mcs_trade_rec rec;
+                            rec.t_s = T;
+                            rec.requester = q;
+                            rec.winner = winner == kEmpty ? -1 : (int32_t)winner;
+                            rec.approvals = napp;
+                            a.trade_log[n_trades] = rec;
+                        } else {
+                            lflags |= MCS_FLAG_LOG_OVERFLOW;
+                        }
+                    }
+                    ++n_trades;
                 }
+                if (g < C) sh.trs[g] = t;
             }
             // the next tick: T+1 while any queue is busy, else the next arrival or trader round
-            bool all_done = true, busy = false;
-            uint32_t nxt = kEmpty, fl = 0;
-            for (uint32_t q = lane; q < C; q += kWave) {
-                const TrRecC rc = sh.rcs[q];
-                all_done = all_done && rc.done;
-                busy = busy || rc.busy;
-                nxt = rc.next_arr_t < nxt ? rc.next_arr_t : nxt;
-                if (a.trader) nxt = sh.trs[q].next_due < nxt ? sh.trs[q].next_due : nxt;
-                fl |= rc.flags;
-            }
-            const bool done_all = !__ballot(!all_done);
-            const bool busy_any = __ballot(busy) != 0ull;
+            uint32_t nxt = next_arr_t;
+            if (a.trader && g < C) nxt = t.next_due < nxt ? t.next_due : nxt;
+            const bool done_all = !__ballot(!done_g);
+            const bool busy_any = __ballot(busy != 0u) != 0ull;
             nxt = wave_min_u32(nxt);
             for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o);
+            lflags = (uint32_t)__shfl((int)lflags, 0);
             if (lane == 0) {
                 uint32_t flags = sh.flags | fl | lflags;
                 uint32_t done = 0, Tn = T;
