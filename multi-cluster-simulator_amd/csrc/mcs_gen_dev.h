@@ -95,15 +95,21 @@ struct GenStream {
                 // job lane l's period = the last period starting at or before it: each period with
                 // jobs marks its first job's lane (distinct lanes), the period holding the batch's
                 // first job comes from a ballot, and a prefix maximum spreads them; the period's
-                // {n, cum, tex} are then read back from its slot
-                const uint32_t off = base - jw;
-                const uint32_t st = cum - n;
-                const uint64_t cov = __ballot(n != 0u && st <= off);
+                // {n, cum, tex} are then read back from its slot.  The period's first job sits in
+                // lane d = st - off; off < 0 when the batch straddles into this window (its first
+                // lanes were decided in the previous one): no period then covers lane 0.
+                const int32_t off = (int32_t)(base - jw);
+                const int32_t d = (int32_t)(cum - n) - off;
+                const uint64_t cov = __ballot(n != 0u && d <= 0);
                 scr[lane] = 0u;
-                if (n != 0u && st > off && st - off < (uint32_t)kWave) scr[st - off] = lane + 1u;
+                if (n != 0u && d > 0 && d < (int32_t)kWave) scr[d] = lane + 1u;
                 scr[kWave + lane * 3u] = n;
                 scr[kWave + lane * 3u + 1u] = cum;
                 scr[kWave + lane * 3u + 2u] = tex;
+                // the reads below take other lanes' stores: a compiler memory barrier, or LLVM
+                // forwards this lane's own `scr[lane] = 0` (measured: it did, and read the slot only
+                // under the marking lanes' exec).  The wave's LDS ops run in order, so no wait.
+                asm volatile("" ::: "memory");
                 uint32_t mk = scr[lane];
                 if (lane == 0u && cov) mk = mk > 64u - (uint32_t)__builtin_clzll(cov) ? mk : 64u - (uint32_t)__builtin_clzll(cov);
                 const uint32_t sm = wave_scan_max_u32(mk);
