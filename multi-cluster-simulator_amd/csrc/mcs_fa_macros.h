@@ -405,6 +405,367 @@
     "s_sub_u32 s80, s80, s75\n\t" MCS_FA_RELOAD16S                                              \
     "v_min_u32 v90, v32, v33\n\t"
 
+// the end of a release scan: the wave's earliest remaining finish (DPP minimum of v90) under the
+// node reload's latency, then the reload's wait
+#define MCS_FA_SCANEND                                                                            \
+    "v_mov_b32 v120, v90\n\t"                                                                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"                  \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"                  \
+    "s_nop 1\n\t"                                                                                 \
+    "v_readlane_b32 s77, v120, 63\n\t"                                                            \
+    "s_waitcnt lgkmcnt(0)\n\t"
+#define MCS_FA_SCANEND32 MCS_FA_SCANEND
+#define MCS_FA_SCANEND16 MCS_FA_SCANEND
+#define MCS_FA_SCANEND16R MCS_FA_SCANEND
+#define MCS_FA_SCANEND16S MCS_FA_SCANEND
+// batch-end hook (the duo loop's ring check); nothing for the one-wave forms
+#define MCS_FA_BENDCHK32 ""
+#define MCS_FA_BENDCHK16 ""
+#define MCS_FA_BENDCHK16R ""
+#define MCS_FA_BENDCHK16S ""
+
+// ---- W16D: the duo loop's decision wave (fifo_duo_kernel, mcs_fifo_asm.hip) --------------------
+// W16R's node format and first fit, with the running slots held by a second wave of the workgroup
+// (the release wave, MCS_FH_LOOP below): a commit posts the slot {kx, finish, payload, seq} to an LDS
+// ring instead of inserting it, and a clock advance past the earliest finish applies the release
+// packet the release wave keeps ready for it (the payloads of the slots finishing at that second,
+// summed per node in the node registers' layout) with four v_pk_add_u16 — no slot scan, no LDS
+// node round trip and no wave minimum on this wave's chain.
+//   s49 slots posted   s60 ring offset of the next post   s62 finish of the last post   s63 waits
+//   v102-v106 the post   v109 ring base   v118 the packet's delta words of this lane (+256 per chunk)
+//   v119 packet header {e1, e2, posts taken, slots} (+16: ack, +20: done)
+// Header check: the packet is for this wave's earliest finish s77 and the release wave has taken
+// every post, or every post but the last one whose finish lies after the packet's second (its own
+// second then becomes the next candidate).  Otherwise the wave re-reads the header (bounded: past
+// 4096 reads the cluster stops as a pool overflow and the engine re-runs it on the compiled kernel).
+#define MCS_FA_FIT16D                                                                             \
+    "v_pk_sub_u16 v72, v64, s48\n\t"                                                              \
+    "v_pk_sub_u16 v73, v65, s48\n\t"                                                              \
+    "v_pk_sub_u16 v74, v66, s48\n\t"                                                              \
+    "v_pk_sub_u16 v75, v67, s48\n\t"                                                              \
+    "v_and_b32_sdwa v80, v72, v72 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v81, v74, v74 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v80, v73, v73 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v81, v75, v75 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "s_nop 1\n\t" /* (the SDWA hazard of MCS_FA_FIT16) */                                       \
+    "v_perm_b32 v86, v81, v80, s72\n\t"
+#define MCS_FA_ANYFIT16D MCS_FA_ANYFIT
+#define MCS_FA_DECIDE16D                                                                          \
+    "v_readlane_b32 s51, v86, s50\n\t"                                                            \
+    "s_lshl_b64 exec, 1, s50\n\t"                                                                 \
+    "s_ff1_i32_b32 s52, s51\n\t"                                                                  \
+    "s_lshr_b32 s53, s52, 3\n\t"                                                                  \
+    "s_lshl3_add_u32 s54, s52, s50\n\t"                                                           \
+    "s_set_gpr_idx_on s53, gpr_idx(SRC0,DST)\n\t"                                                 \
+    "v_mov_b32 v64, v72\n\t" /* the commit (cluster.go:146-147) */                                \
+    "s_set_gpr_idx_off\n\t"                                                                       \
+    /* the post, seq written last (the release wave takes an entry by its seq) */                \
+    "v_mov_b64 v[102:103], s[54:55]\n\t"                                                          \
+    "v_mov_b32 v104, s48\n\t"                                                                     \
+    "v_mov_b32 v105, s49\n\t"                                                                     \
+    "v_add_u32 v106, s60, v109\n\t"                                                               \
+    "ds_write_b96 v106, v[102:104]\n\t"                                                           \
+    "ds_write_b32 v106, v105 offset:12\n\t"                                                       \
+    "s_add_u32 s49, s49, 1\n\t"                                                                   \
+    "s_add_u32 s60, s60, 16\n\t"                                                                  \
+    "s_and_b32 s60, s60, 0x7f0\n\t"                                                               \
+    "s_mov_b32 s62, s55\n\t"
+#define MCS_FA_REC16D MCS_FA_REC16
+#define MCS_FA_ZEROKX16D MCS_FA_ZEROKX
+#define MCS_FA_POOLMAX16D "64*8"
+#define MCS_FA_NODEIDX16D MCS_FA_NODEIDX
+#define MCS_FA_TAKE16D MCS_FA_TAKE16
+#define MCS_FA_RELOAD16D MCS_FA_RELOAD16
+#define MCS_FA_INIT16D                                                                            \
+    "s_mov_b32 s49, 0\n\t" MCS_FD_SPIN0                                                          \
+    "s_mov_b32 s60, 0\n\t"                                                                        \
+    "s_mov_b32 s62, 0\n\t"                                                                        \
+    "s_mov_b32 s63, 0\n\t"                                                                        \
+    "v_mov_b32 v118, %[dl]\n\t"                                                                   \
+    "v_mov_b32 v119, %[hdr]\n\t"
+#define MCS_FA_SCAN16D                                                                            \
+    "mcsfd_rd_%=:\n\t"                                                                            \
+    "ds_read_b128 v[120:123], v119\n\t"                                                           \
+    "ds_read2st64_b32 v[124:125], v118 offset1:1\n\t"                                             \
+    "ds_read2st64_b32 v[126:127], v118 offset0:2 offset1:3\n\t"                                   \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
+    "v_readfirstlane_b32 s86, v120\n\t" /* e1 */                                                 \
+    "v_readfirstlane_b32 s87, v121\n\t" /* e2 */                                                 \
+    "v_readfirstlane_b32 s88, v122\n\t" /* posts taken */                                        \
+    "v_readfirstlane_b32 s75, v123\n\t" /* slots finishing at e1 */                              \
+    "s_sub_u32 s89, s49, s88\n\t"                                                                 \
+    "s_cmp_eq_u32 s89, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_all_%=\n\t"                                                             \
+    "s_cmp_eq_u32 s89, 1\n\t"                                                                     \
+    "s_cbranch_scc0 mcsfd_wait_%=\n\t"                                                            \
+    "s_cmp_gt_u32 s62, s86\n\t"                                                                   \
+    "s_cbranch_scc0 mcsfd_wait_%=\n\t"                                                            \
+    "s_min_u32 s87, s87, s62\n"                                                                   \
+    "mcsfd_all_%=:\n\t"                                                                           \
+    "s_cmp_eq_u32 s86, s77\n\t"                                                                   \
+    "s_cbranch_scc0 mcsfd_wait_%=\n\t"                                                            \
+    "v_pk_add_u16 v64, v64, v124\n\t" /* the releases (cluster.go:153-157) */                   \
+    "v_pk_add_u16 v65, v65, v125\n\t"                                                             \
+    "v_pk_add_u16 v66, v66, v126\n\t"                                                             \
+    "v_pk_add_u16 v67, v67, v127\n\t"                                                             \
+    "v_mov_b32 v120, s86\n\t"                                                                     \
+    "s_mov_b64 exec, 1\n\t"                                                                       \
+    "ds_write_b32 v119, v120 offset:16\n\t" /* ack: the release wave retires e1 */             \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "s_sub_u32 s80, s80, s75\n\t"                                                                 \
+    "s_mov_b32 s77, s87\n\t"                                                                      \
+    "s_mov_b32 s63, 0\n\t"                                                                        \
+    "s_cmp_lt_u32 s40, s77\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfd_done_%=\n\t"                                                            \
+    "s_branch mcsfd_rd_%=\n" /* a second finish second is due too (rare) */                      \
+    "mcsfd_wait_%=:\n\t" MCS_FD_SPIN                                                              \
+    "s_bitcmp1_b32 s75, 31\n\t" /* the release wave's slots overflowed */                       \
+    "s_cbranch_scc1 mcsfa_poolovf_%=\n\t"                                                         \
+    "s_add_u32 s63, s63, 1\n\t"                                                                   \
+    "s_cmp_gt_u32 s63, 0x1000\n\t"                                                                \
+    "s_cbranch_scc1 mcsfa_poolovf_%=\n\t"                                                         \
+    "s_branch mcsfd_rd_%=\n"                                                                      \
+    "mcsfd_done_%=:\n\t"
+#define MCS_FA_SCANEND16D ""
+// the ring holds 128 posts: at a batch end at most 64 may be untaken, so the batch's <= 64 posts
+// cannot overwrite one
+#define MCS_FA_BENDCHK16D                                                                         \
+    "mcsfd_bc_%=:\n\t"                                                                            \
+    "ds_read_b32 v120, v119 offset:8\n\t"                                                         \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
+    "v_readfirstlane_b32 s88, v120\n\t"                                                           \
+    "s_sub_u32 s89, s49, s88\n\t"                                                                 \
+    "s_cmp_le_u32 s89, 64\n\t"                                                                    \
+    "s_cbranch_scc1 mcsfd_bcok_%=\n\t"                                                            \
+    "s_add_u32 s63, s63, 1\n\t"                                                                   \
+    "s_cmp_gt_u32 s63, 0x1000\n\t"                                                                \
+    "s_cbranch_scc1 mcsfa_poolovf_%=\n\t"                                                         \
+    "s_branch mcsfd_bc_%=\n"                                                                      \
+    "mcsfd_bcok_%=:\n\t"                                                                          \
+    "s_mov_b32 s63, 0\n\t"
+#define MCS_FD_CLOBBERS MCS_FA_CLOBBERS, "v102", "v103", "v104", "v105", "v106"
+
+// ---- the duo loop's release wave: the running slots and the release packet ------------------------
+// Rows as W16R (row r of a lane: v(32+r) finish, v(40+r) payload, v(48+r) the node's delta word
+// address), free rows in v89 (+ the 0x100 sentinel).  The wave polls the ack word, the done word and
+// the ring entry of its next post; a post is inserted (and added to the packet when it finishes at
+// e1, or starts a new packet when it finishes earlier), an ack of e1 frees e1's slots and builds the
+// packet of the next finish second.  Every change publishes the header {e1, e2, posts taken, slots
+// at e1} after the delta words it covers (one wave's LDS operations complete in order).
+//   s40 e1  s41 e2  s42 posts taken  s43 slots at e1 (bit 31: a post found no free slot)
+//   s44 ring offset  s45-s55 temps  s56 polls  s57 poll bound  s58 delta base  s59 0x100
+//   v109 ring base  v111 -1  v112 0  v113 ring entry address  v114 this lane's delta words
+//   v115 header address  v117 lowest free row  v120-v127 reads / temps
+#define MCS_FH_FREE(p, MASK, F)                                                                   \
+    "s_and_b64 exec, " MASK ", -1\n\t"                                                            \
+    "s_cbranch_scc0 mcsfh_f" #p "_%=\n\t"                                                         \
+    "v_mov_b32 " F ", -1\n\t"                                                                     \
+    "v_or_b32 v89, 1<<" #p ", v89\n"                                                              \
+    "mcsfh_f" #p "_%=:\n\t"
+#define MCS_FH_ADD(p, MASK, P, A)                                                                 \
+    "s_and_b64 exec, " MASK ", -1\n\t"                                                            \
+    "s_cbranch_scc0 mcsfh_a" #p "_%=\n\t"                                                         \
+    "s_bcnt1_i32_b64 s54, " MASK "\n\t"                                                           \
+    "ds_add_u32 " A ", " P "\n\t"                                                                 \
+    "s_add_u32 s43, s43, s54\n"                                                                   \
+    "mcsfh_a" #p "_%=:\n\t"
+#define MCS_FH_CMP(s0)                                                                            \
+    "v_cmp_eq_u32_e64 s[60:61], " s0 ", v32\n\t"                                                  \
+    "v_cmp_eq_u32_e64 s[62:63], " s0 ", v33\n\t"                                                  \
+    "v_cmp_eq_u32_e64 s[64:65], " s0 ", v34\n\t"                                                  \
+    "v_cmp_eq_u32_e64 s[66:67], " s0 ", v35\n\t"                                                  \
+    "v_cmp_eq_u32_e64 s[68:69], " s0 ", v36\n\t"                                                  \
+    "v_cmp_eq_u32_e64 s[70:71], " s0 ", v37\n\t"                                                  \
+    "v_cmp_eq_u32_e64 s[72:73], " s0 ", v38\n\t"                                                  \
+    "v_cmp_eq_u32_e64 s[74:75], " s0 ", v39\n\t"
+#define MCS_FH_LOOP                                                                               \
+    "s_mov_b32 s40, -1\n\t"                                                                       \
+    "s_mov_b32 s41, -1\n\t"                                                                       \
+    "s_mov_b32 s42, 0\n\t"                                                                        \
+    "s_mov_b32 s43, 0\n\t"                                                                        \
+    "s_mov_b32 s44, 0\n\t"                                                                        \
+    "s_mov_b32 s56, 0\n\t"                                                                        \
+    "s_mov_b32 s57, %[hb]\n\t"                                                                    \
+    "s_mov_b32 s58, %[db]\n\t"                                                                    \
+    "s_mov_b32 s59, 0x100\n\t"                                                                    \
+    "v_mov_b32 v109, %[rb]\n\t"                                                                   \
+    "v_mov_b32 v111, -1\n\t"                                                                      \
+    "v_mov_b32 v112, 0\n\t"                                                                       \
+    "v_mov_b32 v113, %[rb]\n\t"                                                                   \
+    "v_mov_b32 v114, %[dl]\n\t"                                                                   \
+    "v_mov_b32 v115, %[hdr]\n\t"                                                                  \
+    "v_mov_b32 v89, 0x1ff\n\t"                                                                    \
+    "v_mov_b32 v32, -1\n\t"                                                                       \
+    "v_mov_b32 v33, -1\n\t"                                                                       \
+    "v_mov_b32 v34, -1\n\t"                                                                       \
+    "v_mov_b32 v35, -1\n\t"                                                                       \
+    "v_mov_b32 v36, -1\n\t"                                                                       \
+    "v_mov_b32 v37, -1\n\t"                                                                       \
+    "v_mov_b32 v38, -1\n\t"                                                                       \
+    "v_mov_b32 v39, -1\n"                                                                         \
+    "mcsfh_poll_%=:\n\t"                                                                          \
+    /* the ack and done words before the ring entry: a post precedes any later ack of the   */    \
+    /* decision wave, so an ack seen here comes with every post before it                   */    \
+    "ds_read_b32 v120, v115 offset:16\n\t"                                                        \
+    "ds_read_b32 v121, v115 offset:20\n\t"                                                        \
+    "ds_read_b128 v[124:127], v113\n\t"                                                           \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
+    "v_readfirstlane_b32 s45, v127\n\t"                                                           \
+    "s_cmp_eq_u32 s45, s42\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfh_ins_%=\n\t"                                                             \
+    "v_readfirstlane_b32 s45, v120\n\t"                                                           \
+    "s_cmp_eq_u32 s45, s40\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfh_rel_%=\n\t"                                                             \
+    "v_readfirstlane_b32 s45, v121\n\t"                                                           \
+    "s_cmp_lg_u32 s45, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfh_exit_%=\n\t"                                                            \
+    "s_add_u32 s56, s56, 1\n\t"                                                                   \
+    "s_cmp_gt_u32 s56, s57\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfh_exit_%=\n\t" MCS_FH_IDLE                                                \
+    "s_branch mcsfh_poll_%=\n"                                                                    \
+                                                                                                  \
+    /* ---- a post: insert the slot ---- */                                                       \
+    "mcsfh_ins_%=:\n\t"                                                                           \
+    "v_readfirstlane_b32 s48, v124\n\t" /* kx */                                                 \
+    "v_readfirstlane_b32 s46, v125\n\t" /* finish */                                             \
+    "v_readfirstlane_b32 s47, v126\n\t" /* payload */                                            \
+    "s_add_u32 s42, s42, 1\n\t"                                                                   \
+    "s_add_u32 s44, s44, 16\n\t"                                                                  \
+    "s_and_b32 s44, s44, 0x7f0\n\t"                                                               \
+    "v_add_u32 v113, s44, v109\n\t"                                                               \
+    "s_lshl2_add_u32 s49, s48, s58\n\t" /* the node's delta word */                              \
+    "v_cmp_lt_u32_e64 s[50:51], s59, v89\n\t" /* lanes with a free row */                       \
+    "v_ffbl_b32 v117, v89\n\t"                                                                    \
+    "s_ff1_i32_b64 s52, s[50:51]\n\t"                                                             \
+    "s_cmp_eq_u32 s52, -1\n\t"                                                                    \
+    "s_cbranch_scc1 mcsfh_full_%=\n\t"                                                            \
+    "v_readlane_b32 s53, v117, s52\n\t"                                                           \
+    "s_lshl_b64 exec, 1, s52\n\t"                                                                 \
+    "s_set_gpr_idx_on s53, gpr_idx(DST)\n\t"                                                      \
+    "v_mov_b32 v32, s46\n\t"                                                                      \
+    "v_mov_b32 v40, s47\n\t"                                                                      \
+    "v_mov_b32 v48, s49\n\t"                                                                      \
+    "s_set_gpr_idx_off\n\t"                                                                       \
+    "s_lshl_b32 s54, 1, s53\n\t"                                                                  \
+    "v_xor_b32 v89, s54, v89\n\t"                                                                 \
+    /* the packet: a slot at e1 joins it, an earlier one starts a new one (e1 becomes e2) */      \
+    "s_cmp_eq_u32 s46, s40\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfh_add_%=\n\t"                                                             \
+    "s_cmp_lt_u32 s46, s40\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfh_new_%=\n\t"                                                             \
+    "s_min_u32 s41, s41, s46\n\t"                                                                 \
+    "s_branch mcsfh_pub_%=\n"                                                                     \
+    "mcsfh_new_%=:\n\t"                                                                           \
+    "s_mov_b32 s41, s40\n\t"                                                                      \
+    "s_mov_b32 s40, s46\n\t"                                                                      \
+    "s_and_b32 s43, s43, 0x80000000\n\t"                                                          \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "ds_write2st64_b32 v114, v112, v112 offset1:1\n\t"                                            \
+    "ds_write2st64_b32 v114, v112, v112 offset0:2 offset1:3\n\t"                                  \
+    "s_lshl_b64 exec, 1, s52\n"                                                                   \
+    "mcsfh_add_%=:\n\t" /* (exec = the slot's lane) */                                           \
+    "v_mov_b32 v120, s49\n\t"                                                                     \
+    "v_mov_b32 v121, s47\n\t"                                                                     \
+    "ds_add_u32 v120, v121\n\t"                                                                   \
+    "s_add_u32 s43, s43, 1\n"                                                                     \
+    "mcsfh_pub_%=:\n\t"                                                                           \
+    "s_mov_b64 exec, 1\n\t"                                                                       \
+    "v_mov_b32 v120, s40\n\t"                                                                     \
+    "v_mov_b32 v121, s41\n\t"                                                                     \
+    "v_mov_b32 v122, s42\n\t"                                                                     \
+    "v_mov_b32 v123, s43\n\t"                                                                     \
+    "ds_write_b128 v115, v[120:123]\n\t"                                                          \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "s_branch mcsfh_poll_%=\n"                                                                    \
+    "mcsfh_full_%=:\n\t" /* no free slot: the decision wave stops as a pool overflow */          \
+    "s_bitset1_b32 s43, 31\n\t"                                                                   \
+    "s_branch mcsfh_pub_%=\n"                                                                     \
+                                                                                                  \
+    /* ---- an ack of e1: free e1's slots, build the packet of the next finish second ---- */     \
+    "mcsfh_rel_%=:\n\t"                                                                           \
+    "ds_write2st64_b32 v114, v112, v112 offset1:1\n\t"                                            \
+    "ds_write2st64_b32 v114, v112, v112 offset0:2 offset1:3\n\t" MCS_FH_CMP("s40")                \
+    MCS_FH_FREE(0, "s[60:61]", "v32") MCS_FH_FREE(1, "s[62:63]", "v33")                           \
+    MCS_FH_FREE(2, "s[64:65]", "v34") MCS_FH_FREE(3, "s[66:67]", "v35")                           \
+    MCS_FH_FREE(4, "s[68:69]", "v36") MCS_FH_FREE(5, "s[70:71]", "v37")                           \
+    MCS_FH_FREE(6, "s[72:73]", "v38") MCS_FH_FREE(7, "s[74:75]", "v39")                           \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "s_mov_b32 s40, s41\n\t"                                                                      \
+    "s_and_b32 s43, s43, 0x80000000\n\t"                                                          \
+    "s_mov_b32 s41, -1\n\t"                                                                       \
+    "s_cmp_eq_u32 s40, -1\n\t"                                                                    \
+    "s_cbranch_scc1 mcsfh_pub_%=\n\t" MCS_FH_CMP("s40")                                           \
+    MCS_FH_ADD(0, "s[60:61]", "v40", "v48") MCS_FH_ADD(1, "s[62:63]", "v41", "v49")               \
+    MCS_FH_ADD(2, "s[64:65]", "v42", "v50") MCS_FH_ADD(3, "s[66:67]", "v43", "v51")               \
+    MCS_FH_ADD(4, "s[68:69]", "v44", "v52") MCS_FH_ADD(5, "s[70:71]", "v45", "v53")               \
+    MCS_FH_ADD(6, "s[72:73]", "v46", "v54") MCS_FH_ADD(7, "s[74:75]", "v47", "v55")               \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    /* e2: the earliest finish after e1 (f - (e1 + 1) wraps for e1's own slots and free rows) */  \
+    "s_add_u32 s55, s40, 1\n\t"                                                                   \
+    "v_subrev_u32 v120, s55, v32\n\t"                                                             \
+    "v_subrev_u32 v121, s55, v33\n\t"                                                             \
+    "v_subrev_u32 v122, s55, v34\n\t"                                                             \
+    "v_subrev_u32 v123, s55, v35\n\t"                                                             \
+    "v_subrev_u32 v124, s55, v36\n\t"                                                             \
+    "v_subrev_u32 v125, s55, v37\n\t"                                                             \
+    "v_subrev_u32 v126, s55, v38\n\t"                                                             \
+    "v_subrev_u32 v127, s55, v39\n\t"                                                             \
+    "v_min3_u32 v120, v120, v121, v122\n\t"                                                       \
+    "v_min3_u32 v123, v123, v124, v125\n\t"                                                       \
+    "v_min3_u32 v120, v120, v126, v127\n\t"                                                       \
+    "v_min_u32 v120, v120, v123\n\t"                                                              \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"                  \
+    "s_nop 1\n\t"                                                                                 \
+    "v_min_u32_dpp v120, v120, v120 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"                  \
+    "s_nop 1\n\t"                                                                                 \
+    "v_readlane_b32 s41, v120, 63\n\t"                                                            \
+    "s_add_u32 s41, s41, s55\n\t"                                                                 \
+    "s_branch mcsfh_pub_%=\n"                                                                     \
+    "mcsfh_exit_%=:\n\t"                                                                          \
+    "s_waitcnt lgkmcnt(0)"
+#define MCS_FH_CLOBBERS                                                                           \
+    "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53",  \
+        "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66",     \
+        "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "v32", "v33", "v34", "v35",     \
+        "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48",     \
+        "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v89", "v109", "v111", "v112", "v113",        \
+        "v114", "v115", "v117", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "vcc", \
+        "scc", "exec", "memory"
+
+// (probe builds: the decision wave's header re-reads in s85 (MCS_STAMPS); an idle poll of the
+// release wave sleeps (MCS_FH_SLEEP, an A/B of its issue pressure))
+#ifdef MCS_STAMPS
+#define MCS_FD_SPIN "s_add_u32 s85, s85, 1\n\t"
+#define MCS_FD_SPIN0 "s_mov_b32 s85, 0\n\t"
+#else
+#define MCS_FD_SPIN ""
+#define MCS_FD_SPIN0 ""
+#endif
+#ifdef MCS_FH_SLEEP
+#define MCS_FH_IDLE "s_sleep " MCS_FH_SLEEP "\n\t"
+#else
+#define MCS_FH_IDLE ""
+#endif
+
 // ---- MCS_STAMPS probe build (tools/stamp_fa.py): s_memtime cycles per loop segment ------------------
 // s[92:93] segment start, s94 releases, s95 failed fits, s96 batch ends, s97 the whole loop; each
 // stamp waits for its own SMEM read (lgkmcnt, which also drains LDS): read the shares, not the time

@@ -50,7 +50,7 @@ namespace mcs {
 namespace {
 
 #ifdef MCS_STAMPS
-__device__ unsigned long long g_fa_stamps[4];
+__device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-reads
 #endif
 
 #include "mcs_fa_macros.h"
@@ -171,24 +171,7 @@ __device__ unsigned long long g_fa_stamps[4];
     /* release every running job with finish <= t (cluster.go:153-157) */                        \
     MCS_FA_CNTR_##D MCS_FA_T0                                                                     \
     "s_max_u32 s81, s81, s80\n\t" /* peak: used only grows between releases */                   \
-    "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN##W                                                   \
-    /* the wave's earliest remaining finish (DPP minimum of v90) under the reload's latency */   \
-    "v_mov_b32 v120, v90\n\t"                                                                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_min_u32_dpp v120, v120, v120 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_min_u32_dpp v120, v120, v120 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_min_u32_dpp v120, v120, v120 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_min_u32_dpp v120, v120, v120 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_min_u32_dpp v120, v120, v120 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"                  \
-    "s_nop 1\n\t"                                                                                 \
-    "v_min_u32_dpp v120, v120, v120 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"                  \
-    "s_nop 1\n\t"                                                                                 \
-    "v_readlane_b32 s77, v120, 63\n\t"                                                            \
-    "s_waitcnt lgkmcnt(0)\n\t" MCS_FA_T1("s94")                                                   \
+    "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN##W MCS_FA_SCANEND##W MCS_FA_T1("s94")                \
     "s_branch mcsfa_loopend_%=\n"                                                                 \
                                                                                                   \
     "mcsfa_deadlock_%=:\n\t"                                                                      \
@@ -206,7 +189,7 @@ __device__ unsigned long long g_fa_stamps[4];
     "mcsfa_bend_%=:\n\t" MCS_FA_T0                                                               \
     "s_max_u32 s81, s81, s80\n\t"                                                                 \
     "s_cmp_gt_u32 s81, " MCS_FA_POOLMAX##W "\n\t"                                                 \
-    "s_cbranch_scc1 mcsfa_poolovf_%=\n\t"                                                         \
+    "s_cbranch_scc1 mcsfa_poolovf_%=\n\t" MCS_FA_BENDCHK##W                                       \
     "s_add_u32 s76, s57, s47\n\t"                                                                 \
     "s_cmp_ge_u32 s76, s42\n\t"                                                                   \
     "s_cbranch_scc1 mcsfa_exit_%=\n\t"                                                            \
@@ -314,6 +297,58 @@ __device__ unsigned long long g_fa_stamps[4];
     "s_nop 1"
 #define MCS_FA_LOOP_F(W, D) MCS_FA_ENTRY_F(W) MCS_FA_BODY(W, D, F) MCS_FA_EXIT_F
 
+// The end of a run, shared by the loop kernels: the batch holding the last decision (earlier ones
+// are stored in the loop), the undecided rows after a deadlock or a clock overflow, and the
+// cluster's statistics.  A peak above the pool means a skipped insert: the engine re-runs the
+// cluster with a larger pool.
+template <int NPL, int P>
+__device__ __forceinline__ void fa_finish(const FifoArgs& a, uint32_t ci, uint32_t lane, uint32_t J, uint32_t t,
+                                          uint32_t r, uint32_t flags, uint32_t waited, uint32_t peak,
+                                          uint32_t n_slow, uint32_t n_rel, uint32_t on, uint32_t os, uint32_t of,
+                                          int32_t* o_node, uint32_t* o_start, uint32_t* o_finish) {
+    if (peak > (uint32_t)(P * kWave)) flags |= MCS_FLAG_OVERFLOW;
+    const uint32_t placed = r;  // FIFO places every job it decides, in order
+    if (!(flags & MCS_FLAG_OVERFLOW)) {
+        if (r > 0u) {  // the batch holding the last decision (earlier ones are stored)
+            const uint32_t i = ((r - 1u) & ~63u) + lane;
+            if (i < r) {
+                o_node[i] = (int32_t)(NPL == 1 ? on : (on & 63u) * NPL + (on >> 6));
+                o_start[i] = os;
+                o_finish[i] = of;
+            }
+        }
+        if (flags & (MCS_FLAG_DEADLOCK | MCS_FLAG_CLOCK_OVERFLOW)) {
+            for (uint32_t i = r + lane; i < J; i += kWave) {
+                o_node[i] = MCS_NODE_UNPLACED;
+                o_start[i] = MCS_TIME_NONE;
+                o_finish[i] = MCS_TIME_NONE;
+            }
+        }
+    }
+
+    if (lane == 0) {
+        mcs_cluster_stats st;
+        st.t_end = t;
+        st.placed = placed;
+        st.waited = waited;
+        st.peak_running = peak;
+        st.flags = flags;
+        st.pool = (uint32_t)P;
+        st.iterations = n_slow + r;  // passes: one per decision, plus the clock advances
+        st.release_scans = n_rel;
+        a.cstats[ci] = st;
+        if (flags & MCS_FLAG_OVERFLOW) {
+            atomicAdd(&a.totals->overflowed, 1u);
+        } else {
+            atomicAdd(&a.totals->placed, (unsigned long long)placed);
+            atomicAdd(&a.totals->waited, (unsigned long long)waited);
+            atomicAdd(&a.totals->unplaced, (unsigned long long)(J - placed));
+            if (flags & MCS_FLAG_DEADLOCK) atomicAdd(&a.totals->deadlocked, 1u);
+            if (flags & MCS_FLAG_CLOCK_OVERFLOW) atomicAdd(&a.totals->clock_overflowed, 1u);
+        }
+    }
+}
+
 // Node format W (32 or 16 bits per field); LDS: nodes [4][64] (u64 / u32 words) at 0, slot
 // payloads [8][64] (u64 / u32 in a u64 stride) at 2048, slot {node address | finish << 32}
 // [8][64] at 6144 (the offsets in the asm)
@@ -414,7 +449,6 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
 #undef MCS_FA_OPERANDS
 #pragma clang diagnostic pop
 
-    if (peak > (uint32_t)(P * kWave)) flags |= MCS_FLAG_OVERFLOW;  // a skipped insert
 #ifdef MCS_STAMPS
     if (lane == 0) {
         atomicAdd(&g_fa_stamps[0], (unsigned long long)st0);
@@ -423,46 +457,7 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
         atomicAdd(&g_fa_stamps[3], (unsigned long long)st3);
     }
 #endif
-    const uint32_t placed = r;  // FIFO places every job it decides, in order
-    if (!(flags & MCS_FLAG_OVERFLOW)) {
-        if (r > 0u) {  // the batch holding the last decision (earlier ones are stored)
-            const uint32_t i = ((r - 1u) & ~63u) + lane;
-            if (i < r) {
-                o_node[i] = (int32_t)(NPL == 1 ? on : (on & 63u) * NPL + (on >> 6));
-                o_start[i] = os;
-                o_finish[i] = of;
-            }
-        }
-        if (flags & (MCS_FLAG_DEADLOCK | MCS_FLAG_CLOCK_OVERFLOW)) {
-            for (uint32_t i = r + lane; i < J; i += kWave) {
-                o_node[i] = MCS_NODE_UNPLACED;
-                o_start[i] = MCS_TIME_NONE;
-                o_finish[i] = MCS_TIME_NONE;
-            }
-        }
-    }
-
-    if (lane == 0) {
-        mcs_cluster_stats st;
-        st.t_end = t;
-        st.placed = placed;
-        st.waited = waited;
-        st.peak_running = peak;
-        st.flags = flags;
-        st.pool = (uint32_t)P;
-        st.iterations = n_slow + r;  // passes: one per decision, plus the clock advances
-        st.release_scans = n_rel;
-        a.cstats[ci] = st;
-        if (flags & MCS_FLAG_OVERFLOW) {
-            atomicAdd(&a.totals->overflowed, 1u);
-        } else {
-            atomicAdd(&a.totals->placed, (unsigned long long)placed);
-            atomicAdd(&a.totals->waited, (unsigned long long)waited);
-            atomicAdd(&a.totals->unplaced, (unsigned long long)(J - placed));
-            if (flags & MCS_FLAG_DEADLOCK) atomicAdd(&a.totals->deadlocked, 1u);
-            if (flags & MCS_FLAG_CLOCK_OVERFLOW) atomicAdd(&a.totals->clock_overflowed, 1u);
-        }
-    }
+    fa_finish<NPL, P>(a, ci, lane, J, t, r, flags, waited, peak, n_slow, n_rel, on, os, of, o_node, o_start, o_finish);
 }
 
 typedef uint32_t mcs_u32x8 __attribute__((ext_vector_type(8)));
@@ -556,52 +551,155 @@ __global__ __launch_bounds__(64) void fifo_asm_fused_kernel(FifoArgs a) {
 
     const uint32_t r = cb + cursor;
     peak = peak > used ? peak : used;
-    if (peak > (uint32_t)(P * kWave)) flags |= MCS_FLAG_OVERFLOW;  // a skipped insert
-    const uint32_t placed = r;
-    if (!(flags & MCS_FLAG_OVERFLOW)) {
-        if (r > 0u) {  // the batch holding the last decision (earlier ones are stored)
-            const uint32_t i = ((r - 1u) & ~63u) + lane;
-            if (i < r) {
-                o_node[i] = (int32_t)(NPL == 1 ? on : (on & 63u) * NPL + (on >> 6));
-                o_start[i] = os;
-                o_finish[i] = of;
+    fa_finish<NPL, P>(a, ci, lane, J, t, r, flags, waited, peak, n_slow, n_rel, on, os, of, o_node, o_start, o_finish);
+}
+
+// ---- the duo loop: a decision wave and a release wave per cluster (low occupancy) -----------------
+// Under strong sharding a GPU holds few clusters (512 of C4's 4096 at N = 8: two waves per CU), so
+// each cluster's decision chain runs alone on its SIMD and the release scans (8 slot rows, the
+// payload adds, a node reload and a wave minimum: ~35 % of a lone wave's cycles) sit on that chain.
+// Here a second wave of the workgroup, on an otherwise idle SIMD, holds the running slots and keeps
+// the release of the next finish second ready as a packet (MCS_FH_LOOP); the decision wave
+// (MCS_FA_LOOP(16D)) posts each commit to it and applies a packet with four packed adds.  Same
+// decisions and results as W16R, bit for bit.
+struct DuoLds {
+    uint32_t ring[128][4];  // posts {kx, finish, payload, seq}
+    uint32_t hdr[4];        // {e1, e2, posts taken, slots at e1 (bit 31: overflow)}
+    uint32_t ack, done, pad[2];
+    uint32_t delta[4 * kWave];  // the packet: released {cores | mem << 16} per node, [chunk][lane]
+    uint32_t nodes[4 * kWave];  // the node words, read once by the decision wave
+};
+
+template <bool DIAG>
+__global__ __launch_bounds__(2 * kWave) void fifo_duo_kernel(FifoArgs a) {
+    const uint32_t item = blockIdx.x;
+    const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
+    const uint32_t lane = threadIdx.x & (kWave - 1u), wave = threadIdx.x / kWave;
+    __shared__ DuoLds L;
+
+    constexpr uint32_t kGuard = 0x8000u, kClamp = kGuard - 1u;
+    const uint32_t n0 = a.node_off[ci];
+    const uint32_t N = a.node_off[ci + 1] - n0;
+    const uint64_t j0 = a.job_off[ci];
+    const uint32_t J = (uint32_t)(a.job_off[ci + 1] - j0);
+    if (wave == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t node = lane * 4u + c;
+            uint2 v = make_uint2(kClamp, kClamp);  // padding: never fits
+            if (node < N) {
+                v = a.node_free0[n0 + node];
+                v.x += kGuard;
+                v.y += kGuard;
             }
+            L.nodes[c * kWave + lane] = v.x | (v.y << 16);
+            L.delta[c * kWave + lane] = 0u;
         }
-        if (flags & (MCS_FLAG_DEADLOCK | MCS_FLAG_CLOCK_OVERFLOW)) {
-            for (uint32_t i = r + lane; i < J; i += kWave) {
-                o_node[i] = MCS_NODE_UNPLACED;
-                o_start[i] = MCS_TIME_NONE;
-                o_finish[i] = MCS_TIME_NONE;
-            }
+    } else {
+        L.ring[lane][3] = kEmpty;  // (no post has this seq yet)
+        L.ring[lane + kWave][3] = kEmpty;
+        if (lane == 0) {
+            L.hdr[0] = kEmpty;
+            L.hdr[1] = kEmpty;
+            L.hdr[2] = 0u;
+            L.hdr[3] = 0u;
+            L.ack = 0u;  // (finish seconds are >= 1)
+            L.done = 0u;
         }
+    }
+    __syncthreads();
+    const uint32_t rb = lds_addr(&L.ring[0][0]);
+    const uint32_t hb = lds_addr(&L.hdr[0]);
+    const uint32_t dl = lds_addr(&L.delta[0]) + lane * 4u;
+
+    if (wave == 1) {
+        // the release wave: polls until the decision wave is done (bounded: 64 polls per job)
+        const uint64_t pb = 64ull * J + (1ull << 20);
+        const uint32_t hbound = pb > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)pb;
+        const uint32_t db = lds_addr(&L.delta[0]);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+        asm volatile(MCS_FH_LOOP
+                     :
+                     : [hb] "s"(hbound), [db] "s"(db), [rb] "v"(rb), [dl] "v"(dl), [hdr] "v"(hb)
+                     : MCS_FH_CLOBBERS);
+#pragma clang diagnostic pop
+        return;
     }
 
+    const uint4* jobs = a.jobs + j0;
+    int32_t* o_node = a.out_node + j0;
+    uint32_t* o_start = a.out_start + j0;
+    uint32_t* o_finish = a.out_finish + j0;
+    uint4 cur = jobs[lane];  // batch 0 (the array has kJobPad records of slack)
+    cur.z = cur.z < kClamp ? cur.z : kClamp;
+    cur.w = cur.w < kClamp ? cur.w : kClamp;
+    cur.z |= cur.w << 16;
+
+    const uint32_t v_pay = 0u;  // (no LDS slot rows)
+    const uint32_t v_nb = lds_addr(&L.nodes[0]) + lane * 4u;
+    const uint32_t v_nbase = rb;  // (v109: the ring base)
+    const uint32_t sel0 = 0x0b0a0908u, sel1 = 0u;
+
+    uint32_t t = 0, r = 0, flags = 0, have_w = 0;
+    uint32_t frm = 0u, lmin = kEmpty;
+    uint32_t used = 0, peak = 0, waited = 0, n_slow = 0, n_rel = 0;
+    uint32_t on = 0, os = 0, of = 0;
+#ifdef MCS_STAMPS
+    uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0, spins = 0;
+#define MCS_FD_STAMP_OUTS MCS_FA_STAMP_OUTS, [spins] "=s"(spins)
+#define MCS_FD_SPINOUT "\n\ts_mov_b32 %[spins], s85"
+#else
+#define MCS_FD_STAMP_OUTS
+#define MCS_FD_SPINOUT ""
+#endif
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+    if constexpr (DIAG)
+        asm volatile(MCS_FA_LOOP(16D, D1) MCS_FD_SPINOUT
+                     : [t] "+s"(t), [r] "+s"(r), [flags] "+s"(flags), [hw] "+s"(have_w), [used] "+s"(used),
+                       [peak] "+s"(peak), [waited] "+s"(waited), [nslow] "+s"(n_slow), [nrel] "+s"(n_rel),
+                       [on] "+v"(on), [os] "+v"(os), [of] "+v"(of), [frm] "+v"(frm), [lmin] "+v"(lmin)
+                       MCS_FD_STAMP_OUTS
+                     : [J] "s"(J), [jobs] "s"(jobs), [onp] "s"(o_node), [osp] "s"(o_start), [ofp] "s"(o_finish),
+                       [c0] "v"(cur.x), [c1] "v"(cur.y), [c2] "v"(cur.z), [c3] "v"(cur.w), [pay] "v"(v_pay),
+                       [nb] "v"(v_nb), [nbase] "v"(v_nbase), [lane] "v"(lane), [sel0] "s"(sel0),
+                       [sel1] "s"(sel1), [dl] "v"(dl), [hdr] "v"(hb), [fdl] "i"(MCS_FLAG_DEADLOCK),
+                       [fck] "i"(MCS_FLAG_CLOCK_OVERFLOW), [fov] "i"(MCS_FLAG_OVERFLOW)
+                     : MCS_FD_CLOBBERS);
+    else
+        asm volatile(MCS_FA_LOOP(16D, D0) MCS_FD_SPINOUT
+                     : [t] "+s"(t), [r] "+s"(r), [flags] "+s"(flags), [hw] "+s"(have_w), [used] "+s"(used),
+                       [peak] "+s"(peak), [waited] "+s"(waited), [nslow] "+s"(n_slow), [nrel] "+s"(n_rel),
+                       [on] "+v"(on), [os] "+v"(os), [of] "+v"(of), [frm] "+v"(frm), [lmin] "+v"(lmin)
+                       MCS_FD_STAMP_OUTS
+                     : [J] "s"(J), [jobs] "s"(jobs), [onp] "s"(o_node), [osp] "s"(o_start), [ofp] "s"(o_finish),
+                       [c0] "v"(cur.x), [c1] "v"(cur.y), [c2] "v"(cur.z), [c3] "v"(cur.w), [pay] "v"(v_pay),
+                       [nb] "v"(v_nb), [nbase] "v"(v_nbase), [lane] "v"(lane), [sel0] "s"(sel0),
+                       [sel1] "s"(sel1), [dl] "v"(dl), [hdr] "v"(hb), [fdl] "i"(MCS_FLAG_DEADLOCK),
+                       [fck] "i"(MCS_FLAG_CLOCK_OVERFLOW), [fov] "i"(MCS_FLAG_OVERFLOW)
+                     : MCS_FD_CLOBBERS);
+#pragma clang diagnostic pop
+    // the release wave stops polling
+    if (lane == 0) __hip_atomic_store(&L.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef MCS_STAMPS
     if (lane == 0) {
-        mcs_cluster_stats st;
-        st.t_end = t;
-        st.placed = placed;
-        st.waited = waited;
-        st.peak_running = peak;
-        st.flags = flags;
-        st.pool = (uint32_t)P;
-        st.iterations = n_slow + r;
-        st.release_scans = n_rel;
-        a.cstats[ci] = st;
-        if (flags & MCS_FLAG_OVERFLOW) {
-            atomicAdd(&a.totals->overflowed, 1u);
-        } else {
-            atomicAdd(&a.totals->placed, (unsigned long long)placed);
-            atomicAdd(&a.totals->waited, (unsigned long long)waited);
-            atomicAdd(&a.totals->unplaced, (unsigned long long)(J - placed));
-            if (flags & MCS_FLAG_DEADLOCK) atomicAdd(&a.totals->deadlocked, 1u);
-            if (flags & MCS_FLAG_CLOCK_OVERFLOW) atomicAdd(&a.totals->clock_overflowed, 1u);
-        }
+        atomicAdd(&g_fa_stamps[0], (unsigned long long)st0);
+        atomicAdd(&g_fa_stamps[1], (unsigned long long)st1);
+        atomicAdd(&g_fa_stamps[2], (unsigned long long)st2);
+        atomicAdd(&g_fa_stamps[3], (unsigned long long)st3);
+        atomicAdd(&g_fa_stamps[4], (unsigned long long)spins);
     }
+#endif
+#undef MCS_FD_STAMP_OUTS
+#undef MCS_FD_SPINOUT
+    fa_finish<4, 8>(a, ci, lane, J, t, r, flags, waited, peak, n_slow, n_rel, on, os, of, o_node, o_start, o_finish);
 }
 
 }  // namespace
 
-// Form codes: 17 = W16R and 18 = W16S (where the 16-bit format fits), 16 = W16 with LDS slots,
+// Form codes: 21 = W16R's duo loop (a decision and a release wave per cluster, small grids),
+// 17 = W16R and 18 = W16S (where the 16-bit format fits), 16 = W16 with LDS slots,
 // 32 = W32, 19 / 20 = W16R / W16S on a fused job stream, 0 = the compiled kernel.  MCS_FIFO_ASM=0
 // turns the hand-scheduled loop off, =16 / =32 force a form (A/B timing, the variant tests; neither
 // has a small-cluster shape nor a fused one).
@@ -622,7 +720,14 @@ int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor) {
     if (npl != 4 || pool != 8) return 0;
     // register slots: one LDS round trip per release instead of 2 + rows; measured faster than LDS
     // slots at every occupancy from 1 to 16 cluster waves per CU
-    if ((a.guard_ok & 2u) && want != 32) return want == 16 ? 16 : 17;
+    if ((a.guard_ok & 2u) && want != 32) {
+        if (want == 16) return 16;
+        // small grids (a strong shard: at most 4 cluster waves per CU) run the duo loop, whose
+        // release wave takes an otherwise idle SIMD; MCS_FIFO_DUO=0|1 forces either
+        const char* duo = getenv("MCS_FIFO_DUO");
+        const bool d = duo ? atoi(duo) != 0 : a.n_items <= kDuoMaxItems;
+        return d ? 21 : 17;
+    }
     return (a.guard_ok & 1u) ? 32 : 0;
 }
 
@@ -636,6 +741,7 @@ static hipError_t launch_form(const FifoArgs& a, int form, hipStream_t s) {
         case 20: hipLaunchKernelGGL((fifo_asm_fused_kernel<1, 2, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 19: hipLaunchKernelGGL((fifo_asm_fused_kernel<4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 18: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 1, 2, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
+        case 21: hipLaunchKernelGGL((fifo_duo_kernel<DIAG>), dim3(a.n_items), dim3(2 * kWave), 0, s, a); break;
         case 17: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 16: hipLaunchKernelGGL((fifo_asm_kernel<16, false, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 32: hipLaunchKernelGGL((fifo_asm_kernel<32, false, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
@@ -658,7 +764,7 @@ hipError_t launch_fifo_asm(const FifoArgs& a, int npl, int pool, hipStream_t s) 
 // the probe build's segment cycles (releases, failed fits, batch ends, whole loop), summed over the
 // clusters of the launches since the last call; read and reset
 extern "C" int mcs_debug_fa_stamps(unsigned long long* out) {
-    unsigned long long z[4] = {0, 0, 0, 0};
+    unsigned long long z[5] = {0, 0, 0, 0, 0};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_fa_stamps), sizeof(z)) != hipSuccess) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_fa_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }

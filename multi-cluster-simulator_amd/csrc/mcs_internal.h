@@ -18,6 +18,9 @@ constexpr int kWave = 64;
 constexpr int kMaxNpl = 16;   // nodes per lane -> at most 1024 nodes per cluster in ABI v1
 constexpr int kMaxPool = 32;  // running-slot registers per lane -> 2048 slots per cluster
 constexpr uint32_t kAsmMaxJobs = (1u << 28) - 128u;  // hand-scheduled loop: 32-bit record offsets
+// grids up to this many clusters would pick the duo loop by default: none (measured 1.5x slower than
+// W16R at 512-2048 clusters; MCS_FIFO_DUO=1 runs it)
+constexpr uint32_t kDuoMaxItems = 0u;
 constexpr uint32_t kJobPad = 128;  // records of slack after the job array (unmasked batch loads)
 
 struct Totals {  // device-side accumulation of mcs_stats (only clusters that did not overflow)

@@ -18,6 +18,17 @@ pytestmark = pytest.mark.gpu
 KATS = load_kats()
 
 
+
+W16R = "mcs::fifo_asm_kernel<16, true, 4, 8>"
+DUO = "mcs::fifo_duo_kernel"
+
+
+def w16r_form(n_clusters):
+    """The kernel the engine picks for a streamed 129-256-node launch of n_clusters in the 16-bit
+    format: W16R, or the duo loop (a decision and a release wave per cluster) under MCS_FIFO_DUO=1
+    (no grid picks it by default: kDuoMaxItems = 0)."""
+    return DUO if os.environ.get("MCS_FIFO_DUO") == "1" else W16R
+
 def run_engine(eng, arrays, streams):
     eng.load_clusters(arrays)
     eng.submit_jobs(streams)
@@ -268,7 +279,8 @@ def test_heterogeneous_cluster_sizes(engine):
 
 @pytest.mark.parametrize("sizes", [[0, 1, 5, 63, 64, 65, 130, 200, 256], [0, 1, 2, 5, 33, 63, 64]],
                          ids=["asm_4x8", "asm_1x2"])
-def test_heterogeneous_cluster_sizes_hand_scheduled(engine, sizes):
+@pytest.mark.parametrize("duo", ["0", "1"])
+def test_heterogeneous_cluster_sizes_hand_scheduled(engine, sizes, duo, monkeypatch):
     """Clusters of many sizes in one launch of each hand-scheduled loop shape (the largest picks it:
     129-256 nodes -> 4 chunks x 8 slot rows, <= 64 nodes -> 1 chunk x 2 rows): padding nodes, an
     empty cluster (its first job deadlocks), partial JSON availability, zero-duration jobs."""
@@ -291,17 +303,22 @@ def test_heterogeneous_cluster_sizes_hand_scheduled(engine, sizes):
     arrays = pack_clusters(clusters)
     off = np.arange(len(parts) + 1, dtype=np.uint64) * J
     s = JobStreams(*(np.concatenate([p[f] for p in parts]) for f in range(4)), off)
+    monkeypatch.setenv("MCS_FIFO_DUO", duo)
     node, start, fin, st, cs = run_engine(engine, arrays, s)
-    assert engine.last_kernel.startswith("mcs::fifo_asm_kernel<16, true")
+    if max(sizes) > 64:
+        assert engine.last_kernel == w16r_form(len(sizes))
+    else:
+        assert engine.last_kernel == "mcs::fifo_asm_kernel<16, true, 1, 2>"
     assert_parity(arrays, s, node, start, fin, cs)
     assert cs[0]["flags"] & L.MCS_FLAG_DEADLOCK  # zero nodes: the first job never fits
 
 
-@pytest.mark.parametrize("nodes", [256, 5])
-def test_hand_scheduled_diag_build(nodes):
+@pytest.mark.parametrize("nodes,duo", [(256, "0"), (256, "1"), (5, "0")])
+def test_hand_scheduled_diag_build(nodes, duo, monkeypatch):
     """MCS_FIFO_DIAG=1 launches the counting build of the hand-scheduled loop: the same placements
     and per-cluster results, plus the pass and release-scan counters (which the production build
     leaves at the decision count and 0)."""
+    monkeypatch.setenv("MCS_FIFO_DUO", duo)
     arrays, streams, _ = seeded_workload("n256" if nodes == 256 else "small", 64, 3000)
     res = {}
     for diag in ("0", "1"):
@@ -309,7 +326,7 @@ def test_hand_scheduled_diag_build(nodes):
         try:
             with Engine(0) as eng:
                 res[diag] = run_engine(eng, arrays, streams)
-                assert eng.last_kernel.startswith("mcs::fifo_asm_kernel<16, true")
+                assert eng.last_kernel == (w16r_form(64) if nodes == 256 else "mcs::fifo_asm_kernel<16, true, 1, 2>")
         finally:
             os.environ.pop("MCS_FIFO_DIAG", None)
     for i in range(3):
@@ -322,17 +339,18 @@ def test_hand_scheduled_diag_build(nodes):
     assert_parity(arrays, streams, *res["1"][:3], c1)
 
 
-@pytest.mark.parametrize("shape", ["w16s", "w16r", "w32"])
+@pytest.mark.parametrize("shape", ["w16s", "w16r", "duo", "w32"])
 @pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6])
-def test_hand_scheduled_fuzz(engine, shape, seed):
+def test_hand_scheduled_fuzz(engine, shape, seed, monkeypatch):
     """Randomised clusters and streams through each hand-scheduled loop form, bit-exact against the
     oracle: node counts across the shape's range (padding lanes and chunks), random JSON
     availability, bursts of simultaneous arrivals, zero-duration and zero-resource jobs, requests
     equal to a node's free value, and one request per cluster that fits no node (a head-of-line
     deadlock at a random point of the stream)."""
-    arrays, s = fuzz_workload(shape, seed)
+    monkeypatch.setenv("MCS_FIFO_DUO", "1" if shape == "duo" else "0")
+    arrays, s = fuzz_workload("w16r" if shape == "duo" else shape, seed)
     node, start, fin, st, cs = run_engine(engine, arrays, s)
-    want = {"w16s": "mcs::fifo_asm_kernel<16, true, 1, 2>", "w16r": "mcs::fifo_asm_kernel<16, true, 4, 8>",
+    want = {"w16s": "mcs::fifo_asm_kernel<16, true, 1, 2>", "w16r": W16R, "duo": DUO,
             "w32": "mcs::fifo_asm_kernel<32, false, 4, 8>"}[shape]
     if st.escalations == 0:
         assert engine.last_kernel == want
@@ -441,7 +459,7 @@ def test_hand_scheduled_loop_field_bounds(engine, free):
     off = np.arange(len(parts) + 1, dtype=np.uint64) * J
     s = JobStreams(*(np.concatenate([p[f] for p in parts]) for f in range(4)), off)
     node, start, fin, st, cs = run_engine(engine, arrays, s)
-    assert engine.last_kernel == ("mcs::fifo_asm_kernel<16, true, 4, 8>" if free < 0x7FFF
+    assert engine.last_kernel == (w16r_form(len(clusters)) if free < 0x7FFF
                                   else "mcs::fifo_asm_kernel<32, false, 4, 8>")
     assert_parity(arrays, s, node, start, fin, cs)
     assert (cs["flags"] & L.MCS_FLAG_DEADLOCK).all()  # every cluster's last request fits nowhere
@@ -468,13 +486,15 @@ def test_every_kernel_variant(policy):
             # clusters), with LDS slots (MCS_FIFO_ASM=16) and its 32-bit one (=32; =0 turns the loop
             # off), and the compiled kernel's two (the low-occupancy one is picked for small grids;
             # MCS_FIFO_LAT forces either)
-            for fused, lat, asm in ((False, "1", "0"), (False, "0", "0"), (False, None, "1"),
-                                    (False, None, "16"), (False, None, "32"), (True, None, None)):
+            # (and the duo loop, MCS_FIFO_DUO=1, the register-slot form's two-wave variant)
+            for fused, lat, asm, duo in ((False, "1", "0", None), (False, "0", "0", None), (False, None, "1", "0"),
+                                         (False, None, "1", "1"), (False, None, "16", None),
+                                         (False, None, "32", None), (True, None, None, None)):
                 if policy == "DELAY" and lat == "0":
                     continue
                 if policy == "DELAY" and asm in ("1", "16", "32"):
                     continue
-                env = {"MCS_FIFO_LAT": lat, "MCS_FIFO_ASM": asm}
+                env = {"MCS_FIFO_LAT": lat, "MCS_FIFO_ASM": asm, "MCS_FIFO_DUO": duo}
                 old = {k: os.environ.get(k) for k in env}
                 for k, v in env.items():
                     if v is not None:
@@ -492,7 +512,7 @@ def test_every_kernel_variant(policy):
                             os.environ.pop(k, None)
                         else:
                             os.environ[k] = v
-                tag = f"nodes {nn} pool {pool} fused {fused} lat {lat} asm {asm}"
+                tag = f"nodes {nn} pool {pool} fused {fused} lat {lat} asm {asm} duo {duo}"
                 np.testing.assert_array_equal(node, oracle[0], err_msg=tag)
                 np.testing.assert_array_equal(start, oracle[1], err_msg=tag)
                 np.testing.assert_array_equal(fin, oracle[2], err_msg=tag)

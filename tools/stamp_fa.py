@@ -21,7 +21,7 @@ eng = Engine(0, policy="FIFO")
 eng.load_clusters(replicate(uniform_cluster(256), nc))
 eng.generate_jobs(GenParams(arrival_mode=1, lam=scaled_lambda(256, load=0.9)), 16384)
 fn = L.lib().mcs_debug_fa_stamps
-buf = (C.c_ulonglong * 4)()
+buf = (C.c_ulonglong * 5)()
 eng.run(); fn(buf)
 st = eng.run(); assert fn(buf) == 0
 cs = eng.cluster_stats()
@@ -37,11 +37,12 @@ for nc in (sys.argv[2:] or ["256", "512", "1024", "4096"]):
         sys.exit(1)
     d = json.loads(out.stdout.strip().splitlines()[-1])
     J = d["jobs"]
-    rel, nofit, bend, tot = (x / J for x in d["s"])
+    rel, nofit, bend, tot = (x / J for x in d["s"][:4])
     rest = tot - rel - nofit - bend
     print(json.dumps({"clusters": int(nc), "kernel_ms": round(d["ms"], 3), "kernel": d["kernel"],
                       "cycles_per_job": {"total": round(tot, 1), "release": round(rel, 1), "nofit": round(nofit, 1),
                                          "batch_end": round(bend, 1), "decide_and_arrive": round(rest, 1)},
                       "release_scans_per_job": round(d["rel"] / J, 4),
                       "cycles_per_release": round(rel * J / max(d["rel"], 1), 1),
-                      "passes_per_job": round(d["passes"] / J, 4)}), flush=True)
+                      "passes_per_job": round(d["passes"] / J, 4),
+                      "duo_header_rereads_per_job": round(d["s"][4] / J, 4)}), flush=True)
