@@ -268,7 +268,8 @@ def main_c5_delay(args, world, rank, local_rank):
                                   "exchange in HBM")
                                + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "RCCL eager" if ts["loop_form"] == 1
                                                     else "RCCL captured in a hipGraph" if ts["loop_form"] == 2
-                                                    else "resident in one workgroup") + ")",
+                                                    else "resident in one workgroup" if ts["loop_form"] == 3
+                                                    else "resident, one workgroup per 16 clusters") + ")",
             },
             "roofline": {
                 "bound": "hbm",
@@ -375,7 +376,8 @@ def main_c5(args, world, rank, local_rank):
                 "parallelism": (f"{world} shard(s); per-tick RCCL all-gather" if dist_on or args.comm else "1 GPU, exchange in HBM")
                                + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "RCCL eager" if ts["loop_form"] == 1
                                                     else "RCCL captured in a hipGraph" if ts["loop_form"] == 2
-                                                    else "resident in one workgroup") + ")",
+                                                    else "resident in one workgroup" if ts["loop_form"] == 3
+                                                    else "resident, one workgroup per 16 clusters") + ")",
             },
             "roofline": {
                 "bound": "hbm",

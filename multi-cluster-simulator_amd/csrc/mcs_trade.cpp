@@ -28,6 +28,7 @@ struct TradeDev {
     unsigned long long* scm = nullptr;
     TrLq* lq = nullptr;
     unsigned char* xb = nullptr;
+    unsigned long long* gx = nullptr;  // the workgroup-resident tick's granules
     uint32_t* acc = nullptr;
     uint32_t* lqp = nullptr;
     uint32_t* fb = nullptr;
@@ -60,7 +61,7 @@ uint32_t auto_slots(uint32_t max_n) {
 }
 
 // a one-engine system the resident tick kernel can hold (mcs_trade_res.hip; the LDS check is
-// resident_ok's).  Its slot finish times live in VGPRs, so such a system starts at 512 slots per
+// resident_form's).  Its slot finish times live in VGPRs, so such a system starts at 512 slots per
 // cluster (8 rows; 1024 spill): an overflow re-runs it at 1024 like any other pool overflow.
 bool resident_wanted(const mcs_engine* e) {
     const char* env = getenv("MCS_TRADE_RESIDENT");
@@ -180,21 +181,41 @@ int poll_ctl(mcs_engine* e) {
 // replayed.  MCS_TRADE_RESIDENT=0 forces the replayed kernels.
 constexpr uint32_t kResTicks = 1u << 16;
 
-bool resident_ok(mcs_engine* e, size_t* lds) {
+// MCS_TRADE_RESIDENT: 0 = the replayed kernels, 1 = one workgroup, 2 = one workgroup per 16
+// clusters (the default where the shape allows it)
+int resident_form(mcs_engine* e, size_t* lds) {
     const char* env = getenv("MCS_TRADE_RESIDENT");
-    if (env && atoi(env) == 0) return false;
-    if (!trade_resident_shape(e->td->a) || !e->sums_lt24) return false;
+    const int want = env ? atoi(env) : 2;
+    if (want == 0 || !e->sums_lt24) return 0;
     int max_lds = 0;
     if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device) != hipSuccess)
-        return false;
+        return 0;
+    if (want == 2 && trade_mw_shape(e->td->a)) {
+        *lds = trade_mw_lds(e->td->a.ns);
+        if (*lds <= (size_t)max_lds) return 2;
+    }
+    if (!trade_resident_shape(e->td->a)) return 0;
     *lds = trade_resident_lds(e->td->a.Ct, e->td->a.ns);
-    return *lds <= (size_t)max_lds;
+    return *lds <= (size_t)max_lds ? 1 : 0;
 }
 
 int run_local(mcs_engine* e) {
     TradeDev* td = e->td;
     size_t lds = 0;
-    if (resident_ok(e, &lds)) {
+    const int rf = resident_form(e, &lds);
+    if (rf == 2) {
+        td->loop_form = kLoopResidentMw;
+        if (!td->gx) HIPCHK(e, hipMalloc(&td->gx, trade_mw_granules(td->a.Ct) * 8u));
+        for (;;) {
+            const hipError_t st = launch_trade_mw(td->a, td->gx, kResTicks, lds, e->stream);
+            if (st != hipSuccess) return hip_fail(e, "resident tick kernel (workgroups)", st);
+            if (int s = poll_ctl(e)) return s;
+            if (td->h_ctl->flags & kTrFlagMwTimeout)
+                return fail(e, MCS_E_HIP, "resident tick: a workgroup exchange timed out");
+            if (td->h_ctl->done) return MCS_OK;
+        }
+    }
+    if (rf == 1) {
         td->loop_form = kLoopResident;
         for (;;) {
             const hipError_t st = launch_trade_resident(td->a, kResTicks, lds, e->stream);
@@ -333,6 +354,7 @@ void trade_free(mcs_engine* e) {
     dfree(td->scm);
     dfree(td->lq);
     dfree(td->xb);
+    dfree(td->gx);
     dfree(td->acc);
     dfree(td->lqp);
     dfree(td->fb);

@@ -137,5 +137,13 @@ constexpr uint32_t kTrResMaxClusters = 64;
 bool trade_resident_shape(const TradeArgs& a);
 size_t trade_resident_lds(uint32_t n_clusters, uint32_t ns);
 hipError_t launch_trade_resident(const TradeArgs& a, uint32_t tick_budget, size_t lds, hipStream_t s);
+// the system resident in ceil(C / 16) workgroups, one cluster per wave, records traded as tagged
+// granules (mcs_trade_mw.hip): shape check, LDS bytes, granule count, launch
+bool trade_mw_shape(const TradeArgs& a);
+size_t trade_mw_lds(uint32_t ns);
+size_t trade_mw_granules(uint32_t n_clusters);
+hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx, uint32_t tick_budget, size_t lds,
+                           hipStream_t s);
+constexpr uint32_t kTrFlagMwTimeout = 0x80000000u;  // internal: an exchange sweep gave up
 
 }  // namespace mcs

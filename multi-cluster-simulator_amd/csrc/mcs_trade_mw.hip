@@ -1,0 +1,744 @@
+// mcs_trade_mw.hip — the lock-step trading system (mcs_trade.h) resident in a few
+// workgroups that trade records through tagged granules: up to 64 clusters x 256 nodes, one
+// cluster per wave, 16 clusters per workgroup (one CU each), the whole run in one launch per
+// 64k ticks.
+//
+// The one-workgroup resident tick (mcs_trade_res.hip) holds all 64 clusters on ONE CU: four
+// clusters per wave, their slot rows copied into a working set and back around every step, and
+// the tick ran VALU-bound on that CU's four SIMDs (~24k VALU instructions per tick, PMC pass in
+// profiles/r03_res).  Here each wave owns one cluster (its slot finish times in registers, no
+// copies), so a tick's phase A runs on ceil(C / 16) CUs, and the workgroups meet twice per tick:
+//   A  each wave, its cluster: releases, arrivals, the Fifo decisions of the tick
+//      (scheduler.go:216-296), the borrow request (server.go:160-248), the utilization sample
+//      (cluster.go:46-63); it publishes the cluster's post-A record (10 words)
+//   X1 wave 0 of every workgroup gathers all records (the requests for B, the queue state and
+//      samples for C/D)
+//   B  each wave, its cluster as lender: Lend (strict '>', scheduler.go:194-202) against the
+//      tick's requests in borrower order, LentQueue appends (server.go:80-113); the workgroup's
+//      acceptances (a borrower mask) and its lenders' LentQueue lengths are published
+//   X2 wave 0 of every workgroup gathers them
+//   C+D wave 0 of EVERY workgroup, on identical inputs: the borrowers' BorrowedQueue moves (the
+//      owner workgroup writes them), the trader rounds (trader.go:280-325, 193-278;
+//      server.go:31-85) and the next tick — the trader state is replicated, so the workgroups
+//      agree on the clock without a third exchange.
+// Exchange: the data is the flag (cdna_hip_programming.md Guideline 16, R2): every word travels
+// as an 8-byte granule {value, tag} stored write-through (agent-scope atomic store) with
+// tag = the exchange's epoch within the launch (2 * tick + 1 for X1, + 2 for X2); the gathering
+// wave re-reads its granules (agent-scope atomic loads) until every tag matches.  A workgroup
+// publishes X1 of tick n + 1 only after its C/D of tick n, which needed every workgroup's X2 of
+// tick n, which each published after its own X1 sweep of tick n: so a granule is never
+// overwritten before every workgroup has read it.  The engine zeroes the granules before each
+// launch; every sweep is bounded (a timeout stops the run with an internal error).
+// Same results bit for bit as the three-kernel tick and the one-workgroup resident tick
+// (tests/test_gpu_trade.py).
+#include "mcs_trade_internal.h"
+#include "mcs_trader_dev.h"
+#include "mcs_wave.h"
+
+namespace mcs {
+namespace {
+
+constexpr int kMwWaves = 16;             // clusters per workgroup
+constexpr uint32_t kMwNodes = 256;       // nodes per cluster
+constexpr uint32_t kX1Words = 10;        // granules of a cluster's post-A record
+constexpr uint32_t kSpinLimit = 1u << 20;  // sweeps per exchange before the run gives up
+
+__device__ __forceinline__ uint32_t mw_wave_sum(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+// HBM this kernel's own workgroup wrote and reads back (slot payloads, LentQueue entries)
+__device__ __forceinline__ uint64_t mld64(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t mld32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void put_granule(unsigned long long* g, uint32_t tag, uint32_t v) {
+    __hip_atomic_store(g, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr uint32_t kStWords = sizeof(TrCluster) / 4u;
+static_assert(sizeof(TrCluster) % 4u == 0u && kStWords <= (uint32_t)kWave, "TrCluster in one VGPR");
+struct MwField {  // a TrCluster field held in lane f of a VGPR (phase A's cluster state)
+    uint32_t& v;
+    uint32_t f, lane;
+    __device__ __forceinline__ operator uint32_t() const { return readlane(v, f); }
+    __device__ __forceinline__ MwField& operator=(uint32_t x) {
+        v = lane == f ? x : v;
+        return *this;
+    }
+    __device__ __forceinline__ MwField& operator=(const MwField& o) { return *this = (uint32_t)o; }
+    __device__ __forceinline__ MwField& operator+=(uint32_t x) { return *this = (uint32_t)*this + x; }
+    __device__ __forceinline__ MwField& operator-=(uint32_t x) { return *this = (uint32_t)*this - x; }
+    __device__ __forceinline__ MwField& operator|=(uint32_t x) { return *this = (uint32_t)*this | x; }
+    __device__ __forceinline__ MwField& operator++() { return *this += 1u; }
+    __device__ __forceinline__ MwField& operator--() { return *this -= 1u; }
+    __device__ __forceinline__ uint32_t operator++(int) {
+        const uint32_t o = *this;
+        *this = o + 1u;
+        return o;
+    }
+};
+#define MST(field) (MwField{stv, (uint32_t)(offsetof(TrCluster, field) / 4u), lane})
+
+struct MwShared {  // (this workgroup's node vectors follow: kMwWaves * ns u64)
+    // gathered each tick (X1): every cluster's request and queue state
+    uint32_t rq_job[kTrResMaxClusters], rq_c[kTrResMaxClusters], rq_m[kTrResMaxClusters];
+    uint32_t rq_dur[kTrResMaxClusters];
+    uint32_t qs[kTrResMaxClusters];  // has_w | rq_busy << 1
+    uint32_t decided[kTrResMaxClusters], next_arr_t[kTrResMaxClusters], xflags[kTrResMaxClusters];
+    float cu[kTrResMaxClusters], mu[kTrResMaxClusters];
+    // constants of the run, every cluster
+    uint32_t total_c[kTrResMaxClusters], total_m[kTrResMaxClusters], J[kTrResMaxClusters];
+    unsigned long long j0[kTrResMaxClusters];
+    TrTrader trs[kTrResMaxClusters];  // replicated trader state
+    // this workgroup's clusters
+    TrCluster st[kMwWaves];
+    uint32_t capc[kMwWaves], capm[kMwWaves];
+    uint32_t gtab[kMwWaves][64];
+    uint32_t accm[2];  // borrowers some lender of this workgroup accepted this tick
+    uint32_t T, done, ticks, flags;
+    unsigned long long n_trades, n_won;
+};
+
+template <int kRows>  // slot rows per cluster (64 slots each)
+__global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, unsigned long long* gx,
+                                                                 uint32_t tick_budget) {
+    extern __shared__ unsigned long long mw_smem[];
+    MwShared& sh = *reinterpret_cast<MwShared*>(mw_smem);
+    unsigned long long* const nodes_wg = mw_smem + (sizeof(MwShared) + 7) / 8;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t C = a.Ct, ns = a.ns, S = a.S;
+    const uint32_t wg = blockIdx.x, nwg = gridDim.x;
+    const uint32_t c = wg * kMwWaves + wave;  // this wave's cluster
+    const bool own = c < C;
+    unsigned long long* const gx1 = gx;                          // [C][kX1Words]
+    unsigned long long* const gx2 = gx + (size_t)C * kX1Words;   // [C] lender words, then [nwg][2]
+
+    // ---- state in ----
+    unsigned long long* const nodes = nodes_wg + (size_t)wave * ns;
+    uint32_t N = 0, n0 = 0, J = 0;
+    uint64_t j0 = 0;
+    if (own) {
+        n0 = a.node_off[c];
+        N = a.node_off[c + 1] - n0;
+        j0 = a.job_off[c];
+        J = (uint32_t)(a.job_off[c + 1] - j0);
+        for (uint32_t i = lane; i < N; i += kWave) nodes[i] = a.tn[n0 + i];
+        if (lane < kStWords) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = reinterpret_cast<const uint32_t*>(&a.cl[c])[lane];
+        uint32_t uc = 0u, um = 0u;
+        for (uint32_t i = lane; i < N; i += kWave) {
+            const uint2 cp = a.cap[n0 + i];
+            uc += cp.x;
+            um += cp.y;
+        }
+        uc = mw_wave_sum(uc);
+        um = mw_wave_sum(um);
+        if (lane == 0) {
+            sh.capc[wave] = uc;
+            sh.capm[wave] = um;
+        }
+    }
+    for (uint32_t g = threadIdx.x; g < C; g += kMwWaves * kWave) {
+        sh.trs[g] = a.tr[g];
+        sh.total_c[g] = a.cl[g].total_c;
+        sh.total_m[g] = a.cl[g].total_m;
+        sh.j0[g] = a.job_off[g];
+        sh.J[g] = (uint32_t)(a.job_off[g + 1] - a.job_off[g]);
+    }
+    if (threadIdx.x == 0) {
+        const TrCtl ctl = *a.ctl;
+        sh.T = ctl.T;
+        sh.done = ctl.done;
+        sh.ticks = ctl.ticks;
+        sh.flags = ctl.flags;
+        sh.n_trades = ctl.n_trades;
+        sh.n_won = ctl.n_won;
+    }
+    // the wave's slot finish times in registers (row r, lane l = slot r * 64 + l)
+    uint32_t fin[kRows];
+    uint32_t frm = 0u;  // free rows of this lane
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        fin[r] = own ? a.sfin[(size_t)c * S + r * kWave + lane] : kEmpty;
+        if (fin[r] == kEmpty) frm |= 1u << r;
+    }
+    const size_t sb = (size_t)c * S;
+    const uint4* __restrict__ jobs = a.jobs + j0;
+    unsigned long long* const lent_ctr = &a.ctl->n_lent;
+    bool timed_out = false;
+    __syncthreads();
+
+    for (uint32_t it = 0; it < tick_budget; ++it) {
+        if (sh.done) break;
+        const uint32_t T = sh.T;
+        const uint32_t tag1 = 2u * it + 1u, tag2 = 2u * it + 2u;
+
+        // GetResourceUtilization runs on the ticks a trader reads it (see tr_step_kernel)
+        bool sample = false;
+        if (a.trader && T % a.sample_period == 0u) {
+            bool due = false;
+            for (uint32_t q = lane; q < C; q += kWave) due = due || sh.trs[q].next_due <= T;
+            sample = __ballot(due) != 0ull;
+        }
+
+        // ---- phase A: this wave's cluster (tr_step_kernel) ----
+        if (own) {
+            uint32_t stv = lane < kStWords ? reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane] : 0u;
+            // the tick's job records, every load in flight at once: 64 records from the WaitQueue
+            // head (else the ReadyQueue head), 64 arrival times from the first unqueued job, and
+            // the LentQueue head entry
+            const uint32_t hb = MST(has_w) ? MST(w) : MST(rq_head);
+            const uint32_t na0 = MST(next_arr);
+            const uint32_t lqh = MST(lq_head), lqn = MST(lq_len);
+            uint4 hwin = make_uint4(0u, 0u, 0u, 0u);
+            uint32_t awin = kEmpty;
+            if (hb + lane < J) hwin = jobs[hb + lane];
+            if (na0 + lane < J) awin = jobs[na0 + lane].x;
+            unsigned long long lqw = 0ull;
+            if (lqn > 0u && lane < 3u) lqw = mld64(reinterpret_cast<const unsigned long long*>(a.lq + (size_t)c * a.LQ + lqh) + lane);
+
+            // releases due at T (cluster.go:153-157), before the tick's decisions
+            if (MST(minf) <= T) {
+                constexpr int kG = kRows < 4 ? kRows : 4;
+                uint32_t lm = kEmpty, nrel = 0;
+#pragma unroll
+                for (int g = 0; g < kRows; g += kG) {
+                    uint32_t nd[kG];
+                    unsigned long long cm[kG];
+#pragma unroll
+                    for (int r = 0; r < kG; ++r) {
+                        nd[r] = kEmpty;
+                        cm[r] = 0ull;
+                        if (fin[g + r] <= T) {
+                            const uint32_t slot = (g + r) * kWave + lane;
+                            nd[r] = mld32(a.snode + sb + slot);
+                            cm[r] = mld64(a.scm + sb + slot);
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < kG; ++r) {
+                        const uint32_t f = fin[g + r];
+                        if (f <= T) {
+                            if (nd[r] < N) atomicAdd(&nodes[nd[r]], cm[r]);
+                            fin[g + r] = kEmpty;
+                            frm |= 1u << (g + r);
+                            ++nrel;
+                        } else {
+                            lm = f < lm ? f : lm;
+                        }
+                    }
+                }
+                MST(nrun) -= mw_wave_sum(nrel);
+                MST(minf) = wave_min_u32(lm);
+            }
+            // arrivals up to T join the ReadyQueue (jobs are sorted by arrival)
+            uint32_t nat;  // the arrival second of the first job not yet queued (kEmpty: none)
+            {
+                const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(awin <= T && na0 + lane < J));
+                MST(next_arr) = na0 + n;
+                if (n < (uint32_t)kWave) {
+                    nat = readlane(awin, n);
+                } else {
+                    while (MST(next_arr) < J) {
+                        const uint32_t i = MST(next_arr) + lane;
+                        const bool ok = i < J && jobs[i].x <= T;
+                        const uint32_t m = (uint32_t)__builtin_popcountll(__ballot(ok));
+                        MST(next_arr) += m;
+                        if (m < (uint32_t)kWave) break;
+                    }
+                    nat = MST(next_arr) < J ? jobs[MST(next_arr)].x : kEmpty;
+                }
+            }
+            auto job_at = [&](uint32_t j) -> uint4 {
+                const uint32_t d = j - hb;
+                if (d < (uint32_t)kWave)
+                    return make_uint4(readlane(hwin.x, d), readlane(hwin.y, d), readlane(hwin.z, d), readlane(hwin.w, d));
+                return jobs[j];
+            };
+            // ScheduleJob (scheduler.go:127-139): lowest node with both >=; zero-capacity virtual
+            // nodes (AddVirtualNode, cluster.go:79) follow the physical ones
+            const uint32_t vn = sh.trs[c].vnodes;
+            auto first_fit = [&](uint32_t jc, uint32_t jm) -> uint32_t {
+                unsigned long long v[kMwNodes / kWave];
+#pragma unroll
+                for (uint32_t q = 0; q < kMwNodes / kWave; ++q) {
+                    const uint32_t i = q * kWave + lane;
+                    v[q] = i < N ? nodes[i] : 0ull;
+                }
+                uint32_t kk = kEmpty;
+#pragma unroll
+                for (uint32_t q = 0; q < kMwNodes / kWave; ++q) {
+                    const uint32_t i = q * kWave + lane;
+                    const unsigned long long m =
+                        __ballot(i < N && (uint32_t)v[q] >= jc && (uint32_t)(v[q] >> 32) >= jm);
+                    if (m && kk == kEmpty) kk = q * kWave + (uint32_t)__builtin_ctzll(m);
+                }
+                if (kk == kEmpty && jc == 0u && jm == 0u && vn > 0u) kk = N;
+                return kk;
+            };
+            // Node.RunJob commit (cluster.go:144-148) + running-slot insert; false on overflow
+            auto commit = [&](uint32_t kn, uint32_t jc, uint32_t jm, uint32_t f) -> bool {
+                const unsigned long long need = (unsigned long long)jc | ((unsigned long long)jm << 32);
+                const unsigned long long any = __ballot(frm != 0u);
+                if (!any) return false;
+                const uint32_t sel = (uint32_t)__builtin_ctzll(any);
+                const uint32_t row = (uint32_t)__builtin_ctz(readlane(frm, sel));
+                if (lane == sel) {
+                    if (kn < N) atomicSub(&nodes[kn], need);
+                    a.snode[sb + row * kWave + sel] = kn;
+                    a.scm[sb + row * kWave + sel] = need;
+#pragma unroll
+                    for (int r = 0; r < kRows; ++r)
+                        if ((uint32_t)r == row) fin[r] = f;
+                    frm &= ~(1u << row);
+                }
+                ++MST(nrun);
+                MST(peak) = MST(nrun) > MST(peak) ? MST(nrun) : MST(peak);
+                MST(minf) = f < MST(minf) ? f : MST(minf);
+                return true;
+            };
+            auto place_own = [&](uint32_t j, uint32_t kn, uint4 jb) -> bool {
+                const uint32_t f = T + jb.y;
+                if (jb.y != 0u && !commit(kn, jb.z, jb.w, f)) return false;
+                if (lane == 0) {
+                    a.out_node[j0 + j] = (int32_t)kn;
+                    a.out_start[j0 + j] = T;
+                    a.out_finish[j0 + j] = f;
+                }
+                ++MST(placed);
+                ++MST(decided);
+                return true;
+            };
+
+            TrRecA req{kEmpty, 0u, 0u, 0u};
+            for (;;) {
+                if (MST(has_w)) {  // WaitQueue head (scheduler.go:219-251)
+                    const uint4 jb = job_at(MST(w));
+                    const uint32_t kn = first_fit(jb.z, jb.w);
+                    if (kn != kEmpty) {
+                        if (!place_own(MST(w), kn, jb)) {
+                            MST(flags) |= MCS_FLAG_OVERFLOW;
+                            break;
+                        }
+                        MST(has_w) = 0u;
+                    } else if (a.borrow) {
+                        req = TrRecA{MST(w), jb.z, jb.w, jb.y};  // BorrowResources (:234)
+                    }
+                    break;  // time.Sleep(1 s), :250
+                }
+                if (MST(rq_head) < MST(next_arr)) {  // ReadyQueue head (:255-272), no sleep
+                    const uint32_t j = MST(rq_head)++;
+                    const uint4 jb = job_at(j);
+                    const uint32_t kn = first_fit(jb.z, jb.w);
+                    if (kn != kEmpty) {
+                        if (!place_own(j, kn, jb)) {
+                            MST(flags) |= MCS_FLAG_OVERFLOW;
+                            break;
+                        }
+                    } else {
+                        MST(has_w) = 1u;
+                        MST(w) = j;
+                        ++MST(waited);
+                    }
+                    continue;
+                }
+                if (MST(lq_len) > 0u) {  // LentQueue head (:277-290), appended by this wave in phase B
+                    const uint64_t w0 = readlane((uint32_t)lqw, 0) | ((uint64_t)readlane((uint32_t)(lqw >> 32), 0) << 32);
+                    const uint32_t eb = (uint32_t)w0, ej = (uint32_t)(w0 >> 32);
+                    const uint32_t ec = readlane((uint32_t)lqw, 1), em = readlane((uint32_t)(lqw >> 32), 1);
+                    const uint32_t ed = readlane((uint32_t)lqw, 2);
+                    const uint32_t kn = first_fit(ec, em);
+                    if (kn != kEmpty) {
+                        const uint32_t f = T + ed;
+                        if (ed != 0u && !commit(kn, ec, em, f)) {
+                            MST(flags) |= MCS_FLAG_OVERFLOW;
+                            break;
+                        }
+                        if (lane == 0) {
+                            const unsigned long long idx = atomicAdd(lent_ctr, 1ull);
+                            if (idx < a.lent_cap) {
+                                mcs_lent_rec rec;
+                                rec.lender = c;
+                                rec.borrower = eb;
+                                rec.job = ej;
+                                rec.node = kn;
+                                rec.start_s = T;
+                                rec.finish_s = f;
+                                rec.pad = 0u;
+                                a.lent_log[idx] = rec;
+                            }
+                        }
+                        ++MST(lent_runs);
+                        MST(lq_head) = MST(lq_head) + 1u == a.LQ ? 0u : MST(lq_head) + 1u;
+                        --MST(lq_len);
+                    }
+                    break;  // sleep 1 s (:289)
+                }
+                break;  // idle sleep (:294)
+            }
+
+            // GetResourceUtilization (cluster.go:46-63) on the ticks a trader reads it: an exact
+            // integer sum (the engine's eligibility check), capacities minus free
+            if (sample) {
+                uint32_t fc = 0u, fm = 0u;
+                for (uint32_t i = lane; i < N; i += kWave) {
+                    const unsigned long long v = nodes[i];
+                    fc += (uint32_t)v;
+                    fm += (uint32_t)(v >> 32);
+                }
+                const float sc = (float)(int32_t)(sh.capc[wave] - mw_wave_sum(fc));
+                const float sm = (float)(int32_t)(sh.capm[wave] - mw_wave_sum(fm));
+                MST(cu) = __float_as_uint(__fdiv_rn(sc, (float)MST(total_c)));
+                MST(mu) = __float_as_uint(__fdiv_rn(sm, (float)MST(total_m)));
+            }
+            // the post-A record, one granule per lane
+            uint32_t xv = 0u;
+            xv = lane == 0 ? req.job : xv;
+            xv = lane == 1 ? req.c : xv;
+            xv = lane == 2 ? req.m : xv;
+            xv = lane == 3 ? req.dur : xv;
+            const uint32_t qs = (MST(has_w) ? 1u : 0u) | (MST(rq_head) < MST(next_arr) ? 2u : 0u);
+            xv = lane == 4 ? qs : xv;
+            xv = lane == 5 ? (uint32_t)MST(decided) : xv;
+            xv = lane == 6 ? nat : xv;
+            xv = lane == 7 ? (uint32_t)MST(flags) : xv;
+            xv = lane == 8 ? (uint32_t)MST(cu) : xv;
+            xv = lane == 9 ? (uint32_t)MST(mu) : xv;
+            if (lane < kX1Words) put_granule(gx1 + (size_t)c * kX1Words + lane, tag1, xv);
+            if (lane < kStWords) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stv;
+        }
+
+        // ---- X1: every cluster's record (one wave sweeps, the others wait at the barrier) ----
+        if (wave == 0) {
+            const uint32_t nw = C * kX1Words;
+            constexpr int kPer = (int)(kTrResMaxClusters * kX1Words / kWave);  // granules per lane
+            uint32_t xv[kPer];
+            for (uint32_t spins = 0;; ++spins) {
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < kPer; ++k) {
+                    const uint32_t i = lane + (uint32_t)k * kWave;
+                    xv[k] = 0u;
+                    if (i < nw) {
+                        const unsigned long long x = __hip_atomic_load(gx1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok = ok && (uint32_t)(x >> 32) == tag1;
+                        xv[k] = (uint32_t)x;
+                    }
+                }
+                if (__all(ok)) break;
+                if (spins > kSpinLimit) {
+                    timed_out = true;
+                    break;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) {
+                const uint32_t i = lane + (uint32_t)k * kWave;
+                if (i < nw) {
+                    const uint32_t v = xv[k], g = i / kX1Words, w = i - g * kX1Words;
+                    switch (w) {
+                        case 0: sh.rq_job[g] = v; break;
+                        case 1: sh.rq_c[g] = v; break;
+                        case 2: sh.rq_m[g] = v; break;
+                        case 3: sh.rq_dur[g] = v; break;
+                        case 4: sh.qs[g] = v; break;
+                        case 5: sh.decided[g] = v; break;
+                        case 6: sh.next_arr_t[g] = v; break;
+                        case 7: sh.xflags[g] = v; break;
+                        case 8: sh.cu[g] = __uint_as_float(v); break;
+                        default: sh.mu[g] = __uint_as_float(v); break;
+                    }
+                }
+            }
+            if (lane < 2) sh.accm[lane] = 0u;
+            if (timed_out && lane == 0) sh.done = 2u;
+        }
+        __syncthreads();
+        if (sh.done == 2u) break;
+
+        // ---- phase B: this wave's cluster as lender, requests in borrower order (tr_lend_kernel) ----
+        // Lend (scheduler.go:194-202) accepts a request (c, m) when some node has free_c > c and
+        // free_m > m.  With every free_c of the lender at most 64 that is G[c] > m for
+        // G[x] = max free_m over the nodes with free_c > x (0 when none): the lender builds G in a
+        // 64-entry LDS table, and every request of the tick is tested at once, one borrower per
+        // lane (C <= 64); the accepted ones join its LentQueue in borrower order.  A lender with a
+        // larger free_c scans its nodes per request instead.
+        if (own) {
+            const uint32_t L = c;
+            uint32_t rqj = kEmpty, rqc = 0u, rqm = 0u, rqd = 0u;
+            if (lane < C) {
+                rqj = sh.rq_job[lane];
+                rqc = sh.rq_c[lane];
+                rqm = sh.rq_m[lane];
+                rqd = sh.rq_dur[lane];
+            }
+            uint32_t* const tab = sh.gtab[wave];
+            uint32_t lq_len = sh.st[wave].lq_len, fb = 0;
+            const uint32_t lq_head = sh.st[wave].lq_head;
+            const uint32_t LQ = a.LQ;
+            const bool want = rqj != kEmpty && lane != L;  // self skipped (:176)
+            unsigned long long okm = 0ull;
+            if (__ballot(want)) {
+                tab[lane] = 0u;
+                bool big = false;
+                for (uint32_t i = lane; i < N; i += kWave) {
+                    const unsigned long long v = nodes[i];
+                    const uint32_t fc = (uint32_t)v;
+                    if (fc > 64u)
+                        big = true;
+                    else if (fc > 0u)
+                        atomicMax(&tab[fc - 1u], (uint32_t)(v >> 32));
+                }
+                if (!__ballot(big)) {
+                    const uint32_t gm = wave_scan_max_u32(tab[63u - lane]);  // G[63 - lane]
+                    tab[63u - lane] = gm;
+                    okm = __ballot(want && rqc < 64u && tab[rqc < 64u ? rqc : 0u] > rqm);
+                } else {
+                    unsigned long long pend = __ballot(want);
+                    while (pend) {
+                        const uint32_t bi = (uint32_t)__builtin_ctzll(pend);
+                        pend &= pend - 1ull;
+                        const uint32_t rc = readlane(rqc, bi), rm = readlane(rqm, bi);
+                        bool ok = false;
+                        for (uint32_t i0 = 0; i0 < N; i0 += kWave) {
+                            const uint32_t i = i0 + lane;
+                            if (i < N) {
+                                const unsigned long long v = nodes[i];
+                                ok = ok || ((uint32_t)v > rc && (uint32_t)(v >> 32) > rm);
+                            }
+                            if (__ballot(ok)) break;
+                        }
+                        if (__ballot(ok)) okm |= 1ull << bi;
+                    }
+                }
+            }
+            // appends (server.go:80-113): the first LQ - lq_len accepted, in borrower order
+            const uint32_t rank = (uint32_t)__builtin_popcountll(okm & ((1ull << lane) - 1ull));
+            if (((okm >> lane) & 1ull) && lq_len + rank < LQ) {
+                uint32_t at = lq_head + lq_len + rank;
+                at = at >= LQ ? at - LQ : at;
+                TrLq e{};
+                e.borrower = lane;
+                e.job = rqj;
+                e.c = rqc;
+                e.m = rqm;
+                e.dur = rqd;
+                a.lq[(size_t)L * LQ + at] = e;
+            }
+            const uint32_t nacc = (uint32_t)__builtin_popcountll(okm);
+            if (lq_len + nacc > LQ) {
+                fb |= MCS_FLAG_LENT_OVERFLOW;
+                lq_len = LQ;
+            } else {
+                lq_len += nacc;
+            }
+            if (lane == 0) {
+                sh.st[wave].lq_len = lq_len;
+                sh.st[wave].flags |= fb;
+                if (okm) {
+                    atomicOr(&sh.accm[0], (uint32_t)okm);
+                    atomicOr(&sh.accm[1], (uint32_t)(okm >> 32));
+                }
+                // this lender's LentQueue length (bit 31: the append overflowed) for C/D
+                put_granule(gx2 + L, tag2, lq_len | (fb ? 0x80000000u : 0u));
+            }
+        }
+        __syncthreads();
+
+        // ---- X2 + phases C and D: wave 0 of every workgroup, one lane per cluster (C <= 64) ----
+        if (wave == 0) {
+            if (lane < 2) put_granule(gx2 + C + 2u * wg + lane, tag2, sh.accm[lane]);
+            const uint32_t nw = C + 2u * nwg;
+            uint32_t lw = 0u, aw = 0u;  // lane g: cluster g's lender word; the OR of the masks
+            for (uint32_t spins = 0;; ++spins) {
+                bool ok = true;
+                uint32_t m0 = 0u, m1 = 0u;
+                for (uint32_t i = lane; i < nw; i += kWave) {
+                    const unsigned long long x = __hip_atomic_load(gx2 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = ok && (uint32_t)(x >> 32) == tag2;
+                    if (i < C) lw = (uint32_t)x;
+                    else if (((i - C) & 1u) == 0u) m0 |= (uint32_t)x;
+                    else m1 |= (uint32_t)x;
+                }
+                if (__all(ok)) {
+                    for (int o = 32; o > 0; o >>= 1) {
+                        m0 |= (uint32_t)__shfl_xor((int)m0, o);
+                        m1 |= (uint32_t)__shfl_xor((int)m1, o);
+                    }
+                    aw = lane < 32u ? (m0 >> lane) & 1u : (m1 >> (lane - 32u)) & 1u;
+                    break;
+                }
+                if (spins > kSpinLimit) {
+                    timed_out = true;
+                    break;
+                }
+            }
+            const uint32_t g = lane;
+            float cu = 0.0f, mu = 0.0f;
+            uint32_t tot_c = 0u, tot_m = 0u, busy = 0u, next_arr_t = kEmpty, done_g = 1u, fl = 0u;
+            TrTrader t{0u, 0u, 0u, kEmpty, 0u};
+            if (g < C && !timed_out) {
+                const uint32_t qs = sh.qs[g], lq = lw & 0x7FFFFFFFu, fbg = (lw >> 31) ? MCS_FLAG_LENT_OVERFLOW : 0u;
+                uint32_t has_w = qs & 1u, decided = sh.decided[g];
+                const uint32_t rj = sh.rq_job[g];
+                if (rj != kEmpty && aw) {  // BorrowedQueue append (scheduler.go:237-242)
+                    has_w = 0u;
+                    ++decided;
+                    if (g / kMwWaves == wg) {  // (the owner workgroup writes it)
+                        const uint64_t gj0 = sh.j0[g];
+                        a.out_node[gj0 + rj] = MCS_NODE_BORROWED;
+                        a.out_start[gj0 + rj] = T;
+                        a.out_finish[gj0 + rj] = MCS_TIME_NONE;
+                        TrCluster& s = sh.st[g - wg * kMwWaves];
+                        s.has_w = 0u;
+                        ++s.decided;
+                        ++s.borrowed;
+                    }
+                }
+                cu = sh.cu[g];
+                mu = sh.mu[g];
+                tot_c = sh.total_c[g];
+                tot_m = sh.total_m[g];
+                busy = (has_w || lq > 0u || (qs & 2u)) ? 1u : 0u;
+                next_arr_t = sh.next_arr_t[g];
+                done_g = (decided == sh.J[g] && lq == 0u) ? 1u : 0u;
+                fl = sh.xflags[g] | fbg;
+                t = sh.trs[g];
+            }
+            unsigned long long n_trades = sh.n_trades, n_won = sh.n_won;
+            uint32_t lflags = 0;
+            if (a.trader && !timed_out) {
+                const bool due = g < C && t.next_due <= T;
+                const bool broken = cu > 0.8f || mu > 0.8f;  // Utilization (trader.go:127-130)
+                if (due && !broken) t.next_due = T + a.period;
+                // ApproveTrade of this lane as a responder: its sample is fixed for the tick
+                const bool appr = g < C && approve_trade_dev(tot_c, tot_m, cu, mu, 0u, 0u, 0u);
+                unsigned long long pend = __ballot(due && broken);
+                while (pend) {  // RequestPolicyMonitor of requester q (trader.go:282-324)
+                    const uint32_t q = (uint32_t)__builtin_ctzll(pend);
+                    pend &= pend - 1ull;
+                    bool app = false;
+                    if (g < C && g != q) {  // RequestResource, index order
+                        if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
+                        if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
+                            app = appr;
+                            t.lock_id = t.next_id++;  // set even when not approving (:44-46)
+                            t.lock_until = T + a.lock_s;
+                        }
+                    }
+                    const unsigned long long ab = __ballot(app);
+                    const uint32_t napp = (uint32_t)__builtin_popcountll(ab);
+                    const uint32_t winner = ab ? (uint32_t)__builtin_ctzll(ab) : kEmpty;
+                    if (winner != kEmpty) {
+                        if (g == winner) t.lock_id = 0u;  // ApproveContract unlocks (:83)
+                        if (g == q) t.vnodes += 1u;       // AddVirtualNode(0 cores, 0 memory)
+                        ++n_won;
+                    }
+                    if (g == q) t.next_due = T + (winner != kEmpty ? a.ok_sleep : a.fail_sleep) + a.period;
+                    if (lane == 0 && wg == 0) {  // (workgroup 0 keeps the log)
+                        if (n_trades < a.trade_cap) {
+                            mcs_trade_rec rec;
+                            rec.t_s = T;
+                            rec.requester = q;
+                            rec.winner = winner == kEmpty ? -1 : (int32_t)winner;
+                            rec.approvals = napp;
+                            a.trade_log[n_trades] = rec;
+                        }
+                    }
+                    if (n_trades >= a.trade_cap) lflags |= MCS_FLAG_LOG_OVERFLOW;
+                    ++n_trades;
+                }
+                if (g < C) sh.trs[g] = t;
+            }
+            // the next tick: T+1 while any queue is busy, else the next arrival or trader round
+            uint32_t nxt = next_arr_t;
+            if (a.trader && g < C) nxt = t.next_due < nxt ? t.next_due : nxt;
+            const bool done_all = !__ballot(!done_g);
+            const bool busy_any = __ballot(busy != 0u) != 0ull;
+            nxt = wave_min_u32(nxt);
+            for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o);
+            if (lane == 0) {
+                uint32_t flags = sh.flags | fl | lflags;
+                uint32_t done = 0, Tn = T;
+                const uint32_t fatal = MCS_FLAG_OVERFLOW | MCS_FLAG_LENT_OVERFLOW;
+                if (timed_out) {
+                    done = 2u;
+                } else if (done_all || (flags & fatal)) {
+                    done = 1u;
+                } else if (T >= a.t_max || (!busy_any && nxt == kEmpty)) {
+                    done = 1u;
+                    flags |= MCS_FLAG_T_MAX;
+                } else {
+                    Tn = (busy_any || nxt <= T + 1u) ? T + 1u : nxt;
+                }
+                sh.T = Tn;
+                sh.done = done;
+                sh.ticks += 1u;
+                sh.flags = flags;
+                sh.n_trades = n_trades;
+                sh.n_won = n_won;
+            }
+        }
+        __syncthreads();
+        if (sh.done == 2u) break;
+    }
+
+    // ---- state out (the next launch, the stats and the readers take it from HBM) ----
+    if (own) {
+        for (uint32_t i = lane; i < N; i += kWave) a.tn[n0 + i] = nodes[i];
+        if (lane < kStWords) reinterpret_cast<uint32_t*>(&a.cl[c])[lane] = reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane];
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) a.sfin[sb + r * kWave + lane] = fin[r];
+    }
+    if (wg == 0) {
+        for (uint32_t g = threadIdx.x; g < C; g += kMwWaves * kWave) a.tr[g] = sh.trs[g];
+        if (threadIdx.x == 0) {
+            TrCtl* ctl = a.ctl;  // (n_lent is counted in place by the lent-log appends)
+            ctl->T = sh.T;
+            ctl->done = sh.done == 2u ? 1u : sh.done;
+            ctl->ticks = sh.ticks;
+            ctl->flags = sh.flags | (sh.done == 2u ? kTrFlagMwTimeout : 0u);
+            ctl->n_trades = sh.n_trades;
+            ctl->n_won = sh.n_won;
+        }
+    }
+}
+
+}  // namespace
+
+size_t trade_mw_lds(uint32_t ns) { return (sizeof(MwShared) + 7) / 8 * 8 + (size_t)kMwWaves * ns * 8u; }
+
+// up to 64 clusters of <= 256 nodes with 256, 512 or 1024 running slots each on one engine
+bool trade_mw_shape(const TradeArgs& a) {
+    return a.world == 1 && a.Ct <= kTrResMaxClusters && a.ns <= kMwNodes &&
+           (a.S == 4u * kWave || a.S == 8u * kWave || a.S == 16u * kWave);
+}
+
+size_t trade_mw_granules(uint32_t n_clusters) {
+    const uint32_t nwg = (n_clusters + kMwWaves - 1) / kMwWaves;
+    return ((size_t)n_clusters * (kX1Words + 1) + 2u * nwg + 1u) & ~(size_t)1;  // (16-byte multiple)
+}
+
+hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx, uint32_t tick_budget, size_t lds,
+                           hipStream_t s) {
+    const uint32_t nwg = (a.Ct + kMwWaves - 1) / kMwWaves;
+    // the granules carry epochs counted within the launch: zero them first
+    hipError_t st = hipMemsetAsync(gx, 0, trade_mw_granules(a.Ct) * 8u, s);
+    if (st != hipSuccess) return st;
+    const void* fn = a.S == 4u * kWave   ? (const void*)tr_mw_kernel<4>
+                     : a.S == 8u * kWave ? (const void*)tr_mw_kernel<8>
+                                         : (const void*)tr_mw_kernel<16>;
+    st = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (st != hipSuccess) return st;
+    if (a.S == 4u * kWave)
+        hipLaunchKernelGGL(tr_mw_kernel<4>, dim3(nwg), dim3(kMwWaves * kWave), lds, s, a, gx, tick_budget);
+    else if (a.S == 8u * kWave)
+        hipLaunchKernelGGL(tr_mw_kernel<8>, dim3(nwg), dim3(kMwWaves * kWave), lds, s, a, gx, tick_budget);
+    else
+        hipLaunchKernelGGL(tr_mw_kernel<16>, dim3(nwg), dim3(kMwWaves * kWave), lds, s, a, gx, tick_budget);
+    return hipGetLastError();
+}
+
+}  // namespace mcs

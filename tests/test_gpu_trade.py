@@ -207,23 +207,26 @@ def test_gpu_trade_fuzz(shape, seed):
 
 
 @pytest.mark.parametrize("kind,C,J,pool", [("n64_hot", 8, 1500, 0), ("n256", 16, 3000, 8), ("n256", 16, 3000, 0),
-                                           ("small", 64, 1500, 0)])
+                                           ("small", 64, 1500, 0), ("n256", 40, 2000, 16), ("n64", 33, 2000, 4)])
 def test_gpu_trade_resident_equals_kernels_and_oracle(kind, C, J, pool, monkeypatch):
-    """The whole system resident in one workgroup (mcs_trade_res.hip; loop_form 3, picked for one
-    engine of <= 64 clusters of <= 256 nodes with 256/512/1024 slots) == the graph-replayed tick
+    """The system resident on the GPU for the whole run, in its two forms — one workgroup per 16
+    clusters trading records as tagged granules (mcs_trade_mw.hip; loop_form 4, the default for one
+    engine of <= 64 clusters of <= 256 nodes with 256/512/1024 slots) and all of it in one
+    workgroup (mcs_trade_res.hip; MCS_TRADE_RESIDENT=1, loop_form 3) — == the graph-replayed tick
     kernels (MCS_TRADE_RESIDENT=0, loop_form 0) == the oracle, on every output."""
     arrays, streams, _ = seeded_workload(kind, C, J)
     res = {}
-    for mode in ("1", "0"):
+    for mode in ("2", "1", "0"):
         monkeypatch.setenv("MCS_TRADE_RESIDENT", mode)
         res[mode] = gpu_trade(arrays, streams, slot_pool=pool)
-    assert res["1"]["tstats"]["loop_form"] == 3 and res["0"]["tstats"]["loop_form"] == 0
-    for k in ("node", "start", "finish"):
-        np.testing.assert_array_equal(res["1"][k], res["0"][k], err_msg=k)
-    assert lent_rows(res["1"]["lent"]) == lent_rows(res["0"]["lent"])
-    assert res["1"]["trades"].tobytes() == res["0"]["trades"].tobytes()
-    np.testing.assert_array_equal(res["1"]["virtual_nodes"], res["0"]["virtual_nodes"])
-    for f in ("placed", "borrowed", "waited", "undecided", "lent_runs", "lent_pending", "trades", "trades_won",
-              "ticks", "t_final", "flags"):
-        assert res["1"]["tstats"][f] == res["0"]["tstats"][f], f
-    assert_trade_parity(arrays, streams, res["1"])
+    assert [res[m]["tstats"]["loop_form"] for m in ("2", "1", "0")] == [4, 3, 0]
+    for m in ("2", "1"):
+        for k in ("node", "start", "finish"):
+            np.testing.assert_array_equal(res[m][k], res["0"][k], err_msg=f"{k} mode {m}")
+        assert lent_rows(res[m]["lent"]) == lent_rows(res["0"]["lent"])
+        assert res[m]["trades"].tobytes() == res["0"]["trades"].tobytes()
+        np.testing.assert_array_equal(res[m]["virtual_nodes"], res["0"]["virtual_nodes"])
+        for f in ("placed", "borrowed", "waited", "undecided", "lent_runs", "lent_pending", "trades", "trades_won",
+                  "ticks", "t_final", "flags"):
+            assert res[m]["tstats"][f] == res["0"]["tstats"][f], (f, m)
+    assert_trade_parity(arrays, streams, res["2"])
