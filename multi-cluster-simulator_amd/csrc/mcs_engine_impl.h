@@ -91,6 +91,7 @@ struct mcs_engine {
     bool free_lt31 = false;  // every node free value < 2^31 - 1 (fifo_asm_kernel<32> guard bits)
     bool free_lt15 = false;  // every node free value < 2^15 - 1 (fifo_asm_kernel<16>)
     bool sums_lt24 = false;  // every cluster's sum of max(capacity, availability) < 2^24 per resource
+    bool slot_pack_ok = false;  // every node's max(capacity, availability) < 128 cores, < 65536 memory
     uint64_t total_nodes = 0, total_jobs = 0;
     std::vector<uint32_t> node_off;
     std::vector<uint64_t> job_off;

@@ -190,7 +190,7 @@ int resident_form(mcs_engine* e, size_t* lds) {
     int max_lds = 0;
     if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device) != hipSuccess)
         return 0;
-    if (want == 2 && trade_mw_shape(e->td->a)) {
+    if (want == 2 && e->slot_pack_ok && trade_mw_shape(e->td->a)) {
         *lds = trade_mw_lds(e->td->a.ns);
         if (*lds <= (size_t)max_lds) return 2;
     }
@@ -205,7 +205,17 @@ int run_local(mcs_engine* e) {
     const int rf = resident_form(e, &lds);
     if (rf == 2) {
         td->loop_form = kLoopResidentMw;
-        if (!td->gx) HIPCHK(e, hipMalloc(&td->gx, trade_mw_granules(td->a.Ct) * 8u));
+        if (!td->gx) {
+            // the granules live in uncached device memory (MTYPE UC): a poll that re-reads a line
+            // its XCD's L2 already holds would otherwise be served the stale copy until that line
+            // is evicted (measured: ~7 sweep passes per exchange with cached hipMalloc memory);
+            // MCS_MW_GX=0 keeps plain hipMalloc (A/B)
+            const char* gxenv = getenv("MCS_MW_GX");
+            const int gxm = gxenv ? atoi(gxenv) : 3;
+            const size_t gb = trade_mw_granules(td->a.Ct) * 8u;
+            if (gxm == 0) HIPCHK(e, hipMalloc(&td->gx, gb));
+            else HIPCHK(e, hipExtMallocWithFlags((void**)&td->gx, gb, (unsigned)gxm));
+        }
         for (;;) {
             const hipError_t st = launch_trade_mw(td->a, td->gx, kResTicks, lds, e->stream);
             if (st != hipSuccess) return hip_fail(e, "resident tick kernel (workgroups)", st);

@@ -47,16 +47,35 @@ __device__ __forceinline__ uint32_t mw_wave_sum(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
     return v;
 }
-// HBM this kernel's own workgroup wrote and reads back (slot payloads, LentQueue entries)
+// HBM this kernel's own wave wrote in an earlier tick and reads back (LentQueue entries)
 __device__ __forceinline__ uint64_t mld64(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ uint32_t mld32(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
+#ifdef MCS_MW_SYSLOAD
+#define MW_LOAD_SCOPE __HIP_MEMORY_SCOPE_SYSTEM
+#else
+#define MW_LOAD_SCOPE __HIP_MEMORY_SCOPE_AGENT
+#endif
 __device__ __forceinline__ void put_granule(unsigned long long* g, uint32_t tag, uint32_t v) {
     __hip_atomic_store(g, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+#ifdef MCS_STAMPS
+// the probe build's per-wave segment times (s_memrealtime, 100 MHz) summed over the launches since
+// the last read: [workgroup][wave][segment], segments as MW_MARK below
+constexpr int kMwSeg = 12, kMwMaxWg = 4;  // (10, 11: sweep passes of X1, X2)
+__device__ unsigned long long g_mw_stamps[kMwMaxWg * kMwWaves * kMwSeg];
+#define MW_MARK(i)                              \
+    do {                                        \
+        const uint64_t mw_now = wall_clock64(); \
+        mw_acc[i] += mw_now - mw_last;          \
+        mw_last = mw_now;                       \
+    } while (0)
+#else
+#define MW_MARK(i) \
+    do {           \
+    } while (0)
+#endif
 
 constexpr uint32_t kStWords = sizeof(TrCluster) / 4u;
 static_assert(sizeof(TrCluster) % 4u == 0u && kStWords <= (uint32_t)kWave, "TrCluster in one VGPR");
@@ -86,7 +105,7 @@ struct MwShared {  // (this workgroup's node vectors follow: kMwWaves * ns u64)
     // gathered each tick (X1): every cluster's request and queue state
     uint32_t rq_job[kTrResMaxClusters], rq_c[kTrResMaxClusters], rq_m[kTrResMaxClusters];
     uint32_t rq_dur[kTrResMaxClusters];
-    uint32_t qs[kTrResMaxClusters];  // has_w | rq_busy << 1
+    uint32_t qs[kTrResMaxClusters];  // has_w | rq_busy << 1 | lent run this tick << 2
     uint32_t decided[kTrResMaxClusters], next_arr_t[kTrResMaxClusters], xflags[kTrResMaxClusters];
     float cu[kTrResMaxClusters], mu[kTrResMaxClusters];
     // constants of the run, every cluster
@@ -99,7 +118,7 @@ struct MwShared {  // (this workgroup's node vectors follow: kMwWaves * ns u64)
     uint32_t gtab[kMwWaves][64];
     uint32_t accm[2];  // borrowers some lender of this workgroup accepted this tick
     uint32_t T, done, ticks, flags;
-    unsigned long long n_trades, n_won;
+    unsigned long long n_trades, n_won, n_lent;
 };
 
 template <int kRows>  // slot rows per cluster (64 slots each)
@@ -113,8 +132,8 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
     const uint32_t wg = blockIdx.x, nwg = gridDim.x;
     const uint32_t c = wg * kMwWaves + wave;  // this wave's cluster
     const bool own = c < C;
-    unsigned long long* const gx1 = gx;                          // [C][kX1Words]
-    unsigned long long* const gx2 = gx + (size_t)C * kX1Words;   // [C] lender words, then [nwg][2]
+    unsigned long long* const gx1 = gx;  // [C][kX1Words] (room for 64 clusters)
+    unsigned long long* const gx2 = gx + (size_t)kTrResMaxClusters * kX1Words;  // [C] lender words, [nwg][2]
 
     // ---- state in ----
     unsigned long long* const nodes = nodes_wg + (size_t)wave * ns;
@@ -155,23 +174,56 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
         sh.flags = ctl.flags;
         sh.n_trades = ctl.n_trades;
         sh.n_won = ctl.n_won;
+        sh.n_lent = ctl.n_lent;
     }
-    // the wave's slot finish times in registers (row r, lane l = slot r * 64 + l)
-    uint32_t fin[kRows];
+    // the wave's running slots in registers (row r, lane l = slot r * 64 + l): finish time, and the
+    // payload packed as node | cores << 9 | mem << 16 (the engine picks this form only when every
+    // node capacity is below 128 cores and 65536 memory; node >= N: a virtual node, nothing to
+    // release); across launches the payload is kept in snode
+    uint32_t fin[kRows], pay[kRows];
     uint32_t frm = 0u;  // free rows of this lane
+    const size_t sb = (size_t)c * S;
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
-        fin[r] = own ? a.sfin[(size_t)c * S + r * kWave + lane] : kEmpty;
+        fin[r] = own ? a.sfin[sb + r * kWave + lane] : kEmpty;
+        pay[r] = own ? a.snode[sb + r * kWave + lane] : 0u;
         if (fin[r] == kEmpty) frm |= 1u << r;
     }
-    const size_t sb = (size_t)c * S;
-    const uint4* __restrict__ jobs = a.jobs + j0;
-    unsigned long long* const lent_ctr = &a.ctl->n_lent;
-    bool timed_out = false;
     __syncthreads();
+    const uint4* __restrict__ jobs = a.jobs + j0;
+    // the next tick's records, loaded during the previous tick's exchanges: 64 records from the
+    // window base hwb (the WaitQueue head, else the ReadyQueue head), 64 arrival times from the
+    // first unqueued job, the LentQueue head entry
+    uint4 hwin = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t awin = kEmpty, hwb = 0u;
+    unsigned long long lqw = 0ull;
+    auto prefetch_jobs = [&](uint32_t hb, uint32_t na) {
+        hwb = hb;
+        hwin = hb + lane < J ? jobs[hb + lane] : make_uint4(0u, 0u, 0u, 0u);
+        awin = na + lane < J ? jobs[na + lane].x : kEmpty;
+    };
+    auto prefetch_lq = [&](uint32_t lqh, uint32_t lqn) {
+        lqw = 0ull;
+        if (lqn > 0u && lane < 3u) lqw = mld64(reinterpret_cast<const unsigned long long*>(a.lq + (size_t)c * a.LQ + lqh) + lane);
+    };
+    if (own) {
+        const TrCluster& s0 = sh.st[wave];
+        prefetch_jobs(s0.has_w ? s0.w : s0.rq_head, s0.next_arr);
+        prefetch_lq(s0.lq_head, s0.lq_len);
+    }
+    uint32_t lent_tick = 0u;  // lent runs of the whole system this tick
+    uint32_t lent_now = 0u, lr_b = 0u, lr_j = 0u, lr_n = 0u, lr_f = 0u;  // this tick's lent run (bit 2 of qs)
+    bool timed_out = false;
+#ifdef MCS_STAMPS
+    uint64_t mw_acc[kMwSeg];
+#pragma unroll
+    for (int i = 0; i < kMwSeg; ++i) mw_acc[i] = 0u;
+    uint64_t mw_last = wall_clock64();
+#endif
 
     for (uint32_t it = 0; it < tick_budget; ++it) {
         if (sh.done) break;
+        MW_MARK(9);
         const uint32_t T = sh.T;
         const uint32_t tag1 = 2u * it + 1u, tag2 = 2u * it + 2u;
 
@@ -189,50 +241,31 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             // the tick's job records, every load in flight at once: 64 records from the WaitQueue
             // head (else the ReadyQueue head), 64 arrival times from the first unqueued job, and
             // the LentQueue head entry
-            const uint32_t hb = MST(has_w) ? MST(w) : MST(rq_head);
             const uint32_t na0 = MST(next_arr);
-            const uint32_t lqh = MST(lq_head), lqn = MST(lq_len);
-            uint4 hwin = make_uint4(0u, 0u, 0u, 0u);
-            uint32_t awin = kEmpty;
-            if (hb + lane < J) hwin = jobs[hb + lane];
-            if (na0 + lane < J) awin = jobs[na0 + lane].x;
-            unsigned long long lqw = 0ull;
-            if (lqn > 0u && lane < 3u) lqw = mld64(reinterpret_cast<const unsigned long long*>(a.lq + (size_t)c * a.LQ + lqh) + lane);
+            MW_MARK(0);
 
             // releases due at T (cluster.go:153-157), before the tick's decisions
             if (MST(minf) <= T) {
-                constexpr int kG = kRows < 4 ? kRows : 4;
                 uint32_t lm = kEmpty, nrel = 0;
 #pragma unroll
-                for (int g = 0; g < kRows; g += kG) {
-                    uint32_t nd[kG];
-                    unsigned long long cm[kG];
-#pragma unroll
-                    for (int r = 0; r < kG; ++r) {
-                        nd[r] = kEmpty;
-                        cm[r] = 0ull;
-                        if (fin[g + r] <= T) {
-                            const uint32_t slot = (g + r) * kWave + lane;
-                            nd[r] = mld32(a.snode + sb + slot);
-                            cm[r] = mld64(a.scm + sb + slot);
-                        }
-                    }
-#pragma unroll
-                    for (int r = 0; r < kG; ++r) {
-                        const uint32_t f = fin[g + r];
-                        if (f <= T) {
-                            if (nd[r] < N) atomicAdd(&nodes[nd[r]], cm[r]);
-                            fin[g + r] = kEmpty;
-                            frm |= 1u << (g + r);
-                            ++nrel;
-                        } else {
-                            lm = f < lm ? f : lm;
-                        }
+                for (int r = 0; r < kRows; ++r) {
+                    const uint32_t f = fin[r];
+                    if (f <= T) {
+                        const uint32_t p = pay[r], kn = p & 511u;
+                        if (kn < N)
+                            atomicAdd(&nodes[kn], (unsigned long long)((p >> 9) & 127u) |
+                                                      ((unsigned long long)(p >> 16) << 32));
+                        fin[r] = kEmpty;
+                        frm |= 1u << r;
+                        ++nrel;
+                    } else {
+                        lm = f < lm ? f : lm;
                     }
                 }
                 MST(nrun) -= mw_wave_sum(nrel);
                 MST(minf) = wave_min_u32(lm);
             }
+            MW_MARK(1);
             // arrivals up to T join the ReadyQueue (jobs are sorted by arrival)
             uint32_t nat;  // the arrival second of the first job not yet queued (kEmpty: none)
             {
@@ -251,8 +284,9 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                     nat = MST(next_arr) < J ? jobs[MST(next_arr)].x : kEmpty;
                 }
             }
+            MW_MARK(2);
             auto job_at = [&](uint32_t j) -> uint4 {
-                const uint32_t d = j - hb;
+                const uint32_t d = j - hwb;
                 if (d < (uint32_t)kWave)
                     return make_uint4(readlane(hwin.x, d), readlane(hwin.y, d), readlane(hwin.z, d), readlane(hwin.w, d));
                 return jobs[j];
@@ -287,11 +321,13 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                 const uint32_t row = (uint32_t)__builtin_ctz(readlane(frm, sel));
                 if (lane == sel) {
                     if (kn < N) atomicSub(&nodes[kn], need);
-                    a.snode[sb + row * kWave + sel] = kn;
-                    a.scm[sb + row * kWave + sel] = need;
+                    const uint32_t p = (kn < N ? kn : 511u) | (jc << 9) | (jm << 16);
 #pragma unroll
                     for (int r = 0; r < kRows; ++r)
-                        if ((uint32_t)r == row) fin[r] = f;
+                        if ((uint32_t)r == row) {
+                            fin[r] = f;
+                            pay[r] = p;
+                        }
                     frm &= ~(1u << row);
                 }
                 ++MST(nrun);
@@ -313,6 +349,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             };
 
             TrRecA req{kEmpty, 0u, 0u, 0u};
+            lent_now = 0u;
             for (;;) {
                 if (MST(has_w)) {  // WaitQueue head (scheduler.go:219-251)
                     const uint4 jb = job_at(MST(w));
@@ -356,20 +393,13 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                             MST(flags) |= MCS_FLAG_OVERFLOW;
                             break;
                         }
-                        if (lane == 0) {
-                            const unsigned long long idx = atomicAdd(lent_ctr, 1ull);
-                            if (idx < a.lent_cap) {
-                                mcs_lent_rec rec;
-                                rec.lender = c;
-                                rec.borrower = eb;
-                                rec.job = ej;
-                                rec.node = kn;
-                                rec.start_s = T;
-                                rec.finish_s = f;
-                                rec.pad = 0u;
-                                a.lent_log[idx] = rec;
-                            }
-                        }
+                        // the lent-run record is written after X1, at the index every workgroup
+                        // derives from the tick's lent bits (no global counter on this path)
+                        lr_b = eb;
+                        lr_j = ej;
+                        lr_n = kn;
+                        lr_f = f;
+                        lent_now = 4u;
                         ++MST(lent_runs);
                         MST(lq_head) = MST(lq_head) + 1u == a.LQ ? 0u : MST(lq_head) + 1u;
                         --MST(lq_len);
@@ -378,6 +408,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                 }
                 break;  // idle sleep (:294)
             }
+            MW_MARK(3);
 
             // GetResourceUtilization (cluster.go:46-63) on the ticks a trader reads it: an exact
             // integer sum (the engine's eligibility check), capacities minus free
@@ -399,7 +430,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             xv = lane == 1 ? req.c : xv;
             xv = lane == 2 ? req.m : xv;
             xv = lane == 3 ? req.dur : xv;
-            const uint32_t qs = (MST(has_w) ? 1u : 0u) | (MST(rq_head) < MST(next_arr) ? 2u : 0u);
+            const uint32_t qs = (MST(has_w) ? 1u : 0u) | (MST(rq_head) < MST(next_arr) ? 2u : 0u) | lent_now;
             xv = lane == 4 ? qs : xv;
             xv = lane == 5 ? (uint32_t)MST(decided) : xv;
             xv = lane == 6 ? nat : xv;
@@ -408,25 +439,34 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             xv = lane == 9 ? (uint32_t)MST(mu) : xv;
             if (lane < kX1Words) put_granule(gx1 + (size_t)c * kX1Words + lane, tag1, xv);
             if (lane < kStWords) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stv;
+            // the next tick's records (only phase A moves these cursors; a WaitQueue head that C/D
+            // moves to the BorrowedQueue leaves the ReadyQueue head inside the same window, or
+            // job_at loads it directly)
+            prefetch_jobs(MST(has_w) ? MST(w) : MST(rq_head), MST(next_arr));
         }
+        MW_MARK(4);
 
         // ---- X1: every cluster's record (one wave sweeps, the others wait at the barrier) ----
         if (wave == 0) {
             const uint32_t nw = C * kX1Words;
             constexpr int kPer = (int)(kTrResMaxClusters * kX1Words / kWave);  // granules per lane
             uint32_t xv[kPer];
+            unsigned long long xg[kPer];
             for (uint32_t spins = 0;; ++spins) {
                 bool ok = true;
 #pragma unroll
+                for (int k = 0; k < kPer; ++k)  // (every load issued before the first compare; the
+                    // granule block is allocated for 64 clusters, so no index is clamped)
+                    xg[k] = __hip_atomic_load(gx1 + lane + (uint32_t)k * kWave, __ATOMIC_RELAXED, MW_LOAD_SCOPE);
+#pragma unroll
                 for (int k = 0; k < kPer; ++k) {
                     const uint32_t i = lane + (uint32_t)k * kWave;
-                    xv[k] = 0u;
-                    if (i < nw) {
-                        const unsigned long long x = __hip_atomic_load(gx1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        ok = ok && (uint32_t)(x >> 32) == tag1;
-                        xv[k] = (uint32_t)x;
-                    }
+                    ok = ok && (i >= nw || (uint32_t)(xg[k] >> 32) == tag1);
+                    xv[k] = (uint32_t)xg[k];
                 }
+#ifdef MCS_STAMPS
+                mw_acc[10] += 1u;
+#endif
                 if (__all(ok)) break;
                 if (spins > kSpinLimit) {
                     timed_out = true;
@@ -456,6 +496,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             if (timed_out && lane == 0) sh.done = 2u;
         }
         __syncthreads();
+        MW_MARK(5);
         if (sh.done == 2u) break;
 
         // ---- phase B: this wave's cluster as lender, requests in borrower order (tr_lend_kernel) ----
@@ -465,6 +506,27 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
         // 64-entry LDS table, and every request of the tick is tested at once, one borrower per
         // lane (C <= 64); the accepted ones join its LentQueue in borrower order.  A lender with a
         // larger free_c scans its nodes per request instead.
+        // the tick's lent-run records at indices in cluster order, from the gathered lent bits
+        // (every workgroup computes the same ones; the log counter is replicated in LDS)
+        {
+            const bool ln = lane < C && (sh.qs[lane] & 4u);
+            const unsigned long long lm = __ballot(ln);
+            if (own && lent_now && lane == 0) {
+                const unsigned long long idx = sh.n_lent + (uint64_t)__builtin_popcountll(lm & ((1ull << c) - 1ull));
+                if (idx < a.lent_cap) {
+                    mcs_lent_rec rec;
+                    rec.lender = c;
+                    rec.borrower = lr_b;
+                    rec.job = lr_j;
+                    rec.node = lr_n;
+                    rec.start_s = T;
+                    rec.finish_s = lr_f;
+                    rec.pad = 0u;
+                    a.lent_log[idx] = rec;
+                }
+            }
+            lent_tick = (uint32_t)__builtin_popcountll(lm);
+        }
         if (own) {
             const uint32_t L = c;
             uint32_t rqj = kEmpty, rqc = 0u, rqm = 0u, rqd = 0u;
@@ -476,6 +538,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             }
             uint32_t* const tab = sh.gtab[wave];
             uint32_t lq_len = sh.st[wave].lq_len, fb = 0;
+            const uint32_t lq0 = lq_len;
             const uint32_t lq_head = sh.st[wave].lq_head;
             const uint32_t LQ = a.LQ;
             const bool want = rqj != kEmpty && lane != L;  // self skipped (:176)
@@ -544,8 +607,25 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                 // this lender's LentQueue length (bit 31: the append overflowed) for C/D
                 put_granule(gx2 + L, tag2, lq_len | (fb ? 0x80000000u : 0u));
             }
+            // the next tick's LentQueue head: an entry of an earlier tick is loaded; one this tick's
+            // appends just wrote (the queue was empty) is taken from the request registers
+            if (lq0 > 0u) {
+                prefetch_lq(lq_head, lq0);
+            } else if (okm && lq_len > 0u) {
+                const uint32_t b0 = (uint32_t)__builtin_ctzll(okm);
+                const uint32_t j = readlane(rqj, b0), ec = readlane(rqc, b0), em = readlane(rqm, b0),
+                               ed = readlane(rqd, b0);
+                lqw = lane == 0 ? ((unsigned long long)j << 32 | b0)
+                    : lane == 1 ? ((unsigned long long)em << 32 | ec)
+                    : lane == 2 ? (unsigned long long)ed
+                                : 0ull;
+            } else {
+                lqw = 0ull;
+            }
         }
+        MW_MARK(6);
         __syncthreads();
+        MW_MARK(7);
 
         // ---- X2 + phases C and D: wave 0 of every workgroup, one lane per cluster (C <= 64) ----
         if (wave == 0) {
@@ -555,13 +635,17 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             for (uint32_t spins = 0;; ++spins) {
                 bool ok = true;
                 uint32_t m0 = 0u, m1 = 0u;
-                for (uint32_t i = lane; i < nw; i += kWave) {
-                    const unsigned long long x = __hip_atomic_load(gx2 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = ok && (uint32_t)(x >> 32) == tag2;
-                    if (i < C) lw = (uint32_t)x;
-                    else if (((i - C) & 1u) == 0u) m0 |= (uint32_t)x;
-                    else m1 |= (uint32_t)x;
-                }
+                // (nw <= 72: two granules per lane, both loads issued before the first compare)
+                const uint32_t i0 = lane, i1 = lane + kWave;
+                const unsigned long long x0 = __hip_atomic_load(gx2 + i0, __ATOMIC_RELAXED, MW_LOAD_SCOPE);
+                const unsigned long long x1 = __hip_atomic_load(gx2 + i1, __ATOMIC_RELAXED, MW_LOAD_SCOPE);
+                ok = (i0 >= nw || (uint32_t)(x0 >> 32) == tag2) && (i1 >= nw || (uint32_t)(x1 >> 32) == tag2);
+                if (i0 < C) lw = (uint32_t)x0;
+                else if (i0 < nw) (((i0 - C) & 1u) == 0u ? m0 : m1) |= (uint32_t)x0;
+                if (i1 < nw) (((i1 - C) & 1u) == 0u ? m0 : m1) |= (uint32_t)x1;
+#ifdef MCS_STAMPS
+                mw_acc[11] += 1u;
+#endif
                 if (__all(ok)) {
                     for (int o = 32; o > 0; o >>= 1) {
                         m0 |= (uint32_t)__shfl_xor((int)m0, o);
@@ -676,32 +760,43 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                 sh.T = Tn;
                 sh.done = done;
                 sh.ticks += 1u;
+                sh.n_lent += lent_tick;
                 sh.flags = flags;
                 sh.n_trades = n_trades;
                 sh.n_won = n_won;
             }
         }
+        MW_MARK(8);
         __syncthreads();
         if (sh.done == 2u) break;
     }
+#ifdef MCS_STAMPS
+    if (lane == 0 && wg < (uint32_t)kMwMaxWg)
+        for (int i = 0; i < kMwSeg; ++i)
+            atomicAdd(&g_mw_stamps[(wg * kMwWaves + wave) * kMwSeg + i], (unsigned long long)mw_acc[i]);
+#endif
 
     // ---- state out (the next launch, the stats and the readers take it from HBM) ----
     if (own) {
         for (uint32_t i = lane; i < N; i += kWave) a.tn[n0 + i] = nodes[i];
         if (lane < kStWords) reinterpret_cast<uint32_t*>(&a.cl[c])[lane] = reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane];
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) a.sfin[sb + r * kWave + lane] = fin[r];
+        for (int r = 0; r < kRows; ++r) {
+            a.sfin[sb + r * kWave + lane] = fin[r];
+            a.snode[sb + r * kWave + lane] = pay[r];
+        }
     }
     if (wg == 0) {
         for (uint32_t g = threadIdx.x; g < C; g += kMwWaves * kWave) a.tr[g] = sh.trs[g];
         if (threadIdx.x == 0) {
-            TrCtl* ctl = a.ctl;  // (n_lent is counted in place by the lent-log appends)
+            TrCtl* ctl = a.ctl;
             ctl->T = sh.T;
             ctl->done = sh.done == 2u ? 1u : sh.done;
             ctl->ticks = sh.ticks;
             ctl->flags = sh.flags | (sh.done == 2u ? kTrFlagMwTimeout : 0u);
             ctl->n_trades = sh.n_trades;
             ctl->n_won = sh.n_won;
+            ctl->n_lent = sh.n_lent;
         }
     }
 }
@@ -716,10 +811,9 @@ bool trade_mw_shape(const TradeArgs& a) {
            (a.S == 4u * kWave || a.S == 8u * kWave || a.S == 16u * kWave);
 }
 
-size_t trade_mw_granules(uint32_t n_clusters) {
-    const uint32_t nwg = (n_clusters + kMwWaves - 1) / kMwWaves;
-    return ((size_t)n_clusters * (kX1Words + 1) + 2u * nwg + 1u) & ~(size_t)1;  // (16-byte multiple)
-}
+// X1 for 64 clusters, then X2 (64 lender words + 4 x 2 mask words) padded to 128: every sweep load
+// lies inside the block (a multiple of 16 bytes)
+size_t trade_mw_granules(uint32_t) { return (size_t)kTrResMaxClusters * kX1Words + 2u * kWave; }
 
 hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx, uint32_t tick_budget, size_t lds,
                            hipStream_t s) {
@@ -742,3 +836,12 @@ hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx, uint32_t 
 }
 
 }  // namespace mcs
+
+#ifdef MCS_STAMPS
+// the probe build's per-wave segment times (4 workgroups x 16 waves x 10 segments, 100 MHz ticks)
+extern "C" int mcs_debug_mw_stamps(unsigned long long* out) {
+    unsigned long long z[mcs::kMwMaxWg * mcs::kMwWaves * mcs::kMwSeg] = {};  // (768)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_mw_stamps), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_mw_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

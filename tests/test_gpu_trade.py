@@ -230,3 +230,20 @@ def test_gpu_trade_resident_equals_kernels_and_oracle(kind, C, J, pool, monkeypa
                   "ticks", "t_final", "flags"):
             assert res[m]["tstats"][f] == res["0"]["tstats"][f], (f, m)
     assert_trade_parity(arrays, streams, res["2"])
+
+
+def test_gpu_trade_resident_form_by_capacity(monkeypatch):
+    """The workgroup-resident tick packs a running slot's payload into 32 bits, so the engine picks
+    it only when every node's max(capacity, availability) is below 128 cores and 65536 memory: a
+    system with 200-core nodes runs the one-workgroup form instead, and both equal the oracle."""
+    from mcs_amd import GenParams, gen_streams_host, replicate, uniform_cluster
+    from mcs_amd.engine import scaled_lambda
+
+    monkeypatch.delenv("MCS_TRADE_RESIDENT", raising=False)
+    for cores, want in ((127, 4), (200, 3)):
+        arrays = replicate(uniform_cluster(64, cores=cores, memory=65535), 12)
+        gp = GenParams(seed=cores, arrival_mode=1, lam=scaled_lambda(64, load=1.1), max_cores=cores, max_mem=65535)
+        streams = gen_streams_host(gp, arrays, 1500)
+        g = gpu_trade(arrays, streams)
+        assert g["tstats"]["loop_form"] == want, cores
+        assert_trade_parity(arrays, streams, g)

@@ -1,0 +1,59 @@
+"""Segment times of the workgroup-resident lock-step tick (mcs_trade_mw.hip) from an MCS_STAMPS probe
+build (tools/build_asmvariant.sh mw_stamps multi-cluster-simulator_amd/csrc/mcs_trade_mw.hip
+-DMCS_STAMPS): per tick, each wave's time in phase A's segments (prefetch, releases, arrivals,
+decisions, sample + record), the X1 exchange (wave 0 sweeps, the others wait), phase B, its barrier,
+X2 + C/D (wave 0) and the loop barrier, on the C5 system (64 clusters x 256 nodes, jobs per cluster
+from argv).   usage: python tools/stamp_mw.py variants/libmcs_mw_stamps.so [jobs_per_cluster]"""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r'''
+import ctypes as C, json, os, sys
+sys.path.insert(0, os.path.join(os.environ["REPO"], "multi-cluster-simulator_amd"))
+from mcs_amd import Engine, GenParams, replicate, uniform_cluster
+from mcs_amd import _lib as L
+from mcs_amd.engine import scaled_lambda
+J = int(os.environ["JOBS"])
+eng = Engine(0, borrow=True, trader=True)
+eng.load_clusters(replicate(uniform_cluster(256), 64))
+eng.generate_jobs(GenParams(seed=1, arrival_mode=1, lam=scaled_lambda(256, load=0.9)), J)
+fn = L.lib().mcs_debug_mw_stamps
+buf = (C.c_ulonglong * 768)()
+eng.run(); fn(buf)
+st = eng.run(); assert fn(buf) == 0
+ts = eng.trade_stats()
+print(json.dumps({"ms": st.kernel_ms, "ticks": int(ts["ticks"]), "loop_form": int(ts["loop_form"]),
+                  "slot_pool": int(st.slot_pool), "s": list(buf)}))
+'''
+SEG = ["prefetch", "releases", "arrivals", "decisions", "sample+record", "X1_sweep_or_wait",
+       "phase_B", "barrier_B", "X2+CD", "barrier_loop"]
+
+
+def main():
+    lib = sys.argv[1]
+    jobs = sys.argv[2] if len(sys.argv) > 2 else "20000"
+    env = dict(os.environ, MCS_LIB=os.path.abspath(lib), REPO=REPO, JOBS=jobs)
+    out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=600)
+    if out.returncode:
+        print("FAILED", out.stderr[-2000:])
+        sys.exit(1)
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    ticks = d["ticks"]
+    s = d["s"]
+    per_wave = [[s[w * 12 + i] * 10.0 / 1e3 / ticks for i in range(10)] for w in range(64)]  # us per tick
+    passes = [(s[w * 12 + 10] / ticks, s[w * 12 + 11] / ticks) for w in range(0, 64, 16)]  # wave 0 of each wg
+    res = {"jobs_per_cluster": int(jobs), "ticks": ticks, "kernel_ms": round(d["ms"], 3),
+           "us_per_tick": round(d["ms"] * 1e3 / ticks, 3), "loop_form": d["loop_form"], "slot_pool": d["slot_pool"],
+           "us_per_tick_wg0_wave0": {SEG[i]: round(per_wave[0][i], 3) for i in range(10)},
+           "us_per_tick_wg0_wave5": {SEG[i]: round(per_wave[5][i], 3) for i in range(10)},
+           "us_per_tick_max_over_waves": {SEG[i]: round(max(w[i] for w in per_wave), 3) for i in range(10)},
+           "us_per_tick_mean_over_waves": {SEG[i]: round(sum(w[i] for w in per_wave) / 64, 3) for i in range(10)},
+           "sweep_passes_per_tick_x1_x2_by_wg": [[round(a, 2), round(b, 2)] for a, b in passes]}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
