@@ -381,13 +381,17 @@ def main_c5(args, world, rank, local_rank):
             },
             "roofline": {
                 "bound": "hbm",
-                "limiter": "launch/latency: a tick is dependent launches of a few us (DESIGN.md §9)",
+                "limiter": ("latency: the resident tick waits on the inter-workgroup X1 exchange (DESIGN.md §9)"
+                            if ts["loop_form"] >= 3 else
+                            "launch/latency: a tick is dependent launches of a few us (DESIGN.md §9)"),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": "lock-step tick (tr_step/tr_lend/tr_trader, one exchange), launch/latency-bound",
+                "kernel": ("tr_mw_kernel (resident tick, one workgroup per 16 clusters)" if ts["loop_form"] == 4 else
+                           "tr_resident_kernel (resident tick, one workgroup)" if ts["loop_form"] == 3 else
+                           "lock-step tick (tr_step/tr_lend/tr_trader, one exchange), launch/latency-bound"),
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "bytes_per_placement": BYTES_PER_PLACEMENT,
             },

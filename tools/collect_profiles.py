@@ -41,8 +41,12 @@ if stats:
 counters = {}
 launch_ns = []
 for g in sorted(glob.glob(f"{run}/pmc*_g*/pmc_counter_collection.csv")):
-    for r in fifo_rows(g):
-        counters[r["Counter_Name"]] = counters.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    rows = fifo_rows(g)
+    # a pass may hold more than one launch of the kernel (bench.py's untimed first launch):
+    # the counters are summed over each launch's rows and averaged over the launches
+    n_launch = max(len({r["Dispatch_Id"] for r in rows}), 1)
+    for r in rows:
+        counters[r["Counter_Name"]] = counters.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"]) / n_launch
         launch_ns.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 summary["pmc_per_launch"] = counters
 
