@@ -93,7 +93,9 @@ typedef struct mcs_trade_stats {
     uint32_t loop_form;    /* tick loop that ran: 0 = one engine, hipGraph-replayed ticks; 1 = RCCL
                               all-gather per tick, eager launches; 2 = RCCL, kernels and all-gathers
                               captured in a hipGraph (MCS_RCCL_GRAPH=0 forces 1); 3 = one
-                              engine, the whole system resident in one workgroup */
+                              engine, the whole system resident in one workgroup; 4 = resident,
+                              one workgroup per 16 clusters, exchange written through to memory;
+                              5 = the same with every workgroup on one XCD, exchange in its L2 */
     double kernel_ms;      /* device time of the lock-step loop (HIP events) */
     double wall_ms;
 } mcs_trade_stats;

@@ -51,6 +51,7 @@ constexpr uint32_t kLoopGraph = 0;      // one engine, ticks replayed from a cap
 constexpr uint32_t kLoopRcclEager = 1;  // RCCL all-gather per tick, launches enqueued eagerly
 constexpr uint32_t kLoopRcclGraph = 2;  // RCCL all-gather per tick, captured with the kernels
 constexpr uint32_t kLoopResident = 3;   // one engine, the whole system resident in one workgroup
+constexpr uint32_t kLoopResidentMwXcd = 5;  // the same, its workgroups on one XCD (L2 exchange)
 constexpr uint32_t kLoopResidentMw = 4;  // one engine, resident in ceil(C / 16) workgroups (granules)
 
 // Capture `ticks` ticks of `tick(stream)` (kernels and the RCCL all-gather) into one executable

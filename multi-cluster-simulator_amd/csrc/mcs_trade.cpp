@@ -28,7 +28,8 @@ struct TradeDev {
     unsigned long long* scm = nullptr;
     TrLq* lq = nullptr;
     unsigned char* xb = nullptr;
-    unsigned long long* gx = nullptr;  // the workgroup-resident tick's granules
+    unsigned long long* gx = nullptr;   // the workgroup-resident tick's granules (uncached)
+    unsigned long long* gxc = nullptr;  // ... and their cached twin (workgroups on one XCD)
     uint32_t* acc = nullptr;
     uint32_t* lqp = nullptr;
     uint32_t* fb = nullptr;
@@ -206,22 +207,29 @@ int run_local(mcs_engine* e) {
     if (rf == 2) {
         td->loop_form = kLoopResidentMw;
         if (!td->gx) {
-            // the granules live in uncached device memory (MTYPE UC): a poll that re-reads a line
-            // its XCD's L2 already holds would otherwise be served the stale copy until that line
-            // is evicted (measured: ~7 sweep passes per exchange with cached hipMalloc memory);
-            // MCS_MW_GX=0 keeps plain hipMalloc (A/B)
+            // two granule buffers: uncached device memory (MTYPE UC) for workgroups on different
+            // XCDs (a poll that re-reads a line its XCD's L2 already holds would otherwise be served
+            // the stale copy until that line is evicted: ~7 sweep passes per exchange measured with
+            // cached memory), and cached memory for workgroups that all run on one XCD, whose shared
+            // L2 serves the polls (the kernel checks the placement; MCS_MW_GX=0 makes both cached)
             const char* gxenv = getenv("MCS_MW_GX");
             const int gxm = gxenv ? atoi(gxenv) : 3;
             const size_t gb = trade_mw_granules(td->a.Ct) * 8u;
             if (gxm == 0) HIPCHK(e, hipMalloc(&td->gx, gb));
             else HIPCHK(e, hipExtMallocWithFlags((void**)&td->gx, gb, (unsigned)gxm));
+            HIPCHK(e, hipMalloc(&td->gxc, gb));
         }
+        // the workgroups 8 blocks apart: one XCD under the dispatcher's round-robin (MCS_MW_XCD=0:
+        // consecutive blocks, the write-through exchange)
+        const char* xenv = getenv("MCS_MW_XCD");
+        const bool xcd_pack = !xenv || atoi(xenv) != 0;
         for (;;) {
-            const hipError_t st = launch_trade_mw(td->a, td->gx, kResTicks, lds, e->stream);
+            const hipError_t st = launch_trade_mw(td->a, td->gx, td->gxc, kResTicks, lds, xcd_pack, e->stream);
             if (st != hipSuccess) return hip_fail(e, "resident tick kernel (workgroups)", st);
             if (int s = poll_ctl(e)) return s;
             if (td->h_ctl->flags & kTrFlagMwTimeout)
                 return fail(e, MCS_E_HIP, "resident tick: a workgroup exchange timed out");
+            td->loop_form = td->h_ctl->info ? kLoopResidentMwXcd : kLoopResidentMw;
             if (td->h_ctl->done) return MCS_OK;
         }
     }
@@ -365,6 +373,7 @@ void trade_free(mcs_engine* e) {
     dfree(td->lq);
     dfree(td->xb);
     dfree(td->gx);
+    dfree(td->gxc);
     dfree(td->acc);
     dfree(td->lqp);
     dfree(td->fb);

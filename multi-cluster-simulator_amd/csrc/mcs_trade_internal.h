@@ -85,6 +85,7 @@ struct TrLq {
 struct TrCtl {
     uint32_t T, done, ticks, flags;
     unsigned long long n_lent, n_trades, n_won;
+    uint32_t info, pad;  // info: the workgroup-resident tick exchanged through one XCD's L2 (1)
 };
 
 struct TradeArgs {
@@ -142,8 +143,12 @@ hipError_t launch_trade_resident(const TradeArgs& a, uint32_t tick_budget, size_
 bool trade_mw_shape(const TradeArgs& a);
 size_t trade_mw_lds(uint32_t ns);
 size_t trade_mw_granules(uint32_t n_clusters);
-hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx, uint32_t tick_budget, size_t lds,
-                           hipStream_t s);
+// the workgroups' XCD-id granules follow X1 (10 per cluster) and X2 (128) in the uncached buffer
+constexpr size_t trade_mw_xcc_off() { return (size_t)kTrResMaxClusters * 10u + 128u; }
+// gx_uc: uncached granules (any placement); gx_c: cached granules, used when every workgroup runs on
+// one XCD; xcd_pack: launch the workers 8 blocks apart (one XCD under round-robin dispatch)
+hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsigned long long* gx_c,
+                           uint32_t tick_budget, size_t lds, bool xcd_pack, hipStream_t s);
 constexpr uint32_t kTrFlagMwTimeout = 0x80000000u;  // internal: an exchange sweep gave up
 
 }  // namespace mcs

@@ -59,6 +59,20 @@ __device__ __forceinline__ uint64_t mld64(const unsigned long long* p) {
 __device__ __forceinline__ void put_granule(unsigned long long* g, uint32_t tag, uint32_t v) {
     __hip_atomic_store(g, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// the same granule when every workgroup of the launch runs on this XCD (checked at the start of the
+// launch from HW_REG_XCC_ID): a plain store keeps the line in the XCD's shared L2, where the readers'
+// agent-scope loads (L1 bypassed) find it, instead of dropping it to the fabric (write-through)
+// (inline asm: as an atomic store of a narrower scope, LLVM merged it with put_granule's store in
+// the other branch and kept the write-through one)
+__device__ __forceinline__ void put_granule_xcd(unsigned long long* g, uint32_t tag, uint32_t v) {
+    const unsigned long long x = ((unsigned long long)tag << 32) | v;
+    asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(g), "v"(x) : "memory");
+}
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 0xFu;
+}
 
 #ifdef MCS_STAMPS
 // the probe build's per-wave segment times (s_memrealtime, 100 MHz) summed over the launches since
@@ -117,21 +131,53 @@ struct MwShared {  // (this workgroup's node vectors follow: kMwWaves * ns u64)
     uint32_t capc[kMwWaves], capm[kMwWaves];
     uint32_t gtab[kMwWaves][64];
     uint32_t accm[2];  // borrowers some lender of this workgroup accepted this tick
-    uint32_t T, done, ticks, flags;
+    uint32_t T, done, ticks, flags, xcd;
     unsigned long long n_trades, n_won, n_lent;
 };
 
 template <int kRows>  // slot rows per cluster (64 slots each)
-__global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, unsigned long long* gx,
-                                                                 uint32_t tick_budget) {
+__global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, unsigned long long* gx_uc,
+                                                                 unsigned long long* gx_c, uint32_t tick_budget,
+                                                                 uint32_t nwg, uint32_t stride) {
+    // the workers are blocks 0, stride, 2 * stride, ...: with stride 8 they share one XCD under the
+    // dispatcher's observed round-robin placement (speed only: the check below decides the protocol)
+    if (blockIdx.x % stride != 0u) return;
     extern __shared__ unsigned long long mw_smem[];
     MwShared& sh = *reinterpret_cast<MwShared*>(mw_smem);
     unsigned long long* const nodes_wg = mw_smem + (sizeof(MwShared) + 7) / 8;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t C = a.Ct, ns = a.ns, S = a.S;
-    const uint32_t wg = blockIdx.x, nwg = gridDim.x;
+    const uint32_t wg = blockIdx.x / stride;
     const uint32_t c = wg * kMwWaves + wave;  // this wave's cluster
     const bool own = c < C;
+
+    // ---- the exchange protocol of this launch: every workgroup publishes its XCD id (write-through
+    // granule in uncached memory, valid under any placement); when all are equal the tick's granules
+    // use the cached buffer and plain stores (put_granule_xcd), else uncached memory and write-through
+    if (threadIdx.x < 64u) {
+        unsigned long long* const gid = gx_uc + trade_mw_xcc_off();
+        if (threadIdx.x == 0) put_granule(gid + wg, 1u, xcc_id());
+        uint32_t v = 0u;
+        bool ok = false;
+        for (uint32_t spins = 0; spins <= kSpinLimit; ++spins) {
+            const unsigned long long x = lane < nwg ? __hip_atomic_load(gid + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (1ull << 32);
+            v = (uint32_t)x;
+            if (__all((uint32_t)(x >> 32) == 1u)) {
+                ok = true;
+                break;
+            }
+        }
+        const uint32_t v0 = readlane(v, 0);
+        const bool same = ok && __all(lane >= nwg || v == v0);
+        if (threadIdx.x == 0) sh.xcd = same ? 1u : 0u;
+    }
+    __syncthreads();
+    const bool xcd = sh.xcd != 0u;
+    unsigned long long* const gx = xcd ? gx_c : gx_uc;
+    auto put = [&](unsigned long long* g, uint32_t tag, uint32_t v) {
+        if (xcd) put_granule_xcd(g, tag, v);
+        else put_granule(g, tag, v);
+    };
     unsigned long long* const gx1 = gx;  // [C][kX1Words] (room for 64 clusters)
     unsigned long long* const gx2 = gx + (size_t)kTrResMaxClusters * kX1Words;  // [C] lender words, [nwg][2]
 
@@ -437,7 +483,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             xv = lane == 7 ? (uint32_t)MST(flags) : xv;
             xv = lane == 8 ? (uint32_t)MST(cu) : xv;
             xv = lane == 9 ? (uint32_t)MST(mu) : xv;
-            if (lane < kX1Words) put_granule(gx1 + (size_t)c * kX1Words + lane, tag1, xv);
+            if (lane < kX1Words) put(gx1 + (size_t)c * kX1Words + lane, tag1, xv);
             if (lane < kStWords) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stv;
             // the next tick's records (only phase A moves these cursors; a WaitQueue head that C/D
             // moves to the BorrowedQueue leaves the ReadyQueue head inside the same window, or
@@ -605,7 +651,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                     atomicOr(&sh.accm[1], (uint32_t)(okm >> 32));
                 }
                 // this lender's LentQueue length (bit 31: the append overflowed) for C/D
-                put_granule(gx2 + L, tag2, lq_len | (fb ? 0x80000000u : 0u));
+                put(gx2 + L, tag2, lq_len | (fb ? 0x80000000u : 0u));
             }
             // the next tick's LentQueue head: an entry of an earlier tick is loaded; one this tick's
             // appends just wrote (the queue was empty) is taken from the request registers
@@ -629,7 +675,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
 
         // ---- X2 + phases C and D: wave 0 of every workgroup, one lane per cluster (C <= 64) ----
         if (wave == 0) {
-            if (lane < 2) put_granule(gx2 + C + 2u * wg + lane, tag2, sh.accm[lane]);
+            if (lane < 2) put(gx2 + C + 2u * wg + lane, tag2, sh.accm[lane]);
             const uint32_t nw = C + 2u * nwg;
             uint32_t lw = 0u, aw = 0u;  // lane g: cluster g's lender word; the OR of the masks
             for (uint32_t spins = 0;; ++spins) {
@@ -797,6 +843,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             ctl->n_trades = sh.n_trades;
             ctl->n_won = sh.n_won;
             ctl->n_lent = sh.n_lent;
+            ctl->info = sh.xcd;
         }
     }
 }
@@ -812,14 +859,17 @@ bool trade_mw_shape(const TradeArgs& a) {
 }
 
 // X1 for 64 clusters, then X2 (64 lender words + 4 x 2 mask words) padded to 128: every sweep load
-// lies inside the block (a multiple of 16 bytes)
-size_t trade_mw_granules(uint32_t) { return (size_t)kTrResMaxClusters * kX1Words + 2u * kWave; }
+// lies inside the block (a multiple of 16 bytes); then the workgroups' XCD ids (uncached buffer)
+size_t trade_mw_granules(uint32_t) { return trade_mw_xcc_off() + kWave; }
 
-hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx, uint32_t tick_budget, size_t lds,
-                           hipStream_t s) {
+hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsigned long long* gx_c,
+                           uint32_t tick_budget, size_t lds, bool xcd_pack, hipStream_t s) {
     const uint32_t nwg = (a.Ct + kMwWaves - 1) / kMwWaves;
+    const uint32_t stride = xcd_pack ? 8u : 1u, nblk = stride * (nwg - 1u) + 1u;
     // the granules carry epochs counted within the launch: zero them first
-    hipError_t st = hipMemsetAsync(gx, 0, trade_mw_granules(a.Ct) * 8u, s);
+    hipError_t st = hipMemsetAsync(gx_uc, 0, trade_mw_granules(a.Ct) * 8u, s);
+    if (st != hipSuccess) return st;
+    st = hipMemsetAsync(gx_c, 0, trade_mw_granules(a.Ct) * 8u, s);
     if (st != hipSuccess) return st;
     const void* fn = a.S == 4u * kWave   ? (const void*)tr_mw_kernel<4>
                      : a.S == 8u * kWave ? (const void*)tr_mw_kernel<8>
@@ -827,11 +877,14 @@ hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx, uint32_t 
     st = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (st != hipSuccess) return st;
     if (a.S == 4u * kWave)
-        hipLaunchKernelGGL(tr_mw_kernel<4>, dim3(nwg), dim3(kMwWaves * kWave), lds, s, a, gx, tick_budget);
+        hipLaunchKernelGGL(tr_mw_kernel<4>, dim3(nblk), dim3(kMwWaves * kWave), lds, s, a, gx_uc, gx_c, tick_budget,
+                           nwg, stride);
     else if (a.S == 8u * kWave)
-        hipLaunchKernelGGL(tr_mw_kernel<8>, dim3(nwg), dim3(kMwWaves * kWave), lds, s, a, gx, tick_budget);
+        hipLaunchKernelGGL(tr_mw_kernel<8>, dim3(nblk), dim3(kMwWaves * kWave), lds, s, a, gx_uc, gx_c, tick_budget,
+                           nwg, stride);
     else
-        hipLaunchKernelGGL(tr_mw_kernel<16>, dim3(nwg), dim3(kMwWaves * kWave), lds, s, a, gx, tick_budget);
+        hipLaunchKernelGGL(tr_mw_kernel<16>, dim3(nblk), dim3(kMwWaves * kWave), lds, s, a, gx_uc, gx_c, tick_budget,
+                           nwg, stride);
     return hipGetLastError();
 }
 

@@ -700,7 +700,7 @@ __global__ __launch_bounds__(kResWaves * kWave) void tr_resident_kernel(TradeArg
         }
     }
     if (threadIdx.x == 0) {
-        TrCtl ctl;
+        TrCtl ctl{};
         ctl.T = sh.T;
         ctl.done = sh.done;
         ctl.ticks = sh.ticks;
