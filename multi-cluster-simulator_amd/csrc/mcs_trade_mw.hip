@@ -15,19 +15,21 @@
 //      samples for C/D)
 //   B  each wave, its cluster as lender: Lend (strict '>', scheduler.go:194-202) against the
 //      tick's requests in borrower order, LentQueue appends (server.go:80-113); the workgroup's
-//      acceptances (a borrower mask) and its lenders' LentQueue lengths are published
-//   X2 wave 0 of every workgroup gathers them
-//   C+D wave 0 of EVERY workgroup, on identical inputs: the borrowers' BorrowedQueue moves (the
-//      owner workgroup writes them), the trader rounds (trader.go:280-325, 193-278;
-//      server.go:31-85) and the next tick — the trader state is replicated, so the workgroups
-//      agree on the clock without a third exchange.
+//      acceptances (a borrower mask) and an append-overflow bit are published (X2)
+//   C+D wave 0 of EVERY workgroup, on identical inputs from X1: the trader rounds
+//      (trader.go:280-325, 193-278; server.go:31-85) and the next tick — the trader state is
+//      replicated, so the workgroups agree on the clock without another exchange
+//   X2 at the start of the next tick, wave 0 of every workgroup gathers the acceptances and the
+//      owner workgroup applies its borrowers' BorrowedQueue moves (C/D does not wait for them).
 // Exchange: the data is the flag (cdna_hip_programming.md Guideline 16, R2): every word travels
 // as an 8-byte granule {value, tag} stored write-through (agent-scope atomic store) with
 // tag = the exchange's epoch within the launch (2 * tick + 1 for X1, + 2 for X2); the gathering
 // wave re-reads its granules (agent-scope atomic loads) until every tag matches.  A workgroup
-// publishes X1 of tick n + 1 only after its C/D of tick n, which needed every workgroup's X2 of
-// tick n, which each published after its own X1 sweep of tick n: so a granule is never
-// overwritten before every workgroup has read it.  The engine zeroes the granules before each
+// publishes X1 of tick n + 1 only after gathering X2 of tick n, which every workgroup published
+// after its own X1 sweep of tick n; and it publishes X2 of tick n + 1 only after its X1 sweep of
+// tick n + 1, which needed every workgroup's X1 of tick n + 1, each published after that
+// workgroup's X2 gather of tick n: so a granule is never overwritten before every workgroup has
+// read it.  The engine zeroes the granules before each
 // launch; every sweep is bounded (a timeout stops the run with an internal error).
 // Same results bit for bit as the three-kernel tick and the one-workgroup resident tick
 // (tests/test_gpu_trade.py).
@@ -130,8 +132,8 @@ struct MwShared {  // (this workgroup's node vectors follow: kMwWaves * ns u64)
     TrCluster st[kMwWaves];
     uint32_t capc[kMwWaves], capm[kMwWaves];
     uint32_t gtab[kMwWaves][64];
-    uint32_t accm[2];  // borrowers some lender of this workgroup accepted this tick
-    uint32_t T, done, ticks, flags, xcd;
+    uint32_t accm[3];  // borrowers some lender of this workgroup accepted this tick; [2]: an append overflowed
+    uint32_t T, done, ticks, flags, xcd, tmax_now;
     unsigned long long n_trades, n_won, n_lent;
 };
 
@@ -267,7 +269,69 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
     uint64_t mw_last = wall_clock64();
 #endif
 
+    // X2 of tick n at the start of tick n + 1 (and after the last tick of the launch): wave 0 gathers
+    // every workgroup's borrower masks; the owner workgroup moves its accepted borrowers' WaitQueue
+    // heads to the BorrowedQueue (scheduler.go:237-242) with tick n's clock Tn; an append overflow
+    // ends the run at tick n, as the three-kernel tick does (clock Tn, no T_MAX flag of that tick)
+    auto x2_apply = [&](uint32_t tg, uint32_t Tn) {
+        if (wave == 0) {
+            const uint32_t nw = 3u * nwg;
+            unsigned long long x = 0ull;
+            bool got = false;
+            for (uint32_t spins = 0; spins <= kSpinLimit; ++spins) {
+                x = lane < nw ? __hip_atomic_load(gx2 + lane, __ATOMIC_RELAXED, MW_LOAD_SCOPE) : ((unsigned long long)tg << 32);
+#ifdef MCS_STAMPS
+                mw_acc[11] += 1u;
+#endif
+                if (__all((uint32_t)(x >> 32) == tg)) {
+                    got = true;
+                    break;
+                }
+            }
+            if (!got) {
+                timed_out = true;
+                if (lane == 0) sh.done = 2u;
+            } else {
+                const uint32_t v = (uint32_t)x, k = lane % 3u;
+                uint32_t m0 = lane < nw && k == 0u ? v : 0u, m1 = lane < nw && k == 1u ? v : 0u,
+                         fb = lane < nw && k == 2u ? v : 0u;
+                for (int o = 32; o > 0; o >>= 1) {
+                    m0 |= (uint32_t)__shfl_xor((int)m0, o);
+                    m1 |= (uint32_t)__shfl_xor((int)m1, o);
+                    fb |= (uint32_t)__shfl_xor((int)fb, o);
+                }
+                const uint32_t g = lane;
+                const bool acc = ((g < 32u ? m0 >> g : m1 >> (g - 32u)) & 1u) != 0u;
+                if (acc && g < C && g / kMwWaves == wg && sh.rq_job[g] != kEmpty) {
+                    const uint32_t rj = sh.rq_job[g];
+                    const uint64_t gj0 = sh.j0[g];
+                    a.out_node[gj0 + rj] = MCS_NODE_BORROWED;
+                    a.out_start[gj0 + rj] = Tn;
+                    a.out_finish[gj0 + rj] = MCS_TIME_NONE;
+                    TrCluster& s = sh.st[g - wg * kMwWaves];
+                    s.has_w = 0u;
+                    ++s.decided;
+                    ++s.borrowed;
+                }
+                if (fb && lane == 0) {
+                    uint32_t f = sh.flags | MCS_FLAG_LENT_OVERFLOW;
+                    if (sh.tmax_now) f &= ~MCS_FLAG_T_MAX;
+                    sh.flags = f;
+                    sh.T = Tn;
+                    sh.done = 1u;
+                }
+            }
+        }
+        __syncthreads();
+    };
+    bool pend = false;  // a tick's X2 not applied yet
+    uint32_t pend_tag = 0u, pend_T = 0u;
+
     for (uint32_t it = 0; it < tick_budget; ++it) {
+        if (pend) {
+            x2_apply(pend_tag, pend_T);
+            pend = false;
+        }
         if (sh.done) break;
         MW_MARK(9);
         const uint32_t T = sh.T;
@@ -476,7 +540,8 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             xv = lane == 1 ? req.c : xv;
             xv = lane == 2 ? req.m : xv;
             xv = lane == 3 ? req.dur : xv;
-            const uint32_t qs = (MST(has_w) ? 1u : 0u) | (MST(rq_head) < MST(next_arr) ? 2u : 0u) | lent_now;
+            const uint32_t qs = (MST(has_w) ? 1u : 0u) | (MST(rq_head) < MST(next_arr) ? 2u : 0u) | lent_now |
+                                (MST(lq_len) > 0u ? 8u : 0u);
             xv = lane == 4 ? qs : xv;
             xv = lane == 5 ? (uint32_t)MST(decided) : xv;
             xv = lane == 6 ? nat : xv;
@@ -538,7 +603,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                     }
                 }
             }
-            if (lane < 2) sh.accm[lane] = 0u;
+            if (lane < 3) sh.accm[lane] = 0u;
             if (timed_out && lane == 0) sh.done = 2u;
         }
         __syncthreads();
@@ -650,8 +715,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                     atomicOr(&sh.accm[0], (uint32_t)okm);
                     atomicOr(&sh.accm[1], (uint32_t)(okm >> 32));
                 }
-                // this lender's LentQueue length (bit 31: the append overflowed) for C/D
-                put(gx2 + L, tag2, lq_len | (fb ? 0x80000000u : 0u));
+                if (fb) atomicOr(&sh.accm[2], 1u);
             }
             // the next tick's LentQueue head: an entry of an earlier tick is loaded; one this tick's
             // appends just wrote (the queue was empty) is taken from the request registers
@@ -673,60 +737,20 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
         __syncthreads();
         MW_MARK(7);
 
-        // ---- X2 + phases C and D: wave 0 of every workgroup, one lane per cluster (C <= 64) ----
+        // ---- phases C and D: wave 0 of every workgroup, one lane per cluster (C <= 64) ----
+        // They need nothing from phase B: every borrow request leaves its borrower busy (its WaitQueue
+        // head, or the lender's LentQueue when accepted) and not done, so the next tick's clock and
+        // the end of the run follow from X1 alone (queue bits: WaitQueue, ReadyQueue, LentQueue
+        // after A); the acceptances (X2: the workgroup's borrower masks and append-overflow bit) are
+        // published here and applied at the start of the next tick (x2_apply), while C/D runs
         if (wave == 0) {
-            if (lane < 2) put(gx2 + C + 2u * wg + lane, tag2, sh.accm[lane]);
-            const uint32_t nw = C + 2u * nwg;
-            uint32_t lw = 0u, aw = 0u;  // lane g: cluster g's lender word; the OR of the masks
-            for (uint32_t spins = 0;; ++spins) {
-                bool ok = true;
-                uint32_t m0 = 0u, m1 = 0u;
-                // (nw <= 72: two granules per lane, both loads issued before the first compare)
-                const uint32_t i0 = lane, i1 = lane + kWave;
-                const unsigned long long x0 = __hip_atomic_load(gx2 + i0, __ATOMIC_RELAXED, MW_LOAD_SCOPE);
-                const unsigned long long x1 = __hip_atomic_load(gx2 + i1, __ATOMIC_RELAXED, MW_LOAD_SCOPE);
-                ok = (i0 >= nw || (uint32_t)(x0 >> 32) == tag2) && (i1 >= nw || (uint32_t)(x1 >> 32) == tag2);
-                if (i0 < C) lw = (uint32_t)x0;
-                else if (i0 < nw) (((i0 - C) & 1u) == 0u ? m0 : m1) |= (uint32_t)x0;
-                if (i1 < nw) (((i1 - C) & 1u) == 0u ? m0 : m1) |= (uint32_t)x1;
-#ifdef MCS_STAMPS
-                mw_acc[11] += 1u;
-#endif
-                if (__all(ok)) {
-                    for (int o = 32; o > 0; o >>= 1) {
-                        m0 |= (uint32_t)__shfl_xor((int)m0, o);
-                        m1 |= (uint32_t)__shfl_xor((int)m1, o);
-                    }
-                    aw = lane < 32u ? (m0 >> lane) & 1u : (m1 >> (lane - 32u)) & 1u;
-                    break;
-                }
-                if (spins > kSpinLimit) {
-                    timed_out = true;
-                    break;
-                }
-            }
+            if (lane < 3) put(gx2 + 3u * wg + lane, tag2, sh.accm[lane]);
             const uint32_t g = lane;
             float cu = 0.0f, mu = 0.0f;
             uint32_t tot_c = 0u, tot_m = 0u, busy = 0u, next_arr_t = kEmpty, done_g = 1u, fl = 0u;
             TrTrader t{0u, 0u, 0u, kEmpty, 0u};
             if (g < C && !timed_out) {
-                const uint32_t qs = sh.qs[g], lq = lw & 0x7FFFFFFFu, fbg = (lw >> 31) ? MCS_FLAG_LENT_OVERFLOW : 0u;
-                uint32_t has_w = qs & 1u, decided = sh.decided[g];
-                const uint32_t rj = sh.rq_job[g];
-                if (rj != kEmpty && aw) {  // BorrowedQueue append (scheduler.go:237-242)
-                    has_w = 0u;
-                    ++decided;
-                    if (g / kMwWaves == wg) {  // (the owner workgroup writes it)
-                        const uint64_t gj0 = sh.j0[g];
-                        a.out_node[gj0 + rj] = MCS_NODE_BORROWED;
-                        a.out_start[gj0 + rj] = T;
-                        a.out_finish[gj0 + rj] = MCS_TIME_NONE;
-                        TrCluster& s = sh.st[g - wg * kMwWaves];
-                        s.has_w = 0u;
-                        ++s.decided;
-                        ++s.borrowed;
-                    }
-                }
+                const uint32_t qs = sh.qs[g], has_w = qs & 1u, lq = (qs >> 3) & 1u, decided = sh.decided[g];
                 cu = sh.cu[g];
                 mu = sh.mu[g];
                 tot_c = sh.total_c[g];
@@ -734,7 +758,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                 busy = (has_w || lq > 0u || (qs & 2u)) ? 1u : 0u;
                 next_arr_t = sh.next_arr_t[g];
                 done_g = (decided == sh.J[g] && lq == 0u) ? 1u : 0u;
-                fl = sh.xflags[g] | fbg;
+                fl = sh.xflags[g];
                 t = sh.trs[g];
             }
             unsigned long long n_trades = sh.n_trades, n_won = sh.n_won;
@@ -793,6 +817,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                 uint32_t flags = sh.flags | fl | lflags;
                 uint32_t done = 0, Tn = T;
                 const uint32_t fatal = MCS_FLAG_OVERFLOW | MCS_FLAG_LENT_OVERFLOW;
+                sh.tmax_now = 0u;
                 if (timed_out) {
                     done = 2u;
                 } else if (done_all || (flags & fatal)) {
@@ -800,6 +825,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                 } else if (T >= a.t_max || (!busy_any && nxt == kEmpty)) {
                     done = 1u;
                     flags |= MCS_FLAG_T_MAX;
+                    sh.tmax_now = 1u;
                 } else {
                     Tn = (busy_any || nxt <= T + 1u) ? T + 1u : nxt;
                 }
@@ -815,7 +841,11 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
         MW_MARK(8);
         __syncthreads();
         if (sh.done == 2u) break;
+        pend = true;
+        pend_tag = tag2;
+        pend_T = T;
     }
+    if (pend && sh.done != 2u) x2_apply(pend_tag, pend_T);
 #ifdef MCS_STAMPS
     if (lane == 0 && wg < (uint32_t)kMwMaxWg)
         for (int i = 0; i < kMwSeg; ++i)
