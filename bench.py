@@ -94,10 +94,12 @@ def parse():
     }[a.config]
     a.clusters = a.clusters or defaults[0]
     a.jobs_per_cluster = a.jobs_per_cluster or defaults[1]
+    a.cpu_sample_explicit = a.cpu_sample_clusters != 0
     a.cpu_sample_clusters = a.cpu_sample_clusters or defaults[2]
     if a.traffic_json is None:
         a.traffic_json = os.path.join(REPO, "profiles", "traffic_latest" + ("_delay" if a.policy == "delay" else "")
-                                      + ("_fused" if a.gen == "fused" else "") + ".json")
+                                      + ("_fused" if a.gen == "fused" else "")
+                                      + (f"_lam{a.lam:g}_dur{a.max_dur}" if a.lam or a.max_dur != 600 else "") + ".json")
     return a
 
 
@@ -138,6 +140,7 @@ def usable_cpus():
     return max(1, min(n, int(q + 0.5))) if q else n
 
 
+CPU_BUDGET_S = 15.0  # target wall time of one CPU baseline sample (the pilot sizes it)
 NAIVE = ("the CPU oracle is the deliberately naive restatement of the Go loop (it rescans the running "
          "list on every pass); it is a reported baseline, not the target")
 
@@ -494,16 +497,30 @@ def cpu_baseline(args, wl, n_threads, sample_clusters=None):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_ref as O
 
-    if sample_clusters is not None:
-        args = argparse.Namespace(**{**vars(args), "cpu_sample_clusters": sample_clusters})
-    arrays, streams, k = wl.cpu_sample(args)
     O.lib()
-    t0 = time.perf_counter()
-    if args.policy == "delay":
-        O.delay_run_batch(arrays, streams, n_threads=n_threads)
-    else:
-        O.fifo_run_batch(arrays, streams, n_threads=n_threads)
-    dt = time.perf_counter() - t0
+
+    def run(a):
+        arrays, streams, k = wl.cpu_sample(a)
+        t0 = time.perf_counter()
+        if a.policy == "delay":
+            O.delay_run_batch(arrays, streams, n_threads=n_threads)
+        else:
+            O.fifo_run_batch(arrays, streams, n_threads=n_threads)
+        return streams, k, time.perf_counter() - t0
+
+    def with_k(k):
+        return argparse.Namespace(**{**vars(args), "cpu_sample_clusters": k})
+
+    if sample_clusters is not None:
+        args = with_k(sample_clusters)
+    elif not getattr(args, "cpu_sample_explicit", True) and args.cpu_sample_clusters > 2 * n_threads:
+        # keep the sample to about CPU_BUDGET_S of work whatever the stream (a Level1-heavy DELAY
+        # stream costs the naive oracle ~100x more per job): a pilot on 2 clusters per thread
+        k0 = 2 * n_threads
+        _, _, dt0 = run(with_k(k0))
+        k = int(k0 * CPU_BUDGET_S / max(dt0, 1e-6)) // n_threads * n_threads
+        args = with_k(max(k0, min(args.cpu_sample_clusters, k)))
+    streams, k, dt = run(args)
     src = "oracle/mcs_oracle_delay.c" if args.policy == "delay" else "oracle/mcs_oracle.c"
     return {
         "value": streams.n_jobs / dt,
@@ -513,6 +530,7 @@ def cpu_baseline(args, wl, n_threads, sample_clusters=None):
         "sample": f"{k} of {wl.per} clusters ({wl.spec_name}) x {wl.J} jobs ({streams.n_jobs} placements), "
                   f"{src} -O3, OpenMP over clusters on {n_threads} thread(s), {dt:.2f} s wall; {NAIVE}",
         "seconds": dt,
+        "sample_clusters": k,
         "host": host_info(n_threads),
     }
 
@@ -587,6 +605,13 @@ def main_batch(args, world, rank, local_rank):
         diag.pop("waited_frac")
         diag["delay_iterations_per_job"] = diag.pop("loop_passes_per_job")
         diag["level1_moved_frac"] = float(ds["moved_l1"].sum()) / max(n_jobs, 1)
+        handed = int((ds["moved_l1"] > 0).sum())
+        if kernel_name == "mcs::delay_asm_kernel" and handed:
+            # the hand-scheduled loop stops a cluster at its first Level1 move and the engine
+            # re-runs it on delay_kernel: both launches are in kernel_ms
+            diag["clusters_handed_to_delay_kernel"] = handed
+            kernel_name = (f"mcs::delay_asm_kernel + mcs::delay_kernel ({handed} of {wl.per} clusters handed over "
+                           f"at their first Level1 move)")
         diag["level1_peak_max"] = int(ds["peak_l1"].max())
         diag["avg_wait_s"] = float(ds["total_wait_ms"].sum()) / max(float(ds["jobs_count"].sum()), 1.0) / 1e3
 
@@ -599,8 +624,8 @@ def main_batch(args, world, rank, local_rank):
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if (tj.get("clusters"), tj.get("nodes"), tj.get("jobs_per_cluster"), tj.get("policy", "fifo"),
-                    tj.get("gen", "stream"), tj.get("config", "c4")) == \
-                    (wl.per, args.nodes, wl.J, args.policy, args.gen, args.config):
+                    tj.get("gen", "stream"), tj.get("config", "c4"), tj.get("lam", 0.0), tj.get("max_dur", 600)) == \
+                    (wl.per, args.nodes, wl.J, args.policy, args.gen, args.config, args.lam, args.max_dur):
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -613,7 +638,7 @@ def main_batch(args, world, rank, local_rank):
             n_vis = host_info(0)["host_usable_cpus"] or 1
             if args.config != "c2" and not args.cpu_threads and n_vis > n_thr:
                 # one thread per visible cpu as well (oversubscribed under the cgroup quota)
-                sec = cpu_baseline(args, wl, n_vis)
+                sec = cpu_baseline(args, wl, n_vis, sample_clusters=cpu["sample_clusters"])
                 cpu["secondary_all_visible_cpus"] = {k: sec[k] for k in ("value", "cores", "sample", "seconds")}
         value = placed_all / elapsed_max
         metric = {"c4": "job placements/sec (whole node) at 4096 clusters x 256 nodes",
@@ -639,6 +664,8 @@ def main_batch(args, world, rank, local_rank):
                 "nodes": int(wl.arrays.node_off[1] - wl.arrays.node_off[0]),
                 "jobs_per_cluster": wl.J,
                 "gen": args.gen,
+                "lam": args.lam,  # 0: the scaled rate of the workload string
+                "max_dur": args.max_dur,
                 "placements_per_step_per_gpu": placements_per_launch,
                 "parallelism": (f"dp{world}: " + ("one system's clusters split over the GPUs" if wl.scaling == "strong"
                                                   else "independent replicas per GPU")

@@ -20,13 +20,15 @@
 //     overflows): {cores | mem << 32} and {job | dur << 32}, 16 B per entry.  A pass reads it 64
 //     entries per coalesced load (sc1: served by L2, never a stale L1 line of this CU) and
 //     compacts it in the same sweep, so removals cost no extra pass;
-//   * a per-lane fit filter rejects most Level1 entries without a first fit: for clusters of up
-//     to 128 nodes lane l holds best[l] = max free memory over nodes with min(free cores, 63) >= l
-//     (an LDS ds_max_u32 histogram + a wave suffix max), so job (c, m) can fit iff c <= max free
-//     cores and best[min(c, 63)] >= m (exact for c < 63, conservative above); bigger clusters use
-//     the two per-resource maxima, keeping fifo_kernel's 10 KB of LDS per wave (16 waves per CU).
-//     Resources only shrink inside a pass, so a job rejected at the start of the pass stays
-//     rejected; the survivors get a real first fit in list order;
+//   * a per-lane fit filter rejects every Level1 entry that fits no node without a first fit:
+//     lane l holds best[l] = max free memory over nodes with min(free cores, 63) >= l (an LDS
+//     ds_max_u32 histogram + a wave suffix max), so job (c, m) can fit iff c <= max free cores and
+//     best[min(c, 63)] >= m (exact for c < 63, conservative above).  Clusters of > 128 nodes
+//     build it in 256 B borrowed from the running-slot rows (fifo_kernel's 10 KB of LDS per wave,
+//     16 waves per CU); the filter is rebuilt only after a commit or a release (r03: the
+//     per-resource maxima it replaced let ~88 first fits through per placement on a Level1-heavy
+//     stream).  Resources only shrink inside a pass, so a job rejected at the start of the pass
+//     stays rejected; the survivors get a real first fit in list order;
 //   * Level0 results leave in 64-job register batches (masked: moved jobs are written when Level1
 //     places them); Level1 results are three single-lane stores.
 // Fast-forward: after an iteration that placed and moved nothing, the next iteration that can
@@ -55,6 +57,23 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     MCS_DPP_MAX(0x143, 0xc)
 #undef MCS_DPP_MAX
     return readlane(v, 63);
+}
+
+// inclusive prefix max over the wave (lane i: max of lanes 0..i), the DPP steps of wave_max_u32
+__device__ __forceinline__ uint32_t wave_prefix_max_u32(uint32_t v) {
+#define MCS_DPP_MAX(CTRL, RM)                                                                      \
+    {                                                                                              \
+        const uint32_t w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xf, false); \
+        v = w > v ? w : v;                                                                         \
+    }
+    MCS_DPP_MAX(0x111, 0xf)
+    MCS_DPP_MAX(0x112, 0xf)
+    MCS_DPP_MAX(0x114, 0xf)
+    MCS_DPP_MAX(0x118, 0xf)
+    MCS_DPP_MAX(0x142, 0xa)
+    MCS_DPP_MAX(0x143, 0xc)
+#undef MCS_DPP_MAX
+    return v;
 }
 
 // HBM scratch of the Level1 list, read by the wave that wrote it: bypass this CU's vector L1.
@@ -133,6 +152,10 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     uint64_t wacc = 0, l1_t = 0, mv_a = 0;
     uint32_t ovf = 0u;  // a finish time left the u32 clock range (recorded in VALU)
     bool live = true;
+    // the Level1 fit filter (lane l: best[l]) and the largest free core count, valid until a
+    // commit or a release (hdirty)
+    uint32_t best = 0u, max_c = 0u;
+    bool hdirty = true;
     if constexpr (HOR) {  // resume from the previous horizon
         const OnlineState st = a.on.st_in[ci];
         if (st.valid) {
@@ -235,6 +258,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         }
         used -= nexp;
         minf = wave_min_u32(lmin);
+        hdirty = true;
     };
 
     // ScheduleJob (scheduler.go:127-139): lowest node index with both >=
@@ -259,6 +283,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         const uint64_t need = (uint64_t)jc | ((uint64_t)jm << 32);
         const uint64_t any = __ballot(frm != 0u);
         if (!any) return false;  // pool overflow: the run stops and the cluster is re-run
+        hdirty = true;
         if (lane == (uint32_t)__builtin_ctzll(any)) {  // the slot's lane also commits the node
             __hip_atomic_fetch_sub(&nodes[k], need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             const uint32_t ad = (uint32_t)__builtin_ctz(frm) * kWave + lane;
@@ -273,6 +298,51 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         peak = used > peak ? used : peak;
         minf = fin < minf ? fin : minf;
         return true;
+    };
+
+    // the Level1 fit filter (scheduler.go:305, ScheduleJob's outcome without its node): lane i
+    // holds best[63 - i] = max free memory over nodes with min(free cores, 63) >= 63 - i, so job
+    // (c, m) fits some node iff c <= max_c and best[min(c, 63)] >= m (exact for c < 63).  An LDS
+    // ds_max_u32 histogram over the reversed core keys, then a DPP inclusive prefix max.  Clusters
+    // of <= 128 nodes own 256 B of LDS for it; bigger ones keep fifo_kernel's 10 KB per wave (16
+    // waves per CU) and borrow the first 256 B of the running slots' {node | finish} rows: each
+    // lane saves its own word and puts it back (the wave is the workgroup, nothing reads them in
+    // between)
+    auto build_filter = [&]() __attribute__((always_inline)) {
+        hdirty = false;
+        asm volatile("" ::: "memory");  // other lanes' commits and releases since
+        uint32_t mc = 0u;
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) {
+            const uint32_t fc = (uint32_t)nodes[k * kWave + lane];
+            if (nid[k] != kEmpty) mc = fc > mc ? fc : mc;
+        }
+        max_c = wave_max_u32(mc);
+        uint32_t* hist;
+        if constexpr (kHist) {
+            __shared__ uint32_t hist_own[kWave];
+            hist = hist_own;
+        } else {
+            hist = reinterpret_cast<uint32_t*>(pay_nf);
+        }
+        const uint32_t haddr = lds_addr(hist) + lane * 4u;
+        uint32_t saved = 0u;
+        if constexpr (!kHist)
+            asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(saved) : "v"(haddr) : "memory");
+        asm volatile("ds_write_b32 %0, %1" ::"v"(haddr), "v"(0u) : "memory");
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) {
+            const uint64_t v = nodes[k * kWave + lane];
+            const uint32_t fc = (uint32_t)v;
+            if (nid[k] != kEmpty) atomicMax(&hist[63u - (fc < 63u ? fc : 63u)], (uint32_t)(v >> 32));
+        }
+        // the histogram is written by other lanes: without a fence the compiler may forward this
+        // lane's own 0 store to the load below (it reasons per thread)
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        uint32_t v;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(haddr) : "memory");
+        if constexpr (!kHist) asm volatile("ds_write_b32 %0, %1" ::"v"(haddr), "v"(saved) : "memory");
+        best = wave_prefix_max_u32(v);
     };
 
     // writes the Level0 results of batch [base, base + 64); `cur` holds that batch's records
@@ -305,43 +375,9 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
 
         // ---- Level1 pass (scheduler.go:302-329) ----
         if (l1n != 0u) {
-            // fit filter, lane l: best = max free mem over nodes with min(free cores, 63) >= l.
-            // Exact histogram + suffix max for clusters of <= 128 nodes; bigger clusters keep
-            // their LDS budget at 16 waves per CU and use the per-resource maxima instead
-            // (conservative: survivors still get a real first fit).
-            uint32_t mc = 0u, mm = 0u;
-#pragma unroll
-            for (int k = 0; k < NPL; ++k) {
-                const uint64_t v = nodes[k * kWave + lane];
-                const uint32_t fc = (uint32_t)v, fm = (uint32_t)(v >> 32);
-                if (nid[k] != kEmpty) {
-                    mc = fc > mc ? fc : mc;
-                    mm = fm > mm ? fm : mm;
-                }
-            }
-            const uint32_t max_c = wave_max_u32(mc);
-            uint32_t best;
-            if constexpr (kHist) {
-                __shared__ uint32_t hist[kWave];
-                hist[lane] = 0u;
-#pragma unroll
-                for (int k = 0; k < NPL; ++k) {
-                    const uint64_t v = nodes[k * kWave + lane];
-                    const uint32_t fc = (uint32_t)v;
-                    if (nid[k] != kEmpty) atomicMax(&hist[fc < 63u ? fc : 63u], (uint32_t)(v >> 32));
-                }
-                // the histogram is written by other lanes: without a fence the compiler may
-                // forward this lane's own 0 store to the load below (it reasons per thread)
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-                best = hist[lane];
-#pragma unroll
-                for (int o = 1; o < kWave; o <<= 1) {
-                    const uint32_t w = (uint32_t)__shfl_down((int)best, o);
-                    best = (lane + o < (uint32_t)kWave && w > best) ? w : best;
-                }
-            } else {
-                best = wave_max_u32(mm);
-            }
+            // the fit filter (build_filter) is rebuilt when a commit or a release changed the
+            // nodes since the last build, and after every placement of the pass
+            if (hdirty) build_filter();
 
             uint32_t wr = 0u, skip = kEmpty;
             for (uint32_t base = 0; base < l1n && !stop; base += kWave) {
@@ -350,7 +386,10 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                 const uint64_t cm = live ? ld_l2(l1_cm + pos) : 0ull;
                 const uint64_t jdv = live ? ld_l2(l1_jd + pos) : 0ull;
                 const uint32_t c = (uint32_t)cm, m = (uint32_t)(cm >> 32);
-                const uint32_t bm = kHist ? (uint32_t)__shfl((int)best, (int)(c < 63u ? c : 63u)) : best;
+                const uint32_t key = 63u - (c < 63u ? c : 63u);
+                // the lookup outside the && (a ds_bpermute under a partial exec mask reads 0 from
+                // the disabled lanes that hold the filter)
+                uint32_t bm = (uint32_t)__shfl((int)best, (int)key);
                 uint64_t cand = __ballot(live && c <= max_c && bm >= m);
                 uint64_t rem = 0ull;
                 while (cand) {
@@ -376,6 +415,12 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                     }
                     rem |= 1ull << b;
                     skip = base + b + 1u;
+                    // the commit shrank node k: the rest of this row is re-tested on the rebuilt
+                    // filter (the stale one let every entry that only fitted k's old room through
+                    // to a failing first fit: ~29 per placement on a Level1-heavy stream)
+                    build_filter();
+                    bm = (uint32_t)__shfl((int)best, (int)key);
+                    cand &= __ballot(live && c <= max_c && bm >= m);
                     ++placed;
                     ++placed_l1;
                     l1_t += t;

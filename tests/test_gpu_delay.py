@@ -180,3 +180,22 @@ def test_gpu_delay_hand_scheduled_loop(kind, diag, monkeypatch):
         assert (got[5]["moved_l1"] == 0).all()  # (no cluster needed the compiled kernel)
     if kind.startswith("fuzz"):
         assert (got[5]["moved_l1"] > 0).any()
+
+
+@pytest.mark.parametrize("nodes", [64, 128, 200, 256, 512])
+def test_gpu_delay_level1_heavy_generated(nodes):
+    """The Level1-heavy bench stream (bench.py --policy delay --lam 0.95 --max-dur 972: fewer than
+    one arrival per second at 90 % memory load, so heads wait MaxWaitTime and ~70 % of the jobs
+    move to Level1) at reduced size, through every node-count class of delay_kernel (NPL 1, 2, 4,
+    8; the exact fit filter in its own LDS or in the borrowed slot rows) and, for 129-256 nodes,
+    the hand-scheduled loop's hand-over: bit-exact vs the oracle."""
+    from mcs_amd import GenParams, gen_streams_host
+
+    arrays = replicate(uniform_cluster(nodes), 24)
+    # the offered load stays at 90 % with the arrival rate below DELAY's one-per-second drain
+    gp = GenParams(seed=0x4D43535F53494D31, arrival_mode=1, lam=0.95, max_dur_s=972 * nodes // 256)
+    streams = gen_streams_host(gp, arrays, 2500)
+    with Engine(0, policy="DELAY") as eng:
+        node, start, fin, st, cs, ds = run(eng, arrays, streams)
+    assert_delay_parity(arrays, streams, node, start, fin, cs, ds)
+    assert ds["moved_l1"].sum() > streams.n_jobs // 4

@@ -65,6 +65,8 @@ if bench and "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
         "jobs_per_cluster": bench["config"]["jobs_per_cluster"],
         "policy": "delay" if "DELAY" in bench["metric"] else "fifo",
         "gen": bench["config"].get("gen", "stream"),
+        "lam": bench["config"].get("lam", 0.0),
+        "max_dur": bench["config"].get("max_dur", 600),
         "hbm_bytes_per_launch": fetch + write,
         "fetch_bytes_corrected": fetch,
         "write_bytes": write,
@@ -77,7 +79,9 @@ if bench and "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
     with open(f"{out}/traffic.json", "w") as f:
         json.dump(traffic, f, indent=1)
     with open("profiles/traffic_latest" + ("_delay" if traffic["policy"] == "delay" else "")
-              + ("_fused" if traffic["gen"] == "fused" else "") + ".json", "w") as f:
+              + ("_fused" if traffic["gen"] == "fused" else "")
+              + (f"_lam{traffic['lam']:g}_dur{traffic['max_dur']}" if traffic["lam"] or traffic["max_dur"] != 600 else "")
+              + ".json", "w") as f:
         json.dump(traffic, f, indent=1)
 if "SQ_INSTS_SALU" in counters and bench:
     jobs = bench["config"]["placements_per_step_per_gpu"]
