@@ -154,8 +154,12 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     bool live = true;
     // the Level1 fit filter (lane l: best[l]) and the largest free core count, valid until a
     // commit or a release (hdirty)
-    uint32_t best = 0u, max_c = 0u;
+    uint32_t best = 0u;
     bool hdirty = true;
+    // lmv (lane i, as best): a lower bound of the smallest memory demand among the Level1 jobs of
+    // core key 63 - i (~0u: none).  A pass that cannot place anything (best < lmv in every lane)
+    // is skipped whole: it would only have re-read the list (its JobsMap updates are closed-form)
+    uint32_t lmv = ~0u;
     if constexpr (HOR) {  // resume from the previous horizon
         const OnlineState st = a.on.st_in[ci];
         if (st.valid) {
@@ -302,7 +306,8 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
 
     // the Level1 fit filter (scheduler.go:305, ScheduleJob's outcome without its node): lane i
     // holds best[63 - i] = max free memory over nodes with min(free cores, 63) >= 63 - i, so job
-    // (c, m) fits some node iff c <= max_c and best[min(c, 63)] >= m (exact for c < 63).  An LDS
+    // (c, m) fits some node iff best[min(c, 63)] >= m (exact for c < 63 and m > 0; a job without
+    // memory demand passes whenever it cannot be told apart, and its first fit decides).  An LDS
     // ds_max_u32 histogram over the reversed core keys, then a DPP inclusive prefix max.  Clusters
     // of <= 128 nodes own 256 B of LDS for it; bigger ones keep fifo_kernel's 10 KB per wave (16
     // waves per CU) and borrow the first 256 B of the running slots' {node | finish} rows: each
@@ -311,13 +316,6 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     auto build_filter = [&]() __attribute__((always_inline)) {
         hdirty = false;
         asm volatile("" ::: "memory");  // other lanes' commits and releases since
-        uint32_t mc = 0u;
-#pragma unroll
-        for (int k = 0; k < NPL; ++k) {
-            const uint32_t fc = (uint32_t)nodes[k * kWave + lane];
-            if (nid[k] != kEmpty) mc = fc > mc ? fc : mc;
-        }
-        max_c = wave_max_u32(mc);
         uint32_t* hist;
         if constexpr (kHist) {
             __shared__ uint32_t hist_own[kWave];
@@ -345,6 +343,21 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         best = wave_prefix_max_u32(v);
     };
 
+    // Level1 rows in flight: a pass reads rows 0.. kPf - 1 from these registers, loaded at the end of
+    // the iteration before (one L2 round trip per pass instead of one per row; the pass was bound
+    // by them: 57 % of the wave's time waiting on a Level1-heavy stream)
+    constexpr int kPf = 4;
+    uint64_t pf_cm[kPf], pf_jd[kPf];
+    auto prefetch_l1 = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < kPf; ++r) {
+            const uint32_t q = (uint32_t)r * kWave + lane;
+            const bool ql = q < l1n;
+            pf_cm[r] = ql ? ld_l2(l1_cm + q) : 0ull;
+            pf_jd[r] = ql ? ld_l2(l1_jd + q) : 0ull;
+        }
+    };
+
     // writes the Level0 results of batch [base, base + 64); `cur` holds that batch's records
     auto flush = [&](uint32_t base) __attribute__((always_inline)) {
         const uint32_t i = base + lane;
@@ -361,6 +374,10 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     // h is in it.  rend bounds h: the batch end, or 0 once the run stops.  A batch's results are
     // stored at the next batch boundary, after the wait for the prefetched records.
     uint32_t stop = 0u, rend = 0u;
+    if (l1n != 0u) {  // (online resume)
+        lmv = 0u;       // nothing known about the resumed list
+        prefetch_l1();
+    }
     if (live && (HOR || J != 0u)) for (;;) {
     if (cb != cb0) {
         const uint4 nb = nxt;  // waits for the prefetch, issued a whole batch ago
@@ -379,23 +396,40 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
             // nodes since the last build, and after every placement of the pass
             if (hdirty) build_filter();
 
-            uint32_t wr = 0u, skip = kEmpty;
-            for (uint32_t base = 0; base < l1n && !stop; base += kWave) {
+            uint32_t wr = 0u, skip = kEmpty, dfold = ~0u;
+            const bool any = __ballot(best >= lmv) != 0ull;
+            for (uint32_t base = 0; any && base < l1n && !stop; base += kWave) {
                 const uint32_t pos = base + lane;
                 const bool live = pos < l1n;
-                const uint64_t cm = live ? ld_l2(l1_cm + pos) : 0ull;
-                const uint64_t jdv = live ? ld_l2(l1_jd + pos) : 0ull;
+                // the row was loaded kPf rows ahead (the first kPf at the previous iteration's
+                // end): rotate the window and issue row + kPf
+                const uint64_t cm = pf_cm[0], jdv = pf_jd[0];
+#pragma unroll
+                for (int r = 0; r + 1 < kPf; ++r) {
+                    pf_cm[r] = pf_cm[r + 1];
+                    pf_jd[r] = pf_jd[r + 1];
+                }
+                {
+                    const uint32_t q = pos + kPf * kWave;
+                    const bool ql = q < l1n;
+                    pf_cm[kPf - 1] = ql ? ld_l2(l1_cm + q) : 0ull;
+                    pf_jd[kPf - 1] = ql ? ld_l2(l1_jd + q) : 0ull;
+                }
                 const uint32_t c = (uint32_t)cm, m = (uint32_t)(cm >> 32);
                 const uint32_t key = 63u - (c < 63u ? c : 63u);
                 // the lookup outside the && (a ds_bpermute under a partial exec mask reads 0 from
                 // the disabled lanes that hold the filter)
                 uint32_t bm = (uint32_t)__shfl((int)best, (int)key);
-                uint64_t cand = __ballot(live && c <= max_c && bm >= m);
+                uint64_t cand = __ballot(live && bm >= m);
                 uint64_t rem = 0ull;
                 while (cand) {
                     const uint32_t b = (uint32_t)__builtin_ctzll(cand);
                     cand &= cand - 1ull;
-                    if (base + b == skip) continue;  // slid into slot i: not examined (D6)
+                    if (base + b == skip) {  // slid into slot i: not examined (D6)
+                        const uint32_t sk = readlane(key, b), sm = readlane(m, b);
+                        dfold = (lane == sk && sm < dfold) ? sm : dfold;
+                        continue;
+                    }
                     const uint32_t jc = readlane(c, b), jm = readlane(m, b);
                     const uint32_t k = first_fit(jc, jm);
                     if (k == kEmpty) continue;
@@ -420,7 +454,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                     // to a failing first fit: ~29 per placement on a Level1-heavy stream)
                     build_filter();
                     bm = (uint32_t)__shfl((int)best, (int)key);
-                    cand &= __ballot(live && c <= max_c && bm >= m);
+                    cand &= __ballot(live && bm >= m);
                     ++placed;
                     ++placed_l1;
                     l1_t += t;
@@ -440,7 +474,14 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                 l1w |= (wr != base || rem != 0ull) ? 1u : 0u;
                 wr += (uint32_t)__builtin_popcountll(kept);
             }
-            if (!stop) l1n = wr;
+            if (any && !stop) {
+                l1n = wr;
+                // every job left was tested on a filter no smaller than the final one and failed
+                // (exact below key 63 where some node has memory), except the D6-skipped ones
+                const uint32_t raised = best + 1u;
+                if (lane != 0u && best != 0u && raised != 0u) lmv = raised > lmv ? raised : lmv;
+                lmv = dfold < lmv ? dfold : lmv;
+            }
         }
 
         // ---- Level0 head (scheduler.go:332-366) ----
@@ -484,6 +525,10 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
                 }
                 ++l1n;
                 peak_l1 = l1n > peak_l1 ? l1n : peak_l1;
+                {
+                    const uint32_t kk = 63u - (jc < 63u ? jc : 63u);
+                    lmv = (lane == kk && jm < lmv) ? jm : lmv;
+                }
                 ++moved;
                 mv_a += arr;
                 ++h;
@@ -493,6 +538,9 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         }
         // Level1 stores must have reached L2 before the next pass's sc1 loads
         if (l1w) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        // the next pass's first rows, in flight during the clock advance, the releases and the
+        // filter build (the list does not change until that pass)
+        if (l1n != 0u) prefetch_l1();
 
         // ---- time.Sleep(1 s) (:367) and the fast-forward; one exit, tested at the bottom ----
         uint32_t tn = t + 1u;
