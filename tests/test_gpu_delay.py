@@ -199,3 +199,45 @@ def test_gpu_delay_level1_heavy_generated(nodes):
         node, start, fin, st, cs, ds = run(eng, arrays, streams)
     assert_delay_parity(arrays, streams, node, start, fin, cs, ds)
     assert ds["moved_l1"].sum() > streams.n_jobs // 4
+
+
+def _filter_edge_workload(n_clusters, seed):
+    """Clusters of 100 and 200 nodes (the fit filter in its own LDS and in the borrowed slot rows)
+    whose nodes have 40-128 cores, and jobs whose cores straddle the filter's key clamp (62, 63,
+    64, 100: key 63 is conservative) with zero-memory jobs among them (m = 0 passes the filter
+    when no node can be told apart), arriving under DELAY's drain so Level1 fills and the pass
+    skip's bound is raised, lowered and folded by D6 skips."""
+    from mcs_amd.cluster import Node
+
+    rng = np.random.default_rng(seed)
+    clusters = []
+    for k in range(n_clusters):
+        n = 100 if k % 2 else 200
+        cores = rng.choice([40, 64, 80, 128], size=n)
+        mem = rng.choice([4000, 12000, 24000], size=n)
+        from mcs_amd import Cluster
+        clusters.append(Cluster(Id=k + 1, Nodes=[Node(Id=i + 1, Type="physical", Memory=int(mem[i]), Cores=int(cores[i]),
+                                                      MemoryAvailable=int(mem[i]), CoresAvailable=int(cores[i]))
+                                                 for i in range(n)]))
+    arrays = pack_clusters(clusters)
+    J = 1500
+    parts = []
+    for k in range(n_clusters):
+        arr = np.cumsum(rng.poisson(1.1, size=J)).astype(np.uint32)
+        dur = rng.integers(0, 900, size=J).astype(np.uint32)
+        c = rng.choice([0, 1, 8, 32, 62, 63, 64, 100], size=J, p=[.05, .15, .25, .25, .1, .08, .07, .05])
+        m = rng.choice([0, 1, 2000, 8000, 12000, 20000], size=J, p=[.08, .07, .3, .3, .15, .1])
+        parts.append((arr, dur, c.astype(np.uint32), m.astype(np.uint32)))
+    off = np.zeros(n_clusters + 1, np.uint64)
+    off[1:] = np.cumsum([J] * n_clusters)
+    s = JobStreams(*(np.concatenate([p[i] for p in parts]) for i in range(4)), off)
+    return arrays, s
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_gpu_delay_level1_filter_edges(seed):
+    arrays, streams = _filter_edge_workload(16, seed)
+    with Engine(0, policy="DELAY") as eng:
+        node, start, fin, st, cs, ds = run(eng, arrays, streams)
+    assert_delay_parity(arrays, streams, node, start, fin, cs, ds)
+    assert ds["moved_l1"].sum() > 0 and ds["placed_l1"].sum() > 0

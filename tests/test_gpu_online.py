@@ -293,3 +293,25 @@ def test_online_append_floor_is_per_cluster_after_a_drain():
                            np.array([2], np.uint32), np.array([2], np.uint32), np.array([0, 0, 1], np.uint64))
         with pytest.raises(MCSError):
             eng.append_jobs(early)  # cluster 1: before its own clock
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_online_delay_level1_filter_edges(seed):
+    """The Level1 fit filter's edge workload (test_gpu_delay._filter_edge_workload: 100/200-node
+    clusters, keys across the clamp, zero-memory jobs) in 7 online slices: every horizon resumes a
+    non-empty Level1 list (the pass-skip bound restarts from nothing) and the run equals the batch
+    run and the oracle."""
+    from test_gpu_delay import _filter_edge_workload
+
+    arrays, streams = _filter_edge_workload(8, seed)
+    b = batch(arrays, streams, policy="DELAY")
+    g = run_online(arrays, streams, horizons_for(streams, 7), policy="DELAY",
+                   check_prefix=make_prefix_check(b[:3], streams.job_off))
+    for i in range(3):
+        np.testing.assert_array_equal(g[i], b[i])
+    for f in b[5].dtype.names:
+        np.testing.assert_array_equal(g[5][f], b[5][f], err_msg=f)
+    on, os_, of, od = O.delay_run_batch(arrays, streams, n_threads=8)
+    np.testing.assert_array_equal(b[0], on)
+    np.testing.assert_array_equal(b[1], os_)
+    np.testing.assert_array_equal(b[2], of)
