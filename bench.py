@@ -19,6 +19,11 @@ Configs (BASELINE.json `configs`):
   c5 — the lock-step trading system (64 clusters, borrow + trader; --policy delay: DELAY + real
      contracts), sharded over the ranks with RCCL all-gathers.
 
+Ranks: `python bench.py --gpus N` (WORLD_SIZE unset, N > 1) is a parent that never touches a GPU: it
+spawns torchrun with N ranks on this node (127.0.0.1) and exits with their status; rank 0 prints the
+line.  Under an external torchrun WORLD_SIZE must equal --gpus.  Any mismatch (WORLD_SIZE != --gpus,
+fewer visible GPUs than ranks) exits 2 without printing a line, so an N-GPU line is never a 1-GPU run.
+
 Prints ONE JSON line on rank 0 (contract in the task statement), with "roofline" (HBM-bound:
 28 algorithmic bytes per placement; the kernel is latency-bound, see "limiter") and
 "cpu_baseline" (the naive CPU oracle, rank 0, N=1, with the host's core count and CPU model).
@@ -293,6 +298,9 @@ def main_c5_delay(args, world, rank, local_rank):
                         "trades_won": ts["trades_won"], "wait_time_rounds": int((tr["policy"] == 0).sum()),
                         "foreign_jobs": int(len(eng.foreign())), "flags": ts["flags"], "loop_form": ts["loop_form"]},
         }
+        if dist_on:  # the RCCL communicator's size, as torch.distributed sees it
+            out["world"] = world
+            out["comm_world"] = dist.get_world_size()
         print(json.dumps(out), flush=True)
     eng.close()
     if dist_on:
@@ -405,6 +413,9 @@ def main_c5(args, world, rank, local_rank):
                         "borrowed": ts["borrowed"], "lent_runs_all_ranks": lent_all, "trades": ts["trades"],
                         "trades_won": ts["trades_won"], "flags": ts["flags"], "loop_form": ts["loop_form"]},
         }
+        if dist_on:  # the RCCL communicator's size, as torch.distributed sees it
+            out["world"] = world
+            out["comm_world"] = dist.get_world_size()
         print(json.dumps(out), flush=True)
     eng.close()
     if dist_on:
@@ -690,6 +701,9 @@ def main_batch(args, world, rank, local_rank):
             "slot_pool_escalations": escalations,
             "diagnostics": diag,
         }
+        if dist_on:  # the RCCL communicator's size, as torch.distributed sees it
+            out["world"] = world
+            out["comm_world"] = dist.get_world_size()
         print(json.dumps(out), flush=True)
 
     eng.close()
@@ -697,9 +711,67 @@ def main_batch(args, world, rank, local_rank):
         dist.destroy_process_group()
 
 
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(n, argv, port):
+    """The command a `bench.py --gpus N` parent (WORLD_SIZE unset) runs: torchrun with one rank per
+    GPU of this node over 127.0.0.1, each rank re-entering bench.py with the same arguments (so each
+    sees WORLD_SIZE == --gpus)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def world_check(gpus, env, n_devices):
+    """Decide how this process runs.  Returns ("launch", n) for a parent that must spawn n ranks,
+    ("run", world) for a rank (or the N=1 process), or ("refuse", message)."""
+    if gpus < 1:
+        return "refuse", f"--gpus {gpus}: need at least 1"
+    w = env.get("WORLD_SIZE")
+    if w is None:
+        if gpus == 1:
+            return "run", 1
+        if n_devices < gpus:
+            return "refuse", f"--gpus {gpus} but only {n_devices} GPU(s) are visible on this node"
+        return "launch", gpus
+    world = int(w)
+    if world != gpus:
+        return "refuse", f"WORLD_SIZE={world} (launcher) differs from --gpus {gpus}"
+    local = int(env.get("LOCAL_RANK", "0"))
+    if world > 1 and local >= n_devices:
+        return "refuse", f"LOCAL_RANK {local} but only {n_devices} GPU(s) are visible"
+    return "run", world
+
+
+def visible_devices():
+    """GPUs visible to this process without initialising the runtime (device_count() does not on
+    this image; the parent never launches work on a GPU)."""
+    import torch
+
+    return torch.cuda.device_count()
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus == 1:
+        what, val = "run", 1  # the N=1 line, unchanged
+    else:
+        what, val = world_check(args.gpus, os.environ, visible_devices())
+    if what == "refuse":
+        print(f"bench.py: refusing to run: {val}", file=sys.stderr, flush=True)
+        return 2
+    if what == "launch":
+        import subprocess
+
+        # a child process per rank (never exec: this parent must not replace itself); rank 0 prints
+        # the JSON line on the inherited stdout; torchrun exits with the worst rank's status
+        return subprocess.run(launcher_cmd(val, sys.argv[1:], free_port())).returncode
+    world = val
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.config == "c5":
@@ -710,4 +782,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

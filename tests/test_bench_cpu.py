@@ -34,3 +34,62 @@ def test_cpu_baseline_explicit_sample(monkeypatch):
     r = bench.cpu_baseline(a, wl, 2)
     assert r["sample_clusters"] == 6
     assert a.traffic_json.endswith("traffic_latest.json")
+
+
+# ---- bench.py --gpus N: one rank per GPU, and refusal when the world cannot be N ---------------
+def test_launcher_command_line(monkeypatch):
+    bench, _ = _bench([], monkeypatch)
+    cmd = bench.launcher_cmd(8, ["--gpus", "8", "--steps", "20", "--warmup", "5"], 29555)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nnodes=1" in cmd and "--nproc-per-node=8" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
+    i = cmd.index(os.path.join(REPO, "bench.py"))
+    assert cmd[i + 1:] == ["--gpus", "8", "--steps", "20", "--warmup", "5"]
+
+
+def test_world_check_cases(monkeypatch):
+    bench, _ = _bench([], monkeypatch)
+    wc = bench.world_check
+    assert wc(1, {}, 0) == ("run", 1)
+    assert wc(8, {}, 8) == ("launch", 8)
+    assert wc(8, {}, 1)[0] == "refuse"  # --gpus 8 on a 1-GPU box: never a mislabelled 1-GPU line
+    assert wc(8, {"WORLD_SIZE": "8", "LOCAL_RANK": "3"}, 8) == ("run", 8)
+    assert wc(8, {"WORLD_SIZE": "4", "LOCAL_RANK": "0"}, 8)[0] == "refuse"  # torchrun world != --gpus
+    assert wc(1, {"WORLD_SIZE": "2", "LOCAL_RANK": "0"}, 2)[0] == "refuse"
+    assert wc(2, {"WORLD_SIZE": "2", "LOCAL_RANK": "1"}, 1)[0] == "refuse"  # rank without a GPU
+    assert wc(0, {}, 8)[0] == "refuse"
+
+
+def test_launch_spawns_torchrun_child(monkeypatch):
+    bench, _ = _bench(["--gpus", "4", "--steps", "3"], monkeypatch)
+    import subprocess
+
+    seen = {}
+
+    class R:
+        returncode = 7
+
+    def fake_run(cmd, *a, **k):
+        seen["cmd"] = cmd
+        return R()
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "visible_devices", lambda: 4)
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    assert bench.main() == 7  # the worst rank's status (torchrun's) is the parent's
+    assert "--nproc-per-node=4" in seen["cmd"] and seen["cmd"][-3:] == ["--gpus", "4", "--steps", "3"][-3:]
+
+
+def test_refusal_exits_nonzero_without_gpus():
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "refusing" in r.stderr and r.stdout == ""
+    env["WORLD_SIZE"] = "2"
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "differs from --gpus" in r.stderr
