@@ -585,11 +585,13 @@ def main_batch(args, world, rank, local_rank):
     kernel_ms = []
     placed = 0
     escalations = 0
+    handed_over = 0
     for _ in range(args.steps):
         st = eng.run()
         kernel_ms.append(st.kernel_ms)
         placed += st.placed
         escalations += st.escalations
+        handed_over = st.handed_over
     barrier()
     elapsed = time.perf_counter() - t0
 
@@ -616,13 +618,10 @@ def main_batch(args, world, rank, local_rank):
         diag.pop("waited_frac")
         diag["delay_iterations_per_job"] = diag.pop("loop_passes_per_job")
         diag["level1_moved_frac"] = float(ds["moved_l1"].sum()) / max(n_jobs, 1)
-        handed = int((ds["moved_l1"] > 0).sum())
-        if kernel_name == "mcs::delay_asm_kernel" and handed:
-            # the hand-scheduled loop stops a cluster at its first Level1 move and the engine
-            # re-runs it on delay_kernel: both launches are in kernel_ms
-            diag["clusters_handed_to_delay_kernel"] = handed
-            kernel_name = (f"mcs::delay_asm_kernel + mcs::delay_kernel ({handed} of {wl.per} clusters handed over "
-                           f"at their first Level1 move)")
+        # clusters the hand-scheduled loop handed to delay_kernel (re-run from t = 0, both launches in
+        # kernel_ms; the engine names both kernels then): Level1 past its LDS slice, a deadlock, or the
+        # clock range after a move
+        diag["clusters_handed_to_delay_kernel"] = handed_over
         diag["level1_peak_max"] = int(ds["peak_l1"].max())
         diag["avg_wait_s"] = float(ds["total_wait_ms"].sum()) / max(float(ds["jobs_count"].sum()), 1.0) / 1e3
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MCS_ABI_VERSION 5
+#define MCS_ABI_VERSION 6
 
 /* ---- status codes --------------------------------------------------------------------------- */
 typedef enum mcs_status {
@@ -155,6 +155,10 @@ typedef struct mcs_stats {
     uint64_t pending;       /* online runs: jobs not decided yet (queued, or arriving later)       */
     uint32_t t_horizon;     /* online runs: the horizon reached (MCS_TIME_NONE after a drain)      */
     uint32_t online;        /* 1 if this run continued an online session (finite horizons)         */
+    uint32_t handed_over;   /* DELAY, ABI v6: clusters the hand-scheduled loop handed to the compiled
+                               delay_kernel (re-run from t = 0: Level1 past its LDS slice, a Level1
+                               deadlock, or the clock range after a move)                           */
+    uint32_t reserved;
 } mcs_stats;
 
 typedef struct mcs_cluster_stats {

@@ -6,20 +6,39 @@
 // the first fit by v_pk_sub_u16 + SDWA + v_perm, the commit as one indexed move, the running slots
 // in registers and the release with one LDS round trip.
 //
-// The loop is DELAY's fast path: every iteration while Level1 is empty.  One iteration at t:
+// One Delay iteration at t:
 //   * releases due at t (cluster.go:153-157, before anything else, D3);
-//   * the Level1 pass (:302-329) has nothing to examine;
+//   * the Level1 pass (:302-329): every Level1 job in list order gets ScheduleJob; a placed job is
+//     removed with append(Level1[:i], Level1[i+1:]...) and no i--, so the job sliding into slot i
+//     is not examined this pass (D6, replicated);
 //   * the Level0 head (:332-366): placed when it fits (ScheduleJob, :335); otherwise, once it has
-//     waited MaxWaitTime (:353), it would move to Level1: the loop stops there ("bail-out", flag
-//     kDelayBail) and the engine re-runs that cluster from t = 0 on the compiled delay_kernel, which has
-//     the Level1 list.  A cluster that bails does so at its first Level1 move;
-//   * time.Sleep(1 s) (:367): t + 1 after a placement; an iteration that changes nothing
-//     fast-forwards to the next release, the head's arrival or its MaxWaitTime move (exact, the
-//     skipped iterations repeat the same failures).
-// Same results bit for bit as delay_kernel (tests/test_gpu_delay.py, every form).
+//     waited MaxWaitTime (:353), it moves to the Level1 tail;
+//   * time.Sleep(1 s) (:367): t + 1 after an iteration that placed or moved a job; an iteration
+//     that changed nothing fast-forwards to the next release, the head's arrival or its MaxWaitTime
+//     move (exact: the skipped iterations repeat the same failures).
+//
+// Level1 lives in the wave's LDS (r04), three SoA arrays of kL1Cap words: the request {cores |
+// mem << 16} (clamped like the Level0 records), the job's row and its duration.  The loop has two
+// modes with their own copies of the iteration code: mode 0 while Level1 is empty (the r03 loop,
+// no pass), mode 1 while it is not.  A pass reads the list 64 entries per row; one DPP-built fit
+// filter (lane i: the largest guarded free memory over nodes with min(free cores, 63) >= 63 - i,
+// the exact test for jobs of < 63 cores) and one ds_bpermute per row pick the entries that fit
+// some node, each of those gets the real first fit in list order, and the row is compacted in
+// place.  The filter is rebuilt after every Level1 placement (it also is the pass skip's
+// reference: lane i of v106 bounds the smallest guarded memory demand among the Level1 jobs of
+// that core key, so a pass with best < bound in every lane cannot place anything and is skipped).
+// The loop stops a cluster ("bail-out", kDelayBail; the engine re-runs it from t = 0 on the
+// compiled delay_kernel) only when Level1 outgrows its LDS slice or when the clock leaves the u32
+// range after a move.  A Level1 deadlock (nothing runs or arrives and Level1 fits no node) ends the
+// cluster here, as delay_kernel does: its Level1 jobs are written unplaced.
+// Same results bit for bit as delay_kernel and the oracle (tests/test_gpu_delay.py, every form).
 #include "mcs_internal.h"
 #include "mcs_lds.h"
 #include "mcs_wave.h"
+
+#ifdef MCS_STAMPS
+#error "the DELAY loop uses s92-s101: no stamp build"
+#endif
 
 namespace mcs {
 
@@ -27,9 +46,254 @@ namespace {
 
 #include "mcs_fa_macros.h"
 
+// Level1 entries per wave in LDS (10 rows).  LDS words of a wave: the node copy [4][64], the fit
+// filter's histogram [64], then the Level1 arrays cm / jw / dur [kL1Cap] each: 8960 B, so 16 cluster
+// waves per CU (the C4 shape) take 140 KB of the CU's 160 KB.
+constexpr uint32_t kL1Cap = 640;
+constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
 
-// v102/v103: per-lane 64-bit sum of (start - arrival) of the stored Level0 batches (WaitTime,
-// scheduler.go:338-341, at whole seconds); v104 temp.  s56 MaxWaitTime.
+// Register map beyond mcs_fa_macros.h's (DELAY loop only):
+//   s43 changed (this iteration placed or moved a job)   s[58:59] candidates of the row
+//   s82 candidate lane   s74/s75/s76 temps   s[88:89] live (then kept) lanes of the row
+//   s[90:91] removed lanes of the row   s92 Level1 length   s93 write cursor   s94 row base
+//   s95 the D6-skipped position   s96 filter dirty   s97 moved   s98 placed from Level1
+//   s99 Level1 peak   s[100:101] sum over Level1 placements of t minus the moved jobs' arrivals
+//   v56 cm  v57 job row  v58 duration  v59 4 * core key  v60 filter at the key  v61 guarded memory
+//   v62 temp  v63 row address  v88 Level1 lane address (row 0)  v102/v103 per-lane 64-bit sum of
+//   (start - arrival) of the stored Level0 batches  v104 temp  v105 filter  v106 pass-skip bound
+//   v112 histogram lane address  v113 histogram base + 4 * 0x803f  v114/v115/v123 temps
+//   v116 D6 fold  v118 0x8000  v122 0x803f   s56 MaxWaitTime
+//
+// the fit filter (scheduler.go:305, ScheduleJob's outcome without its node): lane i of v105 =
+// max guarded free memory (2^15 + free_m; padding nodes hold 0x7fff, below every request) over the
+// nodes with min(free cores, 63) >= 63 - i.  An LDS ds_max_u32 histogram over the reversed core keys
+// (key address = base - 4 * clamp(2^15 + free_c, 0x8000, 0x803f)), then a DPP inclusive prefix max.
+#define MCS_FD_BUILD                                                                              \
+    "v_mov_b32 v114, 0\n\t"                                                                       \
+    "ds_write_b32 v112, v114\n\t"                                                                 \
+    "v_bfe_u32 v72, v64, 0, 16\n\t"                                                               \
+    "v_bfe_u32 v73, v65, 0, 16\n\t"                                                               \
+    "v_bfe_u32 v74, v66, 0, 16\n\t"                                                               \
+    "v_bfe_u32 v75, v67, 0, 16\n\t"                                                               \
+    "v_med3_u32 v72, v72, v118, v122\n\t"                                                         \
+    "v_med3_u32 v73, v73, v118, v122\n\t"                                                         \
+    "v_med3_u32 v74, v74, v118, v122\n\t"                                                         \
+    "v_med3_u32 v75, v75, v118, v122\n\t"                                                         \
+    "v_mad_i32_i24 v72, v72, -4, v113\n\t"                                                        \
+    "v_mad_i32_i24 v73, v73, -4, v113\n\t"                                                        \
+    "v_mad_i32_i24 v74, v74, -4, v113\n\t"                                                        \
+    "v_mad_i32_i24 v75, v75, -4, v113\n\t"                                                        \
+    "v_lshrrev_b32 v76, 16, v64\n\t"                                                              \
+    "v_lshrrev_b32 v77, 16, v65\n\t"                                                              \
+    "v_lshrrev_b32 v78, 16, v66\n\t"                                                              \
+    "v_lshrrev_b32 v79, 16, v67\n\t"                                                              \
+    "ds_max_u32 v72, v76\n\t"                                                                     \
+    "ds_max_u32 v73, v77\n\t"                                                                     \
+    "ds_max_u32 v74, v78\n\t"                                                                     \
+    "ds_max_u32 v75, v79\n\t"                                                                     \
+    "ds_read_b32 v105, v112\n\t" /* (one wave's LDS operations complete in order) */             \
+    "s_mov_b32 s96, 0\n\t"                                                                        \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v105, v105, v105 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v105, v105, v105 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v105, v105, v105 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v105, v105, v105 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v105, v105, v105 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"                  \
+    "s_nop 1\n\t"                                                                                 \
+    "v_max_u32_dpp v105, v105, v105 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+
+// a Level0 batch's results (the lanes placed on Level0; moved jobs are written when Level1 places
+// them) and their waits; v91 = -1 marks a lane without a Level0 placement
+#define MCS_FD_STORE                                                                              \
+    "v_cmp_ne_u32_e32 vcc, -1, v91\n\t"                                                          \
+    "s_mov_b64 exec, vcc\n\t"                                                                     \
+    "v_add_u32 v125, s57, v110\n\t"                                                               \
+    "v_lshlrev_b32 v125, 2, v125\n\t" MCS_FA_NODEIDX                                              \
+    "global_store_dword v125, v126, s[66:67] nt\n\t"                                              \
+    "global_store_dword v125, v92, s[68:69] nt\n\t"                                               \
+    "v_add_u32 v93, v92, v95\n\t" /* finish = start + the batch's duration column */            \
+    "global_store_dword v125, v93, s[70:71] nt\n\t"                                               \
+    "v_sub_u32 v104, v92, v94\n\t" /* start - arrival */                                         \
+    "v_add_co_u32 v102, vcc, v102, v104\n\t"                                                      \
+    "v_addc_co_u32 v103, vcc, 0, v103, vcc\n\t"                                                   \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "v_mov_b32 v91, -1\n\t"
+
+// the Level0 head (scheduler.go:332-366) of mode M: first fit; a placement commits (HD: the filter
+// is dirty in mode 1), then the cursor moves (the decision is final) and the clock ticks
+#define MCS_FD_HEAD(M, HD)                                                                        \
+    "s_cmp_gt_u32 s45, s40\n\t" /* Level0 empty at t: the head has not arrived */                 \
+    "s_cbranch_scc1 mcsfd_idle" #M "_%=\n\t" MCS_FA_FIT16 MCS_FA_ANYFIT                           \
+    "s_add_u32 s55, s40, s46\n\t"                                                                 \
+    "s_cbranch_vccz mcsfd_nofit" #M "_%=\n\t"                                                     \
+    "s_ff1_i32_b64 s50, vcc\n\t" /* lowest lane with a fit */                                     \
+    "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_zero" #M "_%=\n\t" MCS_FA_DECIDE16R                                     \
+    "s_min_u32 s77, s77, s55\n\t" /* the wave's earliest finish */                                \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "s_mov_b32 m0, s47\n\t"                                                                       \
+    "s_add_u32 s80, s80, 1\n\t" HD                                                                \
+    "v_writelane_b32 v91, s54, m0\n\t"                                                            \
+    "v_writelane_b32 v92, s40, m0\n"                                                              \
+    "mcsfd_placed" #M "_%=:\n\t"                                                                  \
+    "s_add_u32 s47, s47, 1\n\t" MCS_FA_REC16                                                      \
+    "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
+    "s_cbranch_scc0 mcsfd_bend_%=\n"                                                              \
+    /* time.Sleep(1 s) after a change (:367) */                                                   \
+    "mcsfd_tick" #M "_%=:\n\t"                                                                    \
+    "s_add_u32 s40, s40, 1\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfd_clkovf_%=\n"                                                            \
+    /* the clock has advanced: releases at the new instant (cluster.go:153-157) */              \
+    "mcsfd_adv" #M "_%=:\n\t"                                                                     \
+    "s_cmp_lt_u32 s40, s77\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfd_inner" #M "_%=\n\t"
+
+// zero-duration job: committed and released before the next ScheduleJob (D3)
+#define MCS_FD_ZERO(M)                                                                            \
+    "mcsfd_zero" #M "_%=:\n\t" MCS_FA_ZEROKX                                                      \
+    "v_writelane_b32 v91, s54, m0\n\t"                                                            \
+    "v_writelane_b32 v92, s40, m0\n\t"                                                            \
+    "s_branch mcsfd_placed" #M "_%=\n"
+
+// the Level1 pass (scheduler.go:302-329), mode 1 only; falls through to the Level0 head
+#define MCS_FD_PASS                                                                               \
+    "s_mov_b32 s43, 0\n\t"                                                                        \
+    "s_cmp_eq_u32 s96, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_chk_%=\n\t" MCS_FD_BUILD                                                \
+    "mcsfd_chk_%=:\n\t"                                                                           \
+    "v_cmp_ge_u32_e32 vcc, v105, v106\n\t" /* a lane whose jobs may fit */                      \
+    "s_cbranch_vccz mcsfd_head1_%=\n\t"                                                           \
+    "s_mov_b32 s93, 0\n\t"                                                                        \
+    "s_mov_b32 s94, 0\n\t"                                                                        \
+    "s_mov_b32 s95, -1\n\t"                                                                       \
+    "v_mov_b32 v116, -1\n"                                                                        \
+    "mcsfd_row_%=:\n\t"                                                                           \
+    "s_lshl_b32 s74, s94, 2\n\t"                                                                  \
+    "v_add_u32 v63, s74, v88\n\t"                                                                 \
+    "ds_read_b32 v56, v63\n\t"                                                                    \
+    "ds_read_b32 v57, v63 offset:%[cap4]\n\t"                                                     \
+    "ds_read_b32 v58, v63 offset:%[cap8]\n\t"                                                     \
+    "s_sub_u32 s74, s92, s94\n\t"                                                                 \
+    "v_cmp_gt_u32_e64 s[88:89], s74, v110\n\t" /* live: the row's entries */                    \
+    "s_mov_b64 s[90:91], 0\n\t"                                                                   \
+    "s_waitcnt lgkmcnt(2)\n\t"                                                                    \
+    "v_and_b32 v59, 0xffff, v56\n\t"                                                              \
+    "v_lshrrev_b32 v61, 16, v56\n\t"                                                              \
+    "v_min_u32 v59, 63, v59\n\t"                                                                  \
+    "v_add_u32 v61, 0x8000, v61\n\t" /* guarded memory demand */                                \
+    "v_lshlrev_b32 v59, 2, v59\n\t"                                                               \
+    "v_sub_u32 v59, 0xfc, v59\n\t" /* 4 * (63 - min(cores, 63)): the filter lane */             \
+    "ds_bpermute_b32 v60, v59, v105\n\t"                                                          \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
+    "v_cmp_ge_u32_e64 s[58:59], v60, v61\n\t"                                                     \
+    "s_and_b64 s[58:59], s[58:59], s[88:89]\n"                                                    \
+    /* the candidates in list order */                                                            \
+    "mcsfd_cand_%=:\n\t"                                                                          \
+    "s_ff1_i32_b64 s82, s[58:59]\n\t"                                                             \
+    "s_cmp_lt_i32 s82, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_rowend_%=\n\t"                                                          \
+    "v_readlane_b32 s48, v56, s82\n\t"                                                            \
+    "s_bitset0_b64 s[58:59], s82\n\t"                                                             \
+    "s_add_u32 s74, s94, s82\n\t"                                                                 \
+    "s_cmp_eq_u32 s74, s95\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfd_d6_%=\n\t" MCS_FA_FIT16 MCS_FA_ANYFIT                                   \
+    "v_readlane_b32 s46, v58, s82\n\t"                                                            \
+    "v_readlane_b32 s75, v57, s82\n\t"                                                            \
+    "s_cbranch_vccz mcsfd_cand_%=\n\t" /* (key 0, 63 or more cores: the filter is conservative) */ \
+    "s_ff1_i32_b64 s50, vcc\n\t"                                                                  \
+    "s_add_u32 s55, s40, s46\n\t"                                                                 \
+    "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_l1zero_%=\n\t" MCS_FA_DECIDE16R                                         \
+    "s_min_u32 s77, s77, s55\n\t"                                                                 \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "s_add_u32 s80, s80, 1\n\t"                                                                   \
+    "s_mov_b32 s96, 1\n"                                                                          \
+    "mcsfd_l1res_%=:\n\t" /* the job's row: node, start, finish (kx in s54) */                  \
+    "s_and_b32 s74, s54, 63\n\t"                                                                  \
+    "s_lshr_b32 s76, s54, 6\n\t"                                                                  \
+    "s_lshl2_add_u32 s74, s74, s76\n\t" /* node = lane * 4 + chunk */                            \
+    "s_lshl_b32 s75, s75, 2\n\t"                                                                  \
+    "s_mov_b64 exec, 1\n\t"                                                                       \
+    "v_mov_b32 v125, s75\n\t"                                                                     \
+    "v_mov_b32 v126, s74\n\t"                                                                     \
+    "v_mov_b32 v127, s40\n\t"                                                                     \
+    "v_mov_b32 v124, s55\n\t"                                                                     \
+    "global_store_dword v125, v126, s[66:67] nt\n\t"                                              \
+    "global_store_dword v125, v127, s[68:69] nt\n\t"                                              \
+    "global_store_dword v125, v124, s[70:71] nt\n\t"                                              \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "s_bitset1_b64 s[90:91], s82\n\t"                                                             \
+    "s_add_u32 s95, s94, s82\n\t"                                                                 \
+    "s_add_u32 s95, s95, 1\n\t" /* the entry sliding into this slot is not examined (D6) */     \
+    "s_add_u32 s98, s98, 1\n\t"                                                                   \
+    "s_add_u32 s100, s100, s40\n\t"                                                               \
+    "s_addc_u32 s101, s101, 0\n\t"                                                                \
+    "s_mov_b32 s43, 1\n\t"                                                                        \
+    "s_cmp_eq_u32 s96, 0\n\t" /* a zero-duration job changed no node */                          \
+    "s_cbranch_scc1 mcsfd_cand_%=\n\t" MCS_FD_BUILD                                               \
+    /* the commit shrank a node: the rest of the row is re-tested on the rebuilt filter */        \
+    "ds_bpermute_b32 v60, v59, v105\n\t"                                                          \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
+    "v_cmp_ge_u32_e32 vcc, v60, v61\n\t"                                                          \
+    "s_and_b64 s[58:59], s[58:59], vcc\n\t"                                                       \
+    "s_branch mcsfd_cand_%=\n"                                                                    \
+    "mcsfd_l1zero_%=:\n\t"                                                                        \
+    "v_readlane_b32 s51, v86, s50\n\t"                                                            \
+    "s_ff1_i32_b32 s52, s51\n\t"                                                                  \
+    "s_lshl3_add_u32 s54, s52, s50\n\t"                                                           \
+    "s_mov_b32 s55, s40\n\t"                                                                      \
+    "s_branch mcsfd_l1res_%=\n"                                                                   \
+    /* D6-skipped: folded into the pass-skip bound as it is (it was not tested) */               \
+    "mcsfd_d6_%=:\n\t"                                                                            \
+    "v_readlane_b32 s74, v59, s82\n\t"                                                            \
+    "v_readlane_b32 s76, v61, s82\n\t"                                                            \
+    "s_lshr_b32 s74, s74, 2\n\t"                                                                  \
+    "s_lshl_b64 exec, 1, s74\n\t"                                                                 \
+    "v_min_u32 v116, s76, v116\n\t"                                                               \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "s_branch mcsfd_cand_%=\n"                                                                    \
+    /* compaction in the same sweep: the kept entries move down to the write cursor */           \
+    "mcsfd_rowend_%=:\n\t"                                                                        \
+    "s_andn2_b64 s[88:89], s[88:89], s[90:91]\n\t"                                                \
+    "s_cmp_lg_u64 s[90:91], 0\n\t"                                                                \
+    "s_cbranch_scc1 mcsfd_cmp_%=\n\t"                                                             \
+    "s_cmp_eq_u32 s93, s94\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfd_rown_%=\n"                                                              \
+    "mcsfd_cmp_%=:\n\t"                                                                           \
+    "s_mov_b64 exec, s[88:89]\n\t"                                                                \
+    "v_mbcnt_lo_u32_b32 v62, s88, 0\n\t"                                                          \
+    "v_mbcnt_hi_u32_b32 v62, s89, v62\n\t" /* rank among the kept entries */                    \
+    "s_sub_u32 s74, s93, s94\n\t"                                                                 \
+    "s_lshl_b32 s74, s74, 2\n\t"                                                                  \
+    "v_sub_u32 v62, v62, v110\n\t"                                                                \
+    "v_lshl_add_u32 v62, v62, 2, v63\n\t"                                                         \
+    "v_add_u32 v62, s74, v62\n\t" /* Level1 + 4 * (wr + rank) */                                  \
+    "ds_write_b32 v62, v56\n\t"                                                                   \
+    "ds_write_b32 v62, v57 offset:%[cap4]\n\t"                                                    \
+    "ds_write_b32 v62, v58 offset:%[cap8]\n\t"                                                    \
+    "s_mov_b64 exec, -1\n"                                                                        \
+    "mcsfd_rown_%=:\n\t"                                                                          \
+    "s_bcnt1_i32_b64 s74, s[88:89]\n\t"                                                           \
+    "s_add_u32 s93, s93, s74\n\t"                                                                 \
+    "s_add_u32 s94, s94, 64\n\t"                                                                  \
+    "s_cmp_lt_u32 s94, s92\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfd_row_%=\n\t"                                                             \
+    /* the pass is over: every job left (keys 1-63) failed a filter no smaller than the final  */ \
+    /* one, except the D6-skipped ones */                                                         \
+    "s_mov_b32 s92, s93\n\t"                                                                      \
+    "v_readlane_b32 s46, v95, s47\n\t" /* the Level0 head's record again */                     \
+    "v_readlane_b32 s48, v96, s47\n\t"                                                            \
+    "v_add_u32 v62, 1, v105\n\t"                                                                  \
+    "s_mov_b64 exec, -2\n\t"                                                                      \
+    "v_max_u32 v106, v106, v62\n\t"                                                               \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "v_min_u32 v106, v106, v116\n"
+
 #define MCS_FD_LOOP(D)                                                                            \
     /* ---- entry: state into the fixed registers ---- */                                        \
     "s_mov_b32 s40, 0\n\t"                                                                        \
@@ -39,11 +303,17 @@ namespace {
     "s_mov_b32 s56, %[mw]\n\t"                                                                    \
     "s_mov_b32 s57, 0\n\t"                                                                        \
     "s_mov_b32 s78, 0\n\t"                                                                        \
-    "s_lshl2_add_u32 s79, s42, 0x100\n\t"                                                         \
+    "s_lshl3_add_u32 s79, s42, 0x100\n\t" /* failed fits bound (a runaway loop: re-run) */       \
     "s_mov_b32 s80, 0\n\t"                                                                        \
     "s_mov_b32 s81, 0\n\t"                                                                        \
     "s_mov_b32 s83, 0\n\t"                                                                        \
     "s_mov_b32 s84, 0\n\t"                                                                        \
+    "s_mov_b32 s92, 0\n\t"                                                                        \
+    "s_mov_b32 s96, 1\n\t"                                                                        \
+    "s_mov_b32 s97, 0\n\t"                                                                        \
+    "s_mov_b32 s98, 0\n\t"                                                                        \
+    "s_mov_b32 s99, 0\n\t"                                                                        \
+    "s_mov_b64 s[100:101], 0\n\t"                                                                 \
     "s_mov_b32 s77, -1\n\t" /* nothing running */                                                \
     "s_mov_b64 s[64:65], %[jobs]\n\t"                                                             \
     "s_mov_b64 s[66:67], %[onp]\n\t"                                                              \
@@ -59,46 +329,33 @@ namespace {
     "v_mov_b32 v108, %[nb]\n\t"                                                                   \
     "v_mov_b32 v110, %[lane]\n\t"                                                                 \
     "v_mov_b32 v102, 0\n\t"                                                                       \
-    "v_mov_b32 v103, 0\n\t" MCS_FA_INIT16R MCS_FA_RELOAD16 "s_waitcnt lgkmcnt(0)\n\t"             \
+    "v_mov_b32 v103, 0\n\t"                                                                       \
+    "v_mov_b32 v91, -1\n\t"                                                                       \
+    "v_mov_b32 v106, -1\n\t" /* no Level1 job of any key */                                      \
+    "v_mov_b32 v118, 0x8000\n\t"                                                                  \
+    "v_mov_b32 v122, 0x803f\n\t"                                                                  \
+    "v_add_u32 v112, 0x400, v108\n\t" /* the histogram (after the node copy) */                  \
+    "v_add_u32 v88, 0x500, v108\n\t"  /* Level1 (after the histogram) */                         \
+    "v_mov_b32 v113, s73\n\t"                                                                     \
+    "v_add_u32 v113, 0x204fc, v113\n\t" MCS_FA_INIT16R MCS_FA_RELOAD16 "s_waitcnt lgkmcnt(0)\n\t" \
     /* prefetch batch 1 */                                                                        \
     "v_lshlrev_b32 v121, 4, v110\n\t"                                                             \
     "v_add_u32 v121, 0x400, v121\n\t"                                                             \
     "global_load_dwordx4 v[98:101], v121, s[64:65]\n\t"                                           \
     "s_min_u32 s41, s42, 64\n\t" MCS_FA_REC16                                                     \
     "s_cmp_eq_u32 s42, 0\n\t" /* no jobs: no iteration (the clock stays at 0) */                 \
-    "s_cbranch_scc1 mcsfd_exit_%=\n"                                                              \
+    "s_cbranch_scc1 mcsfd_exit_%=\n\t"                                                            \
+    "s_branch mcsfd_inner0_%=\n"                                                                  \
                                                                                                   \
-    /* ---- one iteration at t with Level1 empty: the Level0 head (scheduler.go:332-366) ---- */   \
-    "mcsfd_inner_%=:\n\t" MCS_FA_CNTS_##D                                                         \
-    "s_cmp_gt_u32 s45, s40\n\t" /* Level0 empty at t: the head has not arrived */                 \
-    "s_cbranch_scc1 mcsfd_idle_%=\n\t" MCS_FA_FIT16 MCS_FA_ANYFIT                                 \
-    "s_add_u32 s55, s40, s46\n\t"                                                                 \
-    "s_cbranch_vccz mcsfd_nofit_%=\n\t"                                                           \
-    "s_ff1_i32_b64 s50, vcc\n\t" /* lowest lane with a fit */                                     \
-    "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
-    "s_cbranch_scc1 mcsfd_zero_%=\n\t" MCS_FA_DECIDE16R                                           \
-    "s_min_u32 s77, s77, s55\n\t" /* the wave's earliest finish */                                \
-    "s_mov_b64 exec, -1\n\t"                                                                      \
-    "s_mov_b32 m0, s47\n\t"                                                                       \
-    "s_add_u32 s80, s80, 1\n\t"                                                                   \
-    "v_writelane_b32 v91, s54, m0\n\t"                                                            \
-    "v_writelane_b32 v92, s40, m0\n"                                                              \
-    "mcsfd_placed_%=:\n\t"                                                                        \
-    "s_add_u32 s47, s47, 1\n\t" MCS_FA_REC16                                                      \
-    "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
-    "s_cbranch_scc0 mcsfd_bend_%=\n"                                                              \
-    /* time.Sleep(1 s) after a placement (:367) */                                                \
-    "mcsfd_tick_%=:\n\t"                                                                          \
-    "s_add_u32 s40, s40, 1\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfd_clkovf_%=\n"                                                            \
-    /* the clock has advanced: releases at the new instant (cluster.go:153-157) */              \
-    "mcsfd_adv_%=:\n\t"                                                                           \
-    "s_cmp_lt_u32 s40, s77\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfd_inner_%=\n\t" MCS_FA_CNTR_##D                                           \
+    /* ======== mode 0: Level1 empty ======== */                                                 \
+    "mcsfd_inner0_%=:\n\t" MCS_FA_CNTS_##D MCS_FD_HEAD(0, "")                                     \
+    /* releases: shared by both modes, back to the mode's iteration */                           \
+    "mcsfd_rel_%=:\n\t" MCS_FA_CNTR_##D                                                           \
     "s_max_u32 s81, s81, s80\n\t" /* peak: used only grows between releases */                   \
     "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN16R                                                    \
     "v_mov_b32 v120, v90\n\t"                                                                     \
-    "s_nop 1\n\t"                                                                                 \
+    "s_mov_b32 s96, 1\n\t"                                                                        \
+    "s_nop 0\n\t"                                                                                 \
     "v_min_u32_dpp v120, v120, v120 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"                     \
     "s_nop 1\n\t"                                                                                 \
     "v_min_u32_dpp v120, v120, v120 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"                     \
@@ -113,30 +370,24 @@ namespace {
     "s_nop 1\n\t"                                                                                 \
     "v_readlane_b32 s77, v120, 63\n\t"                                                            \
     "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
-    "s_branch mcsfd_inner_%=\n"                                                                   \
-                                                                                                  \
-    /* zero-duration job: committed and released before the next ScheduleJob (D3) */             \
-    "mcsfd_zero_%=:\n\t" MCS_FA_ZEROKX                                                           \
-    "v_writelane_b32 v91, s54, m0\n\t"                                                            \
-    "v_writelane_b32 v92, s40, m0\n\t"                                                            \
-    "s_branch mcsfd_placed_%=\n"                                                                  \
-                                                                                                  \
+    "s_cmp_lg_u32 s92, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_inner1_%=\n\t"                                                          \
+    "s_branch mcsfd_inner0_%=\n" MCS_FD_ZERO(0)                                                   \
     /* nothing changes at t (Level0 empty): the next iteration that can differ is a release or  */ \
     /* the head's arrival */                                                                      \
-    "mcsfd_idle_%=:\n\t"                                                                          \
+    "mcsfd_idle0_%=:\n\t"                                                                         \
     "s_min_u32 s76, s77, s45\n\t"                                                                 \
     "s_add_u32 s40, s40, 1\n\t"                                                                   \
     "s_cbranch_scc1 mcsfd_clkovf_%=\n\t"                                                          \
     "s_max_u32 s40, s40, s76\n\t"                                                                 \
-    "s_branch mcsfd_adv_%=\n"                                                                     \
-                                                                                                  \
-    /* the head does not fit: after MaxWaitTime it moves to Level1 (:353): the compiled kernel */  \
-    /* continues from here; before, the next iteration that can differ is a release or the move */ \
-    "mcsfd_nofit_%=:\n\t"                                                                         \
+    "s_branch mcsfd_adv0_%=\n"                                                                    \
+    /* the head does not fit: after MaxWaitTime it moves to Level1 (:353); before, the next */    \
+    /* iteration that can differ is a release or the move */                                      \
+    "mcsfd_nofit0_%=:\n\t"                                                                        \
     "s_sub_u32 s76, s40, s45\n\t" /* t - arrival (the head has arrived) */                       \
     "s_cmp_ge_u32 s76, s56\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfd_bail_%=\n\t"                                                            \
-    "s_add_u32 s78, s78, 1\n\t" /* runaway guard (a pool overflow: re-run on delay_kernel) */     \
+    "s_cbranch_scc1 mcsfd_move0_%=\n\t"                                                           \
+    "s_add_u32 s78, s78, 1\n\t"                                                                   \
     "s_cmp_gt_u32 s78, s79\n\t"                                                                   \
     "s_cbranch_scc1 mcsfd_poolovf_%=\n\t"                                                         \
     "s_add_u32 s76, s45, s56\n\t"                                                                 \
@@ -144,39 +395,85 @@ namespace {
     "s_add_u32 s40, s40, 1\n\t"                                                                   \
     "s_cbranch_scc1 mcsfd_clkovf_%=\n\t"                                                          \
     "s_max_u32 s40, s40, s76\n\t"                                                                 \
-    "s_branch mcsfd_adv_%=\n"                                                                     \
+    "s_branch mcsfd_adv0_%=\n"                                                                    \
+    "mcsfd_move0_%=:\n\t" /* into mode 1: the filter was not kept in mode 0 */                   \
+    "s_mov_b32 s96, 1\n\t"                                                                        \
+    "s_branch mcsfd_move1_%=\n"                                                                   \
                                                                                                   \
-    /* bail-out: the cluster is re-run on delay_kernel (it has the Level1 list) */                \
-    "mcsfd_bail_%=:\n\t"                                                                          \
-    "s_or_b32 s44, s44, %[fbail]\n\t"                                                             \
-    "s_branch mcsfd_exit_%=\n"                                                                    \
+    /* ======== mode 1: Level1 holds jobs ======== */                                            \
+    "mcsfd_inner1_%=:\n\t"                                                                        \
+    "s_cmp_eq_u32 s92, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_inner0_%=\n\t" MCS_FA_CNTS_##D MCS_FD_PASS                              \
+    "mcsfd_head1_%=:\n\t" MCS_FD_HEAD(1, "s_mov_b32 s96, 1\n\t")                                  \
+    "s_branch mcsfd_rel_%=\n" MCS_FD_ZERO(1)                                                      \
+    "mcsfd_idle1_%=:\n\t"                                                                         \
+    "s_cmp_eq_u32 s92, 0\n\t"                                                                     \
+    "s_cbranch_scc0 mcsfd_idle1b_%=\n\t"                                                          \
+    "s_cmp_eq_u32 s45, -1\n\t" /* Level0 and Level1 empty for good: the run ends */              \
+    "s_cbranch_scc1 mcsfd_done_%=\n"                                                              \
+    "mcsfd_idle1b_%=:\n\t"                                                                        \
+    "s_cmp_lg_u32 s43, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_tick1_%=\n\t"                                                           \
+    "s_min_u32 s76, s77, s45\n\t"                                                                 \
+    "s_cmp_eq_u32 s76, -1\n\t" /* nothing runs or arrives: Level1 never fits (deadlock) */       \
+    "s_cbranch_scc1 mcsfd_dead_%=\n\t"                                                            \
+    "s_add_u32 s40, s40, 1\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfd_clkovf_%=\n\t"                                                          \
+    "s_max_u32 s40, s40, s76\n\t"                                                                 \
+    "s_branch mcsfd_adv1_%=\n"                                                                    \
+    "mcsfd_nofit1_%=:\n\t"                                                                        \
+    "s_sub_u32 s76, s40, s45\n\t"                                                                 \
+    "s_cmp_ge_u32 s76, s56\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfd_move1_%=\n\t"                                                           \
+    "s_add_u32 s78, s78, 1\n\t"                                                                   \
+    "s_cmp_gt_u32 s78, s79\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfd_poolovf_%=\n\t"                                                         \
+    "s_cmp_lg_u32 s43, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_tick1_%=\n\t"                                                           \
+    "s_add_u32 s76, s45, s56\n\t"                                                                 \
+    "s_min_u32 s76, s76, s77\n\t"                                                                 \
+    "s_add_u32 s40, s40, 1\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfd_clkovf_%=\n\t"                                                          \
+    "s_max_u32 s40, s40, s76\n\t"                                                                 \
+    "s_branch mcsfd_adv1_%=\n"                                                                    \
+    /* the head moves to the Level1 tail (:353-360); its JobsMap value is closed-form */         \
+    "mcsfd_move1_%=:\n\t"                                                                         \
+    "s_cmp_ge_u32 s92, %[cap]\n\t" /* Level1 outgrew its LDS slice: re-run on delay_kernel */    \
+    "s_cbranch_scc1 mcsfd_bail_%=\n\t"                                                            \
+    "s_lshl_b32 s74, s92, 2\n\t"                                                                  \
+    "s_add_u32 s76, s57, s47\n\t" /* the job's row */                                            \
+    "s_mov_b64 exec, 1\n\t"                                                                       \
+    "v_add_u32 v62, s74, v88\n\t"                                                                 \
+    "v_mov_b32 v114, s48\n\t"                                                                     \
+    "v_mov_b32 v115, s76\n\t"                                                                     \
+    "v_mov_b32 v123, s46\n\t"                                                                     \
+    "ds_write_b32 v62, v114\n\t"                                                                  \
+    "ds_write_b32 v62, v115 offset:%[cap4]\n\t"                                                   \
+    "ds_write_b32 v62, v123 offset:%[cap8]\n\t"                                                   \
+    "s_and_b32 s74, s48, 0xffff\n\t"                                                              \
+    "s_min_u32 s74, s74, 63\n\t"                                                                  \
+    "s_sub_u32 s74, 63, s74\n\t" /* its core key */                                             \
+    "s_lshr_b32 s76, s48, 16\n\t"                                                                 \
+    "s_add_u32 s76, s76, 0x8000\n\t"                                                              \
+    "s_lshl_b64 exec, 1, s74\n\t"                                                                 \
+    "v_min_u32 v106, s76, v106\n\t" /* the pass-skip bound of its key */                        \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "s_add_u32 s92, s92, 1\n\t"                                                                   \
+    "s_max_u32 s99, s99, s92\n\t"                                                                 \
+    "s_add_u32 s97, s97, 1\n\t"                                                                   \
+    "s_sub_u32 s100, s100, s45\n\t"                                                               \
+    "s_subb_u32 s101, s101, 0\n\t"                                                                \
+    "s_branch mcsfd_placed1_%=\n"                                                                 \
                                                                                                   \
-    "mcsfd_clkovf_%=:\n\t"                                                                        \
-    "s_mov_b32 s40, -1\n\t" /* the clock stays at the last second it reached */                   \
-    "s_or_b32 s44, s44, %[fck]\n\t"                                                               \
-    "s_branch mcsfd_exit_%=\n"                                                                    \
-    "mcsfd_poolovf_%=:\n\t"                                                                       \
-    "s_or_b32 s44, s44, %[fov]\n\t"                                                               \
-    "s_branch mcsfd_exit_%=\n"                                                                    \
-                                                                                                  \
-    /* ---- batch end: store the 64 results and their waits, take the prefetched records ---- */ \
+    /* ---- batch end: store the Level0 results and their waits, take the prefetched records ---- */ \
     "mcsfd_bend_%=:\n\t"                                                                          \
     "s_max_u32 s81, s81, s80\n\t"                                                                 \
     "s_cmp_gt_u32 s81, 64*8\n\t"                                                                  \
     "s_cbranch_scc1 mcsfd_poolovf_%=\n\t"                                                         \
     "s_add_u32 s76, s57, s47\n\t"                                                                 \
     "s_cmp_ge_u32 s76, s42\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfd_done_%=\n\t"                                                            \
-    "s_waitcnt vmcnt(0)\n\t"                                                                      \
-    "v_add_u32 v125, s57, v110\n\t"                                                               \
-    "v_lshlrev_b32 v125, 2, v125\n\t" MCS_FA_NODEIDX                                              \
-    "global_store_dword v125, v126, s[66:67] nt\n\t"                                              \
-    "global_store_dword v125, v92, s[68:69] nt\n\t"                                               \
-    "v_add_u32 v93, v92, v95\n\t" /* finish = start + the batch's duration column */            \
-    "global_store_dword v125, v93, s[70:71] nt\n\t"                                               \
-    "v_sub_u32 v104, v92, v94\n\t" /* start - arrival */                                         \
-    "v_add_co_u32 v102, vcc, v102, v104\n\t"                                                      \
-    "v_addc_co_u32 v103, vcc, 0, v103, vcc\n\t"                                                   \
+    "s_cbranch_scc1 mcsfd_last_%=\n\t"                                                            \
+    "s_waitcnt vmcnt(0)\n\t" MCS_FD_STORE                                                         \
     "s_add_u32 s57, s57, 64\n\t" MCS_FA_TAKE16                                                    \
     "v_add_u32 v121, s57, v110\n\t"                                                               \
     "v_lshlrev_b32 v121, 4, v121\n\t"                                                             \
@@ -185,14 +482,49 @@ namespace {
     "s_sub_u32 s41, s42, s57\n\t"                                                                 \
     "s_min_u32 s41, s41, 64\n\t"                                                                  \
     "s_mov_b32 s47, 0\n\t" MCS_FA_REC16                                                           \
-    "s_branch mcsfd_tick_%=\n"                                                                    \
-    /* every job placed: the run ends with this iteration's sleep */                             \
+    "s_cmp_lg_u32 s92, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_tick1_%=\n\t"                                                           \
+    "s_branch mcsfd_tick0_%=\n"                                                                   \
+    /* every Level0 job decided: the run ends with this iteration's sleep, unless Level1 holds */ \
+    /* jobs: then the last batch is stored and Level0 stays empty (no arrival: s45 = -1) */       \
+    "mcsfd_last_%=:\n\t"                                                                          \
+    "s_cmp_eq_u32 s92, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_done_%=\n\t"                                                            \
+    "s_waitcnt vmcnt(0)\n\t" MCS_FD_STORE                                                         \
+    "s_mov_b32 s57, s76\n\t"                                                                      \
+    "s_mov_b32 s47, 0\n\t"                                                                        \
+    "s_mov_b32 s41, 0\n\t"                                                                        \
+    "s_mov_b32 s45, -1\n\t"                                                                       \
+    "s_branch mcsfd_tick1_%=\n"                                                                   \
     "mcsfd_done_%=:\n\t"                                                                          \
-    "s_add_u32 s40, s40, 1\n"                                                                     \
+    "s_add_u32 s40, s40, 1\n\t"                                                                   \
+    "s_branch mcsfd_exit_%=\n"                                                                    \
+                                                                                                  \
+    /* the Level1 jobs left are retried forever: their rows are written unplaced after the loop */ \
+    "mcsfd_dead_%=:\n\t"                                                                          \
+    "s_or_b32 s44, s44, %[fdl]\n\t"                                                              \
+    "s_branch mcsfd_exit_%=\n"                                                                    \
+    /* bail-out: the cluster is re-run on delay_kernel */                                          \
+    "mcsfd_bail_%=:\n\t"                                                                          \
+    "s_or_b32 s44, s44, %[fbail]\n\t"                                                             \
+    "s_branch mcsfd_exit_%=\n"                                                                    \
+    "mcsfd_clkovf_%=:\n\t"                                                                        \
+    "s_cmp_eq_u32 s97, 0\n\t" /* jobs went through Level1: delay_kernel writes their rows */     \
+    "s_cbranch_scc0 mcsfd_bail_%=\n\t"                                                            \
+    "s_mov_b32 s40, -1\n\t" /* the clock stays at the last second it reached */                   \
+    "s_or_b32 s44, s44, %[fck]\n\t"                                                               \
+    "s_branch mcsfd_exit_%=\n"                                                                    \
+    "mcsfd_poolovf_%=:\n\t"                                                                       \
+    "s_or_b32 s44, s44, %[fov]\n\t"                                                               \
                                                                                                   \
     /* ---- exit: state back to the compiler's registers ---- */                                 \
     "mcsfd_exit_%=:\n\t"                                                                          \
     "s_waitcnt vmcnt(0) lgkmcnt(0)\n\t"                                                           \
+    "s_mov_b64 exec, 1\n\t" /* the Level1 waits join lane 0's sum */                            \
+    "v_mov_b32 v104, s101\n\t"                                                                    \
+    "v_add_co_u32 v102, vcc, s100, v102\n\t"                                                      \
+    "v_addc_co_u32 v103, vcc, v104, v103, vcc\n\t"                                                \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
     "s_mov_b32 %[t], s40\n\t"                                                                     \
     "s_add_u32 %[r], s57, s47\n\t"                                                                \
     "s_mov_b32 %[cl], s47\n\t"                                                                    \
@@ -201,16 +533,16 @@ namespace {
     "s_max_u32 %[peak], s81, s80\n\t"                                                             \
     "s_mov_b32 %[nslow], s83\n\t"                                                                 \
     "s_mov_b32 %[nrel], s84\n\t"                                                                  \
+    "s_mov_b32 %[moved], s97\n\t"                                                                 \
+    "s_mov_b32 %[pl1], s98\n\t"                                                                   \
+    "s_mov_b32 %[pk1], s99\n\t"                                                                   \
+    "s_mov_b32 %[l1n], s92\n\t"                                                                   \
     "v_mov_b32 %[on], v91\n\t"                                                                    \
     "v_mov_b32 %[os], v92\n\t"                                                                    \
     "v_mov_b32 %[arr], v94\n\t"                                                                   \
     "v_mov_b32 %[wlo], v102\n\t"                                                                  \
     "v_mov_b32 %[whi], v103\n\t"                                                                  \
-    "s_cmp_eq_u32 s47, 0\n\t"                                                                     \
-    "s_cbranch_scc1 mcsfd_xf_%=\n\t"                                                              \
-    "v_add_u32 v93, v92, v95\n"                                                                   \
-    "mcsfd_xf_%=:\n\t"                                                                            \
-    "v_mov_b32 %[of], v93\n\t"                                                                    \
+    "v_add_u32 %[of], v92, v95\n\t"                                                               \
     "s_nop 1"
 
 template <bool DIAG>
@@ -219,7 +551,8 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
     const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
     const uint32_t lane = threadIdx.x;
 
-    __shared__ uint32_t lds[4 * kWave];  // the node copy [4][64] (releases)
+    // the node copy [4][64] (releases), the filter histogram [64], Level1 cm / jw / dur
+    __shared__ uint32_t lds[kLdsWords];
     constexpr uint32_t kGuard = 0x8000u, kClamp = kGuard - 1u;
     const uint32_t n0 = a.node_off[ci];
     const uint32_t N = a.node_off[ci + 1] - n0;
@@ -253,45 +586,68 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
     const uint32_t sel0 = 0x0b0a0908u, sel1 = base;
 
     uint32_t t = 0, r = 0, cl = 0, flags = 0, used = 0, peak = 0, n_slow = 0, n_rel = 0;
+    uint32_t moved = 0, pl1 = 0, pk1 = 0, l1n = 0;
     uint32_t on = 0, os = 0, of = 0, arr = 0, wlo = 0, whi = 0;
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
 #define MCS_FD_OPERANDS                                                                           \
     : [t] "=s"(t), [r] "=s"(r), [cl] "=s"(cl), [flags] "=s"(flags), [used] "=s"(used),          \
-      [peak] "=s"(peak), [nslow] "=s"(n_slow), [nrel] "=s"(n_rel), [on] "=v"(on), [os] "=v"(os), \
-      [of] "=v"(of), [arr] "=v"(arr), [wlo] "=v"(wlo), [whi] "=v"(whi)                           \
+      [peak] "=s"(peak), [nslow] "=s"(n_slow), [nrel] "=s"(n_rel), [moved] "=s"(moved),          \
+      [pl1] "=s"(pl1), [pk1] "=s"(pk1), [l1n] "=s"(l1n), [on] "=v"(on), [os] "=v"(os), [of] "=v"(of),             \
+      [arr] "=v"(arr), [wlo] "=v"(wlo), [whi] "=v"(whi)                                          \
     : [J] "s"(J), [mw] "s"(a.max_wait_s), [jobs] "s"(jobs), [onp] "s"(o_node), [osp] "s"(o_start), \
       [ofp] "s"(o_finish), [c0] "v"(cur.x), [c1] "v"(cur.y), [c2] "v"(cur.z), [c3] "v"(cur.w),    \
       [nb] "v"(v_nb), [lane] "v"(lane), [sel0] "s"(sel0), [sel1] "s"(sel1),                      \
-      [fck] "i"(MCS_FLAG_CLOCK_OVERFLOW), [fov] "i"(MCS_FLAG_OVERFLOW), [fbail] "i"(kDelayBail)        \
-    : MCS_FA_CLOBBERS, "v102", "v103", "v104"
+      [fck] "i"(MCS_FLAG_CLOCK_OVERFLOW), [fov] "i"(MCS_FLAG_OVERFLOW), [fbail] "i"(kDelayBail),  \
+      [fdl] "i"(MCS_FLAG_DEADLOCK),                                                             \
+      [cap] "i"(kL1Cap), [cap4] "i"(kL1Cap * 4), [cap8] "i"(kL1Cap * 8)                          \
+    : MCS_FA_CLOBBERS, "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99", "s100", "s101",    \
+      "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v88", "v102", "v103", "v104",     \
+      "v105", "v106", "v116"
     if constexpr (DIAG) asm volatile(MCS_FD_LOOP(D1) MCS_FD_OPERANDS);
     else asm volatile(MCS_FD_LOOP(D0) MCS_FD_OPERANDS);
 #undef MCS_FD_OPERANDS
 #pragma clang diagnostic pop
 
+    // the Level1 layout above: histogram at +1 KB, Level1 at +1.25 KB (v112 / v88 in the loop)
+    static_assert(4 * kWave * 4 == 0x400 && 5 * kWave * 4 == 0x500, "LDS layout");
+    static_assert(0x400 + 4 * 0x803f == 0x204fc, "filter key base");
+
+    // a pool overflow inside Level1's last stretch (no batch end to catch it): re-run
+    if (peak > 64u * 8u) flags |= MCS_FLAG_OVERFLOW;
     const bool bail = (flags & kDelayBail) != 0u;
-    // WaitTime.TotalTime / 1000 over the placed Level0 jobs: the stored batches (per lane) and the
-    // current batch's first cl rows (not stored yet)
+    // WaitTime.TotalTime / 1000 (scheduler.go:309-312,338-341): the stored Level0 batches (per
+    // lane), the current batch's Level0 placements (not stored yet) and, in lane 0, the Level1
+    // placements' t minus the moved jobs' arrivals
+    const bool mine = lane < cl && on != 0xFFFFFFFFu;
     uint64_t w = (uint64_t)wlo | ((uint64_t)whi << 32);
-    if (lane < cl) w += (uint64_t)(os - arr);
+    if (mine) w += (uint64_t)(os - arr);
     for (int o = 32; o >= 1; o >>= 1) {
         const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)w, o);
         const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(w >> 32), o);
         w += (uint64_t)lo | ((uint64_t)hi << 32);
     }
+    const uint32_t placed = r - moved + pl1;
+    // a deadlock (every Level0 job decided, nothing running, Level1 fits no node): the jobs left in
+    // Level1 hold 1000 * (t - arrival) in JobsMap (their arrivals are already subtracted)
+    const uint32_t left = (flags & MCS_FLAG_DEADLOCK) ? l1n : 0u;
+    if (lane == 0u) w += (uint64_t)left * t;
 
     if (!(flags & MCS_FLAG_OVERFLOW)) {
-        if (r > 0u) {  // the batch holding the last decision (earlier ones are stored)
-            const uint32_t i = ((r - 1u) & ~63u) + lane;
-            if (i < r) {
-                o_node[i] = (int32_t)((on & 63u) * 4u + (on >> 6));
-                o_start[i] = os;
-                o_finish[i] = of;
-            }
+        if (mine) {  // the current batch's Level0 placements (earlier batches are stored)
+            const uint32_t i = r - cl + lane;
+            o_node[i] = (int32_t)((on & 63u) * 4u + (on >> 6));
+            o_start[i] = os;
+            o_finish[i] = of;
         }
-        if (!bail && (flags & MCS_FLAG_CLOCK_OVERFLOW)) {
+        for (uint32_t i = lane; i < left; i += kWave) {  // never placed (scheduler.go:302-329 spins)
+            const uint32_t jw = lds[5 * kWave + kL1Cap + i];
+            o_node[jw] = MCS_NODE_UNPLACED;
+            o_start[jw] = MCS_TIME_NONE;
+            o_finish[jw] = MCS_TIME_NONE;
+        }
+        if (!bail && (flags & MCS_FLAG_CLOCK_OVERFLOW)) {  // (no job went through Level1)
             for (uint32_t i = r + lane; i < J; i += kWave) {
                 o_node[i] = MCS_NODE_UNPLACED;
                 o_start[i] = MCS_TIME_NONE;
@@ -302,8 +658,8 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
     if (lane == 0) {
         mcs_cluster_stats st;
         st.t_end = t;
-        st.placed = r;
-        st.waited = 0u;  // (moved to Level1: none on this path)
+        st.placed = placed;
+        st.waited = moved;
         st.peak_running = peak;
         st.flags = flags;  // (kBail: the engine re-runs the cluster, which rewrites these)
         st.pool = 8u;
@@ -318,13 +674,15 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
             mcs_delay_cluster_stats ds;
             ds.total_wait_ms = (int64_t)(w * 1000ull);
             ds.jobs_count = (flags & MCS_FLAG_CLOCK_OVERFLOW) ? -1 : (int64_t)J;
-            ds.moved_l1 = 0u;
-            ds.placed_l1 = 0u;
-            ds.peak_l1 = 0u;
-            ds.l1_left = 0u;
+            ds.moved_l1 = moved;
+            ds.placed_l1 = pl1;
+            ds.peak_l1 = pk1;
+            ds.l1_left = left;
             a.dstats[ci] = ds;
-            atomicAdd(&a.totals->placed, (unsigned long long)r);
-            atomicAdd(&a.totals->unplaced, (unsigned long long)(J - r));
+            atomicAdd(&a.totals->placed, (unsigned long long)placed);
+            atomicAdd(&a.totals->waited, (unsigned long long)moved);
+            atomicAdd(&a.totals->unplaced, (unsigned long long)(J - placed));
+            if (flags & MCS_FLAG_DEADLOCK) atomicAdd(&a.totals->deadlocked, 1u);
             if (flags & MCS_FLAG_CLOCK_OVERFLOW) atomicAdd(&a.totals->clock_overflowed, 1u);
         }
     }

@@ -511,6 +511,7 @@ int mcs_read_jobs(mcs_engine* e, uint32_t* arrival_s, uint32_t* dur_s, uint32_t*
 
 int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     if (int st = check_engine(e)) return st;
+    if (stats) *stats = mcs_stats{};
     if (!e->has_clusters || !e->has_jobs) return fail(e, MCS_E_STATE, "load clusters and jobs first");
     if (e->online || t_end_s != MCS_TIME_NONE) { /* online mode (mcs_online.cpp) */
         if (e->cfg.borrow || e->cfg.trader)
@@ -602,6 +603,7 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
         default: e->last_kernel = "mcs::fifo_kernel"; break;
     }
     mcs::Totals tot{};
+    uint32_t handed = 0;
     for (;;) {
         HIPCHK(e, hipEventRecord(e->ev0, e->stream));
         if (dasm)
@@ -618,6 +620,13 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
         kms += ms;
         pool_used = pool;
         const bool bailed = dasm && tot.bailed != 0;
+        if (bailed) {
+            handed = tot.bailed;
+            e->last_kernel_buf = std::string("mcs::delay_asm_kernel + mcs::delay_kernel (") +
+                                 std::to_string(handed) + " of " + std::to_string(e->C) +
+                                 " clusters handed over)";
+            e->last_kernel = e->last_kernel_buf.c_str();
+        }
         if (tot.overflowed == 0 && !bailed) break;
         /* clusters the DELAY loop handed over re-run on delay_kernel at the same pool (with the
          * loop's overflows, which then escalate there); capacity escalation: re-run only the
@@ -659,6 +668,7 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
         stats->pending = 0;
         stats->t_horizon = MCS_TIME_NONE;
         stats->online = 0;
+        stats->handed_over = handed;
     }
     if (tot.clock_overflowed)
         return fail(e, MCS_E_RANGE, std::to_string(tot.clock_overflowed) +

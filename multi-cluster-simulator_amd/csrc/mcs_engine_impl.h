@@ -86,6 +86,7 @@ struct mcs_engine {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::string err;
     const char* last_kernel = "";  // mcs_last_kernel: the first placement launch of the last run
+    std::string last_kernel_buf;   // (when last_kernel names a DELAY hand-over)
 
     uint32_t C = 0;
     uint32_t max_n = 0;

@@ -585,6 +585,7 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
 
 int mcs_trade_end(mcs_engine* e, mcs_stats* stats) {
     if (int st = check_engine(e)) return st;
+    if (stats) *stats = mcs_stats{};
     if (mcs::is_dtrade(e)) return mcs::dtrade_end(e, stats);
     mcs::TradeDev* td = e->td;
     if (!td || !td->begun) return fail(e, MCS_E_STATE, "mcs_trade_begin first");

@@ -109,6 +109,8 @@ class mcs_stats(C.Structure):
         ("pending", C.c_uint64),
         ("t_horizon", C.c_uint32),
         ("online", C.c_uint32),
+        ("handed_over", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 

@@ -123,11 +123,13 @@ class RunStats:
     pending: int = 0      # online: jobs not decided yet
     t_horizon: int = L.MCS_TIME_NONE
     online: bool = False
+    handed_over: int = 0  # DELAY: clusters the hand-scheduled loop handed to delay_kernel
 
     @classmethod
     def from_c(cls, st: "L.mcs_stats") -> "RunStats":
         return cls(st.jobs, st.placed, st.waited, st.unplaced, st.clusters, st.deadlocked, st.escalations,
-                   st.slot_pool, st.kernel_ms, st.wall_ms, st.pending, st.t_horizon, bool(st.online))
+                   st.slot_pool, st.kernel_ms, st.wall_ms, st.pending, st.t_horizon, bool(st.online),
+                   st.handed_over)
 
 
 CLUSTER_STATS_DTYPE = np.dtype([("t_end", "<u4"), ("placed", "<u4"), ("waited", "<u4"),

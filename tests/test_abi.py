@@ -36,7 +36,7 @@ def test_library_loads_and_exports_header_symbols():
     # every declared function has a ctypes signature in the binding
     bound = {name for name, _, _ in L.SIGNATURES}
     assert set(declared) == bound
-    assert lib.mcs_abi_version() == 5
+    assert lib.mcs_abi_version() == 6
 
 
 def test_library_is_gfx950_code_object():

@@ -150,10 +150,10 @@ def test_gpu_delay_fuzz(delay_engine, shape, seed):
 ])
 @pytest.mark.parametrize("diag", ["0", "1"])
 def test_gpu_delay_hand_scheduled_loop(kind, diag, monkeypatch):
-    """The hand-scheduled DELAY loop (mcs_delay_asm.hip, picked for 129-256 node clusters): its
-    clusters, and those it hands to delay_kernel at their first Level1 move (re-run from t = 0),
-    equal the oracle and the compiled kernel alone (MCS_DELAY_ASM=0) on every output the oracle
-    defines; MCS_FIFO_DIAG=1 launches its counting build."""
+    """The hand-scheduled DELAY loop (mcs_delay_asm.hip, picked for 129-256 node clusters) with
+    Level1 in LDS: its clusters, and those it hands to delay_kernel (re-run from t = 0: Level1 past
+    its 640-entry LDS slice), equal the oracle and the compiled kernel alone (MCS_DELAY_ASM=0) on
+    every output the oracle defines; MCS_FIFO_DIAG=1 launches its counting build."""
     if kind.startswith("fuzz"):
         arrays, streams = fuzz_workload("w16r", int(kind[4:]), n_clusters=64, J=1500)
     else:
@@ -161,8 +161,12 @@ def test_gpu_delay_hand_scheduled_loop(kind, diag, monkeypatch):
     monkeypatch.setenv("MCS_FIFO_DIAG", diag)
     with Engine(0, policy="DELAY") as eng:
         got = run(eng, arrays, streams)
-        assert eng.last_kernel == "mcs::delay_asm_kernel"
+        handed = got[3].handed_over
+        assert eng.last_kernel == ("mcs::delay_asm_kernel" if handed == 0 else
+                                   f"mcs::delay_asm_kernel + mcs::delay_kernel ({handed} of 64 clusters handed over)")
     assert_delay_parity(arrays, streams, *got[:3], got[4], got[5])
+    if kind.startswith("n256"):
+        assert handed == 0  # Level1 stays in the hand-scheduled loop
     monkeypatch.setenv("MCS_DELAY_ASM", "0")
     with Engine(0, policy="DELAY") as eng:
         ref = run(eng, arrays, streams)
@@ -180,6 +184,9 @@ def test_gpu_delay_hand_scheduled_loop(kind, diag, monkeypatch):
         assert (got[5]["moved_l1"] == 0).all()  # (no cluster needed the compiled kernel)
     if kind.startswith("fuzz"):
         assert (got[5]["moved_l1"] > 0).any()
+        # Level1 placements and deadlocks (the blocking requests) inside the loop; a cluster whose
+        # Level1 outgrows the LDS slice goes to delay_kernel
+        assert handed < 64 and (got[4]["flags"] & L.MCS_FLAG_DEADLOCK).any()
 
 
 @pytest.mark.parametrize("nodes", [64, 128, 200, 256, 512])
@@ -197,6 +204,8 @@ def test_gpu_delay_level1_heavy_generated(nodes):
     streams = gen_streams_host(gp, arrays, 2500)
     with Engine(0, policy="DELAY") as eng:
         node, start, fin, st, cs, ds = run(eng, arrays, streams)
+        if 129 <= nodes <= 256:  # the whole run in the hand-scheduled loop, Level1 included
+            assert eng.last_kernel == "mcs::delay_asm_kernel" and st.handed_over == 0
     assert_delay_parity(arrays, streams, node, start, fin, cs, ds)
     assert ds["moved_l1"].sum() > streams.n_jobs // 4
 
@@ -241,3 +250,39 @@ def test_gpu_delay_level1_filter_edges(seed):
         node, start, fin, st, cs, ds = run(eng, arrays, streams)
     assert_delay_parity(arrays, streams, node, start, fin, cs, ds)
     assert ds["moved_l1"].sum() > 0 and ds["placed_l1"].sum() > 0
+
+
+def _l1_pressure_workload(n_jobs_blocked, n_clusters=8, J=3000):
+    """256-node clusters of 2-core nodes whose streams hold n_jobs_blocked 3-core requests (they fit
+    no node: Level1 fills with them and the run ends in a Level1 deadlock) among small jobs."""
+    from mcs_amd import Cluster
+    from mcs_amd.cluster import Node
+
+    rng = np.random.default_rng(n_jobs_blocked)
+    cl = Cluster(Id=1, Nodes=[Node(Id=i + 1, Cores=2, Memory=4000, CoresAvailable=2, MemoryAvailable=4000)
+                              for i in range(256)])
+    arrays = replicate(cl, n_clusters)
+    parts = []
+    for k in range(n_clusters):
+        arr = np.cumsum(rng.poisson(0.5, J)).astype(np.uint32)
+        dur = rng.integers(0, 400, J).astype(np.uint32)
+        c = rng.integers(0, 3, J).astype(np.uint32)
+        m = rng.integers(0, 4001, J).astype(np.uint32)
+        blk = rng.choice(J, n_jobs_blocked, replace=False)
+        c[blk] = 3
+        parts.append((arr, dur, c, m))
+    off = np.arange(n_clusters + 1, dtype=np.uint64) * J
+    return arrays, JobStreams(*(np.concatenate([p[i] for p in parts]) for i in range(4)), off)
+
+
+@pytest.mark.parametrize("blocked,handed", [(100, False), (900, True)])
+def test_gpu_delay_level1_deadlock_and_capacity(blocked, handed):
+    """A Level1 that never drains: 100 never-fitting jobs end each cluster in a deadlock inside the
+    hand-scheduled loop (Level1 rows written unplaced, WaitTime of the jobs left); 900 outgrow the
+    640-entry LDS slice and the cluster is handed to delay_kernel.  Both bit-exact vs the oracle."""
+    arrays, streams = _l1_pressure_workload(blocked)
+    with Engine(0, policy="DELAY") as eng:
+        node, start, fin, st, cs, ds = run(eng, arrays, streams)
+        assert (st.handed_over == 8) == handed and (st.handed_over == 0) == (not handed)
+    assert_delay_parity(arrays, streams, node, start, fin, cs, ds)
+    assert (cs["flags"] & L.MCS_FLAG_DEADLOCK).all() and (ds["l1_left"] >= blocked).all()
