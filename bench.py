@@ -43,8 +43,18 @@ sys.path.insert(0, os.path.join(REPO, "multi-cluster-simulator_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 BYTES_PER_PLACEMENT = 28  # 16 B job record read + 12 B result write
 BYTES_PER_PLACEMENT_FUSED = 12  # --gen fused: the record is synthesised in registers, only results move
-LIMITER = ("latency: each cluster is a serial chain of decisions (one wave per cluster); HBM bytes are "
-           "exactly the algorithmic ones, the bound is the per-decision dependency chain (DESIGN.md §7)")
+LIMITER = ("latency: each cluster is a serial chain of decisions (one wave per cluster); the bound is the "
+           "per-decision dependency chain and issue work (DESIGN.md §7)")
+
+
+def limiter_text(traffic, algorithmic):
+    """The roofline limiter of this workload: the chain, with the measured HBM traffic against the
+    algorithmic bytes when a PMC pass of the same shape exists (profiles/)."""
+    if traffic is None:
+        return LIMITER + "; HBM traffic of this workload not measured (no PMC file of this shape)"
+    r = traffic / max(algorithmic, 1.0)
+    return LIMITER + f"; PMC HBM traffic {r:.2f}x the algorithmic bytes" + (
+        " (no wasted re-reads)" if r < 1.1 else " (bytes beyond the algorithmic ones: DESIGN.md §10)")
 
 
 def parse():
@@ -274,7 +284,7 @@ def main_c5_delay(args, world, rank, local_rank):
                 "parallelism": f"one system sharded over {world} GPU(s), {per} clusters each; "
                                + ("one RCCL all-gather of the exchange blocks per tick" if world > 1 else
                                   "exchange in HBM")
-                               + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "RCCL eager" if ts["loop_form"] == 1
+                               + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "graph-replayed after a resident timeout" if ts["loop_form"] == 6 else "RCCL eager" if ts["loop_form"] == 1
                                                     else "RCCL captured in a hipGraph" if ts["loop_form"] == 2
                                                     else "resident in one workgroup" if ts["loop_form"] == 3
                                                     else "resident, one workgroup per 16 clusters"
@@ -386,7 +396,7 @@ def main_c5(args, world, rank, local_rank):
                 "nodes": args.nodes,
                 "jobs_per_cluster": args.jobs_per_cluster,
                 "parallelism": (f"{world} shard(s); per-tick RCCL all-gather" if dist_on or args.comm else "1 GPU, exchange in HBM")
-                               + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "RCCL eager" if ts["loop_form"] == 1
+                               + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "graph-replayed after a resident timeout" if ts["loop_form"] == 6 else "RCCL eager" if ts["loop_form"] == 1
                                                     else "RCCL captured in a hipGraph" if ts["loop_form"] == 2
                                                     else "resident in one workgroup" if ts["loop_form"] == 3
                                                     else "resident, one workgroup per 16 clusters"
@@ -395,7 +405,7 @@ def main_c5(args, world, rank, local_rank):
             "roofline": {
                 "bound": "hbm",
                 "limiter": ("latency: the resident tick waits on the inter-workgroup X1 exchange (DESIGN.md §9)"
-                            if ts["loop_form"] >= 3 else
+                            if ts["loop_form"] in (3, 4, 5) else
                             "launch/latency: a tick is dependent launches of a few us (DESIGN.md §9)"),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
@@ -683,7 +693,7 @@ def main_batch(args, world, rank, local_rank):
             },
             "roofline": {
                 "bound": "hbm",
-                "limiter": LIMITER,
+                "limiter": limiter_text(traffic, placements_per_launch * bpp),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

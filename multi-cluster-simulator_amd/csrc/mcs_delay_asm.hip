@@ -64,12 +64,24 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
 //   v112 histogram lane address  v113 histogram base + 4 * 0x803f  v114/v115/v123 temps
 //   v116 D6 fold  v118 0x8000  v122 0x803f   s56 MaxWaitTime
 //
+// probe counters of the counting build (MCS_FIFO_DIAG=1; printed by the engine with
+// MCS_DELAY_PROBE=1): lane k of v119 counts event k (0 passes run, 1 passes skipped by the bound,
+// 2 rows, 3 candidates, 4 candidates whose first fit failed, 5 filter builds, 6 D6 skips,
+// 7 compactions, 8 mode-1 iterations)
+#define MCS_FD_P_D0(k) ""
+#define MCS_FD_P_D1(k) "s_mov_b64 exec, 1<<" #k "\n\tv_add_u32 v119, 1, v119\n\ts_mov_b64 exec, -1\n\t"
+// (a skipped pass: straight to the Level0 head, or through its counter)
+#define MCS_FD_PSK_D0 "mcsfd_head1_%="
+#define MCS_FD_PSK_D1 "mcsfd_pskip_%="
+#define MCS_FD_PSKB_D0 ""
+#define MCS_FD_PSKB_D1 "s_branch mcsfd_head1_%=\nmcsfd_pskip_%=:\n\t" MCS_FD_P_D1(1)
+
 // the fit filter (scheduler.go:305, ScheduleJob's outcome without its node): lane i of v105 =
 // max guarded free memory (2^15 + free_m; padding nodes hold 0x7fff, below every request) over the
 // nodes with min(free cores, 63) >= 63 - i.  An LDS ds_max_u32 histogram over the reversed core keys
 // (key address = base - 4 * clamp(2^15 + free_c, 0x8000, 0x803f)), then a DPP inclusive prefix max.
-#define MCS_FD_BUILD                                                                              \
-    "v_mov_b32 v114, 0\n\t"                                                                       \
+#define MCS_FD_BUILD(D)                                                                           \
+    MCS_FD_P_##D(5) "v_mov_b32 v114, 0\n\t"                                                                       \
     "ds_write_b32 v112, v114\n\t"                                                                 \
     "v_bfe_u32 v72, v64, 0, 16\n\t"                                                               \
     "v_bfe_u32 v73, v65, 0, 16\n\t"                                                               \
@@ -161,18 +173,18 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_branch mcsfd_placed" #M "_%=\n"
 
 // the Level1 pass (scheduler.go:302-329), mode 1 only; falls through to the Level0 head
-#define MCS_FD_PASS                                                                               \
+#define MCS_FD_PASS(D)                                                                               \
     "s_mov_b32 s43, 0\n\t"                                                                        \
     "s_cmp_eq_u32 s96, 0\n\t"                                                                     \
-    "s_cbranch_scc1 mcsfd_chk_%=\n\t" MCS_FD_BUILD                                                \
+    "s_cbranch_scc1 mcsfd_chk_%=\n\t" MCS_FD_BUILD(D)                                             \
     "mcsfd_chk_%=:\n\t"                                                                           \
     "v_cmp_ge_u32_e32 vcc, v105, v106\n\t" /* a lane whose jobs may fit */                      \
-    "s_cbranch_vccz mcsfd_head1_%=\n\t"                                                           \
+    "s_cbranch_vccz " MCS_FD_PSK_##D "\n\t" MCS_FD_P_##D(0)                                       \
     "s_mov_b32 s93, 0\n\t"                                                                        \
     "s_mov_b32 s94, 0\n\t"                                                                        \
     "s_mov_b32 s95, -1\n\t"                                                                       \
     "v_mov_b32 v116, -1\n"                                                                        \
-    "mcsfd_row_%=:\n\t"                                                                           \
+    "mcsfd_row_%=:\n\t" MCS_FD_P_##D(2)                                                           \
     "s_lshl_b32 s74, s94, 2\n\t"                                                                  \
     "v_add_u32 v63, s74, v88\n\t"                                                                 \
     "ds_read_b32 v56, v63\n\t"                                                                    \
@@ -201,10 +213,10 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_bitset0_b64 s[58:59], s82\n\t"                                                             \
     "s_add_u32 s74, s94, s82\n\t"                                                                 \
     "s_cmp_eq_u32 s74, s95\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfd_d6_%=\n\t" MCS_FA_FIT16 MCS_FA_ANYFIT                                   \
+    "s_cbranch_scc1 mcsfd_d6_%=\n\t" MCS_FD_P_##D(3) MCS_FA_FIT16 MCS_FA_ANYFIT                    \
     "v_readlane_b32 s46, v58, s82\n\t"                                                            \
     "v_readlane_b32 s75, v57, s82\n\t"                                                            \
-    "s_cbranch_vccz mcsfd_cand_%=\n\t" /* (key 0, 63 or more cores: the filter is conservative) */ \
+    "s_cbranch_vccz mcsfd_nofitc_%=\n\t" /* (key 0, 63 or more cores: the filter is conservative) */ \
     "s_ff1_i32_b64 s50, vcc\n\t"                                                                  \
     "s_add_u32 s55, s40, s46\n\t"                                                                 \
     "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
@@ -235,12 +247,14 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_addc_u32 s101, s101, 0\n\t"                                                                \
     "s_mov_b32 s43, 1\n\t"                                                                        \
     "s_cmp_eq_u32 s96, 0\n\t" /* a zero-duration job changed no node */                          \
-    "s_cbranch_scc1 mcsfd_cand_%=\n\t" MCS_FD_BUILD                                               \
+    "s_cbranch_scc1 mcsfd_cand_%=\n\t" MCS_FD_BUILD(D)                                            \
     /* the commit shrank a node: the rest of the row is re-tested on the rebuilt filter */        \
     "ds_bpermute_b32 v60, v59, v105\n\t"                                                          \
     "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
     "v_cmp_ge_u32_e32 vcc, v60, v61\n\t"                                                          \
     "s_and_b64 s[58:59], s[58:59], vcc\n\t"                                                       \
+    "s_branch mcsfd_cand_%=\n"                                                                    \
+    "mcsfd_nofitc_%=:\n\t" MCS_FD_P_##D(4)                                                        \
     "s_branch mcsfd_cand_%=\n"                                                                    \
     "mcsfd_l1zero_%=:\n\t"                                                                        \
     "v_readlane_b32 s51, v86, s50\n\t"                                                            \
@@ -249,7 +263,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_mov_b32 s55, s40\n\t"                                                                      \
     "s_branch mcsfd_l1res_%=\n"                                                                   \
     /* D6-skipped: folded into the pass-skip bound as it is (it was not tested) */               \
-    "mcsfd_d6_%=:\n\t"                                                                            \
+    "mcsfd_d6_%=:\n\t" MCS_FD_P_##D(6)                                                            \
     "v_readlane_b32 s74, v59, s82\n\t"                                                            \
     "v_readlane_b32 s76, v61, s82\n\t"                                                            \
     "s_lshr_b32 s74, s74, 2\n\t"                                                                  \
@@ -264,7 +278,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_cbranch_scc1 mcsfd_cmp_%=\n\t"                                                             \
     "s_cmp_eq_u32 s93, s94\n\t"                                                                   \
     "s_cbranch_scc1 mcsfd_rown_%=\n"                                                              \
-    "mcsfd_cmp_%=:\n\t"                                                                           \
+    "mcsfd_cmp_%=:\n\t" MCS_FD_P_##D(7)                                                           \
     "s_mov_b64 exec, s[88:89]\n\t"                                                                \
     "v_mbcnt_lo_u32_b32 v62, s88, 0\n\t"                                                          \
     "v_mbcnt_hi_u32_b32 v62, s89, v62\n\t" /* rank among the kept entries */                    \
@@ -292,7 +306,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_mov_b64 exec, -2\n\t"                                                                      \
     "v_max_u32 v106, v106, v62\n\t"                                                               \
     "s_mov_b64 exec, -1\n\t"                                                                      \
-    "v_min_u32 v106, v106, v116\n"
+    "v_min_u32 v106, v106, v116\n\t" MCS_FD_PSKB_##D
 
 #define MCS_FD_LOOP(D)                                                                            \
     /* ---- entry: state into the fixed registers ---- */                                        \
@@ -332,6 +346,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "v_mov_b32 v103, 0\n\t"                                                                       \
     "v_mov_b32 v91, -1\n\t"                                                                       \
     "v_mov_b32 v106, -1\n\t" /* no Level1 job of any key */                                      \
+    "v_mov_b32 v119, 0\n\t"                                                                       \
     "v_mov_b32 v118, 0x8000\n\t"                                                                  \
     "v_mov_b32 v122, 0x803f\n\t"                                                                  \
     "v_add_u32 v112, 0x400, v108\n\t" /* the histogram (after the node copy) */                  \
@@ -403,7 +418,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     /* ======== mode 1: Level1 holds jobs ======== */                                            \
     "mcsfd_inner1_%=:\n\t"                                                                        \
     "s_cmp_eq_u32 s92, 0\n\t"                                                                     \
-    "s_cbranch_scc1 mcsfd_inner0_%=\n\t" MCS_FA_CNTS_##D MCS_FD_PASS                              \
+    "s_cbranch_scc1 mcsfd_inner0_%=\n\t" MCS_FA_CNTS_##D MCS_FD_P_##D(8) MCS_FD_PASS(D)            \
     "mcsfd_head1_%=:\n\t" MCS_FD_HEAD(1, "s_mov_b32 s96, 1\n\t")                                  \
     "s_branch mcsfd_rel_%=\n" MCS_FD_ZERO(1)                                                      \
     "mcsfd_idle1_%=:\n\t"                                                                         \
@@ -543,6 +558,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "v_mov_b32 %[wlo], v102\n\t"                                                                  \
     "v_mov_b32 %[whi], v103\n\t"                                                                  \
     "v_add_u32 %[of], v92, v95\n\t"                                                               \
+    "v_mov_b32 %[prb], v119\n\t"                                                                  \
     "s_nop 1"
 
 template <bool DIAG>
@@ -587,7 +603,7 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
 
     uint32_t t = 0, r = 0, cl = 0, flags = 0, used = 0, peak = 0, n_slow = 0, n_rel = 0;
     uint32_t moved = 0, pl1 = 0, pk1 = 0, l1n = 0;
-    uint32_t on = 0, os = 0, of = 0, arr = 0, wlo = 0, whi = 0;
+    uint32_t on = 0, os = 0, of = 0, arr = 0, wlo = 0, whi = 0, prb = 0;
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
@@ -595,7 +611,7 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
     : [t] "=s"(t), [r] "=s"(r), [cl] "=s"(cl), [flags] "=s"(flags), [used] "=s"(used),          \
       [peak] "=s"(peak), [nslow] "=s"(n_slow), [nrel] "=s"(n_rel), [moved] "=s"(moved),          \
       [pl1] "=s"(pl1), [pk1] "=s"(pk1), [l1n] "=s"(l1n), [on] "=v"(on), [os] "=v"(os), [of] "=v"(of),             \
-      [arr] "=v"(arr), [wlo] "=v"(wlo), [whi] "=v"(whi)                                          \
+      [arr] "=v"(arr), [wlo] "=v"(wlo), [whi] "=v"(whi), [prb] "=v"(prb)                         \
     : [J] "s"(J), [mw] "s"(a.max_wait_s), [jobs] "s"(jobs), [onp] "s"(o_node), [osp] "s"(o_start), \
       [ofp] "s"(o_finish), [c0] "v"(cur.x), [c1] "v"(cur.y), [c2] "v"(cur.z), [c3] "v"(cur.w),    \
       [nb] "v"(v_nb), [lane] "v"(lane), [sel0] "s"(sel0), [sel1] "s"(sel1),                      \
@@ -604,7 +620,7 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
       [cap] "i"(kL1Cap), [cap4] "i"(kL1Cap * 4), [cap8] "i"(kL1Cap * 8)                          \
     : MCS_FA_CLOBBERS, "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99", "s100", "s101",    \
       "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v88", "v102", "v103", "v104",     \
-      "v105", "v106", "v116"
+      "v105", "v106", "v116", "v119"
     if constexpr (DIAG) asm volatile(MCS_FD_LOOP(D1) MCS_FD_OPERANDS);
     else asm volatile(MCS_FD_LOOP(D0) MCS_FD_OPERANDS);
 #undef MCS_FD_OPERANDS
@@ -614,6 +630,8 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
     static_assert(4 * kWave * 4 == 0x400 && 5 * kWave * 4 == 0x500, "LDS layout");
     static_assert(0x400 + 4 * 0x803f == 0x204fc, "filter key base");
 
+    // the counting build's probe counters: into the cluster's (otherwise unused) HBM Level1 scratch
+    if (DIAG && lane < 9u && 2u * J > lane) reinterpret_cast<uint32_t*>(a.l1_cm + j0)[lane] = prb;
     // a pool overflow inside Level1's last stretch (no batch end to catch it): re-run
     if (peak > 64u * 8u) flags |= MCS_FLAG_OVERFLOW;
     const bool bail = (flags & kDelayBail) != 0u;

@@ -53,6 +53,7 @@ constexpr uint32_t kLoopRcclGraph = 2;  // RCCL all-gather per tick, captured wi
 constexpr uint32_t kLoopResident = 3;   // one engine, the whole system resident in one workgroup
 constexpr uint32_t kLoopResidentMwXcd = 5;  // the same, its workgroups on one XCD (L2 exchange)
 constexpr uint32_t kLoopResidentMw = 4;  // one engine, resident in ceil(C / 16) workgroups (granules)
+constexpr uint32_t kLoopGraphAfterTimeout = 6;  // the replayed kernels after a resident exchange timed out
 
 // Capture `ticks` ticks of `tick(stream)` (kernels and the RCCL all-gather) into one executable
 // graph.  Returns nullptr, with the stream out of capture mode and the HIP error state cleared, when
@@ -129,6 +130,8 @@ struct mcs_engine {
     mcs::TradeDev* td = nullptr;
     bool trade_run = false;  // results of the last run come from the lock-step path
     uint32_t tr_lq = 0, tr_slots = 0;  // capacity escalation of the lock-step path (0 = auto)
+    bool tr_res_start = false;  // trade_run's local loop on a resident form: start at 512 slots
+    bool tr_no_resident = false;  // a resident tick timed out in this run: the replayed kernels
     mcs::DtradeDev* dtd = nullptr;     // DELAY trading state (mcs_dtrade.cpp)
     bool dtrade_run = false;           // results of the last run come from DELAY trading
     uint32_t dt_vnodes = 0;            // virtual-node capacity per cluster (0 = auto)

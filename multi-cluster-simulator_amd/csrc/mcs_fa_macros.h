@@ -4,6 +4,36 @@
 // only (inline-asm text).
 #pragma once
 
+// ---- gfx950 hazard audit of the hand-scheduled loops (FIFO W16R/W16S/fused, duo, DELAY) -----------
+// LLVM's hazard recognizer does not look inside inline asm, so every producer -> consumer pair the
+// hardware does not interlock is covered here by instruction distance or an explicit s_nop.  A
+// "wait state" is one issued instruction of this wave (s_nop N = N + 1 of them).
+//
+//  hazard (CDNA3/gfx950)                           needs  where it occurs                     covered by
+//  VALU writes VGPR -> DPP reads it                  2     every DPP min/max chain (SCANEND,   s_nop 1 between the steps; before
+//                                                          the DELAY filter, the duo e2 scan)  the first: s_nop 1, or (DELAY rel)
+//                                                                                              s_mov s96 + s_nop 0
+//  SDWA / op_sel write preserving the other word     1     MCS_FA_FIT16: v80/v81 (WORD_1,      v_cmp_lt s[60:61] + v_ffbl v117
+//    -> VALU reads that VGPR (DstSelForwarding)            UNUSED_PRESERVE) -> v_perm          between (found by measurement,
+//                                                                                              tools/asm_debug.py); FIT16D: s_nop 1
+//  VALU writes SGPR -> v_readlane / v_writelane      4     none: every lane select is SALU-    (s50/s85/s82 from s_ff1, s47/m0
+//    uses it as the lane select                            written                             from s_add/s_mov)
+//  SALU writes M0 -> v_writelane with an M0 lane     1*    result writes at a Level0 decision  >= 1 other instruction between
+//    select (*not in the ISA table; kept anyway)           (HEAD, ZEROKX)                      (s_add s80 / s_ff1, s_lshl3_add)
+//  VALU writes VGPR -> v_readlane / v_readfirstlane  1     DECIDE16R / ZEROKX read v86, v117;  >= 3 instructions between every
+//    reads it (gfx950)                                     REC16 after TAKE16; SCANEND v120     pair; SCANEND: s_nop 1
+//  VALU writes VCC -> s_cbranch_vccz/vccnz           0     ANYFIT -> the fit branch             (interlocked on gfx9; SALU
+//                                                                                              instructions between anyway)
+//  VALU writes EXEC -> DPP (5) / v_readlane (4)      5/4   none: exec is written by SALU only   (no v_cmpx in any loop)
+//  VMEM store of > 64 bits -> its data VGPRs         1     none: every store is one dword       -
+//    rewritten
+//  VALU writes SGPR -> VMEM reads it (address/      5     none: the store/load bases s[64:71]   -
+//    soffset)                                              are SALU-written
+//  s_set_gpr_idx_on -> indexed VALU, _off -> plain   0     DECIDE16R / COMMIT16 / INSERT16R     (the indexed moves sit between
+//                                                                                              on and off; no non-indexed VALU
+//                                                                                              read inside a region)
+// A reorder that moves a consumer next to its producer in the table must add the s_nop.
+
 // Register map of the loop (all fixed; listed as clobbers).
 //   s40 t     s41 min(64, J - cb)  s42 J   s43 have_w  s44 flags  s45 arr   s46 dur
 //   s47 cursor's lane in the batch (r - cb)  s48 (W16: {cores|mem<<16}) / s[48:49] cores, mem

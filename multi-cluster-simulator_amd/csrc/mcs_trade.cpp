@@ -62,8 +62,10 @@ uint32_t auto_slots(uint32_t max_n) {
 }
 
 // a one-engine system the resident tick kernel can hold (mcs_trade_res.hip; the LDS check is
-// resident_form's).  Its slot finish times live in VGPRs, so such a system starts at 512 slots per
-// cluster (8 rows; 1024 spill): an overflow re-runs it at 1024 like any other pool overflow.
+// resident_form's).  Its slot finish times live in VGPRs, so trade_run's local loop starts such a
+// system at 512 slots per cluster (8 rows; 1024 spill) when a resident form will run it: an overflow
+// re-runs it at 1024 like any other pool overflow.  The caller-driven path (mcs_trade_begin) and the
+// RCCL loop keep auto_slots (they have no resident form and, caller-driven, no escalation).
 bool resident_wanted(const mcs_engine* e) {
     const char* env = getenv("MCS_TRADE_RESIDENT");
     if (env && atoi(env) == 0) return false;
@@ -92,7 +94,7 @@ int trade_alloc(mcs_engine* e) {
     if (e->max_n > kTrMaxNodes) return fail(e, MCS_E_INVALID, "more than 1024 nodes in a cluster");
     const uint32_t S = e->cfg.slot_pool ? 64u * e->cfg.slot_pool
                        : e->tr_slots       ? e->tr_slots
-                       : resident_wanted(e) ? std::min<uint32_t>(512u, auto_slots(e->max_n))
+                       : e->tr_res_start   ? std::min<uint32_t>(512u, auto_slots(e->max_n))
                                            : auto_slots(e->max_n);
     if (S > kTrMaxSlots) return fail(e, MCS_E_INVALID, "slot pool above 4096");
     const uint32_t LQ = e->cfg.lent_queue_cap ? e->cfg.lent_queue_cap : (e->tr_lq ? e->tr_lq : auto_lq(e));
@@ -181,13 +183,20 @@ int poll_ctl(mcs_engine* e) {
 // kResTicks ticks per launch; otherwise the four phases of kGraphTicks ticks are captured once and
 // replayed.  MCS_TRADE_RESIDENT=0 forces the replayed kernels.
 constexpr uint32_t kResTicks = 1u << 16;
+// (MCS_TRADE_RES_TICKS: a smaller budget, so tests cross launch boundaries)
+uint32_t res_ticks() {
+    const char* env = getenv("MCS_TRADE_RES_TICKS");
+    const long v = env ? atol(env) : 0;
+    return v > 0 && v < (long)kResTicks ? (uint32_t)v : kResTicks;
+}
+constexpr int kMwFallback = -100;  // run_local: a resident exchange timed out (trade_run re-runs)
 
 // MCS_TRADE_RESIDENT: 0 = the replayed kernels, 1 = one workgroup, 2 = one workgroup per 16
 // clusters (the default where the shape allows it)
 int resident_form(mcs_engine* e, size_t* lds) {
     const char* env = getenv("MCS_TRADE_RESIDENT");
     const int want = env ? atoi(env) : 2;
-    if (want == 0 || !e->sums_lt24) return 0;
+    if (want == 0 || !e->sums_lt24 || e->tr_no_resident) return 0;
     int max_lds = 0;
     if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device) != hipSuccess)
         return 0;
@@ -223,12 +232,17 @@ int run_local(mcs_engine* e) {
         // consecutive blocks, the write-through exchange)
         const char* xenv = getenv("MCS_MW_XCD");
         const bool xcd_pack = !xenv || atoi(xenv) != 0;
-        for (;;) {
-            const hipError_t st = launch_trade_mw(td->a, td->gx, td->gxc, kResTicks, lds, xcd_pack, e->stream);
+        const uint32_t budget = res_ticks();
+        for (uint32_t launch = 0;; ++launch) {
+            const hipError_t st = launch_trade_mw(td->a, td->gx, td->gxc, budget, launch * budget, lds, xcd_pack,
+                                                  e->stream);
             if (st != hipSuccess) return hip_fail(e, "resident tick kernel (workgroups)", st);
             if (int s = poll_ctl(e)) return s;
-            if (td->h_ctl->flags & kTrFlagMwTimeout)
-                return fail(e, MCS_E_HIP, "resident tick: a workgroup exchange timed out");
+            // every worker block must be resident at once; when another stream or process holds
+            // CUs a bounded exchange sweep gives up: the run is redone on the replayed kernels
+            // (MCS_MW_FORCE_TIMEOUT=1: tests take this path after the first launch)
+            if (td->h_ctl->flags & kTrFlagMwTimeout) return kMwFallback;
+            if (const char* ft = getenv("MCS_MW_FORCE_TIMEOUT"); ft && atoi(ft) != 0) return kMwFallback;
             td->loop_form = td->h_ctl->info ? kLoopResidentMwXcd : kLoopResidentMw;
             if (td->h_ctl->done) return MCS_OK;
         }
@@ -236,7 +250,7 @@ int run_local(mcs_engine* e) {
     if (rf == 1) {
         td->loop_form = kLoopResident;
         for (;;) {
-            const hipError_t st = launch_trade_resident(td->a, kResTicks, lds, e->stream);
+            const hipError_t st = launch_trade_resident(td->a, res_ticks(), lds, e->stream);
             if (st != hipSuccess) return hip_fail(e, "resident tick kernel", st);
             if (int s = poll_ctl(e)) return s;
             if (td->h_ctl->done) return MCS_OK;
@@ -260,7 +274,7 @@ int run_local(mcs_engine* e) {
         if (st != hipSuccess) return hip_fail(e, "hipGraphInstantiate", st);
         td->graph_ticks = kGraphTicks;
     }
-    td->loop_form = kLoopGraph;
+    td->loop_form = e->tr_no_resident ? kLoopGraphAfterTimeout : kLoopGraph;
     for (;;) {
         HIPCHK(e, hipGraphLaunch(td->graph, e->stream));
         if (int s = poll_ctl(e)) return s;
@@ -436,11 +450,36 @@ int trade_run(mcs_engine* e, mcs_stats* stats) {
     if (e->comm && !e->td)
         if (int s = tr_agree_shape(e)) return s;
     e->tr_lq = e->tr_slots = 0;
+    e->tr_no_resident = false;
+    e->tr_res_start = !e->comm && !e->cfg.slot_pool && resident_wanted(e);
+    struct Reset {
+        mcs_engine* e;
+        ~Reset() { e->tr_res_start = e->tr_no_resident = false; }
+    } reset{e};
     uint32_t escalations = 0;
     for (;;) {
         if (int s = mcs_trade_begin(e)) return s;
+        if (e->tr_res_start && !e->tr_slots) {
+            size_t lds = 0;
+            if (resident_form(e, &lds) == 0) {  // no resident form after all: the auto pool
+                e->tr_res_start = false;
+                trade_free(e);
+                continue;
+            }
+        }
         // a communicator selects the RCCL loop (world 1 included: one rank's all-gather is a copy)
-        if (int s = e->comm ? run_rccl(e) : run_local(e)) return s;
+        const int rs = e->comm ? run_rccl(e) : run_local(e);
+        if (rs == kMwFallback) {
+            const uint32_t lq = e->tr_lq, sl = e->tr_slots, ns = e->tr_ns;
+            trade_free(e);
+            e->tr_lq = lq;
+            e->tr_slots = sl;
+            e->tr_ns = ns;
+            e->tr_no_resident = true;
+            e->tr_res_start = false;
+            continue;
+        }
+        if (rs) return rs;
         const int s = mcs_trade_end(e, stats);
         if (s != MCS_E_CAPACITY) {
             if (stats) stats->escalations = escalations;

@@ -148,7 +148,7 @@ constexpr size_t trade_mw_xcc_off() { return (size_t)kTrResMaxClusters * 10u + 1
 // gx_uc: uncached granules (any placement); gx_c: cached granules, used when every workgroup runs on
 // one XCD; xcd_pack: launch the workers 8 blocks apart (one XCD under round-robin dispatch)
 hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsigned long long* gx_c,
-                           uint32_t tick_budget, size_t lds, bool xcd_pack, hipStream_t s);
+                           uint32_t tick_budget, uint32_t tick0, size_t lds, bool xcd_pack, hipStream_t s);
 constexpr uint32_t kTrFlagMwTimeout = 0x80000000u;  // internal: an exchange sweep gave up
 
 }  // namespace mcs

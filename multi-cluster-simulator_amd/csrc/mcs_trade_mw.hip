@@ -140,7 +140,7 @@ struct MwShared {  // (this workgroup's node vectors follow: kMwWaves * ns u64)
 template <int kRows>  // slot rows per cluster (64 slots each)
 __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, unsigned long long* gx_uc,
                                                                  unsigned long long* gx_c, uint32_t tick_budget,
-                                                                 uint32_t nwg, uint32_t stride) {
+                                                                 uint32_t nwg, uint32_t stride, uint32_t tick0) {
     // the workers are blocks 0, stride, 2 * stride, ...: with stride 8 they share one XCD under the
     // dispatcher's observed round-robin placement (speed only: the check below decides the protocol)
     if (blockIdx.x % stride != 0u) return;
@@ -335,7 +335,9 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
         if (sh.done) break;
         MW_MARK(9);
         const uint32_t T = sh.T;
-        const uint32_t tag1 = 2u * it + 1u, tag2 = 2u * it + 2u;
+        // epochs count from the run's first tick, across launches: a granule line another launch
+        // left in an XCD's L2 never carries a current tag
+        const uint32_t tag1 = 2u * (tick0 + it) + 1u, tag2 = tag1 + 1u;
 
         // GetResourceUtilization runs on the ticks a trader reads it (see tr_step_kernel)
         bool sample = false;
@@ -893,10 +895,11 @@ bool trade_mw_shape(const TradeArgs& a) {
 size_t trade_mw_granules(uint32_t) { return trade_mw_xcc_off() + kWave; }
 
 hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsigned long long* gx_c,
-                           uint32_t tick_budget, size_t lds, bool xcd_pack, hipStream_t s) {
+                           uint32_t tick_budget, uint32_t tick0, size_t lds, bool xcd_pack, hipStream_t s) {
     const uint32_t nwg = (a.Ct + kMwWaves - 1) / kMwWaves;
     const uint32_t stride = xcd_pack ? 8u : 1u, nblk = stride * (nwg - 1u) + 1u;
-    // the granules carry epochs counted within the launch: zero them first
+    // the granules carry epochs counted from the run's first tick (tick0 = the ticks of the run's
+    // earlier launches); zeroed before every launch as well (no tag is 0)
     hipError_t st = hipMemsetAsync(gx_uc, 0, trade_mw_granules(a.Ct) * 8u, s);
     if (st != hipSuccess) return st;
     st = hipMemsetAsync(gx_c, 0, trade_mw_granules(a.Ct) * 8u, s);
@@ -908,13 +911,13 @@ hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsign
     if (st != hipSuccess) return st;
     if (a.S == 4u * kWave)
         hipLaunchKernelGGL(tr_mw_kernel<4>, dim3(nblk), dim3(kMwWaves * kWave), lds, s, a, gx_uc, gx_c, tick_budget,
-                           nwg, stride);
+                           nwg, stride, tick0);
     else if (a.S == 8u * kWave)
         hipLaunchKernelGGL(tr_mw_kernel<8>, dim3(nblk), dim3(kMwWaves * kWave), lds, s, a, gx_uc, gx_c, tick_budget,
-                           nwg, stride);
+                           nwg, stride, tick0);
     else
         hipLaunchKernelGGL(tr_mw_kernel<16>, dim3(nblk), dim3(kMwWaves * kWave), lds, s, a, gx_uc, gx_c, tick_budget,
-                           nwg, stride);
+                           nwg, stride, tick0);
     return hipGetLastError();
 }
 

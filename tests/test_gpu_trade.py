@@ -253,3 +253,43 @@ def test_gpu_trade_resident_form_by_capacity(monkeypatch):
         g = gpu_trade(arrays, streams)
         assert g["tstats"]["loop_form"] in ((4, 5) if want == 4 else (want,)), cores
         assert_trade_parity(arrays, streams, g)
+
+
+def test_gpu_trade_caller_driven_256_nodes_world1():
+    """The caller-driven path at world 1 with 256-node clusters keeps the automatic slot pool (the
+    512-slot start is trade_run's, for a resident form only): no capacity error, == the oracle."""
+    arrays, streams, _ = seeded_workload("n256", 16, 1500)
+    g = gpu_trade(arrays, streams, driven=True)
+    assert_trade_parity(arrays, streams, g)
+
+
+@pytest.mark.parametrize("ticks", ["64", "1000"])
+def test_gpu_trade_resident_short_launches(ticks, monkeypatch):
+    """The resident tick over many short launches (MCS_TRADE_RES_TICKS): granule epochs count from
+    the run's first tick, so a line a previous launch left in an XCD's L2 never matches; placements,
+    lent log and trades == the replayed kernels (MCS_TRADE_RESIDENT=0) == the oracle."""
+    arrays, streams, _ = seeded_workload("n256", 64, 1200)
+    monkeypatch.setenv("MCS_TRADE_RES_TICKS", ticks)
+    a = gpu_trade(arrays, streams)
+    assert a["tstats"]["loop_form"] in (4, 5)
+    monkeypatch.delenv("MCS_TRADE_RES_TICKS")
+    monkeypatch.setenv("MCS_TRADE_RESIDENT", "0")
+    b = gpu_trade(arrays, streams)
+    assert b["tstats"]["loop_form"] == 0
+    for k in ("node", "start", "finish", "virtual_nodes"):
+        np.testing.assert_array_equal(a[k], b[k])
+    assert lent_rows(a["lent"]) == lent_rows(b["lent"])
+    assert trade_rows(a["trades"]) == trade_rows(b["trades"])
+    assert a["tstats"]["t_final"] == b["tstats"]["t_final"]
+    assert_trade_parity(arrays, streams, a)
+
+
+def test_gpu_trade_resident_timeout_falls_back(monkeypatch):
+    """A resident exchange that times out (forced after the first launch) is redone from the start
+    on the replayed kernels (loop_form 6) instead of failing the run; results == the oracle."""
+    arrays, streams, _ = seeded_workload("n256", 64, 1200)
+    monkeypatch.setenv("MCS_TRADE_RES_TICKS", "256")
+    monkeypatch.setenv("MCS_MW_FORCE_TIMEOUT", "1")
+    g = gpu_trade(arrays, streams)
+    assert g["tstats"]["loop_form"] == 6
+    assert_trade_parity(arrays, streams, g)

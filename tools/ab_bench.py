@@ -2,7 +2,8 @@
 alternating variants round-robin so box-to-box and thermal drift cancel.
 
 usage: python tools/ab_bench.py lib_a.so lib_b.so[@VAR=value] [...] [--rounds 3] [--steps 5]
-(env AB_POLICY=FIFO|DELAY, AB_NODES, AB_LOAD, AB_CLUSTERS select the workload; default C4 FIFO)
+(env AB_POLICY=FIFO|DELAY, AB_NODES, AB_LOAD, AB_CLUSTERS, AB_LAM, AB_MAXDUR select the workload;
+default C4 FIFO; AB_POLICY=DELAY AB_LAM=0.95 AB_MAXDUR=972 is the Level1-heavy DELAY stream)
 Each variant runs in its own subprocess (MCS_LIB=<path>) per round; prints median kernel ms."""
 import json
 import os
@@ -22,7 +23,8 @@ nn, load = int(os.environ.get("AB_NODES", "256")), float(os.environ.get("AB_LOAD
 eng = Engine(0, policy=os.environ.get("AB_POLICY", "FIFO"))
 nc = int(os.environ.get("AB_CLUSTERS", "4096"))
 eng.load_clusters(replicate(uniform_cluster(nn), nc))
-eng.generate_jobs(GenParams(arrival_mode=1, lam=scaled_lambda(nn, load=load)), 16384)
+lam = float(os.environ.get("AB_LAM", "0")) or scaled_lambda(nn, load=load)
+eng.generate_jobs(GenParams(arrival_mode=1, lam=lam, max_dur_s=int(os.environ.get("AB_MAXDUR", "600"))), 16384)
 eng.run()
 ms = [eng.run().kernel_ms for _ in range(steps)]
 print(json.dumps({"ms": ms}))

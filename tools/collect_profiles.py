@@ -1,12 +1,17 @@
-"""Copy the rocprofv3 summaries of one tools/gpu_check.sh run into profiles/<tag>/ (tracked) and
-derive the per-launch HBM traffic of fifo_kernel for bench.py's roofline.traffic.
+"""Copy the rocprofv3 summaries of one tools/gpu.sh run into profiles/<tag>/ (tracked) and derive
+the per-launch HBM traffic of the measured kernel for bench.py's roofline.traffic.
+
+The kernel is matched by its exact rocprofv3 name: MCS_KERNEL if set, else the engine (mcs::) kernel with
+the most calls in the kernel-trace stats (the bench's production launches; bench.py's single untimed
+counting-build launch, e.g. `fifo_asm_kernel<16, true, 4, 8, true>`, is a different name and is
+never averaged in).
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reads exactly half the bytes of a wide
 coalesced streaming read on gfx950, so it is doubled (the job stream is read 16 B/lane);
-WRITE_SIZE (KB) is taken as is (calibration caveat: our result stores are 4 B/lane).  Counters
-come from separate --pmc passes, one launch (bench --steps 1 --warmup 0) each.
+WRITE_SIZE (KB) is taken as is.  Counters come from separate --pmc passes, one production launch
+(bench --steps 1 --warmup 0) each.
 
-usage: python tools/collect_profiles.py gpurun_out/<run> profiles/<tag>
+usage: python tools/collect_profiles.py gpurun_out/<run> profiles/<tag> [prof_<name>]
 """
 import csv
 import glob
@@ -16,38 +21,34 @@ import shutil
 import sys
 
 run, out = sys.argv[1], sys.argv[2]
+prof = sys.argv[3] if len(sys.argv) > 3 else None
 os.makedirs(out, exist_ok=True)
 
-
-KERNEL = os.environ.get("MCS_KERNEL", "fifo_kernel")  # delay_kernel for --policy delay runs
-
-
-def fifo_rows(path):
-    return [r for r in csv.DictReader(open(path)) if KERNEL in r.get("Kernel_Name", r.get("Name", ""))]
-
-
 summary = {}
-stats = glob.glob(f"{run}/prof/*kernel_stats.csv")
+stats = sorted(glob.glob(f"{run}/{prof or 'prof*'}/*kernel_stats.csv"))
+kernel = os.environ.get("MCS_KERNEL")
 if stats:
     shutil.copy(stats[0], f"{out}/kernel_stats.csv")
-    for r in csv.DictReader(open(stats[0])):
-        if KERNEL in r["Name"]:
-            summary["kernel"] = r["Name"]
-            summary["calls"] = int(r["Calls"])
-            summary["avg_ns"] = float(r["AverageNs"])
-            summary["min_ns"] = float(r["MinNs"])
-            summary["max_ns"] = float(r["MaxNs"])
+    rows = list(csv.DictReader(open(stats[0])))
+    if kernel is None:  # the production kernel: the engine's kernel with the most launches
+        kernel = max((r for r in rows if "mcs::" in r["Name"]), key=lambda r: int(r["Calls"]))["Name"]
+    for r in rows:
+        if r["Name"] == kernel:
+            summary.update(kernel=r["Name"], calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
+                           min_ns=float(r["MinNs"]), max_ns=float(r["MaxNs"]))
+if kernel is None:
+    sys.exit("no kernel_stats.csv in the run and no MCS_KERNEL: cannot tell which kernel to summarise")
 
 counters = {}
-launch_ns = []
+launches = 0
 for g in sorted(glob.glob(f"{run}/pmc*_g*/pmc_counter_collection.csv")):
-    rows = fifo_rows(g)
-    # a pass may hold more than one launch of the kernel (bench.py's untimed first launch):
-    # the counters are summed over each launch's rows and averaged over the launches
+    rows = [r for r in csv.DictReader(open(g)) if r.get("Kernel_Name", r.get("Name", "")) == kernel]
+    # a pass may hold more than one launch of the kernel: summed per launch, averaged over launches
     n_launch = max(len({r["Dispatch_Id"] for r in rows}), 1)
+    launches = max(launches, n_launch)
     for r in rows:
         counters[r["Counter_Name"]] = counters.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"]) / n_launch
-        launch_ns.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+summary["pmc_kernel"] = kernel
 summary["pmc_per_launch"] = counters
 
 bench = None
@@ -67,6 +68,7 @@ if bench and "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
         "gen": bench["config"].get("gen", "stream"),
         "lam": bench["config"].get("lam", 0.0),
         "max_dur": bench["config"].get("max_dur", 600),
+        "kernel": kernel,
         "hbm_bytes_per_launch": fetch + write,
         "fetch_bytes_corrected": fetch,
         "write_bytes": write,
