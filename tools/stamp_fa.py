@@ -1,5 +1,5 @@
 """Segment cycles of the hand-scheduled FIFO loop from an MCS_STAMPS probe build of
-mcs_fifo_asm.hip (tools/build_asmvariant.sh stamps csrc/mcs_fifo_asm.hip -DMCS_STAMPS): per placement,
+mcs_fifo_asm.hip (tools/variant.sh stamps csrc/mcs_fifo_asm.hip -DMCS_STAMPS): per placement,
 the cycles spent in release scans, failed fits, batch ends and the rest (decisions and arrival
 advances), at several cluster counts (waves per CU), with the counting build's pass / release counts.
 s_memtime stamps wait for their SMEM read, which also drains LDS: read the shares, not the time.

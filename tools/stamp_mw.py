@@ -1,5 +1,5 @@
 """Segment times of the workgroup-resident lock-step tick (mcs_trade_mw.hip) from an MCS_STAMPS probe
-build (tools/build_asmvariant.sh mw_stamps multi-cluster-simulator_amd/csrc/mcs_trade_mw.hip
+build (tools/variant.sh mw_stamps multi-cluster-simulator_amd/csrc/mcs_trade_mw.hip
 -DMCS_STAMPS): per tick, each wave's time in phase A's segments (prefetch, releases, arrivals,
 decisions, sample + record), the X1 exchange (wave 0 sweeps, the others wait), phase B, its barrier,
 X2 + C/D (wave 0) and the loop barrier, on the C5 system (64 clusters x 256 nodes, jobs per cluster

@@ -1,5 +1,5 @@
 """Segment times of the resident lock-step tick (mcs_trade_res.hip) from an MCS_STAMPS probe build
-(tools/build_asmvariant.sh res_stamps multi-cluster-simulator_amd/csrc/mcs_trade_res.hip -DMCS_STAMPS):
+(tools/variant.sh res_stamps multi-cluster-simulator_amd/csrc/mcs_trade_res.hip -DMCS_STAMPS):
 per tick, each wave's time in the phase-A segments (prefetch, releases, arrivals, decisions,
 sample + record), phase B, phase C+D and the three barrier waits, on the C5 system (64 clusters x
 256 nodes, jobs per cluster from argv).  s_memrealtime stamps wait for outstanding LDS reads: read

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Build libmcs.so with one source file replaced (e.g. a mcs_fifo_asm.hip variant, or the in-tree
 # mcs_trade_res.hip with -DMCS_STAMPS) into variants/libmcs_<name>.so, the other objects from the
-# last in-tree build.   usage: tools/build_asmvariant.sh <name> <file.hip> [hipcc flags]
+# last in-tree build.   usage: tools/variant.sh <name> <file.hip> [hipcc flags]
 set -eu
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 NAME="$1"; SRC="$2"; shift 2
