@@ -229,11 +229,12 @@ def main_c5_delay(args, world, rank, local_rank):
         eng.run()
     barrier()
     t0 = time.perf_counter()
-    kernel_ms, decided = [], 0
+    kernel_ms, decided, escalations = [], 0, 0
     for _ in range(args.steps):
         st = eng.run()
         kernel_ms.append(st.kernel_ms)
         decided += st.placed
+        escalations += st.escalations
     barrier()
     elapsed = time.perf_counter() - t0
     elapsed_max, decided_all = aggregate(elapsed, decided, device=dev)
@@ -292,13 +293,16 @@ def main_c5_delay(args, world, rank, local_rank):
             },
             "roofline": {
                 "bound": "hbm",
-                "limiter": "launch/latency: a tick is dependent launches of a few us (DESIGN.md §11)",
+                "limiter": ("latency: one workgroup runs every cluster's Delay iteration, then the trader rounds, "
+                            "per tick (DESIGN.md §11)" if ts["loop_form"] == 3 else
+                            "launch/latency: a tick is dependent launches of a few us (DESIGN.md §11)"),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": "lock-step tick (dt_step with the sample, dt_trader), launch/latency-bound",
+                "kernel": ("dt_res_kernel (resident tick, the whole system in one workgroup)" if ts["loop_form"] == 3
+                           else "lock-step tick (dt_step with the sample, dt_trader), launch/latency-bound"),
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "bytes_per_placement": BYTES_PER_PLACEMENT,
             },
@@ -306,7 +310,8 @@ def main_c5_delay(args, world, rank, local_rank):
             "trading": {"ticks": ts["ticks"], "t_final": ts["t_final"],
                         "us_per_tick": avg_kernel_s * 1e6 / max(ts["ticks"], 1), "trades": ts["trades"],
                         "trades_won": ts["trades_won"], "wait_time_rounds": int((tr["policy"] == 0).sum()),
-                        "foreign_jobs": int(len(eng.foreign())), "flags": ts["flags"], "loop_form": ts["loop_form"]},
+                        "foreign_jobs": int(len(eng.foreign())), "flags": ts["flags"], "loop_form": ts["loop_form"],
+                        "slot_pool": st.slot_pool, "escalations_in_timed_runs": escalations},
         }
         if dist_on:  # the RCCL communicator's size, as torch.distributed sees it
             out["world"] = world

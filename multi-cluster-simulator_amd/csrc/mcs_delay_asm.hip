@@ -18,15 +18,13 @@
 //     move (exact: the skipped iterations repeat the same failures).
 //
 // Level1 lives in the wave's LDS (r04), three SoA arrays of kL1Cap words: the request {cores |
-// mem << 16} (clamped like the Level0 records), the job's row and its duration.  The loop has two
-// modes with their own copies of the iteration code: mode 0 while Level1 is empty (the r03 loop,
-// no pass), mode 1 while it is not.  A pass reads the list 64 entries per row; one DPP-built fit
-// filter (lane i: the largest guarded free memory over nodes with min(free cores, 63) >= 63 - i,
-// the exact test for jobs of < 63 cores) and one ds_bpermute per row pick the entries that fit
-// some node, each of those gets the real first fit in list order, and the row is compacted in
-// place.  The filter is rebuilt after every Level1 placement (it also is the pass skip's
-// reference: lane i of v106 bounds the smallest guarded memory demand among the Level1 jobs of
-// that core key, so a pass with best < bound in every lane cannot place anything and is skipped).
+// mem << 16} (clamped like the Level0 records), the job's row (bit 31: not examined since the D6
+// skip) and its duration.  The loop has two modes with their own copies of the iteration code: mode
+// 0 while Level1 is empty (the r03 loop, no pass), mode 1 while it is not.  A pass runs only when a
+// node grew since the last one (a release) or a skipped job waits: every other Level1 job failed
+// every node then, and nodes only shrank since.  It reads the list 64 entries per row and tests each
+// row against the grown nodes alone (their current values, 3 VALU per node), gives each candidate
+// the real first fit in list order, and compacts the row in place.
 // The loop stops a cluster ("bail-out", kDelayBail; the engine re-runs it from t = 0 on the
 // compiled delay_kernel) only when Level1 outgrows its LDS slice or when the clock leaves the u32
 // range after a move.  A Level1 deadlock (nothing runs or arrives and Level1 fits no node) ends the
@@ -46,78 +44,122 @@ namespace {
 
 #include "mcs_fa_macros.h"
 
-// Level1 entries per wave in LDS (10 rows).  LDS words of a wave: the node copy [4][64], the fit
-// filter's histogram [64], then the Level1 arrays cm / jw / dur [kL1Cap] each: 8960 B, so 16 cluster
-// waves per CU (the C4 shape) take 140 KB of the CU's 160 KB.
+// Level1 entries per wave in LDS (10 rows).  LDS words of a wave: the node copy [4][64], then the
+// Level1 arrays cm / jw / dur [kL1Cap] each: 8704 B, so 16 cluster waves per CU (the C4 shape) take
+// 136 KB of the CU's 160 KB.
 constexpr uint32_t kL1Cap = 640;
-constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
+constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
 
+// Which Level1 jobs can fit (r04).  Every job a pass leaves in Level1 failed ScheduleJob against
+// every node, and a job moved in by the Level0 head failed against every node at its move; between
+// passes nodes only shrink, except at releases.  So at the next pass a job can fit only a node that
+// grew since the last pass ("G": some free field above the snapshot v105/v106/v116/v112 taken at
+// the end of the last pass and lowered, field by field, to the nodes' values at every Level1 move,
+// since the moved job was tested against those; tools/delay_g_model.py checks the rule against the
+// oracle), and the exact test of a row is "fits some node of G" with G's current
+// values — 3 VALU per row and per G node, no filter to build.  A job the pass skips (D6) was not
+// tested: it carries bit 31 of its job-row word ("untested", s96 >> 1 of them) and is a candidate at
+// the next pass whatever G holds.  More than 64 grown nodes: every job of the pass is a candidate.
+// Each candidate gets the real first fit (FIT16) in list order; after a commit, node kx's new value
+// replaces its G entry and the rest of the row is re-tested.
+//
 // Register map beyond mcs_fa_macros.h's (DELAY loop only):
-//   s43 changed (this iteration placed or moved a job)   s[58:59] candidates of the row
-//   s82 candidate lane   s74/s75/s76 temps   s[88:89] live (then kept) lanes of the row
-//   s[90:91] removed lanes of the row   s92 Level1 length   s93 write cursor   s94 row base
-//   s95 the D6-skipped position   s96 filter dirty   s97 moved   s98 placed from Level1
-//   s99 Level1 peak   s[100:101] sum over Level1 placements of t minus the moved jobs' arrivals
-//   v56 cm  v57 job row  v58 duration  v59 4 * core key  v60 filter at the key  v61 guarded memory
-//   v62 temp  v63 row address  v88 Level1 lane address (row 0)  v102/v103 per-lane 64-bit sum of
-//   (start - arrival) of the stored Level0 batches  v104 temp  v105 filter  v106 pass-skip bound
-//   v112 histogram lane address  v113 histogram base + 4 * 0x803f  v114/v115/v123 temps
-//   v116 D6 fold  v118 0x8000  v122 0x803f   s56 MaxWaitTime
+//   s43 changed (this iteration placed or moved a job)   s46 (in a pass) |G|, 0xffff = every job
+//   s[58:59] candidates of the row   s82 candidate lane / G cursor   s74/s75/s76 temps
+//   s[88:89] live (then kept) lanes of the row   s[90:91] removed lanes of the row
+//   s92 Level1 length   s93 write cursor   s94 row base   s95 the D6-skipped position
+//   s96 bit 0: a release since the last pass; bits 1-31: untested Level1 jobs
+//   s97 moved   s98 placed from Level1   s99 Level1 peak
+//   s[100:101] sum over Level1 placements of t minus the moved jobs' arrivals
+//   v56 cm  v57 job row (bit 31: untested)  v58 duration  v60-v62 temps  v63 row address
+//   v88 Level1 lane address (row 0)  v102/v103 per-lane 64-bit sum of (start - arrival) of the
+//   stored Level0 batches  v104 temp  v105/v106/v116/v112 the node snapshot (chunks 0-3)
+//   v113 G's node values  v118 G's node indices (kx)  v123 temp   s56 MaxWaitTime
 //
 // probe counters of the counting build (MCS_FIFO_DIAG=1; printed by the engine with
-// MCS_DELAY_PROBE=1): lane k of v119 counts event k (0 passes run, 1 passes skipped by the bound,
-// 2 rows, 3 candidates, 4 candidates whose first fit failed, 5 filter builds, 6 D6 skips,
-// 7 compactions, 8 mode-1 iterations)
+// MCS_DELAY_PROBE=1): lane k of v119 counts event k (0 passes run, 1 passes skipped (nothing grew,
+// nothing untested), 2 rows, 3 candidates, 4 candidates whose first fit failed, 5 G nodes, 6 D6
+// skips, 7 compactions, 8 mode-1 iterations)
 #define MCS_FD_P_D0(k) ""
 #define MCS_FD_P_D1(k) "s_mov_b64 exec, 1<<" #k "\n\tv_add_u32 v119, 1, v119\n\ts_mov_b64 exec, -1\n\t"
+#define MCS_FD_PG_D0 ""
+#define MCS_FD_PG_D1 "s_mov_b64 exec, 1<<5\n\tv_add_u32 v119, s46, v119\n\ts_mov_b64 exec, -1\n\t"
 // (a skipped pass: straight to the Level0 head, or through its counter)
 #define MCS_FD_PSK_D0 "mcsfd_head1_%="
 #define MCS_FD_PSK_D1 "mcsfd_pskip_%="
 #define MCS_FD_PSKB_D0 ""
 #define MCS_FD_PSKB_D1 "s_branch mcsfd_head1_%=\nmcsfd_pskip_%=:\n\t" MCS_FD_P_D1(1)
 
-// the fit filter (scheduler.go:305, ScheduleJob's outcome without its node): lane i of v105 =
-// max guarded free memory (2^15 + free_m; padding nodes hold 0x7fff, below every request) over the
-// nodes with min(free cores, 63) >= 63 - i.  An LDS ds_max_u32 histogram over the reversed core keys
-// (key address = base - 4 * clamp(2^15 + free_c, 0x8000, 0x803f)), then a DPP inclusive prefix max.
-#define MCS_FD_BUILD(D)                                                                           \
-    MCS_FD_P_##D(5) "v_mov_b32 v114, 0\n\t"                                                                       \
-    "ds_write_b32 v112, v114\n\t"                                                                 \
-    "v_bfe_u32 v72, v64, 0, 16\n\t"                                                               \
-    "v_bfe_u32 v73, v65, 0, 16\n\t"                                                               \
-    "v_bfe_u32 v74, v66, 0, 16\n\t"                                                               \
-    "v_bfe_u32 v75, v67, 0, 16\n\t"                                                               \
-    "v_med3_u32 v72, v72, v118, v122\n\t"                                                         \
-    "v_med3_u32 v73, v73, v118, v122\n\t"                                                         \
-    "v_med3_u32 v74, v74, v118, v122\n\t"                                                         \
-    "v_med3_u32 v75, v75, v118, v122\n\t"                                                         \
-    "v_mad_i32_i24 v72, v72, -4, v113\n\t"                                                        \
-    "v_mad_i32_i24 v73, v73, -4, v113\n\t"                                                        \
-    "v_mad_i32_i24 v74, v74, -4, v113\n\t"                                                        \
-    "v_mad_i32_i24 v75, v75, -4, v113\n\t"                                                        \
-    "v_lshrrev_b32 v76, 16, v64\n\t"                                                              \
-    "v_lshrrev_b32 v77, 16, v65\n\t"                                                              \
-    "v_lshrrev_b32 v78, 16, v66\n\t"                                                              \
-    "v_lshrrev_b32 v79, 16, v67\n\t"                                                              \
-    "ds_max_u32 v72, v76\n\t"                                                                     \
-    "ds_max_u32 v73, v77\n\t"                                                                     \
-    "ds_max_u32 v74, v78\n\t"                                                                     \
-    "ds_max_u32 v75, v79\n\t"                                                                     \
-    "ds_read_b32 v105, v112\n\t" /* (one wave's LDS operations complete in order) */             \
-    "s_mov_b32 s96, 0\n\t"                                                                        \
-    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
-    "s_nop 1\n\t"                                                                                 \
-    "v_max_u32_dpp v105, v105, v105 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_max_u32_dpp v105, v105, v105 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_max_u32_dpp v105, v105, v105 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_max_u32_dpp v105, v105, v105 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"                     \
-    "s_nop 1\n\t"                                                                                 \
-    "v_max_u32_dpp v105, v105, v105 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"                  \
-    "s_nop 1\n\t"                                                                                 \
-    "v_max_u32_dpp v105, v105, v105 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+// the grown nodes of chunk C (lane mask MASK, node registers V) into the G list (v113 values, v118
+// kx) at cursor s82
+#define MCS_FD_ENUM(C, MASK, V)                                                                   \
+    "mcsfd_g" #C "_%=:\n\t"                                                                       \
+    "s_ff1_i32_b64 s76, " MASK "\n\t"                                                             \
+    "s_cmp_lt_i32 s76, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_g" #C "e_%=\n\t"                                                        \
+    "v_readlane_b32 s87, " V ", s76\n\t"                                                          \
+    "s_bitset0_b64 " MASK ", s76\n\t"                                                             \
+    "s_mov_b32 m0, s82\n\t"                                                                       \
+    "s_add_u32 s86, s76, " #C "*64\n\t"                                                           \
+    "v_writelane_b32 v113, s87, m0\n\t"                                                           \
+    "v_writelane_b32 v118, s86, m0\n\t"                                                           \
+    "s_add_u32 s82, s82, 1\n\t"                                                                   \
+    "s_branch mcsfd_g" #C "_%=\n"                                                                 \
+    "mcsfd_g" #C "e_%=:\n\t"
+
+// G: nodes with a free field above the snapshot; |G| into s46 (0xffff past 64: every job)
+#define MCS_FD_GROWN                                                                              \
+    "v_pk_max_u16 v60, v64, v105\n\t"                                                             \
+    "v_pk_max_u16 v61, v65, v106\n\t"                                                             \
+    "v_pk_max_u16 v62, v66, v116\n\t"                                                             \
+    "v_pk_max_u16 v123, v67, v112\n\t"                                                            \
+    "v_cmp_ne_u32_e64 s[58:59], v60, v105\n\t"                                                    \
+    "v_cmp_ne_u32_e64 s[88:89], v61, v106\n\t"                                                    \
+    "v_cmp_ne_u32_e64 s[90:91], v62, v116\n\t"                                                    \
+    "v_cmp_ne_u32_e64 s[74:75], v123, v112\n\t"                                                   \
+    "s_bcnt1_i32_b64 s46, s[58:59]\n\t"                                                           \
+    "s_bcnt1_i32_b64 s76, s[88:89]\n\t"                                                           \
+    "s_add_u32 s46, s46, s76\n\t"                                                                 \
+    "s_bcnt1_i32_b64 s76, s[90:91]\n\t"                                                           \
+    "s_add_u32 s46, s46, s76\n\t"                                                                 \
+    "s_bcnt1_i32_b64 s76, s[74:75]\n\t"                                                           \
+    "s_add_u32 s46, s46, s76\n\t"                                                                 \
+    "s_cmp_gt_u32 s46, 64\n\t"                                                                    \
+    "s_cbranch_scc0 mcsfd_gl_%=\n\t"                                                              \
+    "s_mov_b32 s46, 0xffff\n\t"                                                                   \
+    "s_branch mcsfd_gdone_%=\n"                                                                   \
+    "mcsfd_gl_%=:\n\t"                                                                            \
+    "s_mov_b32 s82, 0\n\t" MCS_FD_ENUM(0, "s[58:59]", "v64") MCS_FD_ENUM(1, "s[88:89]", "v65")    \
+    MCS_FD_ENUM(2, "s[90:91]", "v66") MCS_FD_ENUM(3, "s[74:75]", "v67")                           \
+    "mcsfd_gdone_%=:\n\t"
+
+// the row's jobs that fit some node of G (current values) or are untested, into ACC (an SGPR
+// pair, zeroed here); IX is the G cursor (clobbered), s74 a temp; T names the labels
+#define MCS_FD_GTEST(ACC, T, IX)                                                                  \
+    "s_mov_b64 " ACC ", 0\n\t"                                                                    \
+    "s_cmp_eq_u32 s46, 0xffff\n\t"                                                                \
+    "s_cbranch_scc1 mcsfd_" T "all_%=\n\t"                                                        \
+    "s_mov_b32 " IX ", 0\n\t"                                                                     \
+    "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_" T "u_%=\n"                                                            \
+    "mcsfd_" T "_%=:\n\t"                                                                         \
+    "v_readlane_b32 s74, v113, " IX "\n\t"                                                        \
+    "s_add_u32 " IX ", " IX ", 1\n\t"                                                             \
+    "v_pk_sub_u16 v60, s74, v56\n\t" /* guard bits survive in both halves iff the job fits */    \
+    "v_and_b32 v60, 0x80008000, v60\n\t"                                                          \
+    "v_cmp_eq_u32_e32 vcc, 0x80008000, v60\n\t"                                                   \
+    "s_or_b64 " ACC ", " ACC ", vcc\n\t"                                                          \
+    "s_cmp_lt_u32 " IX ", s46\n\t"                                                                \
+    "s_cbranch_scc1 mcsfd_" T "_%=\n"                                                             \
+    "mcsfd_" T "u_%=:\n\t"                                                                        \
+    "s_cmp_lt_u32 s96, 2\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfd_" T "e_%=\n\t"                                                          \
+    "v_cmp_le_u32_e32 vcc, 0x80000000, v57\n\t" /* untested */                                  \
+    "s_or_b64 " ACC ", " ACC ", vcc\n\t"                                                          \
+    "s_branch mcsfd_" T "e_%=\n"                                                                  \
+    "mcsfd_" T "all_%=:\n\t"                                                                      \
+    "s_mov_b64 " ACC ", -1\n"                                                                     \
+    "mcsfd_" T "e_%=:\n\t"
 
 // a Level0 batch's results (the lanes placed on Level0; moved jobs are written when Level1 places
 // them) and their waits; v91 = -1 marks a lane without a Level0 placement
@@ -173,17 +215,24 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_branch mcsfd_placed" #M "_%=\n"
 
 // the Level1 pass (scheduler.go:302-329), mode 1 only; falls through to the Level0 head
-#define MCS_FD_PASS(D)                                                                               \
+#define MCS_FD_PASS(D)                                                                            \
     "s_mov_b32 s43, 0\n\t"                                                                        \
+    "s_cmp_eq_u32 s96, 0\n\t" /* nothing grew, nothing untested: every job fails again */         \
+    "s_cbranch_scc1 " MCS_FD_PSK_##D "\n\t"                                                       \
+    "s_mov_b32 s46, 0\n\t"                                                                        \
+    "s_bitcmp0_b32 s96, 0\n\t"                                                                    \
+    "s_cbranch_scc1 mcsfd_rows_%=\n\t"                                                            \
+    "s_and_b32 s96, s96, -2\n\t" MCS_FD_GROWN                                                     \
+    "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
+    "s_cbranch_scc0 mcsfd_rows_%=\n\t"                                                            \
     "s_cmp_eq_u32 s96, 0\n\t"                                                                     \
-    "s_cbranch_scc1 mcsfd_chk_%=\n\t" MCS_FD_BUILD(D)                                             \
-    "mcsfd_chk_%=:\n\t"                                                                           \
-    "v_cmp_ge_u32_e32 vcc, v105, v106\n\t" /* a lane whose jobs may fit */                      \
-    "s_cbranch_vccz " MCS_FD_PSK_##D "\n\t" MCS_FD_P_##D(0)                                       \
+    "s_cbranch_scc0 mcsfd_rows_%=\n\t"                                                            \
+    "v_readlane_b32 s46, v95, s47\n\t" /* nothing grew after all: the head's duration back */   \
+    "s_branch " MCS_FD_PSK_##D "\n"                                                              \
+    "mcsfd_rows_%=:\n\t" MCS_FD_P_##D(0) MCS_FD_PG_##D                                            \
     "s_mov_b32 s93, 0\n\t"                                                                        \
     "s_mov_b32 s94, 0\n\t"                                                                        \
-    "s_mov_b32 s95, -1\n\t"                                                                       \
-    "v_mov_b32 v116, -1\n"                                                                        \
+    "s_mov_b32 s95, -1\n"                                                                         \
     "mcsfd_row_%=:\n\t" MCS_FD_P_##D(2)                                                           \
     "s_lshl_b32 s74, s94, 2\n\t"                                                                  \
     "v_add_u32 v63, s74, v88\n\t"                                                                 \
@@ -193,16 +242,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_sub_u32 s74, s92, s94\n\t"                                                                 \
     "v_cmp_gt_u32_e64 s[88:89], s74, v110\n\t" /* live: the row's entries */                    \
     "s_mov_b64 s[90:91], 0\n\t"                                                                   \
-    "s_waitcnt lgkmcnt(2)\n\t"                                                                    \
-    "v_and_b32 v59, 0xffff, v56\n\t"                                                              \
-    "v_lshrrev_b32 v61, 16, v56\n\t"                                                              \
-    "v_min_u32 v59, 63, v59\n\t"                                                                  \
-    "v_add_u32 v61, 0x8000, v61\n\t" /* guarded memory demand */                                \
-    "v_lshlrev_b32 v59, 2, v59\n\t"                                                               \
-    "v_sub_u32 v59, 0xfc, v59\n\t" /* 4 * (63 - min(cores, 63)): the filter lane */             \
-    "ds_bpermute_b32 v60, v59, v105\n\t"                                                          \
-    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
-    "v_cmp_ge_u32_e64 s[58:59], v60, v61\n\t"                                                     \
+    "s_waitcnt lgkmcnt(0)\n\t" MCS_FD_GTEST("s[58:59]", "rt", "s82")                                     \
     "s_and_b64 s[58:59], s[58:59], s[88:89]\n"                                                    \
     /* the candidates in list order */                                                            \
     "mcsfd_cand_%=:\n\t"                                                                          \
@@ -210,25 +250,39 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_cmp_lt_i32 s82, 0\n\t"                                                                     \
     "s_cbranch_scc1 mcsfd_rowend_%=\n\t"                                                          \
     "v_readlane_b32 s48, v56, s82\n\t"                                                            \
+    "v_readlane_b32 s75, v57, s82\n\t"                                                            \
     "s_bitset0_b64 s[58:59], s82\n\t"                                                             \
     "s_add_u32 s74, s94, s82\n\t"                                                                 \
     "s_cmp_eq_u32 s74, s95\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfd_d6_%=\n\t" MCS_FD_P_##D(3) MCS_FA_FIT16 MCS_FA_ANYFIT                    \
-    "v_readlane_b32 s46, v58, s82\n\t"                                                            \
-    "v_readlane_b32 s75, v57, s82\n\t"                                                            \
-    "s_cbranch_vccz mcsfd_nofitc_%=\n\t" /* (key 0, 63 or more cores: the filter is conservative) */ \
+    "s_cbranch_scc1 mcsfd_d6_%=\n\t" MCS_FD_P_##D(3) MCS_FA_FIT16 MCS_FA_ANYFIT                   \
+    "v_readlane_b32 s55, v58, s82\n\t"                                                            \
+    "s_bitcmp1_b32 s75, 31\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfd_untested_%=\n"                                                          \
+    "mcsfd_tested_%=:\n\t"                                                                        \
+    "s_cbranch_vccz mcsfd_nofitc_%=\n\t" /* (an untested job that still fits no node) */         \
     "s_ff1_i32_b64 s50, vcc\n\t"                                                                  \
-    "s_add_u32 s55, s40, s46\n\t"                                                                 \
-    "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
+    "s_add_u32 s55, s55, s40\n\t" /* finish */                                                   \
+    "s_cmp_eq_u32 s55, s40\n\t"                                                                   \
     "s_cbranch_scc1 mcsfd_l1zero_%=\n\t" MCS_FA_DECIDE16R                                         \
     "s_min_u32 s77, s77, s55\n\t"                                                                 \
     "s_mov_b64 exec, -1\n\t"                                                                      \
+    "s_set_gpr_idx_on s53, gpr_idx(SRC0)\n\t"                                                     \
+    "v_mov_b32 v123, v64\n\t" /* the committed chunk's new values */                             \
+    "s_set_gpr_idx_off\n\t"                                                                       \
     "s_add_u32 s80, s80, 1\n\t"                                                                   \
-    "s_mov_b32 s96, 1\n"                                                                          \
+    "s_cmp_eq_u32 s46, 0xffff\n\t"                                                                \
+    "v_readlane_b32 s74, v123, s50\n\t" /* node kx's new value */                                \
+    "s_cbranch_scc1 mcsfd_l1res_%=\n\t"                                                           \
+    "v_cmp_eq_u32_e32 vcc, s54, v118\n\t" /* its G entry (if any) follows it */                \
+    "v_mov_b32 v60, s74\n\t"                                                                      \
+    "v_cndmask_b32 v113, v113, v60, vcc\n\t" MCS_FD_GTEST("s[60:61]", "rr", "s76")                       \
+    "s_and_b64 s[58:59], s[58:59], s[60:61]\n"                                                    \
     "mcsfd_l1res_%=:\n\t" /* the job's row: node, start, finish (kx in s54) */                  \
     "s_and_b32 s74, s54, 63\n\t"                                                                  \
     "s_lshr_b32 s76, s54, 6\n\t"                                                                  \
     "s_lshl2_add_u32 s74, s74, s76\n\t" /* node = lane * 4 + chunk */                            \
+    "s_sub_u32 s76, s42, 1\n\t" /* (a row inside the cluster, whatever the list holds) */       \
+    "s_min_u32 s75, s75, s76\n\t"                                                                 \
     "s_lshl_b32 s75, s75, 2\n\t"                                                                  \
     "s_mov_b64 exec, 1\n\t"                                                                       \
     "v_mov_b32 v125, s75\n\t"                                                                     \
@@ -243,32 +297,35 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_add_u32 s95, s94, s82\n\t"                                                                 \
     "s_add_u32 s95, s95, 1\n\t" /* the entry sliding into this slot is not examined (D6) */     \
     "s_add_u32 s98, s98, 1\n\t"                                                                   \
+    "s_cmp_gt_u32 s98, s42\n\t" /* more Level1 placements than jobs: a runaway, re-run */       \
+    "s_cbranch_scc1 mcsfd_poolovf_%=\n\t"                                                         \
     "s_add_u32 s100, s100, s40\n\t"                                                               \
     "s_addc_u32 s101, s101, 0\n\t"                                                                \
     "s_mov_b32 s43, 1\n\t"                                                                        \
-    "s_cmp_eq_u32 s96, 0\n\t" /* a zero-duration job changed no node */                          \
-    "s_cbranch_scc1 mcsfd_cand_%=\n\t" MCS_FD_BUILD(D)                                            \
-    /* the commit shrank a node: the rest of the row is re-tested on the rebuilt filter */        \
-    "ds_bpermute_b32 v60, v59, v105\n\t"                                                          \
-    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
-    "v_cmp_ge_u32_e32 vcc, v60, v61\n\t"                                                          \
-    "s_and_b64 s[58:59], s[58:59], vcc\n\t"                                                       \
     "s_branch mcsfd_cand_%=\n"                                                                    \
+    /* an untested job is tested now: the mark goes (in LDS too, the row may stay in place) */   \
+    "mcsfd_untested_%=:\n\t"                                                                      \
+    "s_sub_u32 s96, s96, 2\n\t"                                                                   \
+    "s_bitset0_b32 s75, 31\n\t"                                                                   \
+    "s_lshl_b64 exec, 1, s82\n\t"                                                                 \
+    "v_and_b32 v57, 0x7fffffff, v57\n\t"                                                          \
+    "ds_write_b32 v63, v57 offset:%[cap4]\n\t"                                                    \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "s_branch mcsfd_tested_%=\n"                                                                  \
     "mcsfd_nofitc_%=:\n\t" MCS_FD_P_##D(4)                                                        \
     "s_branch mcsfd_cand_%=\n"                                                                    \
     "mcsfd_l1zero_%=:\n\t"                                                                        \
     "v_readlane_b32 s51, v86, s50\n\t"                                                            \
     "s_ff1_i32_b32 s52, s51\n\t"                                                                  \
     "s_lshl3_add_u32 s54, s52, s50\n\t"                                                           \
-    "s_mov_b32 s55, s40\n\t"                                                                      \
     "s_branch mcsfd_l1res_%=\n"                                                                   \
-    /* D6-skipped: folded into the pass-skip bound as it is (it was not tested) */               \
+    /* D6-skipped: not examined this pass; untested until the next one */                        \
     "mcsfd_d6_%=:\n\t" MCS_FD_P_##D(6)                                                            \
-    "v_readlane_b32 s74, v59, s82\n\t"                                                            \
-    "v_readlane_b32 s76, v61, s82\n\t"                                                            \
-    "s_lshr_b32 s74, s74, 2\n\t"                                                                  \
-    "s_lshl_b64 exec, 1, s74\n\t"                                                                 \
-    "v_min_u32 v116, s76, v116\n\t"                                                               \
+    "s_bitcmp1_b32 s75, 31\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfd_cand_%=\n\t"                                                            \
+    "s_add_u32 s96, s96, 2\n\t"                                                                   \
+    "s_lshl_b64 exec, 1, s82\n\t"                                                                 \
+    "v_or_b32 v57, 0x80000000, v57\n\t" /* (the row is compacted: the mark reaches LDS) */      \
     "s_mov_b64 exec, -1\n\t"                                                                      \
     "s_branch mcsfd_cand_%=\n"                                                                    \
     /* compaction in the same sweep: the kept entries move down to the write cursor */           \
@@ -297,16 +354,14 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_add_u32 s94, s94, 64\n\t"                                                                  \
     "s_cmp_lt_u32 s94, s92\n\t"                                                                   \
     "s_cbranch_scc1 mcsfd_row_%=\n\t"                                                             \
-    /* the pass is over: every job left (keys 1-63) failed a filter no smaller than the final  */ \
-    /* one, except the D6-skipped ones */                                                         \
+    /* the pass is over: every job left fails every node (the untested aside) */                 \
     "s_mov_b32 s92, s93\n\t"                                                                      \
     "v_readlane_b32 s46, v95, s47\n\t" /* the Level0 head's record again */                     \
     "v_readlane_b32 s48, v96, s47\n\t"                                                            \
-    "v_add_u32 v62, 1, v105\n\t"                                                                  \
-    "s_mov_b64 exec, -2\n\t"                                                                      \
-    "v_max_u32 v106, v106, v62\n\t"                                                               \
-    "s_mov_b64 exec, -1\n\t"                                                                      \
-    "v_min_u32 v106, v106, v116\n\t" MCS_FD_PSKB_##D
+    "v_mov_b32 v105, v64\n\t" /* the snapshot G is measured from at the next pass */             \
+    "v_mov_b32 v106, v65\n\t"                                                                     \
+    "v_mov_b32 v116, v66\n\t"                                                                     \
+    "v_mov_b32 v112, v67\n\t" MCS_FD_PSKB_##D
 
 #define MCS_FD_LOOP(D)                                                                            \
     /* ---- entry: state into the fixed registers ---- */                                        \
@@ -323,7 +378,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_mov_b32 s83, 0\n\t"                                                                        \
     "s_mov_b32 s84, 0\n\t"                                                                        \
     "s_mov_b32 s92, 0\n\t"                                                                        \
-    "s_mov_b32 s96, 1\n\t"                                                                        \
+    "s_mov_b32 s96, 0\n\t"                                                                        \
     "s_mov_b32 s97, 0\n\t"                                                                        \
     "s_mov_b32 s98, 0\n\t"                                                                        \
     "s_mov_b32 s99, 0\n\t"                                                                        \
@@ -345,14 +400,9 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "v_mov_b32 v102, 0\n\t"                                                                       \
     "v_mov_b32 v103, 0\n\t"                                                                       \
     "v_mov_b32 v91, -1\n\t"                                                                       \
-    "v_mov_b32 v106, -1\n\t" /* no Level1 job of any key */                                      \
     "v_mov_b32 v119, 0\n\t"                                                                       \
-    "v_mov_b32 v118, 0x8000\n\t"                                                                  \
-    "v_mov_b32 v122, 0x803f\n\t"                                                                  \
-    "v_add_u32 v112, 0x400, v108\n\t" /* the histogram (after the node copy) */                  \
-    "v_add_u32 v88, 0x500, v108\n\t"  /* Level1 (after the histogram) */                         \
-    "v_mov_b32 v113, s73\n\t"                                                                     \
-    "v_add_u32 v113, 0x204fc, v113\n\t" MCS_FA_INIT16R MCS_FA_RELOAD16 "s_waitcnt lgkmcnt(0)\n\t" \
+    "v_add_u32 v88, 0x400, v108\n\t" /* Level1 (after the node copy) */                          \
+    MCS_FA_INIT16R MCS_FA_RELOAD16 "s_waitcnt lgkmcnt(0)\n\t"                                      \
     /* prefetch batch 1 */                                                                        \
     "v_lshlrev_b32 v121, 4, v110\n\t"                                                             \
     "v_add_u32 v121, 0x400, v121\n\t"                                                             \
@@ -369,7 +419,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_max_u32 s81, s81, s80\n\t" /* peak: used only grows between releases */                   \
     "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN16R                                                    \
     "v_mov_b32 v120, v90\n\t"                                                                     \
-    "s_mov_b32 s96, 1\n\t"                                                                        \
+    "s_or_b32 s96, s96, 1\n\t" /* a release grew nodes: G at the next pass */                   \
     "s_nop 0\n\t"                                                                                 \
     "v_min_u32_dpp v120, v120, v120 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"                     \
     "s_nop 1\n\t"                                                                                 \
@@ -411,15 +461,19 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_cbranch_scc1 mcsfd_clkovf_%=\n\t"                                                          \
     "s_max_u32 s40, s40, s76\n\t"                                                                 \
     "s_branch mcsfd_adv0_%=\n"                                                                    \
-    "mcsfd_move0_%=:\n\t" /* into mode 1: the filter was not kept in mode 0 */                   \
-    "s_mov_b32 s96, 1\n\t"                                                                        \
+    "mcsfd_move0_%=:\n\t" /* into mode 1: the job fails every node as they are now */           \
+    "s_mov_b32 s96, 0\n\t"                                                                        \
+    "v_mov_b32 v105, v64\n\t"                                                                     \
+    "v_mov_b32 v106, v65\n\t"                                                                     \
+    "v_mov_b32 v116, v66\n\t"                                                                     \
+    "v_mov_b32 v112, v67\n\t"                                                                     \
     "s_branch mcsfd_move1_%=\n"                                                                   \
                                                                                                   \
     /* ======== mode 1: Level1 holds jobs ======== */                                            \
     "mcsfd_inner1_%=:\n\t"                                                                        \
     "s_cmp_eq_u32 s92, 0\n\t"                                                                     \
     "s_cbranch_scc1 mcsfd_inner0_%=\n\t" MCS_FA_CNTS_##D MCS_FD_P_##D(8) MCS_FD_PASS(D)            \
-    "mcsfd_head1_%=:\n\t" MCS_FD_HEAD(1, "s_mov_b32 s96, 1\n\t")                                  \
+    "mcsfd_head1_%=:\n\t" MCS_FD_HEAD(1, "")                                                      \
     "s_branch mcsfd_rel_%=\n" MCS_FD_ZERO(1)                                                      \
     "mcsfd_idle1_%=:\n\t"                                                                         \
     "s_cmp_eq_u32 s92, 0\n\t"                                                                     \
@@ -473,6 +527,10 @@ constexpr uint32_t kLdsWords = 4 * kWave + kWave + 3 * kL1Cap;
     "s_lshl_b64 exec, 1, s74\n\t"                                                                 \
     "v_min_u32 v106, s76, v106\n\t" /* the pass-skip bound of its key */                        \
     "s_mov_b64 exec, -1\n\t"                                                                      \
+    "v_pk_min_u16 v105, v105, v64\n\t" /* it failed every node as they are now: the snapshot */ \
+    "v_pk_min_u16 v106, v106, v65\n\t" /* G is measured from may not exceed them */            \
+    "v_pk_min_u16 v116, v116, v66\n\t"                                                            \
+    "v_pk_min_u16 v112, v112, v67\n\t"                                                            \
     "s_add_u32 s92, s92, 1\n\t"                                                                   \
     "s_max_u32 s99, s99, s92\n\t"                                                                 \
     "s_add_u32 s97, s97, 1\n\t"                                                                   \
@@ -567,7 +625,7 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
     const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
     const uint32_t lane = threadIdx.x;
 
-    // the node copy [4][64] (releases), the filter histogram [64], Level1 cm / jw / dur
+    // the node copy [4][64] (releases), Level1 cm / jw / dur
     __shared__ uint32_t lds[kLdsWords];
     constexpr uint32_t kGuard = 0x8000u, kClamp = kGuard - 1u;
     const uint32_t n0 = a.node_off[ci];
@@ -626,9 +684,8 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
 #undef MCS_FD_OPERANDS
 #pragma clang diagnostic pop
 
-    // the Level1 layout above: histogram at +1 KB, Level1 at +1.25 KB (v112 / v88 in the loop)
-    static_assert(4 * kWave * 4 == 0x400 && 5 * kWave * 4 == 0x500, "LDS layout");
-    static_assert(0x400 + 4 * 0x803f == 0x204fc, "filter key base");
+    // the Level1 layout above: Level1 at +1 KB (v88 in the loop)
+    static_assert(4 * kWave * 4 == 0x400, "LDS layout: Level1 after the node copy (v88)");
 
     // the counting build's probe counters: into the cluster's (otherwise unused) HBM Level1 scratch
     if (DIAG && lane < 9u && 2u * J > lane) reinterpret_cast<uint32_t*>(a.l1_cm + j0)[lane] = prb;
@@ -660,7 +717,7 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
             o_finish[i] = of;
         }
         for (uint32_t i = lane; i < left; i += kWave) {  // never placed (scheduler.go:302-329 spins)
-            const uint32_t jw = lds[5 * kWave + kL1Cap + i];
+            const uint32_t jw = lds[4 * kWave + kL1Cap + i] & 0x7FFFFFFFu;  // (bit 31: untested)
             o_node[jw] = MCS_NODE_UNPLACED;
             o_start[jw] = MCS_TIME_NONE;
             o_finish[jw] = MCS_TIME_NONE;

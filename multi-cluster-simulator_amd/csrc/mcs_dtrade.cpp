@@ -144,10 +144,42 @@ int dt_poll(mcs_engine* e) {
     return MCS_OK;
 }
 
+// MCS_DTRADE_RESIDENT=0 keeps the graph-replayed kernels; MCS_TRADE_RES_TICKS caps the ticks of one
+// resident launch (tests cross launch boundaries with it)
+bool dt_resident(mcs_engine* e, size_t* lds) {
+    const char* env = getenv("MCS_DTRADE_RESIDENT");
+    if (env && atoi(env) == 0) return false;
+    if (!dtrade_res_shape(e->dtd->a, e->world, lds)) return false;
+    int max_lds = 0;
+    if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device) != hipSuccess)
+        return false;
+    return *lds <= (size_t)max_lds;
+}
+
 int dt_run_once(mcs_engine* e, double* kernel_ms) {
     DtradeDev* d = e->dtd;
     hipError_t st = launch_dtrade_init(d->a, e->stream);
     if (st != hipSuccess) return dt_hip_fail(e, "DELAY trading init", st);
+    size_t lds = 0;
+    if (dt_resident(e, &lds)) {
+        const char* tenv = getenv("MCS_TRADE_RES_TICKS");
+        const long tv = tenv ? atol(tenv) : 0;
+        const uint32_t budget = tv > 0 && tv < (1l << 16) ? (uint32_t)tv : (1u << 16);
+        d->loop_form = kLoopResident;
+        HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+        for (;;) {
+            st = launch_dtrade_res(d->a, budget, lds, e->stream);
+            if (st != hipSuccess) return dt_hip_fail(e, "resident DELAY trading tick", st);
+            if (int s = dt_poll(e)) return s;
+            if (d->h_ctl->done) break;
+        }
+        HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        float ms = 0.0f;
+        HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+        *kernel_ms = ms;
+        return MCS_OK;
+    }
     if (!d->graph) {
         hipGraph_t g = nullptr;
         HIPCHK(e, hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
@@ -231,13 +263,14 @@ int dt_run_rccl(mcs_engine* e, double* kernel_ms) {
 // the whole system, and the cluster count per rank must match
 int dt_agree_shape(mcs_engine* e) {
     uint32_t* buf = nullptr;
-    HIPCHK(e, hipMalloc(&buf, 3 * sizeof(uint32_t)));
+    HIPCHK(e, hipMalloc(&buf, 5 * sizeof(uint32_t)));
     /* max of C and of ~C (= ~min C): every rank sees the same verdict, so a mismatch fails on
      * every rank instead of leaving the ranks with the largest C in the tick loop */
-    const uint32_t h[3] = {e->max_n, e->C, ~e->C};
-    uint32_t mx[3] = {0, 0, 0};
+    // (and the largest learned capacities, so every rank allocates the same slot and vnode pools)
+    const uint32_t h[5] = {e->max_n, e->C, ~e->C, e->tr_slots, e->dt_vnodes};
+    uint32_t mx[5] = {0, 0, 0, 0, 0};
     HIPCHK(e, hipMemcpy(buf, h, sizeof(h), hipMemcpyHostToDevice));
-    ncclResult_t r = ncclAllReduce(buf, buf, 3, ncclUint32, ncclMax, (ncclComm_t)e->comm, e->stream);
+    ncclResult_t r = ncclAllReduce(buf, buf, 5, ncclUint32, ncclMax, (ncclComm_t)e->comm, e->stream);
     hipError_t st = hipStreamSynchronize(e->stream);
     if (r == ncclSuccess && st == hipSuccess) st = hipMemcpy(mx, buf, sizeof(mx), hipMemcpyDeviceToHost);
     (void)hipFree(buf);
@@ -245,6 +278,8 @@ int dt_agree_shape(mcs_engine* e) {
     if (st != hipSuccess) return dt_hip_fail(e, "shape exchange", st);
     if (mx[1] != ~mx[2]) return fail(e, MCS_E_INVALID, "sharded DELAY trading needs the same cluster count on every rank");
     e->dt_ns = mx[0];
+    e->tr_slots = mx[3];
+    e->dt_vnodes = mx[4];
     return MCS_OK;
 }
 
@@ -290,8 +325,10 @@ int dtrade_run(mcs_engine* e, mcs_stats* stats) {
     if (e->world > 1 && !e->comm)
         return fail(e, MCS_E_STATE, "sharded DELAY trading run needs mcs_comm_init (or mcs_trade_phase)");
     const auto w0 = std::chrono::steady_clock::now();
-    e->tr_slots = 0;
-    e->dt_vnodes = 0;
+    // the capacities the last run of these inputs escalated to (reset when clusters, jobs or the
+    // shard change): a re-run of the same system starts there instead of repeating the overflowed run
+    e->tr_slots = e->dt_learn_s;
+    e->dt_vnodes = e->dt_learn_v;
     // a communicator selects the RCCL loop (world 1 included: one rank's all-gather is a copy)
     const bool rccl = e->comm != nullptr;
     if (rccl) {
@@ -315,12 +352,16 @@ int dtrade_run(mcs_engine* e, mcs_stats* stats) {
         if (!grow_s && !grow_v) break;
         if ((grow_s && (e->cfg.slot_pool || S >= kDtMaxSlots)) || (grow_v && V >= kDtMaxVnodes))
             return fail(e, MCS_E_CAPACITY, "DELAY trading capacity exhausted (slots or virtual nodes)");
-        const uint32_t ns = grow_s ? S * 2u : S, nv = grow_v ? std::min<uint32_t>(V * 4u, kDtMaxVnodes) : V;
+        // slots grow by half (a multiple of 64): the resident tick keeps every slot in LDS, where
+        // the next power of two may not fit when the peak is just above one
+        const uint32_t ns = grow_s ? std::min<uint32_t>((S + S / 2u + 63u) / 64u * 64u, kDtMaxSlots) : S, nv = grow_v ? std::min<uint32_t>(V * 4u, kDtMaxVnodes) : V;
         dtrade_free(e);
         e->tr_slots = ns;
         e->dt_vnodes = nv;
         ++escalations;
     }
+    e->dt_learn_s = e->cfg.slot_pool ? 0u : e->dtd->a.S;
+    e->dt_learn_v = e->dtd->a.V;
     e->has_run = true;
     e->dtrade_run = true;
     e->trade_run = false;

@@ -271,6 +271,7 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
     mcs::trade_free(e);
     mcs::dtrade_free(e);
     e->has_clusters = e->has_jobs = e->has_run = false;
+    e->dt_learn_s = e->dt_learn_v = 0;
     e->C = n_clusters;
     e->max_n = max_n;
     e->total_nodes = nn;
@@ -337,6 +338,7 @@ static int alloc_jobs(mcs_engine* e, const uint64_t* job_offsets, bool records) 
     mcs::trade_free(e);
     mcs::dtrade_free(e);
     e->has_jobs = e->has_run = false;
+    e->dt_learn_s = e->dt_learn_v = 0;
     e->job_off.assign(job_offsets, job_offsets + e->C + 1);
     e->total_jobs = job_offsets[e->C];
     const size_t nj = e->total_jobs ? e->total_jobs : 1;

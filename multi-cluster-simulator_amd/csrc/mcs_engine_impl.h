@@ -135,6 +135,7 @@ struct mcs_engine {
     mcs::DtradeDev* dtd = nullptr;     // DELAY trading state (mcs_dtrade.cpp)
     bool dtrade_run = false;           // results of the last run come from DELAY trading
     uint32_t dt_vnodes = 0;            // virtual-node capacity per cluster (0 = auto)
+    uint32_t dt_learn_s = 0, dt_learn_v = 0;  // the capacities a DELAY-trading run of these inputs ended at
     uint32_t dt_ns = 0;                // node-snapshot stride over all ranks (0 = max_n)
     uint32_t tr_ns = 0;                // the same for FIFO lock-step trading
     // online mode (mcs_online.cpp): per-cluster state kept on the device between horizons

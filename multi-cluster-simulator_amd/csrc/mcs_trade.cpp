@@ -517,6 +517,7 @@ int mcs_set_shard(mcs_engine* e, uint32_t rank, uint32_t world) {
     if ((uint64_t)world * e->C > 0xFFFFFFFFull) return fail(e, MCS_E_INVALID, "too many clusters");
     mcs::trade_free(e);
     mcs::dtrade_free(e);
+    e->dt_learn_s = e->dt_learn_v = 0;
     e->dt_ns = 0;
     e->tr_ns = 0;
     e->rank = rank;

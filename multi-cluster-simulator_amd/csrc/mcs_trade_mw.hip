@@ -81,6 +81,17 @@ __device__ __forceinline__ uint32_t xcc_id() {
 // the last read: [workgroup][wave][segment], segments as MW_MARK below
 constexpr int kMwSeg = 12, kMwMaxWg = 4;  // (10, 11: sweep passes of X1, X2)
 __device__ unsigned long long g_mw_stamps[kMwMaxWg * kMwWaves * kMwSeg];
+// absolute times (s_memrealtime) of every 64th tick of the launch (up to kMwLogTicks of them), to split the X1 wait into
+// skew (the last record's publication after this wave's own) and propagation (the sweep's end after
+// the last publication): [tick][workgroup][slot], slots 0-15 each wave's phase-A end (its X1
+// granules stored), 16 wave 0's first sweep pass, 17 its last
+constexpr int kMwLogTicks = 1024, kMwLogSlots = kMwWaves + 2;
+__device__ unsigned long long g_mw_tlog[kMwLogTicks * kMwMaxWg * kMwLogSlots];
+#define MW_TLOG(it, slot, v)                                                                   \
+    do {                                                                                       \
+        if (((it) & 63u) == 0u && ((it) >> 6) < (uint32_t)kMwLogTicks && wg < (uint32_t)kMwMaxWg && lane == 0) \
+            g_mw_tlog[((size_t)((it) >> 6) * kMwMaxWg + wg) * kMwLogSlots + (slot)] = (v);                   \
+    } while (0)
 #define MW_MARK(i)                              \
     do {                                        \
         const uint64_t mw_now = wall_clock64(); \
@@ -90,6 +101,9 @@ __device__ unsigned long long g_mw_stamps[kMwMaxWg * kMwWaves * kMwSeg];
 #else
 #define MW_MARK(i) \
     do {           \
+    } while (0)
+#define MW_TLOG(it, slot, v) \
+    do {                     \
     } while (0)
 #endif
 
@@ -551,6 +565,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             xv = lane == 8 ? (uint32_t)MST(cu) : xv;
             xv = lane == 9 ? (uint32_t)MST(mu) : xv;
             if (lane < kX1Words) put(gx1 + (size_t)c * kX1Words + lane, tag1, xv);
+            MW_TLOG(it, wave, wall_clock64());
             if (lane < kStWords) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stv;
             // the next tick's records (only phase A moves these cursors; a WaitQueue head that C/D
             // moves to the BorrowedQueue leaves the ReadyQueue head inside the same window, or
@@ -579,6 +594,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                 }
 #ifdef MCS_STAMPS
                 mw_acc[10] += 1u;
+                if (spins == 0u) MW_TLOG(it, kMwWaves, wall_clock64());
 #endif
                 if (__all(ok)) break;
                 if (spins > kSpinLimit) {
@@ -586,6 +602,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                     break;
                 }
             }
+            MW_TLOG(it, kMwWaves + 1, wall_clock64());
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
                 const uint32_t i = lane + (uint32_t)k * kWave;
@@ -929,5 +946,9 @@ extern "C" int mcs_debug_mw_stamps(unsigned long long* out) {
     unsigned long long z[mcs::kMwMaxWg * mcs::kMwWaves * mcs::kMwSeg] = {};  // (768)
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_mw_stamps), sizeof(z)) != hipSuccess) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_mw_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+// the last launch's absolute-time log ([1024 ticks][4 workgroups][18 slots], see g_mw_tlog)
+extern "C" int mcs_debug_mw_tlog(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_mw_tlog), sizeof(mcs::g_mw_tlog)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -87,3 +87,24 @@ def test_delay_batch_matches_single():
         np.testing.assert_array_equal(node[js], a[0])
         np.testing.assert_array_equal(st[js], a[1])
         assert ds["total_wait_ms"][c] == a[3]["total_wait_ms"]
+
+
+def test_grown_node_pass_model_equals_oracle():
+    """The hand-scheduled DELAY loop's Level1 pass (r04) tests a Level1 job only against the nodes
+    that grew since the last pass, measured from a snapshot lowered at every Level1 move, plus the
+    D6-skipped jobs: tools/delay_g_model.py restates that algorithm in Python and must give the
+    oracle's placements on randomised clusters (deadlocks, zero durations, partial availability)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(
+        "delay_g_model", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
+                                      "delay_g_model.py"))
+    M = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(M)
+    import sys
+    argv = sys.argv
+    try:
+        sys.argv = ["delay_g_model.py", "80"]
+        assert M.main() == 0
+    finally:
+        sys.argv = argv

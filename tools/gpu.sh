@@ -2,12 +2,15 @@
 # The one GPU script (run through gpurun): STEPS picks the steps, in order, each under its own time
 # limit; a crash / abort / timeout ends the script (no further GPU work in this call).
 #   TAG      output directory gpurun_out/$TAG
-#   STEPS    any of: tests smoke benches prof pmc ab   (default: tests smoke benches prof pmc)
+#   STEPS    any of: tests smoke benches prof pmc ab py trace   (default: tests smoke benches prof pmc)
 #   PYTEST   pytest selection for `tests` (default: the whole -m gpu suite)
 #   BENCHES  one bench.py argument line per bench (default: every headline line)
 #   PROFS    name|bench args lines for rocprofv3 --kernel-trace --stats (per-dispatch traces dropped)
 #   PMC_ARGS bench.py arguments of the PMC passes (default: the C4 headline shape)
 #   AB       tools/ab_bench.py arguments (interleaved variant timing)
+#   TRACES   name|bench args for `trace`: rocprofv3 --kernel-trace (TRACE_RT=1: + --runtime-trace), summarised by
+#            tools/trace_gaps.py into $OUT/trace_<name>.json (the raw CSVs are deleted on the box)
+#   PY       name|script args lines for `py`: python tools (stamp probes, traces) -> $OUT/py_<name>.txt
 # Summaries go to profiles/ with tools/collect_profiles.py afterwards (on the CPU side).
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -82,6 +85,32 @@ pmc)
 ab)
     timeout -k 10 900 python -u tools/ab_bench.py $AB > "$OUT/ab.txt" 2>&1
     rc=$?; tail -12 "$OUT/ab.txt"; echo "ab rc=$rc"; fatal $rc || exit $rc ;;
+trace)
+    while IFS= read -r spec; do
+        [ -z "$spec" ] && continue
+        name="${spec%%|*}"; args="${spec#*|}"
+        ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace ${TRACE_RT:+--runtime-trace} \
+            --output-format csv -d "$OUT/trace_$name" -o t -- python3 "$ROOT/bench.py" $args --no-cpu-baseline ) \
+            > "$OUT/trace_$name.log" 2>&1
+        rc=$?; echo "trace $name rc=$rc"
+        python tools/trace_gaps.py "$OUT/trace_$name" "$OUT/trace_$name.log" > "$OUT/trace_$name.json" 2>&1
+        head -c 2500 "$OUT/trace_$name.json"; echo
+        rm -rf "$OUT/trace_$name"
+        fatal $rc || exit $rc
+    done <<LIST
+${TRACES:-}
+LIST
+    ;;
+py)
+    while IFS= read -r spec; do
+        [ -z "$spec" ] && continue
+        name="${spec%%|*}"; args="${spec#*|}"
+        timeout -k 10 600 python -u $args > "$OUT/py_$name.txt" 2>&1
+        rc=$?; echo "py $name rc=$rc"; tail -40 "$OUT/py_$name.txt"; fatal $rc || exit $rc
+    done <<LIST
+${PY:-}
+LIST
+    ;;
 esac
 done
 echo "done $OUT"

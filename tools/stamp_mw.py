@@ -22,11 +22,13 @@ eng.load_clusters(replicate(uniform_cluster(256), 64))
 eng.generate_jobs(GenParams(seed=1, arrival_mode=1, lam=scaled_lambda(256, load=0.9)), J)
 fn = L.lib().mcs_debug_mw_stamps
 buf = (C.c_ulonglong * 768)()
+tl = (C.c_ulonglong * (1024 * 4 * 18))()
 eng.run(); fn(buf)
 st = eng.run(); assert fn(buf) == 0
+assert L.lib().mcs_debug_mw_tlog(tl) == 0
 ts = eng.trade_stats()
 print(json.dumps({"ms": st.kernel_ms, "ticks": int(ts["ticks"]), "loop_form": int(ts["loop_form"]),
-                  "slot_pool": int(st.slot_pool), "s": list(buf)}))
+                  "slot_pool": int(st.slot_pool), "s": list(buf), "tl": list(tl)}))
 '''
 SEG = ["prefetch", "releases", "arrivals", "decisions", "sample+record", "X1_sweep_or_wait",
        "phase_B", "barrier_B", "X2+CD", "barrier_loop"]
@@ -52,6 +54,33 @@ def main():
            "us_per_tick_max_over_waves": {SEG[i]: round(max(w[i] for w in per_wave), 3) for i in range(10)},
            "us_per_tick_mean_over_waves": {SEG[i]: round(sum(w[i] for w in per_wave) / 64, 3) for i in range(10)},
            "sweep_passes_per_tick_x1_x2_by_wg": [[round(a, 2), round(b, 2)] for a, b in passes]}
+    # the X1 wait split (absolute times of every 64th tick of the last launch, 10 ns units): skew =
+    # the last record's publication after this workgroup's wave 0 stored its own; propagation =
+    # wave 0's sweep end after the last publication; first_pass = its first sweep's end after the last
+    # publication (negative: the first pass ran before the last record existed)
+    import numpy as np
+    tl = np.array(d["tl"], dtype=np.int64).reshape(1024, 4, 18)
+    nwg = 4
+    tl = tl[:, :nwg]
+    ok = (tl > 0).all(axis=(1, 2))
+    tl = tl[ok]
+    pub = tl[:, :, :16]
+    last_pub = pub.max(axis=(1, 2))
+    last_w = pub.reshape(len(tl), -1).argmax(axis=1)
+    skew = (last_pub[:, None] - tl[:, :, 0]) * 10.0 / 1e3
+    prop = (tl[:, :, 17] - last_pub[:, None]) * 10.0 / 1e3
+    first = (tl[:, :, 16] - last_pub[:, None]) * 10.0 / 1e3
+    spread = (last_pub - pub.min(axis=(1, 2))) * 10.0 / 1e3
+    res["x1_split_us"] = {
+        "ticks_logged": int(len(tl)),
+        "skew_mean_by_wg": [round(float(x), 3) for x in skew.mean(axis=0)],
+        "propagation_mean_by_wg": [round(float(x), 3) for x in prop.mean(axis=0)],
+        "propagation_p50_p90": [round(float(np.percentile(prop, 50)), 3), round(float(np.percentile(prop, 90)), 3)],
+        "first_pass_after_last_pub_mean": round(float(first.mean()), 3),
+        "publication_spread_mean": round(float(spread.mean()), 3),
+        "last_publisher_top": [[int(c), int(k)] for c, k in zip(*np.unique(last_w, return_counts=True))
+                               if k >= max(1, len(tl) // 50)],
+    }
     print(json.dumps(res, indent=1))
 
 
