@@ -84,8 +84,9 @@ __device__ unsigned long long g_mw_stamps[kMwMaxWg * kMwWaves * kMwSeg];
 // absolute times (s_memrealtime) of every 64th tick of the launch (up to kMwLogTicks of them), to split the X1 wait into
 // skew (the last record's publication after this wave's own) and propagation (the sweep's end after
 // the last publication): [tick][workgroup][slot], slots 0-15 each wave's phase-A end (its X1
-// granules stored), 16 wave 0's first sweep pass, 17 its last
-constexpr int kMwLogTicks = 1024, kMwLogSlots = kMwWaves + 2;
+// granules stored), 16-31 each wave's arrival at the X1 barrier, 32 wave 0's first sweep pass, 33
+// its last, 34 wave 0 past the X1 barrier
+constexpr int kMwLogTicks = 1024, kMwLogSlots = 2 * kMwWaves + 3;
 __device__ unsigned long long g_mw_tlog[kMwLogTicks * kMwMaxWg * kMwLogSlots];
 #define MW_TLOG(it, slot, v)                                                                   \
     do {                                                                                       \
@@ -150,6 +151,17 @@ struct MwShared {  // (this workgroup's node vectors follow: kMwWaves * ns u64)
     uint32_t T, done, ticks, flags, xcd, tmax_now;
     unsigned long long n_trades, n_won, n_lent;
 };
+// X1 stores a record's word w at rq_job + w * 64: the ten arrays must stay consecutive, in word order
+static_assert(offsetof(MwShared, rq_c) == offsetof(MwShared, rq_job) + 1 * kTrResMaxClusters * 4 &&
+                  offsetof(MwShared, rq_m) == offsetof(MwShared, rq_job) + 2 * kTrResMaxClusters * 4 &&
+                  offsetof(MwShared, rq_dur) == offsetof(MwShared, rq_job) + 3 * kTrResMaxClusters * 4 &&
+                  offsetof(MwShared, qs) == offsetof(MwShared, rq_job) + 4 * kTrResMaxClusters * 4 &&
+                  offsetof(MwShared, decided) == offsetof(MwShared, rq_job) + 5 * kTrResMaxClusters * 4 &&
+                  offsetof(MwShared, next_arr_t) == offsetof(MwShared, rq_job) + 6 * kTrResMaxClusters * 4 &&
+                  offsetof(MwShared, xflags) == offsetof(MwShared, rq_job) + 7 * kTrResMaxClusters * 4 &&
+                  offsetof(MwShared, cu) == offsetof(MwShared, rq_job) + 8 * kTrResMaxClusters * 4 &&
+                  offsetof(MwShared, mu) == offsetof(MwShared, rq_job) + 9 * kTrResMaxClusters * 4,
+              "X1 record arrays out of word order");
 
 template <int kRows>  // slot rows per cluster (64 slots each)
 __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, unsigned long long* gx_uc,
@@ -594,7 +606,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                 }
 #ifdef MCS_STAMPS
                 mw_acc[10] += 1u;
-                if (spins == 0u) MW_TLOG(it, kMwWaves, wall_clock64());
+                if (spins == 0u) MW_TLOG(it, 2 * kMwWaves, wall_clock64());
 #endif
                 if (__all(ok)) break;
                 if (spins > kSpinLimit) {
@@ -602,30 +614,24 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                     break;
                 }
             }
-            MW_TLOG(it, kMwWaves + 1, wall_clock64());
+            MW_TLOG(it, 2 * kMwWaves + 1, wall_clock64());
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
                 const uint32_t i = lane + (uint32_t)k * kWave;
                 if (i < nw) {
-                    const uint32_t v = xv[k], g = i / kX1Words, w = i - g * kX1Words;
-                    switch (w) {
-                        case 0: sh.rq_job[g] = v; break;
-                        case 1: sh.rq_c[g] = v; break;
-                        case 2: sh.rq_m[g] = v; break;
-                        case 3: sh.rq_dur[g] = v; break;
-                        case 4: sh.qs[g] = v; break;
-                        case 5: sh.decided[g] = v; break;
-                        case 6: sh.next_arr_t[g] = v; break;
-                        case 7: sh.xflags[g] = v; break;
-                        case 8: sh.cu[g] = __uint_as_float(v); break;
-                        default: sh.mu[g] = __uint_as_float(v); break;
-                    }
+                    // the record's ten words land in ten consecutive [64]-arrays of MwShared (rq_job
+                    // .. mu): one LDS store at word w's array, no per-word branch (a switch on the
+                    // lane-varying word index ran as a divergent chain, ~8 us of the tick)
+                    const uint32_t g = i / kX1Words, w = i - g * kX1Words;
+                    reinterpret_cast<uint32_t*>(sh.rq_job)[w * kTrResMaxClusters + g] = xv[k];
                 }
             }
             if (lane < 3) sh.accm[lane] = 0u;
             if (timed_out && lane == 0) sh.done = 2u;
         }
+        MW_TLOG(it, kMwWaves + wave, wall_clock64());
         __syncthreads();
+        if (wave == 0) MW_TLOG(it, 2 * kMwWaves + 2, wall_clock64());
         MW_MARK(5);
         if (sh.done == 2u) break;
 
@@ -947,7 +953,7 @@ extern "C" int mcs_debug_mw_stamps(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_mw_stamps), sizeof(z)) != hipSuccess) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_mw_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
-// the last launch's absolute-time log ([1024 ticks][4 workgroups][18 slots], see g_mw_tlog)
+// the last launch's absolute-time log ([1024 ticks][4 workgroups][35 slots], see g_mw_tlog)
 extern "C" int mcs_debug_mw_tlog(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_mw_tlog), sizeof(mcs::g_mw_tlog)) == hipSuccess ? 0 : -1;
 }

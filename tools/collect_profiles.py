@@ -2,7 +2,7 @@
 the per-launch HBM traffic of the measured kernel for bench.py's roofline.traffic.
 
 The kernel is matched by its exact rocprofv3 name: MCS_KERNEL if set, else the engine (mcs::) kernel with
-the most calls in the kernel-trace stats (the bench's production launches; bench.py's single untimed
+the most calls in the kernel-trace stats (in a PMC-only run: the most dispatches in the counter passes) (the bench's production launches; bench.py's single untimed
 counting-build launch, e.g. `fifo_asm_kernel<16, true, 4, 8, true>`, is a different name and is
 never averaged in).
 
@@ -36,8 +36,22 @@ if stats:
         if r["Name"] == kernel:
             summary.update(kernel=r["Name"], calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
                            min_ns=float(r["MinNs"]), max_ns=float(r["MaxNs"]))
+if kernel is None:  # a PMC-only run: the engine kernel with the most dispatches in the counter passes
+    seen = {}
+    for g in sorted(glob.glob(f"{run}/pmc*_g*/pmc_counter_collection.csv")):
+        for r in csv.DictReader(open(g)):
+            n = r.get("Kernel_Name", r.get("Name", ""))
+            if "mcs::" in n:
+                seen.setdefault(n, set()).add(r["Dispatch_Id"])
+    bk = None
+    if os.path.exists(f"{run}/bench.json"):  # the bench line's kernel (e.g. mcs::delay_asm_kernel)
+        with open(f"{run}/bench.json") as f:
+            bk = json.loads(f.read().strip().splitlines()[-1])["roofline"].get("kernel", "").split("::")[-1]
+    named = {n: v for n, v in seen.items() if bk and bk.split(" ")[0] in n}
+    if named or seen:
+        kernel = max(named or seen, key=lambda n: len((named or seen)[n]))
 if kernel is None:
-    sys.exit("no kernel_stats.csv in the run and no MCS_KERNEL: cannot tell which kernel to summarise")
+    sys.exit("no kernel_stats.csv or PMC pass in the run and no MCS_KERNEL: cannot tell which kernel to summarise")
 
 counters = {}
 launches = 0

@@ -7,8 +7,10 @@
 #   BENCHES  one bench.py argument line per bench (default: every headline line)
 #   PROFS    name|bench args lines for rocprofv3 --kernel-trace --stats (per-dispatch traces dropped)
 #   PMC_ARGS bench.py arguments of the PMC passes (default: the C4 headline shape)
+#   PMC_GROUPS which counter groups (1 FETCH, 2 WRITE, 3-5 SQ/GRBM; default all)
 #   AB       tools/ab_bench.py arguments (interleaved variant timing)
-#   TRACES   name|bench args for `trace`: rocprofv3 --kernel-trace (TRACE_RT=1: + --runtime-trace), summarised by
+#   TRACES   name|bench args for `trace`: rocprofv3 --kernel-trace (TRACE_RT=1: + --runtime-trace) of
+#            TRACE_BENCH (default bench.py; e.g. an older tree's under variants/), summarised by
 #            tools/trace_gaps.py into $OUT/trace_<name>.json (the raw CSVs are deleted on the box)
 #   PY       name|script args lines for `py`: python tools (stamp probes, traces) -> $OUT/py_<name>.txt
 # Summaries go to profiles/ with tools/collect_profiles.py afterwards (on the CPU side).
@@ -74,8 +76,9 @@ pmc)
                "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
                "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INST_CYCLES_SALU"; do
         gi=$((gi+1))
+        case " ${PMC_GROUPS:-1 2 3 4 5} " in *" $gi "*) ;; *) continue ;; esac
         ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace \
-            --output-format csv -d "$OUT/pmc_g$gi" -o pmc -- python3 "$ROOT/bench.py" ${PMC_ARGS:-} --steps 1 \
+            --output-format csv -d "$OUT/pmc_g$gi" -o pmc -- python3 "$ROOT/bench.py" ${PMC_ARGS:-} --steps 2 \
             --warmup 0 --no-cpu-baseline ) > "$OUT/pmc_g$gi.log" 2>&1
         rc=$?; echo "pmc group $gi rc=$rc"; fatal $rc || exit $rc
     done
@@ -90,7 +93,7 @@ trace)
         [ -z "$spec" ] && continue
         name="${spec%%|*}"; args="${spec#*|}"
         ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace ${TRACE_RT:+--runtime-trace} \
-            --output-format csv -d "$OUT/trace_$name" -o t -- python3 "$ROOT/bench.py" $args --no-cpu-baseline ) \
+            --output-format csv -d "$OUT/trace_$name" -o t -- python3 "${TRACE_BENCH:-$ROOT/bench.py}" $args --no-cpu-baseline ) \
             > "$OUT/trace_$name.log" 2>&1
         rc=$?; echo "trace $name rc=$rc"
         python tools/trace_gaps.py "$OUT/trace_$name" "$OUT/trace_$name.log" > "$OUT/trace_$name.json" 2>&1

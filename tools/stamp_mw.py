@@ -22,7 +22,7 @@ eng.load_clusters(replicate(uniform_cluster(256), 64))
 eng.generate_jobs(GenParams(seed=1, arrival_mode=1, lam=scaled_lambda(256, load=0.9)), J)
 fn = L.lib().mcs_debug_mw_stamps
 buf = (C.c_ulonglong * 768)()
-tl = (C.c_ulonglong * (1024 * 4 * 18))()
+tl = (C.c_ulonglong * (1024 * 4 * 35))()
 eng.run(); fn(buf)
 st = eng.run(); assert fn(buf) == 0
 assert L.lib().mcs_debug_mw_tlog(tl) == 0
@@ -59,25 +59,26 @@ def main():
     # wave 0's sweep end after the last publication; first_pass = its first sweep's end after the last
     # publication (negative: the first pass ran before the last record existed)
     import numpy as np
-    tl = np.array(d["tl"], dtype=np.int64).reshape(1024, 4, 18)
-    nwg = 4
-    tl = tl[:, :nwg]
-    ok = (tl > 0).all(axis=(1, 2))
-    tl = tl[ok]
-    pub = tl[:, :, :16]
+    raw = np.array(d["tl"], dtype=np.int64).reshape(1024, 4, 35)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    np.save(os.path.join(REPO, "gpurun_out", "mw_tlog.npy"), raw)
+    tl = raw[:, :4]
+    tl = tl[(tl[:, :, [0, 33, 34]] > 0).all(axis=(1, 2))]
+    us = lambda x: x * 10.0 / 1e3  # noqa: E731  (100 MHz ticks)
+    pub, arr = tl[:, :, :16], tl[:, :, 16:32]
     last_pub = pub.max(axis=(1, 2))
     last_w = pub.reshape(len(tl), -1).argmax(axis=1)
-    skew = (last_pub[:, None] - tl[:, :, 0]) * 10.0 / 1e3
-    prop = (tl[:, :, 17] - last_pub[:, None]) * 10.0 / 1e3
-    first = (tl[:, :, 16] - last_pub[:, None]) * 10.0 / 1e3
-    spread = (last_pub - pub.min(axis=(1, 2))) * 10.0 / 1e3
+    done, after = tl[:, :, 33], tl[:, :, 34]
     res["x1_split_us"] = {
         "ticks_logged": int(len(tl)),
-        "skew_mean_by_wg": [round(float(x), 3) for x in skew.mean(axis=0)],
-        "propagation_mean_by_wg": [round(float(x), 3) for x in prop.mean(axis=0)],
-        "propagation_p50_p90": [round(float(np.percentile(prop, 50)), 3), round(float(np.percentile(prop, 90)), 3)],
-        "first_pass_after_last_pub_mean": round(float(first.mean()), 3),
-        "publication_spread_mean": round(float(spread.mean()), 3),
+        "wave0_pub_to_sweep_end": round(float(us(done - tl[:, :, 0]).mean()), 3),
+        "skew_last_pub_after_wave0_pub": round(float(us(last_pub[:, None] - tl[:, :, 0]).mean()), 3),
+        "propagation_sweep_end_after_last_pub": round(float(us(done - last_pub[:, None]).mean()), 3),
+        "first_pass_after_last_pub": round(float(us(tl[:, :, 32] - last_pub[:, None]).mean()), 3),
+        "sweep_end_to_past_barrier": round(float(us(after - done).mean()), 3),
+        "last_barrier_arrival_after_sweep_end": round(float(us(arr.max(axis=2) - done).mean()), 3),
+        "pub_to_barrier_arrival_by_wave_mean": [round(float(x), 3) for x in us(arr - pub).mean(axis=(0, 1))],
+        "x1_segment_total_wave0": round(float(us(after - tl[:, :, 0]).mean()), 3),
         "last_publisher_top": [[int(c), int(k)] for c, k in zip(*np.unique(last_w, return_counts=True))
                                if k >= max(1, len(tl) // 50)],
     }

@@ -22,6 +22,8 @@ def rows(pattern):
 
 
 def short(name):
+    """The kernel's name without namespaces' '(anonymous namespace)' and its argument list."""
+    name = name.replace("(anonymous namespace)::", "")
     return name.split("(")[0][:80]
 
 
