@@ -162,16 +162,19 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "mcsfd_" T "e_%=:\n\t"
 
 // a Level0 batch's results (the lanes placed on Level0; moved jobs are written when Level1 places
-// them) and their waits; v91 = -1 marks a lane without a Level0 placement
+// them) and their waits; v91 = -1 marks a lane without a Level0 placement.  Result stores are plain
+// (write-back): a row line stays in L2 while Level1 placements fill its holes; as nt stores every
+// partial line went to HBM (127.8 -> 51.4 B/placement on the Level1-heavy stream, with the job
+// records loaded nt so the stream does not evict them; profiles/r04_pmc_head, r04_pmc_plainnt)
 #define MCS_FD_STORE                                                                              \
     "v_cmp_ne_u32_e32 vcc, -1, v91\n\t"                                                          \
     "s_mov_b64 exec, vcc\n\t"                                                                     \
     "v_add_u32 v125, s57, v110\n\t"                                                               \
     "v_lshlrev_b32 v125, 2, v125\n\t" MCS_FA_NODEIDX                                              \
-    "global_store_dword v125, v126, s[66:67] nt\n\t"                                              \
-    "global_store_dword v125, v92, s[68:69] nt\n\t"                                               \
+    "global_store_dword v125, v126, s[66:67]\n\t"                                              \
+    "global_store_dword v125, v92, s[68:69]\n\t"                                               \
     "v_add_u32 v93, v92, v95\n\t" /* finish = start + the batch's duration column */            \
-    "global_store_dword v125, v93, s[70:71] nt\n\t"                                               \
+    "global_store_dword v125, v93, s[70:71]\n\t"                                               \
     "v_sub_u32 v104, v92, v94\n\t" /* start - arrival */                                         \
     "v_add_co_u32 v102, vcc, v102, v104\n\t"                                                      \
     "v_addc_co_u32 v103, vcc, 0, v103, vcc\n\t"                                                   \
@@ -289,9 +292,9 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "v_mov_b32 v126, s74\n\t"                                                                     \
     "v_mov_b32 v127, s40\n\t"                                                                     \
     "v_mov_b32 v124, s55\n\t"                                                                     \
-    "global_store_dword v125, v126, s[66:67] nt\n\t"                                              \
-    "global_store_dword v125, v127, s[68:69] nt\n\t"                                              \
-    "global_store_dword v125, v124, s[70:71] nt\n\t"                                              \
+    "global_store_dword v125, v126, s[66:67]\n\t"                                              \
+    "global_store_dword v125, v127, s[68:69]\n\t"                                              \
+    "global_store_dword v125, v124, s[70:71]\n\t"                                              \
     "s_mov_b64 exec, -1\n\t"                                                                      \
     "s_bitset1_b64 s[90:91], s82\n\t"                                                             \
     "s_add_u32 s95, s94, s82\n\t"                                                                 \
@@ -406,7 +409,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     /* prefetch batch 1 */                                                                        \
     "v_lshlrev_b32 v121, 4, v110\n\t"                                                             \
     "v_add_u32 v121, 0x400, v121\n\t"                                                             \
-    "global_load_dwordx4 v[98:101], v121, s[64:65]\n\t"                                           \
+    "global_load_dwordx4 v[98:101], v121, s[64:65] nt\n\t"                                           \
     "s_min_u32 s41, s42, 64\n\t" MCS_FA_REC16                                                     \
     "s_cmp_eq_u32 s42, 0\n\t" /* no jobs: no iteration (the clock stays at 0) */                 \
     "s_cbranch_scc1 mcsfd_exit_%=\n\t"                                                            \
@@ -519,13 +522,6 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "ds_write_b32 v62, v114\n\t"                                                                  \
     "ds_write_b32 v62, v115 offset:%[cap4]\n\t"                                                   \
     "ds_write_b32 v62, v123 offset:%[cap8]\n\t"                                                   \
-    "s_and_b32 s74, s48, 0xffff\n\t"                                                              \
-    "s_min_u32 s74, s74, 63\n\t"                                                                  \
-    "s_sub_u32 s74, 63, s74\n\t" /* its core key */                                             \
-    "s_lshr_b32 s76, s48, 16\n\t"                                                                 \
-    "s_add_u32 s76, s76, 0x8000\n\t"                                                              \
-    "s_lshl_b64 exec, 1, s74\n\t"                                                                 \
-    "v_min_u32 v106, s76, v106\n\t" /* the pass-skip bound of its key */                        \
     "s_mov_b64 exec, -1\n\t"                                                                      \
     "v_pk_min_u16 v105, v105, v64\n\t" /* it failed every node as they are now: the snapshot */ \
     "v_pk_min_u16 v106, v106, v65\n\t" /* G is measured from may not exceed them */            \
@@ -551,7 +547,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "v_add_u32 v121, s57, v110\n\t"                                                               \
     "v_lshlrev_b32 v121, 4, v121\n\t"                                                             \
     "v_add_u32 v121, 0x400, v121\n\t"                                                             \
-    "global_load_dwordx4 v[98:101], v121, s[64:65]\n\t"                                           \
+    "global_load_dwordx4 v[98:101], v121, s[64:65] nt\n\t"                                           \
     "s_sub_u32 s41, s42, s57\n\t"                                                                 \
     "s_min_u32 s41, s41, 64\n\t"                                                                  \
     "s_mov_b32 s47, 0\n\t" MCS_FA_REC16                                                           \

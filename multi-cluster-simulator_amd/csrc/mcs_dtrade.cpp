@@ -144,11 +144,12 @@ int dt_poll(mcs_engine* e) {
     return MCS_OK;
 }
 
-// MCS_DTRADE_RESIDENT=0 keeps the graph-replayed kernels; MCS_TRADE_RES_TICKS caps the ticks of one
-// resident launch (tests cross launch boundaries with it)
+// MCS_DTRADE_RESIDENT=1 selects the one-workgroup resident tick (opt-in: on C5-DELAY it measured
+// 24.9 us/tick against the graph-replayed kernels' 19.5); MCS_TRADE_RES_TICKS caps
+// the ticks of one resident launch (tests cross launch boundaries with it)
 bool dt_resident(mcs_engine* e, size_t* lds) {
     const char* env = getenv("MCS_DTRADE_RESIDENT");
-    if (env && atoi(env) == 0) return false;
+    if (!env || atoi(env) == 0) return false;
     if (!dtrade_res_shape(e->dtd->a, e->world, lds)) return false;
     int max_lds = 0;
     if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device) != hipSuccess)

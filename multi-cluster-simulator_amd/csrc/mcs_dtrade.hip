@@ -30,6 +30,27 @@
 namespace mcs {
 namespace {
 
+#ifdef MCS_STAMPS
+// the probe build's dt_step segment times (s_memrealtime, 100 MHz), summed over clusters and ticks:
+// 0 state in + LDS copies, 1 releases, 2 arrivals, 3 Level1 pass, 4 Level0 head, 5 copies out +
+// sample, 6 record + snapshot + contract sizes; [7] dt_step calls (clusters x ticks)
+__device__ unsigned long long g_dt_stamps[8];
+// per tick: the slowest cluster's step (and each segment's slowest), summed over ticks by the trader
+// kernel of the tick ([0-6] segments, [7] the whole step); [8] the trader kernel's own time, [9] ticks
+__device__ unsigned long long g_dt_cur[8];
+__device__ unsigned long long g_dt_maxsum[10];
+#define DT_MARK(i)                                  \
+    do {                                            \
+        const uint64_t dt_now = wall_clock64();     \
+        dt_acc[i] += dt_now - dt_last;              \
+        dt_last = dt_now;                           \
+    } while (0)
+#else
+#define DT_MARK(i) \
+    do {           \
+    } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t dt_wave_sum_u32(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
     return v;
@@ -136,6 +157,10 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
     __shared__ uint32_t sfin[kDtMaxSlots];
     __shared__ uint32_t hist[kWave];
     if (a.ctl->done) return;
+#ifdef MCS_STAMPS
+    uint64_t dt_acc[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint64_t dt_last = wall_clock64();
+#endif
     const uint32_t T = a.ctl->T;
     const uint32_t c = blockIdx.x, lane = threadIdx.x;
     const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
@@ -154,6 +179,7 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
     copy_rounds<2>(nodes + N, a.vn + (size_t)c * a.V, NN - N, lane);
     copy_rounds<8>(sfin, a.sfin + sb, S, lane);
     __syncthreads();
+    DT_MARK(0);
 
     // releases due at T (cluster.go:153-157), Foreign jobs included
     if (st.minf <= T) {
@@ -178,6 +204,7 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         st.minf = wave_min_u32(lm);
         __syncthreads();
     }
+    DT_MARK(1);
     // "/delay" arrivals up to T join Level0 (server.go:67-74): JobsMap[id] = 0, JobsCount++
     {
         const uint32_t before = st.next_arr;
@@ -191,6 +218,7 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         st.count += (long long)(st.next_arr - before);
     }
 
+    DT_MARK(2);
     // ScheduleJob (scheduler.go:127-139) over Cluster.Nodes: physical, then virtual
     auto first_fit = [&](uint32_t jc, uint32_t jm) -> uint32_t {
         uint32_t best = kEmpty;
@@ -390,6 +418,7 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         st.l1_dirty = wr != n1 ? 1u : 0u;  // a pass that placed: its skipped entries come next
     }
 
+    DT_MARK(3);
     // ---- Level0 head (scheduler.go:332-366) ----
     if (!(st.flags & MCS_FLAG_OVERFLOW) && st.l0_head < st.next_arr) {
         const uint32_t j = st.l0_head;
@@ -427,6 +456,7 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         }
     }
 
+    DT_MARK(4);
     __syncthreads();
     copy_rounds<4>(a.tn + n0, nodes, N, lane);
     copy_rounds<2>(a.vn + (size_t)c * a.V, nodes + N, NN - N, lane);
@@ -457,6 +487,7 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         }
     }
     if (lane == 0) a.cl[c] = st;
+    DT_MARK(5);
 
     // ---- this cluster's exchange record and, when a trader round is due at T, its node
     // snapshot and both contract sizes over GetLevel1() (ProvideJobs, trader_server.go:69-94) ----
@@ -526,6 +557,19 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         r.pad = 0u;
         reinterpret_cast<DtRec*>(blk)[c] = r;
     }
+#ifdef MCS_STAMPS
+    DT_MARK(6);
+    if (lane == 0) {
+        unsigned long long tot = 0;
+        for (int i = 0; i < 7; ++i) {
+            atomicAdd(&g_dt_stamps[i], (unsigned long long)dt_acc[i]);
+            atomicMax(&g_dt_cur[i], (unsigned long long)dt_acc[i]);
+            tot += dt_acc[i];
+        }
+        atomicMax(&g_dt_cur[7], tot);
+        atomicAdd(&g_dt_stamps[7], 1ull);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -539,6 +583,9 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
     __shared__ uint32_t nvs[kDtMaxClusters];  // virtual nodes per cluster (written here)
     __shared__ uint32_t nfr[kDtMaxClusters];  // free running slots per cluster (taken here)
     if (a.ctl->done) return;
+#ifdef MCS_STAMPS
+    const uint64_t tr_t0 = wall_clock64();
+#endif
     const uint32_t T = a.ctl->T;
     const bool any_due = a.ctl->any_due != 0u;
     const uint32_t lane = threadIdx.x;
@@ -809,6 +856,14 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
         ctl->n_trades = n_trades;
         ctl->n_won = n_won;
         ctl->n_foreign = n_for;
+#ifdef MCS_STAMPS
+        for (int i = 0; i < 8; ++i) {
+            g_dt_maxsum[i] += g_dt_cur[i];
+            g_dt_cur[i] = 0ull;
+        }
+        g_dt_maxsum[8] += wall_clock64() - tr_t0;
+        g_dt_maxsum[9] += 1ull;
+#endif
     }
 }
 
@@ -853,3 +908,18 @@ hipError_t launch_dtrade_tick(const DtArgs& a, hipStream_t s) {
 }
 
 }  // namespace mcs
+
+#ifdef MCS_STAMPS
+// the probe build's dt_step segment sums (see g_dt_stamps), read and cleared
+extern "C" int mcs_debug_dt_stamps(unsigned long long* out) {
+    unsigned long long z[8] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_dt_stamps), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_dt_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+// the per-tick maxima summed over ticks and the trader kernel's time (see g_dt_maxsum), read and cleared
+extern "C" int mcs_debug_dt_maxsum(unsigned long long* out) {
+    unsigned long long z[10] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_dt_maxsum), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_dt_maxsum), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

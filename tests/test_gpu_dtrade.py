@@ -240,6 +240,7 @@ def test_gpu_dtrade_resident_equals_kernels_and_oracle(kind, C, J, ticks, monkey
     one launch or many short ones (MCS_TRADE_RES_TICKS), equals the graph-replayed kernels
     (MCS_DTRADE_RESIDENT=0) and the oracle on every output."""
     arrays, streams, _ = seeded_workload(kind, C, J)
+    monkeypatch.setenv("MCS_DTRADE_RESIDENT", "1")
     if ticks:
         monkeypatch.setenv("MCS_TRADE_RES_TICKS", ticks)
     g = run(arrays, streams)
@@ -264,13 +265,14 @@ def test_gpu_dtrade_resident_equals_kernels_and_oracle(kind, C, J, ticks, monkey
     assert len(g["foreign"]) == o["n_foreign"] and g["ts"]["t_final"] == o["t_final"]
 
 
-def test_gpu_dtrade_learned_capacity_keeps_the_resident_tick():
+def test_gpu_dtrade_learned_capacity_keeps_the_resident_tick(monkeypatch):
     """C5-DELAY's own system (64 cluster_small clusters x 2000 jobs) peaks at 331 running jobs in one
     cluster: the first run overflows the 256 auto slots and escalates by half to 384, where the
     resident tick's LDS still holds every slot (a doubling to 512 would not fit); a second run of the
     same inputs starts at the learned 384 (no overflowed run), and both equal the graph-replayed
     kernels and the oracle."""
     arrays, streams, _ = seeded_workload("small", 64, 2000)
+    monkeypatch.setenv("MCS_DTRADE_RESIDENT", "1")
     with Engine(0, policy="DELAY", trader=True) as eng:
         eng.load_clusters(arrays)
         eng.submit_jobs(streams)
@@ -284,11 +286,8 @@ def test_gpu_dtrade_learned_capacity_keeps_the_resident_tick():
     assert st2.escalations == 0 and st2.slot_pool == 6 and ts2["loop_form"] == 3
     for a, b in ((n1, n2), (s1, s2), (f1, f2)):
         np.testing.assert_array_equal(a, b)
-    os.environ["MCS_DTRADE_RESIDENT"] = "0"
-    try:
-        r = run(arrays, streams)
-    finally:
-        os.environ.pop("MCS_DTRADE_RESIDENT", None)
+    monkeypatch.setenv("MCS_DTRADE_RESIDENT", "0")
+    r = run(arrays, streams)
     assert r["ts"]["loop_form"] == 0
     np.testing.assert_array_equal(n1, r["node"])
     np.testing.assert_array_equal(s1, r["start"])
