@@ -30,6 +30,14 @@
 namespace mcs {
 namespace {
 
+// dt_step_kernel is one wave per block (launch_bounds 64): its LDS traffic is ordered by the wave's
+// own in-order LDS queue, so between its phases a compiler barrier suffices.  __syncthreads() would
+// also wait for every outstanding global load, i.e. drain the Level1 rows prefetched ahead.
+__device__ __forceinline__ void dt_wave_sync() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
 #ifdef MCS_STAMPS
 // the probe build's dt_step segment times (s_memrealtime, 100 MHz), summed over clusters and ticks:
 // 0 state in + LDS copies, 1 releases, 2 arrivals, 3 Level1 pass, 4 Level0 head, 5 copies out +
@@ -39,6 +47,9 @@ __device__ unsigned long long g_dt_stamps[8];
 // kernel of the tick ([0-6] segments, [7] the whole step); [8] the trader kernel's own time, [9] ticks
 __device__ unsigned long long g_dt_cur[8];
 __device__ unsigned long long g_dt_maxsum[10];
+// inside the Level1 pass, summed over every row of every pass: [0] the fit tests and placements,
+// [1] the WaitTime and compaction bookkeeping, [2] rows, [3] placements
+__device__ unsigned long long g_dt_rows[4];
 #define DT_MARK(i)                                  \
     do {                                            \
         const uint64_t dt_now = wall_clock64();     \
@@ -174,6 +185,20 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
     const uint32_t S = a.S;
     DtCluster st = a.cl[c];
     const uint32_t NN = N + st.nv;
+    // the Level1 pass's first rows, in flight from here (their latency overlaps the copies, the
+    // releases and the arrivals); loaded whenever Level1 holds jobs, used when a pass runs
+    constexpr int kL1Ahead = 4;
+    unsigned long long pcm[kL1Ahead], pjd[kL1Ahead], pal[kL1Ahead];
+    {
+        const uint32_t n1 = st.l1n;
+#pragma unroll
+        for (int r = 0; r < kL1Ahead; ++r) {
+            const uint32_t p = (uint32_t)r * kWave + lane;
+            pcm[r] = p < n1 ? l1cm[p] : 0ull;
+            pjd[r] = p < n1 ? l1jd[p] : 0ull;
+            pal[r] = p < n1 ? l1al[p] : 0ull;
+        }
+    }
 
     copy_rounds<4>(nodes, a.tn + n0, N, lane);
     copy_rounds<2>(nodes + N, a.vn + (size_t)c * a.V, NN - N, lane);
@@ -253,7 +278,7 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             a.snode[sb + slot] = k;
             a.scm[sb + slot] = need;
         }
-        __syncthreads();
+        dt_wave_sync();
         ++st.nrun;
         st.peak = st.nrun > st.peak ? st.nrun : st.peak;
         st.minf = fin < st.minf ? fin : st.minf;
@@ -291,11 +316,15 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             }
         }
         // per lane: the lowest node (physical, then virtual) that fits this lane's entry
+        // (the node values come from one LDS read per lane, node i in lane i, then readlanes: no
+        // chain of dependent LDS reads per entry test; called with every lane active)
         auto lane_fit = [&](uint32_t c_l, uint32_t m_l) -> uint32_t {
+            const unsigned long long nv = lane < NN ? nodes[lane] : 0ull;
+            const uint32_t nc = (uint32_t)nv, nm = (uint32_t)(nv >> 32);
             uint32_t kl = kEmpty;
             for (uint32_t i = NN; i-- > 0u;) {
-                const unsigned long long v = nodes[i];
-                kl = ((uint32_t)v >= c_l && (uint32_t)(v >> 32) >= m_l) ? i : kl;
+                const uint32_t vc = readlane(nc, i), vm = readlane(nm, i);
+                kl = (vc >= c_l && vm >= m_l) ? i : kl;
             }
             return kl;
         };
@@ -306,30 +335,26 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         // reduced once after the sweep (a wave reduction per row would serialise the pass)
         long long tot_l = 0ll;
         unsigned long long snew_l = 0ull;
-        // rows of 64 entries, each row's three coalesced loads issued one row ahead
-        unsigned long long ncm = 0, njd = 0, nal = 0;
-        if (lane < n1) {
-            ncm = l1cm[lane];
-            njd = l1jd[lane];
-            nal = l1al[lane];
-        }
-        for (uint32_t base = 0; base < n1; base += kWave) {
+        // rows of 64 entries; each row's three coalesced loads are issued kL1Ahead rows ahead (the
+        // first ones before the pass), so a row's HBM latency hides behind the rows before it
+        // (compaction writes only at or below the row in hand: never into a prefetched row)
+        // one row of the pass; false: a slot overflow (the run stops, the engine re-runs bigger)
+        auto row = [&](const uint32_t base, const unsigned long long cm, const unsigned long long jdv,
+                       const unsigned long long al) -> bool {
             const uint32_t pos = base + lane;
             const bool live = pos < n1;
-            const unsigned long long cm = ncm, jdv = njd, al = nal;
-            if (pos + kWave < n1) {
-                ncm = l1cm[pos + kWave];
-                njd = l1jd[pos + kWave];
-                nal = l1al[pos + kWave];
-            }
+#ifdef MCS_STAMPS
+            const uint64_t rt0 = wall_clock64();
+#endif
             const uint32_t jc_l = (uint32_t)cm, jm_l = (uint32_t)(cm >> 32);
             unsigned long long placedm = 0ull, skipm = carry_skip ? 1ull : 0ull;
             bool overflow = false;
             if (exact) {
                 uint32_t from = 0;
                 for (;;) {  // the next entry in list order that fits now and is not skipped
-                    __syncthreads();
-                    const uint32_t kl = live ? lane_fit(jc_l, jm_l) : kEmpty;
+                    dt_wave_sync();
+                    const uint32_t kf = lane_fit(jc_l, jm_l);  // (all lanes: it reads across lanes)
+                    const uint32_t kl = live ? kf : kEmpty;
                     const unsigned long long fitm = __ballot(kl != kEmpty) & ~skipm &
                                                     (from < 64u ? (~0ull << from) : 0ull);
                     if (!fitm) break;
@@ -383,8 +408,11 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             if (overflow) {
                 st.flags |= MCS_FLAG_OVERFLOW;
                 wr = n1;  // state is abandoned (the engine re-runs with more slots)
-                break;
+                return false;
             }
+#ifdef MCS_STAMPS
+            const uint64_t rt1 = wall_clock64();
+#endif
             const unsigned long long livem = __ballot(live);
             const uint32_t last = 63u - (uint32_t)__builtin_clzll(livem);
             carry_skip = ((placedm >> last) & 1ull) != 0ull && last == 63u;
@@ -411,6 +439,31 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             }
             snew_l += live && !placed ? (unsigned long long)nl : 0ull;
             wr += (uint32_t)__builtin_popcountll(kept);
+#ifdef MCS_STAMPS
+            if (lane == 0) {
+                atomicAdd(&g_dt_rows[0], (unsigned long long)(rt1 - rt0));
+                atomicAdd(&g_dt_rows[1], (unsigned long long)(wall_clock64() - rt1));
+                atomicAdd(&g_dt_rows[2], 1ull);
+                atomicAdd(&g_dt_rows[3], (unsigned long long)__builtin_popcountll(placedm));
+            }
+#endif
+            return true;
+        };
+        bool ok_pass = true;
+        for (uint32_t base0 = 0; base0 < n1 && ok_pass; base0 += kL1Ahead * kWave) {
+#pragma unroll
+            for (int r = 0; r < kL1Ahead; ++r) {
+                const uint32_t base = base0 + (uint32_t)r * kWave;
+                if (!ok_pass || base >= n1) break;
+                const unsigned long long cm = pcm[r], jdv = pjd[r], al = pal[r];
+                const uint32_t nx = base + kL1Ahead * kWave + lane;
+                if (nx < n1) {
+                    pcm[r] = l1cm[nx];
+                    pjd[r] = l1jd[nx];
+                    pal[r] = l1al[nx];
+                }
+                ok_pass = row(base, cm, jdv, al);
+            }
         }
         st.l1n = wr;
         st.total += dt_wave_sum_i64(tot_l);
@@ -915,6 +968,12 @@ extern "C" int mcs_debug_dt_stamps(unsigned long long* out) {
     unsigned long long z[8] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_dt_stamps), sizeof(z)) != hipSuccess) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_dt_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+// the Level1 pass's row split (see g_dt_rows), read and cleared
+extern "C" int mcs_debug_dt_rows(unsigned long long* out) {
+    unsigned long long z[4] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_dt_rows), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_dt_rows), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 // the per-tick maxima summed over ticks and the trader kernel's time (see g_dt_maxsum), read and cleared
 extern "C" int mcs_debug_dt_maxsum(unsigned long long* out) {

@@ -22,13 +22,15 @@ eng.load_clusters(replicate(spec, 64))
 eng.generate_jobs(GenParams(seed=0x4D43535F53494D31), J)
 fn = L.lib().mcs_debug_dt_stamps
 fm = L.lib().mcs_debug_dt_maxsum
+fr = L.lib().mcs_debug_dt_rows
 buf = (C.c_ulonglong * 8)()
 mx = (C.c_ulonglong * 10)()
-eng.run(); fn(buf); fm(mx)
-st = eng.run(); assert fn(buf) == 0 and fm(mx) == 0
+rw = (C.c_ulonglong * 4)()
+eng.run(); fn(buf); fm(mx); fr(rw)
+st = eng.run(); assert fn(buf) == 0 and fm(mx) == 0 and fr(rw) == 0
 ts = eng.trade_stats()
 print(json.dumps({"ms": st.kernel_ms, "ticks": int(ts["ticks"]), "loop_form": int(ts["loop_form"]), "s": list(buf),
-                  "mx": list(mx)}))
+                  "mx": list(mx), "rw": list(rw)}))
 '''
 SEG = ["state_in+lds_copies", "releases", "arrivals", "level1_pass", "level0_head", "copies_out+sample",
        "record+snapshot+contracts"]
@@ -52,6 +54,11 @@ def main():
     res["per_tick_slowest_cluster_us"] = {SEG[i]: round(mx[i] * 10.0 / 1e3 / nt, 3) for i in range(7)}
     res["per_tick_slowest_step_us"] = round(mx[7] * 10.0 / 1e3 / nt, 3)
     res["per_tick_trader_kernel_us"] = round(mx[8] * 10.0 / 1e3 / nt, 3)
+    rw = d["rw"]
+    nr = max(rw[2], 1)
+    res["level1_rows"] = {"rows": rw[2], "placements": rw[3], "rows_per_tick": round(rw[2] / nt, 2),
+                          "us_per_row_tests_and_placements": round(rw[0] * 10.0 / 1e3 / nr, 4),
+                          "us_per_row_bookkeeping": round(rw[1] * 10.0 / 1e3 / nr, 4)}
     print(json.dumps(res, indent=1))
 
 
