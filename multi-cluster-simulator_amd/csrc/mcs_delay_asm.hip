@@ -79,9 +79,17 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
 // probe counters of the counting build (MCS_FIFO_DIAG=1; printed by the engine with
 // MCS_DELAY_PROBE=1): lane k of v119 counts event k (0 passes run, 1 passes skipped (nothing grew,
 // nothing untested), 2 rows, 3 candidates, 4 candidates whose first fit failed, 5 G nodes, 6 D6
-// skips, 7 compactions, 8 mode-1 iterations)
+// skips, 7 compactions, 8 mode-1 iterations; 9-11 cycle sums, below)
 #define MCS_FD_P_D0(k) ""
 #define MCS_FD_P_D1(k) "s_mov_b64 exec, 1<<" #k "\n\tv_add_u32 v119, 1, v119\n\ts_mov_b64 exec, -1\n\t"
+// cycle stamps of the counting build (s_memtime, low 32 bits of the delta, summed in v119 lanes
+// 9 passes, 10 the whole loop, 11 releases): TS starts the pair R, TE(R, k) adds now - R to lane k
+#define MCS_FD_TS_D0(R) ""
+#define MCS_FD_TS_D1(R) "s_memtime s[" #R ":" #R "+1]\n\ts_waitcnt lgkmcnt(0)\n\t"
+#define MCS_FD_TE_D0(R, k) ""
+#define MCS_FD_TE_D1(R, k)                                                                        \
+    "s_memtime s[38:39]\n\ts_waitcnt lgkmcnt(0)\n\ts_sub_u32 s38, s38, s" #R "\n\t"              \
+    "s_mov_b64 exec, 1<<" #k "\n\tv_add_u32 v119, s38, v119\n\ts_mov_b64 exec, -1\n\t"
 #define MCS_FD_PG_D0 ""
 #define MCS_FD_PG_D1 "s_mov_b64 exec, 1<<5\n\tv_add_u32 v119, s46, v119\n\ts_mov_b64 exec, -1\n\t"
 // (a skipped pass: straight to the Level0 head, or through its counter)
@@ -232,7 +240,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "s_cbranch_scc0 mcsfd_rows_%=\n\t"                                                            \
     "v_readlane_b32 s46, v95, s47\n\t" /* nothing grew after all: the head's duration back */   \
     "s_branch " MCS_FD_PSK_##D "\n"                                                              \
-    "mcsfd_rows_%=:\n\t" MCS_FD_P_##D(0) MCS_FD_PG_##D                                            \
+    "mcsfd_rows_%=:\n\t" MCS_FD_P_##D(0) MCS_FD_PG_##D MCS_FD_TS_##D(36)                         \
     "s_mov_b32 s93, 0\n\t"                                                                        \
     "s_mov_b32 s94, 0\n\t"                                                                        \
     "s_mov_b32 s95, -1\n"                                                                         \
@@ -364,7 +372,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "v_mov_b32 v105, v64\n\t" /* the snapshot G is measured from at the next pass */             \
     "v_mov_b32 v106, v65\n\t"                                                                     \
     "v_mov_b32 v116, v66\n\t"                                                                     \
-    "v_mov_b32 v112, v67\n\t" MCS_FD_PSKB_##D
+    "v_mov_b32 v112, v67\n\t" MCS_FD_TE_##D(36, 9) MCS_FD_PSKB_##D
 
 #define MCS_FD_LOOP(D)                                                                            \
     /* ---- entry: state into the fixed registers ---- */                                        \
@@ -405,7 +413,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "v_mov_b32 v91, -1\n\t"                                                                       \
     "v_mov_b32 v119, 0\n\t"                                                                       \
     "v_add_u32 v88, 0x400, v108\n\t" /* Level1 (after the node copy) */                          \
-    MCS_FA_INIT16R MCS_FA_RELOAD16 "s_waitcnt lgkmcnt(0)\n\t"                                      \
+    MCS_FA_INIT16R MCS_FA_RELOAD16 "s_waitcnt lgkmcnt(0)\n\t" MCS_FD_TS_##D(34)                   \
     /* prefetch batch 1 */                                                                        \
     "v_lshlrev_b32 v121, 4, v110\n\t"                                                             \
     "v_add_u32 v121, 0x400, v121\n\t"                                                             \
@@ -418,7 +426,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     /* ======== mode 0: Level1 empty ======== */                                                 \
     "mcsfd_inner0_%=:\n\t" MCS_FA_CNTS_##D MCS_FD_HEAD(0, "")                                     \
     /* releases: shared by both modes, back to the mode's iteration */                           \
-    "mcsfd_rel_%=:\n\t" MCS_FA_CNTR_##D                                                           \
+    "mcsfd_rel_%=:\n\t" MCS_FA_CNTR_##D MCS_FD_TS_##D(36)                                         \
     "s_max_u32 s81, s81, s80\n\t" /* peak: used only grows between releases */                   \
     "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN16R                                                    \
     "v_mov_b32 v120, v90\n\t"                                                                     \
@@ -437,7 +445,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "v_min_u32_dpp v120, v120, v120 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"                  \
     "s_nop 1\n\t"                                                                                 \
     "v_readlane_b32 s77, v120, 63\n\t"                                                            \
-    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
+    "s_waitcnt lgkmcnt(0)\n\t" MCS_FD_TE_##D(36, 11)                                              \
     "s_cmp_lg_u32 s92, 0\n\t"                                                                     \
     "s_cbranch_scc1 mcsfd_inner1_%=\n\t"                                                          \
     "s_branch mcsfd_inner0_%=\n" MCS_FD_ZERO(0)                                                   \
@@ -587,7 +595,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "s_or_b32 s44, s44, %[fov]\n\t"                                                               \
                                                                                                   \
     /* ---- exit: state back to the compiler's registers ---- */                                 \
-    "mcsfd_exit_%=:\n\t"                                                                          \
+    "mcsfd_exit_%=:\n\t" MCS_FD_TE_##D(34, 10)                                                  \
     "s_waitcnt vmcnt(0) lgkmcnt(0)\n\t"                                                           \
     "s_mov_b64 exec, 1\n\t" /* the Level1 waits join lane 0's sum */                            \
     "v_mov_b32 v104, s101\n\t"                                                                    \
@@ -674,7 +682,7 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
       [cap] "i"(kL1Cap), [cap4] "i"(kL1Cap * 4), [cap8] "i"(kL1Cap * 8)                          \
     : MCS_FA_CLOBBERS, "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99", "s100", "s101",    \
       "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v88", "v102", "v103", "v104",     \
-      "v105", "v106", "v116", "v119"
+      "v105", "v106", "v116", "v119", "s34", "s35", "s36", "s37", "s38", "s39"
     if constexpr (DIAG) asm volatile(MCS_FD_LOOP(D1) MCS_FD_OPERANDS);
     else asm volatile(MCS_FD_LOOP(D0) MCS_FD_OPERANDS);
 #undef MCS_FD_OPERANDS
@@ -684,7 +692,7 @@ __global__ __launch_bounds__(64) void delay_asm_kernel(DelayArgs a) {
     static_assert(4 * kWave * 4 == 0x400, "LDS layout: Level1 after the node copy (v88)");
 
     // the counting build's probe counters: into the cluster's (otherwise unused) HBM Level1 scratch
-    if (DIAG && lane < 9u && 2u * J > lane) reinterpret_cast<uint32_t*>(a.l1_cm + j0)[lane] = prb;
+    if (DIAG && lane < 12u && 2u * J > lane) reinterpret_cast<uint32_t*>(a.l1_cm + j0)[lane] = prb;
     // a pool overflow inside Level1's last stretch (no batch end to catch it): re-run
     if (peak > 64u * 8u) flags |= MCS_FLAG_OVERFLOW;
     const bool bail = (flags & kDelayBail) != 0u;

@@ -625,17 +625,18 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
             /* the DELAY loop's probe counters (its counting build wrote 9 per cluster into the
              * start of the cluster's Level1 scratch; clusters handed over are included up to the
              * hand-over): summed over the clusters, one line on stderr (tools only) */
-            unsigned long long sum[9] = {0};
-            std::vector<uint32_t> w(18);
+            unsigned long long sum[12] = {0};
+            std::vector<uint32_t> w(24);
             for (uint32_t c = 0; c < e->C; ++c) {
-                const uint64_t n = std::min<uint64_t>(9, 2 * (e->job_off[c + 1] - e->job_off[c]));
+                const uint64_t n = std::min<uint64_t>(12, 2 * (e->job_off[c + 1] - e->job_off[c]));
                 if (!n) continue;
                 HIPCHK(e, hipMemcpy(w.data(), e->d_l1_cm + e->job_off[c], n * 4, hipMemcpyDeviceToHost));
                 for (uint64_t k = 0; k < n; ++k) sum[k] += w[k];
             }
             fprintf(stderr, "MCS_DELAY_PROBE passes_run=%llu passes_skipped=%llu rows=%llu candidates=%llu "
-                            "failed_fits=%llu filter_builds=%llu d6_skips=%llu compactions=%llu mode1_iterations=%llu\n",
-                    sum[0], sum[1], sum[2], sum[3], sum[4], sum[5], sum[6], sum[7], sum[8]);
+                            "failed_fits=%llu grown_nodes=%llu d6_skips=%llu compactions=%llu mode1_iterations=%llu "
+                            "cycles_passes=%llu cycles_loop=%llu cycles_releases=%llu\n",
+                    sum[0], sum[1], sum[2], sum[3], sum[4], sum[5], sum[6], sum[7], sum[8], sum[9], sum[10], sum[11]);
         }
         const bool bailed = dasm && tot.bailed != 0;
         if (bailed) {
