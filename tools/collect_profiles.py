@@ -65,7 +65,24 @@ for g in sorted(glob.glob(f"{run}/pmc*_g*/pmc_counter_collection.csv")):
 summary["pmc_kernel"] = kernel
 summary["pmc_per_launch"] = counters
 
+
+def short_name(n):
+    """The engine's name for a rocprofv3 kernel name (mcs_last_kernel, bench.py's roofline.kernel): no
+    'void', no anonymous namespace, no parameter list, no trailing counting-build flag (', false')."""
+    n = n.replace("void ", "", 1).replace("(anonymous namespace)::", "")
+    n = n.split("(")[0]
+    return n.replace(", false>", ">").replace("<false>", "")
+
+
+summary["kernel_short"] = short_name(kernel)
+
 bench = None
+bench_file = f"{run}/bench.json" if os.path.exists(f"{run}/bench.json") else os.environ.get("MCS_BENCH_JSON")
+if bench_file and os.path.exists(bench_file):
+    with open(bench_file) as f:
+        bk = json.loads(f.read().strip().splitlines()[-1])["roofline"].get("kernel", "")
+    summary["bench_kernel"] = bk
+    summary["kernel_matches_bench"] = summary["kernel_short"] == bk
 if os.path.exists(f"{run}/bench.json"):
     shutil.copy(f"{run}/bench.json", f"{out}/bench.json")
     with open(f"{run}/bench.json") as f:
