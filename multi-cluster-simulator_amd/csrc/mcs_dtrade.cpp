@@ -32,6 +32,7 @@ struct DtradeDev {
     DtCluster* cl = nullptr;
     DtTrader* tr = nullptr;
     DtCtl* ctl = nullptr;
+    unsigned long long* l1snap = nullptr;
     mcs_contract_rec* trades = nullptr;
     mcs_foreign_rec* foreign = nullptr;
     unsigned char* xb = nullptr;  // world exchange blocks
@@ -89,6 +90,7 @@ int dtrade_alloc(mcs_engine* e) {
     HIPCHK(e, hipMemset(d->xb, 0, blk * e->world));
     HIPCHK(e, hipMalloc(&d->nv_all, Ct * 4));
     HIPCHK(e, hipMalloc(&d->ctl, sizeof(DtCtl)));
+    HIPCHK(e, hipMalloc(&d->l1snap, (size_t)C * W * 8));
     HIPCHK(e, hipMalloc(&d->trades, trade_cap * sizeof(mcs_contract_rec)));
     HIPCHK(e, hipMalloc(&d->foreign, foreign_cap * sizeof(mcs_foreign_rec)));
     HIPCHK(e, hipHostMalloc(&d->h_ctl, sizeof(DtCtl), hipHostMallocDefault));
@@ -133,6 +135,7 @@ int dtrade_alloc(mcs_engine* e) {
     a.cl = d->cl;
     a.tr = d->tr;
     a.ctl = d->ctl;
+    a.l1snap = d->l1snap;
     a.trade_log = d->trades;
     a.foreign_log = d->foreign;
     return MCS_OK;
@@ -312,6 +315,7 @@ void dtrade_free(mcs_engine* e) {
     dfree(d->cl);
     dfree(d->tr);
     dfree(d->ctl);
+    dfree(d->l1snap);
     dfree(d->trades);
     dfree(d->foreign);
     dfree(d->xb);

@@ -133,6 +133,7 @@ __global__ __launch_bounds__(64) void dt_init_kernel(DtArgs a) {
     sc = dt_wave_sum_u32(sc);
     sm = dt_wave_sum_u32(sm);
     for (uint32_t s = lane; s < a.S; s += kWave) a.sfin[(size_t)c * a.S + s] = kEmpty;
+    for (uint32_t i = lane; i < a.W; i += kWave) a.l1snap[(size_t)c * a.W + i] = 0ull;  // every node "grown"
     const uint64_t j0 = a.job_off[c], j1 = a.job_off[c + 1];
     for (uint64_t j = j0 + lane; j < j1; j += kWave) {
         a.out_node[j] = MCS_NODE_UNPLACED;
@@ -185,21 +186,13 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
     const uint32_t S = a.S;
     DtCluster st = a.cl[c];
     const uint32_t NN = N + st.nv;
-    // the Level1 pass's first rows, in flight from here (their latency overlaps the copies, the
-    // releases and the arrivals); loaded whenever Level1 holds jobs, used when a pass runs
-    constexpr int kL1Ahead = 4;
-    unsigned long long pcm[kL1Ahead], pjd[kL1Ahead], pal[kL1Ahead];
-    {
-        const uint32_t n1 = st.l1n;
-#pragma unroll
-        for (int r = 0; r < kL1Ahead; ++r) {
-            const uint32_t p = (uint32_t)r * kWave + lane;
-            pcm[r] = p < n1 ? l1cm[p] : 0ull;
-            pjd[r] = p < n1 ? l1jd[p] : 0ull;
-            pal[r] = p < n1 ? l1al[p] : 0ull;
-        }
-    }
-
+    const bool exact = NN <= (uint32_t)kWave;  // small clusters: per-lane exact first fit
+    // (exact clusters) the node values the Level1 jobs last failed against: taken at the end of each
+    // pass, lowered at each move to Level1; a job that failed every node can fit now only on a node
+    // that grew past it since (releases, new virtual nodes, wrapped counters), or if it was skipped
+    // (D6) and so never tested: the pass tests the others against the grown nodes only
+    unsigned long long snap_l = exact && lane < NN ? a.l1snap[(size_t)c * a.W + lane] : 0ull;
+    bool snap_dirty = false;
     copy_rounds<4>(nodes, a.tn + n0, N, lane);
     copy_rounds<2>(nodes + N, a.vn + (size_t)c * a.V, NN - N, lane);
     copy_rounds<8>(sfin, a.sfin + sb, S, lane);
@@ -243,6 +236,25 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         st.count += (long long)(st.next_arr - before);
     }
 
+    // the Level1 pass's first rows, in flight from here (vmcnt waits in issue order: a load issued
+    // before the copies, the releases or the arrivals would be drained by their waits)
+    constexpr int kL1Ahead = 4;
+    unsigned long long pcm[kL1Ahead], pjd[kL1Ahead], pal[kL1Ahead];
+    // (every lane loads, at an index clamped into the list: a load under a lane condition ends in a
+    // merge of old and new values that waits for it on the spot)
+    if (st.l1n != 0u) {
+        const uint32_t n1 = st.l1n;
+#pragma unroll
+        for (int r = 0; r < kL1Ahead; ++r) {
+            const uint32_t p = (uint32_t)r * kWave + lane, pi = p < n1 ? p : n1 - 1u;
+            pcm[r] = l1cm[pi];
+            pjd[r] = l1jd[pi];
+            pal[r] = l1al[pi];
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < kL1Ahead; ++r) pcm[r] = pjd[r] = pal[r] = 0ull;
+    }
     DT_MARK(2);
     // ScheduleJob (scheduler.go:127-139) over Cluster.Nodes: physical, then virtual
     auto first_fit = [&](uint32_t jc, uint32_t jm) -> uint32_t {
@@ -293,7 +305,6 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         st.s_last = (unsigned long long)st.l1n * T;
         st.t_all = T;
     } else if (st.l1n != 0u) {
-        const bool exact = NN <= (uint32_t)kWave;  // small clusters: per-lane exact first fit
         // bigger clusters: exact fit filter (see mcs_delay.hip): lane l holds the max free memory
         // over nodes with min(free cores, 63) >= l; conservative for wrapped counters
         uint32_t best = 0u, max_c = 0u;
@@ -328,6 +339,25 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             }
             return kl;
         };
+        // the grown nodes (exact clusters): more than 16 -> every job is tested on every node
+        unsigned long long gmask = 0ull;
+        if (exact) {
+            const unsigned long long cur = lane < NN ? nodes[lane] : 0ull;
+            gmask = __ballot(lane < NN && ((uint32_t)cur > (uint32_t)snap_l ||
+                                           (uint32_t)(cur >> 32) > (uint32_t)(snap_l >> 32)));
+        }
+        const bool g_all = __builtin_popcountll(gmask) > 16;
+        // does this lane's job fit some grown node (current values)?  (every lane active)
+        auto g_fit = [&](uint32_t c_l, uint32_t m_l) -> bool {
+            const unsigned long long nv = lane < NN ? nodes[lane] : 0ull;
+            const uint32_t nc = (uint32_t)nv, nm = (uint32_t)(nv >> 32);
+            bool f = false;
+            for (unsigned long long g = gmask; g; g &= g - 1ull) {
+                const uint32_t k = (uint32_t)__builtin_ctzll(g);
+                f = f || (readlane(nc, k) >= c_l && readlane(nm, k) >= m_l);
+            }
+            return f;
+        };
         uint32_t wr = 0;
         bool carry_skip = false;  // the last entry of the previous row was placed
         const uint32_t n1 = st.l1n, t_all = st.t_all;
@@ -350,18 +380,30 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             unsigned long long placedm = 0ull, skipm = carry_skip ? 1ull : 0ull;
             bool overflow = false;
             if (exact) {
+                const bool untested = ((uint32_t)jdv >> 31) != 0u;
                 uint32_t from = 0;
                 for (;;) {  // the next entry in list order that fits now and is not skipped
                     dt_wave_sync();
-                    const uint32_t kf = lane_fit(jc_l, jm_l);  // (all lanes: it reads across lanes)
-                    const uint32_t kl = live ? kf : kEmpty;
-                    const unsigned long long fitm = __ballot(kl != kEmpty) & ~skipm &
+                    // candidates: jobs that fit a grown node, and the untested (all lanes: the
+                    // tests read across lanes)
+                    bool cf;
+                    if (g_all) {
+                        cf = lane_fit(jc_l, jm_l) != kEmpty;
+                    } else {
+                        cf = g_fit(jc_l, jm_l) || untested;
+                    }
+                    const unsigned long long fitm = __ballot(live && cf) & ~skipm &
                                                     (from < 64u ? (~0ull << from) : 0ull);
                     if (!fitm) break;
                     const uint32_t b = (uint32_t)__builtin_ctzll(fitm);
-                    const uint32_t k = readlane(kl, b);
                     const uint32_t jc = readlane(jc_l, b), jm = readlane(jm_l, b);
-                    const uint32_t jd = readlane((uint32_t)(jdv >> 32), b), jj = readlane((uint32_t)jdv, b);
+                    const uint32_t k = first_fit(jc, jm);
+                    if (k == kEmpty) {  // an untested job that fits no node after all
+                        from = b + 1u;
+                        continue;
+                    }
+                    const uint32_t jd = readlane((uint32_t)(jdv >> 32), b),
+                                   jj = readlane((uint32_t)jdv, b) & 0x7FFFFFFFu;
                     const uint32_t fin = T + jd;
                     if (jd != 0u && !commit(k, jc, jm, fin)) {
                         overflow = true;
@@ -388,7 +430,8 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
                     const uint32_t jc = readlane(jc_l, b), jm = readlane(jm_l, b);
                     const uint32_t k = first_fit(jc, jm);
                     if (k == kEmpty) continue;
-                    const uint32_t jd = readlane((uint32_t)(jdv >> 32), b), jj = readlane((uint32_t)jdv, b);
+                    const uint32_t jd = readlane((uint32_t)(jdv >> 32), b),
+                                   jj = readlane((uint32_t)jdv, b) & 0x7FFFFFFFu;
                     const uint32_t fin = T + jd;
                     if (jd != 0u && !commit(k, jc, jm, fin)) {
                         overflow = true;
@@ -431,9 +474,14 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
                 const uint32_t np = wr + (uint32_t)__builtin_amdgcn_mbcnt_hi(
                                              (uint32_t)(kept >> 32),
                                              __builtin_amdgcn_mbcnt_lo((uint32_t)kept, 0u));
+                // the untested mark (bit 31 of the job word): set on a skipped job, cleared on an
+                // examined one
+                const unsigned long long jdn = examined ? (jdv & ~0x80000000ull) : (jdv | 0x80000000ull);
                 if (np != pos) {
                     l1cm[np] = cm;
-                    l1jd[np] = jdv;
+                    l1jd[np] = jdn;
+                } else if (jdn != jdv) {
+                    l1jd[np] = jdn;
                 }
                 if (np != pos || nl != sl) l1al[np] = (al & 0xFFFFFFFFull) | ((unsigned long long)nl << 32);
             }
@@ -456,12 +504,10 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
                 const uint32_t base = base0 + (uint32_t)r * kWave;
                 if (!ok_pass || base >= n1) break;
                 const unsigned long long cm = pcm[r], jdv = pjd[r], al = pal[r];
-                const uint32_t nx = base + kL1Ahead * kWave + lane;
-                if (nx < n1) {
-                    pcm[r] = l1cm[nx];
-                    pjd[r] = l1jd[nx];
-                    pal[r] = l1al[nx];
-                }
+                const uint32_t nx = base + kL1Ahead * kWave + lane, nxi = nx < n1 ? nx : n1 - 1u;
+                pcm[r] = l1cm[nxi];  // (unconditional: see the first rows' loads)
+                pjd[r] = l1jd[nxi];
+                pal[r] = l1al[nxi];
                 ok_pass = row(base, cm, jdv, al);
             }
         }
@@ -469,6 +515,10 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         st.total += dt_wave_sum_i64(tot_l);
         st.s_last = (unsigned long long)dt_wave_sum_i64((long long)snew_l);
         st.l1_dirty = wr != n1 ? 1u : 0u;  // a pass that placed: its skipped entries come next
+        if (exact) {  // the jobs left failed every node as they are now
+            snap_l = lane < NN ? nodes[lane] : 0ull;
+            snap_dirty = true;
+        }
     }
 
     DT_MARK(3);
@@ -505,11 +555,20 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             st.s_last += T;
             ++st.l0_head;
             ++st.moved;
+            if (exact) {  // it failed every node as they are now: the snapshot may not exceed them
+                const unsigned long long cur = lane < NN ? nodes[lane] : 0ull;
+                const uint32_t lo = (uint32_t)cur < (uint32_t)snap_l ? (uint32_t)cur : (uint32_t)snap_l;
+                const uint32_t hi = (uint32_t)(cur >> 32) < (uint32_t)(snap_l >> 32) ? (uint32_t)(cur >> 32)
+                                                                                     : (uint32_t)(snap_l >> 32);
+                snap_l = (unsigned long long)lo | ((unsigned long long)hi << 32);
+                snap_dirty = true;
+            }
             st.head_last = kEmpty;
         }
     }
 
     DT_MARK(4);
+    if (snap_dirty && lane < NN) a.l1snap[(size_t)c * a.W + lane] = snap_l;
     __syncthreads();
     copy_rounds<4>(a.tn + n0, nodes, N, lane);
     copy_rounds<2>(a.vn + (size_t)c * a.V, nodes + N, NN - N, lane);

@@ -122,6 +122,7 @@ struct DtArgs {
     DtCluster* cl;
     DtTrader* tr;  // Ct entries, replicated
     DtCtl* ctl;
+    unsigned long long* l1snap;  // [C][W] node values the Level1 jobs last failed against (dt_step)
     mcs_contract_rec* trade_log;
     mcs_foreign_rec* foreign_log;
 };
