@@ -497,18 +497,73 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
 #endif
             return true;
         };
+        // a quiet row: no job of it fits now (none fits a grown node, none is untested) and its first
+        // job is examined (no skip carried in): only the WaitTime and compaction bookkeeping, as the
+        // general row does it with nothing placed (the live jobs are a prefix: rank = lane)
+        auto quiet_row = [&](const uint32_t base, const unsigned long long cm, const unsigned long long jdv,
+                             const unsigned long long al, const uint32_t wr0) {
+            const uint32_t pos = base + lane;
+            const bool live = pos < n1;
+            const uint32_t sl = (uint32_t)(al >> 32);
+            const uint32_t eff = sl > t_all ? sl : t_all;
+            tot_l += live ? (long long)(T - eff) * 1000ll : 0ll;
+            snew_l += live ? (unsigned long long)T : 0ull;
+            if (live) {
+                const uint32_t np = wr0 + lane;
+                const unsigned long long jdn = jdv & ~0x80000000ull;
+                if (np != pos) {
+                    l1cm[np] = cm;
+                    l1jd[np] = jdn;
+                } else if (jdn != jdv) {
+                    l1jd[np] = jdn;
+                }
+                if (np != pos || T != sl) l1al[np] = (al & 0xFFFFFFFFull) | ((unsigned long long)T << 32);
+            }
+        };
+        // is the row quiet?  (every lane active: the test reads across lanes)
+        auto is_quiet = [&](const uint32_t base, const unsigned long long cm, const unsigned long long jdv) -> bool {
+            const bool live = base + lane < n1;
+            const bool f = g_fit((uint32_t)cm, (uint32_t)(cm >> 32)) || ((uint32_t)jdv >> 31) != 0u;
+            return __ballot(live && f) == 0ull;
+        };
+        const bool quiet_ok = exact && !g_all;
         bool ok_pass = true;
+        // rows in pairs: two quiet rows are tested and booked together (independent instruction
+        // streams for the one wave of the CU); a row with a candidate, or with a skip carried into
+        // it, goes through row()  (r04: 19.2 -> 17.1 us per C5-DELAY tick; testing and booking a
+        // whole group of four first measured 17.6)
         for (uint32_t base0 = 0; base0 < n1 && ok_pass; base0 += kL1Ahead * kWave) {
 #pragma unroll
-            for (int r = 0; r < kL1Ahead; ++r) {
-                const uint32_t base = base0 + (uint32_t)r * kWave;
-                if (!ok_pass || base >= n1) break;
-                const unsigned long long cm = pcm[r], jdv = pjd[r], al = pal[r];
-                const uint32_t nx = base + kL1Ahead * kWave + lane, nxi = nx < n1 ? nx : n1 - 1u;
-                pcm[r] = l1cm[nxi];  // (unconditional: see the first rows' loads)
-                pjd[r] = l1jd[nxi];
-                pal[r] = l1al[nxi];
-                ok_pass = row(base, cm, jdv, al);
+            for (int r = 0; r < kL1Ahead; r += 2) {
+                const uint32_t ba = base0 + (uint32_t)r * kWave, bb = ba + kWave;
+                if (!ok_pass || ba >= n1) break;
+                const unsigned long long cma = pcm[r], jda = pjd[r], ala = pal[r];
+                const unsigned long long cmb = pcm[r + 1], jdb = pjd[r + 1], alb = pal[r + 1];
+                const uint32_t nxa = ba + kL1Ahead * kWave + lane, nxb = nxa + kWave;
+                const uint32_t nia = nxa < n1 ? nxa : n1 - 1u, nib = nxb < n1 ? nxb : n1 - 1u;
+                pcm[r] = l1cm[nia];  // (unconditional: see the first rows' loads)
+                pjd[r] = l1jd[nia];
+                pal[r] = l1al[nia];
+                pcm[r + 1] = l1cm[nib];
+                pjd[r + 1] = l1jd[nib];
+                pal[r + 1] = l1al[nib];
+                const bool has_b = bb < n1;
+                bool qa = false, qb = false;
+                if (quiet_ok && !carry_skip) {
+                    qa = is_quiet(ba, cma, jda);
+                    qb = has_b && is_quiet(bb, cmb, jdb);
+                }
+                if (qa) {
+                    const uint32_t ka = n1 - ba < (uint32_t)kWave ? n1 - ba : (uint32_t)kWave;
+                    quiet_row(ba, cma, jda, ala, wr);
+                    if (qb) quiet_row(bb, cmb, jdb, alb, wr + ka);
+                    wr += ka;
+                    if (qb) wr += n1 - bb < (uint32_t)kWave ? n1 - bb : (uint32_t)kWave;
+                    else if (has_b) ok_pass = row(bb, cmb, jdb, alb);
+                } else {
+                    ok_pass = row(ba, cma, jda, ala);
+                    if (ok_pass && has_b) ok_pass = row(bb, cmb, jdb, alb);
+                }
             }
         }
         st.l1n = wr;
