@@ -348,9 +348,10 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         }
         const bool g_all = __builtin_popcountll(gmask) > 16;
         // does this lane's job fit some grown node (current values)?  (every lane active)
+        // (the node values in a register for the pass, node i in lane i; refreshed after a commit)
+        unsigned long long nvv = exact && lane < NN ? nodes[lane] : 0ull;
         auto g_fit = [&](uint32_t c_l, uint32_t m_l) -> bool {
-            const unsigned long long nv = lane < NN ? nodes[lane] : 0ull;
-            const uint32_t nc = (uint32_t)nv, nm = (uint32_t)(nv >> 32);
+            const uint32_t nc = (uint32_t)nvv, nm = (uint32_t)(nvv >> 32);
             bool f = false;
             for (unsigned long long g = gmask; g; g &= g - 1ull) {
                 const uint32_t k = (uint32_t)__builtin_ctzll(g);
@@ -409,6 +410,7 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
                         overflow = true;
                         break;
                     }
+                    if (jd != 0u) nvv = lane < NN ? nodes[lane] : 0ull;  // (node k shrank)
                     if (lane == 0) {
                         a.out_node[j0 + jj] = (int32_t)k;
                         a.out_start[j0 + jj] = T;
