@@ -206,7 +206,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
         if (xcd) put_granule_xcd(g, tag, v);
         else put_granule(g, tag, v);
     };
-    unsigned long long* const gx1 = gx;  // [C][kX1Words] (room for 64 clusters)
+    unsigned long long* const gx1 = gx;  // [kX1Words][64]: word w of cluster g at w * 64 + g (r04)
     unsigned long long* const gx2 = gx + (size_t)kTrResMaxClusters * kX1Words;  // [C] lender words, [nwg][2]
 
     // ---- state in ----
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             xv = lane == 7 ? (uint32_t)MST(flags) : xv;
             xv = lane == 8 ? (uint32_t)MST(cu) : xv;
             xv = lane == 9 ? (uint32_t)MST(mu) : xv;
-            if (lane < kX1Words) put(gx1 + (size_t)c * kX1Words + lane, tag1, xv);
+            if (lane < kX1Words) put(gx1 + (size_t)lane * kTrResMaxClusters + c, tag1, xv);
             MW_TLOG(it, wave, wall_clock64());
             if (lane < kStWords) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stv;
             // the next tick's records (only phase A moves these cursors; a WaitQueue head that C/D
@@ -588,8 +588,12 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
 
         // ---- X1: every cluster's record (one wave sweeps, the others wait at the barrier) ----
         if (wave == 0) {
-            const uint32_t nw = C * kX1Words;
-            constexpr int kPer = (int)(kTrResMaxClusters * kX1Words / kWave);  // granules per lane
+            // word-major granules: lane g sweeps cluster g's ten words (granule k * 64 + g), and stores
+            // word k of it at rq_job + k * 64 + g: consecutive LDS words, no division, no bank
+            // conflict (record-major, lane i held word i % 10 of cluster i / 10: up to ten lanes of
+            // one store on one bank)
+            static_assert(kTrResMaxClusters == (uint32_t)kWave, "one lane per cluster in the X1 sweep");
+            constexpr int kPer = (int)kX1Words;  // granules per lane
             uint32_t xv[kPer];
             unsigned long long xg[kPer];
             for (uint32_t spins = 0;; ++spins) {
@@ -600,8 +604,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                     xg[k] = __hip_atomic_load(gx1 + lane + (uint32_t)k * kWave, __ATOMIC_RELAXED, MW_LOAD_SCOPE);
 #pragma unroll
                 for (int k = 0; k < kPer; ++k) {
-                    const uint32_t i = lane + (uint32_t)k * kWave;
-                    ok = ok && (i >= nw || (uint32_t)(xg[k] >> 32) == tag1);
+                    ok = ok && (lane >= C || (uint32_t)(xg[k] >> 32) == tag1);
                     xv[k] = (uint32_t)xg[k];
                 }
 #ifdef MCS_STAMPS
@@ -615,16 +618,12 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                 }
             }
             MW_TLOG(it, 2 * kMwWaves + 1, wall_clock64());
+            // the record's ten words land in ten consecutive [64]-arrays of MwShared (rq_job .. mu)
+            // (r04: a switch on the word index here ran as a divergent chain, ~8 us of the tick)
+            if (lane < C) {
 #pragma unroll
-            for (int k = 0; k < kPer; ++k) {
-                const uint32_t i = lane + (uint32_t)k * kWave;
-                if (i < nw) {
-                    // the record's ten words land in ten consecutive [64]-arrays of MwShared (rq_job
-                    // .. mu): one LDS store at word w's array, no per-word branch (a switch on the
-                    // lane-varying word index ran as a divergent chain, ~8 us of the tick)
-                    const uint32_t g = i / kX1Words, w = i - g * kX1Words;
-                    reinterpret_cast<uint32_t*>(sh.rq_job)[w * kTrResMaxClusters + g] = xv[k];
-                }
+                for (int k = 0; k < kPer; ++k)
+                    reinterpret_cast<uint32_t*>(sh.rq_job)[(uint32_t)k * kTrResMaxClusters + lane] = xv[k];
             }
             if (lane < 3) sh.accm[lane] = 0u;
             if (timed_out && lane == 0) sh.done = 2u;
