@@ -150,6 +150,7 @@ struct MwShared {  // (this workgroup's node vectors follow: kMwWaves * ns u64)
     uint32_t accm[3];  // borrowers some lender of this workgroup accepted this tick; [2]: an append overflowed
     uint32_t T, done, ticks, flags, xcd, tmax_now;
     unsigned long long n_trades, n_won, n_lent;
+    unsigned long long n_lent_next;  // C/D's lent-run count for the next tick (phase B still reads n_lent)
 };
 // X1 stores a record's word w at rq_job + w * 64: the ten arrays must stay consecutive, in word order
 static_assert(offsetof(MwShared, rq_c) == offsetof(MwShared, rq_job) + 1 * kTrResMaxClusters * 4 &&
@@ -662,6 +663,108 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             }
             lent_tick = (uint32_t)__builtin_popcountll(lm);
         }
+        // ---- phases C and D: wave 0 of every workgroup, one lane per cluster (C <= 64), while the
+        // other waves run phase B (r04: C/D needs X1 alone, and its writes are read only after the
+        // phase-B barrier; the lent-run count goes to n_lent_next, since phase B indexes by n_lent) ----
+        // They need nothing from phase B: every borrow request leaves its borrower busy (its WaitQueue
+        // head, or the lender's LentQueue when accepted) and not done, so the next tick's clock and
+        // the end of the run follow from X1 alone (queue bits: WaitQueue, ReadyQueue, LentQueue
+        // after A); the acceptances (X2: the workgroup's borrower masks and append-overflow bit) are
+        // published here and applied at the start of the next tick (x2_apply), while C/D runs
+        if (wave == 0) {
+            const uint32_t g = lane;
+            float cu = 0.0f, mu = 0.0f;
+            uint32_t tot_c = 0u, tot_m = 0u, busy = 0u, next_arr_t = kEmpty, done_g = 1u, fl = 0u;
+            TrTrader t{0u, 0u, 0u, kEmpty, 0u};
+            if (g < C && !timed_out) {
+                const uint32_t qs = sh.qs[g], has_w = qs & 1u, lq = (qs >> 3) & 1u, decided = sh.decided[g];
+                cu = sh.cu[g];
+                mu = sh.mu[g];
+                tot_c = sh.total_c[g];
+                tot_m = sh.total_m[g];
+                busy = (has_w || lq > 0u || (qs & 2u)) ? 1u : 0u;
+                next_arr_t = sh.next_arr_t[g];
+                done_g = (decided == sh.J[g] && lq == 0u) ? 1u : 0u;
+                fl = sh.xflags[g];
+                t = sh.trs[g];
+            }
+            unsigned long long n_trades = sh.n_trades, n_won = sh.n_won;
+            uint32_t lflags = 0;
+            if (a.trader && !timed_out) {
+                const bool due = g < C && t.next_due <= T;
+                const bool broken = cu > 0.8f || mu > 0.8f;  // Utilization (trader.go:127-130)
+                if (due && !broken) t.next_due = T + a.period;
+                // ApproveTrade of this lane as a responder: its sample is fixed for the tick
+                const bool appr = g < C && approve_trade_dev(tot_c, tot_m, cu, mu, 0u, 0u, 0u);
+                unsigned long long pend = __ballot(due && broken);
+                while (pend) {  // RequestPolicyMonitor of requester q (trader.go:282-324)
+                    const uint32_t q = (uint32_t)__builtin_ctzll(pend);
+                    pend &= pend - 1ull;
+                    bool app = false;
+                    if (g < C && g != q) {  // RequestResource, index order
+                        if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
+                        if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
+                            app = appr;
+                            t.lock_id = t.next_id++;  // set even when not approving (:44-46)
+                            t.lock_until = T + a.lock_s;
+                        }
+                    }
+                    const unsigned long long ab = __ballot(app);
+                    const uint32_t napp = (uint32_t)__builtin_popcountll(ab);
+                    const uint32_t winner = ab ? (uint32_t)__builtin_ctzll(ab) : kEmpty;
+                    if (winner != kEmpty) {
+                        if (g == winner) t.lock_id = 0u;  // ApproveContract unlocks (:83)
+                        if (g == q) t.vnodes += 1u;       // AddVirtualNode(0 cores, 0 memory)
+                        ++n_won;
+                    }
+                    if (g == q) t.next_due = T + (winner != kEmpty ? a.ok_sleep : a.fail_sleep) + a.period;
+                    if (lane == 0 && wg == 0) {  // (workgroup 0 keeps the log)
+                        if (n_trades < a.trade_cap) {
+                            mcs_trade_rec rec;
+                            rec.t_s = T;
+                            rec.requester = q;
+                            rec.winner = winner == kEmpty ? -1 : (int32_t)winner;
+                            rec.approvals = napp;
+                            a.trade_log[n_trades] = rec;
+                        }
+                    }
+                    if (n_trades >= a.trade_cap) lflags |= MCS_FLAG_LOG_OVERFLOW;
+                    ++n_trades;
+                }
+                if (g < C) sh.trs[g] = t;
+            }
+            // the next tick: T+1 while any queue is busy, else the next arrival or trader round
+            uint32_t nxt = next_arr_t;
+            if (a.trader && g < C) nxt = t.next_due < nxt ? t.next_due : nxt;
+            const bool done_all = !__ballot(!done_g);
+            const bool busy_any = __ballot(busy != 0u) != 0ull;
+            nxt = wave_min_u32(nxt);
+            for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o);
+            if (lane == 0) {
+                uint32_t flags = sh.flags | fl | lflags;
+                uint32_t done = 0, Tn = T;
+                const uint32_t fatal = MCS_FLAG_OVERFLOW | MCS_FLAG_LENT_OVERFLOW;
+                sh.tmax_now = 0u;
+                if (timed_out) {
+                    done = 2u;
+                } else if (done_all || (flags & fatal)) {
+                    done = 1u;
+                } else if (T >= a.t_max || (!busy_any && nxt == kEmpty)) {
+                    done = 1u;
+                    flags |= MCS_FLAG_T_MAX;
+                    sh.tmax_now = 1u;
+                } else {
+                    Tn = (busy_any || nxt <= T + 1u) ? T + 1u : nxt;
+                }
+                sh.T = Tn;
+                sh.done = done;
+                sh.ticks += 1u;
+                sh.n_lent_next = sh.n_lent + lent_tick;
+                sh.flags = flags;
+                sh.n_trades = n_trades;
+                sh.n_won = n_won;
+            }
+        }
         if (own) {
             const uint32_t L = c;
             uint32_t rqj = kEmpty, rqc = 0u, rqm = 0u, rqd = 0u;
@@ -760,111 +863,14 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
         MW_MARK(6);
         __syncthreads();
         MW_MARK(7);
-
-        // ---- phases C and D: wave 0 of every workgroup, one lane per cluster (C <= 64) ----
-        // They need nothing from phase B: every borrow request leaves its borrower busy (its WaitQueue
-        // head, or the lender's LentQueue when accepted) and not done, so the next tick's clock and
-        // the end of the run follow from X1 alone (queue bits: WaitQueue, ReadyQueue, LentQueue
-        // after A); the acceptances (X2: the workgroup's borrower masks and append-overflow bit) are
-        // published here and applied at the start of the next tick (x2_apply), while C/D runs
+        // X2: this workgroup's acceptances and append-overflow bit (applied at the next tick's start)
         if (wave == 0) {
             if (lane < 3) put(gx2 + 3u * wg + lane, tag2, sh.accm[lane]);
-            const uint32_t g = lane;
-            float cu = 0.0f, mu = 0.0f;
-            uint32_t tot_c = 0u, tot_m = 0u, busy = 0u, next_arr_t = kEmpty, done_g = 1u, fl = 0u;
-            TrTrader t{0u, 0u, 0u, kEmpty, 0u};
-            if (g < C && !timed_out) {
-                const uint32_t qs = sh.qs[g], has_w = qs & 1u, lq = (qs >> 3) & 1u, decided = sh.decided[g];
-                cu = sh.cu[g];
-                mu = sh.mu[g];
-                tot_c = sh.total_c[g];
-                tot_m = sh.total_m[g];
-                busy = (has_w || lq > 0u || (qs & 2u)) ? 1u : 0u;
-                next_arr_t = sh.next_arr_t[g];
-                done_g = (decided == sh.J[g] && lq == 0u) ? 1u : 0u;
-                fl = sh.xflags[g];
-                t = sh.trs[g];
-            }
-            unsigned long long n_trades = sh.n_trades, n_won = sh.n_won;
-            uint32_t lflags = 0;
-            if (a.trader && !timed_out) {
-                const bool due = g < C && t.next_due <= T;
-                const bool broken = cu > 0.8f || mu > 0.8f;  // Utilization (trader.go:127-130)
-                if (due && !broken) t.next_due = T + a.period;
-                // ApproveTrade of this lane as a responder: its sample is fixed for the tick
-                const bool appr = g < C && approve_trade_dev(tot_c, tot_m, cu, mu, 0u, 0u, 0u);
-                unsigned long long pend = __ballot(due && broken);
-                while (pend) {  // RequestPolicyMonitor of requester q (trader.go:282-324)
-                    const uint32_t q = (uint32_t)__builtin_ctzll(pend);
-                    pend &= pend - 1ull;
-                    bool app = false;
-                    if (g < C && g != q) {  // RequestResource, index order
-                        if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
-                        if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
-                            app = appr;
-                            t.lock_id = t.next_id++;  // set even when not approving (:44-46)
-                            t.lock_until = T + a.lock_s;
-                        }
-                    }
-                    const unsigned long long ab = __ballot(app);
-                    const uint32_t napp = (uint32_t)__builtin_popcountll(ab);
-                    const uint32_t winner = ab ? (uint32_t)__builtin_ctzll(ab) : kEmpty;
-                    if (winner != kEmpty) {
-                        if (g == winner) t.lock_id = 0u;  // ApproveContract unlocks (:83)
-                        if (g == q) t.vnodes += 1u;       // AddVirtualNode(0 cores, 0 memory)
-                        ++n_won;
-                    }
-                    if (g == q) t.next_due = T + (winner != kEmpty ? a.ok_sleep : a.fail_sleep) + a.period;
-                    if (lane == 0 && wg == 0) {  // (workgroup 0 keeps the log)
-                        if (n_trades < a.trade_cap) {
-                            mcs_trade_rec rec;
-                            rec.t_s = T;
-                            rec.requester = q;
-                            rec.winner = winner == kEmpty ? -1 : (int32_t)winner;
-                            rec.approvals = napp;
-                            a.trade_log[n_trades] = rec;
-                        }
-                    }
-                    if (n_trades >= a.trade_cap) lflags |= MCS_FLAG_LOG_OVERFLOW;
-                    ++n_trades;
-                }
-                if (g < C) sh.trs[g] = t;
-            }
-            // the next tick: T+1 while any queue is busy, else the next arrival or trader round
-            uint32_t nxt = next_arr_t;
-            if (a.trader && g < C) nxt = t.next_due < nxt ? t.next_due : nxt;
-            const bool done_all = !__ballot(!done_g);
-            const bool busy_any = __ballot(busy != 0u) != 0ull;
-            nxt = wave_min_u32(nxt);
-            for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o);
-            if (lane == 0) {
-                uint32_t flags = sh.flags | fl | lflags;
-                uint32_t done = 0, Tn = T;
-                const uint32_t fatal = MCS_FLAG_OVERFLOW | MCS_FLAG_LENT_OVERFLOW;
-                sh.tmax_now = 0u;
-                if (timed_out) {
-                    done = 2u;
-                } else if (done_all || (flags & fatal)) {
-                    done = 1u;
-                } else if (T >= a.t_max || (!busy_any && nxt == kEmpty)) {
-                    done = 1u;
-                    flags |= MCS_FLAG_T_MAX;
-                    sh.tmax_now = 1u;
-                } else {
-                    Tn = (busy_any || nxt <= T + 1u) ? T + 1u : nxt;
-                }
-                sh.T = Tn;
-                sh.done = done;
-                sh.ticks += 1u;
-                sh.n_lent += lent_tick;
-                sh.flags = flags;
-                sh.n_trades = n_trades;
-                sh.n_won = n_won;
-            }
+            if (lane == 0) sh.n_lent = sh.n_lent_next;
         }
+
         MW_MARK(8);
-        __syncthreads();
-        if (sh.done == 2u) break;
+        if (sh.done == 2u) break;  // (C/D wrote it before the phase-B barrier)
         pend = true;
         pend_tag = tag2;
         pend_T = T;
