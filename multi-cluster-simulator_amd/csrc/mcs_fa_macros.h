@@ -20,8 +20,14 @@
 //    uses it as the lane select                            written                             from s_add/s_mov)
 //  SALU writes M0 -> v_writelane with an M0 lane     1*    result writes at a Level0 decision  >= 1 other instruction between
 //    select (*not in the ISA table; kept anyway)           (HEAD, ZEROKX)                      (s_add s80 / s_ff1, s_lshl3_add)
+//                                                          DELAY G list (MCS_FD_ENUM: m0 =     s_add s86 between
+//                                                          cursor -> v_writelane v113/v118)
 //  VALU writes VGPR -> v_readlane / v_readfirstlane  1     DECIDE16R / ZEROKX read v86, v117;  >= 3 instructions between every
 //    reads it (gfx950)                                     REC16 after TAKE16; SCANEND v120     pair; SCANEND: s_nop 1
+//                                                          DELAY G pass (r04): v_cndmask v113  >= 6 (GTEST's scalar prologue)
+//                                                          -> GTEST's v_readlane v113; v123
+//                                                          (indexed move) -> v_readlane s74     >= 3 (s_set_gpr_idx_off, s_add,
+//                                                                                              s_cmp)
 //  VALU writes VCC -> s_cbranch_vccz/vccnz           0     ANYFIT -> the fit branch             (interlocked on gfx9; SALU
 //                                                                                              instructions between anyway)
 //  VALU writes EXEC -> DPP (5) / v_readlane (4)      5/4   none: exec is written by SALU only   (no v_cmpx in any loop)
