@@ -303,12 +303,15 @@ def delay_run_batch(arrays, streams, n_threads=1, max_wait_s=10):
     return node[:n], st[:n], fi[:n], stats[:k]
 
 
-def dtrade_run(arrays, streams, t_max=0xFFFFFFFE, trader=True, max_vnodes=64, period_s=10, trade_ok_sleep_s=240,
+def dtrade_run(arrays, streams, t_max=0xFFFFFFFE, trader=True, max_vnodes=256, period_s=10, trade_ok_sleep_s=240,
                trade_fail_sleep_s=120, lock_s=20, sample_period_s=5, max_wait_s=10, trade_cap=1 << 16,
                foreign_cap=1 << 20):
     """Lock-step DELAY clusters with traders (oracle/mcs_oracle_dtrade.c).  Returns a dict with node,
     start, finish, trades (DTRADE_DTYPE), foreign (FOREIGN_DTYPE), vnodes (list per cluster of (c, m)),
-    stats (DTRADE_STATS_DTYPE) and t_final."""
+    stats (DTRADE_STATS_DTYPE) and t_final.  max_vnodes bounds the oracle's arrays only (Go's
+    AddVirtualNode is unbounded): 256, the engine's own ceiling (kDtMaxVnodes, reached by escalation;
+    a system that needs more fails there with MCS_E_CAPACITY), so the two agree wherever the engine runs
+    (r04: at the old 64 the oracle silently dropped a 65th virtual node the engine kept)."""
     n = streams.n_jobs
     k = arrays.n_clusters
     node = np.empty(max(n, 1), np.int32)

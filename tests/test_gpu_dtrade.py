@@ -211,11 +211,15 @@ def test_gpu_approve_trade_sweep_vs_oracle(engine):
     assert 0.2 < got.mean() < 0.8  # both outcomes are exercised
 
 
-@pytest.mark.parametrize("shape,seed", [("w16s", 1), ("w16s", 2), ("mid", 3)])
-def test_gpu_dtrade_fuzz(shape, seed):
+@pytest.mark.parametrize("shape,seed,J", [("w16s", 1, 300), ("w16s", 2, 300), ("mid", 3, 300),
+                                          # (r04: longer streams through the grown-node pass: the
+                                          # snapshot, the untested marks across rows, quiet row pairs)
+                                          ("w16s", 4, 900), ("w16s", 5, 900), ("w16s", 6, 1500),
+                                          ("mid", 7, 900), ("mid", 8, 1500)])
+def test_gpu_dtrade_fuzz(shape, seed, J):
     """kat_util's randomised clusters and streams in a DELAY trading system (real contracts, Foreign
     jobs, virtual nodes): every output bit-exact against the oracle."""
-    arrays, streams = fuzz_workload(shape, seed, n_clusters=8, J=300, blocking=False)
+    arrays, streams = fuzz_workload(shape, seed, n_clusters=8, J=J, blocking=False)
     g = run(arrays, streams)
     o = O.dtrade_run(arrays, streams)
     bad = np.nonzero((g["node"] != o["node"]) | (g["start"] != o["start"]) | (g["finish"] != o["finish"]))[0]
