@@ -87,6 +87,8 @@ if os.path.exists(f"{run}/bench.json"):
     shutil.copy(f"{run}/bench.json", f"{out}/bench.json")
     with open(f"{run}/bench.json") as f:
         bench = json.loads(f.read().strip().splitlines()[-1])
+if bench and "placements_per_step_per_gpu" not in bench.get("config", {}):
+    bench = None  # (a trading line: no per-placement traffic; the raw counters stay in pmc_per_launch)
 if bench and "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
     jobs = bench["config"]["placements_per_step_per_gpu"]
     fetch = counters["FETCH_SIZE"] * 1024.0 * 2.0
