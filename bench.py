@@ -288,7 +288,7 @@ def main_c5_delay(args, world, rank, local_rank):
                                + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "graph-replayed after a resident timeout" if ts["loop_form"] == 6 else "RCCL eager" if ts["loop_form"] == 1
                                                     else "RCCL captured in a hipGraph" if ts["loop_form"] == 2
                                                     else "resident in one workgroup" if ts["loop_form"] == 3
-                                                    else "resident, one workgroup per 16 clusters"
+                                                    else "resident, one workgroup per 4 clusters"
                                                     + (", all on one XCD (L2 exchange)" if ts["loop_form"] == 5 else "")) + ")",
             },
             "roofline": {
@@ -404,7 +404,7 @@ def main_c5(args, world, rank, local_rank):
                                + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "graph-replayed after a resident timeout" if ts["loop_form"] == 6 else "RCCL eager" if ts["loop_form"] == 1
                                                     else "RCCL captured in a hipGraph" if ts["loop_form"] == 2
                                                     else "resident in one workgroup" if ts["loop_form"] == 3
-                                                    else "resident, one workgroup per 16 clusters"
+                                                    else "resident, one workgroup per 4 clusters"
                                                     + (", all on one XCD (L2 exchange)" if ts["loop_form"] == 5 else "")) + ")",
             },
             "roofline": {
@@ -417,7 +417,7 @@ def main_c5(args, world, rank, local_rank):
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": ("tr_mw_kernel (resident tick, one workgroup per 16 clusters)" if ts["loop_form"] in (4, 5) else
+                "kernel": ("tr_mw_kernel (resident tick, one workgroup per 4 clusters)" if ts["loop_form"] in (4, 5) else
                            "tr_resident_kernel (resident tick, one workgroup)" if ts["loop_form"] == 3 else
                            "lock-step tick (tr_step/tr_lend/tr_trader, one exchange), launch/latency-bound"),
                 "kernel_ms_avg": avg_kernel_s * 1e3,

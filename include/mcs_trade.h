@@ -94,7 +94,7 @@ typedef struct mcs_trade_stats {
                               all-gather per tick, eager launches; 2 = RCCL, kernels and all-gathers
                               captured in a hipGraph (MCS_RCCL_GRAPH=0 forces 1); 3 = one
                               engine, the whole system resident in one workgroup; 4 = resident,
-                              one workgroup per 16 clusters, exchange written through to memory;
+                              one workgroup per 4 clusters, exchange written through to memory;
                               5 = the same with every workgroup on one XCD, exchange in its L2;
                               6 = form 0 after a resident exchange timed out (workers not all
                               resident at once: the run was redone on the replayed kernels) */

@@ -191,7 +191,7 @@ uint32_t res_ticks() {
 }
 constexpr int kMwFallback = -100;  // run_local: a resident exchange timed out (trade_run re-runs)
 
-// MCS_TRADE_RESIDENT: 0 = the replayed kernels, 1 = one workgroup, 2 = one workgroup per 16
+// MCS_TRADE_RESIDENT: 0 = the replayed kernels, 1 = one workgroup, 2 = one workgroup per 4
 // clusters (the default where the shape allows it)
 int resident_form(mcs_engine* e, size_t* lds) {
     const char* env = getenv("MCS_TRADE_RESIDENT");

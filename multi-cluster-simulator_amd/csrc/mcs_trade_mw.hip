@@ -1,13 +1,13 @@
 // mcs_trade_mw.hip — the lock-step trading system (mcs_trade.h) resident in a few
 // workgroups that trade records through tagged granules: up to 64 clusters x 256 nodes, one
-// cluster per wave, 16 clusters per workgroup (one CU each), the whole run in one launch per
+// cluster per wave, 4 clusters per workgroup (one CU each), the whole run in one launch per
 // 64k ticks.
 //
 // The one-workgroup resident tick (mcs_trade_res.hip) holds all 64 clusters on ONE CU: four
 // clusters per wave, their slot rows copied into a working set and back around every step, and
 // the tick ran VALU-bound on that CU's four SIMDs (~24k VALU instructions per tick, PMC pass in
 // profiles/r03_res).  Here each wave owns one cluster (its slot finish times in registers, no
-// copies), so a tick's phase A runs on ceil(C / 16) CUs, and the workgroups meet twice per tick:
+// copies), so a tick's phase A runs on ceil(C / 4) CUs, and the workgroups meet twice per tick:
 //   A  each wave, its cluster: releases, arrivals, the Fifo decisions of the tick
 //      (scheduler.go:216-296), the borrow request (server.go:160-248), the utilization sample
 //      (cluster.go:46-63); it publishes the cluster's post-A record (10 words)
@@ -40,7 +40,15 @@
 namespace mcs {
 namespace {
 
-constexpr int kMwWaves = 16;             // clusters per workgroup
+// clusters (waves) per workgroup: 4, one wave per SIMD of the worker's CU (r04: 16 put four cluster
+// waves on each SIMD, and the last-issued of them published their records last; 4 -> 5.56, 8 -> 5.78,
+// 16 -> 6.59 us per C5 tick).  At most 64 / 3 workgroups (the X2 sweep's one granule per lane) and 32
+// (one XCD's CUs for the L2 exchange): with 64 clusters, 16.  (MCS_MW_WAVES: A/B builds.)
+#ifndef MCS_MW_WAVES
+#define MCS_MW_WAVES 4
+#endif
+constexpr int kMwWaves = MCS_MW_WAVES;
+static_assert(3 * ((int)kTrResMaxClusters / kMwWaves) <= kWave, "X2: one granule per lane");
 constexpr uint32_t kMwNodes = 256;       // nodes per cluster
 constexpr uint32_t kX1Words = 10;        // granules of a cluster's post-A record
 constexpr uint32_t kSpinLimit = 1u << 20;  // sweeps per exchange before the run gives up
@@ -79,7 +87,7 @@ __device__ __forceinline__ uint32_t xcc_id() {
 #ifdef MCS_STAMPS
 // the probe build's per-wave segment times (s_memrealtime, 100 MHz) summed over the launches since
 // the last read: [workgroup][wave][segment], segments as MW_MARK below
-constexpr int kMwSeg = 12, kMwMaxWg = 4;  // (10, 11: sweep passes of X1, X2)
+constexpr int kMwSeg = 12, kMwMaxWg = 64 / kMwWaves;  // (10, 11: sweep passes of X1, X2)
 __device__ unsigned long long g_mw_stamps[kMwMaxWg * kMwWaves * kMwSeg];
 // absolute times (s_memrealtime) of every 64th tick of the launch (up to kMwLogTicks of them), to split the X1 wait into
 // skew (the last record's publication after this wave's own) and propagation (the sweep's end after
@@ -952,13 +960,13 @@ hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsign
 }  // namespace mcs
 
 #ifdef MCS_STAMPS
-// the probe build's per-wave segment times (4 workgroups x 16 waves x 10 segments, 100 MHz ticks)
+// the probe build's per-wave segment times (kMwMaxWg workgroups x kMwWaves waves x segments, 100 MHz)
 extern "C" int mcs_debug_mw_stamps(unsigned long long* out) {
-    unsigned long long z[mcs::kMwMaxWg * mcs::kMwWaves * mcs::kMwSeg] = {};  // (768)
+    unsigned long long z[mcs::kMwMaxWg * mcs::kMwWaves * mcs::kMwSeg] = {};  // (64 waves x 12)
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_mw_stamps), sizeof(z)) != hipSuccess) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_mw_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
-// the last launch's absolute-time log ([1024 ticks][4 workgroups][35 slots], see g_mw_tlog)
+// the last launch's absolute-time log ([1024 ticks][kMwMaxWg][2 kMwWaves + 3 slots], see g_mw_tlog)
 extern "C" int mcs_debug_mw_tlog(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_mw_tlog), sizeof(mcs::g_mw_tlog)) == hipSuccess ? 0 : -1;
 }

@@ -209,7 +209,7 @@ def test_gpu_trade_fuzz(shape, seed):
 @pytest.mark.parametrize("kind,C,J,pool", [("n64_hot", 8, 1500, 0), ("n256", 16, 3000, 8), ("n256", 16, 3000, 0),
                                            ("small", 64, 1500, 0), ("n256", 40, 2000, 16), ("n64", 33, 2000, 4)])
 def test_gpu_trade_resident_equals_kernels_and_oracle(kind, C, J, pool, monkeypatch):
-    """The system resident on the GPU for the whole run, in its two forms — one workgroup per 16
+    """The system resident on the GPU for the whole run, in its two forms — one workgroup per 4
     clusters trading records as tagged granules (mcs_trade_mw.hip; loop_form 4, the default for one
     engine of <= 64 clusters of <= 256 nodes with 256/512/1024 slots) and all of it in one
     workgroup (mcs_trade_res.hip; MCS_TRADE_RESIDENT=1, loop_form 3) — == the graph-replayed tick
@@ -225,7 +225,8 @@ def test_gpu_trade_resident_equals_kernels_and_oracle(kind, C, J, pool, monkeypa
         res[mode] = gpu_trade(arrays, streams, slot_pool=pool)
     lf = {m: res[m]["tstats"]["loop_form"] for m in res}
     assert lf["2"] in (4, 5) and lf["1"] == 3 and lf["0"] == 0, lf
-    assert lf["2u"] == (5 if C <= 16 else 4), lf
+    # (one workgroup, necessarily on one XCD, when C fits the smallest workgroup the kernel is built with)
+    assert lf["2u"] == 5 if C <= 4 else lf["2u"] in (4, 5), lf
     for m in ("2", "2u", "1"):
         for k in ("node", "start", "finish"):
             np.testing.assert_array_equal(res[m][k], res["0"][k], err_msg=f"{k} mode {m}")
