@@ -19,18 +19,50 @@ import test_gpu_parity as TP  # noqa: E402
 import test_gpu_trade as TT  # noqa: E402
 from mcs_amd import Engine  # noqa: E402
 
+
+
+class _MonkeyPatch:
+    """The part of pytest's monkeypatch fixture the fuzz tests use (environment variables)."""
+
+    def __init__(self):
+        self.saved = {}
+
+    def setenv(self, k, v):
+        self.saved.setdefault(k, os.environ.get(k))
+        os.environ[k] = v
+
+    def delenv(self, k, raising=True):
+        self.saved.setdefault(k, os.environ.get(k))
+        os.environ.pop(k, None)
+
+    def undo(self):
+        for k, v in self.saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def fifo_fuzz(eng, shape, seed):
+    mp = _MonkeyPatch()
+    try:
+        TP.test_hand_scheduled_fuzz(eng, shape, seed, mp)
+    finally:
+        mp.undo()
+
+
 base, count = int(sys.argv[1]), int(sys.argv[2])
 fails, runs = [], 0
 t0 = time.time()
 with Engine(0) as eng, Engine(0, policy="DELAY") as deng:
     for seed in range(base, base + count):
-        cases = [(f"fifo/{s}", lambda s=s: TP.test_hand_scheduled_fuzz(eng, s, seed)) for s in ("w16s", "w16r", "w32")]
+        cases = [(f"fifo/{s}", lambda s=s: fifo_fuzz(eng, s, seed)) for s in ("w16s", "w16r", "duo", "w32")]
         cases += [(f"delay/{s}", lambda s=s: TD.test_gpu_delay_fuzz(deng, s, seed)) for s in ("w16s", "mid", "w16r", "w32")]
         cases += [(f"fused/{p}", lambda p=p: TF.test_fused_fuzz(p, seed)) for p in ("FIFO", "DELAY")]
         cases += [(f"online/{p}/{s}", lambda p=p, s=s: TO.test_online_fuzz_slices_equal_batch_and_oracle(p, s, seed))
                   for p in ("FIFO", "DELAY") for s in ("w16s", "w16r", "w32")]
         cases += [(f"trade/{s}", lambda s=s: TT.test_gpu_trade_fuzz(s, seed)) for s in ("w16s", "mid", "w16r")]
-        cases += [(f"dtrade/{s}", lambda s=s: TDT.test_gpu_dtrade_fuzz(s, seed)) for s in ("w16s", "mid")]
+        cases += [(f"dtrade/{s}", lambda s=s: TDT.test_gpu_dtrade_fuzz(s, seed, 600)) for s in ("w16s", "mid")]
         if os.environ.get("SWEEP_BIG"):  # FIFO 600 x 6000, DELAY 400 x 5000 jobs per case
             def big(shape, seed=seed):
                 arrays, st = TP.fuzz_workload(shape, seed, n_clusters=600, J=6000)
