@@ -551,7 +551,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "s_cmp_ge_u32 s76, s42\n\t"                                                                   \
     "s_cbranch_scc1 mcsfd_last_%=\n\t"                                                            \
     "s_waitcnt vmcnt(0)\n\t" MCS_FD_STORE                                                         \
-    "s_add_u32 s57, s57, 64\n\t" MCS_FA_TAKE16                                                    \
+    "s_add_u32 s57, s57, 64\n\t" MCS_FA_PRIO("mcsfd_") MCS_FA_TAKE16                              \
     "v_add_u32 v121, s57, v110\n\t"                                                               \
     "v_lshlrev_b32 v121, 4, v121\n\t"                                                             \
     "v_add_u32 v121, 0x400, v121\n\t"                                                             \

@@ -201,7 +201,7 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     "global_store_dword v125, v92, s[68:69] nt\n\t"                                               \
     "v_add_u32 v93, v92, v95\n\t" /* finish = start + the batch's duration column */            \
     "global_store_dword v125, v93, s[70:71] nt\n\t"                                               \
-    "s_add_u32 s57, s57, 64\n\t" MCS_FA_BENDTAIL_##F(W)
+    "s_add_u32 s57, s57, 64\n\t" MCS_FA_PRIO("mcsfa_") MCS_FA_BENDTAIL_##F(W)
 
 // streamed records: the prefetched batch becomes current, the next one is prefetched
 #define MCS_FA_BENDTAIL_S(W)                                                                      \
