@@ -41,26 +41,30 @@
 // A reorder that moves a consumer next to its producer in the table must add the s_nop.
 
 // progress-based wave priority at each batch end: the fewer of its jobs a wave has decided, the higher
-// its issue priority (s_setprio 3 below a quarter of J, 2 below a half, 1 below three quarters, else 0).
-// The waves sharing a SIMD then keep pace, instead of the oldest racing ahead under age-ordered issue and
-// the youngest finishing alone, latency-bound, after the others have left (r04 A/B: C4 FIFO 8.08 -> 7.25
-// ms, C4 DELAY 7.58 -> 6.80, Level1-heavy DELAY 29.6 -> 26.3; profiles/r04_prio_*).  s76 scratch; P
-// prefixes the labels.
+// its issue priority (s_setprio 3 while more than J/2 of the wave's jobs remain, 2 while more than J/4,
+// 1 while more than J/8, else 0).  The waves sharing a SIMD then keep pace, instead of the oldest racing
+// ahead under age-ordered issue and the youngest finishing alone, latency-bound, after the others have
+// left.  r04 A/B (profiles/r04_prio_*, r04_geo*): quarters of J against no priority, C4 FIFO 8.08 ->
+// 7.25 ms, C4 DELAY 7.58 -> 6.80, Level1-heavy DELAY 29.6 -> 26.3; these halving thresholds, which
+// tighten the pack towards the end, a further 7.28 -> 7.08 and 26.45 -> 26.02 (1/4, 1/8, 1/16 lost;
+// 1/2, 1/4, 1/16 tied).  s76 scratch (SCC from the subtraction: 0 remaining once the cursor passed J);
+// P prefixes the labels.
 #define MCS_FA_PRIO(P)                                                                            \
-    "s_lshl_b32 s76, s57, 2\n\t"                                                                  \
-    "s_cmp_lt_u32 s76, s42\n\t"                                                                   \
+    "s_sub_u32 s76, s42, s57\n\t"                                                                 \
+    "s_cselect_b32 s76, 0, s76\n\t"                                                               \
+    "s_lshl_b32 s76, s76, 1\n\t"                                                                  \
+    "s_cmp_gt_u32 s76, s42\n\t"                                                                   \
     "s_cbranch_scc0 " P "p2_%=\n\t"                                                              \
     "s_setprio 3\n\t"                                                                            \
     "s_branch " P "pe_%=\n"                                                                       \
     P "p2_%=:\n\t"                                                                               \
-    "s_lshr_b32 s76, s76, 1\n\t"                                                                  \
-    "s_cmp_lt_u32 s76, s42\n\t"                                                                   \
+    "s_lshl_b32 s76, s76, 1\n\t"                                                                  \
+    "s_cmp_gt_u32 s76, s42\n\t"                                                                   \
     "s_cbranch_scc0 " P "p1_%=\n\t"                                                              \
     "s_setprio 2\n\t"                                                                            \
     "s_branch " P "pe_%=\n"                                                                       \
     P "p1_%=:\n\t"                                                                               \
-    "s_sub_u32 s76, s42, s57\n\t"                                                                 \
-    "s_lshl_b32 s76, s76, 2\n\t"                                                                  \
+    "s_lshl_b32 s76, s76, 1\n\t"                                                                  \
     "s_cmp_gt_u32 s76, s42\n\t"                                                                   \
     "s_cbranch_scc0 " P "p0_%=\n\t"                                                              \
     "s_setprio 1\n\t"                                                                            \
