@@ -586,6 +586,7 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
     } while (h < rend);
     if (rend == 0u) break;
     cb += kWave;
+    wave_progress_prio(cb, J);
     }
 
     // a finish past the u32 clock released its job early: every result of the cluster is void

@@ -511,6 +511,7 @@ __global__ __launch_bounds__(64) void fifo_kernel(FifoArgs a) {
 #endif
     } while (r < rend);
     cb += kWave;
+    wave_progress_prio(cb, J);
     } while (rend != 0u);
     }  // live
 

@@ -45,6 +45,18 @@ __device__ __forceinline__ uint32_t lds_addr(T* p) {
     return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)p;
 }
 
+// Progress-based issue priority at a batch boundary, the compiled kernels' form of the hand-scheduled
+// loops' MCS_FA_PRIO (mcs_fa_macros.h): 3 while more than half of the wave's J jobs
+// remain past the cursor, 2 while more than a quarter, 1 while more than an eighth, else 0.  Both
+// arguments are wave-uniform; only the issue order among a SIMD's waves changes.
+__device__ __forceinline__ void wave_progress_prio(uint32_t cursor, uint32_t J) {
+    const uint32_t rem = cursor < J ? J - cursor : 0u;
+    if (2u * rem > J) __builtin_amdgcn_s_setprio(3);
+    else if (4u * rem > J) __builtin_amdgcn_s_setprio(2);
+    else if (8u * rem > J) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
 __device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
