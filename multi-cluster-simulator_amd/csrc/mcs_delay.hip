@@ -539,8 +539,13 @@ __global__ __launch_bounds__(64) void delay_kernel(DelayArgs a) {
         // Level1 stores must have reached L2 before the next pass's sc1 loads
         if (l1w) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         // the next pass's first rows, in flight during the clock advance, the releases and the
-        // filter build (the list does not change until that pass)
-        if (l1n != 0u) prefetch_l1();
+        // filter build (the list does not change until that pass).  The moves' appends and the
+        // pass's compaction stores are waited for explicitly first: a one-wave workgroup's release
+        // fence waits on LDS only, and the re-read rows are the ones just written.
+        if (l1n != 0u) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            prefetch_l1();
+        }
 
         // ---- time.Sleep(1 s) (:367) and the fast-forward; one exit, tested at the bottom ----
         uint32_t tn = t + 1u;
