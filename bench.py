@@ -634,8 +634,8 @@ def main_batch(args, world, rank, local_rank):
         diag["delay_iterations_per_job"] = diag.pop("loop_passes_per_job")
         diag["level1_moved_frac"] = float(ds["moved_l1"].sum()) / max(n_jobs, 1)
         # clusters the hand-scheduled loop handed to delay_kernel (re-run from t = 0, both launches in
-        # kernel_ms; the engine names both kernels then): Level1 past its LDS slice, a deadlock, or the
-        # clock range after a move
+        # kernel_ms; the engine names both kernels then): Level1 past its LDS slice, the clock range
+        # after a move, or a runaway guard of the loop
         diag["clusters_handed_to_delay_kernel"] = handed_over
         diag["level1_peak_max"] = int(ds["peak_l1"].max())
         diag["avg_wait_s"] = float(ds["total_wait_ms"].sum()) / max(float(ds["jobs_count"].sum()), 1.0) / 1e3
@@ -762,12 +762,62 @@ def world_check(gpus, env, n_devices):
     return "run", world
 
 
-def visible_devices():
-    """GPUs visible to this process without initialising the runtime (device_count() does not on
-    this image; the parent never launches work on a GPU)."""
-    import torch
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
 
-    return torch.cuda.device_count()
+
+def _visible_list(val, n):
+    """How many of n devices a *_VISIBLE_DEVICES value leaves: the leading entries that name a device
+    (an index in range, or a UUID string for ROCR), stopping at the first invalid one, duplicates
+    dropped; an empty value hides every device."""
+    seen = []
+    for tok in (x.strip() for x in val.split(",")):
+        if not tok:
+            break
+        if tok.isdigit():
+            if int(tok) >= n:
+                break
+        elif not tok.startswith("GPU-"):
+            break
+        if tok not in seen:
+            seen.append(tok)
+    return min(len(seen), n)
+
+
+def visible_devices(env=None, root=KFD_NODES):
+    """GPUs this process could use, counted from the KFD topology in sysfs (a node with SIMDs is a
+    GPU), then narrowed by ROCR_VISIBLE_DEVICES and HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES (which
+    index the ROCR-visible list).  No HIP, amdsmi or torch call: the `--gpus N` parent never opens
+    /dev/kfd, so nothing in it can initialise a GPU before it spawns the ranks."""
+    env = os.environ if env is None else env
+    n = 0
+    try:
+        names = os.listdir(root)
+    except OSError:
+        names = []
+    for d in names:
+        try:
+            with open(os.path.join(root, d, "properties")) as f:
+                props = dict(line.split(None, 1) for line in f if len(line.split(None, 1)) == 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0").strip() or 0) > 0:
+            n += 1
+    if "ROCR_VISIBLE_DEVICES" in env:
+        n = _visible_list(env["ROCR_VISIBLE_DEVICES"], n)
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if var in env:
+            n = _visible_list(env[var], n)
+            break
+    return n
+
+
+def _dump_parent_maps():
+    """MCS_BENCH_PARENT_MAPS=<path>: the parent's /proc/self/maps at its decision, for the test that
+    it never mapped /dev/kfd (tests/test_gpu_launcher.py, tests/test_bench_cpu.py)."""
+    path = os.environ.get("MCS_BENCH_PARENT_MAPS")
+    if path:
+        with open("/proc/self/maps") as f, open(path, "w") as g:
+            g.write(f.read())
 
 
 def main():
@@ -776,6 +826,8 @@ def main():
         what, val = "run", 1  # the N=1 line, unchanged
     else:
         what, val = world_check(args.gpus, os.environ, visible_devices())
+        if what != "run":
+            _dump_parent_maps()
     if what == "refuse":
         print(f"bench.py: refusing to run: {val}", file=sys.stderr, flush=True)
         return 2

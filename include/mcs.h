@@ -156,8 +156,8 @@ typedef struct mcs_stats {
     uint32_t t_horizon;     /* online runs: the horizon reached (MCS_TIME_NONE after a drain)      */
     uint32_t online;        /* 1 if this run continued an online session (finite horizons)         */
     uint32_t handed_over;   /* DELAY, ABI v6: clusters the hand-scheduled loop handed to the compiled
-                               delay_kernel (re-run from t = 0: Level1 past its LDS slice, a Level1
-                               deadlock, or the clock range after a move)                           */
+                               delay_kernel (re-run from t = 0: Level1 past its LDS slice, the clock
+                               range after a move, or a runaway guard of the loop)                           */
     uint32_t reserved;
 } mcs_stats;
 

@@ -26,8 +26,10 @@
 // row against the grown nodes alone (their current values, 3 VALU per node), gives each candidate
 // the real first fit in list order, and compacts the row in place.
 // The loop stops a cluster ("bail-out", kDelayBail; the engine re-runs it from t = 0 on the
-// compiled delay_kernel) only when Level1 outgrows its LDS slice or when the clock leaves the u32
-// range after a move.  A Level1 deadlock (nothing runs or arrives and Level1 fits no node) ends the
+// compiled delay_kernel) only when Level1 outgrows its LDS slice, when the clock leaves the u32
+// range after a move, or when a runaway guard trips (more Level1 placements than jobs, or more
+// failed fits than 8J + 256: a loop fault, re-run at the same pool and counted in handed_over;
+// MCS_FLAG_OVERFLOW stays the real slot exhaustion, which escalates the pool).  A Level1 deadlock (nothing runs or arrives and Level1 fits no node) ends the
 // cluster here, as delay_kernel does: its Level1 jobs are written unplaced.
 // Same results bit for bit as delay_kernel and the oracle (tests/test_gpu_delay.py, every form).
 #include "mcs_internal.h"
@@ -309,7 +311,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "s_add_u32 s95, s95, 1\n\t" /* the entry sliding into this slot is not examined (D6) */     \
     "s_add_u32 s98, s98, 1\n\t"                                                                   \
     "s_cmp_gt_u32 s98, s42\n\t" /* more Level1 placements than jobs: a runaway, re-run */       \
-    "s_cbranch_scc1 mcsfd_poolovf_%=\n\t"                                                         \
+    "s_cbranch_scc1 mcsfd_bail_%=\n\t"                                                         \
     "s_add_u32 s100, s100, s40\n\t"                                                               \
     "s_addc_u32 s101, s101, 0\n\t"                                                                \
     "s_mov_b32 s43, 1\n\t"                                                                        \
@@ -465,7 +467,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "s_cbranch_scc1 mcsfd_move0_%=\n\t"                                                           \
     "s_add_u32 s78, s78, 1\n\t"                                                                   \
     "s_cmp_gt_u32 s78, s79\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfd_poolovf_%=\n\t"                                                         \
+    "s_cbranch_scc1 mcsfd_bail_%=\n\t"                                                         \
     "s_add_u32 s76, s45, s56\n\t"                                                                 \
     "s_min_u32 s76, s76, s77\n\t"                                                                 \
     "s_add_u32 s40, s40, 1\n\t"                                                                   \
@@ -507,7 +509,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "s_cbranch_scc1 mcsfd_move1_%=\n\t"                                                           \
     "s_add_u32 s78, s78, 1\n\t"                                                                   \
     "s_cmp_gt_u32 s78, s79\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfd_poolovf_%=\n\t"                                                         \
+    "s_cbranch_scc1 mcsfd_bail_%=\n\t"                                                         \
     "s_cmp_lg_u32 s43, 0\n\t"                                                                     \
     "s_cbranch_scc1 mcsfd_tick1_%=\n\t"                                                           \
     "s_add_u32 s76, s45, s56\n\t"                                                                 \

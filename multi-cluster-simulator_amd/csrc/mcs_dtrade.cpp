@@ -297,6 +297,14 @@ int dt_clusters(mcs_engine* e, std::vector<DtCluster>& cl) {
 
 }  // namespace
 
+void dtrade_release_graphs(mcs_engine* e) {
+    if (DtradeDev* d = e->dtd) {
+        if (d->graph) (void)hipGraphExecDestroy(d->graph);
+        if (d->rgraph) (void)hipGraphExecDestroy(d->rgraph);
+        d->graph = d->rgraph = nullptr;
+    }
+}
+
 void dtrade_free(mcs_engine* e) {
     DtradeDev* d = e->dtd;
     if (!d) return;

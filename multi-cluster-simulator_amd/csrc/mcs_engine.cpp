@@ -225,9 +225,14 @@ int mcs_engine_destroy(mcs_engine* e) {
     if (!e) return MCS_E_INVALID;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    // teardown order: the captured tick graphs (they reference RCCL resources), then the RCCL
+    // communicator (finalized: no proxy work outstanding), then device memory, events and the stream
+    mcs::trade_release_graphs(e);
+    mcs::dtrade_release_graphs(e);
+    mcs::comm_free(e);
+    (void)hipDeviceSynchronize();
     mcs::trade_free(e);
     mcs::dtrade_free(e);
-    mcs::comm_free(e);
     mcs::online_free(e);
     free_clusters(e);
     free_jobs(e);

@@ -13,11 +13,13 @@
 namespace mcs {
 struct TradeDev;  // mcs_trade.cpp
 void trade_free(mcs_engine* e);
+void trade_release_graphs(mcs_engine* e);  // the captured tick graphs only (before comm_free)
 void comm_free(mcs_engine* e);
 int trade_run(mcs_engine* e, mcs_stats* stats);
 int trade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n_clusters);
 struct DtradeDev;  // mcs_dtrade.cpp: lock-step trading with DELAY schedulers
 void dtrade_free(mcs_engine* e);
+void dtrade_release_graphs(mcs_engine* e);
 int dtrade_run(mcs_engine* e, mcs_stats* stats);
 int dtrade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n);
 int dtrade_delay_stats(mcs_engine* e, mcs_delay_cluster_stats* out, uint32_t n);
@@ -52,7 +54,7 @@ constexpr uint32_t kLoopRcclEager = 1;  // RCCL all-gather per tick, launches en
 constexpr uint32_t kLoopRcclGraph = 2;  // RCCL all-gather per tick, captured with the kernels
 constexpr uint32_t kLoopResident = 3;   // one engine, the whole system resident in one workgroup
 constexpr uint32_t kLoopResidentMwXcd = 5;  // the same, its workgroups on one XCD (L2 exchange)
-constexpr uint32_t kLoopResidentMw = 4;  // one engine, resident in ceil(C / 16) workgroups (granules)
+constexpr uint32_t kLoopResidentMw = 4;  // one engine, resident in ceil(C / kMwWaves) workgroups, 4 clusters each (granules)
 constexpr uint32_t kLoopGraphAfterTimeout = 6;  // the replayed kernels after a resident exchange timed out
 
 // Capture `ticks` ticks of `tick(stream)` (kernels and the RCCL all-gather) into one executable

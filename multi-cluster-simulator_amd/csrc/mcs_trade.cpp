@@ -232,10 +232,12 @@ int run_local(mcs_engine* e) {
         // consecutive blocks, the write-through exchange)
         const char* xenv = getenv("MCS_MW_XCD");
         const bool xcd_pack = !xenv || atoi(xenv) != 0;
+        const char* uenv = getenv("MCS_MW_FORCE_UC");  // tests: the write-through exchange (form 4)
+        const bool force_uc = uenv && atoi(uenv) != 0;
         const uint32_t budget = res_ticks();
         for (uint32_t launch = 0;; ++launch) {
             const hipError_t st = launch_trade_mw(td->a, td->gx, td->gxc, budget, launch * budget, lds, xcd_pack,
-                                                  e->stream);
+                                                  force_uc, e->stream);
             if (st != hipSuccess) return hip_fail(e, "resident tick kernel (workgroups)", st);
             if (int s = poll_ctl(e)) return s;
             // every worker block must be resident at once; when another stream or process holds
@@ -369,8 +371,23 @@ int fill_stats(mcs_engine* e, mcs_trade_stats* ts, mcs_stats* st) {
 }  // namespace
 
 void comm_free(mcs_engine* e) {
-    if (e->comm) (void)ncclCommDestroy((ncclComm_t)e->comm);
+    if (e->comm) {
+        // finalize (flushes the communicator's outstanding work and stops its proxy) before the
+        // destroy, so nothing of RCCL's touches the engine's buffers after mcs_engine_destroy frees them
+        (void)ncclCommFinalize((ncclComm_t)e->comm);
+        (void)ncclCommDestroy((ncclComm_t)e->comm);
+    }
     e->comm = nullptr;
+}
+
+// the captured tick graphs hold RCCL's graph-user objects (references to the communicator's
+// resources): they go before the communicator, which goes before any device memory
+void trade_release_graphs(mcs_engine* e) {
+    if (TradeDev* td = e->td) {
+        if (td->graph) (void)hipGraphExecDestroy(td->graph);
+        if (td->rgraph) (void)hipGraphExecDestroy(td->rgraph);
+        td->graph = td->rgraph = nullptr;
+    }
 }
 
 void trade_free(mcs_engine* e) {

@@ -138,7 +138,7 @@ constexpr uint32_t kTrResMaxClusters = 64;
 bool trade_resident_shape(const TradeArgs& a);
 size_t trade_resident_lds(uint32_t n_clusters, uint32_t ns);
 hipError_t launch_trade_resident(const TradeArgs& a, uint32_t tick_budget, size_t lds, hipStream_t s);
-// the system resident in ceil(C / 16) workgroups, one cluster per wave, records traded as tagged
+// the system resident in ceil(C / kMwWaves) workgroups (4 clusters each), one cluster per wave, records traded as tagged
 // granules (mcs_trade_mw.hip): shape check, LDS bytes, granule count, launch
 bool trade_mw_shape(const TradeArgs& a);
 size_t trade_mw_lds(uint32_t ns);
@@ -148,7 +148,8 @@ constexpr size_t trade_mw_xcc_off() { return (size_t)kTrResMaxClusters * 10u + 1
 // gx_uc: uncached granules (any placement); gx_c: cached granules, used when every workgroup runs on
 // one XCD; xcd_pack: launch the workers 8 blocks apart (one XCD under round-robin dispatch)
 hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsigned long long* gx_c,
-                           uint32_t tick_budget, uint32_t tick0, size_t lds, bool xcd_pack, hipStream_t s);
+                           uint32_t tick_budget, uint32_t tick0, size_t lds, bool xcd_pack, bool force_uc,
+                           hipStream_t s);
 constexpr uint32_t kTrFlagMwTimeout = 0x80000000u;  // internal: an exchange sweep gave up
 
 }  // namespace mcs

@@ -23,7 +23,8 @@
 //      owner workgroup applies its borrowers' BorrowedQueue moves (C/D does not wait for them).
 // Exchange: the data is the flag (cdna_hip_programming.md Guideline 16, R2): every word travels
 // as an 8-byte granule {value, tag} stored write-through (agent-scope atomic store) with
-// tag = the exchange's epoch within the launch (2 * tick + 1 for X1, + 2 for X2); the gathering
+// tag = the exchange's epoch counted from the run's first tick, across launches (2 * tick + 1 for
+// X1, + 2 for X2, the tick taken modulo 2^31 - 1 so no tag is 0); the gathering
 // wave re-reads its granules (agent-scope atomic loads) until every tag matches.  A workgroup
 // publishes X1 of tick n + 1 only after gathering X2 of tick n, which every workgroup published
 // after its own X1 sweep of tick n; and it publishes X2 of tick n + 1 only after its X1 sweep of
@@ -175,7 +176,8 @@ static_assert(offsetof(MwShared, rq_c) == offsetof(MwShared, rq_job) + 1 * kTrRe
 template <int kRows>  // slot rows per cluster (64 slots each)
 __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, unsigned long long* gx_uc,
                                                                  unsigned long long* gx_c, uint32_t tick_budget,
-                                                                 uint32_t nwg, uint32_t stride, uint32_t tick0) {
+                                                                 uint32_t nwg, uint32_t stride, uint32_t tick0,
+                                                                 uint32_t force_uc) {
     // the workers are blocks 0, stride, 2 * stride, ...: with stride 8 they share one XCD under the
     // dispatcher's observed round-robin placement (speed only: the check below decides the protocol)
     if (blockIdx.x % stride != 0u) return;
@@ -205,7 +207,9 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             }
         }
         const uint32_t v0 = readlane(v, 0);
-        const bool same = ok && __all(lane >= nwg || v == v0);
+        // (force_uc, MCS_MW_FORCE_UC=1: the write-through exchange whatever the placement, so the
+        // tests pin loop_form 4 even when every worker landed on one XCD)
+        const bool same = ok && force_uc == 0u && __all(lane >= nwg || v == v0);
         if (threadIdx.x == 0) sh.xcd = same ? 1u : 0u;
     }
     __syncthreads();
@@ -371,8 +375,10 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
         MW_MARK(9);
         const uint32_t T = sh.T;
         // epochs count from the run's first tick, across launches: a granule line another launch
-        // left in an XCD's L2 never carries a current tag
-        const uint32_t tag1 = 2u * (tick0 + it) + 1u, tag2 = tag1 + 1u;
+        // left in an XCD's L2 never carries a current tag.  Taken modulo 2^31 - 1, so tag1 is odd in
+        // [1, 2^32 - 3] and tag2 = tag1 + 1 never wraps to 0 (the zeroed granules' tag)
+        const uint32_t ep = (tick0 + it) % 0x7FFFFFFFu;
+        const uint32_t tag1 = 2u * ep + 1u, tag2 = tag1 + 1u;
 
         // GetResourceUtilization runs on the ticks a trader reads it (see tr_step_kernel)
         bool sample = false;
@@ -931,7 +937,8 @@ bool trade_mw_shape(const TradeArgs& a) {
 size_t trade_mw_granules(uint32_t) { return trade_mw_xcc_off() + kWave; }
 
 hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsigned long long* gx_c,
-                           uint32_t tick_budget, uint32_t tick0, size_t lds, bool xcd_pack, hipStream_t s) {
+                           uint32_t tick_budget, uint32_t tick0, size_t lds, bool xcd_pack, bool force_uc,
+                           hipStream_t s) {
     const uint32_t nwg = (a.Ct + kMwWaves - 1) / kMwWaves;
     const uint32_t stride = xcd_pack ? 8u : 1u, nblk = stride * (nwg - 1u) + 1u;
     // the granules carry epochs counted from the run's first tick (tick0 = the ticks of the run's
@@ -947,13 +954,13 @@ hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsign
     if (st != hipSuccess) return st;
     if (a.S == 4u * kWave)
         hipLaunchKernelGGL(tr_mw_kernel<4>, dim3(nblk), dim3(kMwWaves * kWave), lds, s, a, gx_uc, gx_c, tick_budget,
-                           nwg, stride, tick0);
+                           nwg, stride, tick0, force_uc ? 1u : 0u);
     else if (a.S == 8u * kWave)
         hipLaunchKernelGGL(tr_mw_kernel<8>, dim3(nblk), dim3(kMwWaves * kWave), lds, s, a, gx_uc, gx_c, tick_budget,
-                           nwg, stride, tick0);
+                           nwg, stride, tick0, force_uc ? 1u : 0u);
     else
         hipLaunchKernelGGL(tr_mw_kernel<16>, dim3(nblk), dim3(kMwWaves * kWave), lds, s, a, gx_uc, gx_c, tick_budget,
-                           nwg, stride, tick0);
+                           nwg, stride, tick0, force_uc ? 1u : 0u);
     return hipGetLastError();
 }
 

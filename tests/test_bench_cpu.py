@@ -93,3 +93,48 @@ def test_refusal_exits_nonzero_without_gpus():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 2 and "differs from --gpus" in r.stderr
+
+
+def _fake_kfd(tmp_path, kinds):
+    """A KFD topology tree: one node directory per entry, 'gpu' nodes with SIMDs, 'cpu' without."""
+    root = tmp_path / "nodes"
+    for i, k in enumerate(kinds):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        simd = 1024 if k == "gpu" else 0
+        (d / "properties").write_text(f"cpu_cores_count {0 if k == 'gpu' else 64}\nsimd_count {simd}\n"
+                                      f"gfx_target_version {90500 if k == 'gpu' else 0}\n")
+    return str(root)
+
+
+def test_visible_devices_from_kfd_sysfs(tmp_path, monkeypatch):
+    """The parent counts GPUs from the KFD topology (nodes with SIMDs) and narrows the count by
+    ROCR_VISIBLE_DEVICES, then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES, without HIP or torch."""
+    bench, _ = _bench(["--gpus", "2"], monkeypatch)
+    root = _fake_kfd(tmp_path, ["cpu", "gpu", "gpu", "gpu", "cpu", "gpu"])
+    assert bench.visible_devices({}, root) == 4
+    assert bench.visible_devices({"HIP_VISIBLE_DEVICES": "0,2"}, root) == 2
+    assert bench.visible_devices({"HIP_VISIBLE_DEVICES": ""}, root) == 0
+    assert bench.visible_devices({"CUDA_VISIBLE_DEVICES": "3,7,1"}, root) == 1  # stops at the invalid 7
+    assert bench.visible_devices({"ROCR_VISIBLE_DEVICES": "1,2", "HIP_VISIBLE_DEVICES": "0,1,2"}, root) == 2
+    assert bench.visible_devices({"ROCR_VISIBLE_DEVICES": "GPU-1234abcd"}, root) == 1
+    assert bench.visible_devices({}, str(tmp_path / "absent")) == 0
+
+
+def test_parent_maps_no_gpu_runtime(tmp_path):
+    """`bench.py --gpus 2` as a parent: its /proc/self/maps at the decision (MCS_BENCH_PARENT_MAPS)
+    shows neither /dev/kfd nor any HIP or torch library, i.e. the parent cannot have initialised a
+    GPU before spawning (or refusing)."""
+    import subprocess
+
+    maps = tmp_path / "maps.txt"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MCS_BENCH_PARENT_MAPS"] = str(maps)
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "refusing" in r.stderr
+    text = maps.read_text()
+    assert "python" in text  # the dump is real
+    for bad in ("/dev/kfd", "libamdhip64", "libtorch", "libhsa-runtime"):
+        assert bad not in text, bad

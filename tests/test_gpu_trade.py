@@ -239,6 +239,19 @@ def test_gpu_trade_resident_equals_kernels_and_oracle(kind, C, J, pool, monkeypa
     assert_trade_parity(arrays, streams, res["2"])
 
 
+@pytest.mark.parametrize("kind,C,J,pool", [("n256", 16, 3000, 8), ("small", 64, 1500, 0), ("n64", 33, 2000, 4)])
+def test_gpu_trade_resident_write_through_form(kind, C, J, pool, monkeypatch):
+    """The uncached write-through exchange of the workgroup-resident tick (loop_form 4) pinned
+    explicitly: MCS_MW_FORCE_UC=1 makes every launch take it whatever XCDs its workers landed on (the
+    default picks the L2 exchange, form 5, when they share one), and it must equal the oracle."""
+    monkeypatch.setenv("MCS_TRADE_RESIDENT", "2")
+    monkeypatch.setenv("MCS_MW_FORCE_UC", "1")
+    arrays, streams, _ = seeded_workload(kind, C, J)
+    g = gpu_trade(arrays, streams, slot_pool=pool)
+    assert g["tstats"]["loop_form"] == 4, g["tstats"]["loop_form"]
+    assert_trade_parity(arrays, streams, g)
+
+
 def test_gpu_trade_resident_form_by_capacity(monkeypatch):
     """The workgroup-resident tick packs a running slot's payload into 32 bits, so the engine picks
     it only when every node's max(capacity, availability) is below 128 cores and 65536 memory: a
