@@ -450,7 +450,7 @@ constexpr uint32_t kLdsWords = 4 * kWave + 3 * kL1Cap;
     "s_waitcnt lgkmcnt(0)\n\t" MCS_FD_TE_##D(36, 11)                                              \
     "s_cmp_lg_u32 s92, 0\n\t"                                                                     \
     "s_cbranch_scc1 mcsfd_inner1_%=\n\t"                                                          \
-    "s_branch mcsfd_inner0_%=\n" MCS_FD_ZERO(0)                                                   \
+    "s_branch mcsfd_inner0_%=\n" MCS_FA_RBODY16R MCS_FD_ZERO(0)                                   \
     /* nothing changes at t (Level0 empty): the next iteration that can differ is a release or  */ \
     /* the head's arrival */                                                                      \
     "mcsfd_idle0_%=:\n\t"                                                                         \

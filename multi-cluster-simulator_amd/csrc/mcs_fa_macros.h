@@ -303,16 +303,22 @@
     "s_set_gpr_idx_off\n\t"                                                                      \
     "v_xor_b32 v89, s76, v89\n\t" /* the row is taken */
 // (exec = the row's expiry mask, SCC = any: no separate test, and exec is restored to the full
-// wave once after the last row)
+// wave once after the last row).  r05: a row with an expiry branches to its body out of line
+// (MCS_FR_BODY, placed by the loop after an unconditional branch) and returns; a row without one
+// falls through.  ~1.5 of the 8 rows expire per scan, so a scan takes ~3 taken branches instead of
+// ~6.5: at one wave per SIMD a taken branch costs ~20 cycles, the row test ~8.
 #define MCS_FR_ROW(p, MASK, F, P, A)                                                              \
     "s_and_b64 exec, " MASK ", -1\n\t"                                                           \
-    "s_cbranch_scc0 mcsfa_r" #p "_%=\n\t"                                                        \
+    "s_cbranch_scc1 mcsfa_rb" #p "_%=\n"                                                         \
+    "mcsfa_r" #p "_%=:\n\t"
+#define MCS_FR_BODY(p, MASK, F, P, A)                                                             \
+    "mcsfa_rb" #p "_%=:\n\t"                                                                     \
     "s_bcnt1_i32_b64 s76, " MASK "\n\t"                                                          \
     "ds_add_u32 " A ", " P "\n\t"                                                               \
     "v_mov_b32 " F ", -1\n\t"                                                                    \
     "s_add_u32 s75, s75, s76\n\t"                                                                \
-    "v_or_b32 v89, 1<<" #p ", v89\n"                                                             \
-    "mcsfa_r" #p "_%=:\n\t"
+    "v_or_b32 v89, 1<<" #p ", v89\n\t"                                                           \
+    "s_branch mcsfa_r" #p "_%=\n"
 #define MCS_FA_SCAN16R                                                                            \
     /* the LDS node copy is refreshed from the registers first (commits do not touch it) */       \
     "ds_write_b32 v108, v64 offset:0\n\t"                                                        \
@@ -339,6 +345,17 @@
     "v_min3_u32 v90, v90, v35, v36\n\t"                                                          \
     "v_min3_u32 v90, v90, v37, v38\n\t"                                                          \
     "v_min_u32 v90, v90, v39\n\t"
+// the expiring rows' bodies of MCS_FA_SCAN16R (out of line: after an unconditional branch)
+#define MCS_FA_RBODY16R                                                                           \
+    MCS_FR_BODY(0, "s[50:51]", "v32", "v40", "v48") MCS_FR_BODY(1, "s[52:53]", "v33", "v41", "v49") \
+    MCS_FR_BODY(2, "s[54:55]", "v34", "v42", "v50") MCS_FR_BODY(3, "s[60:61]", "v35", "v43", "v51") \
+    MCS_FR_BODY(4, "s[62:63]", "v36", "v44", "v52") MCS_FR_BODY(5, "s[86:87]", "v37", "v45", "v53") \
+    MCS_FR_BODY(6, "s[88:89]", "v38", "v46", "v54") MCS_FR_BODY(7, "s[90:91]", "v39", "v47", "v55")
+#define MCS_FA_RBODY16S                                                                           \
+    MCS_FR_BODY(0, "s[50:51]", "v32", "v40", "v48") MCS_FR_BODY(1, "s[52:53]", "v33", "v41", "v49")
+#define MCS_FA_RBODY32 ""
+#define MCS_FA_RBODY16 ""
+#define MCS_FA_RBODY16D ""
 
 // node registers back from the LDS copy
 #define MCS_FA_RELOAD32                                                                           \

@@ -127,7 +127,11 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     "s_cbranch_scc0 mcsfa_bend_%=\n\t"                                                            \
     "s_sub_u32 s41, s42, s57\n\t"                                                                 \
     "s_min_u32 s41, s41, 64\n\t"                                                                  \
-    "s_branch mcsfa_hwadv_%=\n"                                                                   \
+    /* (the clock moves by t + 1 here and on a failed fit: the carry is the u32 clock's overflow) */ \
+    "s_mov_b32 s43, 0\n\t"                                                                        \
+    "s_add_u32 s40, s40, 1\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_clkovf_%=\n\t"                                                          \
+    "s_branch mcsfa_adv_%=\n"                                                                     \
                                                                                                   \
     /* zero-duration job: committed and released before the next decision (D3) */               \
     "mcsfa_zero_%=:\n\t" MCS_FA_ZEROKX##W                                                        \
@@ -135,14 +139,13 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     "v_writelane_b32 v92, s40, m0\n\t"                                                            \
     "s_branch mcsfa_placed_%=\n"                                                                  \
                                                                                                   \
-    /* (the clock moves by t + 1 here and on a failed fit: the carry is the u32 clock's overflow) */ \
-    "mcsfa_hwadv_%=:\n\t"                                                                         \
-    "s_mov_b32 s43, 0\n\t"                                                                        \
-    "s_add_u32 s40, s40, 1\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfa_clkovf_%=\n\t"                                                          \
+    "mcsfa_arrive_%=:\n\t"                                                                        \
+    "s_mov_b32 s40, s45\n\t" /* (> t) */                                                         \
+    MCS_FA_CNTS_##D                                                                               \
     "s_branch mcsfa_adv_%=\n"                                                                     \
                                                                                                   \
-    /* no node fits: WaitQueue append (:264-268), sleep to the next completion (A.3) */          \
+    /* no node fits: WaitQueue append (:264-268), sleep to the next completion (A.3); falls */   \
+    /* through to the release (a failed head sleeps to a completion, so it always releases) */  \
     "mcsfa_nofit_%=:\n\t" MCS_FA_T0                                                              \
     "s_sub_u32 s76, 1, s43\n\t"                                                                   \
     "s_add_u32 s82, s82, s76\n\t"                                                                 \
@@ -159,11 +162,7 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     "s_add_u32 s40, s40, 1\n\t"                                                                   \
     "s_cbranch_scc1 mcsfa_clkovf_%=\n\t"                                                          \
     "s_max_u32 s40, s40, s77\n\t" /* (every running job finishes after t: no wrap) */           \
-    MCS_FA_T1("s95") "s_branch mcsfa_adv_%=\n"                                                    \
-                                                                                                  \
-    "mcsfa_arrive_%=:\n\t"                                                                        \
-    "s_mov_b32 s40, s45\n\t" /* (> t) */                                                         \
-    MCS_FA_CNTS_##D "\n"                                                                          \
+    MCS_FA_T1("s95")                                                                              \
     /* the clock has advanced: releases at the new instant (A.2 step 1) */                       \
     "mcsfa_adv_%=:\n\t"                                                                           \
     "s_cmp_lt_u32 s40, s77\n\t" /* nothing finishes by t: no release */                          \
@@ -172,7 +171,10 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     MCS_FA_CNTR_##D MCS_FA_T0                                                                     \
     "s_max_u32 s81, s81, s80\n\t" /* peak: used only grows between releases */                   \
     "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN##W MCS_FA_SCANEND##W MCS_FA_T1("s94")                \
-    "s_branch mcsfa_loopend_%=\n"                                                                 \
+    /* (loopend's test, so the usual continuation is one taken branch) */                        \
+    "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_inner_%=\n\t"                                                           \
+    "s_branch mcsfa_loopend_%=\n" MCS_FA_RBODY##W                                                 \
                                                                                                   \
     "mcsfa_deadlock_%=:\n\t"                                                                      \
     "s_or_b32 s44, s44, %[fdl]\n\t"                                                               \
