@@ -56,6 +56,9 @@ constexpr uint32_t kLoopResident = 3;   // one engine, the whole system resident
 constexpr uint32_t kLoopResidentMwXcd = 5;  // the same, its workgroups on one XCD (L2 exchange)
 constexpr uint32_t kLoopResidentMw = 4;  // one engine, resident in ceil(C / kMwWaves) workgroups, 4 clusters each (granules)
 constexpr uint32_t kLoopGraphAfterTimeout = 6;  // the replayed kernels after a resident exchange timed out
+constexpr uint32_t kLoopRkGraph = 7;  // RCCL: one launch + one all-gather per tick, captured in a hipGraph
+constexpr uint32_t kLoopRkEager = 8;  // the same, enqueued eagerly
+constexpr uint32_t kLoopRkDriven = 9;  // the one-launch tick on the caller-driven phase API
 
 // Capture `ticks` ticks of `tick(stream)` (kernels and the RCCL all-gather) into one executable
 // graph.  Returns nullptr, with the stream out of capture mode and the HIP error state cleared, when
@@ -140,6 +143,7 @@ struct mcs_engine {
     uint32_t dt_learn_s = 0, dt_learn_v = 0;  // the capacities a DELAY-trading run of these inputs ended at
     uint32_t dt_ns = 0;                // node-snapshot stride over all ranks (0 = max_n)
     uint32_t tr_ns = 0;                // the same for FIFO lock-step trading
+    bool tr_rk_ok = true;              // every rank can run the one-launch tick (tr_agree_shape)
     // online mode (mcs_online.cpp): per-cluster state kept on the device between horizons
     bool online = false;               // a session is active
     bool segmented = false;            // job_off holds segment starts with slack (appends)

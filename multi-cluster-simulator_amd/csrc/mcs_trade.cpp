@@ -37,6 +37,11 @@ struct TradeDev {
     TrCtl* ctl = nullptr;
     mcs_lent_rec* lent = nullptr;
     mcs_trade_rec* trades = nullptr;
+    uint4* lrp = nullptr;                // one-launch tick: pending lent-run records
+    unsigned long long* gx2 = nullptr;   // one-launch tick: X2 granules (uncached)
+    bool rk = false;                     // the one-launch tick runs this system (trade_alloc)
+    bool rk_started = false;             // its tick-0 phase A has run
+    size_t rk_lds = 0;
     TrCtl* h_ctl = nullptr;  // pinned
     hipGraphExec_t graph = nullptr;
     uint32_t graph_ticks = 0;
@@ -120,6 +125,7 @@ int trade_alloc(mcs_engine* e) {
     HIPCHK(e, hipMalloc(&td->lent, lent_cap * sizeof(mcs_lent_rec)));
     HIPCHK(e, hipMalloc(&td->trades, trade_cap * sizeof(mcs_trade_rec)));
     HIPCHK(e, hipHostMalloc(&td->h_ctl, sizeof(TrCtl), hipHostMallocDefault));
+    HIPCHK(e, hipMalloc(&td->lrp, std::max<uint32_t>(Cl, 1u) * sizeof(uint4)));
 
     TradeArgs& a = td->a;
     a.Cl = Cl;
@@ -163,6 +169,21 @@ int trade_alloc(mcs_engine* e) {
     a.ctl = td->ctl;
     a.lent_log = td->lent;
     a.trade_log = td->trades;
+    a.lrp = td->lrp;
+    // the one-launch tick (mcs_trade_rk.hip) runs sharded systems (a communicator or the caller-driven
+    // API) whose shape it holds; every rank decides alike (tr_agree_shape on the RCCL path; the
+    // caller-driven ranks hold alike clusters).  MCS_TRADE_RK=0 keeps the three-kernel tick.
+    const char* rkenv = getenv("MCS_TRADE_RK");
+    const bool want_rk = !rkenv || atoi(rkenv) != 0;
+    if (want_rk && e->sums_lt24 && e->slot_pack_ok && e->tr_rk_ok && trade_rk_shape(a)) {
+        int max_lds = 0;
+        td->rk_lds = trade_rk_lds(ns);
+        if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device) == hipSuccess &&
+            td->rk_lds <= (size_t)max_lds) {
+            HIPCHK(e, hipExtMallocWithFlags((void**)&td->gx2, trade_rk_granules(Ct) * 8u, 3u));
+            td->rk = true;
+        }
+    }
     return MCS_OK;
 }
 
@@ -293,8 +314,50 @@ int nccl_fail(mcs_engine* e, const char* what, ncclResult_t r) {
 // Captured once into a hipGraph of kGraphTicks ticks (kernels and all-gathers: no host enqueue per
 // tick); eager when the capture is refused.  Every rank captures and replays the same
 // sequence, so the collectives stay matched.
+// The one-launch tick (r05): tick 0's phase A eagerly, then {in-place ncclAllGather of the blocks,
+// tr_rk_kernel (B/C/D of tick n + A of tick n + 1)} per tick, kGraphTicks ticks per captured graph
+int run_rccl_rk(mcs_engine* e) {
+    TradeDev* td = e->td;
+    const TradeArgs& a = td->a;
+    ncclComm_t comm = (ncclComm_t)e->comm;
+    {
+        const hipError_t st = launch_trade_rk(a, td->gx2, 0u, td->rk_lds, e->stream);
+        if (st != hipSuccess) return hip_fail(e, "one-launch tick (tick 0)", st);
+        td->rk_started = true;
+    }
+    auto tick = [&](hipStream_t s) -> bool {
+        if (ncclAllGather(td->xb + (size_t)e->rank * a.blk, td->xb, a.blk, ncclUint8, comm, s) != ncclSuccess)
+            return false;
+        return launch_trade_rk(a, td->gx2, 1u, td->rk_lds, s) == hipSuccess;
+    };
+    if (!td->rgraph_tried) {
+        td->rgraph_tried = true;
+        td->rgraph = capture_tick_graph(e->stream, kGraphTicks, tick);
+    }
+    td->loop_form = td->rgraph ? kLoopRkGraph : kLoopRkEager;
+    for (;;) {
+        if (td->rgraph) {
+            HIPCHK(e, hipGraphLaunch(td->rgraph, e->stream));
+        } else {
+            for (uint32_t t = 0; t < kGraphTicks; ++t) {
+                const ncclResult_t r = ncclAllGather(td->xb + (size_t)e->rank * a.blk, td->xb, a.blk, ncclUint8,
+                                                     comm, e->stream);
+                if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(exchange blocks)", r);
+                const hipError_t st = launch_trade_rk(a, td->gx2, 1u, td->rk_lds, e->stream);
+                if (st != hipSuccess) return hip_fail(e, "one-launch tick", st);
+            }
+        }
+        if (int s = poll_ctl(e)) return s;
+        // a bounded X2 sweep gave up (a worker was not resident): no rank can re-run alone
+        if (td->h_ctl->flags & kTrFlagMwTimeout)
+            return fail(e, MCS_E_HIP, "one-launch tick: the X2 exchange timed out (workgroups not co-resident)");
+        if (td->h_ctl->done) return MCS_OK;
+    }
+}
+
 int run_rccl(mcs_engine* e) {
     TradeDev* td = e->td;
+    if (td->rk) return run_rccl_rk(e);
     const TradeArgs& a = td->a;
     ncclComm_t comm = (ncclComm_t)e->comm;
     auto tick = [&](hipStream_t s) -> bool {
@@ -412,6 +475,8 @@ void trade_free(mcs_engine* e) {
     dfree(td->ctl);
     dfree(td->lent);
     dfree(td->trades);
+    dfree(td->lrp);
+    dfree(td->gx2);
     if (td->h_ctl) (void)hipHostFree(td->h_ctl);
     delete td;
     e->td = nullptr;
@@ -444,13 +509,14 @@ int trade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n) {
 // the whole system, and the cluster count per rank must match (one all-reduce before the run)
 int tr_agree_shape(mcs_engine* e) {
     uint32_t* buf = nullptr;
-    HIPCHK(e, hipMalloc(&buf, 3 * sizeof(uint32_t)));
+    HIPCHK(e, hipMalloc(&buf, 4 * sizeof(uint32_t)));
     /* max of C and of ~C (= ~min C): every rank sees the same verdict, so a mismatch fails on
-     * every rank instead of leaving the ranks with the largest C in the tick loop */
-    const uint32_t h[3] = {e->max_n, e->C, ~e->C};
-    uint32_t mx[3] = {0, 0, 0};
+     * every rank instead of leaving the ranks with the largest C in the tick loop; the 4th word:
+     * some rank cannot pack the one-launch tick's slot payload or sum utilization exactly */
+    const uint32_t h[4] = {e->max_n, e->C, ~e->C, (e->sums_lt24 && e->slot_pack_ok) ? 0u : 1u};
+    uint32_t mx[4] = {0, 0, 0, 0};
     HIPCHK(e, hipMemcpy(buf, h, sizeof(h), hipMemcpyHostToDevice));
-    ncclResult_t r = ncclAllReduce(buf, buf, 3, ncclUint32, ncclMax, (ncclComm_t)e->comm, e->stream);
+    ncclResult_t r = ncclAllReduce(buf, buf, 4, ncclUint32, ncclMax, (ncclComm_t)e->comm, e->stream);
     hipError_t st = hipStreamSynchronize(e->stream);
     if (r == ncclSuccess && st == hipSuccess) st = hipMemcpy(mx, buf, sizeof(mx), hipMemcpyDeviceToHost);
     (void)hipFree(buf);
@@ -458,6 +524,7 @@ int tr_agree_shape(mcs_engine* e) {
     if (st != hipSuccess) return hip_fail(e, "shape exchange", st);
     if (mx[1] != ~mx[2]) return fail(e, MCS_E_INVALID, "sharded lock-step trading needs the same cluster count on every rank");
     e->tr_ns = mx[0];
+    e->tr_rk_ok = mx[3] == 0u;
     return MCS_OK;
 }
 
@@ -537,6 +604,7 @@ int mcs_set_shard(mcs_engine* e, uint32_t rank, uint32_t world) {
     e->dt_learn_s = e->dt_learn_v = 0;
     e->dt_ns = 0;
     e->tr_ns = 0;
+    e->tr_rk_ok = true;
     e->rank = rank;
     e->world = world;
     return MCS_OK;
@@ -580,6 +648,8 @@ int mcs_trade_begin(mcs_engine* e) {
     td->w0 = std::chrono::steady_clock::now();
     const hipError_t st = mcs::launch_trade_init(td->a, e->stream);
     if (st != hipSuccess) return mcs::hip_fail(e, "trade init", st);
+    td->rk_started = false;
+    if (td->gx2) HIPCHK(e, hipMemsetAsync(td->gx2, 0, mcs::trade_rk_granules(td->a.Ct) * 8u, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));  // kernel_ms: the lock-step loop only
     td->begun = true;
@@ -617,6 +687,35 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
     if (in_bytes != ib || out_bytes != ob || (ib && !in) || (ob && !out))
         return fail(e, MCS_E_INVALID, "exchange buffer sizes do not match mcs_trade_xfer_bytes");
     const mcs::TradeArgs& a = td->a;
+    if (td->rk) {  // the one-launch tick: phase 1 runs B/C/D of tick n and A of tick n + 1
+        td->loop_form = mcs::kLoopRkDriven;
+        hipError_t hs = hipSuccess;
+        switch (phase) {
+            case 0:
+                if (!td->rk_started) {
+                    hs = mcs::launch_trade_rk(a, td->gx2, 0u, td->rk_lds, e->stream);
+                    td->rk_started = true;
+                }
+                if (hs == hipSuccess)
+                    hs = hipMemcpyAsync(out, td->xb + (size_t)e->rank * a.blk, ob, hipMemcpyDeviceToHost, e->stream);
+                break;
+            case 1:
+                hs = hipMemcpyAsync(td->xb, in, ib, hipMemcpyHostToDevice, e->stream);
+                if (hs == hipSuccess) hs = mcs::launch_trade_rk(a, td->gx2, 1u, td->rk_lds, e->stream);
+                break;
+            case 2:
+                break;
+            default:
+                hs = hipMemcpyAsync(td->h_ctl, td->ctl, sizeof(mcs::TrCtl), hipMemcpyDeviceToHost, e->stream);
+                break;
+        }
+        if (hs != hipSuccess) return mcs::hip_fail(e, "one-launch tick (caller-driven)", hs);
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (phase == 3 && (td->h_ctl->flags & mcs::kTrFlagMwTimeout))
+            return fail(e, MCS_E_HIP, "one-launch tick: the X2 exchange timed out (workgroups not co-resident)");
+        if (done) *done = phase == 3 ? td->h_ctl->done : 0u;
+        return MCS_OK;
+    }
     switch (phase) {
         case 0:
             if (int s = mcs::launch_phase(e, a, 0)) return s;

@@ -118,6 +118,7 @@ struct TradeArgs {
     TrCtl* ctl;
     mcs_lent_rec* lent_log;
     mcs_trade_rec* trade_log;
+    uint4* lrp;  // (one-launch tick) this rank's lent run of the last phase A per cluster {b, j, node, fin}
 };
 
 // the exchange record and node snapshot of global cluster g
@@ -151,5 +152,11 @@ hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsign
                            uint32_t tick_budget, uint32_t tick0, size_t lds, bool xcd_pack, bool force_uc,
                            hipStream_t s);
 constexpr uint32_t kTrFlagMwTimeout = 0x80000000u;  // internal: an exchange sweep gave up
+// N ranks, one launch per tick (mcs_trade_rk.hip): B/C/D of tick n + A of tick n + 1, the ranks'
+// blocks all-gathered between launches; mode 0 = phase A of tick 0 only
+bool trade_rk_shape(const TradeArgs& a);
+size_t trade_rk_lds(uint32_t ns);
+size_t trade_rk_granules(uint32_t n_clusters);
+hipError_t launch_trade_rk(const TradeArgs& a, unsigned long long* gx2, uint32_t mode, size_t lds, hipStream_t s);
 
 }  // namespace mcs

@@ -1,0 +1,739 @@
+// mcs_trade_rk.hip — the lock-step FIFO trading tick for N ranks in ONE launch per tick (r05).
+//
+// The RCCL tick loop used to run four launches and one all-gather per tick (tr_step / tr_lend /
+// tr_trader, mcs_trade.hip).  Here a tick is {tr_rk_kernel, in-place ncclAllGather of the ranks'
+// exchange blocks}, captured in a hipGraph: launch n runs phases B, C and D of tick n — replicated on
+// every rank over the whole system, from the gathered blocks — and then phase A of tick n + 1 for
+// this rank's clusters, which writes the rank's block for the next all-gather.  The layout is the
+// workgroup-resident tick's (mcs_trade_mw.hip): one wave per cluster of the system, 4 clusters per
+// workgroup, so every rank launches the same ceil(C_t / 4) workgroups:
+//   X1  (launch start) wave 0 of every workgroup reads every cluster's post-A record from the
+//       gathered blocks (one 64-byte record per cluster, RkRec below)
+//   B   each wave, its cluster as lender (Lend, strict '>', scheduler.go:194-202) against the tick's
+//       requests in borrower order, on the lender's post-A nodes (this rank's: its LDS copy; another
+//       rank's: the gathered snapshot); only the owner rank appends to the LentQueue
+//       (server.go:80-113)
+//   C+D wave 0 of every workgroup on identical inputs: the trader rounds (trader.go:280-325,
+//       193-278; server.go:31-85) and the next tick's clock — replicated, as in the MW tick
+//   X2  every workgroup publishes its acceptances as tagged granules (uncached, write-through) and
+//       gathers everyone's: the owner moves its borrowers' WaitQueue heads to the BorrowedQueue
+//       (scheduler.go:237-242)
+//   A   tick n + 1 (tr_step_kernel's phase, scheduler.go:216-296 + the borrow request): this rank's
+//       waves; the record and the node snapshot go to the rank's block of the exchange buffer
+// The first launch of a run (mode 0) runs phase A of tick 0 only.  The state between launches
+// (nodes, running slots, queue cursors, trader state, the clock) lives in HBM, as across the MW
+// kernel's launches.  The caller-driven phase API (mcs_trade_phase) runs the same launches with the
+// caller's all-gather in between, so 2- and 4-rank runs over gloo cover this path on one GPU.
+// Same results bit for bit as the three-kernel tick and the oracle (tests/test_gpu_trade.py,
+// tests/trade_2rank.py).
+#include "mcs_trade_internal.h"
+#include "mcs_trader_dev.h"
+#include "mcs_wave.h"
+
+namespace mcs {
+namespace {
+
+constexpr int kRkWaves = 4;                // clusters (waves) per workgroup
+constexpr uint32_t kRkNodes = 256;         // nodes per cluster
+constexpr uint32_t kRkSpinLimit = 1u << 20;  // X2 sweeps before the run gives up
+static_assert(3 * ((int)kTrResMaxClusters / kRkWaves) <= kWave, "X2: one granule per lane");
+
+// a cluster's post-A record in the exchange block: 16 words, the size of TrXRec (the three-kernel
+// record), so both forms lay the blocks out alike (records, then the node snapshots)
+enum : uint32_t {
+    kRkJob = 0, kRkC, kRkM, kRkDur, kRkQs, kRkDecided, kRkNat, kRkFlags, kRkCu, kRkMu, kRkLq, kRkN, kRkTc, kRkTm,
+    kRkWords = 16
+};
+static_assert(kRkWords * 4u == sizeof(TrXRec), "record size");
+// qs bits: WaitQueue head, ReadyQueue busy, a lent run this tick, LentQueue non-empty, cluster done
+constexpr uint32_t kQsW = 1u, kQsRq = 2u, kQsLent = 4u, kQsLq = 8u, kQsDone = 16u;
+
+__device__ __forceinline__ uint32_t rk_wave_sum(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+__device__ __forceinline__ void rk_put(unsigned long long* g, uint32_t tag, uint32_t v) {
+    __hip_atomic_store(g, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr uint32_t kStW = sizeof(TrCluster) / 4u;
+static_assert(sizeof(TrCluster) % 4u == 0u && kStW <= (uint32_t)kWave, "TrCluster in one VGPR");
+struct RkField {  // a TrCluster field held in lane f of a VGPR (phase A's cluster state)
+    uint32_t& v;
+    uint32_t f, lane;
+    __device__ __forceinline__ operator uint32_t() const { return readlane(v, f); }
+    __device__ __forceinline__ RkField& operator=(uint32_t x) {
+        v = lane == f ? x : v;
+        return *this;
+    }
+    __device__ __forceinline__ RkField& operator=(const RkField& o) { return *this = (uint32_t)o; }
+    __device__ __forceinline__ RkField& operator+=(uint32_t x) { return *this = (uint32_t)*this + x; }
+    __device__ __forceinline__ RkField& operator-=(uint32_t x) { return *this = (uint32_t)*this - x; }
+    __device__ __forceinline__ RkField& operator|=(uint32_t x) { return *this = (uint32_t)*this | x; }
+    __device__ __forceinline__ RkField& operator++() { return *this += 1u; }
+    __device__ __forceinline__ RkField& operator--() { return *this -= 1u; }
+    __device__ __forceinline__ uint32_t operator++(int) {
+        const uint32_t o = *this;
+        *this = o + 1u;
+        return o;
+    }
+};
+#define RST(field) (RkField{stv, (uint32_t)(offsetof(TrCluster, field) / 4u), lane})
+
+struct RkShared {  // (the workgroup's node vectors follow: kRkWaves * ns u64)
+    // X1 of tick n, every cluster of the system (word k of cluster g at rq_job + k * 64 + g)
+    uint32_t rq_job[kTrResMaxClusters], rq_c[kTrResMaxClusters], rq_m[kTrResMaxClusters];
+    uint32_t rq_dur[kTrResMaxClusters], qs[kTrResMaxClusters], decided[kTrResMaxClusters];
+    uint32_t nat[kTrResMaxClusters], xflags[kTrResMaxClusters];
+    float cu[kTrResMaxClusters], mu[kTrResMaxClusters];
+    uint32_t lq[kTrResMaxClusters], nn[kTrResMaxClusters], total_c[kTrResMaxClusters], total_m[kTrResMaxClusters];
+    TrTrader trs[kTrResMaxClusters];  // replicated trader state
+    TrCluster st[kRkWaves];           // this workgroup's clusters (this rank's only)
+    uint32_t gtab[kRkWaves][64];
+    uint32_t accm[3];  // borrowers a lender of this workgroup accepted; [2]: an append overflowed
+    uint32_t T, T0, done, ticks, flags, tmax_now;
+    unsigned long long n_trades, n_won, n_lent, n_lent_next;
+};
+
+template <int kRows>  // slot rows per cluster (64 slots each)
+__global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, unsigned long long* gx2,
+                                                                 uint32_t mode, uint32_t nwg) {
+    if (a.ctl->done) return;  // (the graph's launches after the end of the run)
+    extern __shared__ unsigned long long rk_smem[];
+    RkShared& sh = *reinterpret_cast<RkShared*>(rk_smem);
+    unsigned long long* const nodes_wg = rk_smem + (sizeof(RkShared) + 7) / 8;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t C = a.Ct, ns = a.ns, S = a.S, Cl = a.Cl;
+    const uint32_t wg = blockIdx.x;
+    const uint32_t g = wg * kRkWaves + wave;  // this wave's cluster of the system
+    const uint32_t lo = a.rank * Cl;          // this rank's clusters: [lo, lo + Cl)
+    const bool sys = g < C;
+    const bool own = sys && g >= lo && g < lo + Cl;
+    const uint32_t c = own ? g - lo : 0u;  // its local index
+    unsigned long long* const nodes = nodes_wg + (size_t)wave * ns;
+    auto rec_of = [&](uint32_t q) -> const uint32_t* {
+        const uint32_t r = q / Cl;
+        return reinterpret_cast<const uint32_t*>(a.xb + (size_t)r * a.blk + (size_t)(q - r * Cl) * sizeof(TrXRec));
+    };
+
+    // ---- state in: the replicated trader state and clock, this rank's clusters ----
+    uint32_t N = 0, n0 = 0, J = 0;
+    uint64_t j0 = 0;
+    if (own) {
+        n0 = a.node_off[c];
+        N = a.node_off[c + 1] - n0;
+        j0 = a.job_off[c];
+        J = (uint32_t)(a.job_off[c + 1] - j0);
+        copy_rounds<4>(nodes, a.tn + n0, N, lane);
+        if (lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = reinterpret_cast<const uint32_t*>(&a.cl[c])[lane];
+    } else if (sys && mode != 0u) {  // another rank's cluster: its post-A snapshot, for phase B
+        N = rec_of(g)[kRkN];
+        copy_rounds<4>(nodes, tr_snap(a, g), N, lane);
+    }
+    for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) sh.trs[q] = a.tr[q];
+    if (threadIdx.x == 0) {
+        const TrCtl ctl = *a.ctl;
+        sh.T = sh.T0 = ctl.T;
+        sh.done = ctl.done;
+        sh.ticks = ctl.ticks;
+        sh.flags = ctl.flags;
+        sh.n_trades = ctl.n_trades;
+        sh.n_won = ctl.n_won;
+        sh.n_lent = sh.n_lent_next = ctl.n_lent;
+        sh.tmax_now = 0u;
+    }
+    // the wave's running slots in registers (row r, lane l = slot r * 64 + l): finish time and the
+    // payload node | cores << 9 | mem << 16, as the MW tick keeps them (sfin / snode across launches)
+    uint32_t fin[kRows], pay[kRows];
+    uint32_t frm = 0u;
+    const size_t sb = (size_t)c * S;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        fin[r] = own ? a.sfin[sb + r * kWave + lane] : kEmpty;
+        pay[r] = own ? a.snode[sb + r * kWave + lane] : 0u;
+        if (fin[r] == kEmpty) frm |= 1u << r;
+    }
+    // X1 of tick n: lane q of wave 0 takes cluster q's record from the gathered blocks
+    if (mode != 0u && wave == 0 && lane < C) {
+        const uint4* rp = reinterpret_cast<const uint4*>(rec_of(lane));
+        const uint4 w0 = rp[0], w1 = rp[1], w2 = rp[2], w3 = rp[3];
+        sh.rq_job[lane] = w0.x;
+        sh.rq_c[lane] = w0.y;
+        sh.rq_m[lane] = w0.z;
+        sh.rq_dur[lane] = w0.w;
+        sh.qs[lane] = w1.x;
+        sh.decided[lane] = w1.y;
+        sh.nat[lane] = w1.z;
+        sh.xflags[lane] = w1.w;
+        sh.cu[lane] = __uint_as_float(w2.x);
+        sh.mu[lane] = __uint_as_float(w2.y);
+        sh.lq[lane] = w2.z;
+        sh.nn[lane] = w2.w;
+        sh.total_c[lane] = w3.x;
+        sh.total_m[lane] = w3.y;
+    }
+    if (threadIdx.x < 3u) sh.accm[threadIdx.x] = 0u;
+    __syncthreads();
+
+    const uint4* __restrict__ jobs = a.jobs + j0;
+    uint4 hwin = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t awin = kEmpty, hwb = 0u;
+    unsigned long long lqw = 0ull;
+    auto prefetch_jobs = [&](uint32_t hb, uint32_t na) {
+        hwb = hb;
+        hwin = hb + lane < J ? jobs[hb + lane] : make_uint4(0u, 0u, 0u, 0u);
+        awin = na + lane < J ? jobs[na + lane].x : kEmpty;
+    };
+    auto prefetch_lq = [&](uint32_t lqh, uint32_t lqn) {
+        lqw = 0ull;
+        if (lqn > 0u && lane < 3u)
+            lqw = reinterpret_cast<const unsigned long long*>(a.lq + (size_t)c * a.LQ + lqh)[lane];
+    };
+    if (own) {
+        const TrCluster& s0 = sh.st[wave];
+        prefetch_jobs(s0.has_w ? s0.w : s0.rq_head, s0.next_arr);
+    }
+
+    if (mode != 0u) {
+        const uint32_t T = sh.T0;
+        // ---- the lent-run records of tick n (this rank's lenders), at indices in cluster order from
+        // the gathered lent bits: this rank's log counts its own runs (ctl->n_lent is per rank) ----
+        {
+            const unsigned long long rmask = (Cl >= 64u ? ~0ull : ((1ull << Cl) - 1ull)) << lo;
+            const unsigned long long lm = __ballot(lane < C && (sh.qs[lane] & kQsLent)) & rmask;
+            if (own && lane == 0 && (sh.qs[g] & kQsLent)) {
+                const unsigned long long idx = sh.n_lent + (uint64_t)__builtin_popcountll(lm & ((1ull << g) - 1ull));
+                if (idx < a.lent_cap) {
+                    const uint4 lr = a.lrp[c];
+                    mcs_lent_rec rec;
+                    rec.lender = g;
+                    rec.borrower = lr.x;
+                    rec.job = lr.y;
+                    rec.node = lr.z;
+                    rec.start_s = T;
+                    rec.finish_s = lr.w;
+                    rec.pad = 0u;
+                    a.lent_log[idx] = rec;
+                }
+            }
+            if (threadIdx.x == 0) sh.n_lent_next = sh.n_lent + (uint64_t)__builtin_popcountll(lm);
+        }
+        // ---- C and D: wave 0 of every workgroup, one lane per cluster, on X1 alone (as the MW tick:
+        // every borrow request leaves its borrower busy, so the clock and the end of the run follow
+        // from X1; the acceptances are applied after the X2 exchange, before phase A) ----
+        if (wave == 0) {
+            const uint32_t q = lane;
+            float cu = 0.0f, mu = 0.0f;
+            uint32_t tot_c = 0u, tot_m = 0u, busy = 0u, next_arr_t = kEmpty, done_g = 1u, fl = 0u;
+            TrTrader t{0u, 0u, 0u, kEmpty, 0u};
+            if (q < C) {
+                const uint32_t qs = sh.qs[q];
+                cu = sh.cu[q];
+                mu = sh.mu[q];
+                tot_c = sh.total_c[q];
+                tot_m = sh.total_m[q];
+                busy = (qs & (kQsW | kQsRq | kQsLq)) ? 1u : 0u;
+                next_arr_t = sh.nat[q];
+                done_g = (qs & kQsDone) ? 1u : 0u;
+                fl = sh.xflags[q];
+                t = sh.trs[q];
+            }
+            unsigned long long n_trades = sh.n_trades, n_won = sh.n_won;
+            uint32_t lflags = 0;
+            if (a.trader) {
+                const bool due = q < C && t.next_due <= T;
+                const bool broken = cu > 0.8f || mu > 0.8f;  // Utilization (trader.go:127-130)
+                if (due && !broken) t.next_due = T + a.period;
+                const bool appr = q < C && approve_trade_dev(tot_c, tot_m, cu, mu, 0u, 0u, 0u);
+                unsigned long long pend = __ballot(due && broken);
+                while (pend) {  // RequestPolicyMonitor of requester r (trader.go:282-324), index order
+                    const uint32_t r = (uint32_t)__builtin_ctzll(pend);
+                    pend &= pend - 1ull;
+                    bool app = false;
+                    if (q < C && q != r) {  // RequestResource, index order
+                        if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
+                        if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
+                            app = appr;
+                            t.lock_id = t.next_id++;  // set even when not approving (:44-46)
+                            t.lock_until = T + a.lock_s;
+                        }
+                    }
+                    const unsigned long long ab = __ballot(app);
+                    const uint32_t napp = (uint32_t)__builtin_popcountll(ab);
+                    const uint32_t winner = ab ? (uint32_t)__builtin_ctzll(ab) : kEmpty;
+                    if (winner != kEmpty) {
+                        if (q == winner) t.lock_id = 0u;  // ApproveContract unlocks (:83)
+                        if (q == r) t.vnodes += 1u;       // AddVirtualNode(0 cores, 0 memory)
+                        ++n_won;
+                    }
+                    if (q == r) t.next_due = T + (winner != kEmpty ? a.ok_sleep : a.fail_sleep) + a.period;
+                    if (lane == 0 && wg == 0) {  // (workgroup 0 keeps the log; every rank alike)
+                        if (n_trades < a.trade_cap) {
+                            mcs_trade_rec rec;
+                            rec.t_s = T;
+                            rec.requester = r;
+                            rec.winner = winner == kEmpty ? -1 : (int32_t)winner;
+                            rec.approvals = napp;
+                            a.trade_log[n_trades] = rec;
+                        }
+                    }
+                    if (n_trades >= a.trade_cap) lflags |= MCS_FLAG_LOG_OVERFLOW;
+                    ++n_trades;
+                }
+            }
+            // the next tick: T+1 while any queue is busy, else the next arrival or trader round
+            uint32_t nxt = next_arr_t;
+            if (a.trader && q < C) nxt = t.next_due < nxt ? t.next_due : nxt;
+            const bool done_all = !__ballot(!done_g);
+            const bool busy_any = __ballot(busy != 0u) != 0ull;
+            nxt = wave_min_u32(nxt);
+            for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o);
+            // (C/D reads trs[q] of its own lane only before this barrier-free store: lane q owns q)
+            if (a.trader && q < C) sh.trs[q] = t;
+            if (lane == 0) {
+                uint32_t flags = sh.flags | fl | lflags;
+                uint32_t done = 0, Tn = T;
+                const uint32_t fatal = MCS_FLAG_OVERFLOW | MCS_FLAG_LENT_OVERFLOW;
+                if (done_all || (flags & fatal)) {
+                    done = 1u;
+                } else if (T >= a.t_max || (!busy_any && nxt == kEmpty)) {
+                    done = 1u;
+                    flags |= MCS_FLAG_T_MAX;
+                    sh.tmax_now = 1u;
+                } else {
+                    Tn = (busy_any || nxt <= T + 1u) ? T + 1u : nxt;
+                }
+                sh.T = Tn;
+                sh.done = done;
+                sh.ticks += 1u;
+                sh.flags = flags;
+                sh.n_trades = n_trades;
+                sh.n_won = n_won;
+            }
+        }
+        // ---- B: this wave's cluster as lender, the tick's requests in borrower order ----
+        // (tr_lend_kernel / the MW tick: G[x] = max free_m over the nodes with free_c > x when
+        // every free_c <= 64, else a node scan per request)
+        if (sys) {
+            const uint32_t L = g;
+            uint32_t rqj = kEmpty, rqc = 0u, rqm = 0u, rqd = 0u;
+            if (lane < C) {
+                rqj = sh.rq_job[lane];
+                rqc = sh.rq_c[lane];
+                rqm = sh.rq_m[lane];
+                rqd = sh.rq_dur[lane];
+            }
+            const uint32_t NL = own ? N : sh.nn[L];
+            uint32_t* const tab = sh.gtab[wave];
+            uint32_t lq_len = own ? sh.st[wave].lq_len : sh.lq[L], fb = 0;
+            const uint32_t lq0 = lq_len;
+            const uint32_t lq_head = own ? sh.st[wave].lq_head : 0u;
+            const uint32_t LQ = a.LQ;
+            const bool want = rqj != kEmpty && lane != L;  // self skipped (:176)
+            unsigned long long okm = 0ull;
+            if (__ballot(want)) {
+                tab[lane] = 0u;
+                bool big = false;
+                for (uint32_t i = lane; i < NL; i += kWave) {
+                    const unsigned long long v = nodes[i];
+                    const uint32_t fc = (uint32_t)v;
+                    if (fc > 64u)
+                        big = true;
+                    else if (fc > 0u)
+                        atomicMax(&tab[fc - 1u], (uint32_t)(v >> 32));
+                }
+                if (!__ballot(big)) {
+                    const uint32_t gm = wave_scan_max_u32(tab[63u - lane]);  // G[63 - lane]
+                    tab[63u - lane] = gm;
+                    okm = __ballot(want && rqc < 64u && tab[rqc < 64u ? rqc : 0u] > rqm);
+                } else {
+                    unsigned long long pend = __ballot(want);
+                    while (pend) {
+                        const uint32_t bi = (uint32_t)__builtin_ctzll(pend);
+                        pend &= pend - 1ull;
+                        const uint32_t rc = readlane(rqc, bi), rm = readlane(rqm, bi);
+                        bool ok = false;
+                        for (uint32_t i0 = 0; i0 < NL; i0 += kWave) {
+                            const uint32_t i = i0 + lane;
+                            if (i < NL) {
+                                const unsigned long long v = nodes[i];
+                                ok = ok || ((uint32_t)v > rc && (uint32_t)(v >> 32) > rm);
+                            }
+                            if (__ballot(ok)) break;
+                        }
+                        if (__ballot(ok)) okm |= 1ull << bi;
+                    }
+                }
+            }
+            // appends (server.go:80-113): the first LQ - lq_len accepted, in borrower order (owner)
+            const uint32_t rank = (uint32_t)__builtin_popcountll(okm & ((1ull << lane) - 1ull));
+            if (own && ((okm >> lane) & 1ull) && lq_len + rank < LQ) {
+                uint32_t at = lq_head + lq_len + rank;
+                at = at >= LQ ? at - LQ : at;
+                TrLq e{};
+                e.borrower = lane;
+                e.job = rqj;
+                e.c = rqc;
+                e.m = rqm;
+                e.dur = rqd;
+                a.lq[(size_t)c * LQ + at] = e;
+            }
+            const uint32_t nacc = (uint32_t)__builtin_popcountll(okm);
+            if (lq_len + nacc > LQ) {
+                fb |= MCS_FLAG_LENT_OVERFLOW;
+                lq_len = LQ;
+            } else {
+                lq_len += nacc;
+            }
+            if (lane == 0) {
+                if (own) {
+                    sh.st[wave].lq_len = lq_len;
+                    sh.st[wave].flags |= fb;
+                }
+                if (okm) {
+                    atomicOr(&sh.accm[0], (uint32_t)okm);
+                    atomicOr(&sh.accm[1], (uint32_t)(okm >> 32));
+                }
+                if (fb) atomicOr(&sh.accm[2], 1u);
+            }
+            // the next tick's LentQueue head: an entry of an earlier tick is loaded; one this tick's
+            // appends just wrote (the queue was empty) is taken from the request registers
+            if (own) {
+                if (lq0 > 0u) {
+                    prefetch_lq(lq_head, lq0);
+                } else if (okm && lq_len > 0u) {
+                    const uint32_t b0 = (uint32_t)__builtin_ctzll(okm);
+                    const uint32_t j = readlane(rqj, b0), ec = readlane(rqc, b0), em = readlane(rqm, b0),
+                                   ed = readlane(rqd, b0);
+                    lqw = lane == 0 ? ((unsigned long long)j << 32 | b0)
+                        : lane == 1 ? ((unsigned long long)em << 32 | ec)
+                        : lane == 2 ? (unsigned long long)ed
+                                    : 0ull;
+                }
+            }
+        }
+        __syncthreads();
+        // ---- X2: the workgroups' acceptances (epoch: the tick, from the run's first one; no tag is 0) ----
+        const uint32_t tag2 = 2u * ((sh.ticks - 1u) % 0x7FFFFFFFu) + 2u;
+        if (wave == 0) {
+            if (lane < 3) rk_put(gx2 + 3u * wg + lane, tag2, sh.accm[lane]);
+            const uint32_t nw = 3u * nwg;
+            unsigned long long x = 0ull;
+            bool got = false;
+            for (uint32_t spins = 0; spins <= kRkSpinLimit; ++spins) {
+                x = lane < nw ? __hip_atomic_load(gx2 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : ((unsigned long long)tag2 << 32);
+                if (__all((uint32_t)(x >> 32) == tag2)) {
+                    got = true;
+                    break;
+                }
+            }
+            if (!got) {
+                if (lane == 0) sh.done = 2u;
+            } else {
+                const uint32_t v = (uint32_t)x, k = lane % 3u;
+                uint32_t m0 = lane < nw && k == 0u ? v : 0u, m1 = lane < nw && k == 1u ? v : 0u,
+                         fbx = lane < nw && k == 2u ? v : 0u;
+                for (int o = 32; o > 0; o >>= 1) {
+                    m0 |= (uint32_t)__shfl_xor((int)m0, o);
+                    m1 |= (uint32_t)__shfl_xor((int)m1, o);
+                    fbx |= (uint32_t)__shfl_xor((int)fbx, o);
+                }
+                // BorrowedQueue append, WaitQueue pop (scheduler.go:237-242): the owner's workgroup
+                const uint32_t q = lane;
+                const bool acc = ((q < 32u ? m0 >> q : m1 >> (q - 32u)) & 1u) != 0u;
+                if (acc && q < C && q / kRkWaves == wg && q >= lo && q < lo + Cl && sh.rq_job[q] != kEmpty) {
+                    const uint32_t rj = sh.rq_job[q];
+                    const uint64_t qj0 = a.job_off[q - lo];
+                    a.out_node[qj0 + rj] = MCS_NODE_BORROWED;
+                    a.out_start[qj0 + rj] = T;
+                    a.out_finish[qj0 + rj] = MCS_TIME_NONE;
+                    TrCluster& s = sh.st[q - wg * kRkWaves];
+                    s.has_w = 0u;
+                    ++s.decided;
+                    ++s.borrowed;
+                }
+                // an append overflow ends the run at tick n (clock T, no T_MAX flag of that tick)
+                if (fbx && lane == 0) {
+                    uint32_t f = sh.flags | MCS_FLAG_LENT_OVERFLOW;
+                    if (sh.tmax_now) f &= ~MCS_FLAG_T_MAX;
+                    sh.flags = f;
+                    sh.T = T;
+                    sh.done = 1u;
+                }
+            }
+            if (lane == 0) sh.n_lent = sh.n_lent_next;
+        }
+        __syncthreads();
+    }
+
+    // ---- A: tick n + 1 (tick 0 in mode 0) for this rank's clusters (tr_step_kernel) ----
+    if (own && sh.done == 0u) {
+        const uint32_t T = sh.T;
+        bool sample = false;
+        if (a.trader && T % a.sample_period == 0u) {
+            bool due = false;
+            for (uint32_t q = lane; q < C; q += kWave) due = due || sh.trs[q].next_due <= T;
+            sample = __ballot(due) != 0ull;
+        }
+        uint32_t stv = lane < kStW ? reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane] : 0u;
+        // (the WaitQueue head may have left for the BorrowedQueue in X2: the window still holds
+        // the ReadyQueue head or job_at loads it)
+        const uint32_t na0 = RST(next_arr);
+        // releases due at T (cluster.go:153-157), before the tick's decisions
+        if (RST(minf) <= T) {
+            uint32_t lm = kEmpty, nrel = 0;
+#pragma unroll
+            for (int r = 0; r < kRows; ++r) {
+                const uint32_t f = fin[r];
+                if (f <= T) {
+                    const uint32_t p = pay[r], kn = p & 511u;
+                    if (kn < N)
+                        atomicAdd(&nodes[kn], (unsigned long long)((p >> 9) & 127u) |
+                                                  ((unsigned long long)(p >> 16) << 32));
+                    fin[r] = kEmpty;
+                    frm |= 1u << r;
+                    ++nrel;
+                } else {
+                    lm = f < lm ? f : lm;
+                }
+            }
+            RST(nrun) -= rk_wave_sum(nrel);
+            RST(minf) = wave_min_u32(lm);
+        }
+        // arrivals up to T join the ReadyQueue (jobs are sorted by arrival)
+        uint32_t nat;
+        {
+            const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(awin <= T && na0 + lane < J));
+            RST(next_arr) = na0 + n;
+            if (n < (uint32_t)kWave) {
+                nat = readlane(awin, n);
+            } else {
+                while (RST(next_arr) < J) {
+                    const uint32_t i = RST(next_arr) + lane;
+                    const bool ok = i < J && jobs[i].x <= T;
+                    const uint32_t m = (uint32_t)__builtin_popcountll(__ballot(ok));
+                    RST(next_arr) += m;
+                    if (m < (uint32_t)kWave) break;
+                }
+                nat = RST(next_arr) < J ? jobs[RST(next_arr)].x : kEmpty;
+            }
+        }
+        auto job_at = [&](uint32_t j) -> uint4 {
+            const uint32_t d = j - hwb;
+            if (d < (uint32_t)kWave)
+                return make_uint4(readlane(hwin.x, d), readlane(hwin.y, d), readlane(hwin.z, d), readlane(hwin.w, d));
+            return jobs[j];
+        };
+        // ScheduleJob (scheduler.go:127-139); zero-capacity virtual nodes follow the physical ones
+        const uint32_t vn = sh.trs[g].vnodes;
+        auto first_fit = [&](uint32_t jc, uint32_t jm) -> uint32_t {
+            unsigned long long v[kRkNodes / kWave];
+#pragma unroll
+            for (uint32_t q = 0; q < kRkNodes / kWave; ++q) {
+                const uint32_t i = q * kWave + lane;
+                v[q] = i < N ? nodes[i] : 0ull;
+            }
+            uint32_t kk = kEmpty;
+#pragma unroll
+            for (uint32_t q = 0; q < kRkNodes / kWave; ++q) {
+                const uint32_t i = q * kWave + lane;
+                const unsigned long long m = __ballot(i < N && (uint32_t)v[q] >= jc && (uint32_t)(v[q] >> 32) >= jm);
+                if (m && kk == kEmpty) kk = q * kWave + (uint32_t)__builtin_ctzll(m);
+            }
+            if (kk == kEmpty && jc == 0u && jm == 0u && vn > 0u) kk = N;
+            return kk;
+        };
+        // Node.RunJob commit (cluster.go:144-148) + running-slot insert; false on overflow
+        auto commit = [&](uint32_t kn, uint32_t jc, uint32_t jm, uint32_t f) -> bool {
+            const unsigned long long need = (unsigned long long)jc | ((unsigned long long)jm << 32);
+            const unsigned long long any = __ballot(frm != 0u);
+            if (!any) return false;
+            const uint32_t sel = (uint32_t)__builtin_ctzll(any);
+            const uint32_t row = (uint32_t)__builtin_ctz(readlane(frm, sel));
+            if (lane == sel) {
+                if (kn < N) atomicSub(&nodes[kn], need);
+                const uint32_t p = (kn < N ? kn : 511u) | (jc << 9) | (jm << 16);
+#pragma unroll
+                for (int r = 0; r < kRows; ++r)
+                    if ((uint32_t)r == row) {
+                        fin[r] = f;
+                        pay[r] = p;
+                    }
+                frm &= ~(1u << row);
+            }
+            ++RST(nrun);
+            RST(peak) = RST(nrun) > RST(peak) ? RST(nrun) : RST(peak);
+            RST(minf) = f < RST(minf) ? f : RST(minf);
+            return true;
+        };
+        auto place_own = [&](uint32_t j, uint32_t kn, uint4 jb) -> bool {
+            const uint32_t f = T + jb.y;
+            if (jb.y != 0u && !commit(kn, jb.z, jb.w, f)) return false;
+            if (lane == 0) {
+                a.out_node[j0 + j] = (int32_t)kn;
+                a.out_start[j0 + j] = T;
+                a.out_finish[j0 + j] = f;
+            }
+            ++RST(placed);
+            ++RST(decided);
+            return true;
+        };
+
+        TrRecA req{kEmpty, 0u, 0u, 0u};
+        uint32_t lent_now = 0u;
+        uint4 lr = make_uint4(0u, 0u, 0u, 0u);
+        for (;;) {
+            if (RST(has_w)) {  // WaitQueue head (scheduler.go:219-251)
+                const uint4 jb = job_at(RST(w));
+                const uint32_t kn = first_fit(jb.z, jb.w);
+                if (kn != kEmpty) {
+                    if (!place_own(RST(w), kn, jb)) {
+                        RST(flags) |= MCS_FLAG_OVERFLOW;
+                        break;
+                    }
+                    RST(has_w) = 0u;
+                } else if (a.borrow) {
+                    req = TrRecA{RST(w), jb.z, jb.w, jb.y};  // BorrowResources (:234)
+                }
+                break;  // time.Sleep(1 s), :250
+            }
+            if (RST(rq_head) < RST(next_arr)) {  // ReadyQueue head (:255-272), no sleep
+                const uint32_t j = RST(rq_head)++;
+                const uint4 jb = job_at(j);
+                const uint32_t kn = first_fit(jb.z, jb.w);
+                if (kn != kEmpty) {
+                    if (!place_own(j, kn, jb)) {
+                        RST(flags) |= MCS_FLAG_OVERFLOW;
+                        break;
+                    }
+                } else {
+                    RST(has_w) = 1u;
+                    RST(w) = j;
+                    ++RST(waited);
+                }
+                continue;
+            }
+            if (RST(lq_len) > 0u) {  // LentQueue head (:277-290)
+                const uint64_t w0 = readlane((uint32_t)lqw, 0) | ((uint64_t)readlane((uint32_t)(lqw >> 32), 0) << 32);
+                const uint32_t eb = (uint32_t)w0, ej = (uint32_t)(w0 >> 32);
+                const uint32_t ec = readlane((uint32_t)lqw, 1), em = readlane((uint32_t)(lqw >> 32), 1);
+                const uint32_t ed = readlane((uint32_t)lqw, 2);
+                const uint32_t kn = first_fit(ec, em);
+                if (kn != kEmpty) {
+                    const uint32_t f = T + ed;
+                    if (ed != 0u && !commit(kn, ec, em, f)) {
+                        RST(flags) |= MCS_FLAG_OVERFLOW;
+                        break;
+                    }
+                    // the lent-run record is written by the next launch, at the index the gathered
+                    // lent bits give it
+                    lr = make_uint4(eb, ej, kn, f);
+                    lent_now = kQsLent;
+                    ++RST(lent_runs);
+                    RST(lq_head) = RST(lq_head) + 1u == a.LQ ? 0u : RST(lq_head) + 1u;
+                    --RST(lq_len);
+                }
+                break;  // sleep 1 s (:289)
+            }
+            break;  // idle sleep (:294)
+        }
+
+        // GetResourceUtilization (cluster.go:46-63) on the ticks a trader reads it: an exact integer
+        // sum (the engine's eligibility check), capacities minus free
+        if (sample) {
+            uint32_t fc = 0u, fm = 0u, cc = 0u, cm = 0u;
+            for (uint32_t i = lane; i < N; i += kWave) {
+                const unsigned long long v = nodes[i];
+                const uint2 cp = a.cap[n0 + i];
+                fc += (uint32_t)v;
+                fm += (uint32_t)(v >> 32);
+                cc += cp.x;
+                cm += cp.y;
+            }
+            const float sc = (float)(int32_t)(rk_wave_sum(cc) - rk_wave_sum(fc));
+            const float sm = (float)(int32_t)(rk_wave_sum(cm) - rk_wave_sum(fm));
+            RST(cu) = __float_as_uint(__fdiv_rn(sc, (float)RST(total_c)));
+            RST(mu) = __float_as_uint(__fdiv_rn(sm, (float)RST(total_m)));
+        }
+        // the post-A record and the node snapshot: this rank's block of the next all-gather
+        const uint32_t lql = RST(lq_len);
+        const uint32_t qs = (RST(has_w) ? kQsW : 0u) | (RST(rq_head) < RST(next_arr) ? kQsRq : 0u) | lent_now |
+                            (lql > 0u ? kQsLq : 0u) | (RST(decided) == J && lql == 0u ? kQsDone : 0u);
+        uint32_t xv = 0u;
+        xv = lane == kRkJob ? req.job : xv;
+        xv = lane == kRkC ? req.c : xv;
+        xv = lane == kRkM ? req.m : xv;
+        xv = lane == kRkDur ? req.dur : xv;
+        xv = lane == kRkQs ? qs : xv;
+        xv = lane == kRkDecided ? (uint32_t)RST(decided) : xv;
+        xv = lane == kRkNat ? nat : xv;
+        xv = lane == kRkFlags ? (uint32_t)RST(flags) : xv;
+        xv = lane == kRkCu ? (uint32_t)RST(cu) : xv;
+        xv = lane == kRkMu ? (uint32_t)RST(mu) : xv;
+        xv = lane == kRkLq ? lql : xv;
+        xv = lane == kRkN ? N : xv;
+        xv = lane == kRkTc ? (uint32_t)RST(total_c) : xv;
+        xv = lane == kRkTm ? (uint32_t)RST(total_m) : xv;
+        uint32_t* const rp = reinterpret_cast<uint32_t*>(a.xb + (size_t)a.rank * a.blk + (size_t)c * sizeof(TrXRec));
+        if (lane < kRkWords) rp[lane] = xv;
+        copy_rounds<4>(tr_snap(a, g), nodes, N, lane);
+        if (lane == 0 && lent_now) a.lrp[c] = lr;
+        if (lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stv;
+    }
+
+    // ---- state out (the next launch takes it from HBM) ----
+    if (own) {
+        copy_rounds<4>(a.tn + n0, nodes, N, lane);
+        if (lane < kStW) reinterpret_cast<uint32_t*>(&a.cl[c])[lane] = reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane];
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+            a.sfin[sb + r * kWave + lane] = fin[r];
+            a.snode[sb + r * kWave + lane] = pay[r];
+        }
+    }
+    if (wg == 0) {
+        for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) a.tr[q] = sh.trs[q];
+        if (threadIdx.x == 0) {
+            TrCtl* ctl = a.ctl;
+            ctl->T = sh.T;
+            ctl->done = sh.done == 2u ? 1u : sh.done;
+            ctl->ticks = sh.ticks;
+            ctl->flags = sh.flags | (sh.done == 2u ? kTrFlagMwTimeout : 0u);
+            ctl->n_trades = sh.n_trades;
+            ctl->n_won = sh.n_won;
+            ctl->n_lent = sh.n_lent;
+        }
+    }
+}
+
+}  // namespace
+
+size_t trade_rk_lds(uint32_t ns) { return (sizeof(RkShared) + 7) / 8 * 8 + (size_t)kRkWaves * ns * 8u; }
+
+// up to 64 clusters of the system with <= 256 nodes and 256, 512 or 1024 running slots each, any
+// world size (the engine also needs the packed slot payload and exact utilization sums)
+bool trade_rk_shape(const TradeArgs& a) {
+    return a.Ct <= kTrResMaxClusters && a.ns <= kRkNodes && a.Cl > 0u &&
+           (a.S == 4u * kWave || a.S == 8u * kWave || a.S == 16u * kWave);
+}
+
+size_t trade_rk_granules(uint32_t n_clusters) { return 3u * ((n_clusters + kRkWaves - 1u) / kRkWaves) + kWave; }
+
+hipError_t launch_trade_rk(const TradeArgs& a, unsigned long long* gx2, uint32_t mode, size_t lds, hipStream_t s) {
+    const uint32_t nwg = (a.Ct + kRkWaves - 1u) / kRkWaves;
+    const void* fn = a.S == 4u * kWave   ? (const void*)tr_rk_kernel<4>
+                     : a.S == 8u * kWave ? (const void*)tr_rk_kernel<8>
+                                         : (const void*)tr_rk_kernel<16>;
+    hipError_t st = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (st != hipSuccess) return st;
+    if (a.S == 4u * kWave)
+        hipLaunchKernelGGL(tr_rk_kernel<4>, dim3(nwg), dim3(kRkWaves * kWave), lds, s, a, gx2, mode, nwg);
+    else if (a.S == 8u * kWave)
+        hipLaunchKernelGGL(tr_rk_kernel<8>, dim3(nwg), dim3(kRkWaves * kWave), lds, s, a, gx2, mode, nwg);
+    else
+        hipLaunchKernelGGL(tr_rk_kernel<16>, dim3(nwg), dim3(kRkWaves * kWave), lds, s, a, gx2, mode, nwg);
+    return hipGetLastError();
+}
+
+}  // namespace mcs

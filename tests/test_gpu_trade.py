@@ -109,33 +109,41 @@ def test_gpu_trade_cadences_and_small_lent_queue():
         gpu_trade(arrays, streams, lent_queue_cap=1)
 
 
-def test_gpu_trade_two_ranks_one_gpu():
+@pytest.mark.parametrize("rk", ["1", "0"])
+def test_gpu_trade_two_ranks_one_gpu(rk):
     """world = 2 shards (two processes, two engines on device 0) exchanging records over gloo via
-    the caller-driven phase API == one engine holding all clusters == the oracle."""
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29581")
+    the caller-driven phase API == one engine holding all clusters == the oracle; in both tick forms:
+    the one-launch tick (MCS_TRADE_RK=1, loop_form 9: B/C/D of tick n + A of tick n + 1 per launch,
+    mcs_trade_rk.hip) and the three-kernel tick (MCS_TRADE_RK=0)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29581" if rk == "1" else "29582",
+               MCS_TRADE_RK=rk, MCS_EXPECT_FORM="9" if rk == "1" else "0")
     r = subprocess.run([sys.executable, os.path.join(HERE, "trade_2rank.py")], env=env, capture_output=True,
                        text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "TRADE-2RANK OK" in r.stdout
 
 
-def test_gpu_trade_four_ranks_one_gpu():
+@pytest.mark.parametrize("rk", ["1", "0"])
+def test_gpu_trade_four_ranks_one_gpu(rk):
     """world = 4 shards of a 64-cluster system (the C5 shape: 64 clusters, reduced jobs), four
     processes on device 0 exchanging blocks over gloo: rank offsets rank * blk beyond rank 1, the
-    replicated trader rounds and escalation on four ranks == the oracle of the whole system."""
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29585", MCS_WORLD="4",
-               MCS_TRADE_CASE="n64_hot:64:300")
+    replicated trader rounds and escalation on four ranks == the oracle of the whole system; both
+    tick forms (one launch per tick: loop_form 9; three kernels: 0)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29585" if rk == "1" else "29586", MCS_WORLD="4",
+               MCS_TRADE_CASE="n64_hot:64:300", MCS_TRADE_RK=rk, MCS_EXPECT_FORM="9" if rk == "1" else "0")
     r = subprocess.run([sys.executable, os.path.join(HERE, "trade_2rank.py")], env=env, capture_output=True,
                        text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "TRADE-2RANK OK world 4" in r.stdout
 
 
+@pytest.mark.parametrize("rk", ["1", "0"])
 @pytest.mark.parametrize("graph", ["1", "0"])
-def test_gpu_trade_rccl_loop_world1(graph, monkeypatch):
+def test_gpu_trade_rccl_loop_world1(graph, rk, monkeypatch):
     """The RCCL tick loop (one ncclAllGather per tick, mcs_trade.cpp run_rccl), captured in a hipGraph or eager, on a world-1
     communicator == the HBM-exchange loop: exercises the RCCL transport on a one-GPU box."""
     monkeypatch.setenv("MCS_RCCL_GRAPH", graph)  # 1: kernels + all-gathers captured in a hipGraph; 0: eager
+    monkeypatch.setenv("MCS_TRADE_RK", rk)  # 1: one launch per tick (loop_form 7 / 8), 0: three kernels (2 / 1)
     arrays, streams, _ = seeded_workload("n64_hot", 8, 1500)
     want = gpu_trade(arrays, streams)
     with Engine(0, borrow=True, trader=True, t_max_s=20_000_000) as eng:
@@ -144,7 +152,7 @@ def test_gpu_trade_rccl_loop_world1(graph, monkeypatch):
         eng.comm_init(Engine.comm_unique_id())
         eng.submit_jobs(streams)
         eng.run()
-        assert eng.trade_stats()["loop_form"] == (2 if graph == "1" else 1)
+        assert eng.trade_stats()["loop_form"] == ((7 if graph == "1" else 8) if rk == "1" else (2 if graph == "1" else 1))
         node, start, fin = eng.placements()
         got = dict(lent=eng.lent(), trades=eng.trades(), vn=eng.virtual_nodes(), ts=eng.trade_stats())
     np.testing.assert_array_equal(node, want["node"])
@@ -267,6 +275,41 @@ def test_gpu_trade_resident_form_by_capacity(monkeypatch):
         g = gpu_trade(arrays, streams)
         assert g["tstats"]["loop_form"] in ((4, 5) if want == 4 else (want,)), cores
         assert_trade_parity(arrays, streams, g)
+
+
+@pytest.mark.parametrize("shape,seed", [("w16s", 5), ("w16s", 17), ("mid", 3), ("w16r", 9)])
+def test_gpu_trade_one_launch_tick_fuzz(shape, seed, monkeypatch):
+    """The one-launch tick (mcs_trade_rk.hip) on the caller-driven path at world 1 (loop_form 9) over
+    kat_util's randomised systems (mixed node counts and availability, bursts, idle stretches,
+    zero-duration and zero-resource jobs) == the oracle on every output."""
+    monkeypatch.setenv("MCS_TRADE_RK", "1")
+    arrays, streams = fuzz_workload(shape, seed, n_clusters=12, J=500, blocking=False)
+    g = gpu_trade(arrays, streams, driven=True)
+    assert g["tstats"]["loop_form"] == 9, g["tstats"]["loop_form"]
+    assert_trade_parity(arrays, streams, g)
+
+
+def test_gpu_trade_one_launch_tick_c5_shape_rccl(monkeypatch):
+    """The C5 shape (64 clusters x 256 nodes, 1024 slots: 16 slot rows) through the RCCL loop of the
+    one-launch tick on a world-1 communicator (loop_form 7) == the oracle."""
+    monkeypatch.setenv("MCS_TRADE_RK", "1")
+    arrays, streams, _ = seeded_workload("n256", 64, 400)
+    want = gpu_trade(arrays, streams)
+    with Engine(0, borrow=True, trader=True, t_max_s=20_000_000) as eng:
+        eng.load_clusters(arrays)
+        eng.set_shard(0, 1)
+        eng.comm_init(Engine.comm_unique_id())
+        eng.submit_jobs(streams)
+        eng.run()
+        assert eng.trade_stats()["loop_form"] == 7, eng.trade_stats()["loop_form"]
+        node, start, fin = eng.placements()
+        lent, trades, vn = eng.lent(), eng.trades(), eng.virtual_nodes()
+    np.testing.assert_array_equal(node, want["node"])
+    np.testing.assert_array_equal(start, want["start"])
+    np.testing.assert_array_equal(fin, want["finish"])
+    assert lent_rows(lent) == lent_rows(want["lent"])
+    assert trade_rows(trades) == trade_rows(want["trades"])
+    np.testing.assert_array_equal(vn, want["virtual_nodes"])
 
 
 def test_gpu_trade_caller_driven_256_nodes_world1():

@@ -50,7 +50,8 @@ def worker(rank):
         run_lockstep(eng, torch_allgather())
         node, start, fin = eng.placements()
         mine = dict(node=node, start=start, finish=fin, lent=eng.lent(), trades=eng.trades(),
-                    vn=eng.virtual_nodes(), t_final=eng.trade_stats()["t_final"])
+                    vn=eng.virtual_nodes(), t_final=eng.trade_stats()["t_final"],
+                    form=eng.trade_stats()["loop_form"])
     # device generation keyed by the global cluster index == the host generator of the full system
     with Engine(0) as eng:
         eng.load_clusters(a)
@@ -80,6 +81,8 @@ def worker(rank):
             assert trade_rows(p["trades"]) == trade_rows(o["trades"])
             assert p["vn"].tolist() == o["virtual_nodes"].tolist()
             assert p["t_final"] == o["t_final"]
+            if os.environ.get("MCS_EXPECT_FORM"):
+                assert p["form"] == int(os.environ["MCS_EXPECT_FORM"]), p["form"]
         print("TRADE-2RANK OK", f"world {WORLD}, {C} clusters:", len(lent), "lent runs", len(o["trades"]), "trades",
               flush=True)
     dist.barrier()
