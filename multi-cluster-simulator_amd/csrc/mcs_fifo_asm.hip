@@ -97,8 +97,9 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
     "s_cbranch_scc0 mcsfa_bend_%=\n"
 
-// one pass = one decision (scheduler.go:216-296); the out-of-line paths are shared by both copies
-#define MCS_FA_PASS(W)                                                                            \
+#define MCS_FA_BODY(W, D, F)                                                                      \
+    /* ---- one pass = one decision (scheduler.go:216-296) ---- */                               \
+    "mcsfa_inner_%=:\n\t"                                                                         \
     "s_cmp_gt_u32 s45, s40\n\t" /* ready head not arrived: sleep to it */                         \
     "s_cbranch_scc1 mcsfa_arrive_%=\n\t" MCS_FA_FIT##W MCS_FA_ANYFIT##W                           \
     "s_add_u32 s55, s40, s46\n\t"                                                                 \
@@ -112,23 +113,14 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     "s_mov_b32 m0, s47\n\t"                                                                       \
     "s_add_u32 s80, s80, 1\n\t"                                                                   \
     "v_writelane_b32 v91, s54, m0\n\t"                                                            \
-    "v_writelane_b32 v92, s40, m0\n\t"
-// r05: the pass is unrolled twice, so a run of decisions takes the loop's back edge (a taken
-// branch, ~20 cycles for a lone wave) every other pass; every out-of-line path returns to the first
-// copy (the cursor, not the copy, carries the state)
-#define MCS_FA_BODY(W, D, F)                                                                      \
-    "mcsfa_inner_%=:\n\t" MCS_FA_PASS(W)                                                          \
-    "s_add_u32 s47, s47, 1\n\t" MCS_FA_REC##W                                                     \
-    "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
-    "s_cbranch_scc0 mcsfa_lexit_%=\n\t" MCS_FA_PASS(W)                                           \
+    "v_writelane_b32 v92, s40, m0\n"                                                              \
     /* next ready job; a WaitQueue head placed sleeps 1 s (:250) */                               \
     "mcsfa_placed_%=:\n\t"                                                                        \
     "s_add_u32 s47, s47, 1\n\t"                                                                   \
  MCS_FA_REC##W                                                                                   \
     "mcsfa_loopend_%=:\n\t"                                                                       \
     "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfa_inner_%=\n"                                                              \
-    "mcsfa_lexit_%=:\n\t"                                                                         \
+    "s_cbranch_scc1 mcsfa_inner_%=\n\t"                                                           \
     /* the pass bound ends here after a placed WaitQueue head (s41 = its cursor + 1 while one */  \
     /* waits): it sleeps 1 s (:250) with the batch bound restored */                             \
     "s_cmp_lg_u32 s43, 0\n\t"                                                                     \
@@ -139,12 +131,7 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     "s_mov_b32 s43, 0\n\t"                                                                        \
     "s_add_u32 s40, s40, 1\n\t"                                                                   \
     "s_cbranch_scc1 mcsfa_clkovf_%=\n\t"                                                          \
-    /* (the release test of mcsfa_adv and loopend's, so no release is one taken branch) */       \
-    "s_cmp_lt_u32 s40, s77\n\t"                                                                   \
-    "s_cbranch_scc0 mcsfa_scan_%=\n\t"                                                            \
-    "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfa_inner_%=\n\t"                                                           \
-    "s_branch mcsfa_bend_%=\n"                                                                    \
+    "s_branch mcsfa_adv_%=\n"                                                                     \
                                                                                                   \
     /* zero-duration job: committed and released before the next decision (D3) */               \
     "mcsfa_zero_%=:\n\t" MCS_FA_ZEROKX##W                                                        \
@@ -179,9 +166,9 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     /* the clock has advanced: releases at the new instant (A.2 step 1) */                       \
     "mcsfa_adv_%=:\n\t"                                                                           \
     "s_cmp_lt_u32 s40, s77\n\t" /* nothing finishes by t: no release */                          \
-    "s_cbranch_scc1 mcsfa_loopend_%=\n"                                                            \
+    "s_cbranch_scc1 mcsfa_loopend_%=\n\t"                                                         \
     /* release every running job with finish <= t (cluster.go:153-157) */                        \
-    "mcsfa_scan_%=:\n\t" MCS_FA_CNTR_##D MCS_FA_T0                                                \
+    MCS_FA_CNTR_##D MCS_FA_T0                                                                     \
     "s_max_u32 s81, s81, s80\n\t" /* peak: used only grows between releases */                   \
     "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN##W MCS_FA_SCANEND##W MCS_FA_T1("s94")                \
     /* (loopend's test, so the usual continuation is one taken branch) */                        \

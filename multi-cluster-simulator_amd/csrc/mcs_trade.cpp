@@ -38,7 +38,6 @@ struct TradeDev {
     mcs_lent_rec* lent = nullptr;
     mcs_trade_rec* trades = nullptr;
     uint4* lrp = nullptr;                // one-launch tick: pending lent-run records
-    unsigned long long* gx2 = nullptr;   // one-launch tick: X2 granules (uncached)
     bool rk = false;                     // the one-launch tick runs this system (trade_alloc)
     bool rk_started = false;             // its tick-0 phase A has run
     size_t rk_lds = 0;
@@ -115,7 +114,9 @@ int trade_alloc(mcs_engine* e) {
     HIPCHK(e, hipMalloc(&td->scm, (size_t)Cl * S * 8));
     HIPCHK(e, hipMalloc(&td->lq, (size_t)Cl * LQ * sizeof(TrLq)));
     const uint32_t ns = std::max<uint32_t>(e->tr_ns ? e->tr_ns : e->max_n, 1u);
-    const uint64_t blk = (uint64_t)Cl * sizeof(TrXRec) + (uint64_t)Cl * ns * 8u;
+    // (16-byte aligned blocks: the records are read as 16-byte vectors on every rank's block; the
+    // one-launch tick's G tables, 256 B per cluster, follow the snapshots)
+    const uint64_t blk = ((uint64_t)Cl * sizeof(TrXRec) + (uint64_t)Cl * ns * 8u + (uint64_t)Cl * 256u + 15u) & ~15ull;
     HIPCHK(e, hipMalloc(&td->xb, (size_t)e->world * blk));
     HIPCHK(e, hipMalloc(&td->acc, Ct * 4));
     HIPCHK(e, hipMalloc(&td->lqp, Ct * 4));
@@ -180,7 +181,6 @@ int trade_alloc(mcs_engine* e) {
         td->rk_lds = trade_rk_lds(ns);
         if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device) == hipSuccess &&
             td->rk_lds <= (size_t)max_lds) {
-            HIPCHK(e, hipExtMallocWithFlags((void**)&td->gx2, trade_rk_granules(Ct) * 8u, 3u));
             td->rk = true;
         }
     }
@@ -321,14 +321,14 @@ int run_rccl_rk(mcs_engine* e) {
     const TradeArgs& a = td->a;
     ncclComm_t comm = (ncclComm_t)e->comm;
     {
-        const hipError_t st = launch_trade_rk(a, td->gx2, 0u, td->rk_lds, e->stream);
+        const hipError_t st = launch_trade_rk(a, 0u, td->rk_lds, e->stream);
         if (st != hipSuccess) return hip_fail(e, "one-launch tick (tick 0)", st);
         td->rk_started = true;
     }
     auto tick = [&](hipStream_t s) -> bool {
         if (ncclAllGather(td->xb + (size_t)e->rank * a.blk, td->xb, a.blk, ncclUint8, comm, s) != ncclSuccess)
             return false;
-        return launch_trade_rk(a, td->gx2, 1u, td->rk_lds, s) == hipSuccess;
+        return launch_trade_rk(a, 1u, td->rk_lds, s) == hipSuccess;
     };
     if (!td->rgraph_tried) {
         td->rgraph_tried = true;
@@ -343,14 +343,11 @@ int run_rccl_rk(mcs_engine* e) {
                 const ncclResult_t r = ncclAllGather(td->xb + (size_t)e->rank * a.blk, td->xb, a.blk, ncclUint8,
                                                      comm, e->stream);
                 if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(exchange blocks)", r);
-                const hipError_t st = launch_trade_rk(a, td->gx2, 1u, td->rk_lds, e->stream);
+                const hipError_t st = launch_trade_rk(a, 1u, td->rk_lds, e->stream);
                 if (st != hipSuccess) return hip_fail(e, "one-launch tick", st);
             }
         }
         if (int s = poll_ctl(e)) return s;
-        // a bounded X2 sweep gave up (a worker was not resident): no rank can re-run alone
-        if (td->h_ctl->flags & kTrFlagMwTimeout)
-            return fail(e, MCS_E_HIP, "one-launch tick: the X2 exchange timed out (workgroups not co-resident)");
         if (td->h_ctl->done) return MCS_OK;
     }
 }
@@ -476,7 +473,6 @@ void trade_free(mcs_engine* e) {
     dfree(td->lent);
     dfree(td->trades);
     dfree(td->lrp);
-    dfree(td->gx2);
     if (td->h_ctl) (void)hipHostFree(td->h_ctl);
     delete td;
     e->td = nullptr;
@@ -649,7 +645,6 @@ int mcs_trade_begin(mcs_engine* e) {
     const hipError_t st = mcs::launch_trade_init(td->a, e->stream);
     if (st != hipSuccess) return mcs::hip_fail(e, "trade init", st);
     td->rk_started = false;
-    if (td->gx2) HIPCHK(e, hipMemsetAsync(td->gx2, 0, mcs::trade_rk_granules(td->a.Ct) * 8u, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));  // kernel_ms: the lock-step loop only
     td->begun = true;
@@ -667,7 +662,7 @@ int mcs_trade_xfer_bytes(mcs_engine* e, uint32_t phase, uint64_t* in_bytes, uint
     // size, as the shard helpers do.)
     const uint64_t Cl = e->C;
     const uint64_t ns = std::max<uint32_t>(e->tr_ns ? e->tr_ns : e->max_n, 1u);
-    const uint64_t blk = Cl * sizeof(mcs::TrXRec) + Cl * ns * 8u;
+    const uint64_t blk = (Cl * sizeof(mcs::TrXRec) + Cl * ns * 8u + Cl * 256u + 15u) & ~15ull;  // (as trade_alloc)
     switch (phase) {
         case 0: *in_bytes = 0; *out_bytes = blk; break;
         case 1: *in_bytes = (uint64_t)e->world * blk; *out_bytes = 0; break;
@@ -693,7 +688,7 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
         switch (phase) {
             case 0:
                 if (!td->rk_started) {
-                    hs = mcs::launch_trade_rk(a, td->gx2, 0u, td->rk_lds, e->stream);
+                    hs = mcs::launch_trade_rk(a, 0u, td->rk_lds, e->stream);
                     td->rk_started = true;
                 }
                 if (hs == hipSuccess)
@@ -701,7 +696,7 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
                 break;
             case 1:
                 hs = hipMemcpyAsync(td->xb, in, ib, hipMemcpyHostToDevice, e->stream);
-                if (hs == hipSuccess) hs = mcs::launch_trade_rk(a, td->gx2, 1u, td->rk_lds, e->stream);
+                if (hs == hipSuccess) hs = mcs::launch_trade_rk(a, 1u, td->rk_lds, e->stream);
                 break;
             case 2:
                 break;
@@ -711,8 +706,6 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
         }
         if (hs != hipSuccess) return mcs::hip_fail(e, "one-launch tick (caller-driven)", hs);
         HIPCHK(e, hipStreamSynchronize(e->stream));
-        if (phase == 3 && (td->h_ctl->flags & mcs::kTrFlagMwTimeout))
-            return fail(e, MCS_E_HIP, "one-launch tick: the X2 exchange timed out (workgroups not co-resident)");
         if (done) *done = phase == 3 ? td->h_ctl->done : 0u;
         return MCS_OK;
     }

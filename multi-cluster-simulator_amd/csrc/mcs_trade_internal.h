@@ -8,7 +8,8 @@
 // Exchange blocks, one per rank (world * blk bytes), the tick's only exchange (all-gathered once):
 //   rank r's block holds TrXRec[C_l] (the post-A record of its clusters: borrow request, queue
 //   state, utilization sample) followed by the node snapshots u64 [C_l][ns] (post-A free vectors,
-//   which every rank's lender scan reads)
+//   which every rank's lender scan reads) and, for the one-launch tick, the lenders' G tables
+//   u32 [C_l][64] (mcs_trade_rk.hip)
 // Replicated per global cluster (C_t = world * C_l); every rank computes them alike from the
 // gathered blocks:
 //   acc     u32 [C_t] "some lender accepted borrower b this tick" (phase B -> C)
@@ -156,7 +157,6 @@ constexpr uint32_t kTrFlagMwTimeout = 0x80000000u;  // internal: an exchange swe
 // blocks all-gathered between launches; mode 0 = phase A of tick 0 only
 bool trade_rk_shape(const TradeArgs& a);
 size_t trade_rk_lds(uint32_t ns);
-size_t trade_rk_granules(uint32_t n_clusters);
-hipError_t launch_trade_rk(const TradeArgs& a, unsigned long long* gx2, uint32_t mode, size_t lds, hipStream_t s);
+hipError_t launch_trade_rk(const TradeArgs& a, uint32_t mode, size_t lds, hipStream_t s);
 
 }  // namespace mcs

@@ -9,17 +9,19 @@
 // workgroup, so every rank launches the same ceil(C_t / 4) workgroups:
 //   X1  (launch start) wave 0 of every workgroup reads every cluster's post-A record from the
 //       gathered blocks (one 64-byte record per cluster, RkRec below)
-//   B   each wave, its cluster as lender (Lend, strict '>', scheduler.go:194-202) against the tick's
-//       requests in borrower order, on the lender's post-A nodes (this rank's: its LDS copy; another
-//       rank's: the gathered snapshot); only the owner rank appends to the LentQueue
-//       (server.go:80-113)
+//   B   every workgroup computes the whole tick's acceptance matrix (Lend, strict '>',
+//       scheduler.go:194-202, every lender against every request): lender L accepts (c, m) when
+//       G_L[c] > m, G_L[x] = max free_m over L's post-A nodes with free_c > x, a 64-entry table its
+//       owner builds in phase A and ships in the block (a lender with some free_c > 64 is scanned
+//       from its snapshot instead).  So the acceptances need no exchange inside the launch: every
+//       workgroup moves its own borrowers' WaitQueue heads to the BorrowedQueue
+//       (scheduler.go:237-242), every lender's wave appends to its LentQueue in borrower order
+//       (server.go:80-113, owner rank), and the append-overflow verdict is replicated
 //   C+D wave 0 of every workgroup on identical inputs: the trader rounds (trader.go:280-325,
 //       193-278; server.go:31-85) and the next tick's clock — replicated, as in the MW tick
-//   X2  every workgroup publishes its acceptances as tagged granules (uncached, write-through) and
-//       gathers everyone's: the owner moves its borrowers' WaitQueue heads to the BorrowedQueue
-//       (scheduler.go:237-242)
 //   A   tick n + 1 (tr_step_kernel's phase, scheduler.go:216-296 + the borrow request): this rank's
 //       waves; the record and the node snapshot go to the rank's block of the exchange buffer
+// The workgroups never wait for each other (no granule exchange, no co-residency requirement).
 // The first launch of a run (mode 0) runs phase A of tick 0 only.  The state between launches
 // (nodes, running slots, queue cursors, trader state, the clock) lives in HBM, as across the MW
 // kernel's launches.  The caller-driven phase API (mcs_trade_phase) runs the same launches with the
@@ -35,8 +37,7 @@ namespace {
 
 constexpr int kRkWaves = 4;                // clusters (waves) per workgroup
 constexpr uint32_t kRkNodes = 256;         // nodes per cluster
-constexpr uint32_t kRkSpinLimit = 1u << 20;  // X2 sweeps before the run gives up
-static_assert(3 * ((int)kTrResMaxClusters / kRkWaves) <= kWave, "X2: one granule per lane");
+constexpr uint32_t kRkLenders = kTrResMaxClusters / kRkWaves;  // lenders per wave in phase B
 
 // a cluster's post-A record in the exchange block: 16 words, the size of TrXRec (the three-kernel
 // record), so both forms lay the blocks out alike (records, then the node snapshots)
@@ -45,15 +46,19 @@ enum : uint32_t {
     kRkWords = 16
 };
 static_assert(kRkWords * 4u == sizeof(TrXRec), "record size");
-// qs bits: WaitQueue head, ReadyQueue busy, a lent run this tick, LentQueue non-empty, cluster done
-constexpr uint32_t kQsW = 1u, kQsRq = 2u, kQsLent = 4u, kQsLq = 8u, kQsDone = 16u;
+// qs bits: WaitQueue head, ReadyQueue busy, a lent run this tick, LentQueue non-empty, cluster done,
+// some node with free_c > 64 (no G table: phase B scans the snapshot)
+constexpr uint32_t kQsW = 1u, kQsRq = 2u, kQsLent = 4u, kQsLq = 8u, kQsDone = 16u, kQsBig = 32u;
 
 __device__ __forceinline__ uint32_t rk_wave_sum(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
     return v;
 }
-__device__ __forceinline__ void rk_put(unsigned long long* g, uint32_t tag, uint32_t v) {
-    __hip_atomic_store(g, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// cluster g's G table in its rank's block (after the records and the node snapshots)
+__device__ __forceinline__ uint32_t* rk_gtab(const TradeArgs& a, uint32_t g) {
+    const uint32_t r = g / a.Cl, c = g - r * a.Cl;
+    return reinterpret_cast<uint32_t*>(a.xb + (size_t)r * a.blk + (size_t)a.Cl * sizeof(TrXRec) +
+                                       (size_t)a.Cl * a.ns * 8u) + (size_t)c * 64u;
 }
 
 constexpr uint32_t kStW = sizeof(TrCluster) / 4u;
@@ -90,14 +95,13 @@ struct RkShared {  // (the workgroup's node vectors follow: kRkWaves * ns u64)
     TrTrader trs[kTrResMaxClusters];  // replicated trader state
     TrCluster st[kRkWaves];           // this workgroup's clusters (this rank's only)
     uint32_t gtab[kRkWaves][64];
-    uint32_t accm[3];  // borrowers a lender of this workgroup accepted; [2]: an append overflowed
+    uint32_t accm[3];  // borrowers some lender accepted (the whole system's); [2]: an append overflowed
     uint32_t T, T0, done, ticks, flags, tmax_now;
     unsigned long long n_trades, n_won, n_lent, n_lent_next;
 };
 
 template <int kRows>  // slot rows per cluster (64 slots each)
-__global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, unsigned long long* gx2,
-                                                                 uint32_t mode, uint32_t nwg) {
+__global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, uint32_t mode) {
     if (a.ctl->done) return;  // (the graph's launches after the end of the run)
     extern __shared__ unsigned long long rk_smem[];
     RkShared& sh = *reinterpret_cast<RkShared*>(rk_smem);
@@ -126,9 +130,6 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, un
         J = (uint32_t)(a.job_off[c + 1] - j0);
         copy_rounds<4>(nodes, a.tn + n0, N, lane);
         if (lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = reinterpret_cast<const uint32_t*>(&a.cl[c])[lane];
-    } else if (sys && mode != 0u) {  // another rank's cluster: its post-A snapshot, for phase B
-        N = rec_of(g)[kRkN];
-        copy_rounds<4>(nodes, tr_snap(a, g), N, lane);
     }
     for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) sh.trs[q] = a.tr[q];
     if (threadIdx.x == 0) {
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, un
     // the wave's running slots in registers (row r, lane l = slot r * 64 + l): finish time and the
     // payload node | cores << 9 | mem << 16, as the MW tick keeps them (sfin / snode across launches)
     uint32_t fin[kRows], pay[kRows];
-    uint32_t frm = 0u;
+    uint32_t frm = 0u, drt = 0u;  // free rows; rows this lane changed (only those are stored back)
     const size_t sb = (size_t)c * S;
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
@@ -311,43 +312,41 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, un
                 sh.n_won = n_won;
             }
         }
-        // ---- B: this wave's cluster as lender, the tick's requests in borrower order ----
-        // (tr_lend_kernel / the MW tick: G[x] = max free_m over the nodes with free_c > x when
-        // every free_c <= 64, else a node scan per request)
-        if (sys) {
-            const uint32_t L = g;
-            uint32_t rqj = kEmpty, rqc = 0u, rqm = 0u, rqd = 0u;
-            if (lane < C) {
-                rqj = sh.rq_job[lane];
-                rqc = sh.rq_c[lane];
-                rqm = sh.rq_m[lane];
-                rqd = sh.rq_dur[lane];
+        // ---- B (replicated in every workgroup): the acceptance matrix of tick n.  Wave w takes
+        // lenders w, w + 4, ...; lane b holds borrower b's request.  Lender L accepts b when
+        // G_L[c_b] > m_b (free_c > c_b and free_m > m_b on some node; c_b >= 64 fits no node of a
+        // lender whose free_c are all <= 64); a "big" lender is scanned from its snapshot ----
+        uint32_t rqj = kEmpty, rqc = 0u, rqm = 0u, rqd = 0u;
+        if (lane < C) {
+            rqj = sh.rq_job[lane];
+            rqc = sh.rq_c[lane];
+            rqm = sh.rq_m[lane];
+            rqd = sh.rq_dur[lane];
+        }
+        const bool want = rqj != kEmpty;
+        if (__ballot(want)) {
+            // every G-table read of the wave issued before the first compare (one round trip)
+            uint32_t gv[kRkLenders];
+#pragma unroll
+            for (uint32_t k = 0; k < kRkLenders; ++k) {
+                const uint32_t L = wave + k * (uint32_t)kRkWaves;
+                gv[k] = 0u;
+                if (L < C && want && lane != L && rqc < 64u && !(sh.qs[L] & kQsBig)) gv[k] = rk_gtab(a, L)[rqc];
             }
-            const uint32_t NL = own ? N : sh.nn[L];
-            uint32_t* const tab = sh.gtab[wave];
-            uint32_t lq_len = own ? sh.st[wave].lq_len : sh.lq[L], fb = 0;
-            const uint32_t lq0 = lq_len;
-            const uint32_t lq_head = own ? sh.st[wave].lq_head : 0u;
-            const uint32_t LQ = a.LQ;
-            const bool want = rqj != kEmpty && lane != L;  // self skipped (:176)
-            unsigned long long okm = 0ull;
-            if (__ballot(want)) {
-                tab[lane] = 0u;
-                bool big = false;
-                for (uint32_t i = lane; i < NL; i += kWave) {
-                    const unsigned long long v = nodes[i];
-                    const uint32_t fc = (uint32_t)v;
-                    if (fc > 64u)
-                        big = true;
-                    else if (fc > 0u)
-                        atomicMax(&tab[fc - 1u], (uint32_t)(v >> 32));
-                }
-                if (!__ballot(big)) {
-                    const uint32_t gm = wave_scan_max_u32(tab[63u - lane]);  // G[63 - lane]
-                    tab[63u - lane] = gm;
-                    okm = __ballot(want && rqc < 64u && tab[rqc < 64u ? rqc : 0u] > rqm);
+            uint32_t accw0 = 0u, accw1 = 0u, fbw = 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < kRkLenders; ++k) {
+                const uint32_t L = wave + k * (uint32_t)kRkWaves;
+                if (L >= C) break;
+                const bool want_l = want && lane != L;  // self skipped (:176)
+                unsigned long long okm;
+                if (!(sh.qs[L] & kQsBig)) {
+                    okm = __ballot(want_l && rqc < 64u && gv[k] > rqm);
                 } else {
-                    unsigned long long pend = __ballot(want);
+                    okm = 0ull;
+                    const unsigned long long* sn = tr_snap(a, L);
+                    const uint32_t NL = sh.nn[L];
+                    unsigned long long pend = __ballot(want_l);
                     while (pend) {
                         const uint32_t bi = (uint32_t)__builtin_ctzll(pend);
                         pend &= pend - 1ull;
@@ -356,7 +355,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, un
                         for (uint32_t i0 = 0; i0 < NL; i0 += kWave) {
                             const uint32_t i = i0 + lane;
                             if (i < NL) {
-                                const unsigned long long v = nodes[i];
+                                const unsigned long long v = sn[i];
                                 ok = ok || ((uint32_t)v > rc && (uint32_t)(v >> 32) > rm);
                             }
                             if (__ballot(ok)) break;
@@ -364,105 +363,82 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, un
                         if (__ballot(ok)) okm |= 1ull << bi;
                     }
                 }
-            }
-            // appends (server.go:80-113): the first LQ - lq_len accepted, in borrower order (owner)
-            const uint32_t rank = (uint32_t)__builtin_popcountll(okm & ((1ull << lane) - 1ull));
-            if (own && ((okm >> lane) & 1ull) && lq_len + rank < LQ) {
-                uint32_t at = lq_head + lq_len + rank;
-                at = at >= LQ ? at - LQ : at;
-                TrLq e{};
-                e.borrower = lane;
-                e.job = rqj;
-                e.c = rqc;
-                e.m = rqm;
-                e.dur = rqd;
-                a.lq[(size_t)c * LQ + at] = e;
-            }
-            const uint32_t nacc = (uint32_t)__builtin_popcountll(okm);
-            if (lq_len + nacc > LQ) {
-                fb |= MCS_FLAG_LENT_OVERFLOW;
-                lq_len = LQ;
-            } else {
-                lq_len += nacc;
+                const uint32_t nacc = (uint32_t)__builtin_popcountll(okm);
+                const uint32_t lq0 = sh.lq[L];  // (post-A; == the owner's own count)
+                const uint32_t LQ = a.LQ;
+                if (lq0 + nacc > LQ) fbw = 1u;
+                accw0 |= (uint32_t)okm;
+                accw1 |= (uint32_t)(okm >> 32);
+                if (L == g && own) {  // the lender's own wave: appends in borrower order (owner rank)
+                    const uint32_t lq_head = sh.st[wave].lq_head;
+                    const uint32_t rank = (uint32_t)__builtin_popcountll(okm & ((1ull << lane) - 1ull));
+                    if (((okm >> lane) & 1ull) && lq0 + rank < LQ) {
+                        uint32_t at = lq_head + lq0 + rank;
+                        at = at >= LQ ? at - LQ : at;
+                        TrLq e{};
+                        e.borrower = lane;
+                        e.job = rqj;
+                        e.c = rqc;
+                        e.m = rqm;
+                        e.dur = rqd;
+                        a.lq[(size_t)c * LQ + at] = e;
+                    }
+                    const uint32_t lq_len = lq0 + nacc > LQ ? LQ : lq0 + nacc;
+                    if (lane == 0) {
+                        sh.st[wave].lq_len = lq_len;
+                        if (lq0 + nacc > LQ) sh.st[wave].flags |= MCS_FLAG_LENT_OVERFLOW;
+                    }
+                    // the next tick's LentQueue head: an entry of an earlier tick is loaded; one this
+                    // tick's appends just wrote (the queue was empty) comes from the request registers
+                    if (lq0 > 0u) {
+                        prefetch_lq(lq_head, lq0);
+                    } else if (okm && lq_len > 0u) {
+                        const uint32_t b0 = (uint32_t)__builtin_ctzll(okm);
+                        const uint32_t j = readlane(rqj, b0), ec = readlane(rqc, b0), em = readlane(rqm, b0),
+                                       ed = readlane(rqd, b0);
+                        lqw = lane == 0 ? ((unsigned long long)j << 32 | b0)
+                            : lane == 1 ? ((unsigned long long)em << 32 | ec)
+                            : lane == 2 ? (unsigned long long)ed
+                                        : 0ull;
+                    }
+                }
             }
             if (lane == 0) {
-                if (own) {
-                    sh.st[wave].lq_len = lq_len;
-                    sh.st[wave].flags |= fb;
-                }
-                if (okm) {
-                    atomicOr(&sh.accm[0], (uint32_t)okm);
-                    atomicOr(&sh.accm[1], (uint32_t)(okm >> 32));
-                }
-                if (fb) atomicOr(&sh.accm[2], 1u);
+                if (accw0) atomicOr(&sh.accm[0], accw0);
+                if (accw1) atomicOr(&sh.accm[1], accw1);
+                if (fbw) atomicOr(&sh.accm[2], 1u);
             }
-            // the next tick's LentQueue head: an entry of an earlier tick is loaded; one this tick's
-            // appends just wrote (the queue was empty) is taken from the request registers
-            if (own) {
-                if (lq0 > 0u) {
-                    prefetch_lq(lq_head, lq0);
-                } else if (okm && lq_len > 0u) {
-                    const uint32_t b0 = (uint32_t)__builtin_ctzll(okm);
-                    const uint32_t j = readlane(rqj, b0), ec = readlane(rqc, b0), em = readlane(rqm, b0),
-                                   ed = readlane(rqd, b0);
-                    lqw = lane == 0 ? ((unsigned long long)j << 32 | b0)
-                        : lane == 1 ? ((unsigned long long)em << 32 | ec)
-                        : lane == 2 ? (unsigned long long)ed
-                                    : 0ull;
-                }
-            }
+        } else if (own && sh.st[wave].lq_len > 0u) {
+            prefetch_lq(sh.st[wave].lq_head, sh.st[wave].lq_len);
         }
         __syncthreads();
-        // ---- X2: the workgroups' acceptances (epoch: the tick, from the run's first one; no tag is 0) ----
-        const uint32_t tag2 = 2u * ((sh.ticks - 1u) % 0x7FFFFFFFu) + 2u;
+        // ---- the acceptances (identical in every workgroup and on every rank): BorrowedQueue append,
+        // WaitQueue pop (scheduler.go:237-242) for this workgroup's own borrowers; an append overflow
+        // ends the run at tick n (clock T, no T_MAX flag of that tick) ----
         if (wave == 0) {
-            if (lane < 3) rk_put(gx2 + 3u * wg + lane, tag2, sh.accm[lane]);
-            const uint32_t nw = 3u * nwg;
-            unsigned long long x = 0ull;
-            bool got = false;
-            for (uint32_t spins = 0; spins <= kRkSpinLimit; ++spins) {
-                x = lane < nw ? __hip_atomic_load(gx2 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                              : ((unsigned long long)tag2 << 32);
-                if (__all((uint32_t)(x >> 32) == tag2)) {
-                    got = true;
-                    break;
-                }
+            const uint32_t q = lane;
+            const bool acc = ((q < 32u ? sh.accm[0] >> q : sh.accm[1] >> (q - 32u)) & 1u) != 0u;
+            if (acc && q < C && q / kRkWaves == wg && q >= lo && q < lo + Cl && sh.rq_job[q] != kEmpty) {
+                const uint32_t rj = sh.rq_job[q];
+                const uint64_t qj0 = a.job_off[q - lo];
+                a.out_node[qj0 + rj] = MCS_NODE_BORROWED;
+                a.out_start[qj0 + rj] = T;
+                a.out_finish[qj0 + rj] = MCS_TIME_NONE;
+                TrCluster& s = sh.st[q - wg * kRkWaves];
+                s.has_w = 0u;
+                ++s.decided;
+                ++s.borrowed;
             }
-            if (!got) {
-                if (lane == 0) sh.done = 2u;
-            } else {
-                const uint32_t v = (uint32_t)x, k = lane % 3u;
-                uint32_t m0 = lane < nw && k == 0u ? v : 0u, m1 = lane < nw && k == 1u ? v : 0u,
-                         fbx = lane < nw && k == 2u ? v : 0u;
-                for (int o = 32; o > 0; o >>= 1) {
-                    m0 |= (uint32_t)__shfl_xor((int)m0, o);
-                    m1 |= (uint32_t)__shfl_xor((int)m1, o);
-                    fbx |= (uint32_t)__shfl_xor((int)fbx, o);
-                }
-                // BorrowedQueue append, WaitQueue pop (scheduler.go:237-242): the owner's workgroup
-                const uint32_t q = lane;
-                const bool acc = ((q < 32u ? m0 >> q : m1 >> (q - 32u)) & 1u) != 0u;
-                if (acc && q < C && q / kRkWaves == wg && q >= lo && q < lo + Cl && sh.rq_job[q] != kEmpty) {
-                    const uint32_t rj = sh.rq_job[q];
-                    const uint64_t qj0 = a.job_off[q - lo];
-                    a.out_node[qj0 + rj] = MCS_NODE_BORROWED;
-                    a.out_start[qj0 + rj] = T;
-                    a.out_finish[qj0 + rj] = MCS_TIME_NONE;
-                    TrCluster& s = sh.st[q - wg * kRkWaves];
-                    s.has_w = 0u;
-                    ++s.decided;
-                    ++s.borrowed;
-                }
-                // an append overflow ends the run at tick n (clock T, no T_MAX flag of that tick)
-                if (fbx && lane == 0) {
+            if (lane == 0) {
+                if (sh.accm[2]) {
                     uint32_t f = sh.flags | MCS_FLAG_LENT_OVERFLOW;
                     if (sh.tmax_now) f &= ~MCS_FLAG_T_MAX;
                     sh.flags = f;
                     sh.T = T;
                     sh.done = 1u;
                 }
+                sh.n_lent = sh.n_lent_next;
             }
-            if (lane == 0) sh.n_lent = sh.n_lent_next;
         }
         __syncthreads();
     }
@@ -493,6 +469,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, un
                                                   ((unsigned long long)(p >> 16) << 32));
                     fin[r] = kEmpty;
                     frm |= 1u << r;
+                    drt |= 1u << r;
                     ++nrel;
                 } else {
                     lm = f < lm ? f : lm;
@@ -561,6 +538,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, un
                         pay[r] = p;
                     }
                 frm &= ~(1u << row);
+                drt |= 1u << row;
             }
             ++RST(nrun);
             RST(peak) = RST(nrun) > RST(peak) ? RST(nrun) : RST(peak);
@@ -656,10 +634,26 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, un
             RST(cu) = __float_as_uint(__fdiv_rn(sc, (float)RST(total_c)));
             RST(mu) = __float_as_uint(__fdiv_rn(sm, (float)RST(total_m)));
         }
+        // the lender's G table of the post-A nodes (phase B of the next launch, every workgroup):
+        // G[x] = max free_m over the nodes with free_c > x, x < 64; "big" when some free_c > 64
+        uint32_t* const tab = sh.gtab[wave];
+        tab[lane] = 0u;
+        bool big = false;
+        for (uint32_t i = lane; i < N; i += kWave) {
+            const unsigned long long v = nodes[i];
+            const uint32_t fc = (uint32_t)v;
+            if (fc > 64u)
+                big = true;
+            else if (fc > 0u)
+                atomicMax(&tab[fc - 1u], (uint32_t)(v >> 32));
+        }
+        const bool bigw = __ballot(big) != 0ull;
+        rk_gtab(a, g)[63u - lane] = wave_scan_max_u32(tab[63u - lane]);  // G[63 - lane]
         // the post-A record and the node snapshot: this rank's block of the next all-gather
         const uint32_t lql = RST(lq_len);
         const uint32_t qs = (RST(has_w) ? kQsW : 0u) | (RST(rq_head) < RST(next_arr) ? kQsRq : 0u) | lent_now |
-                            (lql > 0u ? kQsLq : 0u) | (RST(decided) == J && lql == 0u ? kQsDone : 0u);
+                            (lql > 0u ? kQsLq : 0u) | (RST(decided) == J && lql == 0u ? kQsDone : 0u) |
+                            (bigw ? kQsBig : 0u);
         uint32_t xv = 0u;
         xv = lane == kRkJob ? req.job : xv;
         xv = lane == kRkC ? req.c : xv;
@@ -677,7 +671,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, un
         xv = lane == kRkTm ? (uint32_t)RST(total_m) : xv;
         uint32_t* const rp = reinterpret_cast<uint32_t*>(a.xb + (size_t)a.rank * a.blk + (size_t)c * sizeof(TrXRec));
         if (lane < kRkWords) rp[lane] = xv;
-        copy_rounds<4>(tr_snap(a, g), nodes, N, lane);
+        if (bigw) copy_rounds<4>(tr_snap(a, g), nodes, N, lane);  // (read only for a big lender)
         if (lane == 0 && lent_now) a.lrp[c] = lr;
         if (lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stv;
     }
@@ -688,8 +682,10 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, un
         if (lane < kStW) reinterpret_cast<uint32_t*>(&a.cl[c])[lane] = reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane];
 #pragma unroll
         for (int r = 0; r < kRows; ++r) {
-            a.sfin[sb + r * kWave + lane] = fin[r];
-            a.snode[sb + r * kWave + lane] = pay[r];
+            if ((drt >> r) & 1u) {
+                a.sfin[sb + r * kWave + lane] = fin[r];
+                a.snode[sb + r * kWave + lane] = pay[r];
+            }
         }
     }
     if (wg == 0) {
@@ -718,9 +714,7 @@ bool trade_rk_shape(const TradeArgs& a) {
            (a.S == 4u * kWave || a.S == 8u * kWave || a.S == 16u * kWave);
 }
 
-size_t trade_rk_granules(uint32_t n_clusters) { return 3u * ((n_clusters + kRkWaves - 1u) / kRkWaves) + kWave; }
-
-hipError_t launch_trade_rk(const TradeArgs& a, unsigned long long* gx2, uint32_t mode, size_t lds, hipStream_t s) {
+hipError_t launch_trade_rk(const TradeArgs& a, uint32_t mode, size_t lds, hipStream_t s) {
     const uint32_t nwg = (a.Ct + kRkWaves - 1u) / kRkWaves;
     const void* fn = a.S == 4u * kWave   ? (const void*)tr_rk_kernel<4>
                      : a.S == 8u * kWave ? (const void*)tr_rk_kernel<8>
@@ -728,11 +722,11 @@ hipError_t launch_trade_rk(const TradeArgs& a, unsigned long long* gx2, uint32_t
     hipError_t st = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (st != hipSuccess) return st;
     if (a.S == 4u * kWave)
-        hipLaunchKernelGGL(tr_rk_kernel<4>, dim3(nwg), dim3(kRkWaves * kWave), lds, s, a, gx2, mode, nwg);
+        hipLaunchKernelGGL(tr_rk_kernel<4>, dim3(nwg), dim3(kRkWaves * kWave), lds, s, a, mode);
     else if (a.S == 8u * kWave)
-        hipLaunchKernelGGL(tr_rk_kernel<8>, dim3(nwg), dim3(kRkWaves * kWave), lds, s, a, gx2, mode, nwg);
+        hipLaunchKernelGGL(tr_rk_kernel<8>, dim3(nwg), dim3(kRkWaves * kWave), lds, s, a, mode);
     else
-        hipLaunchKernelGGL(tr_rk_kernel<16>, dim3(nwg), dim3(kRkWaves * kWave), lds, s, a, gx2, mode, nwg);
+        hipLaunchKernelGGL(tr_rk_kernel<16>, dim3(nwg), dim3(kRkWaves * kWave), lds, s, a, mode);
     return hipGetLastError();
 }
 
