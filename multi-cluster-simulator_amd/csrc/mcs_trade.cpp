@@ -40,6 +40,7 @@ struct TradeDev {
     uint4* lrp = nullptr;                // one-launch tick: pending lent-run records
     bool rk = false;                     // the one-launch tick runs this system (trade_alloc)
     bool rk_started = false;             // its tick-0 phase A has run
+    uint64_t rk_tick = 0;                // one-launch ticks launched (the exchange buffer's parity)
     size_t rk_lds = 0;
     TrCtl* h_ctl = nullptr;  // pinned
     hipGraphExec_t graph = nullptr;
@@ -117,7 +118,8 @@ int trade_alloc(mcs_engine* e) {
     // (16-byte aligned blocks: the records are read as 16-byte vectors on every rank's block; the
     // one-launch tick's G tables, 256 B per cluster, follow the snapshots)
     const uint64_t blk = ((uint64_t)Cl * sizeof(TrXRec) + (uint64_t)Cl * ns * 8u + (uint64_t)Cl * 256u + 15u) & ~15ull;
-    HIPCHK(e, hipMalloc(&td->xb, (size_t)e->world * blk));
+    // (two buffers of world blocks: the one-launch tick alternates them by tick parity)
+    HIPCHK(e, hipMalloc(&td->xb, 2u * (size_t)e->world * blk));
     HIPCHK(e, hipMalloc(&td->acc, Ct * 4));
     HIPCHK(e, hipMalloc(&td->lqp, Ct * 4));
     HIPCHK(e, hipMalloc(&td->fb, Ct * 4));
@@ -325,9 +327,16 @@ int run_rccl_rk(mcs_engine* e) {
         if (st != hipSuccess) return hip_fail(e, "one-launch tick (tick 0)", st);
         td->rk_started = true;
     }
+    // tick n gathers buffer n & 1 (a graph replays kGraphTicks ticks, an even count, so the parity
+    // of a captured tick is that of its index in the graph)
+    const size_t xbuf = (size_t)e->world * a.blk;
+    uint32_t cap_t = 0;
+    auto gather = [&](uint64_t t, hipStream_t s) -> ncclResult_t {
+        unsigned char* xb = td->xb + (size_t)(t & 1u) * xbuf;
+        return ncclAllGather(xb + (size_t)e->rank * a.blk, xb, a.blk, ncclUint8, comm, s);
+    };
     auto tick = [&](hipStream_t s) -> bool {
-        if (ncclAllGather(td->xb + (size_t)e->rank * a.blk, td->xb, a.blk, ncclUint8, comm, s) != ncclSuccess)
-            return false;
+        if (gather(cap_t++, s) != ncclSuccess) return false;
         return launch_trade_rk(a, 1u, td->rk_lds, s) == hipSuccess;
     };
     if (!td->rgraph_tried) {
@@ -340,8 +349,7 @@ int run_rccl_rk(mcs_engine* e) {
             HIPCHK(e, hipGraphLaunch(td->rgraph, e->stream));
         } else {
             for (uint32_t t = 0; t < kGraphTicks; ++t) {
-                const ncclResult_t r = ncclAllGather(td->xb + (size_t)e->rank * a.blk, td->xb, a.blk, ncclUint8,
-                                                     comm, e->stream);
+                const ncclResult_t r = gather(t, e->stream);
                 if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(exchange blocks)", r);
                 const hipError_t st = launch_trade_rk(a, 1u, td->rk_lds, e->stream);
                 if (st != hipSuccess) return hip_fail(e, "one-launch tick", st);
@@ -645,6 +653,7 @@ int mcs_trade_begin(mcs_engine* e) {
     const hipError_t st = mcs::launch_trade_init(td->a, e->stream);
     if (st != hipSuccess) return mcs::hip_fail(e, "trade init", st);
     td->rk_started = false;
+    td->rk_tick = 0;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));  // kernel_ms: the lock-step loop only
     td->begun = true;
@@ -685,6 +694,7 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
     if (td->rk) {  // the one-launch tick: phase 1 runs B/C/D of tick n and A of tick n + 1
         td->loop_form = mcs::kLoopRkDriven;
         hipError_t hs = hipSuccess;
+        unsigned char* const xb = td->xb + (size_t)(td->rk_tick & 1u) * ((size_t)e->world * a.blk);  // tick n's buffer
         switch (phase) {
             case 0:
                 if (!td->rk_started) {
@@ -692,11 +702,12 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
                     td->rk_started = true;
                 }
                 if (hs == hipSuccess)
-                    hs = hipMemcpyAsync(out, td->xb + (size_t)e->rank * a.blk, ob, hipMemcpyDeviceToHost, e->stream);
+                    hs = hipMemcpyAsync(out, xb + (size_t)e->rank * a.blk, ob, hipMemcpyDeviceToHost, e->stream);
                 break;
             case 1:
-                hs = hipMemcpyAsync(td->xb, in, ib, hipMemcpyHostToDevice, e->stream);
+                hs = hipMemcpyAsync(xb, in, ib, hipMemcpyHostToDevice, e->stream);
                 if (hs == hipSuccess) hs = mcs::launch_trade_rk(a, 1u, td->rk_lds, e->stream);
+                ++td->rk_tick;
                 break;
             case 2:
                 break;

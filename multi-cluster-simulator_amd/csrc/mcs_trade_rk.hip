@@ -54,11 +54,31 @@ __device__ __forceinline__ uint32_t rk_wave_sum(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
     return v;
 }
-// cluster g's G table in its rank's block (after the records and the node snapshots)
-__device__ __forceinline__ uint32_t* rk_gtab(const TradeArgs& a, uint32_t g) {
-    const uint32_t r = g / a.Cl, c = g - r * a.Cl;
-    return reinterpret_cast<uint32_t*>(a.xb + (size_t)r * a.blk + (size_t)a.Cl * sizeof(TrXRec) +
-                                       (size_t)a.Cl * a.ns * 8u) + (size_t)c * 64u;
+// The exchange blocks are double-buffered by tick parity: launch n reads tick n's blocks (buffer
+// n & 1, gathered) while its phase A writes tick n + 1's (buffer (n + 1) & 1), so a workgroup that
+// reaches phase A early never overwrites a record, G table or snapshot another workgroup of the
+// launch is still reading (the workgroups do not wait for each other).
+// cluster g's record, node snapshot and G table in the buffer at xb (its rank's block: the records,
+// then the snapshots, then the G tables)
+__device__ __forceinline__ unsigned char* rk_blk(const TradeArgs& a, unsigned char* xb, uint32_t g, uint32_t* c) {
+    const uint32_t r = g / a.Cl;
+    *c = g - r * a.Cl;
+    return xb + (size_t)r * a.blk;
+}
+__device__ __forceinline__ uint32_t* rk_rec(const TradeArgs& a, unsigned char* xb, uint32_t g) {
+    uint32_t c;
+    unsigned char* b = rk_blk(a, xb, g, &c);
+    return reinterpret_cast<uint32_t*>(b + (size_t)c * sizeof(TrXRec));
+}
+__device__ __forceinline__ unsigned long long* rk_snap(const TradeArgs& a, unsigned char* xb, uint32_t g) {
+    uint32_t c;
+    unsigned char* b = rk_blk(a, xb, g, &c);
+    return reinterpret_cast<unsigned long long*>(b + (size_t)a.Cl * sizeof(TrXRec)) + (size_t)c * a.ns;
+}
+__device__ __forceinline__ uint32_t* rk_gtab(const TradeArgs& a, unsigned char* xb, uint32_t g) {
+    uint32_t c;
+    unsigned char* b = rk_blk(a, xb, g, &c);
+    return reinterpret_cast<uint32_t*>(b + (size_t)a.Cl * sizeof(TrXRec) + (size_t)a.Cl * a.ns * 8u) + (size_t)c * 64u;
 }
 
 constexpr uint32_t kStW = sizeof(TrCluster) / 4u;
@@ -115,10 +135,11 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     const bool own = sys && g >= lo && g < lo + Cl;
     const uint32_t c = own ? g - lo : 0u;  // its local index
     unsigned long long* const nodes = nodes_wg + (size_t)wave * ns;
-    auto rec_of = [&](uint32_t q) -> const uint32_t* {
-        const uint32_t r = q / Cl;
-        return reinterpret_cast<const uint32_t*>(a.xb + (size_t)r * a.blk + (size_t)(q - r * Cl) * sizeof(TrXRec));
-    };
+    // tick n's blocks (read) and tick n + 1's (written); mode 0 writes tick 0's
+    const uint32_t n_tick = a.ctl->ticks;
+    const size_t xbuf = (size_t)a.world * a.blk;
+    unsigned char* const xr = a.xb + (size_t)(n_tick & 1u) * xbuf;
+    unsigned char* const xw = a.xb + (size_t)((mode == 0u ? 0u : n_tick + 1u) & 1u) * xbuf;
 
     // ---- state in: the replicated trader state and clock, this rank's clusters ----
     uint32_t N = 0, n0 = 0, J = 0;
@@ -156,7 +177,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     }
     // X1 of tick n: lane q of wave 0 takes cluster q's record from the gathered blocks
     if (mode != 0u && wave == 0 && lane < C) {
-        const uint4* rp = reinterpret_cast<const uint4*>(rec_of(lane));
+        const uint4* rp = reinterpret_cast<const uint4*>(rk_rec(a, xr, lane));
         const uint4 w0 = rp[0], w1 = rp[1], w2 = rp[2], w3 = rp[3];
         sh.rq_job[lane] = w0.x;
         sh.rq_c[lane] = w0.y;
@@ -190,9 +211,13 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         if (lqn > 0u && lane < 3u)
             lqw = reinterpret_cast<const unsigned long long*>(a.lq + (size_t)c * a.LQ + lqh)[lane];
     };
+    // (both windows in flight from here: the job records of the next phase A, and the LentQueue head
+    // when the queue already held entries after tick n's phase A; one this launch's appends write into
+    // an empty queue is taken from the request registers in phase B)
     if (own) {
         const TrCluster& s0 = sh.st[wave];
         prefetch_jobs(s0.has_w ? s0.w : s0.rq_head, s0.next_arr);
+        prefetch_lq(s0.lq_head, s0.lq_len);
     }
 
     if (mode != 0u) {
@@ -331,7 +356,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             for (uint32_t k = 0; k < kRkLenders; ++k) {
                 const uint32_t L = wave + k * (uint32_t)kRkWaves;
                 gv[k] = 0u;
-                if (L < C && want && lane != L && rqc < 64u && !(sh.qs[L] & kQsBig)) gv[k] = rk_gtab(a, L)[rqc];
+                if (L < C && want && lane != L && rqc < 64u && !(sh.qs[L] & kQsBig)) gv[k] = rk_gtab(a, xr, L)[rqc];
             }
             uint32_t accw0 = 0u, accw1 = 0u, fbw = 0u;
 #pragma unroll
@@ -344,7 +369,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
                     okm = __ballot(want_l && rqc < 64u && gv[k] > rqm);
                 } else {
                     okm = 0ull;
-                    const unsigned long long* sn = tr_snap(a, L);
+                    const unsigned long long* sn = rk_snap(a, xr, L);
                     const uint32_t NL = sh.nn[L];
                     unsigned long long pend = __ballot(want_l);
                     while (pend) {
@@ -388,11 +413,10 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
                         sh.st[wave].lq_len = lq_len;
                         if (lq0 + nacc > LQ) sh.st[wave].flags |= MCS_FLAG_LENT_OVERFLOW;
                     }
-                    // the next tick's LentQueue head: an entry of an earlier tick is loaded; one this
-                    // tick's appends just wrote (the queue was empty) comes from the request registers
-                    if (lq0 > 0u) {
-                        prefetch_lq(lq_head, lq0);
-                    } else if (okm && lq_len > 0u) {
+                    // the next tick's LentQueue head: an entry of an earlier tick was loaded at the
+                    // launch start; one this tick's appends just wrote (the queue was empty) comes from
+                    // the request registers
+                    if (lq0 == 0u && okm && lq_len > 0u) {
                         const uint32_t b0 = (uint32_t)__builtin_ctzll(okm);
                         const uint32_t j = readlane(rqj, b0), ec = readlane(rqc, b0), em = readlane(rqm, b0),
                                        ed = readlane(rqd, b0);
@@ -408,8 +432,6 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
                 if (accw1) atomicOr(&sh.accm[1], accw1);
                 if (fbw) atomicOr(&sh.accm[2], 1u);
             }
-        } else if (own && sh.st[wave].lq_len > 0u) {
-            prefetch_lq(sh.st[wave].lq_head, sh.st[wave].lq_len);
         }
         __syncthreads();
         // ---- the acceptances (identical in every workgroup and on every rank): BorrowedQueue append,
@@ -648,7 +670,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
                 atomicMax(&tab[fc - 1u], (uint32_t)(v >> 32));
         }
         const bool bigw = __ballot(big) != 0ull;
-        rk_gtab(a, g)[63u - lane] = wave_scan_max_u32(tab[63u - lane]);  // G[63 - lane]
+        rk_gtab(a, xw, g)[63u - lane] = wave_scan_max_u32(tab[63u - lane]);  // G[63 - lane]
         // the post-A record and the node snapshot: this rank's block of the next all-gather
         const uint32_t lql = RST(lq_len);
         const uint32_t qs = (RST(has_w) ? kQsW : 0u) | (RST(rq_head) < RST(next_arr) ? kQsRq : 0u) | lent_now |
@@ -669,9 +691,9 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         xv = lane == kRkN ? N : xv;
         xv = lane == kRkTc ? (uint32_t)RST(total_c) : xv;
         xv = lane == kRkTm ? (uint32_t)RST(total_m) : xv;
-        uint32_t* const rp = reinterpret_cast<uint32_t*>(a.xb + (size_t)a.rank * a.blk + (size_t)c * sizeof(TrXRec));
+        uint32_t* const rp = rk_rec(a, xw, g);
         if (lane < kRkWords) rp[lane] = xv;
-        if (bigw) copy_rounds<4>(tr_snap(a, g), nodes, N, lane);  // (read only for a big lender)
+        if (bigw) copy_rounds<4>(rk_snap(a, xw, g), nodes, N, lane);  // (read only for a big lender)
         if (lane == 0 && lent_now) a.lrp[c] = lr;
         if (lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stv;
     }
