@@ -289,9 +289,13 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     "mcsfa_start_%=:\n\t" MCS_FA_REC##W                                                          \
     "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
     "s_cbranch_scc0 mcsfa_bend_%=\n"
+// (r05: no vmcnt wait at the exit: the batch's three result stores just issued complete while the
+// generator synthesises the next batch; the compiler's code issues no store, and any wait it takes
+// on its own loads only waits longer for the older stores, which complete in issue order.  The LDS
+// operations of a release are waited for: the generator uses the wave's LDS scratch.)
 #define MCS_FA_EXIT_F                                                                             \
     "mcsfa_exit_%=:\n\t"                                                                          \
-    "s_waitcnt vmcnt(0) lgkmcnt(0)\n\t"                                                           \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                                    \
     "s_cmp_eq_u32 s47, 0\n\t" /* (as MCS_FA_EXIT_S) */                                           \
     "s_cbranch_scc1 mcsfa_xf_%=\n\t"                                                              \
     "v_add_u32 v93, v92, v95\n"                                                                   \

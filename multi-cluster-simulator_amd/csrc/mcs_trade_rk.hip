@@ -105,6 +105,24 @@ struct RkField {  // a TrCluster field held in lane f of a VGPR (phase A's clust
 };
 #define RST(field) (RkField{stv, (uint32_t)(offsetof(TrCluster, field) / 4u), lane})
 
+#ifdef MCS_RK_STAMPS
+// probe build (tools/variant.sh ... -DMCS_RK_STAMPS): per-wave segment times (s_memrealtime, 100 MHz)
+// summed over the launches since the last read: [wave of the system][segment]; segments: 0 launch
+// start -> state in, 1 -> B and C/D done, 2 -> acceptances applied, 3 -> phase A done, 4 -> state out
+constexpr int kRkSeg = 5;
+__device__ unsigned long long g_rk_stamps[kTrResMaxClusters * kRkSeg];
+#define RK_MARK(i)                                                          \
+    do {                                                                    \
+        const uint64_t rk_now = __builtin_amdgcn_s_memrealtime();           \
+        rk_acc[i] += rk_now - rk_last;                                      \
+        rk_last = rk_now;                                                   \
+    } while (0)
+#else
+#define RK_MARK(i) \
+    do {           \
+    } while (0)
+#endif
+
 struct RkShared {  // (the workgroup's node vectors follow: kRkWaves * ns u64)
     // X1 of tick n, every cluster of the system (word k of cluster g at rq_job + k * 64 + g)
     uint32_t rq_job[kTrResMaxClusters], rq_c[kTrResMaxClusters], rq_m[kTrResMaxClusters];
@@ -123,6 +141,10 @@ struct RkShared {  // (the workgroup's node vectors follow: kRkWaves * ns u64)
 template <int kRows>  // slot rows per cluster (64 slots each)
 __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, uint32_t mode) {
     if (a.ctl->done) return;  // (the graph's launches after the end of the run)
+#ifdef MCS_RK_STAMPS
+    uint64_t rk_acc[kRkSeg] = {0, 0, 0, 0, 0};
+    uint64_t rk_last = __builtin_amdgcn_s_memrealtime();
+#endif
     extern __shared__ unsigned long long rk_smem[];
     RkShared& sh = *reinterpret_cast<RkShared*>(rk_smem);
     unsigned long long* const nodes_wg = rk_smem + (sizeof(RkShared) + 7) / 8;
@@ -195,7 +217,16 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         sh.total_m[lane] = w3.y;
     }
     if (threadIdx.x < 3u) sh.accm[threadIdx.x] = 0u;
+    // the G tables of this wave's lenders (w, w + 4, ...), lane x holding G_L[x], in flight with the
+    // records: phase B then reads G_L[c_b] across lanes (ds_bpermute) instead of a second round trip
+    uint32_t gl[kRkLenders];
+#pragma unroll
+    for (uint32_t k = 0; k < kRkLenders; ++k) {
+        const uint32_t L = wave + k * (uint32_t)kRkWaves;
+        gl[k] = mode != 0u && L < C ? rk_gtab(a, xr, L)[lane] : 0u;
+    }
     __syncthreads();
+    RK_MARK(0);
 
     const uint4* __restrict__ jobs = a.jobs + j0;
     uint4 hwin = make_uint4(0u, 0u, 0u, 0u);
@@ -350,14 +381,11 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         }
         const bool want = rqj != kEmpty;
         if (__ballot(want)) {
-            // every G-table read of the wave issued before the first compare (one round trip)
+            // G_L[c_b] for every lender of the wave (a lane permute of the tables loaded at the start)
             uint32_t gv[kRkLenders];
+            const int src = (int)(rqc < 64u ? rqc : 0u);
 #pragma unroll
-            for (uint32_t k = 0; k < kRkLenders; ++k) {
-                const uint32_t L = wave + k * (uint32_t)kRkWaves;
-                gv[k] = 0u;
-                if (L < C && want && lane != L && rqc < 64u && !(sh.qs[L] & kQsBig)) gv[k] = rk_gtab(a, xr, L)[rqc];
-            }
+            for (uint32_t k = 0; k < kRkLenders; ++k) gv[k] = (uint32_t)__shfl((int)gl[k], src);
             uint32_t accw0 = 0u, accw1 = 0u, fbw = 0u;
 #pragma unroll
             for (uint32_t k = 0; k < kRkLenders; ++k) {
@@ -434,6 +462,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             }
         }
         __syncthreads();
+        RK_MARK(1);
         // ---- the acceptances (identical in every workgroup and on every rank): BorrowedQueue append,
         // WaitQueue pop (scheduler.go:237-242) for this workgroup's own borrowers; an append overflow
         // ends the run at tick n (clock T, no T_MAX flag of that tick) ----
@@ -463,6 +492,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             }
         }
         __syncthreads();
+        RK_MARK(2);
     }
 
     // ---- A: tick n + 1 (tick 0 in mode 0) for this rank's clusters (tr_step_kernel) ----
@@ -698,6 +728,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         if (lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stv;
     }
 
+    RK_MARK(3);
     // ---- state out (the next launch takes it from HBM) ----
     if (own) {
         copy_rounds<4>(a.tn + n0, nodes, N, lane);
@@ -723,6 +754,12 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             ctl->n_lent = sh.n_lent;
         }
     }
+#ifdef MCS_RK_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    RK_MARK(4);
+    if (lane == 0 && g < kTrResMaxClusters)
+        for (int i = 0; i < kRkSeg; ++i) atomicAdd(&g_rk_stamps[g * kRkSeg + i], (unsigned long long)rk_acc[i]);
+#endif
 }
 
 }  // namespace
@@ -753,3 +790,11 @@ hipError_t launch_trade_rk(const TradeArgs& a, uint32_t mode, size_t lds, hipStr
 }
 
 }  // namespace mcs
+
+#ifdef MCS_RK_STAMPS
+extern "C" int mcs_debug_rk_stamps(unsigned long long* out) {
+    unsigned long long z[mcs::kTrResMaxClusters * mcs::kRkSeg] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_rk_stamps), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_rk_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -24,7 +24,8 @@ eng = Engine(0, policy=os.environ.get("AB_POLICY", "FIFO"))
 nc = int(os.environ.get("AB_CLUSTERS", "4096"))
 eng.load_clusters(replicate(uniform_cluster(nn), nc))
 lam = float(os.environ.get("AB_LAM", "0")) or scaled_lambda(nn, load=load)
-eng.generate_jobs(GenParams(arrival_mode=1, lam=lam, max_dur_s=int(os.environ.get("AB_MAXDUR", "600"))), 16384)
+eng.generate_jobs(GenParams(arrival_mode=1, lam=lam, max_dur_s=int(os.environ.get("AB_MAXDUR", "600")),
+                             fused=os.environ.get("AB_FUSED", "0") == "1"), 16384)
 eng.run()
 ms = [eng.run().kernel_ms for _ in range(steps)]
 print(json.dumps({"ms": ms}))
