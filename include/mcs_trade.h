@@ -97,7 +97,11 @@ typedef struct mcs_trade_stats {
                               one workgroup per 4 clusters, exchange written through to memory;
                               5 = the same with every workgroup on one XCD, exchange in its L2;
                               6 = form 0 after a resident exchange timed out (workers not all
-                              resident at once: the run was redone on the replayed kernels) */
+                              resident at once: the run was redone on the replayed kernels);
+                              7 = RCCL, ONE launch per tick (phases B-D of tick n + A of tick
+                              n + 1, mcs_trade_rk.hip) and one all-gather, captured in a hipGraph;
+                              8 = the same, eager; 9 = the one-launch tick on the caller-driven
+                              phase API (MCS_TRADE_RK=0: the three-kernel forms 0-2) */
     double kernel_ms;      /* device time of the lock-step loop (HIP events) */
     double wall_ms;
 } mcs_trade_stats;

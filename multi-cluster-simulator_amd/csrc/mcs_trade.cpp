@@ -38,6 +38,7 @@ struct TradeDev {
     mcs_lent_rec* lent = nullptr;
     mcs_trade_rec* trades = nullptr;
     uint4* lrp = nullptr;                // one-launch tick: pending lent-run records
+    unsigned long long* tnr = nullptr;   // one-launch tick: dense node state [C_l][ns]
     bool rk = false;                     // the one-launch tick runs this system (trade_alloc)
     bool rk_started = false;             // its tick-0 phase A has run
     uint64_t rk_tick = 0;                // one-launch ticks launched (the exchange buffer's parity)
@@ -183,6 +184,8 @@ int trade_alloc(mcs_engine* e) {
         td->rk_lds = trade_rk_lds(ns);
         if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device) == hipSuccess &&
             td->rk_lds <= (size_t)max_lds) {
+            HIPCHK(e, hipMalloc(&td->tnr, (size_t)Cl * ns * 8u));
+            a.tnr = td->tnr;
             td->rk = true;
         }
     }
@@ -336,8 +339,9 @@ int run_rccl_rk(mcs_engine* e) {
         return ncclAllGather(xb + (size_t)e->rank * a.blk, xb, a.blk, ncclUint8, comm, s);
     };
     auto tick = [&](hipStream_t s) -> bool {
-        if (gather(cap_t++, s) != ncclSuccess) return false;
-        return launch_trade_rk(a, 1u, td->rk_lds, s) == hipSuccess;
+        const uint32_t t = cap_t++;
+        if (gather(t, s) != ncclSuccess) return false;
+        return launch_trade_rk(a, 1u + (t & 1u), td->rk_lds, s) == hipSuccess;
     };
     if (!td->rgraph_tried) {
         td->rgraph_tried = true;
@@ -351,7 +355,7 @@ int run_rccl_rk(mcs_engine* e) {
             for (uint32_t t = 0; t < kGraphTicks; ++t) {
                 const ncclResult_t r = gather(t, e->stream);
                 if (r != ncclSuccess) return nccl_fail(e, "ncclAllGather(exchange blocks)", r);
-                const hipError_t st = launch_trade_rk(a, 1u, td->rk_lds, e->stream);
+                const hipError_t st = launch_trade_rk(a, 1u + (t & 1u), td->rk_lds, e->stream);
                 if (st != hipSuccess) return hip_fail(e, "one-launch tick", st);
             }
         }
@@ -481,6 +485,7 @@ void trade_free(mcs_engine* e) {
     dfree(td->lent);
     dfree(td->trades);
     dfree(td->lrp);
+    dfree(td->tnr);
     if (td->h_ctl) (void)hipHostFree(td->h_ctl);
     delete td;
     e->td = nullptr;
@@ -706,7 +711,7 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
                 break;
             case 1:
                 hs = hipMemcpyAsync(xb, in, ib, hipMemcpyHostToDevice, e->stream);
-                if (hs == hipSuccess) hs = mcs::launch_trade_rk(a, 1u, td->rk_lds, e->stream);
+                if (hs == hipSuccess) hs = mcs::launch_trade_rk(a, 1u + (uint32_t)(td->rk_tick & 1u), td->rk_lds, e->stream);
                 ++td->rk_tick;
                 break;
             case 2:

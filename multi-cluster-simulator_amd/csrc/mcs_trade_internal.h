@@ -119,6 +119,7 @@ struct TradeArgs {
     TrCtl* ctl;
     mcs_lent_rec* lent_log;
     mcs_trade_rec* trade_log;
+    unsigned long long* tnr;  // (one-launch tick) this rank's nodes, dense [C_l][ns], across launches
     uint4* lrp;  // (one-launch tick) this rank's lent run of the last phase A per cluster {b, j, node, fin}
 };
 

@@ -140,7 +140,9 @@ struct RkShared {  // (the workgroup's node vectors follow: kRkWaves * ns u64)
 
 template <int kRows>  // slot rows per cluster (64 slots each)
 __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, uint32_t mode) {
-    if (a.ctl->done) return;  // (the graph's launches after the end of the run)
+    // mode 0: phase A of tick 0 (writes buffer 0); mode 1 / 2: tick n with n & 1 = mode - 1 (the host
+    // knows the parity: a graph replays an even number of ticks, the caller-driven path counts them),
+    // so every address below is known at the launch start and all of its loads issue at once
 #ifdef MCS_RK_STAMPS
     uint64_t rk_acc[kRkSeg] = {0, 0, 0, 0, 0};
     uint64_t rk_last = __builtin_amdgcn_s_memrealtime();
@@ -158,10 +160,10 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     const uint32_t c = own ? g - lo : 0u;  // its local index
     unsigned long long* const nodes = nodes_wg + (size_t)wave * ns;
     // tick n's blocks (read) and tick n + 1's (written); mode 0 writes tick 0's
-    const uint32_t n_tick = a.ctl->ticks;
     const size_t xbuf = (size_t)a.world * a.blk;
-    unsigned char* const xr = a.xb + (size_t)(n_tick & 1u) * xbuf;
-    unsigned char* const xw = a.xb + (size_t)((mode == 0u ? 0u : n_tick + 1u) & 1u) * xbuf;
+    const uint32_t par = mode == 2u ? 1u : 0u;  // tick n's parity (mode 0: none read)
+    unsigned char* const xr = a.xb + (size_t)par * xbuf;
+    unsigned char* const xw = a.xb + (size_t)(mode == 0u ? 0u : par ^ 1u) * xbuf;
 
     // ---- state in: the replicated trader state and clock, this rank's clusters ----
     uint32_t N = 0, n0 = 0, J = 0;
@@ -171,7 +173,10 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         N = a.node_off[c + 1] - n0;
         j0 = a.job_off[c];
         J = (uint32_t)(a.job_off[c + 1] - j0);
-        copy_rounds<4>(nodes, a.tn + n0, N, lane);
+        // the nodes: from the CSR initial state at tick 0, then from the dense [C_l][ns] copy the
+        // launches keep (an address known at the launch start: no wait on node_off first)
+        if (mode == 0u) copy_rounds<4>(nodes, a.tn + n0, N, lane);
+        else copy_rounds<4>(nodes, a.tnr + (size_t)c * ns, ns, lane);
         if (lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = reinterpret_cast<const uint32_t*>(&a.cl[c])[lane];
     }
     for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) sh.trs[q] = a.tr[q];
@@ -226,6 +231,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         gl[k] = mode != 0u && L < C ? rk_gtab(a, xr, L)[lane] : 0u;
     }
     __syncthreads();
+    if (sh.done) return;  // (the graph's launches after the end of the run; uniform)
     RK_MARK(0);
 
     const uint4* __restrict__ jobs = a.jobs + j0;
@@ -731,7 +737,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     RK_MARK(3);
     // ---- state out (the next launch takes it from HBM) ----
     if (own) {
-        copy_rounds<4>(a.tn + n0, nodes, N, lane);
+        copy_rounds<4>(a.tnr + (size_t)c * ns, nodes, ns, lane);
         if (lane < kStW) reinterpret_cast<uint32_t*>(&a.cl[c])[lane] = reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane];
 #pragma unroll
         for (int r = 0; r < kRows; ++r) {
