@@ -168,15 +168,25 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     // ---- state in: the replicated trader state and clock, this rank's clusters ----
     uint32_t N = 0, n0 = 0, J = 0;
     uint64_t j0 = 0;
+    unsigned long long nreg[kRkNodes / kWave];
     if (own) {
         n0 = a.node_off[c];
         N = a.node_off[c + 1] - n0;
         j0 = a.job_off[c];
         J = (uint32_t)(a.job_off[c + 1] - j0);
-        // the nodes: from the CSR initial state at tick 0, then from the dense [C_l][ns] copy the
-        // launches keep (an address known at the launch start: no wait on node_off first)
-        if (mode == 0u) copy_rounds<4>(nodes, a.tn + n0, N, lane);
-        else copy_rounds<4>(nodes, a.tnr + (size_t)c * ns, ns, lane);
+        // the nodes, into registers (phase A alone reads them, from LDS): from the CSR initial state
+        // at tick 0, then from the dense [C_l][ns] copy the launches keep (an address known at the
+        // launch start); they land during phases B-D
+#pragma unroll
+        for (uint32_t q = 0; q < kRkNodes / kWave; ++q) {
+            const uint32_t i = q * kWave + lane;
+            nreg[q] = 0ull;
+            if (mode == 0u) {
+                if (i < N) nreg[q] = a.tn[n0 + i];
+            } else if (i < ns) {
+                nreg[q] = a.tnr[(size_t)c * ns + i];
+            }
+        }
         if (lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = reinterpret_cast<const uint32_t*>(&a.cl[c])[lane];
     }
     for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) sh.trs[q] = a.tr[q];
@@ -200,7 +210,6 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     for (int r = 0; r < kRows; ++r) {
         fin[r] = own ? a.sfin[sb + r * kWave + lane] : kEmpty;
         pay[r] = own ? a.snode[sb + r * kWave + lane] : 0u;
-        if (fin[r] == kEmpty) frm |= 1u << r;
     }
     // X1 of tick n: lane q of wave 0 takes cluster q's record from the gathered blocks
     if (mode != 0u && wave == 0 && lane < C) {
@@ -502,7 +511,16 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     }
 
     // ---- A: tick n + 1 (tick 0 in mode 0) for this rank's clusters (tr_step_kernel) ----
+    if (own) {  // the nodes to the wave's LDS copy (the loads of the launch start)
+#pragma unroll
+        for (uint32_t q = 0; q < kRkNodes / kWave; ++q)
+            if (q * kWave + lane < ns) nodes[q * kWave + lane] = nreg[q];
+    }
     if (own && sh.done == 0u) {
+        // the free slot rows
+#pragma unroll
+        for (int r = 0; r < kRows; ++r)
+            if (fin[r] == kEmpty) frm |= 1u << r;
         const uint32_t T = sh.T;
         bool sample = false;
         if (a.trader && T % a.sample_period == 0u) {
