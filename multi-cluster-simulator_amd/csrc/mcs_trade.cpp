@@ -124,8 +124,10 @@ int trade_alloc(mcs_engine* e) {
     HIPCHK(e, hipMalloc(&td->acc, Ct * 4));
     HIPCHK(e, hipMalloc(&td->lqp, Ct * 4));
     HIPCHK(e, hipMalloc(&td->fb, Ct * 4));
-    HIPCHK(e, hipMalloc(&td->tr, Ct * sizeof(TrTrader)));
-    HIPCHK(e, hipMalloc(&td->ctl, sizeof(TrCtl)));
+    // (two copies of the trader state and of the clock: the one-launch tick alternates them by tick
+    // parity; every other form uses the first)
+    HIPCHK(e, hipMalloc(&td->tr, 2u * Ct * sizeof(TrTrader)));
+    HIPCHK(e, hipMalloc(&td->ctl, 2u * sizeof(TrCtl)));
     HIPCHK(e, hipMalloc(&td->lent, lent_cap * sizeof(mcs_lent_rec)));
     HIPCHK(e, hipMalloc(&td->trades, trade_cap * sizeof(mcs_trade_rec)));
     HIPCHK(e, hipHostMalloc(&td->h_ctl, sizeof(TrCtl), hipHostMallocDefault));
@@ -716,8 +718,9 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
                 break;
             case 2:
                 break;
-            default:
-                hs = hipMemcpyAsync(td->h_ctl, td->ctl, sizeof(mcs::TrCtl), hipMemcpyDeviceToHost, e->stream);
+            default:  // (the copy the last launch wrote)
+                hs = hipMemcpyAsync(td->h_ctl, td->ctl + (td->rk_tick & 1u), sizeof(mcs::TrCtl),
+                                    hipMemcpyDeviceToHost, e->stream);
                 break;
         }
         if (hs != hipSuccess) return mcs::hip_fail(e, "one-launch tick (caller-driven)", hs);
@@ -754,6 +757,11 @@ int mcs_trade_end(mcs_engine* e, mcs_stats* stats) {
     if (mcs::is_dtrade(e)) return mcs::dtrade_end(e, stats);
     mcs::TradeDev* td = e->td;
     if (!td || !td->begun) return fail(e, MCS_E_STATE, "mcs_trade_begin first");
+    if (td->rk && (td->rk_tick & 1u)) {  // caller-driven one-launch tick: the final copies into the first
+        HIPCHK(e, hipMemcpyAsync(td->ctl, td->ctl + 1, sizeof(mcs::TrCtl), hipMemcpyDeviceToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(td->tr, td->tr + td->a.Ct, td->a.Ct * sizeof(mcs::TrTrader),
+                                 hipMemcpyDeviceToDevice, e->stream));
+    }
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     e->has_run = true;

@@ -164,6 +164,13 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     const uint32_t par = mode == 2u ? 1u : 0u;  // tick n's parity (mode 0: none read)
     unsigned char* const xr = a.xb + (size_t)par * xbuf;
     unsigned char* const xw = a.xb + (size_t)(mode == 0u ? 0u : par ^ 1u) * xbuf;
+    // the clock and the replicated trader state are double-buffered alike (read copy par, workgroup 0
+    // writes copy par ^ 1 at its end): a workgroup that starts after workgroup 0 finished still reads
+    // tick n's values.  Mode 0 changes neither.
+    const TrCtl* const ctl_r = a.ctl + par;
+    TrCtl* const ctl_w = a.ctl + (par ^ 1u);
+    const TrTrader* const tr_r = a.tr + (size_t)par * C;
+    TrTrader* const tr_w = a.tr + (size_t)(par ^ 1u) * C;
 
     // ---- state in: the replicated trader state and clock, this rank's clusters ----
     uint32_t N = 0, n0 = 0, J = 0;
@@ -189,9 +196,9 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         }
         if (lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = reinterpret_cast<const uint32_t*>(&a.cl[c])[lane];
     }
-    for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) sh.trs[q] = a.tr[q];
+    for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) sh.trs[q] = tr_r[q];
     if (threadIdx.x == 0) {
-        const TrCtl ctl = *a.ctl;
+        const TrCtl ctl = *ctl_r;
         sh.T = sh.T0 = ctl.T;
         sh.done = ctl.done;
         sh.ticks = ctl.ticks;
@@ -240,7 +247,13 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         gl[k] = mode != 0u && L < C ? rk_gtab(a, xr, L)[lane] : 0u;
     }
     __syncthreads();
-    if (sh.done) return;  // (the graph's launches after the end of the run; uniform)
+    if (sh.done) {  // the graph's launches after the end of the run: the final state carried forward
+        if (mode != 0u && wg == 0) {
+            for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) tr_w[q] = sh.trs[q];
+            if (threadIdx.x == 0) *ctl_w = *ctl_r;
+        }
+        return;  // (uniform)
+    }
     RK_MARK(0);
 
     const uint4* __restrict__ jobs = a.jobs + j0;
@@ -765,10 +778,10 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             }
         }
     }
-    if (wg == 0) {
-        for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) a.tr[q] = sh.trs[q];
+    if (wg == 0 && mode != 0u) {
+        for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) tr_w[q] = sh.trs[q];
         if (threadIdx.x == 0) {
-            TrCtl* ctl = a.ctl;
+            TrCtl* ctl = ctl_w;
             ctl->T = sh.T;
             ctl->done = sh.done == 2u ? 1u : sh.done;
             ctl->ticks = sh.ticks;
