@@ -288,6 +288,9 @@ def main_c5_delay(args, world, rank, local_rank):
                                + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "graph-replayed after a resident timeout" if ts["loop_form"] == 6 else "RCCL eager" if ts["loop_form"] == 1
                                                     else "RCCL captured in a hipGraph" if ts["loop_form"] == 2
                                                     else "resident in one workgroup" if ts["loop_form"] == 3
+                                                    else "one launch per tick, captured with the all-gather in a hipGraph" if ts["loop_form"] == 7
+                                                    else "one launch per tick, eager" if ts["loop_form"] == 8
+                                                    else "one launch per tick, caller-driven" if ts["loop_form"] == 9
                                                     else "resident, one workgroup per 4 clusters"
                                                     + (", all on one XCD (L2 exchange)" if ts["loop_form"] == 5 else "")) + ")",
             },
@@ -404,6 +407,9 @@ def main_c5(args, world, rank, local_rank):
                                + " (tick loop: " + ("graph-replayed" if ts["loop_form"] == 0 else "graph-replayed after a resident timeout" if ts["loop_form"] == 6 else "RCCL eager" if ts["loop_form"] == 1
                                                     else "RCCL captured in a hipGraph" if ts["loop_form"] == 2
                                                     else "resident in one workgroup" if ts["loop_form"] == 3
+                                                    else "one launch per tick, captured with the all-gather in a hipGraph" if ts["loop_form"] == 7
+                                                    else "one launch per tick, eager" if ts["loop_form"] == 8
+                                                    else "one launch per tick, caller-driven" if ts["loop_form"] == 9
                                                     else "resident, one workgroup per 4 clusters"
                                                     + (", all on one XCD (L2 exchange)" if ts["loop_form"] == 5 else "")) + ")",
             },
@@ -419,6 +425,8 @@ def main_c5(args, world, rank, local_rank):
                 "traffic": None,
                 "kernel": ("tr_mw_kernel (resident tick, one workgroup per 4 clusters)" if ts["loop_form"] in (4, 5) else
                            "tr_resident_kernel (resident tick, one workgroup)" if ts["loop_form"] == 3 else
+                           "tr_rk_kernel (the whole tick in one launch, one workgroup per 4 clusters), launch/latency-bound"
+                           if ts["loop_form"] in (7, 8, 9) else
                            "lock-step tick (tr_step/tr_lend/tr_trader, one exchange), launch/latency-bound"),
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "bytes_per_placement": BYTES_PER_PLACEMENT,

@@ -82,6 +82,9 @@ __device__ __forceinline__ uint32_t* rk_gtab(const TradeArgs& a, unsigned char* 
 }
 
 constexpr uint32_t kStW = sizeof(TrCluster) / 4u;
+constexpr uint32_t kTrW = sizeof(TrTrader) / 4u;
+static_assert(sizeof(TrTrader) % 4u == 0u && kTrResMaxClusters * kTrW <= 2u * kRkWaves * kWave,
+              "the trader state in two words per thread");
 static_assert(sizeof(TrCluster) % 4u == 0u && kStW <= (uint32_t)kWave, "TrCluster in one VGPR");
 struct RkField {  // a TrCluster field held in lane f of a VGPR (phase A's cluster state)
     uint32_t& v;
@@ -109,8 +112,10 @@ struct RkField {  // a TrCluster field held in lane f of a VGPR (phase A's clust
 // probe build (tools/variant.sh ... -DMCS_RK_STAMPS): per-wave segment times (s_memrealtime, 100 MHz)
 // summed over the launches since the last read: [wave of the system][segment]; segments: 0 launch
 // start -> state in, 1 -> B and C/D done, 2 -> acceptances applied, 3 -> phase A done, 4 -> state out
-constexpr int kRkSeg = 5;
+constexpr int kRkSeg = 12;
 __device__ unsigned long long g_rk_stamps[kTrResMaxClusters * kRkSeg];
+constexpr uint32_t kRkTl = 8192;  // timeline ring: [tick & (kRkTl - 1)][workgroup] {start, end}
+__device__ unsigned long long g_rk_tl[kRkTl * 16 * 2];
 #define RK_MARK(i)                                                          \
     do {                                                                    \
         const uint64_t rk_now = __builtin_amdgcn_s_memrealtime();           \
@@ -120,6 +125,14 @@ __device__ unsigned long long g_rk_stamps[kTrResMaxClusters * kRkSeg];
 #else
 #define RK_MARK(i) \
     do {           \
+    } while (0)
+#endif
+// the stamp build splits the launch start: kernel arguments in (0), the loads issued (1)
+#ifdef MCS_RK_STAMPS
+#define RK_WAIT_ARGS(v) asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(v) : "memory")
+#else
+#define RK_WAIT_ARGS(v) \
+    do {                \
     } while (0)
 #endif
 
@@ -138,14 +151,15 @@ struct RkShared {  // (the workgroup's node vectors follow: kRkWaves * ns u64)
     unsigned long long n_trades, n_won, n_lent, n_lent_next;
 };
 
-template <int kRows>  // slot rows per cluster (64 slots each)
+template <int kRows>  // slot rows per cluster (64 slots each; a multiple of 4)
 __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, uint32_t mode) {
     // mode 0: phase A of tick 0 (writes buffer 0); mode 1 / 2: tick n with n & 1 = mode - 1 (the host
     // knows the parity: a graph replays an even number of ticks, the caller-driven path counts them),
     // so every address below is known at the launch start and all of its loads issue at once
 #ifdef MCS_RK_STAMPS
-    uint64_t rk_acc[kRkSeg] = {0, 0, 0, 0, 0};
+    uint64_t rk_acc[kRkSeg] = {};
     uint64_t rk_last = __builtin_amdgcn_s_memrealtime();
+    const uint64_t rk_t0 = rk_last;
 #endif
     extern __shared__ unsigned long long rk_smem[];
     RkShared& sh = *reinterpret_cast<RkShared*>(rk_smem);
@@ -153,6 +167,8 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t C = a.Ct, ns = a.ns, S = a.S, Cl = a.Cl;
     const uint32_t wg = blockIdx.x;
+    RK_WAIT_ARGS(C);
+    RK_MARK(0);
     const uint32_t g = wg * kRkWaves + wave;  // this wave's cluster of the system
     const uint32_t lo = a.rank * Cl;          // this rank's clusters: [lo, lo + Cl)
     const bool sys = g < C;
@@ -172,56 +188,84 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     const TrTrader* const tr_r = a.tr + (size_t)par * C;
     TrTrader* const tr_w = a.tr + (size_t)(par ^ 1u) * C;
 
-    // ---- state in: the replicated trader state and clock, this rank's clusters ----
-    uint32_t N = 0, n0 = 0, J = 0;
-    uint64_t j0 = 0;
-    unsigned long long nreg[kRkNodes / kWave];
-    if (own) {
-        n0 = a.node_off[c];
-        N = a.node_off[c + 1] - n0;
-        j0 = a.job_off[c];
-        J = (uint32_t)(a.job_off[c + 1] - j0);
-        // the nodes, into registers (phase A alone reads them, from LDS): from the CSR initial state
-        // at tick 0, then from the dense [C_l][ns] copy the launches keep (an address known at the
-        // launch start); they land during phases B-D
+    // ---- state in: every load of the launch issued before any of its values is used, in the order
+    // the launch needs them (vmcnt retires in order: the copies before the barrier wait for the
+    // trader state and the exchange alone; the slot rows and nodes land during phases B-D).  The
+    // loads are unconditional, from clamped in-range addresses (a value no one uses is never read):
+    // a load under a branch makes the compiler merge, and so wait for, its value at the join. ----
+    // Every address first, then (past a scheduling fence) every load: a load's destination register
+    // reused by an address computation after it would make the compiler wait for that load.
+    const TrCtl ctlv = *ctl_r;  // (uniform: scalar loads)
+    // the replicated trader state as flat words (C * kTrW <= 2 * 256)
+    const uint32_t trn = C * kTrW, tq = threadIdx.x;
+    const uint32_t* const trp0 = reinterpret_cast<const uint32_t*>(tr_r) + min(tq, trn - 1u);
+    const uint32_t* const trp1 = reinterpret_cast<const uint32_t*>(tr_r) + min(tq + (uint32_t)(kRkWaves * kWave), trn - 1u);
+    // this wave's cluster (c = 0 for a wave that owns none: its values are never read): TrCluster
+    // (lane f < kStW: word f), CSR bounds, the dense node copy (tick 0's from the CSR initial state,
+    // after the barrier), the running slots in registers (row r, lane l: slot (r / 4) * 256 + 4l +
+    // r % 4, so a lane's four rows are one 16-byte load; finish time and payload node | cores << 9 |
+    // mem << 16, in this kernel's own order in sfin / snode)
+    const uint32_t* const stp = reinterpret_cast<const uint32_t*>(&a.cl[c]) + min(lane, kStW - 1u);
+    const unsigned long long* np[kRkNodes / kWave];
 #pragma unroll
-        for (uint32_t q = 0; q < kRkNodes / kWave; ++q) {
-            const uint32_t i = q * kWave + lane;
-            nreg[q] = 0ull;
-            if (mode == 0u) {
-                if (i < N) nreg[q] = a.tn[n0 + i];
-            } else if (i < ns) {
-                nreg[q] = a.tnr[(size_t)c * ns + i];
-            }
-        }
-        if (lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = reinterpret_cast<const uint32_t*>(&a.cl[c])[lane];
+    for (uint32_t q = 0; q < kRkNodes / kWave; ++q) np[q] = a.tnr + (size_t)c * ns + min(q * kWave + lane, ns - 1u);
+    const size_t sb = (size_t)c * S;
+    const uint4* const finp = reinterpret_cast<const uint4*>(a.sfin + sb) + lane;
+    const uint4* const payp = reinterpret_cast<const uint4*>(a.snode + sb) + lane;
+    // X1 of tick n: lane q of wave 0 takes cluster q's record from the gathered blocks
+    const bool x1 = mode != 0u && wave == 0 && lane < C;
+    const uint4* const rp = reinterpret_cast<const uint4*>(rk_rec(a, xr, min(lane, C - 1u)));
+    const uint4* const lrpp = a.lrp + c;  // this cluster's lent run of tick n (read when it lent)
+    // the G tables of this wave's lenders (w, w + 4, ...), lane x holding G_L[x]: phase B reads
+    // G_L[c_b] across lanes (ds_bpermute) instead of a second round trip (L >= C: never read)
+    const uint32_t* glp[kRkLenders];
+#pragma unroll
+    for (uint32_t k = 0; k < kRkLenders; ++k) {
+        const uint32_t L = wave + k * (uint32_t)kRkWaves;
+        glp[k] = rk_gtab(a, xr, L < C ? L : 0u) + lane;
     }
-    for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) sh.trs[q] = tr_r[q];
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t trv0 = *trp0, trv1 = *trp1;
+    const uint32_t stw = *stp;
+    const uint32_t nb0 = a.node_off[c], nb1 = a.node_off[c + 1];
+    const unsigned long long jb0 = a.job_off[c], jb1 = a.job_off[c + 1];
+    unsigned long long nreg[kRkNodes / kWave];
+#pragma unroll
+    for (uint32_t q = 0; q < kRkNodes / kWave; ++q) nreg[q] = *np[q];
+    uint32_t fin[kRows], pay[kRows];
+#pragma unroll
+    for (int k = 0; k < kRows / 4; ++k) {
+        const uint4 f = finp[k * kWave], p = payp[k * kWave];
+        fin[4 * k] = f.x;
+        fin[4 * k + 1] = f.y;
+        fin[4 * k + 2] = f.z;
+        fin[4 * k + 3] = f.w;
+        pay[4 * k] = p.x;
+        pay[4 * k + 1] = p.y;
+        pay[4 * k + 2] = p.z;
+        pay[4 * k + 3] = p.w;
+    }
+    const uint4 w0 = rp[0], w1 = rp[1], w2 = rp[2], w3 = rp[3];
+    const uint4 lrv = *lrpp;
+    uint32_t gl[kRkLenders];
+#pragma unroll
+    for (uint32_t k = 0; k < kRkLenders; ++k) gl[k] = *glp[k];
+    RK_MARK(1);
+    // the LDS copies
+    if (own && lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stw;
+    if (tq < trn) reinterpret_cast<uint32_t*>(sh.trs)[tq] = trv0;
+    if (tq + kRkWaves * kWave < trn) reinterpret_cast<uint32_t*>(sh.trs)[tq + kRkWaves * kWave] = trv1;
     if (threadIdx.x == 0) {
-        const TrCtl ctl = *ctl_r;
-        sh.T = sh.T0 = ctl.T;
-        sh.done = ctl.done;
-        sh.ticks = ctl.ticks;
-        sh.flags = ctl.flags;
-        sh.n_trades = ctl.n_trades;
-        sh.n_won = ctl.n_won;
-        sh.n_lent = sh.n_lent_next = ctl.n_lent;
+        sh.T = sh.T0 = ctlv.T;
+        sh.done = ctlv.done;
+        sh.ticks = ctlv.ticks;
+        sh.flags = ctlv.flags;
+        sh.n_trades = ctlv.n_trades;
+        sh.n_won = ctlv.n_won;
+        sh.n_lent = sh.n_lent_next = ctlv.n_lent;
         sh.tmax_now = 0u;
     }
-    // the wave's running slots in registers (row r, lane l = slot r * 64 + l): finish time and the
-    // payload node | cores << 9 | mem << 16, as the MW tick keeps them (sfin / snode across launches)
-    uint32_t fin[kRows], pay[kRows];
-    uint32_t frm = 0u, drt = 0u;  // free rows; rows this lane changed (only those are stored back)
-    const size_t sb = (size_t)c * S;
-#pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-        fin[r] = own ? a.sfin[sb + r * kWave + lane] : kEmpty;
-        pay[r] = own ? a.snode[sb + r * kWave + lane] : 0u;
-    }
-    // X1 of tick n: lane q of wave 0 takes cluster q's record from the gathered blocks
-    if (mode != 0u && wave == 0 && lane < C) {
-        const uint4* rp = reinterpret_cast<const uint4*>(rk_rec(a, xr, lane));
-        const uint4 w0 = rp[0], w1 = rp[1], w2 = rp[2], w3 = rp[3];
+    if (x1) {
         sh.rq_job[lane] = w0.x;
         sh.rq_c[lane] = w0.y;
         sh.rq_m[lane] = w0.z;
@@ -238,23 +282,26 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         sh.total_m[lane] = w3.y;
     }
     if (threadIdx.x < 3u) sh.accm[threadIdx.x] = 0u;
-    // the G tables of this wave's lenders (w, w + 4, ...), lane x holding G_L[x], in flight with the
-    // records: phase B then reads G_L[c_b] across lanes (ds_bpermute) instead of a second round trip
-    uint32_t gl[kRkLenders];
-#pragma unroll
-    for (uint32_t k = 0; k < kRkLenders; ++k) {
-        const uint32_t L = wave + k * (uint32_t)kRkWaves;
-        gl[k] = mode != 0u && L < C ? rk_gtab(a, xr, L)[lane] : 0u;
-    }
-    __syncthreads();
+    // the barrier orders the LDS copies alone (the slot rows, nodes and TrCluster stay in flight)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     if (sh.done) {  // the graph's launches after the end of the run: the final state carried forward
         if (mode != 0u && wg == 0) {
             for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) tr_w[q] = sh.trs[q];
-            if (threadIdx.x == 0) *ctl_w = *ctl_r;
+            if (threadIdx.x == 0) *ctl_w = ctlv;
         }
         return;  // (uniform)
     }
-    RK_MARK(0);
+    RK_MARK(2);
+    const uint32_t n0 = nb0, N = nb1 - nb0, J = (uint32_t)(jb1 - jb0);
+    const uint64_t j0 = jb0;
+    if (own && mode == 0u) {  // tick 0: the nodes from the CSR initial state
+#pragma unroll
+        for (uint32_t q = 0; q < kRkNodes / kWave; ++q)
+            if (q * kWave + lane < N) nreg[q] = a.tn[n0 + q * kWave + lane];
+    }
+    uint32_t frm = 0u, drt = 0u;  // free rows; rows this lane changed (only those are stored back)
 
     const uint4* __restrict__ jobs = a.jobs + j0;
     uint4 hwin = make_uint4(0u, 0u, 0u, 0u);
@@ -289,7 +336,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             if (own && lane == 0 && (sh.qs[g] & kQsLent)) {
                 const unsigned long long idx = sh.n_lent + (uint64_t)__builtin_popcountll(lm & ((1ull << g) - 1ull));
                 if (idx < a.lent_cap) {
-                    const uint4 lr = a.lrp[c];
+                    const uint4 lr = lrv;
                     mcs_lent_rec rec;
                     rec.lender = g;
                     rec.borrower = lr.x;
@@ -490,24 +537,24 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             }
         }
         __syncthreads();
-        RK_MARK(1);
+        RK_MARK(3);
         // ---- the acceptances (identical in every workgroup and on every rank): BorrowedQueue append,
         // WaitQueue pop (scheduler.go:237-242) for this workgroup's own borrowers; an append overflow
         // ends the run at tick n (clock T, no T_MAX flag of that tick) ----
-        if (wave == 0) {
-            const uint32_t q = lane;
-            const bool acc = ((q < 32u ? sh.accm[0] >> q : sh.accm[1] >> (q - 32u)) & 1u) != 0u;
-            if (acc && q < C && q / kRkWaves == wg && q >= lo && q < lo + Cl && sh.rq_job[q] != kEmpty) {
-                const uint32_t rj = sh.rq_job[q];
-                const uint64_t qj0 = a.job_off[q - lo];
-                a.out_node[qj0 + rj] = MCS_NODE_BORROWED;
-                a.out_start[qj0 + rj] = T;
-                a.out_finish[qj0 + rj] = MCS_TIME_NONE;
-                TrCluster& s = sh.st[q - wg * kRkWaves];
+        if (own && lane == 0) {  // (the owner's wave: its job offset is in registers)
+            const bool acc = ((g < 32u ? sh.accm[0] >> g : sh.accm[1] >> (g - 32u)) & 1u) != 0u;
+            if (acc && sh.rq_job[g] != kEmpty) {
+                const uint32_t rj = sh.rq_job[g];
+                a.out_node[j0 + rj] = MCS_NODE_BORROWED;
+                a.out_start[j0 + rj] = T;
+                a.out_finish[j0 + rj] = MCS_TIME_NONE;
+                TrCluster& s = sh.st[wave];
                 s.has_w = 0u;
                 ++s.decided;
                 ++s.borrowed;
             }
+        }
+        if (wave == 0) {
             if (lane == 0) {
                 if (sh.accm[2]) {
                     uint32_t f = sh.flags | MCS_FLAG_LENT_OVERFLOW;
@@ -520,7 +567,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             }
         }
         __syncthreads();
-        RK_MARK(2);
+        RK_MARK(4);
     }
 
     // ---- A: tick n + 1 (tick 0 in mode 0) for this rank's clusters (tr_step_kernel) ----
@@ -545,6 +592,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         // (the WaitQueue head may have left for the BorrowedQueue in X2: the window still holds
         // the ReadyQueue head or job_at loads it)
         const uint32_t na0 = RST(next_arr);
+        RK_MARK(7);
         // releases due at T (cluster.go:153-157), before the tick's decisions
         if (RST(minf) <= T) {
             uint32_t lm = kEmpty, nrel = 0;
@@ -567,6 +615,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             RST(nrun) -= rk_wave_sum(nrel);
             RST(minf) = wave_min_u32(lm);
         }
+        RK_MARK(8);
         // arrivals up to T join the ReadyQueue (jobs are sorted by arrival)
         uint32_t nat;
         {
@@ -705,21 +754,20 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             }
             break;  // idle sleep (:294)
         }
+        RK_MARK(9);
 
         // GetResourceUtilization (cluster.go:46-63) on the ticks a trader reads it: an exact integer
         // sum (the engine's eligibility check), capacities minus free
         if (sample) {
-            uint32_t fc = 0u, fm = 0u, cc = 0u, cm = 0u;
+            // (the capacities' uint32 sum is total_c / total_m, tr_init_kernel's SetTotalResources)
+            uint32_t fc = 0u, fm = 0u;
             for (uint32_t i = lane; i < N; i += kWave) {
                 const unsigned long long v = nodes[i];
-                const uint2 cp = a.cap[n0 + i];
                 fc += (uint32_t)v;
                 fm += (uint32_t)(v >> 32);
-                cc += cp.x;
-                cm += cp.y;
             }
-            const float sc = (float)(int32_t)(rk_wave_sum(cc) - rk_wave_sum(fc));
-            const float sm = (float)(int32_t)(rk_wave_sum(cm) - rk_wave_sum(fm));
+            const float sc = (float)(int32_t)((uint32_t)RST(total_c) - rk_wave_sum(fc));
+            const float sm = (float)(int32_t)((uint32_t)RST(total_m) - rk_wave_sum(fm));
             RST(cu) = __float_as_uint(__fdiv_rn(sc, (float)RST(total_c)));
             RST(mu) = __float_as_uint(__fdiv_rn(sm, (float)RST(total_m)));
         }
@@ -738,6 +786,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         }
         const bool bigw = __ballot(big) != 0ull;
         rk_gtab(a, xw, g)[63u - lane] = wave_scan_max_u32(tab[63u - lane]);  // G[63 - lane]
+        RK_MARK(10);
         // the post-A record and the node snapshot: this rank's block of the next all-gather
         const uint32_t lql = RST(lq_len);
         const uint32_t qs = (RST(has_w) ? kQsW : 0u) | (RST(rq_head) < RST(next_arr) ? kQsRq : 0u) | lent_now |
@@ -765,16 +814,26 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         if (lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stv;
     }
 
-    RK_MARK(3);
+    RK_MARK(5);
     // ---- state out (the next launch takes it from HBM) ----
     if (own) {
-        copy_rounds<4>(a.tnr + (size_t)c * ns, nodes, ns, lane);
+        // the nodes this launch changed (against the values it loaded; tick 0 writes them all): the
+        // stores, and the L2 write-back at the launch end, scale with the tick's changes
+#pragma unroll
+        for (uint32_t q = 0; q < kRkNodes / kWave; ++q) {
+            const uint32_t i = q * kWave + lane;
+            if (i < ns) {
+                const unsigned long long v = nodes[i];
+                if (mode == 0u || v != nreg[q]) a.tnr[(size_t)c * ns + i] = v;
+            }
+        }
         if (lane < kStW) reinterpret_cast<uint32_t*>(&a.cl[c])[lane] = reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane];
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-            if ((drt >> r) & 1u) {
-                a.sfin[sb + r * kWave + lane] = fin[r];
-                a.snode[sb + r * kWave + lane] = pay[r];
+        for (int k = 0; k < kRows / 4; ++k) {  // a quad with a changed row, back as one 16-byte store
+            if ((drt >> (4 * k)) & 15u) {
+                const size_t q = sb + (size_t)k * 4u * kWave + 4u * lane;
+                *reinterpret_cast<uint4*>(a.sfin + q) = make_uint4(fin[4 * k], fin[4 * k + 1], fin[4 * k + 2], fin[4 * k + 3]);
+                *reinterpret_cast<uint4*>(a.snode + q) = make_uint4(pay[4 * k], pay[4 * k + 1], pay[4 * k + 2], pay[4 * k + 3]);
             }
         }
     }
@@ -793,9 +852,14 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     }
 #ifdef MCS_RK_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
-    RK_MARK(4);
+    RK_MARK(6);
     if (lane == 0 && g < kTrResMaxClusters)
         for (int i = 0; i < kRkSeg; ++i) atomicAdd(&g_rk_stamps[g * kRkSeg + i], (unsigned long long)rk_acc[i]);
+    if (threadIdx.x == 0 && wg < 16u && mode != 0u) {
+        unsigned long long* tl = g_rk_tl + ((size_t)(ctlv.ticks & (kRkTl - 1u)) * 16u + wg) * 2u;
+        tl[0] = rk_t0;
+        tl[1] = __builtin_amdgcn_s_memrealtime();
+    }
 #endif
 }
 
@@ -833,5 +897,9 @@ extern "C" int mcs_debug_rk_stamps(unsigned long long* out) {
     unsigned long long z[mcs::kTrResMaxClusters * mcs::kRkSeg] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_rk_stamps), sizeof(z)) != hipSuccess) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_rk_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+// the launch timeline ring of the stamp build: kRkTl ticks x 16 workgroups x {start, end} (100 MHz)
+extern "C" int mcs_debug_rk_timeline(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_rk_tl), sizeof(mcs::g_rk_tl)) == hipSuccess ? 0 : -1;
 }
 #endif
