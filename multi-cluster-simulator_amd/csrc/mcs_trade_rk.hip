@@ -461,6 +461,11 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             const int src = (int)(rqc < 64u ? rqc : 0u);
 #pragma unroll
             for (uint32_t k = 0; k < kRkLenders; ++k) gv[k] = (uint32_t)__shfl((int)gl[k], src);
+            // the wave's lenders' queue state, lane k holding lender w + 4k's (read once, before the
+            // loop's LDS stores)
+            const uint32_t Lk = wave + lane * (uint32_t)kRkWaves;
+            const uint32_t qsk = lane < kRkLenders && Lk < C ? sh.qs[Lk] : 0u;
+            const uint32_t lqk = lane < kRkLenders && Lk < C ? sh.lq[Lk] : 0u;
             uint32_t accw0 = 0u, accw1 = 0u, fbw = 0u;
 #pragma unroll
             for (uint32_t k = 0; k < kRkLenders; ++k) {
@@ -468,7 +473,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
                 if (L >= C) break;
                 const bool want_l = want && lane != L;  // self skipped (:176)
                 unsigned long long okm;
-                if (!(sh.qs[L] & kQsBig)) {
+                if (!(readlane(qsk, k) & kQsBig)) {
                     okm = __ballot(want_l && rqc < 64u && gv[k] > rqm);
                 } else {
                     okm = 0ull;
@@ -492,7 +497,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
                     }
                 }
                 const uint32_t nacc = (uint32_t)__builtin_popcountll(okm);
-                const uint32_t lq0 = sh.lq[L];  // (post-A; == the owner's own count)
+                const uint32_t lq0 = readlane(lqk, k);  // (post-A; == the owner's own count)
                 const uint32_t LQ = a.LQ;
                 if (lq0 + nacc > LQ) fbw = 1u;
                 accw0 |= (uint32_t)okm;
@@ -571,30 +576,31 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     }
 
     // ---- A: tick n + 1 (tick 0 in mode 0) for this rank's clusters (tr_step_kernel) ----
-    if (own) {  // the nodes to the wave's LDS copy (the loads of the launch start)
+    // (the LDS values A starts from, read in one batch)
+    const uint32_t doneA = sh.done, TA = sh.T;
+    const uint32_t ndue = lane < C ? sh.trs[lane].next_due : kEmpty;  // (C <= 64)
+    uint32_t stv = lane < kStW ? reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane] : 0u;
+    // the nodes in registers (node q * 64 + l in lane l, word q; 0 past N): the releases alone go
+    // through the wave's LDS copy (a scatter), first fit and the commits stay in registers
+    unsigned long long nv[kRkNodes / kWave];
 #pragma unroll
-        for (uint32_t q = 0; q < kRkNodes / kWave; ++q)
-            if (q * kWave + lane < ns) nodes[q * kWave + lane] = nreg[q];
-    }
-    if (own && sh.done == 0u) {
+    for (uint32_t q = 0; q < kRkNodes / kWave; ++q) nv[q] = q * kWave + lane < N ? nreg[q] : 0ull;
+    if (own && doneA == 0u) {
         // the free slot rows
 #pragma unroll
         for (int r = 0; r < kRows; ++r)
             if (fin[r] == kEmpty) frm |= 1u << r;
-        const uint32_t T = sh.T;
-        bool sample = false;
-        if (a.trader && T % a.sample_period == 0u) {
-            bool due = false;
-            for (uint32_t q = lane; q < C; q += kWave) due = due || sh.trs[q].next_due <= T;
-            sample = __ballot(due) != 0ull;
-        }
-        uint32_t stv = lane < kStW ? reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane] : 0u;
+        const uint32_t T = TA;
+        const bool sample = a.trader && T % a.sample_period == 0u && __ballot(ndue <= T) != 0ull;
         // (the WaitQueue head may have left for the BorrowedQueue in X2: the window still holds
         // the ReadyQueue head or job_at loads it)
         const uint32_t na0 = RST(next_arr);
         RK_MARK(7);
         // releases due at T (cluster.go:153-157), before the tick's decisions
         if (RST(minf) <= T) {
+#pragma unroll
+            for (uint32_t q = 0; q < kRkNodes / kWave; ++q)
+                if (q * kWave + lane < N) nodes[q * kWave + lane] = nv[q];
             uint32_t lm = kEmpty, nrel = 0;
 #pragma unroll
             for (int r = 0; r < kRows; ++r) {
@@ -614,6 +620,9 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             }
             RST(nrun) -= rk_wave_sum(nrel);
             RST(minf) = wave_min_u32(lm);
+#pragma unroll
+            for (uint32_t q = 0; q < kRkNodes / kWave; ++q)
+                if (q * kWave + lane < N) nv[q] = nodes[q * kWave + lane];
         }
         RK_MARK(8);
         // arrivals up to T join the ReadyQueue (jobs are sorted by arrival)
@@ -643,17 +652,11 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         // ScheduleJob (scheduler.go:127-139); zero-capacity virtual nodes follow the physical ones
         const uint32_t vn = sh.trs[g].vnodes;
         auto first_fit = [&](uint32_t jc, uint32_t jm) -> uint32_t {
-            unsigned long long v[kRkNodes / kWave];
-#pragma unroll
-            for (uint32_t q = 0; q < kRkNodes / kWave; ++q) {
-                const uint32_t i = q * kWave + lane;
-                v[q] = i < N ? nodes[i] : 0ull;
-            }
             uint32_t kk = kEmpty;
 #pragma unroll
             for (uint32_t q = 0; q < kRkNodes / kWave; ++q) {
                 const uint32_t i = q * kWave + lane;
-                const unsigned long long m = __ballot(i < N && (uint32_t)v[q] >= jc && (uint32_t)(v[q] >> 32) >= jm);
+                const unsigned long long m = __ballot(i < N && (uint32_t)nv[q] >= jc && (uint32_t)(nv[q] >> 32) >= jm);
                 if (m && kk == kEmpty) kk = q * kWave + (uint32_t)__builtin_ctzll(m);
             }
             if (kk == kEmpty && jc == 0u && jm == 0u && vn > 0u) kk = N;
@@ -666,8 +669,13 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             if (!any) return false;
             const uint32_t sel = (uint32_t)__builtin_ctzll(any);
             const uint32_t row = (uint32_t)__builtin_ctz(readlane(frm, sel));
+            {  // node kn: lane kn % 64, word kn / 64 (masks, not an index: nv stays in registers)
+                const bool mine = kn < N && lane == (kn & 63u);
+#pragma unroll
+                for (uint32_t q = 0; q < kRkNodes / kWave; ++q)
+                    nv[q] -= need & (0ull - (unsigned long long)(mine && q == (kn >> 6)));
+            }
             if (lane == sel) {
-                if (kn < N) atomicSub(&nodes[kn], need);
                 const uint32_t p = (kn < N ? kn : 511u) | (jc << 9) | (jm << 16);
 #pragma unroll
                 for (int r = 0; r < kRows; ++r)
@@ -761,10 +769,10 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         if (sample) {
             // (the capacities' uint32 sum is total_c / total_m, tr_init_kernel's SetTotalResources)
             uint32_t fc = 0u, fm = 0u;
-            for (uint32_t i = lane; i < N; i += kWave) {
-                const unsigned long long v = nodes[i];
-                fc += (uint32_t)v;
-                fm += (uint32_t)(v >> 32);
+#pragma unroll
+            for (uint32_t q = 0; q < kRkNodes / kWave; ++q) {  // (0 past N)
+                fc += (uint32_t)nv[q];
+                fm += (uint32_t)(nv[q] >> 32);
             }
             const float sc = (float)(int32_t)((uint32_t)RST(total_c) - rk_wave_sum(fc));
             const float sm = (float)(int32_t)((uint32_t)RST(total_m) - rk_wave_sum(fm));
@@ -776,13 +784,13 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         uint32_t* const tab = sh.gtab[wave];
         tab[lane] = 0u;
         bool big = false;
-        for (uint32_t i = lane; i < N; i += kWave) {
-            const unsigned long long v = nodes[i];
-            const uint32_t fc = (uint32_t)v;
+#pragma unroll
+        for (uint32_t q = 0; q < kRkNodes / kWave; ++q) {  // (0 past N: no entry)
+            const uint32_t fc = (uint32_t)nv[q];
             if (fc > 64u)
                 big = true;
             else if (fc > 0u)
-                atomicMax(&tab[fc - 1u], (uint32_t)(v >> 32));
+                atomicMax(&tab[fc - 1u], (uint32_t)(nv[q] >> 32));
         }
         const bool bigw = __ballot(big) != 0ull;
         rk_gtab(a, xw, g)[63u - lane] = wave_scan_max_u32(tab[63u - lane]);  // G[63 - lane]
@@ -809,7 +817,12 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         xv = lane == kRkTm ? (uint32_t)RST(total_m) : xv;
         uint32_t* const rp = rk_rec(a, xw, g);
         if (lane < kRkWords) rp[lane] = xv;
-        if (bigw) copy_rounds<4>(rk_snap(a, xw, g), nodes, N, lane);  // (read only for a big lender)
+        if (bigw) {  // (read only for a big lender)
+            unsigned long long* const sn = rk_snap(a, xw, g);
+#pragma unroll
+            for (uint32_t q = 0; q < kRkNodes / kWave; ++q)
+                if (q * kWave + lane < N) sn[q * kWave + lane] = nv[q];
+        }
         if (lane == 0 && lent_now) a.lrp[c] = lr;
         if (lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stv;
     }
@@ -822,10 +835,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
 #pragma unroll
         for (uint32_t q = 0; q < kRkNodes / kWave; ++q) {
             const uint32_t i = q * kWave + lane;
-            if (i < ns) {
-                const unsigned long long v = nodes[i];
-                if (mode == 0u || v != nreg[q]) a.tnr[(size_t)c * ns + i] = v;
-            }
+            if (i < N && (mode == 0u || nv[q] != nreg[q])) a.tnr[(size_t)c * ns + i] = nv[q];
         }
         if (lane < kStW) reinterpret_cast<uint32_t*>(&a.cl[c])[lane] = reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane];
 #pragma unroll
