@@ -50,9 +50,15 @@ static_assert(kRkWords * 4u == sizeof(TrXRec), "record size");
 // some node with free_c > 64 (no G table: phase B scans the snapshot)
 constexpr uint32_t kQsW = 1u, kQsRq = 2u, kQsLent = 4u, kQsLq = 8u, kQsDone = 16u, kQsBig = 32u;
 
-__device__ __forceinline__ uint32_t rk_wave_sum(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-    return v;
+// a wave's uint32 sum (wrapping), on the DPP scan: VALU steps, no LDS-pipe round trips
+__device__ __forceinline__ uint32_t rk_wave_sum(uint32_t v) { return readlane(wave_scan_add_u32(v), 63u); }
+// a wave's OR of a flags word: one ballot per bit some lane holds (none on most ticks)
+__device__ __forceinline__ uint32_t rk_wave_or(uint32_t v) {
+    uint32_t r = 0u;
+    if (__ballot(v != 0u))
+        for (uint32_t b = 0; b < 32u; ++b)
+            if (__ballot((v >> b) & 1u)) r |= 1u << b;
+    return r;
 }
 // The exchange blocks are double-buffered by tick parity: launch n reads tick n's blocks (buffer
 // n & 1, gathered) while its phase A writes tick n + 1's (buffer (n + 1) & 1), so a workgroup that
@@ -188,9 +194,8 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     const TrTrader* const tr_r = a.tr + (size_t)par * C;
     TrTrader* const tr_w = a.tr + (size_t)(par ^ 1u) * C;
 
-    // ---- state in: every load of the launch issued before any of its values is used, in the order
-    // the launch needs them (vmcnt retires in order: the copies before the barrier wait for the
-    // trader state and the exchange alone; the slot rows and nodes land during phases B-D).  The
+    // ---- state in: every load phases B-D need issued before any of its values is used (one round
+    // trip; phase A's nodes and slot rows follow the barrier and land during B-D).  The
     // loads are unconditional, from clamped in-range addresses (a value no one uses is never read):
     // a load under a branch makes the compiler merge, and so wait for, its value at the join. ----
     // Every address first, then (past a scheduling fence) every load: a load's destination register
@@ -229,22 +234,6 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     const uint32_t stw = *stp;
     const uint32_t nb0 = a.node_off[c], nb1 = a.node_off[c + 1];
     const unsigned long long jb0 = a.job_off[c], jb1 = a.job_off[c + 1];
-    unsigned long long nreg[kRkNodes / kWave];
-#pragma unroll
-    for (uint32_t q = 0; q < kRkNodes / kWave; ++q) nreg[q] = *np[q];
-    uint32_t fin[kRows], pay[kRows];
-#pragma unroll
-    for (int k = 0; k < kRows / 4; ++k) {
-        const uint4 f = finp[k * kWave], p = payp[k * kWave];
-        fin[4 * k] = f.x;
-        fin[4 * k + 1] = f.y;
-        fin[4 * k + 2] = f.z;
-        fin[4 * k + 3] = f.w;
-        pay[4 * k] = p.x;
-        pay[4 * k + 1] = p.y;
-        pay[4 * k + 2] = p.z;
-        pay[4 * k + 3] = p.w;
-    }
     const uint4 w0 = rp[0], w1 = rp[1], w2 = rp[2], w3 = rp[3];
     const uint4 lrv = *lrpp;
     uint32_t gl[kRkLenders];
@@ -294,6 +283,24 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         return;  // (uniform)
     }
     RK_MARK(2);
+    // phase A's nodes and slot rows: issued after the barrier, they land while phases B-D run (no
+    // load before A waits for them), and the launch-start batch above stays small
+    unsigned long long nreg[kRkNodes / kWave];
+#pragma unroll
+    for (uint32_t q = 0; q < kRkNodes / kWave; ++q) nreg[q] = *np[q];
+    uint32_t fin[kRows], pay[kRows];
+#pragma unroll
+    for (int k = 0; k < kRows / 4; ++k) {
+        const uint4 f = finp[k * kWave], p = payp[k * kWave];
+        fin[4 * k] = f.x;
+        fin[4 * k + 1] = f.y;
+        fin[4 * k + 2] = f.z;
+        fin[4 * k + 3] = f.w;
+        pay[4 * k] = p.x;
+        pay[4 * k + 1] = p.y;
+        pay[4 * k + 2] = p.z;
+        pay[4 * k + 3] = p.w;
+    }
     const uint32_t n0 = nb0, N = nb1 - nb0, J = (uint32_t)(jb1 - jb0);
     const uint64_t j0 = jb0;
     if (own && mode == 0u) {  // tick 0: the nodes from the CSR initial state
@@ -419,7 +426,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             const bool done_all = !__ballot(!done_g);
             const bool busy_any = __ballot(busy != 0u) != 0ull;
             nxt = wave_min_u32(nxt);
-            for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o);
+            fl = rk_wave_or(fl);
             // (C/D reads trs[q] of its own lane only before this barrier-free store: lane q owns q)
             if (a.trader && q < C) sh.trs[q] = t;
             if (lane == 0) {
@@ -601,10 +608,11 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
 #pragma unroll
             for (uint32_t q = 0; q < kRkNodes / kWave; ++q)
                 if (q * kWave + lane < N) nodes[q * kWave + lane] = nv[q];
-            uint32_t lm = kEmpty, nrel = 0;
+            uint32_t lm = kEmpty, nrel = 0;  // (nrel: the wave's releases, from the rows' ballots)
 #pragma unroll
             for (int r = 0; r < kRows; ++r) {
                 const uint32_t f = fin[r];
+                nrel += (uint32_t)__builtin_popcountll(__ballot(f <= T));
                 if (f <= T) {
                     const uint32_t p = pay[r], kn = p & 511u;
                     if (kn < N)
@@ -613,12 +621,11 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
                     fin[r] = kEmpty;
                     frm |= 1u << r;
                     drt |= 1u << r;
-                    ++nrel;
                 } else {
                     lm = f < lm ? f : lm;
                 }
             }
-            RST(nrun) -= rk_wave_sum(nrel);
+            RST(nrun) -= nrel;
             RST(minf) = wave_min_u32(lm);
 #pragma unroll
             for (uint32_t q = 0; q < kRkNodes / kWave; ++q)
