@@ -17,11 +17,15 @@
 //       workgroup moves its own borrowers' WaitQueue heads to the BorrowedQueue
 //       (scheduler.go:237-242), every lender's wave appends to its LentQueue in borrower order
 //       (server.go:80-113, owner rank), and the append-overflow verdict is replicated
-//   C+D wave 0 of every workgroup on identical inputs: the trader rounds (trader.go:280-325,
-//       193-278; server.go:31-85) and the next tick's clock — replicated, as in the MW tick
+//   C+D a fifth (helper) wave of every workgroup on identical inputs, while the cluster waves run B:
+//       the trader rounds (trader.go:280-325, 193-278; server.go:31-85) and the next tick's clock —
+//       replicated, as in the MW tick
 //   A   tick n + 1 (tr_step_kernel's phase, scheduler.go:216-296 + the borrow request): this rank's
 //       waves; the record and the node snapshot go to the rank's block of the exchange buffer
 // The workgroups never wait for each other (no granule exchange, no co-residency requirement).
+// A launch is latency-bound: every load B-D needs issues in one batch at the start,
+// phase A's nodes and slot rows right after the first barrier (they land during B-D), and phase A
+// keeps the nodes in registers.
 // The first launch of a run (mode 0) runs phase A of tick 0 only.  The state between launches
 // (nodes, running slots, queue cursors, trader state, the clock) lives in HBM, as across the MW
 // kernel's launches.  The caller-driven phase API (mcs_trade_phase) runs the same launches with the
@@ -38,6 +42,9 @@ namespace {
 constexpr int kRkWaves = 4;                // clusters (waves) per workgroup
 constexpr uint32_t kRkNodes = 256;         // nodes per cluster
 constexpr uint32_t kRkLenders = kTrResMaxClusters / kRkWaves;  // lenders per wave in phase B
+// + one helper wave per workgroup: phases C/D (the trader rounds and the clock) while the cluster
+// waves run phase B, so the two overlap instead of adding up on wave 0
+constexpr int kRkThreads = (kRkWaves + 1) * kWave;
 
 // a cluster's post-A record in the exchange block: 16 words, the size of TrXRec (the three-kernel
 // record), so both forms lay the blocks out alike (records, then the node snapshots)
@@ -89,8 +96,8 @@ __device__ __forceinline__ uint32_t* rk_gtab(const TradeArgs& a, unsigned char* 
 
 constexpr uint32_t kStW = sizeof(TrCluster) / 4u;
 constexpr uint32_t kTrW = sizeof(TrTrader) / 4u;
-static_assert(sizeof(TrTrader) % 4u == 0u && kTrResMaxClusters * kTrW <= 2u * kRkWaves * kWave,
-              "the trader state in two words per thread");
+static_assert(sizeof(TrTrader) % 4u == 0u && kTrResMaxClusters * kTrW <= (uint32_t)kRkThreads,
+              "the trader state in one word per thread");
 static_assert(sizeof(TrCluster) % 4u == 0u && kStW <= (uint32_t)kWave, "TrCluster in one VGPR");
 struct RkField {  // a TrCluster field held in lane f of a VGPR (phase A's cluster state)
     uint32_t& v;
@@ -118,7 +125,7 @@ struct RkField {  // a TrCluster field held in lane f of a VGPR (phase A's clust
 // probe build (tools/variant.sh ... -DMCS_RK_STAMPS): per-wave segment times (s_memrealtime, 100 MHz)
 // summed over the launches since the last read: [wave of the system][segment]; segments: 0 launch
 // start -> state in, 1 -> B and C/D done, 2 -> acceptances applied, 3 -> phase A done, 4 -> state out
-constexpr int kRkSeg = 12;
+constexpr int kRkSeg = 14;
 __device__ unsigned long long g_rk_stamps[kTrResMaxClusters * kRkSeg];
 constexpr uint32_t kRkTl = 8192;  // timeline ring: [tick & (kRkTl - 1)][workgroup] {start, end}
 __device__ unsigned long long g_rk_tl[kRkTl * 16 * 2];
@@ -158,7 +165,7 @@ struct RkShared {  // (the workgroup's node vectors follow: kRkWaves * ns u64)
 };
 
 template <int kRows>  // slot rows per cluster (64 slots each; a multiple of 4)
-__global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, uint32_t mode) {
+__global__ __launch_bounds__(kRkThreads) void tr_rk_kernel(TradeArgs a, uint32_t mode) {
     // mode 0: phase A of tick 0 (writes buffer 0); mode 1 / 2: tick n with n & 1 = mode - 1 (the host
     // knows the parity: a graph replays an even number of ticks, the caller-driven path counts them),
     // so every address below is known at the launch start and all of its loads issue at once
@@ -175,11 +182,13 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     const uint32_t wg = blockIdx.x;
     RK_WAIT_ARGS(C);
     RK_MARK(0);
-    const uint32_t g = wg * kRkWaves + wave;  // this wave's cluster of the system
+    const bool helper = wave == (uint32_t)kRkWaves;  // (C/D; no cluster)
+    const uint32_t g = wg * kRkWaves + (helper ? 0u : wave);  // this wave's cluster of the system
     const uint32_t lo = a.rank * Cl;          // this rank's clusters: [lo, lo + Cl)
-    const bool sys = g < C;
+    const bool sys = !helper && g < C;
     const bool own = sys && g >= lo && g < lo + Cl;
-    const uint32_t c = own ? g - lo : 0u;  // its local index
+    // its local index (the helper: wave 0's, so its unused loads hit the lines wave 0 reads)
+    const uint32_t c = g < C && g >= lo && g < lo + Cl ? g - lo : 0u;
     unsigned long long* const nodes = nodes_wg + (size_t)wave * ns;
     // tick n's blocks (read) and tick n + 1's (written); mode 0 writes tick 0's
     const size_t xbuf = (size_t)a.world * a.blk;
@@ -201,10 +210,9 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     // Every address first, then (past a scheduling fence) every load: a load's destination register
     // reused by an address computation after it would make the compiler wait for that load.
     const TrCtl ctlv = *ctl_r;  // (uniform: scalar loads)
-    // the replicated trader state as flat words (C * kTrW <= 2 * 256)
+    // the replicated trader state as flat words (C * kTrW <= the workgroup's threads)
     const uint32_t trn = C * kTrW, tq = threadIdx.x;
     const uint32_t* const trp0 = reinterpret_cast<const uint32_t*>(tr_r) + min(tq, trn - 1u);
-    const uint32_t* const trp1 = reinterpret_cast<const uint32_t*>(tr_r) + min(tq + (uint32_t)(kRkWaves * kWave), trn - 1u);
     // this wave's cluster (c = 0 for a wave that owns none: its values are never read): TrCluster
     // (lane f < kStW: word f), CSR bounds, the dense node copy (tick 0's from the CSR initial state,
     // after the barrier), the running slots in registers (row r, lane l: slot (r / 4) * 256 + 4l +
@@ -230,7 +238,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         glp[k] = rk_gtab(a, xr, L < C ? L : 0u) + lane;
     }
     __builtin_amdgcn_sched_barrier(0);
-    const uint32_t trv0 = *trp0, trv1 = *trp1;
+    const uint32_t trv0 = *trp0;
     const uint32_t stw = *stp;
     const uint32_t nb0 = a.node_off[c], nb1 = a.node_off[c + 1];
     const unsigned long long jb0 = a.job_off[c], jb1 = a.job_off[c + 1];
@@ -243,7 +251,6 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     // the LDS copies
     if (own && lane < kStW) reinterpret_cast<uint32_t*>(&sh.st[wave])[lane] = stw;
     if (tq < trn) reinterpret_cast<uint32_t*>(sh.trs)[tq] = trv0;
-    if (tq + kRkWaves * kWave < trn) reinterpret_cast<uint32_t*>(sh.trs)[tq + kRkWaves * kWave] = trv1;
     if (threadIdx.x == 0) {
         sh.T = sh.T0 = ctlv.T;
         sh.done = ctlv.done;
@@ -277,7 +284,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     if (sh.done) {  // the graph's launches after the end of the run: the final state carried forward
         if (mode != 0u && wg == 0) {
-            for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) tr_w[q] = sh.trs[q];
+            for (uint32_t q = threadIdx.x; q < C; q += kRkThreads) tr_w[q] = sh.trs[q];
             if (threadIdx.x == 0) *ctl_w = ctlv;
         }
         return;  // (uniform)
@@ -327,10 +334,11 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     // (both windows in flight from here: the job records of the next phase A, and the LentQueue head
     // when the queue already held entries after tick n's phase A; one this launch's appends write into
     // an empty queue is taken from the request registers in phase B)
-    if (own) {
-        const TrCluster& s0 = sh.st[wave];
-        prefetch_jobs(s0.has_w ? s0.w : s0.rq_head, s0.next_arr);
-        prefetch_lq(s0.lq_head, s0.lq_len);
+    if (own) {  // (the cluster state as loaded: lane f of stw holds word f)
+#define RK_STW(field) readlane(stw, (uint32_t)(offsetof(TrCluster, field) / 4u))
+        prefetch_jobs(RK_STW(has_w) ? RK_STW(w) : RK_STW(rq_head), RK_STW(next_arr));
+        prefetch_lq(RK_STW(lq_head), RK_STW(lq_len));
+#undef RK_STW
     }
 
     if (mode != 0u) {
@@ -339,9 +347,11 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         // the gathered lent bits: this rank's log counts its own runs (ctl->n_lent is per rank) ----
         {
             const unsigned long long rmask = (Cl >= 64u ? ~0ull : ((1ull << Cl) - 1ull)) << lo;
-            const unsigned long long lm = __ballot(lane < C && (sh.qs[lane] & kQsLent)) & rmask;
-            if (own && lane == 0 && (sh.qs[g] & kQsLent)) {
-                const unsigned long long idx = sh.n_lent + (uint64_t)__builtin_popcountll(lm & ((1ull << g) - 1ull));
+            const uint32_t qsl = lane < C ? sh.qs[lane] : 0u;
+            const unsigned long long lm = __ballot(qsl & kQsLent) & rmask;
+            const bool lent_g = own && ((lm >> g) & 1ull);  // (g < 64)
+            if (lent_g && lane == 0) {
+                const unsigned long long idx = ctlv.n_lent + (uint64_t)__builtin_popcountll(lm & ((1ull << g) - 1ull));
                 if (idx < a.lent_cap) {
                     const uint4 lr = lrv;
                     mcs_lent_rec rec;
@@ -355,12 +365,13 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
                     a.lent_log[idx] = rec;
                 }
             }
-            if (threadIdx.x == 0) sh.n_lent_next = sh.n_lent + (uint64_t)__builtin_popcountll(lm);
+            if (threadIdx.x == 0) sh.n_lent_next = ctlv.n_lent + (uint64_t)__builtin_popcountll(lm);
         }
-        // ---- C and D: wave 0 of every workgroup, one lane per cluster, on X1 alone (as the MW tick:
+        RK_MARK(11);
+        // ---- C and D: the helper wave of every workgroup, one lane per cluster, on X1 alone (as the MW tick:
         // every borrow request leaves its borrower busy, so the clock and the end of the run follow
         // from X1; the acceptances are applied after the X2 exchange, before phase A) ----
-        if (wave == 0) {
+        if (helper) {
             const uint32_t q = lane;
             float cu = 0.0f, mu = 0.0f;
             uint32_t tot_c = 0u, tot_m = 0u, busy = 0u, next_arr_t = kEmpty, done_g = 1u, fl = 0u;
@@ -450,6 +461,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
                 sh.n_won = n_won;
             }
         }
+        RK_MARK(12);
         // ---- B (replicated in every workgroup): the acceptance matrix of tick n.  Wave w takes
         // lenders w, w + 4, ...; lane b holds borrower b's request.  Lender L accepts b when
         // G_L[c_b] > m_b (free_c > c_b and free_m > m_b on some node; c_b >= 64 fits no node of a
@@ -462,7 +474,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
             rqd = sh.rq_dur[lane];
         }
         const bool want = rqj != kEmpty;
-        if (__ballot(want)) {
+        if (!helper && __ballot(want)) {
             // G_L[c_b] for every lender of the wave (a lane permute of the tables loaded at the start)
             uint32_t gv[kRkLenders];
             const int src = (int)(rqc < 64u ? rqc : 0u);
@@ -548,6 +560,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
                 if (fbw) atomicOr(&sh.accm[2], 1u);
             }
         }
+        RK_MARK(13);
         __syncthreads();
         RK_MARK(3);
         // ---- the acceptances (identical in every workgroup and on every rank): BorrowedQueue append,
@@ -586,7 +599,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
     // (the LDS values A starts from, read in one batch)
     const uint32_t doneA = sh.done, TA = sh.T;
     const uint32_t ndue = lane < C ? sh.trs[lane].next_due : kEmpty;  // (C <= 64)
-    uint32_t stv = lane < kStW ? reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane] : 0u;
+    uint32_t stv = !helper && lane < kStW ? reinterpret_cast<const uint32_t*>(&sh.st[wave])[lane] : 0u;
     // the nodes in registers (node q * 64 + l in lane l, word q; 0 past N): the releases alone go
     // through the wave's LDS copy (a scatter), first fit and the commits stay in registers
     unsigned long long nv[kRkNodes / kWave];
@@ -855,7 +868,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
         }
     }
     if (wg == 0 && mode != 0u) {
-        for (uint32_t q = threadIdx.x; q < C; q += kRkWaves * kWave) tr_w[q] = sh.trs[q];
+        for (uint32_t q = threadIdx.x; q < C; q += kRkThreads) tr_w[q] = sh.trs[q];
         if (threadIdx.x == 0) {
             TrCtl* ctl = ctl_w;
             ctl->T = sh.T;
@@ -870,7 +883,7 @@ __global__ __launch_bounds__(kRkWaves * kWave) void tr_rk_kernel(TradeArgs a, ui
 #ifdef MCS_RK_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
     RK_MARK(6);
-    if (lane == 0 && g < kTrResMaxClusters)
+    if (lane == 0 && !helper && g < kTrResMaxClusters)
         for (int i = 0; i < kRkSeg; ++i) atomicAdd(&g_rk_stamps[g * kRkSeg + i], (unsigned long long)rk_acc[i]);
     if (threadIdx.x == 0 && wg < 16u && mode != 0u) {
         unsigned long long* tl = g_rk_tl + ((size_t)(ctlv.ticks & (kRkTl - 1u)) * 16u + wg) * 2u;
@@ -899,11 +912,11 @@ hipError_t launch_trade_rk(const TradeArgs& a, uint32_t mode, size_t lds, hipStr
     hipError_t st = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (st != hipSuccess) return st;
     if (a.S == 4u * kWave)
-        hipLaunchKernelGGL(tr_rk_kernel<4>, dim3(nwg), dim3(kRkWaves * kWave), lds, s, a, mode);
+        hipLaunchKernelGGL(tr_rk_kernel<4>, dim3(nwg), dim3(kRkThreads), lds, s, a, mode);
     else if (a.S == 8u * kWave)
-        hipLaunchKernelGGL(tr_rk_kernel<8>, dim3(nwg), dim3(kRkWaves * kWave), lds, s, a, mode);
+        hipLaunchKernelGGL(tr_rk_kernel<8>, dim3(nwg), dim3(kRkThreads), lds, s, a, mode);
     else
-        hipLaunchKernelGGL(tr_rk_kernel<16>, dim3(nwg), dim3(kRkWaves * kWave), lds, s, a, mode);
+        hipLaunchKernelGGL(tr_rk_kernel<16>, dim3(nwg), dim3(kRkThreads), lds, s, a, mode);
     return hipGetLastError();
 }
 

@@ -20,7 +20,7 @@ from mcs_amd import _lib as L  # noqa: E402
 J = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
 arrays, streams, _ = seeded_workload("n256", 64, J)
 fn = L.lib().mcs_debug_rk_stamps
-buf = (C.c_ulonglong * (64 * 12))()
+buf = (C.c_ulonglong * (64 * 14))()
 with Engine(0, borrow=True, trader=True, t_max_s=20_000_000) as eng:
     eng.load_clusters(arrays)
     eng.set_shard(0, 1)
@@ -31,9 +31,9 @@ with Engine(0, borrow=True, trader=True, t_max_s=20_000_000) as eng:
     assert fn(buf) == 0
     ts = eng.trade_stats()
 ticks = ts["ticks"]
-seg = [[buf[w * 12 + i] for i in range(12)] for w in range(64)]
-avg = [sum(s[i] for s in seg) / 64 / ticks * 10.0 / 1000.0 for i in range(12)]  # us per tick (100 MHz)
-mx = [max(s[i] for s in seg) / ticks * 10.0 / 1000.0 for i in range(12)]
+seg = [[buf[w * 14 + i] for i in range(14)] for w in range(64)]
+avg = [sum(s[i] for s in seg) / 64 / ticks * 10.0 / 1000.0 for i in range(14)]  # us per tick (100 MHz)
+mx = [max(s[i] for s in seg) / ticks * 10.0 / 1000.0 for i in range(14)]
 # the launch timeline: per tick, the workgroups' first start, last start and last end
 tl = (C.c_ulonglong * (8192 * 16 * 2))()
 assert L.lib().mcs_debug_rk_timeline(tl) == 0
@@ -56,5 +56,5 @@ timeline = {"ticks_seen": len(rows), "launch_us": round(sum(dur) / max(len(dur),
             "gap_min_us": round(min(gap), 3) if gap else None}
 print(json.dumps({"timeline": timeline, "ticks": ticks, "loop_form": ts["loop_form"], "kernel_ms": st.kernel_ms,
                   "us_per_tick": st.kernel_ms * 1e3 / max(ticks, 1),
-                  "segments": ["args", "loads_issued", "loads_back_and_barrier", "B_and_CD", "apply", "A_record", "state_out", "A_nodes_to_lds", "A_releases", "A_arrivals_decisions", "A_sample_gtable", "unused"],
+                  "segments": ["args", "loads_issued", "loads_back_and_barrier", "B_barrier", "apply", "A_record", "state_out", "A_nodes_to_lds", "A_releases", "A_arrivals_decisions", "A_sample_gtable", "lent_log", "CD_wave0", "B"],
                   "avg_us_per_tick": [round(x, 3) for x in avg], "max_wave_us_per_tick": [round(x, 3) for x in mx]}))
