@@ -147,43 +147,10 @@ int dt_poll(mcs_engine* e) {
     return MCS_OK;
 }
 
-// MCS_DTRADE_RESIDENT=1 selects the one-workgroup resident tick (opt-in: on C5-DELAY it measured
-// 24.9 us/tick against the graph-replayed kernels' 19.5); MCS_TRADE_RES_TICKS caps
-// the ticks of one resident launch (tests cross launch boundaries with it)
-bool dt_resident(mcs_engine* e, size_t* lds) {
-    const char* env = getenv("MCS_DTRADE_RESIDENT");
-    if (!env || atoi(env) == 0) return false;
-    if (!dtrade_res_shape(e->dtd->a, e->world, lds)) return false;
-    int max_lds = 0;
-    if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device) != hipSuccess)
-        return false;
-    return *lds <= (size_t)max_lds;
-}
-
 int dt_run_once(mcs_engine* e, double* kernel_ms) {
     DtradeDev* d = e->dtd;
     hipError_t st = launch_dtrade_init(d->a, e->stream);
     if (st != hipSuccess) return dt_hip_fail(e, "DELAY trading init", st);
-    size_t lds = 0;
-    if (dt_resident(e, &lds)) {
-        const char* tenv = getenv("MCS_TRADE_RES_TICKS");
-        const long tv = tenv ? atol(tenv) : 0;
-        const uint32_t budget = tv > 0 && tv < (1l << 16) ? (uint32_t)tv : (1u << 16);
-        d->loop_form = kLoopResident;
-        HIPCHK(e, hipEventRecord(e->ev0, e->stream));
-        for (;;) {
-            st = launch_dtrade_res(d->a, budget, lds, e->stream);
-            if (st != hipSuccess) return dt_hip_fail(e, "resident DELAY trading tick", st);
-            if (int s = dt_poll(e)) return s;
-            if (d->h_ctl->done) break;
-        }
-        HIPCHK(e, hipEventRecord(e->ev1, e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
-        float ms = 0.0f;
-        HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
-        *kernel_ms = ms;
-        return MCS_OK;
-    }
     if (!d->graph) {
         hipGraph_t g = nullptr;
         HIPCHK(e, hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
@@ -365,8 +332,8 @@ int dtrade_run(mcs_engine* e, mcs_stats* stats) {
         if (!grow_s && !grow_v) break;
         if ((grow_s && (e->cfg.slot_pool || S >= kDtMaxSlots)) || (grow_v && V >= kDtMaxVnodes))
             return fail(e, MCS_E_CAPACITY, "DELAY trading capacity exhausted (slots or virtual nodes)");
-        // slots grow by half (a multiple of 64): the resident tick keeps every slot in LDS, where
-        // the next power of two may not fit when the peak is just above one
+        // slots grow by half (a multiple of 64): C5-DELAY peaks just above 256 (384, not 512, slots
+        // for dt_step to stage through LDS every tick)
         const uint32_t ns = grow_s ? std::min<uint32_t>((S + S / 2u + 63u) / 64u * 64u, kDtMaxSlots) : S, nv = grow_v ? std::min<uint32_t>(V * 4u, kDtMaxVnodes) : V;
         dtrade_free(e);
         e->tr_slots = ns;

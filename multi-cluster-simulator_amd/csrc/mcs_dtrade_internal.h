@@ -133,9 +133,5 @@ hipError_t launch_approve(const mcs_approve_query* q, uint32_t n, int32_t* out, 
 hipError_t launch_dtrade_step(const DtArgs& a, hipStream_t s);
 hipError_t launch_dtrade_trader(const DtArgs& a, hipStream_t s);
 hipError_t launch_dtrade_tick(const DtArgs& a, hipStream_t s);  // world 1: both
-// the whole one-engine system resident in one workgroup (mcs_dtrade_res.hip): up to `budget` ticks
-// per launch; false when the system does not have that shape (lds: the dynamic LDS it needs)
-bool dtrade_res_shape(const DtArgs& a, uint32_t world, size_t* lds);
-hipError_t launch_dtrade_res(const DtArgs& a, uint32_t budget, size_t lds, hipStream_t s);
 
 }  // namespace mcs

@@ -237,46 +237,32 @@ def test_gpu_dtrade_fuzz(shape, seed, J):
         np.testing.assert_array_equal(g["ds"][f], o["stats"][f], err_msg=f)
 
 
-@pytest.mark.parametrize("kind,C,J,ticks", [("small", 64, 500, ""), ("small", 64, 500, "50"), ("big", 8, 800, ""),
-                                            ("n64_hot", 8, 1500, "333")])
-def test_gpu_dtrade_resident_equals_kernels_and_oracle(kind, C, J, ticks, monkeypatch):
-    """The resident tick (mcs_dtrade_res.hip: the whole system in one workgroup, loop_form 3), over
-    one launch or many short ones (MCS_TRADE_RES_TICKS), equals the graph-replayed kernels
-    (MCS_DTRADE_RESIDENT=0) and the oracle on every output."""
+@pytest.mark.parametrize("kind,C,J", [("small", 64, 500), ("big", 8, 800), ("n64_hot", 8, 1500), ("small", 16, 3000)])
+def test_gpu_dtrade_level1_rows_equal_oracle(kind, C, J):
+    """The Level1 pass over the list with holes (DtRow summaries: only rows where a job may fit are
+    visited job by job, the others take their JobsMap moves in O(1)) equals the oracle's compacted
+    slice on every output: placements, contracts, Foreign jobs, virtual nodes and the WaitTime sums
+    (exact clusters through the grown-node test, "big" ones through the histogram filter)."""
     arrays, streams, _ = seeded_workload(kind, C, J)
-    monkeypatch.setenv("MCS_DTRADE_RESIDENT", "1")
-    if ticks:
-        monkeypatch.setenv("MCS_TRADE_RES_TICKS", ticks)
     g = run(arrays, streams)
-    assert g["ts"]["loop_form"] == 3
-    monkeypatch.delenv("MCS_TRADE_RES_TICKS", raising=False)
-    monkeypatch.setenv("MCS_DTRADE_RESIDENT", "0")
-    r = run(arrays, streams)
-    assert r["ts"]["loop_form"] == 0
-    for k in ("node", "start", "finish"):
-        np.testing.assert_array_equal(g[k], r[k], err_msg=k)
-    for f in g["trades"].dtype.names:
-        np.testing.assert_array_equal(g["trades"][f], r["trades"][f], err_msg=f)
-    for f in g["foreign"].dtype.names:
-        np.testing.assert_array_equal(g["foreign"][f], r["foreign"][f], err_msg=f)
-    assert g["vnodes"] == r["vnodes"]
-    for f in g["ds"].dtype.names:
-        np.testing.assert_array_equal(g["ds"][f], r["ds"][f], err_msg=f)
-    assert g["ts"]["t_final"] == r["ts"]["t_final"] and g["ts"]["ticks"] == r["ts"]["ticks"]
+    assert g["ts"]["loop_form"] == 0
     o = O.dtrade_run(arrays, streams)
-    np.testing.assert_array_equal(g["node"], o["node"])
-    np.testing.assert_array_equal(g["start"], o["start"])
-    assert len(g["foreign"]) == o["n_foreign"] and g["ts"]["t_final"] == o["t_final"]
+    for k in ("node", "start", "finish"):
+        np.testing.assert_array_equal(g[k], o[k], err_msg=k)
+    assert len(g["trades"]) == len(o["trades"])
+    for f in ("t", "requester", "winner", "approvals", "policy", "cores", "mem", "time_s", "failed"):
+        np.testing.assert_array_equal(g["trades"][f], o["trades"][f], err_msg=f)
+    assert len(g["foreign"]) == o["n_foreign"] and g["vnodes"] == o["vnodes"]
+    for f in ("total_wait_ms", "jobs_count", "moved_l1", "placed_l1"):
+        np.testing.assert_array_equal(g["ds"][f], o["stats"][f], err_msg=f)
+    assert g["ts"]["t_final"] == o["t_final"]
 
 
-def test_gpu_dtrade_learned_capacity_keeps_the_resident_tick(monkeypatch):
+def test_gpu_dtrade_learned_capacity():
     """C5-DELAY's own system (64 cluster_small clusters x 2000 jobs) peaks at 331 running jobs in one
-    cluster: the first run overflows the 256 auto slots and escalates by half to 384, where the
-    resident tick's LDS still holds every slot (a doubling to 512 would not fit); a second run of the
-    same inputs starts at the learned 384 (no overflowed run), and both equal the graph-replayed
-    kernels and the oracle."""
+    cluster: the first run overflows the 256 auto slots and escalates by half to 384; a second run of
+    the same inputs starts at the learned 384 (no overflowed run), and both equal the oracle."""
     arrays, streams, _ = seeded_workload("small", 64, 2000)
-    monkeypatch.setenv("MCS_DTRADE_RESIDENT", "1")
     with Engine(0, policy="DELAY", trader=True) as eng:
         eng.load_clusters(arrays)
         eng.submit_jobs(streams)
@@ -286,17 +272,12 @@ def test_gpu_dtrade_learned_capacity_keeps_the_resident_tick(monkeypatch):
         st2 = eng.run()
         ts2 = eng.trade_stats()
         n2, s2, f2 = eng.placements()
-    assert st1.escalations == 1 and st1.slot_pool == 6 and ts1["loop_form"] == 3
-    assert st2.escalations == 0 and st2.slot_pool == 6 and ts2["loop_form"] == 3
+    assert st1.escalations == 1 and st1.slot_pool == 6 and ts1["loop_form"] == 0
+    assert st2.escalations == 0 and st2.slot_pool == 6 and ts2["loop_form"] == 0
     for a, b in ((n1, n2), (s1, s2), (f1, f2)):
         np.testing.assert_array_equal(a, b)
-    monkeypatch.setenv("MCS_DTRADE_RESIDENT", "0")
-    r = run(arrays, streams)
-    assert r["ts"]["loop_form"] == 0
-    np.testing.assert_array_equal(n1, r["node"])
-    np.testing.assert_array_equal(s1, r["start"])
-    np.testing.assert_array_equal(f1, r["finish"])
     o = O.dtrade_run(arrays, streams)
     np.testing.assert_array_equal(n1, o["node"])
     np.testing.assert_array_equal(s1, o["start"])
+    np.testing.assert_array_equal(f1, o["finish"])
     assert ts1["t_final"] == o["t_final"]
