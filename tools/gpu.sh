@@ -49,6 +49,7 @@ ${BENCHES:---gpus 1 --steps 20 --warmup 5
 --policy delay --lam 0.95 --max-dur 972 --steps 5 --warmup 1
 --gen fused --steps 10 --warmup 2
 --config c5 --steps 1 --warmup 1
+--config c5 --comm --steps 1 --warmup 1
 --config c5 --policy delay --steps 1 --warmup 1}
 LIST
     ;;
@@ -66,7 +67,8 @@ prof)
 ${PROFS:-c4|--steps 3 --warmup 1
 c4_512|--clusters 512 --steps 3 --warmup 1
 delay_l1|--policy delay --lam 0.95 --max-dur 972 --steps 3 --warmup 1
-c5|--config c5 --steps 1 --warmup 0}
+c5|--config c5 --steps 1 --warmup 0
+c5comm|--config c5 --comm --steps 1 --warmup 0}
 LIST
     ;;
 pmc)
