@@ -128,6 +128,21 @@ def test_gpu_dtrade_four_ranks_gloo():
     assert "DTRADE-2RANK OK" in r.stdout
 
 
+def test_gpu_dtrade_eight_ranks_gloo():
+    """world = 8, the N = 8 shape of C5-DELAY: the 64-cluster system in eight shards of 8 clusters
+    (reduced jobs), eight processes on device 0 over gloo == the oracle of the whole system."""
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29590", MCS_WORLD="8",
+               MCS_DTRADE_CASES="small:64:300")
+    r = subprocess.run([sys.executable, os.path.join(here, "dtrade_2rank.py")], env=env, capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "DTRADE-2RANK OK" in r.stdout
+
+
 @pytest.mark.parametrize("graph", ["1", "0"])
 def test_gpu_dtrade_rccl_loop_world1(graph, monkeypatch):
     """The RCCL tick loop (shape all-reduce, one in-place ncclAllGather of the exchange blocks per

@@ -137,6 +137,18 @@ def test_gpu_trade_four_ranks_one_gpu(rk):
     assert "TRADE-2RANK OK world 4" in r.stdout
 
 
+def test_gpu_trade_eight_ranks_one_gpu():
+    """world = 8, the N = 8 shape of BASELINE config 5: eight shards of 8 clusters of one 64-cluster
+    system, eight processes on device 0 exchanging blocks over gloo through the one-launch tick
+    (loop_form 9) == the oracle of the whole system."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29587", MCS_WORLD="8",
+               MCS_TRADE_CASE="n64_hot:64:300", MCS_TRADE_RK="1", MCS_EXPECT_FORM="9")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "trade_2rank.py")], env=env, capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "TRADE-2RANK OK world 8" in r.stdout
+
+
 @pytest.mark.parametrize("rk", ["1", "0"])
 @pytest.mark.parametrize("graph", ["1", "0"])
 def test_gpu_trade_rccl_loop_world1(graph, rk, monkeypatch):
