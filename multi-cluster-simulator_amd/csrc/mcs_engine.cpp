@@ -297,6 +297,7 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
     }
     e->sums_lt24 = true;
     e->slot_pack_ok = true;
+    e->cores_le64 = true;
     for (uint32_t c = 0; c < n_clusters; ++c) { /* setMaxCluster, client.go:68-83 */
         uint32_t a = 0, b = 0;
         uint64_t sc = 0, sm = 0;
@@ -309,6 +310,7 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
              * packs a running slot's {cores, memory} into 7 + 16 bits (mcs_trade_mw.hip) */
             if (std::max(cap_c[i], free_c[i]) > 127u || std::max(cap_m[i], free_m[i]) > 0xFFFFu)
                 e->slot_pack_ok = false;
+            if (std::max(cap_c[i], free_c[i]) > 64u) e->cores_le64 = false;
         }
         mxc[c] = a;
         mxm[c] = b;

@@ -100,6 +100,7 @@ struct mcs_engine {
     bool free_lt15 = false;  // every node free value < 2^15 - 1 (fifo_asm_kernel<16>)
     bool sums_lt24 = false;  // every cluster's sum of max(capacity, availability) < 2^24 per resource
     bool slot_pack_ok = false;  // every node's max(capacity, availability) < 128 cores, < 65536 memory
+    bool cores_le64 = false;    // every node's max(capacity, availability) <= 64 cores (no "big" lender)
     uint64_t total_nodes = 0, total_jobs = 0;
     std::vector<uint32_t> node_off;
     std::vector<uint64_t> job_off;
@@ -144,6 +145,8 @@ struct mcs_engine {
     uint32_t dt_ns = 0;                // node-snapshot stride over all ranks (0 = max_n)
     uint32_t tr_ns = 0;                // the same for FIFO lock-step trading
     bool tr_rk_ok = true;              // every rank can run the one-launch tick (tr_agree_shape)
+    bool tr_nosnap = false;            // no rank has a node above 64 cores: the one-launch tick's
+                                       // exchange blocks carry no node snapshots (tr_agree_shape)
     // online mode (mcs_online.cpp): per-cluster state kept on the device between horizons
     bool online = false;               // a session is active
     bool segmented = false;            // job_off holds segment starts with slack (appends)

@@ -116,9 +116,32 @@ int trade_alloc(mcs_engine* e) {
     HIPCHK(e, hipMalloc(&td->scm, (size_t)Cl * S * 8));
     HIPCHK(e, hipMalloc(&td->lq, (size_t)Cl * LQ * sizeof(TrLq)));
     const uint32_t ns = std::max<uint32_t>(e->tr_ns ? e->tr_ns : e->max_n, 1u);
+    // the one-launch tick (mcs_trade_rk.hip) runs sharded systems (a communicator or the caller-driven
+    // API) whose shape it holds; every rank decides alike (tr_agree_shape on the RCCL path; the
+    // caller-driven ranks hold alike clusters).  MCS_TRADE_RK=0 keeps the three-kernel tick.
+    bool rk = false;
+    size_t rk_lds = 0;
+    {
+        const char* rkenv = getenv("MCS_TRADE_RK");
+        const bool want_rk = !rkenv || atoi(rkenv) != 0;
+        TradeArgs shp{};
+        shp.Ct = Ct;
+        shp.Cl = Cl;
+        shp.ns = ns;
+        shp.S = S;
+        int max_lds = 0;
+        rk_lds = trade_rk_lds(ns);
+        rk = want_rk && e->sums_lt24 && e->slot_pack_ok && e->tr_rk_ok && trade_rk_shape(shp) &&
+             hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device) == hipSuccess &&
+             rk_lds <= (size_t)max_lds;
+    }
     // (16-byte aligned blocks: the records are read as 16-byte vectors on every rank's block; the
-    // one-launch tick's G tables, 256 B per cluster, follow the snapshots)
-    const uint64_t blk = ((uint64_t)Cl * sizeof(TrXRec) + (uint64_t)Cl * ns * 8u + (uint64_t)Cl * 256u + 15u) & ~15ull;
+    // one-launch tick's G tables, 256 B per cluster, follow the snapshots.  On the RCCL path, when no
+    // rank has a node above 64 cores, no lender is ever "big": the one-launch tick's blocks then
+    // carry no snapshots at all — 320 B per cluster instead of 320 B + 8 B per node)
+    const bool snaps = !(rk && e->comm && e->tr_nosnap);
+    const uint64_t blk = ((uint64_t)Cl * sizeof(TrXRec) + (snaps ? (uint64_t)Cl * ns * 8u : 0ull) +
+                          (uint64_t)Cl * 256u + 15u) & ~15ull;
     // (two buffers of world blocks: the one-launch tick alternates them by tick parity)
     HIPCHK(e, hipMalloc(&td->xb, 2u * (size_t)e->world * blk));
     HIPCHK(e, hipMalloc(&td->acc, Ct * 4));
@@ -176,20 +199,12 @@ int trade_alloc(mcs_engine* e) {
     a.lent_log = td->lent;
     a.trade_log = td->trades;
     a.lrp = td->lrp;
-    // the one-launch tick (mcs_trade_rk.hip) runs sharded systems (a communicator or the caller-driven
-    // API) whose shape it holds; every rank decides alike (tr_agree_shape on the RCCL path; the
-    // caller-driven ranks hold alike clusters).  MCS_TRADE_RK=0 keeps the three-kernel tick.
-    const char* rkenv = getenv("MCS_TRADE_RK");
-    const bool want_rk = !rkenv || atoi(rkenv) != 0;
-    if (want_rk && e->sums_lt24 && e->slot_pack_ok && e->tr_rk_ok && trade_rk_shape(a)) {
-        int max_lds = 0;
-        td->rk_lds = trade_rk_lds(ns);
-        if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device) == hipSuccess &&
-            td->rk_lds <= (size_t)max_lds) {
-            HIPCHK(e, hipMalloc(&td->tnr, (size_t)Cl * ns * 8u));
-            a.tnr = td->tnr;
-            td->rk = true;
-        }
+    a.snaps = snaps ? 1u : 0u;
+    if (rk) {
+        td->rk_lds = rk_lds;
+        HIPCHK(e, hipMalloc(&td->tnr, (size_t)Cl * ns * 8u));
+        a.tnr = td->tnr;
+        td->rk = true;
     }
     return MCS_OK;
 }
@@ -520,14 +535,15 @@ int trade_cluster_stats(mcs_engine* e, mcs_cluster_stats* out, uint32_t n) {
 // the whole system, and the cluster count per rank must match (one all-reduce before the run)
 int tr_agree_shape(mcs_engine* e) {
     uint32_t* buf = nullptr;
-    HIPCHK(e, hipMalloc(&buf, 4 * sizeof(uint32_t)));
+    HIPCHK(e, hipMalloc(&buf, 5 * sizeof(uint32_t)));
     /* max of C and of ~C (= ~min C): every rank sees the same verdict, so a mismatch fails on
      * every rank instead of leaving the ranks with the largest C in the tick loop; the 4th word:
-     * some rank cannot pack the one-launch tick's slot payload or sum utilization exactly */
-    const uint32_t h[4] = {e->max_n, e->C, ~e->C, (e->sums_lt24 && e->slot_pack_ok) ? 0u : 1u};
-    uint32_t mx[4] = {0, 0, 0, 0};
+     * some rank cannot pack the one-launch tick's slot payload or sum utilization exactly; the 5th:
+     * some rank has a node above 64 cores (a lender can be "big": the blocks carry snapshots) */
+    const uint32_t h[5] = {e->max_n, e->C, ~e->C, (e->sums_lt24 && e->slot_pack_ok) ? 0u : 1u, e->cores_le64 ? 0u : 1u};
+    uint32_t mx[5] = {0, 0, 0, 0, 0};
     HIPCHK(e, hipMemcpy(buf, h, sizeof(h), hipMemcpyHostToDevice));
-    ncclResult_t r = ncclAllReduce(buf, buf, 4, ncclUint32, ncclMax, (ncclComm_t)e->comm, e->stream);
+    ncclResult_t r = ncclAllReduce(buf, buf, 5, ncclUint32, ncclMax, (ncclComm_t)e->comm, e->stream);
     hipError_t st = hipStreamSynchronize(e->stream);
     if (r == ncclSuccess && st == hipSuccess) st = hipMemcpy(mx, buf, sizeof(mx), hipMemcpyDeviceToHost);
     (void)hipFree(buf);
@@ -536,6 +552,7 @@ int tr_agree_shape(mcs_engine* e) {
     if (mx[1] != ~mx[2]) return fail(e, MCS_E_INVALID, "sharded lock-step trading needs the same cluster count on every rank");
     e->tr_ns = mx[0];
     e->tr_rk_ok = mx[3] == 0u;
+    e->tr_nosnap = mx[4] == 0u;
     return MCS_OK;
 }
 
@@ -616,6 +633,7 @@ int mcs_set_shard(mcs_engine* e, uint32_t rank, uint32_t world) {
     e->dt_ns = 0;
     e->tr_ns = 0;
     e->tr_rk_ok = true;
+    e->tr_nosnap = false;
     e->rank = rank;
     e->world = world;
     return MCS_OK;
@@ -678,7 +696,8 @@ int mcs_trade_xfer_bytes(mcs_engine* e, uint32_t phase, uint64_t* in_bytes, uint
     // size, as the shard helpers do.)
     const uint64_t Cl = e->C;
     const uint64_t ns = std::max<uint32_t>(e->tr_ns ? e->tr_ns : e->max_n, 1u);
-    const uint64_t blk = (Cl * sizeof(mcs::TrXRec) + Cl * ns * 8u + Cl * 256u + 15u) & ~15ull;  // (as trade_alloc)
+    // (as trade_alloc: the caller-driven path always carries the snapshots; an allocated state knows)
+    const uint64_t blk = e->td ? e->td->a.blk : (Cl * sizeof(mcs::TrXRec) + Cl * ns * 8u + Cl * 256u + 15u) & ~15ull;
     switch (phase) {
         case 0: *in_bytes = 0; *out_bytes = blk; break;
         case 1: *in_bytes = (uint64_t)e->world * blk; *out_bytes = 0; break;

@@ -112,6 +112,8 @@ struct TradeArgs {
     unsigned char* xb;       // world exchange blocks
     unsigned long long blk;  // bytes of one rank's block
     uint32_t ns, rank;       // snapshot stride (nodes), this rank
+    uint32_t snaps;          // one-launch tick: 1 = the blocks carry node snapshots (a lender may be
+                             // "big"), 0 = records and G tables only
     uint32_t* acc;
     uint32_t* lqp;
     uint32_t* fb;

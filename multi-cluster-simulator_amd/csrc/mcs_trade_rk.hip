@@ -91,7 +91,8 @@ __device__ __forceinline__ unsigned long long* rk_snap(const TradeArgs& a, unsig
 __device__ __forceinline__ uint32_t* rk_gtab(const TradeArgs& a, unsigned char* xb, uint32_t g) {
     uint32_t c;
     unsigned char* b = rk_blk(a, xb, g, &c);
-    return reinterpret_cast<uint32_t*>(b + (size_t)a.Cl * sizeof(TrXRec) + (size_t)a.Cl * a.ns * 8u) + (size_t)c * 64u;
+    return reinterpret_cast<uint32_t*>(b + (size_t)a.Cl * sizeof(TrXRec) + (a.snaps ? (size_t)a.Cl * a.ns * 8u : 0u)) +
+           (size_t)c * 64u;
 }
 
 constexpr uint32_t kStW = sizeof(TrCluster) / 4u;
@@ -813,6 +814,9 @@ __global__ __launch_bounds__(kRkThreads) void tr_rk_kernel(TradeArgs a, uint32_t
                 atomicMax(&tab[fc - 1u], (uint32_t)(nv[q] >> 32));
         }
         const bool bigw = __ballot(big) != 0ull;
+        // (no snapshot room when the engine proved no node exceeds 64 cores: cannot happen, and is
+        // refused loudly, as an overflow of this tick's record, if it ever does)
+        if (bigw && !a.snaps) RST(flags) |= MCS_FLAG_OVERFLOW;
         rk_gtab(a, xw, g)[63u - lane] = wave_scan_max_u32(tab[63u - lane]);  // G[63 - lane]
         RK_MARK(10);
         // the post-A record and the node snapshot: this rank's block of the next all-gather
@@ -837,7 +841,7 @@ __global__ __launch_bounds__(kRkThreads) void tr_rk_kernel(TradeArgs a, uint32_t
         xv = lane == kRkTm ? (uint32_t)RST(total_m) : xv;
         uint32_t* const rp = rk_rec(a, xw, g);
         if (lane < kRkWords) rp[lane] = xv;
-        if (bigw) {  // (read only for a big lender)
+        if (bigw && a.snaps) {  // (read only for a big lender)
             unsigned long long* const sn = rk_snap(a, xw, g);
 #pragma unroll
             for (uint32_t q = 0; q < kRkNodes / kWave; ++q)
