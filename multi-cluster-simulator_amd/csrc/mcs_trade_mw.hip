@@ -54,10 +54,10 @@ constexpr uint32_t kMwNodes = 256;       // nodes per cluster
 constexpr uint32_t kX1Words = 10;        // granules of a cluster's post-A record
 constexpr uint32_t kSpinLimit = 1u << 20;  // sweeps per exchange before the run gives up
 
-__device__ __forceinline__ uint32_t mw_wave_sum(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-    return v;
-}
+// a wave's uint32 sum / OR on the DPP scans: VALU steps, no chain of LDS-pipe permutes (every
+// lane active)
+__device__ __forceinline__ uint32_t mw_wave_sum(uint32_t v) { return readlane(wave_scan_add_u32(v), 63u); }
+__device__ __forceinline__ uint32_t mw_wave_or(uint32_t v) { return readlane(wave_scan_or_u32(v), 63u); }
 // HBM this kernel's own wave wrote in an earlier tick and reads back (LentQueue entries)
 __device__ __forceinline__ uint64_t mld64(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -334,11 +334,9 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                 const uint32_t v = (uint32_t)x, k = lane % 3u;
                 uint32_t m0 = lane < nw && k == 0u ? v : 0u, m1 = lane < nw && k == 1u ? v : 0u,
                          fb = lane < nw && k == 2u ? v : 0u;
-                for (int o = 32; o > 0; o >>= 1) {
-                    m0 |= (uint32_t)__shfl_xor((int)m0, o);
-                    m1 |= (uint32_t)__shfl_xor((int)m1, o);
-                    fb |= (uint32_t)__shfl_xor((int)fb, o);
-                }
+                m0 = mw_wave_or(m0);
+                m1 = mw_wave_or(m1);
+                fb = mw_wave_or(fb);
                 const uint32_t g = lane;
                 const bool acc = ((g < 32u ? m0 >> g : m1 >> (g - 32u)) & 1u) != 0u;
                 if (acc && g < C && g / kMwWaves == wg && sh.rq_job[g] != kEmpty) {
@@ -403,6 +401,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
 #pragma unroll
                 for (int r = 0; r < kRows; ++r) {
                     const uint32_t f = fin[r];
+                    nrel += (uint32_t)__builtin_popcountll(__ballot(f <= T));  // (the wave's releases)
                     if (f <= T) {
                         const uint32_t p = pay[r], kn = p & 511u;
                         if (kn < N)
@@ -410,12 +409,11 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
                                                       ((unsigned long long)(p >> 16) << 32));
                         fin[r] = kEmpty;
                         frm |= 1u << r;
-                        ++nrel;
                     } else {
                         lm = f < lm ? f : lm;
                     }
                 }
-                MST(nrun) -= mw_wave_sum(nrel);
+                MST(nrun) -= nrel;
                 MST(minf) = wave_min_u32(lm);
             }
             MW_MARK(1);
@@ -753,7 +751,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             const bool done_all = !__ballot(!done_g);
             const bool busy_any = __ballot(busy != 0u) != 0ull;
             nxt = wave_min_u32(nxt);
-            for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o);
+            fl = mw_wave_or(fl);
             if (lane == 0) {
                 uint32_t flags = sh.flags | fl | lflags;
                 uint32_t done = 0, Tn = T;

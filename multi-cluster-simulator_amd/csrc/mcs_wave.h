@@ -104,6 +104,15 @@ __device__ __forceinline__ uint32_t wave_scan_max_u32(uint32_t v) {
     w = dpp_src0<0x143, 0xc>(v); v = w > v ? w : v;
     return v;
 }
+__device__ __forceinline__ uint32_t wave_scan_or_u32(uint32_t v) {
+    v |= dpp_src0<0x111, 0xf>(v);
+    v |= dpp_src0<0x112, 0xf>(v);
+    v |= dpp_src0<0x114, 0xf>(v);
+    v |= dpp_src0<0x118, 0xf>(v);
+    v |= dpp_src0<0x142, 0xa>(v);
+    v |= dpp_src0<0x143, 0xc>(v);
+    return v;
+}
 __device__ __forceinline__ uint32_t wave_scan_add_u32(uint32_t v) {
     v += dpp_src0<0x111, 0xf>(v);
     v += dpp_src0<0x112, 0xf>(v);
