@@ -62,27 +62,27 @@ __device__ unsigned long long g_dt_rows[4];
     } while (0)
 #endif
 
-__device__ __forceinline__ uint32_t dt_wave_sum_u32(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-    return v;
-}
+// wave reductions on the DPP scans of mcs_wave.h, read at lane 63: VALU steps instead of a chain
+// of six dependent ds_bpermute round trips (every lane active at every call site)
+__device__ __forceinline__ uint32_t dt_wave_sum_u32(uint32_t v) { return readlane(wave_scan_add_u32(v), 63u); }
 
 __device__ __forceinline__ long long dt_wave_sum_i64(long long v) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)(unsigned long long)v, o);
-        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)((unsigned long long)v >> 32), o);
-        v += (long long)((unsigned long long)lo | ((unsigned long long)hi << 32));
-    }
-    return v;
+    unsigned long long u = (unsigned long long)v;  // (two's complement: the same adds)
+    auto step = [&](unsigned long long w) { u += w; };
+#define DT_DPP64(CTRL, MASK)                                                                  \
+    step((unsigned long long)dpp_src0<CTRL, MASK>((uint32_t)u) |                              \
+         ((unsigned long long)dpp_src0<CTRL, MASK>((uint32_t)(u >> 32)) << 32))
+    DT_DPP64(0x111, 0xf);
+    DT_DPP64(0x112, 0xf);
+    DT_DPP64(0x114, 0xf);
+    DT_DPP64(0x118, 0xf);
+    DT_DPP64(0x142, 0xa);
+    DT_DPP64(0x143, 0xc);
+#undef DT_DPP64
+    return (long long)(((unsigned long long)readlane((uint32_t)(u >> 32), 63u) << 32) | readlane((uint32_t)u, 63u));
 }
 
-__device__ __forceinline__ uint32_t dt_wave_max_u32(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t w = (uint32_t)__shfl_xor((int)v, o);
-        v = w > v ? w : v;
-    }
-    return v;
-}
+__device__ __forceinline__ uint32_t dt_wave_max_u32(uint32_t v) { return readlane(wave_scan_max_u32(v), 63u); }
 
 // Go uint64 value of a device free counter (sign extension of the u32, see the header)
 __device__ __forceinline__ unsigned long long go_u64(uint32_t x) {
@@ -320,11 +320,9 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             }
             __syncthreads();
             max_c = dt_wave_max_u32(mc);
-            best = hist[lane];
-            for (int o = 1; o < kWave; o <<= 1) {
-                const uint32_t w = (uint32_t)__shfl_down((int)best, o);
-                best = (lane + (uint32_t)o < (uint32_t)kWave && w > best) ? w : best;
-            }
+            // suffix maximum: a DPP prefix scan of the reversed histogram, reversed back
+            const uint32_t sc = wave_scan_max_u32(hist[63u - lane]);
+            best = (uint32_t)__shfl((int)sc, (int)(63u - lane));
         }
         // per lane: the lowest node (physical, then virtual) that fits this lane's entry
         // (the node values come from one LDS read per lane, node i in lane i, then readlanes: no
@@ -999,7 +997,7 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
     ndue = wave_min_u32(ndue);
     nxt = wave_min_u32(nxt);
     nxt = ndue < nxt ? ndue : nxt;
-    for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o);
+    fl = readlane(wave_scan_or_u32(fl), 63u);
     __syncthreads();
     for (uint32_t q = lane; q < Ct; q += kWave) {
         a.tr[q] = trs[q];
