@@ -50,6 +50,14 @@ namespace {
 #endif
 constexpr int kMwWaves = MCS_MW_WAVES;
 static_assert(3 * ((int)kTrResMaxClusters / kMwWaves) <= kWave, "X2: one granule per lane");
+// the control wave: X2's gather (x2_apply), the X1 sweep, phases C and D and X2's publication.  With
+// MCS_MW_HELPER a fifth wave of its own, so C/D runs beside every cluster wave's phase B and the
+// sweep starts at the tick's start; else cluster wave 0 after its own phase A
+#ifndef MCS_MW_HELPER
+#define MCS_MW_HELPER 1
+#endif
+constexpr uint32_t kMwCtl = MCS_MW_HELPER ? (uint32_t)kMwWaves : 0u;
+constexpr int kMwThreads = (kMwWaves + (MCS_MW_HELPER ? 1 : 0)) * kWave;
 constexpr uint32_t kMwNodes = 256;       // nodes per cluster
 constexpr uint32_t kX1Words = 10;        // granules of a cluster's post-A record
 constexpr uint32_t kSpinLimit = 1u << 20;  // sweeps per exchange before the run gives up
@@ -174,7 +182,7 @@ static_assert(offsetof(MwShared, rq_c) == offsetof(MwShared, rq_job) + 1 * kTrRe
               "X1 record arrays out of word order");
 
 template <int kRows>  // slot rows per cluster (64 slots each)
-__global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, unsigned long long* gx_uc,
+__global__ __launch_bounds__(kMwThreads) void tr_mw_kernel(TradeArgs a, unsigned long long* gx_uc,
                                                                  unsigned long long* gx_c, uint32_t tick_budget,
                                                                  uint32_t nwg, uint32_t stride, uint32_t tick0,
                                                                  uint32_t force_uc) {
@@ -188,7 +196,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
     const uint32_t C = a.Ct, ns = a.ns, S = a.S;
     const uint32_t wg = blockIdx.x / stride;
     const uint32_t c = wg * kMwWaves + wave;  // this wave's cluster
-    const bool own = c < C;
+    const bool own = wave < (uint32_t)kMwWaves && c < C;
 
     // ---- the exchange protocol of this launch: every workgroup publishes its XCD id (write-through
     // granule in uncached memory, valid under any placement); when all are equal the tick's granules
@@ -223,7 +231,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
     unsigned long long* const gx2 = gx + (size_t)kTrResMaxClusters * kX1Words;  // [C] lender words, [nwg][2]
 
     // ---- state in ----
-    unsigned long long* const nodes = nodes_wg + (size_t)wave * ns;
+    unsigned long long* const nodes = nodes_wg + (size_t)(wave < (uint32_t)kMwWaves ? wave : 0u) * ns;
     uint32_t N = 0, n0 = 0, J = 0;
     uint64_t j0 = 0;
     if (own) {
@@ -246,7 +254,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             sh.capm[wave] = um;
         }
     }
-    for (uint32_t g = threadIdx.x; g < C; g += kMwWaves * kWave) {
+    for (uint32_t g = threadIdx.x; g < C; g += kMwThreads) {
         sh.trs[g] = a.tr[g];
         sh.total_c[g] = a.cl[g].total_c;
         sh.total_m[g] = a.cl[g].total_m;
@@ -313,7 +321,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
     // heads to the BorrowedQueue (scheduler.go:237-242) with tick n's clock Tn; an append overflow
     // ends the run at tick n, as the three-kernel tick does (clock Tn, no T_MAX flag of that tick)
     auto x2_apply = [&](uint32_t tg, uint32_t Tn) {
-        if (wave == 0) {
+        if (wave == kMwCtl) {
             const uint32_t nw = 3u * nwg;
             unsigned long long x = 0ull;
             bool got = false;
@@ -600,7 +608,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
         MW_MARK(4);
 
         // ---- X1: every cluster's record (one wave sweeps, the others wait at the barrier) ----
-        if (wave == 0) {
+        if (wave == kMwCtl) {
             // word-major granules: lane g sweeps cluster g's ten words (granule k * 64 + g), and stores
             // word k of it at rq_job + k * 64 + g: consecutive LDS words, no division, no bank
             // conflict (record-major, lane i held word i % 10 of cluster i / 10: up to ten lanes of
@@ -641,9 +649,9 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
             if (lane < 3) sh.accm[lane] = 0u;
             if (timed_out && lane == 0) sh.done = 2u;
         }
-        MW_TLOG(it, kMwWaves + wave, wall_clock64());
+        if (wave < (uint32_t)kMwWaves) MW_TLOG(it, kMwWaves + wave, wall_clock64());
         __syncthreads();
-        if (wave == 0) MW_TLOG(it, 2 * kMwWaves + 2, wall_clock64());
+        if (wave == kMwCtl) MW_TLOG(it, 2 * kMwWaves + 2, wall_clock64());
         MW_MARK(5);
         if (sh.done == 2u) break;
 
@@ -683,7 +691,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
         // the end of the run follow from X1 alone (queue bits: WaitQueue, ReadyQueue, LentQueue
         // after A); the acceptances (X2: the workgroup's borrower masks and append-overflow bit) are
         // published here and applied at the start of the next tick (x2_apply), while C/D runs
-        if (wave == 0) {
+        if (wave == kMwCtl) {
             const uint32_t g = lane;
             float cu = 0.0f, mu = 0.0f;
             uint32_t tot_c = 0u, tot_m = 0u, busy = 0u, next_arr_t = kEmpty, done_g = 1u, fl = 0u;
@@ -876,7 +884,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
         __syncthreads();
         MW_MARK(7);
         // X2: this workgroup's acceptances and append-overflow bit (applied at the next tick's start)
-        if (wave == 0) {
+        if (wave == kMwCtl) {
             if (lane < 3) put(gx2 + 3u * wg + lane, tag2, sh.accm[lane]);
             if (lane == 0) sh.n_lent = sh.n_lent_next;
         }
@@ -889,7 +897,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
     }
     if (pend && sh.done != 2u) x2_apply(pend_tag, pend_T);
 #ifdef MCS_STAMPS
-    if (lane == 0 && wg < (uint32_t)kMwMaxWg)
+    if (lane == 0 && wg < (uint32_t)kMwMaxWg && wave < (uint32_t)kMwWaves)
         for (int i = 0; i < kMwSeg; ++i)
             atomicAdd(&g_mw_stamps[(wg * kMwWaves + wave) * kMwSeg + i], (unsigned long long)mw_acc[i]);
 #endif
@@ -905,7 +913,7 @@ __global__ __launch_bounds__(kMwWaves * kWave) void tr_mw_kernel(TradeArgs a, un
         }
     }
     if (wg == 0) {
-        for (uint32_t g = threadIdx.x; g < C; g += kMwWaves * kWave) a.tr[g] = sh.trs[g];
+        for (uint32_t g = threadIdx.x; g < C; g += kMwThreads) a.tr[g] = sh.trs[g];
         if (threadIdx.x == 0) {
             TrCtl* ctl = a.ctl;
             ctl->T = sh.T;
@@ -951,13 +959,13 @@ hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsign
     st = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (st != hipSuccess) return st;
     if (a.S == 4u * kWave)
-        hipLaunchKernelGGL(tr_mw_kernel<4>, dim3(nblk), dim3(kMwWaves * kWave), lds, s, a, gx_uc, gx_c, tick_budget,
+        hipLaunchKernelGGL(tr_mw_kernel<4>, dim3(nblk), dim3(kMwThreads), lds, s, a, gx_uc, gx_c, tick_budget,
                            nwg, stride, tick0, force_uc ? 1u : 0u);
     else if (a.S == 8u * kWave)
-        hipLaunchKernelGGL(tr_mw_kernel<8>, dim3(nblk), dim3(kMwWaves * kWave), lds, s, a, gx_uc, gx_c, tick_budget,
+        hipLaunchKernelGGL(tr_mw_kernel<8>, dim3(nblk), dim3(kMwThreads), lds, s, a, gx_uc, gx_c, tick_budget,
                            nwg, stride, tick0, force_uc ? 1u : 0u);
     else
-        hipLaunchKernelGGL(tr_mw_kernel<16>, dim3(nblk), dim3(kMwWaves * kWave), lds, s, a, gx_uc, gx_c, tick_budget,
+        hipLaunchKernelGGL(tr_mw_kernel<16>, dim3(nblk), dim3(kMwThreads), lds, s, a, gx_uc, gx_c, tick_budget,
                            nwg, stride, tick0, force_uc ? 1u : 0u);
     return hipGetLastError();
 }
