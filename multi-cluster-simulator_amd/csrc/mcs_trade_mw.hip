@@ -654,6 +654,9 @@ __global__ __launch_bounds__(kMwThreads) void tr_mw_kernel(TradeArgs a, unsigned
         if (wave == kMwCtl) MW_TLOG(it, 2 * kMwWaves + 2, wall_clock64());
         MW_MARK(5);
         if (sh.done == 2u) break;
+        // a tick without a borrow request has no acceptance and no append to overflow: its X2 is
+        // neither published nor gathered (every workgroup sees the same requests in X1)
+        const bool any_req = __ballot(lane < C && sh.rq_job[lane] != kEmpty) != 0ull;
 
         // ---- phase B: this wave's cluster as lender, requests in borrower order (tr_lend_kernel) ----
         // Lend (scheduler.go:194-202) accepts a request (c, m) when some node has free_c > c and
@@ -885,13 +888,13 @@ __global__ __launch_bounds__(kMwThreads) void tr_mw_kernel(TradeArgs a, unsigned
         MW_MARK(7);
         // X2: this workgroup's acceptances and append-overflow bit (applied at the next tick's start)
         if (wave == kMwCtl) {
-            if (lane < 3) put(gx2 + 3u * wg + lane, tag2, sh.accm[lane]);
+            if (any_req && lane < 3) put(gx2 + 3u * wg + lane, tag2, sh.accm[lane]);
             if (lane == 0) sh.n_lent = sh.n_lent_next;
         }
 
         MW_MARK(8);
         if (sh.done == 2u) break;  // (C/D wrote it before the phase-B barrier)
-        pend = true;
+        pend = any_req;
         pend_tag = tag2;
         pend_T = T;
     }
