@@ -348,6 +348,30 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         // does this lane's job fit some grown node (current values)?  (every lane active)
         // (the node values in a register for the pass, node i in lane i; refreshed after a commit)
         unsigned long long nvv = exact && lane < NN ? nodes[lane] : 0ull;
+#ifndef MCS_DT_GLOOP
+        // G as a staircase: lane 63 - x holds the largest free memory over the grown nodes with
+        // min(free cores, 63) >= x (0: none), so a job (c, m) fits some grown node only if
+        // gtab[63 - min(c, 63)] >= m: one permute per test instead of a readlane chain over G.  A
+        // superset (cores clamped at 63, m = 0): every candidate still gets the real first fit, and a
+        // quiet row is one where nothing passes.  Rebuilt after each commit (nodes only shrink).
+        uint32_t gtab = 0u;
+        auto g_build = [&]() {
+            hist[lane] = 0u;
+            dt_wave_sync();
+            if ((gmask >> lane) & 1ull) {
+                const uint32_t nc = (uint32_t)nvv;
+                atomicMax(&hist[nc < 63u ? nc : 63u], (uint32_t)(nvv >> 32));
+            }
+            dt_wave_sync();
+            gtab = wave_scan_max_u32(hist[63u - lane]);
+        };
+        if (exact && !g_all && gmask) g_build();
+        auto g_fit = [&](uint32_t c_l, uint32_t m_l) -> bool {
+            const uint32_t t = (uint32_t)__shfl((int)gtab, (int)(63u - (c_l < 63u ? c_l : 63u)));
+            return gmask != 0ull && t >= m_l;
+        };
+#else
+        auto g_build = [&]() {};
         auto g_fit = [&](uint32_t c_l, uint32_t m_l) -> bool {
             const uint32_t nc = (uint32_t)nvv, nm = (uint32_t)(nvv >> 32);
             bool f = false;
@@ -357,6 +381,7 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             }
             return f;
         };
+#endif
         uint32_t wr = 0;
         bool carry_skip = false;  // the last entry of the previous row was placed
         const uint32_t n1 = st.l1n, t_all = st.t_all;
@@ -408,7 +433,10 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
                         overflow = true;
                         break;
                     }
-                    if (jd != 0u) nvv = lane < NN ? nodes[lane] : 0ull;  // (node k shrank)
+                    if (jd != 0u) {  // (node k shrank)
+                        nvv = lane < NN ? nodes[lane] : 0ull;
+                        if (!g_all && ((gmask >> k) & 1ull)) g_build();
+                    }
                     if (lane == 0) {
                         a.out_node[j0 + jj] = (int32_t)k;
                         a.out_start[j0 + jj] = T;
