@@ -150,6 +150,7 @@ size_t trade_mw_lds(uint32_t ns);
 size_t trade_mw_granules(uint32_t n_clusters);
 // the workgroups' XCD-id granules follow X1 (10 per cluster) and X2 (128) in the uncached buffer
 constexpr size_t trade_mw_xcc_off() { return (size_t)kTrResMaxClusters * 10u + 128u; }
+constexpr size_t trade_mw_x1b_off() { return trade_mw_xcc_off() + 64u; }  // X1's second buffer
 // gx_uc: uncached granules (any placement); gx_c: cached granules, used when every workgroup runs on
 // one XCD; xcd_pack: launch the workers 8 blocks apart (one XCD under round-robin dispatch)
 hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsigned long long* gx_c,

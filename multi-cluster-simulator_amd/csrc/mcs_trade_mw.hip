@@ -227,7 +227,12 @@ __global__ __launch_bounds__(kMwThreads) void tr_mw_kernel(TradeArgs a, unsigned
         if (xcd) put_granule_xcd(g, tag, v);
         else put_granule(g, tag, v);
     };
-    unsigned long long* const gx1 = gx;  // [kX1Words][64]: word w of cluster g at w * 64 + g (r04)
+    // X1, two buffers by tick parity: [kX1Words][64] each, word w of cluster g at w * 64 + g (r04).
+    // (A tick without a borrow request has no X2, so a workgroup may publish tick n + 1's X1 while
+    // another still sweeps tick n's: it writes the other buffer.  It can write this one again only
+    // at tick n + 2, after its own sweep of tick n + 1, i.e. after every workgroup published tick
+    // n + 1's record, which each did after its sweep of tick n.)
+    unsigned long long* const gx1b[2] = {gx, gx + trade_mw_x1b_off()};
     unsigned long long* const gx2 = gx + (size_t)kTrResMaxClusters * kX1Words;  // [C] lender words, [nwg][2]
 
     // ---- state in ----
@@ -385,6 +390,7 @@ __global__ __launch_bounds__(kMwThreads) void tr_mw_kernel(TradeArgs a, unsigned
         // [1, 2^32 - 3] and tag2 = tag1 + 1 never wraps to 0 (the zeroed granules' tag)
         const uint32_t ep = (tick0 + it) % 0x7FFFFFFFu;
         const uint32_t tag1 = 2u * ep + 1u, tag2 = tag1 + 1u;
+        unsigned long long* const gx1 = gx1b[(tick0 + it) & 1u];
 
         // GetResourceUtilization runs on the ticks a trader reads it (see tr_step_kernel)
         bool sample = false;
@@ -943,7 +949,7 @@ bool trade_mw_shape(const TradeArgs& a) {
 
 // X1 for 64 clusters, then X2 (64 lender words + 4 x 2 mask words) padded to 128: every sweep load
 // lies inside the block (a multiple of 16 bytes); then the workgroups' XCD ids (uncached buffer)
-size_t trade_mw_granules(uint32_t) { return trade_mw_xcc_off() + kWave; }
+size_t trade_mw_granules(uint32_t) { return trade_mw_x1b_off() + (size_t)kTrResMaxClusters * kX1Words; }
 
 hipError_t launch_trade_mw(const TradeArgs& a, unsigned long long* gx_uc, unsigned long long* gx_c,
                            uint32_t tick_budget, uint32_t tick0, size_t lds, bool xcd_pack, bool force_uc,
