@@ -777,6 +777,10 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
     __shared__ uint32_t appr[kDtMaxClusters];
     __shared__ uint32_t nvs[kDtMaxClusters];  // virtual nodes per cluster (written here)
     __shared__ uint32_t nfr[kDtMaxClusters];  // free running slots per cluster (taken here)
+    // every cluster's record of the tick, copied once: the rounds read a requester's sample and
+    // contract sizes and every responder's totals and sample (each an L2 round trip per round
+    // otherwise); no round writes a record
+    extern __shared__ DtRec srec[];  // [Ct] (dynamic)
     if (a.ctl->done) return;
 #ifdef MCS_STAMPS
     const uint64_t tr_t0 = wall_clock64();
@@ -787,9 +791,17 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
     const uint32_t Ct = a.Ct;
     for (uint32_t q = lane; q < Ct; q += kWave) {
         trs[q] = a.tr[q];
-        const DtRec* rq = dt_rec(a, q);
-        nvs[q] = rq->nv;
-        nfr[q] = rq->nfree;
+        const uint4* rq = reinterpret_cast<const uint4*>(dt_rec(a, q));
+        uint4* rd = reinterpret_cast<uint4*>(&srec[q]);
+        static_assert(sizeof(DtRec) == 5 * sizeof(uint4), "DtRec copy");
+        const uint4 w0 = rq[0], w1 = rq[1], w2 = rq[2], w3 = rq[3], w4 = rq[4];
+        rd[0] = w0;
+        rd[1] = w1;
+        rd[2] = w2;
+        rd[3] = w3;
+        rd[4] = w4;
+        nvs[q] = srec[q].nv;
+        nfr[q] = srec[q].nfree;
     }
     __syncthreads();
     unsigned long long n_trades = a.ctl->n_trades, n_won = a.ctl->n_won, n_for = a.ctl->n_foreign;
@@ -801,7 +813,7 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
         while (due) {
             const uint32_t q = q0 + (uint32_t)__builtin_ctzll(due);
             due &= due - 1ull;
-            const DtRec* rq = dt_rec(a, q);
+            const DtRec* rq = &srec[q];
             const uint32_t ql_ = q - a.base;  // local index when q is on this rank
             const bool qloc = ql_ < a.C;
             // RequestPolicyMonitor of requester q (trader.go:282-324): two-stage machine
@@ -837,7 +849,7 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
                         DtTrader t = trs[r];
                         if (t.lock_id != 0u && T >= t.lock_until) t.lock_id = 0u;  // 20 s expiry
                         if (t.lock_id == 0u) {  // else Approve:false (server.go:35-40)
-                            const DtRec* rr = dt_rec(a, r);
+                            const DtRec* rr = &srec[r];
                             app = approve_trade_dev(rr->total_c, rr->total_m, rr->cu, rr->mu, kc, km, ksec);
                             t.lock_id = t.next_id++;  // set even when not approving (:44-46)
                             t.lock_until = T + a.lock_s;
@@ -863,7 +875,7 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
                     // ApproveContract (server.go:63-85): the lock set in this round still
                     // matches; AllocateVirtualNodeResources on the responder (cluster.go:87-125)
                     uint32_t rc_ = kc, rm_ = km;
-                    const uint32_t rN = dt_rec(a, r)->N;
+                    const uint32_t rN = srec[r].N;
                     const uint32_t rNN = rN + nvs[r];
                     unsigned long long* rs = dt_snap(a, r);
                     const uint32_t rl = r - a.base;  // local index when r is on this rank
@@ -1013,7 +1025,7 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
     bool all_done = true, queued = false;
     uint32_t nxt = T + a.sample_period - T % a.sample_period, fl = 0, ndue = kEmpty;
     for (uint32_t q = lane; q < Ct; q += kWave) {
-        const DtRec* rq = dt_rec(a, q);
+        const DtRec* rq = &srec[q];
         all_done = all_done && rq->done != 0u;
         queued = queued || rq->queued != 0u;
         nxt = rq->nxt < nxt ? rq->nxt : nxt;
@@ -1092,7 +1104,10 @@ hipError_t launch_dtrade_step(const DtArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_dtrade_trader(const DtArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(dt_trader_kernel, dim3(1), dim3(kWave), 0, s, a);
+    const size_t lds = (size_t)a.Ct * sizeof(DtRec);
+    const hipError_t st = hipFuncSetAttribute((const void*)dt_trader_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (st != hipSuccess) return st;
+    hipLaunchKernelGGL(dt_trader_kernel, dim3(1), dim3(kWave), lds, s, a);
     return hipGetLastError();
 }
 
