@@ -781,12 +781,23 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
     // contract sizes and every responder's totals and sample (each an L2 round trip per round
     // otherwise); no round writes a record
     extern __shared__ DtRec srec[];  // [Ct] (dynamic)
-    if (a.ctl->done) return;
 #ifdef MCS_STAMPS
     const uint64_t tr_t0 = wall_clock64();
 #endif
-    const uint32_t T = a.ctl->T;
-    const bool any_due = a.ctl->any_due != 0u;
+    // the control block and every record in one batch of loads: the done test comes after them
+    // (a return before them would make every load wait for the control block's round trip)
+    static_assert(sizeof(DtCtl) == 3 * sizeof(uint4), "DtCtl copy");
+    DtCtl c0;
+    {
+        const uint4* cp = reinterpret_cast<const uint4*>(a.ctl);
+        uint4* cd = reinterpret_cast<uint4*>(&c0);
+        const uint4 x0 = cp[0], x1 = cp[1], x2 = cp[2];
+        cd[0] = x0;
+        cd[1] = x1;
+        cd[2] = x2;
+    }
+    const uint32_t T = c0.T;
+    const bool any_due = c0.any_due != 0u;
     const uint32_t lane = threadIdx.x;
     const uint32_t Ct = a.Ct;
     for (uint32_t q = lane; q < Ct; q += kWave) {
@@ -804,7 +815,8 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
         nfr[q] = srec[q].nfree;
     }
     __syncthreads();
-    unsigned long long n_trades = a.ctl->n_trades, n_won = a.ctl->n_won, n_for = a.ctl->n_foreign;
+    if (c0.done) return;  // (uniform: after the block-wide barrier above)
+    unsigned long long n_trades = c0.n_trades, n_won = c0.n_won, n_for = c0.n_foreign;
     uint32_t lflags = 0;
 
     for (uint32_t q0 = 0; q0 < Ct && a.period && any_due; q0 += kWave) {
@@ -1045,7 +1057,7 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
     }
     if (lane == 0) {
         DtCtl* ctl = a.ctl;
-        uint32_t flags = ctl->flags | fl | lflags;
+        uint32_t flags = c0.flags | fl | lflags;
         uint32_t done = 0, Tn = T;
         if (done_all || (flags & MCS_FLAG_OVERFLOW)) {
             done = 1u;
@@ -1058,7 +1070,7 @@ __global__ __launch_bounds__(64) void dt_trader_kernel(DtArgs a) {
         ctl->T = Tn;
         ctl->done = done;
         ctl->any_due = ndue <= Tn ? 1u : 0u;
-        ctl->ticks += 1u;
+        ctl->ticks = c0.ticks + 1u;
         ctl->flags = flags;
         ctl->n_trades = n_trades;
         ctl->n_won = n_won;
