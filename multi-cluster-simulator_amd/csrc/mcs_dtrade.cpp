@@ -37,7 +37,8 @@ struct DtradeDev {
     mcs_foreign_rec* foreign = nullptr;
     unsigned char* xb = nullptr;  // world exchange blocks
     uint32_t* nv_all = nullptr;
-    DtCtl* h_ctl = nullptr;
+    DtCtl* h_ctl = nullptr;  // [3]: the control block as last read; [1], [2]: the graph loop's polls
+    hipEvent_t pev[2] = {nullptr, nullptr};
     hipGraphExec_t graph = nullptr;
     hipGraphExec_t rgraph = nullptr;  // RCCL loop: kernels + all-gathers of kDtGraphTicks ticks
     bool rgraph_tried = false;
@@ -93,7 +94,7 @@ int dtrade_alloc(mcs_engine* e) {
     HIPCHK(e, hipMalloc(&d->l1snap, (size_t)C * W * 8));
     HIPCHK(e, hipMalloc(&d->trades, trade_cap * sizeof(mcs_contract_rec)));
     HIPCHK(e, hipMalloc(&d->foreign, foreign_cap * sizeof(mcs_foreign_rec)));
-    HIPCHK(e, hipHostMalloc(&d->h_ctl, sizeof(DtCtl), hipHostMallocDefault));
+    HIPCHK(e, hipHostMalloc(&d->h_ctl, 3 * sizeof(DtCtl), hipHostMallocDefault));
     DtArgs& a = d->a;
     a.C = C;
     a.V = V;
@@ -168,14 +169,24 @@ int dt_run_once(mcs_engine* e, double* kernel_ms) {
         if (st != hipSuccess) return dt_hip_fail(e, "hipGraphInstantiate", st);
     }
     d->loop_form = kLoopGraph;
+    for (hipEvent_t& ev : d->pev)
+        if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    // the polls are pipelined: replay k + 1 is queued before replay k's control block is read, so
+    // the GPU never idles through a host round trip (a run that ended in replay k runs one more
+    // replay of finished ticks, whose kernels return at once and write nothing)
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
-    for (;;) {
+    DtCtl* const hp = d->h_ctl + 1;
+    for (uint32_t k = 0;; ++k) {
         HIPCHK(e, hipGraphLaunch(d->graph, e->stream));
-        if (int s = dt_poll(e)) return s;
-        if (d->h_ctl->done) break;
+        HIPCHK(e, hipMemcpyAsync(hp + (k & 1u), d->ctl, sizeof(DtCtl), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipEventRecord(d->pev[k & 1u], e->stream));
+        if (k == 0u) continue;
+        HIPCHK(e, hipEventSynchronize(d->pev[(k - 1u) & 1u]));
+        if (hp[(k - 1u) & 1u].done) break;
     }
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (int s = dt_poll(e)) return s;  // (the final control block into h_ctl[0])
     float ms = 0.0f;
     HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
     *kernel_ms = ms;
@@ -296,6 +307,8 @@ void dtrade_free(mcs_engine* e) {
     dfree(d->xb);
     dfree(d->nv_all);
     if (d->h_ctl) (void)hipHostFree(d->h_ctl);
+    for (hipEvent_t& ev : d->pev)
+        if (ev) (void)hipEventDestroy(ev);
     delete d;
     e->dtd = nullptr;
     e->dtrade_run = false;
