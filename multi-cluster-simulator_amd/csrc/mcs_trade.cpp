@@ -43,7 +43,8 @@ struct TradeDev {
     bool rk_started = false;             // its tick-0 phase A has run
     uint64_t rk_tick = 0;                // one-launch ticks launched (the exchange buffer's parity)
     size_t rk_lds = 0;
-    TrCtl* h_ctl = nullptr;  // pinned
+    TrCtl* h_ctl = nullptr;  // pinned, [3]: the control block as last read; [1], [2]: pipelined polls
+    hipEvent_t pev[2] = {nullptr, nullptr};
     hipGraphExec_t graph = nullptr;
     uint32_t graph_ticks = 0;
     hipGraphExec_t rgraph = nullptr;  // RCCL loop: kernels + all-gathers of kGraphTicks ticks
@@ -153,7 +154,7 @@ int trade_alloc(mcs_engine* e) {
     HIPCHK(e, hipMalloc(&td->ctl, 2u * sizeof(TrCtl)));
     HIPCHK(e, hipMalloc(&td->lent, lent_cap * sizeof(mcs_lent_rec)));
     HIPCHK(e, hipMalloc(&td->trades, trade_cap * sizeof(mcs_trade_rec)));
-    HIPCHK(e, hipHostMalloc(&td->h_ctl, sizeof(TrCtl), hipHostMallocDefault));
+    HIPCHK(e, hipHostMalloc(&td->h_ctl, 3 * sizeof(TrCtl), hipHostMallocDefault));
     HIPCHK(e, hipMalloc(&td->lrp, std::max<uint32_t>(Cl, 1u) * sizeof(uint4)));
 
     TradeArgs& a = td->a;
@@ -219,6 +220,27 @@ int poll_ctl(mcs_engine* e) {
     HIPCHK(e, hipMemcpyAsync(e->td->h_ctl, e->td->ctl, sizeof(TrCtl), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return MCS_OK;
+}
+
+// replays of a captured tick loop until the run is done, the polls pipelined: replay k + 1 is queued
+// before replay k's control block is read, so the GPU never idles through a host round trip.  A
+// run that ended in replay k runs one more replay of finished ticks (their kernels return at once;
+// every rank reads the same replicated flag, so the collectives stay matched).
+template <class Replay>
+int replay_until_done(mcs_engine* e, Replay&& replay) {
+    TradeDev* td = e->td;
+    for (hipEvent_t& ev : td->pev)
+        if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    TrCtl* const hp = td->h_ctl + 1;
+    for (uint32_t k = 0;; ++k) {
+        if (int s = replay()) return s;
+        HIPCHK(e, hipMemcpyAsync(hp + (k & 1u), td->ctl, sizeof(TrCtl), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipEventRecord(td->pev[k & 1u], e->stream));
+        if (k == 0u) continue;
+        HIPCHK(e, hipEventSynchronize(td->pev[(k - 1u) & 1u]));
+        if (hp[(k - 1u) & 1u].done) break;
+    }
+    return poll_ctl(e);  // (the final control block into h_ctl[0])
 }
 
 // one engine holds the whole system.  When it fits one workgroup (<= 64 clusters of <= 256 nodes,
@@ -320,11 +342,10 @@ int run_local(mcs_engine* e) {
         td->graph_ticks = kGraphTicks;
     }
     td->loop_form = e->tr_no_resident ? kLoopGraphAfterTimeout : kLoopGraph;
-    for (;;) {
+    return replay_until_done(e, [&]() -> int {
         HIPCHK(e, hipGraphLaunch(td->graph, e->stream));
-        if (int s = poll_ctl(e)) return s;
-        if (td->h_ctl->done) return MCS_OK;
-    }
+        return MCS_OK;
+    });
 }
 
 int nccl_fail(mcs_engine* e, const char* what, ncclResult_t r) {
@@ -365,7 +386,7 @@ int run_rccl_rk(mcs_engine* e) {
         td->rgraph = capture_tick_graph(e->stream, kGraphTicks, tick);
     }
     td->loop_form = td->rgraph ? kLoopRkGraph : kLoopRkEager;
-    for (;;) {
+    return replay_until_done(e, [&]() -> int {
         if (td->rgraph) {
             HIPCHK(e, hipGraphLaunch(td->rgraph, e->stream));
         } else {
@@ -376,9 +397,8 @@ int run_rccl_rk(mcs_engine* e) {
                 if (st != hipSuccess) return hip_fail(e, "one-launch tick", st);
             }
         }
-        if (int s = poll_ctl(e)) return s;
-        if (td->h_ctl->done) return MCS_OK;
-    }
+        return MCS_OK;
+    });
 }
 
 int run_rccl(mcs_engine* e) {
@@ -399,7 +419,7 @@ int run_rccl(mcs_engine* e) {
         td->rgraph = capture_tick_graph(e->stream, kGraphTicks, tick);
     }
     td->loop_form = td->rgraph ? kLoopRcclGraph : kLoopRcclEager;
-    for (;;) {
+    return replay_until_done(e, [&]() -> int {
         if (td->rgraph) {
             HIPCHK(e, hipGraphLaunch(td->rgraph, e->stream));
         } else {
@@ -412,9 +432,8 @@ int run_rccl(mcs_engine* e) {
                     if (int s = launch_phase(e, a, p)) return s;
             }
         }
-        if (int s = poll_ctl(e)) return s;
-        if (td->h_ctl->done) return MCS_OK;
-    }
+        return MCS_OK;
+    });
 }
 
 int fill_stats(mcs_engine* e, mcs_trade_stats* ts, mcs_stats* st) {
@@ -504,6 +523,8 @@ void trade_free(mcs_engine* e) {
     dfree(td->lrp);
     dfree(td->tnr);
     if (td->h_ctl) (void)hipHostFree(td->h_ctl);
+    for (hipEvent_t& ev : td->pev)
+        if (ev) (void)hipEventDestroy(ev);
     delete td;
     e->td = nullptr;
     e->trade_run = false;
