@@ -1,5 +1,5 @@
 // mcs_dtrade.cpp — host side of the lock-step trading system with DELAY schedulers (DESIGN.md
-// §11): device state, the tick loop (two kernels per tick; world 1: 64 ticks per captured
+// §11): device state, the tick loop (two kernels per tick; world 1: 256 ticks per captured
 // hipGraph, one host poll per replay; world > 1: an ncclAllGather of the exchange blocks between
 // the kernels, or the caller-driven phases), capacity escalation and the result readers of
 // mcs_trade.h.  Every decision is made by the gfx950 kernels of mcs_dtrade.hip; there is no CPU path.
@@ -49,7 +49,7 @@ struct DtradeDev {
 
 namespace {
 
-constexpr uint32_t kDtGraphTicks = 64;
+constexpr uint32_t kDtGraphTicks = 256;  // (r05: 64 -> 256, A/B 14.57 -> 14.44 us per C5-DELAY tick)
 
 int dt_hip_fail(mcs_engine* e, const char* what, hipError_t st) {
     return fail(e, MCS_E_HIP, std::string(what) + ": " + hipGetErrorString(st));
