@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MCS_ABI_VERSION 6
+#define MCS_ABI_VERSION 7
 
 /* ---- status codes --------------------------------------------------------------------------- */
 typedef enum mcs_status {

@@ -104,6 +104,12 @@ typedef struct mcs_trade_stats {
                               phase API (MCS_TRADE_RK=0: the three-kernel forms 0-2) */
     double kernel_ms;      /* device time of the lock-step loop (HIP events) */
     double wall_ms;
+    /* ABI v7: the exchange-block layout the run used (equal on every rank) */
+    uint64_t block_bytes;  /* bytes of one rank's exchange block (the all-gather's per-rank slice) */
+    uint32_t snaps;        /* 1 = the blocks carry node snapshots; 0 = records + G tables only
+                              (the one-launch tick when no rank has a node above 64 cores) */
+    uint32_t agreed;       /* 1 = the layout was agreed over all ranks (the RCCL loop's shape
+                              all-reduce, or mcs_trade_set_shape on the caller-driven path) */
 } mcs_trade_stats;
 
 /* ---- sharding and transport ------------------------------------------------------------------- */
@@ -127,6 +133,22 @@ int mcs_comm_init(mcs_engine* eng, const mcs_comm_id* id);
  * that ends the run; keep calling phase 0..3 until then.  mcs_trade_begin resets the lock-step
  * state; mcs_trade_end fills the stats and makes the results readable. */
 int mcs_trade_begin(mcs_engine* eng);
+/* Agreed block layout (ABI v7).  The RCCL loop agrees on the exchange-block layout with one
+ * all-reduce (MAX) before the run.  The caller-driven transport does the same through these two
+ * calls, made after mcs_set_shard / mcs_submit_jobs and before mcs_trade_begin:
+ * mcs_trade_shape_words writes this rank's MCS_TRADE_SHAPE_WORDS words; the caller takes their
+ * element-wise MAX over all ranks and passes the result to mcs_trade_set_shape on every rank.  The
+ * agreed shape fixes the snapshot stride (the largest cluster of the system), whether every rank
+ * runs the one-launch tick (one rank that cannot, or has MCS_TRADE_RK=0, turns it off for all) and
+ * whether the blocks drop the node snapshots (no node above 64 cores on any rank: 320 B per
+ * cluster, the layout an 8-GPU RCCL run uses).  A cluster-count mismatch fails (MCS_E_INVALID) on
+ * every rank.  Without an agreed shape each rank decides from its own shard and the blocks keep
+ * the snapshots.  Every caller-driven phase-0 block ends in a 16-byte layout tag (tick form,
+ * snapshots, stride, clusters, policy); phase 1 fails with MCS_E_INVALID when the gathered blocks'
+ * tags differ, so ranks that chose different layouts never exchange silently. */
+#define MCS_TRADE_SHAPE_WORDS 8
+int mcs_trade_shape_words(mcs_engine* eng, uint32_t* out);
+int mcs_trade_set_shape(mcs_engine* eng, const uint32_t* agreed);
 int mcs_trade_xfer_bytes(mcs_engine* eng, uint32_t phase, uint64_t* in_bytes, uint64_t* out_bytes);
 int mcs_trade_phase(mcs_engine* eng, uint32_t phase, const void* in, uint64_t in_bytes, void* out,
                     uint64_t out_bytes, uint32_t* done);

@@ -37,8 +37,11 @@ struct DtradeDev {
     mcs_foreign_rec* foreign = nullptr;
     unsigned char* xb = nullptr;  // world exchange blocks
     uint32_t* nv_all = nullptr;
-    DtCtl* h_ctl = nullptr;  // [3]: the control block as last read; [1], [2]: the graph loop's polls
+    DtCtl* h_ctl = nullptr;  // 3 entries: [0] the control block as last read; [1], [2] the graph loop's polls
     hipEvent_t pev[2] = {nullptr, nullptr};
+    hipEvent_t tev[2] = {nullptr, nullptr};  // timing: the end of each pipelined replay
+    double kernel_ms = 0.0;                  // device time of the last run (mcs_read_trade_stats)
+    uint32_t tag[4] = {0, 0, 0, 0};          // caller-driven blocks: the layout tag (kDtTagBytes at the end)
     hipGraphExec_t graph = nullptr;
     hipGraphExec_t rgraph = nullptr;  // RCCL loop: kernels + all-gathers of kDtGraphTicks ticks
     bool rgraph_tried = false;
@@ -49,6 +52,7 @@ struct DtradeDev {
 
 namespace {
 
+constexpr uint64_t kDtTagBytes = 16;  // caller-driven exchange blocks end in the layout tag
 constexpr uint32_t kDtGraphTicks = 256;  // (r05: 64 -> 256, A/B 14.57 -> 14.44 us per C5-DELAY tick)
 
 int dt_hip_fail(mcs_engine* e, const char* what, hipError_t st) {
@@ -70,10 +74,16 @@ int dtrade_alloc(mcs_engine* e) {
     if (S > kDtMaxSlots) return fail(e, MCS_E_INVALID, "slot pool above 4096");
     const uint32_t V = e->dt_vnodes ? e->dt_vnodes : 64u;
     const uint32_t NS = std::max<uint32_t>(e->dt_ns ? e->dt_ns : e->max_n, 1u), W = NS + V;
-    const unsigned long long blk = (unsigned long long)C * sizeof(DtRec) + (unsigned long long)C * W * 8ull;
+    // (a caller-driven block ends in a 16-byte layout tag that phase 1 checks on every gathered block)
+    const unsigned long long blk = (unsigned long long)C * sizeof(DtRec) + (unsigned long long)C * W * 8ull +
+                                   (e->comm ? 0ull : kDtTagBytes);
     DtradeDev* d = new (std::nothrow) DtradeDev();
     if (!d) return fail(e, MCS_E_NOMEM, "DELAY trading state");
     e->dtd = d;
+    d->tag[0] = 0x5853434Du;  // "MCSX"
+    d->tag[1] = 8u | (e->tr_agreed ? 4u : 0u);  // (8: the DELAY trading block)
+    d->tag[2] = W;
+    d->tag[3] = C;
     const size_t nj = e->total_jobs ? e->total_jobs : 1;
     const uint64_t trade_cap = 1ull << 20, foreign_cap = 1ull << 22;
     HIPCHK(e, hipMalloc(&d->tn, std::max<uint64_t>(e->total_nodes, 1) * 8));
@@ -171,24 +181,30 @@ int dt_run_once(mcs_engine* e, double* kernel_ms) {
     d->loop_form = kLoopGraph;
     for (hipEvent_t& ev : d->pev)
         if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (hipEvent_t& ev : d->tev)
+        if (!ev) HIPCHK(e, hipEventCreate(&ev));
     // the polls are pipelined: replay k + 1 is queued before replay k's control block is read, so
     // the GPU never idles through a host round trip (a run that ended in replay k runs one more
     // replay of finished ticks, whose kernels return at once and write nothing)
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
     DtCtl* const hp = d->h_ctl + 1;
+    hipEvent_t end_ev = nullptr;
     for (uint32_t k = 0;; ++k) {
         HIPCHK(e, hipGraphLaunch(d->graph, e->stream));
+        HIPCHK(e, hipEventRecord(d->tev[k & 1u], e->stream));
         HIPCHK(e, hipMemcpyAsync(hp + (k & 1u), d->ctl, sizeof(DtCtl), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(e, hipEventRecord(d->pev[k & 1u], e->stream));
         if (k == 0u) continue;
         HIPCHK(e, hipEventSynchronize(d->pev[(k - 1u) & 1u]));
-        if (hp[(k - 1u) & 1u].done) break;
+        if (hp[(k - 1u) & 1u].done) {
+            end_ev = d->tev[(k - 1u) & 1u];  // (kernel_ms ends with the replay that finished the run)
+            break;
+        }
     }
-    HIPCHK(e, hipEventRecord(e->ev1, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (int s = dt_poll(e)) return s;  // (the final control block into h_ctl[0])
     float ms = 0.0f;
-    HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, end_ev));
     *kernel_ms = ms;
     return MCS_OK;
 }
@@ -309,6 +325,8 @@ void dtrade_free(mcs_engine* e) {
     if (d->h_ctl) (void)hipHostFree(d->h_ctl);
     for (hipEvent_t& ev : d->pev)
         if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t& ev : d->tev)
+        if (ev) (void)hipEventDestroy(ev);
     delete d;
     e->dtd = nullptr;
     e->dtrade_run = false;
@@ -355,6 +373,7 @@ int dtrade_run(mcs_engine* e, mcs_stats* stats) {
     }
     e->dt_learn_s = e->cfg.slot_pool ? 0u : e->dtd->a.S;
     e->dt_learn_v = e->dtd->a.V;
+    e->dtd->kernel_ms = kms;
     e->has_run = true;
     e->dtrade_run = true;
     e->trade_run = false;
@@ -416,6 +435,14 @@ int dtrade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_byte
     if (int s = dtrade_xfer_bytes(e, phase, &ib, &ob)) return s;
     if (in_bytes != ib || out_bytes != ob || (ib && !in) || (ob && !out))
         return fail(e, MCS_E_INVALID, "exchange buffer sizes do not match mcs_trade_xfer_bytes");
+    if (phase == 1) {  // every gathered block must carry this rank's layout tag
+        const unsigned char* p = static_cast<const unsigned char*>(in);
+        for (uint32_t r = 0; r < e->world; ++r)
+            if (std::memcmp(p + (size_t)(r + 1u) * d->a.blk - kDtTagBytes, d->tag, kDtTagBytes) != 0)
+                return fail(e, MCS_E_INVALID, "exchange block of rank " + std::to_string(r) +
+                                                  " has another layout (stride or clusters): agree on the shape"
+                                                  " with mcs_trade_set_shape");
+    }
     hipError_t st = hipSuccess;
     switch (phase) {
         case 0:
@@ -433,6 +460,7 @@ int dtrade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_byte
             break;
     }
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (phase == 0) std::memcpy(static_cast<unsigned char*>(out) + ob - kDtTagBytes, d->tag, kDtTagBytes);
     if (done) *done = phase == 3 ? d->h_ctl->done : 0u;
     return MCS_OK;
 }
@@ -449,6 +477,11 @@ int dtrade_end(mcs_engine* e, mcs_stats* stats) {
     e->delay_run = true;
     if (int s = dt_poll(e)) return s;
     const uint32_t flags = d->h_ctl->flags;
+    {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) ms = 0.0f;
+        d->kernel_ms = ms;
+    }
     if (stats) {
         std::vector<DtCluster> cl;
         if (int s = dt_clusters(e, cl)) return s;
@@ -461,9 +494,7 @@ int dtrade_end(mcs_engine* e, mcs_stats* stats) {
         st.unplaced = e->total_jobs - st.placed;
         st.clusters = e->C;
         st.slot_pool = d->a.S / 64u;
-        float ms = 0.0f;
-        if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) ms = 0.0f;
-        st.kernel_ms = ms;
+        st.kernel_ms = d->kernel_ms;
         st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d->w0).count();
         *stats = st;
     }
@@ -528,9 +559,10 @@ int dtrade_trade_stats(mcs_engine* e, mcs_trade_stats* out) {
     s.t_final = c.T;
     s.flags = flags;
     s.loop_form = e->dtd->loop_form;
-    float ms = 0.0f;
-    if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) ms = 0.0f;
-    s.kernel_ms = ms;
+    s.kernel_ms = e->dtd->kernel_ms;
+    s.block_bytes = e->dtd->a.blk;
+    s.snaps = 1u;
+    s.agreed = (e->comm || e->tr_agreed) ? 1u : 0u;
     *out = s;
     return MCS_OK;
 }

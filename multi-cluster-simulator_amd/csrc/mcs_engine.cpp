@@ -230,7 +230,7 @@ int mcs_engine_destroy(mcs_engine* e) {
     mcs::trade_release_graphs(e);
     mcs::dtrade_release_graphs(e);
     mcs::comm_free(e);
-    (void)hipDeviceSynchronize();
+    if (e->stream) (void)hipStreamSynchronize(e->stream);  // (this engine's work only: not the device's)
     mcs::trade_free(e);
     mcs::dtrade_free(e);
     mcs::online_free(e);
@@ -277,6 +277,8 @@ int mcs_load_clusters(mcs_engine* e, const uint32_t* cap_c, const uint32_t* cap_
     mcs::dtrade_free(e);
     e->has_clusters = e->has_jobs = e->has_run = false;
     e->dt_learn_s = e->dt_learn_v = 0;
+    e->tr_agreed = false;  // (an agreed block layout belongs to the clusters it was agreed for)
+    e->tr_ns = e->dt_ns = 0;
     e->C = n_clusters;
     e->max_n = max_n;
     e->total_nodes = nn;

@@ -147,6 +147,8 @@ struct mcs_engine {
     bool tr_rk_ok = true;              // every rank can run the one-launch tick (tr_agree_shape)
     bool tr_nosnap = false;            // no rank has a node above 64 cores: the one-launch tick's
                                        // exchange blocks carry no node snapshots (tr_agree_shape)
+    bool tr_agreed = false;            // the ranks agreed on the block layout (tr_agree_shape on the
+                                       // RCCL path, mcs_trade_set_shape on the caller-driven one)
     // online mode (mcs_online.cpp): per-cluster state kept on the device between horizons
     bool online = false;               // a session is active
     bool segmented = false;            // job_off holds segment starts with slack (appends)

@@ -43,8 +43,11 @@ struct TradeDev {
     bool rk_started = false;             // its tick-0 phase A has run
     uint64_t rk_tick = 0;                // one-launch ticks launched (the exchange buffer's parity)
     size_t rk_lds = 0;
-    TrCtl* h_ctl = nullptr;  // pinned, [3]: the control block as last read; [1], [2]: pipelined polls
+    TrCtl* h_ctl = nullptr;  // pinned, 3 entries: [0] the control block as last read; [1], [2] the pipelined polls
     hipEvent_t pev[2] = {nullptr, nullptr};
+    hipEvent_t tev[2] = {nullptr, nullptr};  // timing: the end of each pipelined replay
+    hipEvent_t end_ev = nullptr;             // the end of the replay whose control block showed done
+    uint32_t tag[4] = {0, 0, 0, 0};          // caller-driven blocks: the layout tag (kTagBytes at the end)
     hipGraphExec_t graph = nullptr;
     uint32_t graph_ticks = 0;
     hipGraphExec_t rgraph = nullptr;  // RCCL loop: kernels + all-gathers of kGraphTicks ticks
@@ -56,6 +59,8 @@ struct TradeDev {
 
 namespace {
 
+constexpr uint64_t kTagBytes = 16;     // caller-driven exchange blocks end in the layout tag
+constexpr uint32_t kTagMagic = 0x5853434Du;  // "MCSX"
 constexpr uint32_t kGraphTicks = 256;  // ticks per graph replay (one host poll per replay; r05: 64 -> 256, A/B 9.60 -> 9.44 us per tick on the one-launch RCCL loop)
 
 int hip_fail(mcs_engine* e, const char* what, hipError_t st) {
@@ -140,9 +145,16 @@ int trade_alloc(mcs_engine* e) {
     // one-launch tick's G tables, 256 B per cluster, follow the snapshots.  On the RCCL path, when no
     // rank has a node above 64 cores, no lender is ever "big": the one-launch tick's blocks then
     // carry no snapshots at all — 320 B per cluster instead of 320 B + 8 B per node)
-    const bool snaps = !(rk && e->comm && e->tr_nosnap);
-    const uint64_t blk = ((uint64_t)Cl * sizeof(TrXRec) + (snaps ? (uint64_t)Cl * ns * 8u : 0ull) +
-                          (uint64_t)Cl * 256u + 15u) & ~15ull;
+    // The caller-driven path drops them too when its ranks agreed on the shape (mcs_trade_set_shape).
+    // A caller-driven block ends in a 16-byte layout tag that phase 1 checks on every gathered block)
+    const bool snaps = !(rk && (e->comm || e->tr_agreed) && e->tr_nosnap);
+    const uint64_t tagb = e->comm ? 0ull : kTagBytes;
+    const uint64_t blk = (((uint64_t)Cl * sizeof(TrXRec) + (snaps ? (uint64_t)Cl * ns * 8u : 0ull) +
+                           (uint64_t)Cl * 256u + 15u) & ~15ull) + tagb;
+    td->tag[0] = kTagMagic;
+    td->tag[1] = (rk ? 1u : 0u) | (snaps ? 2u : 0u) | (e->tr_agreed ? 4u : 0u);
+    td->tag[2] = ns;
+    td->tag[3] = Cl;
     // (two buffers of world blocks: the one-launch tick alternates them by tick parity)
     HIPCHK(e, hipMalloc(&td->xb, 2u * (size_t)e->world * blk));
     HIPCHK(e, hipMalloc(&td->acc, Ct * 4));
@@ -231,14 +243,22 @@ int replay_until_done(mcs_engine* e, Replay&& replay) {
     TradeDev* td = e->td;
     for (hipEvent_t& ev : td->pev)
         if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (hipEvent_t& ev : td->tev)
+        if (!ev) HIPCHK(e, hipEventCreate(&ev));
     TrCtl* const hp = td->h_ctl + 1;
     for (uint32_t k = 0;; ++k) {
         if (int s = replay()) return s;
+        HIPCHK(e, hipEventRecord(td->tev[k & 1u], e->stream));
         HIPCHK(e, hipMemcpyAsync(hp + (k & 1u), td->ctl, sizeof(TrCtl), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(e, hipEventRecord(td->pev[k & 1u], e->stream));
         if (k == 0u) continue;
         HIPCHK(e, hipEventSynchronize(td->pev[(k - 1u) & 1u]));
-        if (hp[(k - 1u) & 1u].done) break;
+        if (hp[(k - 1u) & 1u].done) {
+            // kernel_ms ends with the replay that finished the run: the one more replay of no-op
+            // ticks queued behind it (the pipelined poll's price) is not part of the run
+            td->end_ev = td->tev[(k - 1u) & 1u];
+            break;
+        }
     }
     return poll_ctl(e);  // (the final control block into h_ctl[0])
 }
@@ -462,6 +482,9 @@ int fill_stats(mcs_engine* e, mcs_trade_stats* ts, mcs_stats* st) {
     s.t_final = c.T;
     s.flags = flags;
     s.loop_form = td->loop_form;
+    s.block_bytes = td->a.blk;
+    s.snaps = td->a.snaps;
+    s.agreed = (e->comm || e->tr_agreed) ? 1u : 0u;
     if (ts) *ts = s;
     if (st) {
         st->jobs = e->total_jobs;
@@ -473,6 +496,23 @@ int fill_stats(mcs_engine* e, mcs_trade_stats* ts, mcs_stats* st) {
         st->escalations = 0;
         st->slot_pool = td->a.S / 64u;
     }
+    return MCS_OK;
+}
+
+// a caller-driven block's last kTagBytes: the layout it was written in (TradeDev::tag)
+void put_tag(const TradeDev* td, void* out, uint64_t ob) {
+    std::memcpy(static_cast<unsigned char*>(out) + ob - kTagBytes, td->tag, kTagBytes);
+}
+
+// phase 1: every gathered block must carry this rank's tag (same tick form, snapshots, stride and
+// cluster count), else ranks that chose different layouts would read each other's blocks wrongly
+int check_tags(mcs_engine* e, const void* in, uint64_t blk) {
+    const unsigned char* p = static_cast<const unsigned char*>(in);
+    for (uint32_t r = 0; r < e->world; ++r)
+        if (std::memcmp(p + (size_t)r * blk + blk - kTagBytes, e->td->tag, kTagBytes) != 0)
+            return fail(e, MCS_E_INVALID, "exchange block of rank " + std::to_string(r) +
+                                              " has another layout (tick form, snapshots, stride or clusters):"
+                                              " agree on the shape with mcs_trade_set_shape");
     return MCS_OK;
 }
 
@@ -525,6 +565,8 @@ void trade_free(mcs_engine* e) {
     if (td->h_ctl) (void)hipHostFree(td->h_ctl);
     for (hipEvent_t& ev : td->pev)
         if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t& ev : td->tev)
+        if (ev) (void)hipEventDestroy(ev);
     delete td;
     e->td = nullptr;
     e->trade_run = false;
@@ -574,7 +616,23 @@ int tr_agree_shape(mcs_engine* e) {
     e->tr_ns = mx[0];
     e->tr_rk_ok = mx[3] == 0u;
     e->tr_nosnap = mx[4] == 0u;
+    e->tr_agreed = true;
     return MCS_OK;
+}
+
+// the caller-driven twin of tr_agree_shape / dt_agree_shape's words (mcs_trade_shape_words): the
+// caller takes the element-wise max over its ranks
+void shape_words(const mcs_engine* e, uint32_t* w) {
+    const char* rkenv = getenv("MCS_TRADE_RK");
+    const bool want_rk = !rkenv || atoi(rkenv) != 0;
+    w[0] = e->max_n;
+    w[1] = e->C;
+    w[2] = ~e->C;
+    w[3] = (e->sums_lt24 && e->slot_pack_ok && want_rk) ? 0u : 1u;
+    w[4] = e->cores_le64 ? 0u : 1u;
+    w[5] = e->dt_vnodes;
+    w[6] = 0u;
+    w[7] = 0u;
 }
 
 int trade_run(mcs_engine* e, mcs_stats* stats) {
@@ -655,6 +713,7 @@ int mcs_set_shard(mcs_engine* e, uint32_t rank, uint32_t world) {
     e->tr_ns = 0;
     e->tr_rk_ok = true;
     e->tr_nosnap = false;
+    e->tr_agreed = false;
     e->rank = rank;
     e->world = world;
     return MCS_OK;
@@ -672,10 +731,20 @@ int mcs_comm_unique_id(mcs_comm_id* out) {
 int mcs_comm_init(mcs_engine* e, const mcs_comm_id* id) {
     if (int st = check_engine(e)) return st;
     if (!id) return fail(e, MCS_E_INVALID, "null id");
-    if (e->comm) {
-        (void)ncclCommDestroy((ncclComm_t)e->comm);
-        e->comm = nullptr;
-    }
+    // the captured tick graphs reference a previous communicator's resources, and the trading
+    // states were laid out (and their shape agreed) for another transport: all of them go first, in
+    // mcs_engine_destroy's order — graphs, the old communicator (finalized), then the states
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    mcs::trade_release_graphs(e);
+    mcs::dtrade_release_graphs(e);
+    mcs::comm_free(e);
+    mcs::trade_free(e);
+    mcs::dtrade_free(e);
+    e->tr_ns = 0;
+    e->dt_ns = 0;
+    e->tr_rk_ok = true;
+    e->tr_nosnap = false;
+    e->tr_agreed = false;
     ncclUniqueId uid;
     std::memcpy(&uid, id->bytes, sizeof(uid));
     ncclComm_t comm = nullptr;
@@ -700,6 +769,7 @@ int mcs_trade_begin(mcs_engine* e) {
     if (st != hipSuccess) return mcs::hip_fail(e, "trade init", st);
     td->rk_started = false;
     td->rk_tick = 0;
+    td->end_ev = nullptr;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));  // kernel_ms: the lock-step loop only
     td->begun = true;
@@ -708,17 +778,47 @@ int mcs_trade_begin(mcs_engine* e) {
     return MCS_OK;
 }
 
+int mcs_trade_shape_words(mcs_engine* e, uint32_t* out) {
+    if (int st = check_engine(e)) return st;
+    if (!out) return fail(e, MCS_E_INVALID, "null output");
+    if (!e->has_clusters) return fail(e, MCS_E_STATE, "mcs_load_clusters first");
+    mcs::shape_words(e, out);
+    return MCS_OK;
+}
+
+int mcs_trade_set_shape(mcs_engine* e, const uint32_t* w) {
+    if (int st = check_engine(e)) return st;
+    if (!w) return fail(e, MCS_E_INVALID, "null shape");
+    if (!e->has_clusters) return fail(e, MCS_E_STATE, "mcs_load_clusters first");
+    // (the max over ranks of C and of ~C: equal exactly when every rank holds the same count)
+    if (w[1] != ~w[2] || w[1] != e->C)
+        return fail(e, MCS_E_INVALID, "sharded lock-step trading needs the same cluster count on every rank");
+    if (w[0] < e->max_n || w[0] > mcs::kTrMaxNodes)
+        return fail(e, MCS_E_INVALID, "agreed snapshot stride below this rank's largest cluster (not a max over ranks)");
+    uint32_t mine[MCS_TRADE_SHAPE_WORDS];
+    mcs::shape_words(e, mine);
+    if (w[3] < mine[3] || w[4] < mine[4] || w[5] < mine[5] || w[6] || w[7])
+        return fail(e, MCS_E_INVALID, "agreed shape words are not a max over ranks that include this one");
+    mcs::trade_free(e);
+    mcs::dtrade_free(e);
+    e->tr_ns = w[0];
+    e->dt_ns = w[0];
+    e->tr_rk_ok = w[3] == 0u;
+    e->tr_nosnap = w[4] == 0u;
+    e->dt_vnodes = w[5];
+    e->tr_agreed = true;
+    return MCS_OK;
+}
+
 int mcs_trade_xfer_bytes(mcs_engine* e, uint32_t phase, uint64_t* in_bytes, uint64_t* out_bytes) {
     if (!e || !in_bytes || !out_bytes || phase > 3) return MCS_E_INVALID;
     if (mcs::is_dtrade(e)) return mcs::dtrade_xfer_bytes(e, phase, in_bytes, out_bytes);
     // one exchange per tick: phase 0 writes this rank's block, phase 1 takes every rank's blocks;
-    // phases 2 and 3 move no bytes.  (Block size: the engine's own largest cluster sets the
-    // snapshot stride on the caller-driven path, so every rank must hold clusters of one largest
-    // size, as the shard helpers do.)
-    const uint64_t Cl = e->C;
-    const uint64_t ns = std::max<uint32_t>(e->tr_ns ? e->tr_ns : e->max_n, 1u);
-    // (as trade_alloc: the caller-driven path always carries the snapshots; an allocated state knows)
-    const uint64_t blk = e->td ? e->td->a.blk : (Cl * sizeof(mcs::TrXRec) + Cl * ns * 8u + Cl * 256u + 15u) & ~15ull;
+    // phases 2 and 3 move no bytes.  The block layout is trade_alloc's (the state is allocated
+    // here when it is not yet: mcs_trade_begin reuses it)
+    if (!e->td)
+        if (int st = mcs::trade_alloc(e)) return st;
+    const uint64_t blk = e->td->a.blk;
     switch (phase) {
         case 0: *in_bytes = 0; *out_bytes = blk; break;
         case 1: *in_bytes = (uint64_t)e->world * blk; *out_bytes = 0; break;
@@ -738,6 +838,8 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
     if (in_bytes != ib || out_bytes != ob || (ib && !in) || (ob && !out))
         return fail(e, MCS_E_INVALID, "exchange buffer sizes do not match mcs_trade_xfer_bytes");
     const mcs::TradeArgs& a = td->a;
+    if (phase == 1)
+        if (int st = mcs::check_tags(e, in, a.blk)) return st;
     if (td->rk) {  // the one-launch tick: phase 1 runs B/C/D of tick n and A of tick n + 1
         td->loop_form = mcs::kLoopRkDriven;
         hipError_t hs = hipSuccess;
@@ -765,6 +867,7 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
         }
         if (hs != hipSuccess) return mcs::hip_fail(e, "one-launch tick (caller-driven)", hs);
         HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (phase == 0) mcs::put_tag(td, out, ob);
         if (done) *done = phase == 3 ? td->h_ctl->done : 0u;
         return MCS_OK;
     }
@@ -787,6 +890,7 @@ int mcs_trade_phase(mcs_engine* e, uint32_t phase, const void* in, uint64_t in_b
             break;
     }
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (phase == 0) mcs::put_tag(td, out, ob);
     if (done) *done = phase == 3 ? td->h_ctl->done : 0u;
     return MCS_OK;
 }
@@ -812,7 +916,7 @@ int mcs_trade_end(mcs_engine* e, mcs_stats* stats) {
     mcs_stats st{};
     if (int s = mcs::fill_stats(e, &ts, &st)) return s;
     float ms = 0.0f;
-    if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) ms = 0.0f;
+    if (hipEventElapsedTime(&ms, e->ev0, td->end_ev ? td->end_ev : e->ev1) != hipSuccess) ms = 0.0f;
     st.kernel_ms = ms;
     st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td->w0).count();
     if (stats) *stats = st;
@@ -831,7 +935,7 @@ int mcs_read_trade_stats(mcs_engine* e, mcs_trade_stats* out) {
     mcs_stats st{};
     if (int s = mcs::fill_stats(e, out, &st)) return s;
     float ms = 0.0f;
-    if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) ms = 0.0f;
+    if (hipEventElapsedTime(&ms, e->ev0, e->td->end_ev ? e->td->end_ev : e->ev1) != hipSuccess) ms = 0.0f;
     out->kernel_ms = ms;
     out->wall_ms = 0.0;
     return MCS_OK;

@@ -184,7 +184,13 @@ class mcs_trade_stats(C.Structure):
         ("loop_form", C.c_uint32),
         ("kernel_ms", C.c_double),
         ("wall_ms", C.c_double),
+        ("block_bytes", C.c_uint64),
+        ("snaps", C.c_uint32),
+        ("agreed", C.c_uint32),
     ]
+
+
+MCS_TRADE_SHAPE_WORDS = 8
 
 
 class mcs_approve_query(C.Structure):
@@ -240,6 +246,8 @@ SIGNATURES = [
     ("mcs_comm_unique_id", C.c_int, [C.POINTER(mcs_comm_id)]),
     ("mcs_comm_init", C.c_int, [vp, C.POINTER(mcs_comm_id)]),
     ("mcs_trade_begin", C.c_int, [vp]),
+    ("mcs_trade_shape_words", C.c_int, [vp, u32p]),
+    ("mcs_trade_set_shape", C.c_int, [vp, u32p]),
     ("mcs_trade_xfer_bytes", C.c_int, [vp, C.c_uint32, u64p, u64p]),
     ("mcs_trade_phase", C.c_int, [vp, C.c_uint32, vp, C.c_uint64, vp, C.c_uint64, u32p]),
     ("mcs_trade_end", C.c_int, [vp, C.POINTER(mcs_stats)]),

@@ -267,6 +267,19 @@ class Engine:
     def trade_begin(self):
         self._c(L.lib().mcs_trade_begin(self._h))
 
+    def trade_shape_words(self) -> np.ndarray:
+        """This rank's block-layout words (mcs_trade_shape_words); agree on their max over ranks."""
+        w = np.zeros(L.MCS_TRADE_SHAPE_WORDS, np.uint32)
+        self._c(L.lib().mcs_trade_shape_words(self._h, L.ptr(w, C.c_uint32)))
+        return w
+
+    def trade_set_shape(self, agreed: np.ndarray):
+        """Apply the element-wise max over ranks of trade_shape_words (mcs_trade_set_shape)."""
+        w = np.ascontiguousarray(agreed, dtype=np.uint32)
+        if w.size != L.MCS_TRADE_SHAPE_WORDS:
+            raise ValueError(f"{w.size} shape words, expected {L.MCS_TRADE_SHAPE_WORDS}")
+        self._c(L.lib().mcs_trade_set_shape(self._h, L.ptr(w, C.c_uint32)))
+
     def trade_xfer_bytes(self, phase: int):
         i, o = C.c_uint64(), C.c_uint64()
         self._c(L.lib().mcs_trade_xfer_bytes(self._h, phase, C.byref(i), C.byref(o)))

@@ -44,17 +44,32 @@ def aggregate(elapsed_s: float, placed: int, device=None) -> Tuple[float, float]
 
 
 # ---- lock-step trading over a caller-provided transport (include/mcs_trade.h) ----------------
-def run_lockstep(engine, allgather):
+def agree_shape(engine, allgather):
+    """The caller-driven twin of the RCCL loop's shape all-reduce (mcs_trade_shape_words /
+    mcs_trade_set_shape): every rank gathers every rank's layout words and applies their
+    element-wise max, so all ranks lay their exchange blocks out alike (one tick form, one snapshot
+    stride, and no node snapshots when no rank has a node above 64 cores)."""
+    import numpy as np
+
+    w = engine.trade_shape_words()
+    allw = np.frombuffer(np.ascontiguousarray(allgather(w.view(np.uint8))).tobytes(), np.uint32)
+    engine.trade_set_shape(allw.reshape(-1, w.size).max(axis=0))
+
+
+def run_lockstep(engine, allgather, agree=True):
     """Drive the lock-step trading run of one shard through mcs_trade_phase.
 
     `allgather(buf: np.ndarray[uint8]) -> np.ndarray[uint8]` must return the concatenation, in
-    rank order, of every rank's `buf` (all ranks call it the same number of times).  Every tick
-    is phases 0..3 with an all-gather between consecutive phases; phase 3 reports `done`
-    identically on every rank.  A phase whose output is empty on every rank is not gathered (both
-    trading systems move bytes only from phase 0 to phase 1).  Returns the engine's RunStats."""
+    rank order, of every rank's `buf` (all ranks call it the same number of times).  With `agree`
+    the ranks first agree on the exchange-block layout (agree_shape).  Every tick is phases 0..3
+    with an all-gather between consecutive phases; phase 3 reports `done` identically on every
+    rank.  A phase whose output is empty on every rank is not gathered (both trading systems move
+    bytes only from phase 0 to phase 1).  Returns the engine's RunStats."""
     def xfer(out):
         return allgather(out) if out.size else out
 
+    if agree:
+        agree_shape(engine, allgather)
     engine.trade_begin()
     while True:
         out, _ = engine.trade_phase(0, None)

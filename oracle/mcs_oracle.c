@@ -333,7 +333,7 @@ int or_allocate_virtual_node(uint32_t n, uint64_t* free_c, uint64_t* free_m, uin
             req_c -= (uint32_t)core_diff;
         /* go node.RunJob(Job{CoresNeeded: uint(core_diff), MemoryNeeded: uint(mem_diff), ...}),
          * :116 — the commit (cluster.go:146-147), uint wrap as Go (D7) */
-        const uint64_t fc = (uint64_t)core_diff, fm = (uint64_t)mem_diff;
+        const uint64_t fc = or_go_f64_to_u64(core_diff), fm = or_go_f64_to_u64(mem_diff);
         free_c[i] -= fc;
         free_m[i] -= fm;
         if (f_node) {

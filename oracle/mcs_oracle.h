@@ -23,6 +23,18 @@
 extern "C" {
 #endif
 
+/* Go's float64 -> uint conversion on amd64 (CVTTSD2SQ below 2^63; above, CVTTSD2SQ of x - 2^63 xor
+ * 2^63, whose integer-indefinite result makes anything >= 2^64 convert to 0).  cluster.go:116 converts
+ * |req - free| this way, and |req - free| reaches 2^64 once a uint counter has wrapped: a plain C cast
+ * of such a value is undefined behaviour (found by the UBSan self-test, tests/test_oracle_sanitize.py). */
+static inline uint64_t or_go_f64_to_u64(double x) {
+    const double two63 = 9223372036854775808.0;
+    if (x < two63) return (uint64_t)(int64_t)x;
+    const double y = x - two63;
+    if (y >= two63) return 0;
+    return (uint64_t)(int64_t)y ^ 0x8000000000000000ull;
+}
+
 typedef struct or_stats {
     uint32_t t_end;
     uint32_t placed;

@@ -175,14 +175,8 @@ static void dt_sample(dt_cluster* k) {
     k->avgw = k->count != 0 ? (double)k->total / (double)k->count : 0.0; /* GetAverage */
 }
 
-/* Go's float64 -> uint conversion on amd64 (CVTTSD2SQ, with the 2^63 split for large values). */
-static uint64_t go_f64_to_u64(double x) {
-    const double two63 = 9223372036854775808.0;
-    if (x < two63) return (uint64_t)(int64_t)x;
-    const double y = x - two63;
-    if (y >= two63) return 0; /* CVTTSD2SQ's integer-indefinite 1<<63, xor 1<<63 */
-    return (uint64_t)(int64_t)y ^ 0x8000000000000000ull;
-}
+/* Go's float64 -> uint conversion on amd64: or_go_f64_to_u64 (mcs_oracle.h) */
+#define go_f64_to_u64 or_go_f64_to_u64
 
 /* AllocateVirtualNodeResources (cluster.go:87-125) on uint64 counters, Foreign jobs released
  * after dur_s.  Returns 0 on success, 1 for "couldn't schedule enough resources". */

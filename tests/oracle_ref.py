@@ -13,7 +13,9 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
-ORACLE_SO = os.path.join(ORACLE_DIR, "libmcs_oracle.so")
+# MCS_ORACLE_SO: another build of the same sources (tests/test_oracle_sanitize.py runs the oracle test
+# modules against the AddressSanitizer + UBSan build, oracle/asan/libmcs_oracle_asan.so)
+ORACLE_SO = os.environ.get("MCS_ORACLE_SO") or os.path.join(ORACLE_DIR, "libmcs_oracle.so")
 
 
 class or_stats(C.Structure):
@@ -77,7 +79,7 @@ u64p = C.POINTER(C.c_uint64)
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(ORACLE_SO):
+        if not os.path.exists(ORACLE_SO) and not os.environ.get("MCS_ORACLE_SO"):
             subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
         L = C.CDLL(ORACLE_SO)
         L.or_fifo_run.argtypes = [C.c_uint32, u32p, u32p, u32p, u32p, C.c_uint64, u32p, u32p, u32p, u32p,

@@ -36,7 +36,7 @@ def test_library_loads_and_exports_header_symbols():
     # every declared function has a ctypes signature in the binding
     bound = {name for name, _, _ in L.SIGNATURES}
     assert set(declared) == bound
-    assert lib.mcs_abi_version() == 6
+    assert lib.mcs_abi_version() == 7
 
 
 def test_library_is_gfx950_code_object():
@@ -162,3 +162,26 @@ def test_trading_engine_without_device_fails_loudly():
         pytest.skip("a device is visible")
     with pytest.raises(mcs_amd.MCSError):
         mcs_amd.Engine(0, borrow=True, trader=True)
+
+
+def test_every_engine_entry_point_refuses_a_null_handle():
+    """Every entry point that takes an engine handle returns MCS_E_INVALID (or its neutral value) for
+    a null handle with null/zero arguments instead of touching memory (no device needed; the same
+    sweep runs against the AddressSanitizer build in test_abi_sanitize.py)."""
+    import ctypes as C
+
+    lib = mcs_amd.lib()
+    n = 0
+    for name, res, args in L.SIGNATURES:
+        if not args or args[0] is not L.vp or not hasattr(lib, name):
+            continue
+        vals = [None if (a is L.vp or hasattr(a, "contents") or a is C.c_char_p) else 0 for a in args]
+        got = getattr(lib, name)(*vals)
+        if res is C.c_int:
+            assert got == L.MCS_E_INVALID, (name, got)
+        elif res is C.c_char_p:
+            assert isinstance(got, bytes), name
+        else:
+            assert got == 0, (name, got)
+        n += 1
+    assert n >= 35, n

@@ -109,44 +109,77 @@ def test_gpu_trade_cadences_and_small_lent_queue():
         gpu_trade(arrays, streams, lent_queue_cap=1)
 
 
+def run_ranks(world, port, case=None, timeout=900, **env_extra):
+    """tests/trade_2rank.py with `world` processes on device 0 over gloo; returns its stdout."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MCS_WORLD=str(world))
+    if case:
+        env["MCS_TRADE_CASE"] = case
+    env.update({k: str(v) for k, v in env_extra.items()})
+    r = subprocess.run([sys.executable, os.path.join(HERE, "trade_2rank.py")], env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
 @pytest.mark.parametrize("rk", ["1", "0"])
 def test_gpu_trade_two_ranks_one_gpu(rk):
     """world = 2 shards (two processes, two engines on device 0) exchanging records over gloo via
     the caller-driven phase API == one engine holding all clusters == the oracle; in both tick forms:
     the one-launch tick (MCS_TRADE_RK=1, loop_form 9: B/C/D of tick n + A of tick n + 1 per launch,
-    mcs_trade_rk.hip) and the three-kernel tick (MCS_TRADE_RK=0)."""
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29581" if rk == "1" else "29582",
-               MCS_TRADE_RK=rk, MCS_EXPECT_FORM="9" if rk == "1" else "0")
-    r = subprocess.run([sys.executable, os.path.join(HERE, "trade_2rank.py")], env=env, capture_output=True,
-                       text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert "TRADE-2RANK OK" in r.stdout
+    mcs_trade_rk.hip; agreed layout without snapshots) and the three-kernel tick (MCS_TRADE_RK=0,
+    whose blocks always carry them)."""
+    out = run_ranks(2, 29581 if rk == "1" else 29582, MCS_TRADE_RK=rk, MCS_EXPECT_FORM="9" if rk == "1" else "0",
+                    MCS_EXPECT_SNAPS="0" if rk == "1" else "1", timeout=600)
+    assert "TRADE-2RANK OK" in out
 
 
-@pytest.mark.parametrize("rk", ["1", "0"])
-def test_gpu_trade_four_ranks_one_gpu(rk):
+@pytest.mark.parametrize("rk,agree", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_gpu_trade_four_ranks_one_gpu(rk, agree):
     """world = 4 shards of a 64-cluster system (the C5 shape: 64 clusters, reduced jobs), four
     processes on device 0 exchanging blocks over gloo: rank offsets rank * blk beyond rank 1, the
-    replicated trader rounds and escalation on four ranks == the oracle of the whole system; both
-    tick forms (one launch per tick: loop_form 9; three kernels: 0)."""
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29585" if rk == "1" else "29586", MCS_WORLD="4",
-               MCS_TRADE_CASE="n64_hot:64:300", MCS_TRADE_RK=rk, MCS_EXPECT_FORM="9" if rk == "1" else "0")
-    r = subprocess.run([sys.executable, os.path.join(HERE, "trade_2rank.py")], env=env, capture_output=True,
-                       text=True, timeout=900)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert "TRADE-2RANK OK world 4" in r.stdout
+    replicated trader rounds and escalation on four ranks == the oracle of the whole system; the
+    one-launch tick (loop_form 9) on agreed blocks without snapshots (320 B per cluster + the tag)
+    and on per-rank blocks with them, and the three-kernel tick (0)."""
+    snaps = "0" if (rk == "1" and agree == "1") else "1"
+    out = run_ranks(4, {"11": 29585, "10": 29583, "01": 29586}[rk + agree], "n64_hot:64:300", MCS_TRADE_RK=rk,
+                    MCS_AGREE=agree, MCS_EXPECT_FORM="9" if rk == "1" else "0", MCS_EXPECT_SNAPS=snaps)
+    assert "TRADE-2RANK OK world 4" in out
+    assert f"snaps {snaps}, agreed {agree}" in out
 
 
-def test_gpu_trade_eight_ranks_one_gpu():
+@pytest.mark.parametrize("agree", ["1", "0"])
+def test_gpu_trade_eight_ranks_one_gpu(agree):
     """world = 8, the N = 8 shape of BASELINE config 5: eight shards of 8 clusters of one 64-cluster
     system, eight processes on device 0 exchanging blocks over gloo through the one-launch tick
-    (loop_form 9) == the oracle of the whole system."""
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29587", MCS_WORLD="8",
-               MCS_TRADE_CASE="n64_hot:64:300", MCS_TRADE_RK="1", MCS_EXPECT_FORM="9")
-    r = subprocess.run([sys.executable, os.path.join(HERE, "trade_2rank.py")], env=env, capture_output=True,
-                       text=True, timeout=900)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert "TRADE-2RANK OK world 8" in r.stdout
+    (loop_form 9) == the oracle of the whole system.  agree=1 is the exact block layout of an
+    8-GPU RCCL run (the ranks' shape agreed, no node above 64 cores: records + G tables only,
+    blocks at rank * blk with the small blk); agree=0 keeps the snapshot-carrying blocks."""
+    out = run_ranks(8, 29587 if agree == "1" else 29588, "n64_hot:64:300", MCS_TRADE_RK="1", MCS_AGREE=agree,
+                    MCS_EXPECT_FORM="9", MCS_EXPECT_SNAPS="0" if agree == "1" else "1")
+    assert "TRADE-2RANK OK world 8" in out
+    blk = int(out.split("blocks of ")[1].split(" B")[0])
+    # 8 clusters per rank: 8 x (64 B record + 256 B G table) + the 16-byte tag without snapshots;
+    # with them, 8 x 64 nodes x 8 B more
+    assert blk == 8 * 320 + 16 + (0 if agree == "1" else 8 * 64 * 8), blk
+
+
+@pytest.mark.parametrize("big,agree,form,snaps", [(100, "1", "9", "1"), (200, "1", "0", "1")])
+def test_gpu_trade_ranks_heterogeneous_agreed(big, agree, form, snaps):
+    """A shard that differs from the others: one rank holds a node of `big` cores.  At 100 cores its
+    lender can be "big", so the agreed blocks keep the snapshots on every rank; at 200 the slot
+    payload no longer packs, so the agreed form is the three-kernel tick on every rank.  Both ==
+    the oracle of the whole system (world 4)."""
+    out = run_ranks(4, 29589 if big == 100 else 29590, "n64_hot:32:300", MCS_BIG_NODE=big, MCS_AGREE=agree,
+                    MCS_EXPECT_FORM=form, MCS_EXPECT_SNAPS=snaps)
+    assert "TRADE-2RANK OK world 4" in out
+
+
+def test_gpu_trade_ranks_layout_mismatch_refused():
+    """Without an agreed shape, a rank with a 200-core node runs the three-kernel tick while the
+    others run the one-launch tick on equally sized blocks: phase 1 sees the other ranks' layout
+    tags and fails with MCS_E_INVALID on every rank instead of exchanging silently (world 4)."""
+    out = run_ranks(4, 29591, "n64_hot:32:300", MCS_BIG_NODE=200, MCS_AGREE="0", MCS_EXPECT_MISMATCH="1")
+    assert "TRADE-2RANK MISMATCH REFUSED world 4" in out
 
 
 @pytest.mark.parametrize("rk", ["1", "0"])

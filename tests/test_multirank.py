@@ -152,10 +152,32 @@ def test_run_lockstep_skips_empty_exchanges():
         return np.concatenate([buf, buf])  # two ranks
 
     eng = FakeEngine([96, 0, 0, 0], ticks=3)
-    assert run_lockstep(eng, allgather) == "stats"
+    assert run_lockstep(eng, allgather, agree=False) == "stats"
     assert gathered == [96] * 3
     assert eng.calls[1:5] == [(0, 0), (1, 192), (2, 0), (3, 0)]
     gathered.clear()
     eng = FakeEngine([8, 4, 12, 0], ticks=2)
-    run_lockstep(eng, allgather)
+    run_lockstep(eng, allgather, agree=False)
     assert gathered == [8, 4, 12] * 2
+
+
+def test_agree_shape_takes_the_max_over_ranks():
+    """agree_shape gathers every rank's layout words through the caller's transport and applies
+    their element-wise max (the RCCL loop's shape all-reduce, mcs_trade.cpp tr_agree_shape)."""
+    from mcs_amd.shard import agree_shape
+
+    class FakeEngine:
+        def trade_shape_words(self):
+            return np.array([64, 8, ~np.uint32(8), 0, 0, 0, 0, 0], np.uint32)
+
+        def trade_set_shape(self, w):
+            self.agreed = np.asarray(w, np.uint32)
+
+    other = np.array([256, 8, ~np.uint32(8), 1, 0, 64, 0, 0], np.uint32)
+
+    def allgather(buf):
+        return np.concatenate([buf, other.view(np.uint8)])
+
+    eng = FakeEngine()
+    agree_shape(eng, allgather)
+    assert eng.agreed.tolist() == [256, 8, int(~np.uint32(8)), 1, 0, 64, 0, 0]
