@@ -1,0 +1,41 @@
+"""Python legs of the rocprofv3 --runtime-trace exit-fault isolation.
+
+mode torch_nccl      torch alone: a world-1 'nccl' (RCCL) process group, one all_reduce, destroyed
+mode mcs_run_notorch libmcs alone (no torch import: /opt/rocm's RCCL), a world-1 communicator and a
+                     small C5-DELAY run through the RCCL tick loop, engine destroyed
+mode torch_mcs_run   the same after `import torch` (bench.py's order: torch's librccl is the one bound)
+Each prints "<mode> OK" and exits 0; the profiler's own exit decides the status seen by the caller."""
+import os
+import sys
+
+mode = sys.argv[1]
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(REPO, "multi-cluster-simulator_amd"), os.path.join(REPO, "tests")]
+
+if mode == "torch_nccl":
+    import torch
+    import torch.distributed as dist
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29655")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    t = torch.ones(1024, device="cuda")
+    dist.all_reduce(t)
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+else:
+    if mode == "torch_mcs_run":
+        import torch  # noqa: F401
+    from kat_util import seeded_workload
+    from mcs_amd import Engine
+
+    arrays, streams, _ = seeded_workload("small", 64, 200)
+    with Engine(0, policy="DELAY", trader=True) as eng:
+        eng.load_clusters(arrays)
+        eng.set_shard(0, 1)
+        eng.comm_init(Engine.comm_unique_id())
+        eng.submit_jobs(streams)
+        st = eng.run()
+        assert st.placed > 0
+print(mode, "OK", flush=True)
