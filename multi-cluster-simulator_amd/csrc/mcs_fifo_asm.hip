@@ -251,6 +251,211 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
 
 #define MCS_FA_LOOP(W, D) MCS_FA_ENTRY_S(W) MCS_FA_BODY(W, D, S) MCS_FA_EXIT_S
 
+// ---- W16L: W16R with a one-job lookahead (r06; form 22) -----------------------
+// Every pass also tests the NEXT job's request (s92, read one record ahead) against the nodes as they
+// stand before this pass's commit (SWEEP, v76-v79 / v82-v83 -> byte masks v87, lanes s[94:95]), and
+// picks its first fit s58 (kx = chunk * 64 + lane) at the end of the pass.  The next pass decides from
+// s58 without a fit test on its chain (the L pass) when nothing has changed since the sweep but the
+// commit of this pass: its node s59 (h) is then the only node whose fit may have changed, and it can
+// only have lost a fit, so s58 != h is the exact first fit (scheduler.go:127-139: every lower node
+// failed before and still fails; s58 itself is unchanged).  s58 == h (the next job's first fit is the
+// node just committed; also the "no lookahead" code, s58 := s59) runs the full pass: W16R's fit test
+// of the job, plus the sweep of the one after it.  A release (nodes gain) and a batch end (new
+// records) invalidate; an arrival advance without a release changes no node and keeps the lookahead.
+// The L pass commits with one indexed v_subrev (the job fits, so the packed halves do not borrow).
+//   s58 lookahead kx   s59 h   s92 next request   s[94:95] lanes where it fits   s96-s98 temps
+//   v76-v79 next diffs   v82-v83 next fit bits   v87 next byte masks
+#define MCS_FL_SWEEP_A                                                                            \
+    "v_pk_sub_u16 v76, v64, s92\n\t"                                                              \
+    "v_pk_sub_u16 v77, v65, s92\n\t"                                                              \
+    "v_pk_sub_u16 v78, v66, s92\n\t"                                                              \
+    "v_pk_sub_u16 v79, v67, s92\n\t"                                                              \
+    "v_and_b32_sdwa v82, v76, v76 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v83, v78, v78 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v82, v77, v77 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v83, v79, v79 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t"
+// (two instructions of the caller between A and B: the SDWA-preserve hazard of MCS_FA_FIT16)
+#define MCS_FL_SWEEP_B                                                                            \
+    "v_perm_b32 v87, v83, v82, s72\n\t"                                                           \
+    "v_cmp_ne_u32_e64 s[94:95], 0, v87\n\t"
+// the record at the cursor, and the next record's request (lane 64 wraps to lane 0: a batch end
+// invalidates whatever the last pass of the batch looked ahead at)
+#define MCS_FL_REC                                                                                \
+    "v_readlane_b32 s45, v94, s47\n\t"                                                            \
+    "v_readlane_b32 s46, v95, s47\n\t"                                                            \
+    "v_readlane_b32 s48, v96, s47\n\t"                                                            \
+    "s_add_u32 s97, s47, 1\n\t"                                                                   \
+    "s_and_b32 s97, s97, 63\n\t"                                                                  \
+    "v_readlane_b32 s92, v96, s97\n\t"
+// the L pass's decision: node s58 (lane s50), commit + slot insert in one register-index region
+#define MCS_FL_DECIDE                                                                             \
+    "s_ff1_i32_b64 s85, s[60:61]\n\t"                                                             \
+    "s_lshr_b32 s53, s58, 6\n\t"                                                                  \
+    "s_lshl_b64 exec, 1, s50\n\t"                                                                 \
+    "v_readlane_b32 s86, v117, s85\n\t" /* 0-7, or 8 with exec empty: in range either way */    \
+    "s_lshl2_add_u32 s87, s58, s73\n\t"                                                           \
+    "s_mov_b32 s54, s58\n\t"                                                                      \
+    "s_set_gpr_idx_on s53, gpr_idx(SRC1,DST)\n\t"                                                 \
+    "v_subrev_u32 v64, s48, v64\n\t" /* the commit (cluster.go:146-147) */                        \
+    "s_lshl_b64 s[62:63], 1, s85\n\t"                                                             \
+    "s_and_b64 exec, s[62:63], s[60:61]\n\t"                                                      \
+    "s_set_gpr_idx_idx s86\n\t"                                                                   \
+    "v_mov_b32 v32, s55\n\t"                                                                      \
+    "v_mov_b32 v40, s48\n\t"                                                                      \
+    "v_mov_b32 v48, s87\n\t"                                                                      \
+    "s_set_gpr_idx_off\n\t"                                                                       \
+    "s_lshl_b32 s76, 1, s86\n\t"                                                                  \
+    "v_xor_b32 v89, s76, v89\n\t"
+
+#define MCS_FL_ENTRY                                                                              \
+    "s_mov_b32 s58, -1\n\t"                                                                       \
+    "s_mov_b32 s59, -1\n\t" MCS_FA_ENTRY_S(16R)
+// (MCS_FA_ENTRY_S(16R) ends with MCS_FA_REC16R: the entry's first pass is a full pass, which needs
+// only the cursor's record; the next request is read here, before the first sweep)
+#define MCS_FL_BODY(D)                                                                            \
+    "mcsfl_first_%=:\n\t"                                                                         \
+    "s_add_u32 s97, s47, 1\n\t"                                                                   \
+    "s_and_b32 s97, s97, 63\n\t"                                                                  \
+    "v_readlane_b32 s92, v96, s97\n"                                                              \
+    "mcsfa_inner_%=:\n\t"                                                                         \
+    "s_cmp_gt_u32 s45, s40\n\t" /* ready head not arrived: sleep to it */                         \
+    "s_cbranch_scc1 mcsfa_arrive_%=\n\t"                                                          \
+    "s_cmp_eq_u32 s58, s59\n\t" /* no usable lookahead: the full pass */                          \
+    "s_cbranch_scc1 mcsfl_full_%=\n\t"                                                            \
+    /* ---- L pass: the job's first fit is s58 ---- */                                            \
+    MCS_FL_SWEEP_A                                                                                \
+    "v_cmp_lt_u32_e64 s[60:61], s49, v89\n\t" /* the insert's lanes with a free row */           \
+    "v_ffbl_b32 v117, v89\n\t"                                                                    \
+    MCS_FL_SWEEP_B                                                                                \
+    "s_add_u32 s55, s40, s46\n\t"                                                                 \
+    "s_and_b32 s50, s58, 63\n\t"                                                                  \
+    "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfl_lzero_%=\n\t" MCS_FL_DECIDE                                             \
+    "s_branch mcsfl_common_%=\n"                                                                  \
+    "mcsfl_lzero_%=:\n\t"                                                                         \
+    "s_mov_b32 m0, s47\n\t"                                                                       \
+    "s_mov_b32 s54, s58\n\t"                                                                      \
+    "v_writelane_b32 v91, s54, m0\n\t"                                                            \
+    "v_writelane_b32 v92, s40, m0\n\t"                                                            \
+    "s_branch mcsfl_pick_%=\n"                                                                    \
+    /* ---- full pass: W16R's fit test of the job, the sweep of the next one ---- */              \
+    "mcsfl_full_%=:\n\t" MCS_FA_FIT16 MCS_FL_SWEEP_A MCS_FA_ANYFIT                                \
+    "s_add_u32 s55, s40, s46\n\t" MCS_FL_SWEEP_B                                                  \
+    "s_cbranch_vccz mcsfa_nofit_%=\n\t"                                                           \
+    "s_ff1_i32_b64 s50, vcc\n\t" /* lowest lane with a fit */                                     \
+    "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
+    "s_cbranch_scc1 mcsfa_zero_%=\n\t" MCS_FA_DECIDE16R                                           \
+    "mcsfl_common_%=:\n\t"                                                                        \
+    "s_mov_b32 s59, s54\n\t" /* h: the node this pass committed */                                \
+    "s_min_u32 s77, s77, s55\n\t" /* the wave's earliest finish */                                \
+    "s_mov_b64 exec, -1\n\t"                                                                      \
+    "s_mov_b32 m0, s47\n\t"                                                                       \
+    "s_add_u32 s80, s80, 1\n\t"                                                                   \
+    "v_writelane_b32 v91, s54, m0\n\t"                                                            \
+    "v_writelane_b32 v92, s40, m0\n"                                                              \
+    /* the next job's first fit before this commit (none: the next pass is a full one) */         \
+    "mcsfl_pick_%=:\n\t"                                                                          \
+    "s_mov_b32 s58, s59\n\t"                                                                      \
+    "s_cmp_lg_u64 s[94:95], 0\n\t"                                                                \
+    "s_cbranch_scc0 mcsfa_placed_%=\n\t"                                                          \
+    "s_ff1_i32_b64 s96, s[94:95]\n\t"                                                             \
+    "v_readlane_b32 s98, v87, s96\n\t"                                                            \
+    "s_add_u32 s47, s47, 1\n\t" MCS_FL_REC                                                        \
+    "s_ff1_i32_b32 s98, s98\n\t"                                                                  \
+    "s_lshl3_add_u32 s58, s98, s96\n"                                                             \
+    "mcsfa_loopend_%=:\n\t"                                                                       \
+    "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_inner_%=\n\t"                                                           \
+    "s_cmp_lg_u32 s43, 0\n\t"                                                                     \
+    "s_cbranch_scc0 mcsfa_bend_%=\n\t"                                                            \
+    "s_sub_u32 s41, s42, s57\n\t"                                                                 \
+    "s_min_u32 s41, s41, 64\n\t"                                                                  \
+    "s_mov_b32 s43, 0\n\t"                                                                        \
+    "s_add_u32 s40, s40, 1\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_clkovf_%=\n\t"                                                          \
+    "s_branch mcsfa_adv_%=\n"                                                                     \
+                                                                                                  \
+    /* a pass whose next job fits no node (before the commit, so none after it either) */        \
+    "mcsfa_placed_%=:\n\t"                                                                        \
+    "s_add_u32 s47, s47, 1\n\t" MCS_FL_REC                                                        \
+    "s_branch mcsfa_loopend_%=\n"                                                                 \
+                                                                                                  \
+    "mcsfa_zero_%=:\n\t" MCS_FA_ZEROKX16R                                                        \
+    "v_writelane_b32 v91, s54, m0\n\t"                                                            \
+    "v_writelane_b32 v92, s40, m0\n\t"                                                            \
+    "s_branch mcsfl_pick_%=\n"                                                                    \
+                                                                                                  \
+    "mcsfa_arrive_%=:\n\t"                                                                        \
+    "s_mov_b32 s40, s45\n\t"                                                                      \
+    MCS_FA_CNTS_##D                                                                               \
+    "s_branch mcsfa_adv_%=\n"                                                                     \
+                                                                                                  \
+    "mcsfa_nofit_%=:\n\t"                                                                         \
+    "s_sub_u32 s76, 1, s43\n\t"                                                                   \
+    "s_add_u32 s82, s82, s76\n\t"                                                                 \
+    "s_mov_b32 s43, 1\n\t"                                                                        \
+    "s_add_u32 s41, s47, 1\n\t"                                                                   \
+    MCS_FA_CNTS_##D                                                                               \
+    "s_add_u32 s78, s78, 1\n\t"                                                                   \
+    "s_cmp_gt_u32 s78, s79\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_poolovf_%=\n\t"                                                         \
+    "s_cmp_eq_u32 s77, -1\n\t"                                                                    \
+    "s_cbranch_scc1 mcsfa_deadlock_%=\n\t"                                                        \
+    "s_add_u32 s40, s40, 1\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_clkovf_%=\n\t"                                                          \
+    "s_max_u32 s40, s40, s77\n"                                                                   \
+    "mcsfa_adv_%=:\n\t"                                                                           \
+    "s_cmp_lt_u32 s40, s77\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_loopend_%=\n\t"                                                         \
+    MCS_FA_CNTR_##D                                                                               \
+    "s_max_u32 s81, s81, s80\n\t"                                                                 \
+    "s_mov_b32 s58, s59\n\t" /* a release: the lookahead is void */                               \
+    "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN16R MCS_FA_SCANEND16R                                  \
+    "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_inner_%=\n\t"                                                           \
+    "s_branch mcsfa_loopend_%=\n" MCS_FA_RBODY16R                                                 \
+                                                                                                  \
+    "mcsfa_deadlock_%=:\n\t"                                                                      \
+    "s_or_b32 s44, s44, %[fdl]\n\t"                                                               \
+    "s_branch mcsfa_exit_%=\n"                                                                    \
+    "mcsfa_clkovf_%=:\n\t"                                                                        \
+    "s_mov_b32 s40, -1\n\t"                                                                       \
+    "s_or_b32 s44, s44, %[fck]\n\t"                                                               \
+    "s_branch mcsfa_exit_%=\n"                                                                    \
+    "mcsfa_poolovf_%=:\n\t"                                                                       \
+    "s_or_b32 s44, s44, %[fov]\n\t"                                                               \
+    "s_branch mcsfa_exit_%=\n"                                                                    \
+                                                                                                  \
+    "mcsfa_bend_%=:\n\t"                                                                          \
+    "s_max_u32 s81, s81, s80\n\t"                                                                 \
+    "s_cmp_gt_u32 s81, 64*8\n\t"                                                                  \
+    "s_cbranch_scc1 mcsfa_poolovf_%=\n\t"                                                         \
+    "s_add_u32 s76, s57, s47\n\t"                                                                 \
+    "s_cmp_ge_u32 s76, s42\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_exit_%=\n\t"                                                            \
+    "s_waitcnt vmcnt(0)\n\t"                                                                      \
+    "v_add_u32 v125, s57, v110\n\t"                                                               \
+    "v_lshlrev_b32 v125, 2, v125\n\t" MCS_FA_NODEIDX                                              \
+    "global_store_dword v125, v126, s[66:67] nt\n\t"                                              \
+    "global_store_dword v125, v92, s[68:69] nt\n\t"                                               \
+    "v_add_u32 v93, v92, v95\n\t"                                                                 \
+    "global_store_dword v125, v93, s[70:71] nt\n\t"                                               \
+    "s_add_u32 s57, s57, 64\n\t" MCS_FA_PRIO("mcsfa_") MCS_FA_TAKE16                              \
+    "v_add_u32 v121, s57, v110\n\t"                                                               \
+    "v_lshlrev_b32 v121, 4, v121\n\t"                                                             \
+    "v_add_u32 v121, 0x400, v121\n\t"                                                             \
+    "global_load_dwordx4 v[98:101], v121, s[64:65]\n\t"                                           \
+    "s_sub_u32 s41, s42, s57\n\t"                                                                 \
+    "s_min_u32 s41, s41, 64\n\t"                                                                  \
+    "s_mov_b32 s47, 0\n\t"                                                                        \
+    "s_mov_b32 s58, s59\n\t" /* new records: the lookahead is void */                            \
+    MCS_FL_REC                                                                                    \
+    "s_branch mcsfa_inner_%=\n"
+#define MCS_FL_LOOP(D) MCS_FL_ENTRY MCS_FL_BODY(D) MCS_FA_EXIT_S
+// the lookahead loop's clobbers: W16R's plus its own (no probe build of this form: MCS_STAMPS uses
+// s92-s99 for its segment clocks)
+#define MCS_FL_CLOBBERS MCS_FA_CLOBBERS, "s92", "s93", "s94", "s95", "s96", "s97", "s98"
+
 // ---- the loop with the job stream synthesised in the kernel (mcs_gen_params.fused) ---------------
 // The statement runs one batch of records and ends at its batch end with s59 = 1 (or at the end of
 // the cluster with s59 = 0); the kernel then generates the next batch (GenStream, mcs_gen_dev.h)
@@ -362,9 +567,11 @@ __device__ __forceinline__ void fa_finish(const FifoArgs& a, uint32_t ci, uint32
 // (NPL nodes per lane, P slot rows: 4/8 for 129-256 node clusters, 1/2 for at most 64 nodes)
 // (DIAG: count the passes without a decision and the release scans into mcs_cluster_stats; the
 // production launches skip them, 1.6 % of the C4 loop)
-template <int W, bool RS, int NPL, int P, bool DIAG>
+// (LOOK: the W16L lookahead loop, W16R's shape only)
+template <int W, bool RS, int NPL, int P, bool DIAG, bool LOOK = false>
 __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
     static_assert(W == 16 || !RS, "register slots: 16-bit node format only");
+    static_assert(!LOOK || (W == 16 && RS && NPL == 4 && P == 8), "lookahead: the W16R shape");
     static_assert((NPL == 4 && P == 8) || (NPL == 1 && P == 2 && W == 16 && RS), "loop shapes");
     const uint32_t item = blockIdx.x;
     const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
@@ -429,7 +636,7 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
-#define MCS_FA_OPERANDS                                                                           \
+#define MCS_FA_OPERANDS_IO                                                                        \
     : [t] "+s"(t), [r] "+s"(r), [flags] "+s"(flags), [hw] "+s"(have_w), [used] "+s"(used),      \
       [peak] "+s"(peak), [waited] "+s"(waited), [nslow] "+s"(n_slow), [nrel] "+s"(n_rel),       \
       [on] "+v"(on), [os] "+v"(os), [of] "+v"(of), [frm] "+v"(frm), [lmin] "+v"(lmin)            \
@@ -438,9 +645,15 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
       [c0] "v"(cur.x), [c1] "v"(cur.y), [c2] "v"(cur.z), [c3] "v"(cur.w), [pay] "v"(v_pay),     \
       [nb] "v"(v_nb), [nbase] "v"(v_nbase), [lane] "v"(lane), [sel0] "s"(sel0),                 \
       [sel1] "s"(sel1), [fdl] "i"(MCS_FLAG_DEADLOCK), [fck] "i"(MCS_FLAG_CLOCK_OVERFLOW),        \
-      [fov] "i"(MCS_FLAG_OVERFLOW)                                                              \
-    : MCS_FA_CLOBBERS
-    if constexpr (W == 32)
+      [fov] "i"(MCS_FLAG_OVERFLOW)
+#define MCS_FA_OPERANDS MCS_FA_OPERANDS_IO : MCS_FA_CLOBBERS
+#define MCS_FL_OPERANDS MCS_FA_OPERANDS_IO : MCS_FL_CLOBBERS
+    if constexpr (LOOK) {
+#ifndef MCS_STAMPS
+        if constexpr (DIAG) asm volatile(MCS_FL_LOOP(D1) MCS_FL_OPERANDS);
+        else asm volatile(MCS_FL_LOOP(D0) MCS_FL_OPERANDS);
+#endif
+    } else if constexpr (W == 32)
         if constexpr (DIAG) asm volatile(MCS_FA_LOOP(32, D1) MCS_FA_OPERANDS);
         else asm volatile(MCS_FA_LOOP(32, D0) MCS_FA_OPERANDS);
     else if constexpr (NPL == 1)
@@ -453,6 +666,8 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
         if constexpr (DIAG) asm volatile(MCS_FA_LOOP(16, D1) MCS_FA_OPERANDS);
         else asm volatile(MCS_FA_LOOP(16, D0) MCS_FA_OPERANDS);
 #undef MCS_FA_OPERANDS
+#undef MCS_FL_OPERANDS
+#undef MCS_FA_OPERANDS_IO
 #pragma clang diagnostic pop
 
 #ifdef MCS_STAMPS
@@ -704,7 +919,7 @@ __global__ __launch_bounds__(2 * kWave) void fifo_duo_kernel(FifoArgs a) {
 
 }  // namespace
 
-// Form codes: 21 = W16R's duo loop (a decision and a release wave per cluster, small grids),
+// Form codes: 22 = W16R's one-job lookahead loop (W16L), 21 = W16R's duo loop (a decision and a release wave per cluster, small grids),
 // 17 = W16R and 18 = W16S (where the 16-bit format fits), 16 = W16 with LDS slots,
 // 32 = W32, 19 / 20 = W16R / W16S on a fused job stream, 0 = the compiled kernel.  MCS_FIFO_ASM=0
 // turns the hand-scheduled loop off, =16 / =32 force a form (A/B timing, the variant tests; neither
@@ -732,7 +947,12 @@ int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor) {
         // release wave takes an otherwise idle SIMD; MCS_FIFO_DUO=0|1 forces either
         const char* duo = getenv("MCS_FIFO_DUO");
         const bool d = duo ? atoi(duo) != 0 : a.n_items <= kDuoMaxItems;
-        return d ? 21 : 17;
+        if (d) return 21;
+        // the one-job lookahead loop (W16L) for grids of at most kLookMaxItems clusters (one cluster
+        // wave per SIMD and fewer); MCS_FIFO_LOOK=0|1 forces either
+        const char* look = getenv("MCS_FIFO_LOOK");
+        const bool l = look ? atoi(look) != 0 : a.n_items <= kLookMaxItems;
+        return l ? 22 : 17;
     }
     return (a.guard_ok & 1u) ? 32 : 0;
 }
@@ -749,6 +969,9 @@ static hipError_t launch_form(const FifoArgs& a, int form, hipStream_t s) {
         case 18: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 1, 2, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 21: hipLaunchKernelGGL((fifo_duo_kernel<DIAG>), dim3(a.n_items), dim3(2 * kWave), 0, s, a); break;
         case 17: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
+#ifndef MCS_STAMPS
+        case 22: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 4, 8, DIAG, true>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
+#endif
         case 16: hipLaunchKernelGGL((fifo_asm_kernel<16, false, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 32: hipLaunchKernelGGL((fifo_asm_kernel<32, false, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         default: return hipErrorInvalidValue;

@@ -21,13 +21,23 @@ KATS = load_kats()
 
 W16R = "mcs::fifo_asm_kernel<16, true, 4, 8>"
 DUO = "mcs::fifo_duo_kernel"
+LOOK = "mcs::fifo_asm_kernel<16, true, 4, 8, look>"
 
 
 def w16r_form(n_clusters):
     """The kernel the engine picks for a streamed 129-256-node launch of n_clusters in the 16-bit
-    format: W16R, or the duo loop (a decision and a release wave per cluster) under MCS_FIFO_DUO=1
-    (no grid picks it by default: kDuoMaxItems = 0)."""
-    return DUO if os.environ.get("MCS_FIFO_DUO") == "1" else W16R
+    format: W16R, the duo loop (a decision and a release wave per cluster) under MCS_FIFO_DUO=1, or
+    the one-job lookahead loop W16L under MCS_FIFO_LOOK=1 (no grid picks either by default:
+    kDuoMaxItems = kLookMaxItems = 0)."""
+    if os.environ.get("MCS_FIFO_DUO") == "1":
+        return DUO
+    return LOOK if os.environ.get("MCS_FIFO_LOOK") == "1" else W16R
+
+
+def set_form(monkeypatch, form):
+    """form: "0" W16R, "1" the duo loop, "look" the lookahead loop (the parametrisations below)."""
+    monkeypatch.setenv("MCS_FIFO_DUO", "1" if form == "1" else "0")
+    monkeypatch.setenv("MCS_FIFO_LOOK", "1" if form == "look" else "0")
 
 def run_engine(eng, arrays, streams):
     eng.load_clusters(arrays)
@@ -157,12 +167,38 @@ def test_config3_small_replicas(engine):
     assert_parity(arrays, streams, node, start, fin, cs)
 
 
+@pytest.mark.parametrize("form", ["0", "look"])
 @pytest.mark.parametrize("kind", ["n256", "n256_hot"])
-def test_config4_shape_reduced(engine, kind):
-    """BASELINE config 4 shape (256 nodes, scaled arrivals) at 128 clusters x 6k jobs."""
+def test_config4_shape_reduced(engine, kind, form, monkeypatch):
+    """BASELINE config 4 shape (256 nodes, scaled arrivals) at 128 clusters x 6k jobs (W16R and the
+    lookahead loop)."""
+    set_form(monkeypatch, form)
     arrays, streams, _ = seeded_workload(kind, 128, 6000)
     node, start, fin, st, cs = run_engine(engine, arrays, streams)
+    assert engine.last_kernel == w16r_form(128)
     assert_parity(arrays, streams, node, start, fin, cs)
+
+
+def test_config4_strong_shard_512_lookahead(monkeypatch):
+    """The strong shard an 8-GPU node runs (512 of C4's 4096 clusters, full streams) through the
+    lookahead loop: every cluster bit-exact against the oracle."""
+    from mcs_amd.engine import scaled_lambda
+
+    monkeypatch.setenv("MCS_FIFO_LOOK", "1")
+    n, J = 512, 16384
+    arrays = replicate(uniform_cluster(256), n)
+    gp = GenParams(seed=0x4D43535F53494D31, arrival_mode=1, lam=scaled_lambda(256, load=0.9))
+    with Engine(0) as eng:
+        eng.load_clusters(arrays)
+        eng.set_shard(3, 8)  # rank 3 of 8: global clusters 1536..2047
+        eng.generate_jobs(gp, J)
+        st = eng.run()
+        assert eng.last_kernel == LOOK
+        assert st.placed == n * J
+        node, start, fin = eng.placements()
+        jobs = eng.read_jobs()
+        cs = eng.cluster_stats()
+    assert_parity(arrays, jobs, node, start, fin, cs, n_threads=16)
 
 
 def test_config4_full_size_parity(engine):
@@ -279,7 +315,7 @@ def test_heterogeneous_cluster_sizes(engine):
 
 @pytest.mark.parametrize("sizes", [[0, 1, 5, 63, 64, 65, 130, 200, 256], [0, 1, 2, 5, 33, 63, 64]],
                          ids=["asm_4x8", "asm_1x2"])
-@pytest.mark.parametrize("duo", ["0", "1"])
+@pytest.mark.parametrize("duo", ["0", "1", "look"])
 def test_heterogeneous_cluster_sizes_hand_scheduled(engine, sizes, duo, monkeypatch):
     """Clusters of many sizes in one launch of each hand-scheduled loop shape (the largest picks it:
     129-256 nodes -> 4 chunks x 8 slot rows, <= 64 nodes -> 1 chunk x 2 rows): padding nodes, an
@@ -303,7 +339,7 @@ def test_heterogeneous_cluster_sizes_hand_scheduled(engine, sizes, duo, monkeypa
     arrays = pack_clusters(clusters)
     off = np.arange(len(parts) + 1, dtype=np.uint64) * J
     s = JobStreams(*(np.concatenate([p[f] for p in parts]) for f in range(4)), off)
-    monkeypatch.setenv("MCS_FIFO_DUO", duo)
+    set_form(monkeypatch, duo)
     node, start, fin, st, cs = run_engine(engine, arrays, s)
     if max(sizes) > 64:
         assert engine.last_kernel == w16r_form(len(sizes))
@@ -313,12 +349,12 @@ def test_heterogeneous_cluster_sizes_hand_scheduled(engine, sizes, duo, monkeypa
     assert cs[0]["flags"] & L.MCS_FLAG_DEADLOCK  # zero nodes: the first job never fits
 
 
-@pytest.mark.parametrize("nodes,duo", [(256, "0"), (256, "1"), (5, "0")])
+@pytest.mark.parametrize("nodes,duo", [(256, "0"), (256, "1"), (256, "look"), (5, "0")])
 def test_hand_scheduled_diag_build(nodes, duo, monkeypatch):
     """MCS_FIFO_DIAG=1 launches the counting build of the hand-scheduled loop: the same placements
     and per-cluster results, plus the pass and release-scan counters (which the production build
     leaves at the decision count and 0)."""
-    monkeypatch.setenv("MCS_FIFO_DUO", duo)
+    set_form(monkeypatch, duo)
     arrays, streams, _ = seeded_workload("n256" if nodes == 256 else "small", 64, 3000)
     res = {}
     for diag in ("0", "1"):
@@ -339,7 +375,7 @@ def test_hand_scheduled_diag_build(nodes, duo, monkeypatch):
     assert_parity(arrays, streams, *res["1"][:3], c1)
 
 
-@pytest.mark.parametrize("shape", ["w16s", "w16r", "duo", "w32"])
+@pytest.mark.parametrize("shape", ["w16s", "w16r", "duo", "look", "w32"])
 @pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6])
 def test_hand_scheduled_fuzz(engine, shape, seed, monkeypatch):
     """Randomised clusters and streams through each hand-scheduled loop form, bit-exact against the
@@ -347,10 +383,10 @@ def test_hand_scheduled_fuzz(engine, shape, seed, monkeypatch):
     availability, bursts of simultaneous arrivals, zero-duration and zero-resource jobs, requests
     equal to a node's free value, and one request per cluster that fits no node (a head-of-line
     deadlock at a random point of the stream)."""
-    monkeypatch.setenv("MCS_FIFO_DUO", "1" if shape == "duo" else "0")
-    arrays, s = fuzz_workload("w16r" if shape == "duo" else shape, seed)
+    set_form(monkeypatch, {"duo": "1", "look": "look"}.get(shape, "0"))
+    arrays, s = fuzz_workload("w16r" if shape in ("duo", "look") else shape, seed)
     node, start, fin, st, cs = run_engine(engine, arrays, s)
-    want = {"w16s": "mcs::fifo_asm_kernel<16, true, 1, 2>", "w16r": W16R, "duo": DUO,
+    want = {"w16s": "mcs::fifo_asm_kernel<16, true, 1, 2>", "w16r": W16R, "duo": DUO, "look": LOOK,
             "w32": "mcs::fifo_asm_kernel<32, false, 4, 8>"}[shape]
     if st.escalations == 0:
         assert engine.last_kernel == want
@@ -488,13 +524,15 @@ def test_every_kernel_variant(policy):
             # MCS_FIFO_LAT forces either)
             # (and the duo loop, MCS_FIFO_DUO=1, the register-slot form's two-wave variant)
             for fused, lat, asm, duo in ((False, "1", "0", None), (False, "0", "0", None), (False, None, "1", "0"),
-                                         (False, None, "1", "1"), (False, None, "16", None),
-                                         (False, None, "32", None), (True, None, None, None)):
+                                         (False, None, "1", "1"), (False, None, "1", "look"),
+                                         (False, None, "16", None), (False, None, "32", None),
+                                         (True, None, None, None)):
                 if policy == "DELAY" and lat == "0":
                     continue
                 if policy == "DELAY" and asm in ("1", "16", "32"):
                     continue
-                env = {"MCS_FIFO_LAT": lat, "MCS_FIFO_ASM": asm, "MCS_FIFO_DUO": duo}
+                env = {"MCS_FIFO_LAT": lat, "MCS_FIFO_ASM": asm, "MCS_FIFO_DUO": "0" if duo == "look" else duo,
+                       "MCS_FIFO_LOOK": "1" if duo == "look" else None}
                 old = {k: os.environ.get(k) for k in env}
                 for k, v in env.items():
                     if v is not None:

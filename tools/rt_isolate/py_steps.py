@@ -4,6 +4,8 @@ mode torch_nccl      torch alone: a world-1 'nccl' (RCCL) process group, one all
 mode mcs_run_notorch libmcs alone (no torch import: /opt/rocm's RCCL), a world-1 communicator and a
                      small C5-DELAY run through the RCCL tick loop, engine destroyed
 mode torch_mcs_run   the same after `import torch` (bench.py's order: torch's librccl is the one bound)
+mode torch_cuda_mcs_run  the same after torch has initialised the device (a CUDA tensor and a synchronize,
+                     as bench.py's barrier does)
 Each prints "<mode> OK" and exits 0; the profiler's own exit decides the status seen by the caller."""
 import os
 import sys
@@ -25,8 +27,11 @@ if mode == "torch_nccl":
     torch.cuda.synchronize()
     dist.destroy_process_group()
 else:
-    if mode == "torch_mcs_run":
-        import torch  # noqa: F401
+    if mode in ("torch_mcs_run", "torch_cuda_mcs_run"):
+        import torch
+        if mode == "torch_cuda_mcs_run":
+            x = torch.ones(1024, device="cuda")
+            torch.cuda.synchronize()
     from kat_util import seeded_workload
     from mcs_amd import Engine
 
