@@ -253,18 +253,24 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
 
 // ---- W16L: W16R with a one-job lookahead (r06; form 22) -----------------------
 // Every pass also tests the NEXT job's request (s92, read one record ahead) against the nodes as they
-// stand before this pass's commit (SWEEP, v76-v79 / v82-v83 -> byte masks v87, lanes s[94:95]), and
-// picks its first fit s58 (kx = chunk * 64 + lane) at the end of the pass.  The next pass decides from
-// s58 without a fit test on its chain (the L pass) when nothing has changed since the sweep but the
-// commit of this pass: its node s59 (h) is then the only node whose fit may have changed, and it can
-// only have lost a fit, so s58 != h is the exact first fit (scheduler.go:127-139: every lower node
-// failed before and still fails; s58 itself is unchanged).  s58 == h (the next job's first fit is the
-// node just committed; also the "no lookahead" code, s58 := s59) runs the full pass: W16R's fit test
-// of the job, plus the sweep of the one after it.  A release (nodes gain) and a batch end (new
-// records) invalidate; an arrival advance without a release changes no node and keeps the lookahead.
-// The L pass commits with one indexed v_subrev (the job fits, so the packed halves do not borrow).
+// stand before this pass's commit (v76-v79 / v82-v83 -> byte masks v87, lanes s[94:95]), and picks
+// its first fit s58 (kx = chunk * 64 + lane) at the end of the pass.  The next pass decides from s58
+// without a fit test on its chain (the L pass) when nothing has changed since that test but this
+// pass's commit: its node s59 (h) is then the only node whose fit may have changed, and it can only
+// have lost one, so s58 != h is the exact first fit (scheduler.go:127-139: every lower node failed
+// before and still fails; s58 itself is unchanged).  s58 == h (the next job's first fit is the node
+// just committed; also the "no lookahead" code, s58 := s59) runs the full pass (F): W16R's fit test
+// of the job interleaved with the next one's.  A release (nodes gain) and a batch end (new records)
+// invalidate; an arrival advance without a release changes no node and keeps the lookahead.
+// The insert's slot (lowest lane with a free row: s85, its row s86, exec mask s[62:63]) is picked at
+// the end of the pass that changed the free rows (and after a release), off the next decision's chain.
+// Each pass type ends with its own copy of the tail, so a pass takes one taken branch, to the next
+// pass of either type.  The L pass commits with one indexed v_subrev (the job fits: the packed
+// halves do not borrow).
 //   s58 lookahead kx   s59 h   s92 next request   s[94:95] lanes where it fits   s96-s98 temps
 //   v76-v79 next diffs   v82-v83 next fit bits   v87 next byte masks
+// (r06 A/B against W16R, profiles/r06_look/: the first form, with the insert's slot on the chain and
+// two taken branches per pass, measured 6.44 vs 4.96 ms at 512 clusters)
 #define MCS_FL_SWEEP_A                                                                            \
     "v_pk_sub_u16 v76, v64, s92\n\t"                                                              \
     "v_pk_sub_u16 v77, v65, s92\n\t"                                                              \
@@ -278,6 +284,30 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
 #define MCS_FL_SWEEP_B                                                                            \
     "v_perm_b32 v87, v83, v82, s72\n\t"                                                           \
     "v_cmp_ne_u32_e64 s[94:95], 0, v87\n\t"
+// the F pass's two fit tests (the job's: v72-v75 -> v80/v81 -> v86 and vcc; the next one's),
+// interleaved so that each SDWA-preserve write has two instructions before its reader
+#define MCS_FL_FIT2                                                                               \
+    "v_pk_sub_u16 v72, v64, s48\n\t"                                                              \
+    "v_pk_sub_u16 v73, v65, s48\n\t"                                                              \
+    "v_pk_sub_u16 v74, v66, s48\n\t"                                                              \
+    "v_pk_sub_u16 v75, v67, s48\n\t"                                                              \
+    "v_pk_sub_u16 v76, v64, s92\n\t"                                                              \
+    "v_pk_sub_u16 v77, v65, s92\n\t"                                                              \
+    "v_pk_sub_u16 v78, v66, s92\n\t"                                                              \
+    "v_pk_sub_u16 v79, v67, s92\n\t"                                                              \
+    "v_and_b32_sdwa v80, v72, v72 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v81, v74, v74 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v82, v76, v76 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v83, v78, v78 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v80, v73, v73 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v81, v75, v75 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v82, v77, v77 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_and_b32_sdwa v83, v79, v79 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
+    "v_perm_b32 v86, v81, v80, s72\n\t"                                                           \
+    "v_cmp_ne_u32_e32 vcc, 0, v86\n\t"                                                            \
+    "v_perm_b32 v87, v83, v82, s72\n\t"                                                           \
+    "s_add_u32 s55, s40, s46\n\t"                                                                 \
+    "v_cmp_ne_u32_e64 s[94:95], 0, v87\n\t"
 // the record at the cursor, and the next record's request (lane 64 wraps to lane 0: a batch end
 // invalidates whatever the last pass of the batch looked ahead at)
 #define MCS_FL_REC                                                                                \
@@ -287,18 +317,25 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     "s_add_u32 s97, s47, 1\n\t"                                                                   \
     "s_and_b32 s97, s97, 63\n\t"                                                                  \
     "v_readlane_b32 s92, v96, s97\n\t"
-// the L pass's decision: node s58 (lane s50), commit + slot insert in one register-index region
-#define MCS_FL_DECIDE                                                                             \
+// the next insert's slot from the free rows v89 (exec = the full wave): the vector half, then the
+// scalar half a few instructions later (pool full: s[62:63] empty, s86 = 8, as MCS_FA_DECIDE16R)
+#define MCS_FL_INSPICK_V                                                                          \
+    "v_cmp_lt_u32_e64 s[60:61], s49, v89\n\t"                                                    \
+    "v_ffbl_b32 v117, v89\n\t"
+#define MCS_FL_INSPICK_S                                                                          \
     "s_ff1_i32_b64 s85, s[60:61]\n\t"                                                             \
+    "v_readlane_b32 s86, v117, s85\n\t"                                                           \
+    "s_lshl_b64 s[62:63], 1, s85\n\t"                                                             \
+    "s_and_b64 s[62:63], s[62:63], s[60:61]\n\t"
+// the L pass's decision: node s58 (lane s50); commit + slot insert in one register-index region
+#define MCS_FL_DECIDE_L                                                                           \
     "s_lshr_b32 s53, s58, 6\n\t"                                                                  \
     "s_lshl_b64 exec, 1, s50\n\t"                                                                 \
-    "v_readlane_b32 s86, v117, s85\n\t" /* 0-7, or 8 with exec empty: in range either way */    \
     "s_lshl2_add_u32 s87, s58, s73\n\t"                                                           \
     "s_mov_b32 s54, s58\n\t"                                                                      \
     "s_set_gpr_idx_on s53, gpr_idx(SRC1,DST)\n\t"                                                 \
     "v_subrev_u32 v64, s48, v64\n\t" /* the commit (cluster.go:146-147) */                        \
-    "s_lshl_b64 s[62:63], 1, s85\n\t"                                                             \
-    "s_and_b64 exec, s[62:63], s[60:61]\n\t"                                                      \
+    "s_mov_b64 exec, s[62:63]\n\t"                                                                \
     "s_set_gpr_idx_idx s86\n\t"                                                                   \
     "v_mov_b32 v32, s55\n\t"                                                                      \
     "v_mov_b32 v40, s48\n\t"                                                                      \
@@ -306,66 +343,126 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     "s_set_gpr_idx_off\n\t"                                                                       \
     "s_lshl_b32 s76, 1, s86\n\t"                                                                  \
     "v_xor_b32 v89, s76, v89\n\t"
+// the F pass's decision: MCS_FA_DECIDE16R with the insert's slot already picked
+#define MCS_FL_DECIDE_F                                                                           \
+    "v_readlane_b32 s51, v86, s50\n\t"                                                            \
+    "s_lshl_b64 exec, 1, s50\n\t"                                                                 \
+    "s_ff1_i32_b32 s52, s51\n\t"                                                                  \
+    "s_lshr_b32 s53, s52, 3\n\t"                                                                  \
+    "s_lshl3_add_u32 s54, s52, s50\n\t"                                                           \
+    "s_set_gpr_idx_on s53, gpr_idx(SRC0,DST)\n\t"                                                 \
+    "v_mov_b32 v64, v72\n\t" /* the commit (cluster.go:146-147) */                                \
+    "s_mov_b64 exec, s[62:63]\n\t"                                                                \
+    "s_lshl2_add_u32 s87, s54, s73\n\t"                                                           \
+    "s_set_gpr_idx_idx s86\n\t"                                                                   \
+    "v_mov_b32 v32, s55\n\t"                                                                      \
+    "v_mov_b32 v40, s48\n\t"                                                                      \
+    "v_mov_b32 v48, s87\n\t"                                                                      \
+    "s_set_gpr_idx_off\n\t"                                                                       \
+    "s_lshl_b32 s76, 1, s86\n\t"                                                                  \
+    "v_xor_b32 v89, s76, v89\n\t"
+// the end of a placing pass of type X (L or F): exec back, the next insert's slot, counters and
+// results, the next job's first fit from the sweep (none: s58 = h, the next pass is an F pass),
+// and the branch to the next pass (cursor past the pass bound: mcsfl_pend)
+#define MCS_FL_TAIL(X, BACK)                                                                      \
+    "s_mov_b32 s59, s54\n\t" /* h: the node this pass committed */                                \
+    "s_mov_b64 exec, -1\n\t" MCS_FL_INSPICK_V                                                    \
+    "s_min_u32 s77, s77, s55\n\t" /* the wave's earliest finish */                                \
+    "s_mov_b32 m0, s47\n\t"                                                                       \
+    "s_add_u32 s80, s80, 1\n\t"                                                                   \
+    "v_writelane_b32 v91, s54, m0\n\t"                                                            \
+    "v_writelane_b32 v92, s40, m0\n"                                                              \
+    "mcsfl_pick" X "_%=:\n\t"                                                                     \
+    "s_mov_b32 s58, s59\n\t"                                                                      \
+    "s_cmp_lg_u64 s[94:95], 0\n\t"                                                                \
+    "s_cbranch_scc0 mcsfl_nopick_%=\n\t"                                                          \
+    "s_ff1_i32_b64 s96, s[94:95]\n\t"                                                             \
+    "v_readlane_b32 s98, v87, s96\n\t" MCS_FL_INSPICK_S                                          \
+    "s_add_u32 s47, s47, 1\n\t" MCS_FL_REC                                                        \
+    "s_ff1_i32_b32 s98, s98\n\t"                                                                  \
+    "s_lshl3_add_u32 s58, s98, s96\n\t"                                                           \
+    "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
+    "s_cbranch_scc0 mcsfl_pend_%=\n\t"                                                            \
+    "s_cmp_eq_u32 s58, s59\n\t" BACK
+#define MCS_FL_BACK_L "s_cbranch_scc0 mcsfl_innerL_%=\n\ts_branch mcsfl_innerF_%=\n"
+#define MCS_FL_BACK_F "s_cbranch_scc1 mcsfl_innerF_%=\n\ts_branch mcsfl_innerL_%=\n"
+
+// W16R's release scan with the next insert's slot picked after its rows (they free slot rows)
+#define MCS_FL_SCAN                                                                               \
+    "ds_write_b32 v108, v64 offset:0\n\t"                                                        \
+    "ds_write_b32 v108, v65 offset:256\n\t"                                                      \
+    "ds_write_b32 v108, v66 offset:512\n\t"                                                      \
+    "ds_write_b32 v108, v67 offset:768\n\t"                                                      \
+    "s_mov_b32 s75, 0\n\t"                                                                       \
+    "v_cmp_ge_u32_e64 s[50:51], s40, v32\n\t"                                                    \
+    "v_cmp_ge_u32_e64 s[52:53], s40, v33\n\t"                                                    \
+    "v_cmp_ge_u32_e64 s[54:55], s40, v34\n\t"                                                    \
+    "v_cmp_ge_u32_e64 s[60:61], s40, v35\n\t"                                                    \
+    "v_cmp_ge_u32_e64 s[62:63], s40, v36\n\t"                                                    \
+    "v_cmp_ge_u32_e64 s[86:87], s40, v37\n\t"                                                    \
+    "v_cmp_ge_u32_e64 s[88:89], s40, v38\n\t"                                                    \
+    "v_cmp_ge_u32_e64 s[90:91], s40, v39\n\t"                                                    \
+    MCS_FR_ROW(0, "s[50:51]", "v32", "v40", "v48") MCS_FR_ROW(1, "s[52:53]", "v33", "v41", "v49")  \
+    MCS_FR_ROW(2, "s[54:55]", "v34", "v42", "v50") MCS_FR_ROW(3, "s[60:61]", "v35", "v43", "v51")  \
+    MCS_FR_ROW(4, "s[62:63]", "v36", "v44", "v52") MCS_FR_ROW(5, "s[86:87]", "v37", "v45", "v53")  \
+    MCS_FR_ROW(6, "s[88:89]", "v38", "v46", "v54") MCS_FR_ROW(7, "s[90:91]", "v39", "v47", "v55")  \
+    "s_mov_b64 exec, -1\n\t" MCS_FL_INSPICK_V                                                    \
+    "s_sub_u32 s80, s80, s75\n\t" MCS_FA_RELOAD16                                               \
+    "v_min3_u32 v90, v32, v33, v34\n\t"                                                          \
+    "v_min3_u32 v90, v90, v35, v36\n\t"                                                          \
+    "v_min3_u32 v90, v90, v37, v38\n\t"                                                          \
+    "v_min_u32 v90, v90, v39\n\t" MCS_FA_SCANEND16R MCS_FL_INSPICK_S
 
 #define MCS_FL_ENTRY                                                                              \
     "s_mov_b32 s58, -1\n\t"                                                                       \
     "s_mov_b32 s59, -1\n\t" MCS_FA_ENTRY_S(16R)
-// (MCS_FA_ENTRY_S(16R) ends with MCS_FA_REC16R: the entry's first pass is a full pass, which needs
-// only the cursor's record; the next request is read here, before the first sweep)
+// (MCS_FA_ENTRY_S(16R) ends with MCS_FA_REC16R and a branch to the batch end when the first batch is
+// empty; the first pass also needs the next request and the insert's slot)
 #define MCS_FL_BODY(D)                                                                            \
-    "mcsfl_first_%=:\n\t"                                                                         \
     "s_add_u32 s97, s47, 1\n\t"                                                                   \
     "s_and_b32 s97, s97, 63\n\t"                                                                  \
-    "v_readlane_b32 s92, v96, s97\n"                                                              \
+    "v_readlane_b32 s92, v96, s97\n\t" MCS_FL_INSPICK_V                                          \
+    "s_nop 4\n\t" MCS_FL_INSPICK_S                                                                \
+    "s_branch mcsfa_inner_%=\n"                                                                   \
+    "mcsfa_loopend_%=:\n\t"                                                                       \
+    "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
+    "s_cbranch_scc0 mcsfl_pend_%=\n"                                                              \
     "mcsfa_inner_%=:\n\t"                                                                         \
-    "s_cmp_gt_u32 s45, s40\n\t" /* ready head not arrived: sleep to it */                         \
-    "s_cbranch_scc1 mcsfa_arrive_%=\n\t"                                                          \
-    "s_cmp_eq_u32 s58, s59\n\t" /* no usable lookahead: the full pass */                          \
-    "s_cbranch_scc1 mcsfl_full_%=\n\t"                                                            \
+    "s_cmp_eq_u32 s58, s59\n\t" /* no usable lookahead: the F pass */                            \
+    "s_cbranch_scc1 mcsfl_innerF_%=\n"                                                            \
     /* ---- L pass: the job's first fit is s58 ---- */                                            \
-    MCS_FL_SWEEP_A                                                                                \
-    "v_cmp_lt_u32_e64 s[60:61], s49, v89\n\t" /* the insert's lanes with a free row */           \
-    "v_ffbl_b32 v117, v89\n\t"                                                                    \
-    MCS_FL_SWEEP_B                                                                                \
+    "mcsfl_innerL_%=:\n\t"                                                                        \
+    "s_cmp_gt_u32 s45, s40\n\t" /* ready head not arrived: sleep to it */                         \
+    "s_cbranch_scc1 mcsfa_arrive_%=\n\t" MCS_FL_SWEEP_A                                          \
     "s_add_u32 s55, s40, s46\n\t"                                                                 \
-    "s_and_b32 s50, s58, 63\n\t"                                                                  \
+    "s_and_b32 s50, s58, 63\n\t" MCS_FL_SWEEP_B                                                  \
     "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
-    "s_cbranch_scc1 mcsfl_lzero_%=\n\t" MCS_FL_DECIDE                                             \
-    "s_branch mcsfl_common_%=\n"                                                                  \
+    "s_cbranch_scc1 mcsfl_lzero_%=\n\t" MCS_FL_DECIDE_L MCS_FL_TAIL("L", MCS_FL_BACK_L)          \
     "mcsfl_lzero_%=:\n\t"                                                                         \
     "s_mov_b32 m0, s47\n\t"                                                                       \
     "s_mov_b32 s54, s58\n\t"                                                                      \
     "v_writelane_b32 v91, s54, m0\n\t"                                                            \
     "v_writelane_b32 v92, s40, m0\n\t"                                                            \
-    "s_branch mcsfl_pick_%=\n"                                                                    \
-    /* ---- full pass: W16R's fit test of the job, the sweep of the next one ---- */              \
-    "mcsfl_full_%=:\n\t" MCS_FA_FIT16 MCS_FL_SWEEP_A MCS_FA_ANYFIT                                \
-    "s_add_u32 s55, s40, s46\n\t" MCS_FL_SWEEP_B                                                  \
+    "s_branch mcsfl_pickL_%=\n"                                                                   \
+    /* ---- F pass: W16R's fit test of the job, with the next one's ---- */                      \
+    "mcsfl_innerF_%=:\n\t"                                                                        \
+    "s_cmp_gt_u32 s45, s40\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_arrive_%=\n\t" MCS_FL_FIT2                                             \
     "s_cbranch_vccz mcsfa_nofit_%=\n\t"                                                           \
     "s_ff1_i32_b64 s50, vcc\n\t" /* lowest lane with a fit */                                     \
     "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
-    "s_cbranch_scc1 mcsfa_zero_%=\n\t" MCS_FA_DECIDE16R                                           \
-    "mcsfl_common_%=:\n\t"                                                                        \
-    "s_mov_b32 s59, s54\n\t" /* h: the node this pass committed */                                \
-    "s_min_u32 s77, s77, s55\n\t" /* the wave's earliest finish */                                \
-    "s_mov_b64 exec, -1\n\t"                                                                      \
-    "s_mov_b32 m0, s47\n\t"                                                                       \
-    "s_add_u32 s80, s80, 1\n\t"                                                                   \
+    "s_cbranch_scc1 mcsfa_zero_%=\n\t" MCS_FL_DECIDE_F MCS_FL_TAIL("F", MCS_FL_BACK_F)           \
+    "mcsfa_zero_%=:\n\t" MCS_FA_ZEROKX16R                                                        \
     "v_writelane_b32 v91, s54, m0\n\t"                                                            \
-    "v_writelane_b32 v92, s40, m0\n"                                                              \
-    /* the next job's first fit before this commit (none: the next pass is a full one) */         \
-    "mcsfl_pick_%=:\n\t"                                                                          \
-    "s_mov_b32 s58, s59\n\t"                                                                      \
-    "s_cmp_lg_u64 s[94:95], 0\n\t"                                                                \
-    "s_cbranch_scc0 mcsfa_placed_%=\n\t"                                                          \
-    "s_ff1_i32_b64 s96, s[94:95]\n\t"                                                             \
-    "v_readlane_b32 s98, v87, s96\n\t"                                                            \
+    "v_writelane_b32 v92, s40, m0\n\t"                                                            \
+    "s_branch mcsfl_pickF_%=\n"                                                                   \
+    /* a pass whose next job fits no node (before the commit, so none after it either) */        \
+    "mcsfl_nopick_%=:\n\t" MCS_FL_INSPICK_S                                                       \
     "s_add_u32 s47, s47, 1\n\t" MCS_FL_REC                                                        \
-    "s_ff1_i32_b32 s98, s98\n\t"                                                                  \
-    "s_lshl3_add_u32 s58, s98, s96\n"                                                             \
-    "mcsfa_loopend_%=:\n\t"                                                                       \
-    "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfa_inner_%=\n\t"                                                           \
+    "s_branch mcsfa_loopend_%=\n"                                                                 \
+    /* the cursor reached the pass bound: a placed WaitQueue head sleeps 1 s (:250), or the */    \
+    /* batch ends */                                                                              \
+    "mcsfl_pend_%=:\n\t"                                                                          \
     "s_cmp_lg_u32 s43, 0\n\t"                                                                     \
     "s_cbranch_scc0 mcsfa_bend_%=\n\t"                                                            \
     "s_sub_u32 s41, s42, s57\n\t"                                                                 \
@@ -374,16 +471,6 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     "s_add_u32 s40, s40, 1\n\t"                                                                   \
     "s_cbranch_scc1 mcsfa_clkovf_%=\n\t"                                                          \
     "s_branch mcsfa_adv_%=\n"                                                                     \
-                                                                                                  \
-    /* a pass whose next job fits no node (before the commit, so none after it either) */        \
-    "mcsfa_placed_%=:\n\t"                                                                        \
-    "s_add_u32 s47, s47, 1\n\t" MCS_FL_REC                                                        \
-    "s_branch mcsfa_loopend_%=\n"                                                                 \
-                                                                                                  \
-    "mcsfa_zero_%=:\n\t" MCS_FA_ZEROKX16R                                                        \
-    "v_writelane_b32 v91, s54, m0\n\t"                                                            \
-    "v_writelane_b32 v92, s40, m0\n\t"                                                            \
-    "s_branch mcsfl_pick_%=\n"                                                                    \
                                                                                                   \
     "mcsfa_arrive_%=:\n\t"                                                                        \
     "s_mov_b32 s40, s45\n\t"                                                                      \
@@ -410,10 +497,10 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     MCS_FA_CNTR_##D                                                                               \
     "s_max_u32 s81, s81, s80\n\t"                                                                 \
     "s_mov_b32 s58, s59\n\t" /* a release: the lookahead is void */                               \
-    "s_add_u32 s74, s40, 1\n\t" MCS_FA_SCAN16R MCS_FA_SCANEND16R                                  \
+    "s_add_u32 s74, s40, 1\n\t" MCS_FL_SCAN                                                      \
     "s_cmp_lt_u32 s47, s41\n\t"                                                                   \
-    "s_cbranch_scc1 mcsfa_inner_%=\n\t"                                                           \
-    "s_branch mcsfa_loopend_%=\n" MCS_FA_RBODY16R                                                 \
+    "s_cbranch_scc1 mcsfl_innerF_%=\n\t"                                                          \
+    "s_branch mcsfl_pend_%=\n" MCS_FA_RBODY16R                                                    \
                                                                                                   \
     "mcsfa_deadlock_%=:\n\t"                                                                      \
     "s_or_b32 s44, s44, %[fdl]\n\t"                                                               \
@@ -450,7 +537,7 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     "s_mov_b32 s47, 0\n\t"                                                                        \
     "s_mov_b32 s58, s59\n\t" /* new records: the lookahead is void */                            \
     MCS_FL_REC                                                                                    \
-    "s_branch mcsfa_inner_%=\n"
+    "s_branch mcsfl_innerF_%=\n"
 #define MCS_FL_LOOP(D) MCS_FL_ENTRY MCS_FL_BODY(D) MCS_FA_EXIT_S
 // the lookahead loop's clobbers: W16R's plus its own (no probe build of this form: MCS_STAMPS uses
 // s92-s99 for its segment clocks)

@@ -26,6 +26,7 @@ leg() {   # leg NAME PROGRAM ARGS...
 for l in ${LEGS:-comm_only torch_nccl mcs_run_notorch torch_mcs_run}; do
     case "$l" in
     comm_only) leg comm_only "$ROOT/tools/rt_isolate/comm_only" ;;
+    graph_only) leg graph_only "$ROOT/tools/rt_isolate/graph_only" ;;
     bench_c5d_comm) leg bench_c5d_comm python3 "$ROOT/bench.py" --config c5 --policy delay --comm \
                         --jobs-per-cluster 200 --steps 1 --warmup 0 --no-cpu-baseline ;;
     bench_c5d) leg bench_c5d python3 "$ROOT/bench.py" --config c5 --policy delay \
