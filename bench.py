@@ -828,6 +828,15 @@ def _dump_parent_maps():
             g.write(f.read())
 
 
+def _dump_exit_maps():
+    """MCS_BENCH_EXIT_MAPS=<path>: this process's /proc/self/maps once the run is over, so the frames
+    of a fault at exit can be mapped to their libraries."""
+    path = os.environ.get("MCS_BENCH_EXIT_MAPS")
+    if path:
+        with open("/proc/self/maps") as f, open(path, "w") as g:
+            g.write(f.read())
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus == 1:
@@ -849,10 +858,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.config == "c5":
-        if args.policy == "delay":
-            return main_c5_delay(args, world, rank, local_rank)
-        return main_c5(args, world, rank, local_rank)
-    return main_batch(args, world, rank, local_rank)
+        rc = main_c5_delay(args, world, rank, local_rank) if args.policy == "delay" else \
+            main_c5(args, world, rank, local_rank)
+    else:
+        rc = main_batch(args, world, rank, local_rank)
+    _dump_exit_maps()
+    return rc
 
 
 if __name__ == "__main__":

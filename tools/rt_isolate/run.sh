@@ -31,6 +31,12 @@ for l in ${LEGS:-comm_only torch_nccl mcs_run_notorch torch_mcs_run}; do
                         --jobs-per-cluster 200 --steps 1 --warmup 0 --no-cpu-baseline ;;
     bench_c5d) leg bench_c5d python3 "$ROOT/bench.py" --config c5 --policy delay \
                    --jobs-per-cluster 200 --steps 1 --warmup 0 --no-cpu-baseline ;;
+    bench_c5d_maps) export MCS_BENCH_EXIT_MAPS="$OUT/bench_c5d_maps.txt"
+                    leg bench_c5d_maps python3 "$ROOT/bench.py" --config c5 --policy delay \
+                        --jobs-per-cluster 200 --steps 1 --warmup 0 --no-cpu-baseline
+                    unset MCS_BENCH_EXIT_MAPS ;;
+    bench_c4_small) leg bench_c4_small python3 "$ROOT/bench.py" --clusters 256 --jobs-per-cluster 2048 \
+                   --steps 1 --warmup 0 --no-cpu-baseline ;;
     *) leg "$l" python3 "$ROOT/tools/rt_isolate/py_steps.py" "$l" ;;
     esac
 done
