@@ -492,7 +492,9 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
             const bool examined = live && !((skipm >> lane) & 1ull);
             const bool placed = ((placedm >> lane) & 1ull) != 0ull;
             const uint32_t sl = (uint32_t)(al >> 32);
-            const uint32_t eff = sl > t_all ? sl : t_all;
+            // the entry's last examination: its own stamp while it is marked untested (a D6 skip
+            // materialised it), else the later of the stamp and the list's floor t_all
+            const uint32_t eff = ((uint32_t)jdv >> 31) != 0u ? sl : (sl > t_all ? sl : t_all);
             const long long delta = examined ? (long long)(T - eff) * 1000ll : 0ll;
             tot_l += delta;
             // compaction in the same sweep (append(Level1[:i], Level1[i+1:]...), :319)
@@ -511,6 +513,11 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
                 } else if (jdn != jdv) {
                     l1jd[np] = jdn;
                 }
+                // (an examined entry left in place keeps its stamp: the floor t_all = T set after
+                // the pass makes its last examination T; a skipped one carries its own)
+                // (an examined entry left in place could keep its stamp, the floor t_all = T set after
+                // the pass makes its last examination T, but testing for it here costs the kernel 50
+                // more SGPR spills: rows with a candidate are rare, quiet rows skip the store)
                 if (np != pos || nl != sl) l1al[np] = (al & 0xFFFFFFFFull) | ((unsigned long long)nl << 32);
             }
             snew_l += live && !placed ? (unsigned long long)nl : 0ull;
@@ -545,7 +552,7 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
                 } else if (jdn != jdv) {
                     l1jd[np] = jdn;
                 }
-                if (np != pos || T != sl) l1al[np] = (al & 0xFFFFFFFFull) | ((unsigned long long)T << 32);
+                if (np != pos) l1al[np] = (al & 0xFFFFFFFFull) | ((unsigned long long)T << 32);
             }
         };
         // is the row quiet?  (every lane active: the test reads across lanes)
@@ -597,6 +604,7 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
         st.l1n = wr;
         st.total += dt_wave_sum_i64(tot_l);
         st.s_last = (unsigned long long)dt_wave_sum_i64((long long)snew_l);
+        st.t_all = T;  // every entry examined at T: its stamp is not rewritten (the skipped ones are marked)
         st.l1_dirty = wr != n1 ? 1u : 0u;  // a pass that placed: its skipped entries come next
         if (exact) {  // the jobs left failed every node as they are now
             snap_l = lane < NN ? nodes[lane] : 0ull;

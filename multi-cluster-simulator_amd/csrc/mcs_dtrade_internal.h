@@ -56,7 +56,10 @@ struct DtCluster {
     // Level1 pass elision: a pass can only place a job after something raised a free counter
     // (a release, a new virtual node, a Foreign job wrapping a counter) or after a pass that
     // placed (its skipped entries).  Otherwise every entry fails again and only its JobsMap entry
-    // moves to T: entries' effective last = max(stored last, t_all), s_last = their sum.
+    // moves to T: entries' effective last = max(stored last, t_all), s_last = their sum.  A pass
+    // that runs sets t_all = T too and rewrites no stamp of an examined entry left in place; an entry
+    // the pass skips (D6, marked untested in bit 31 of its job word) carries its own last
+    // examination in its stamp, which is then its effective last whatever t_all holds (r06).
     uint32_t l1_dirty;
     uint32_t t_all;
     unsigned long long s_last;
