@@ -68,9 +68,11 @@ summary["pmc_per_launch"] = counters
 
 def short_name(n):
     """The engine's name for a rocprofv3 kernel name (mcs_last_kernel, bench.py's roofline.kernel): no
-    'void', no anonymous namespace, no parameter list, no trailing counting-build flag (', false')."""
+    'void', no anonymous namespace, no parameter list, no trailing counting-build flag (', false');
+    fifo_asm_kernel's lookahead flag (r06) reads ', look' when set and is dropped when not."""
     n = n.replace("void ", "", 1).replace("(anonymous namespace)::", "")
     n = n.split("(")[0]
+    n = n.replace(", false, false>", ">").replace(", false, true>", ", look>")
     return n.replace(", false>", ">").replace("<false>", "")
 
 
