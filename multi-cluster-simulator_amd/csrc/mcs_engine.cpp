@@ -604,7 +604,6 @@ int mcs_run(mcs_engine* e, uint32_t t_end_s, mcs_stats* stats) {
     switch (delay ? (dasm ? -2 : -1) : mcs::fifo_asm_form(a, npl, pool, false)) {
         case -2: e->last_kernel = "mcs::delay_asm_kernel"; break;
         case -1: e->last_kernel = "mcs::delay_kernel"; break;
-        case 23: e->last_kernel = "mcs::fifo_asm_kernel<16, true, 4, 8, track>"; break;
         case 22: e->last_kernel = "mcs::fifo_asm_kernel<16, true, 4, 8, look>"; break;
         case 21: e->last_kernel = "mcs::fifo_duo_kernel"; break;
         case 20: e->last_kernel = "mcs::fifo_asm_fused_kernel<1, 2>"; break;

@@ -417,21 +417,6 @@
     "s_set_gpr_idx_off\n\t"                                                                       \
     "s_lshl_b32 s76, 1, s86\n\t"                                                                  \
     "v_xor_b32 v89, s76, v89\n\t" /* the row is taken */
-// the decision's finish and the zero-duration test, after the fit test (W16T moves the first into it)
-#define MCS_FA_ADDFIN "s_add_u32 s55, s40, s46\n\t"
-#define MCS_FA_ADDFIN32 MCS_FA_ADDFIN
-#define MCS_FA_ADDFIN16 MCS_FA_ADDFIN
-#define MCS_FA_ADDFIN16R MCS_FA_ADDFIN
-#define MCS_FA_ADDFIN16S MCS_FA_ADDFIN
-#define MCS_FA_ADDFIN16D MCS_FA_ADDFIN
-#define MCS_FA_ADDFIN16T ""
-#define MCS_FA_ZTEST "s_cmp_eq_u32 s46, 0\n\t"
-#define MCS_FA_ZTEST32 MCS_FA_ZTEST
-#define MCS_FA_ZTEST16 MCS_FA_ZTEST
-#define MCS_FA_ZTEST16R MCS_FA_ZTEST
-#define MCS_FA_ZTEST16S MCS_FA_ZTEST
-#define MCS_FA_ZTEST16D MCS_FA_ZTEST
-#define MCS_FA_ZTEST16T MCS_FA_ZTEST
 // lanes with a fit into vcc
 #define MCS_FA_ANYFIT "v_cmp_ne_u32_e32 vcc, 0, v86\n\t"
 #define MCS_FA_ANYFIT32 MCS_FA_ANYFIT
@@ -467,82 +452,6 @@
 #define MCS_FA_NODEIDX32 MCS_FA_NODEIDX
 #define MCS_FA_NODEIDX16 MCS_FA_NODEIDX
 #define MCS_FA_NODEIDX16R MCS_FA_NODEIDX
-
-// ---- W16T: W16R with the insert's slot tracked in scalars (r06) -----------------------------------
-// Any free slot serves an insert (a release scans every row; the node copy's adds commute), so the
-// slot need not be the lowest free row of the lowest lane with one, which W16R recomputes on every
-// decision (a v_cmp and a v_ffbl over the free-row masks v89 in the fit test, a v_readlane of the
-// row).  W16T keeps one lane's free rows as they were when it picked that lane: s58 (the row mask,
-// bit 8 the sentinel when the pool is full), s[92:93] the lane's exec mask (0 when full).  An
-// insert takes the lowest row of s58 (its s_ff1 sits in the fit test's hazard slot, off the chain),
-// clears it, and re-picks a lane (the lowest with a free row in v89) only when s58 runs out: the
-// rows it holds stay free, since only inserts take rows and releases only free them.  3 VALU less
-// per decision, one not-taken branch more.
-#define MCS_FA_FIT16T                                                                             \
-    "v_pk_sub_u16 v72, v64, s48\n\t"                                                              \
-    "v_pk_sub_u16 v73, v65, s48\n\t"                                                              \
-    "v_pk_sub_u16 v74, v66, s48\n\t"                                                              \
-    "v_pk_sub_u16 v75, v67, s48\n\t"                                                              \
-    "v_and_b32_sdwa v80, v72, v72 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
-    "v_and_b32_sdwa v81, v74, v74 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
-    "v_and_b32_sdwa v80, v73, v73 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
-    "v_and_b32_sdwa v81, v75, v75 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_0\n\t" \
-    /* (two instructions between the last SDWA-preserve write and the v_perm: MCS_FA_FIT16) */    \
-    "s_add_u32 s55, s40, s46\n\t"                                                                 \
-    "s_ff1_i32_b32 s86, s58\n\t" /* the insert's row in the tracked lane (8: the pool is full) */ \
-    "v_perm_b32 v86, v81, v80, s72\n\t"
-#define MCS_FA_ANYFIT16T MCS_FA_ANYFIT
-#define MCS_FA_DECIDE16T                                                                          \
-    "v_readlane_b32 s51, v86, s50\n\t"                                                            \
-    "s_lshl_b64 exec, 1, s50\n\t"                                                                 \
-    "s_lshl_b32 s76, 1, s86\n\t"                                                                  \
-    "s_ff1_i32_b32 s52, s51\n\t"                                                                  \
-    "s_lshr_b32 s53, s52, 3\n\t"                                                                  \
-    "s_lshl3_add_u32 s54, s52, s50\n\t"                                                           \
-    "s_set_gpr_idx_on s53, gpr_idx(SRC0,DST)\n\t"                                                 \
-    "v_mov_b32 v64, v72\n\t" /* the commit (cluster.go:146-147) */                                \
-    "s_mov_b64 exec, s[92:93]\n\t" /* the tracked lane (empty when the pool is full) */          \
-    "s_lshl2_add_u32 s87, s54, s73\n\t"                                                           \
-    "s_set_gpr_idx_idx s86\n\t"                                                                   \
-    "v_mov_b32 v32, s55\n\t" /* the slot: finish, payload, node address */                       \
-    "v_mov_b32 v40, s48\n\t"                                                                      \
-    "v_mov_b32 v48, s87\n\t"                                                                      \
-    "s_set_gpr_idx_off\n\t"                                                                       \
-    "v_xor_b32 v89, s76, v89\n\t" /* the row is taken */                                         \
-    "s_andn2_b32 s58, s58, s76\n\t" /* SCC: rows left in the tracked lane */                    \
-    "s_cbranch_scc0 mcsft_ref_%=\n"                                                               \
-    "mcsft_ins_%=:\n\t"
-// (out of line, after an unconditional branch) the tracked lane ran out: the lowest lane with a free
-// row, or the pool is full (the insert after it is skipped; peak > 64 * 8 ends the cluster at the
-// batch end and the engine re-runs it with a bigger pool, as W16R)
-#define MCS_FA_RBODY16T                                                                           \
-    MCS_FA_RBODY16R                                                                               \
-    "mcsft_ref_%=:\n\t"                                                                           \
-    "s_mov_b64 exec, -1\n\t"                                                                      \
-    "v_cmp_lt_u32_e64 s[60:61], s49, v89\n\t" /* (v89 = free rows | 0x100, s49 = 0x100) */      \
-    "s_ff1_i32_b64 s59, s[60:61]\n\t"                                                             \
-    "s_cmp_lt_i32 s59, 0\n\t"                                                                     \
-    "s_cbranch_scc1 mcsft_full_%=\n\t"                                                            \
-    "v_readlane_b32 s58, v89, s59\n\t"                                                            \
-    "s_lshl_b64 s[92:93], 1, s59\n\t"                                                             \
-    "s_and_b32 s58, s58, 0xff\n\t"                                                                \
-    "s_branch mcsft_ins_%=\n"                                                                     \
-    "mcsft_full_%=:\n\t"                                                                          \
-    "s_mov_b32 s58, 0x100\n\t"                                                                    \
-    "s_mov_b64 s[92:93], 0\n\t"                                                                   \
-    "s_branch mcsft_ins_%=\n"
-#define MCS_FA_INIT16T MCS_FA_INIT16R "s_mov_b32 s58, 0xff\n\ts_mov_b64 s[92:93], 1\n\t"
-#define MCS_FA_REC16T MCS_FA_REC16
-#define MCS_FA_TAKE16T MCS_FA_TAKE16
-#define MCS_FA_RELOAD16T MCS_FA_RELOAD16
-#define MCS_FA_SCAN16T MCS_FA_SCAN16R
-#define MCS_FA_SCANEND16T MCS_FA_SCANEND
-#define MCS_FA_ZEROKX16T MCS_FA_ZEROKX
-#define MCS_FA_POOLMAX16T "64*8"
-#define MCS_FA_NODEIDX16T MCS_FA_NODEIDX
-#define MCS_FA_BENDCHK16T ""
-#define MCS_FA_FREELANES16T ""
-#define MCS_FT_CLOBBERS MCS_FA_CLOBBERS, "s92", "s93"
 
 // ---- W16S: W16R for clusters of at most 64 nodes (one chunk, node = lane) and 2 slot rows --------
 // (cluster_small / cluster_big: C1-C3).  The fit bit is bit 15 of one SDWA AND; no chunk pick, and

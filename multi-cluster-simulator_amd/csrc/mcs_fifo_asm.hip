@@ -101,10 +101,11 @@ __device__ unsigned long long g_fa_stamps[5];  // [4]: the duo loop's header re-
     /* ---- one pass = one decision (scheduler.go:216-296) ---- */                               \
     "mcsfa_inner_%=:\n\t"                                                                         \
     "s_cmp_gt_u32 s45, s40\n\t" /* ready head not arrived: sleep to it */                         \
-    "s_cbranch_scc1 mcsfa_arrive_%=\n\t" MCS_FA_FIT##W MCS_FA_ANYFIT##W MCS_FA_ADDFIN##W        \
+    "s_cbranch_scc1 mcsfa_arrive_%=\n\t" MCS_FA_FIT##W MCS_FA_ANYFIT##W                           \
+    "s_add_u32 s55, s40, s46\n\t"                                                                 \
     "s_cbranch_vccz mcsfa_nofit_%=\n\t"                                                           \
     "s_ff1_i32_b64 s50, vcc\n\t" /* lowest lane with a fit */                                     \
-    MCS_FA_ZTEST##W                                                                               \
+    "s_cmp_eq_u32 s46, 0\n\t"                                                                     \
     "s_cbranch_scc1 mcsfa_zero_%=\n\t"                                                            \
     MCS_FA_DECIDE##W                                                                              \
     "s_min_u32 s77, s77, s55\n\t" /* the wave's earliest finish */                                \
@@ -653,12 +654,11 @@ __device__ __forceinline__ void fa_finish(const FifoArgs& a, uint32_t ci, uint32
 // (NPL nodes per lane, P slot rows: 4/8 for 129-256 node clusters, 1/2 for at most 64 nodes)
 // (DIAG: count the passes without a decision and the release scans into mcs_cluster_stats; the
 // production launches skip them, 1.6 % of the C4 loop)
-// (LOOK: the W16L lookahead loop; TRACK: the W16T tracked-insert loop; both W16R's shape only)
-template <int W, bool RS, int NPL, int P, bool DIAG, bool LOOK = false, bool TRACK = false>
+// (LOOK: the W16L lookahead loop, W16R's shape only)
+template <int W, bool RS, int NPL, int P, bool DIAG, bool LOOK = false>
 __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
     static_assert(W == 16 || !RS, "register slots: 16-bit node format only");
     static_assert(!LOOK || (W == 16 && RS && NPL == 4 && P == 8), "lookahead: the W16R shape");
-    static_assert(!TRACK || (W == 16 && RS && NPL == 4 && P == 8 && !LOOK), "tracked insert: the W16R shape");
     static_assert((NPL == 4 && P == 8) || (NPL == 1 && P == 2 && W == 16 && RS), "loop shapes");
     const uint32_t item = blockIdx.x;
     const uint32_t ci = a.cluster_list ? a.cluster_list[item] : item;
@@ -735,16 +735,10 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
       [fov] "i"(MCS_FLAG_OVERFLOW)
 #define MCS_FA_OPERANDS MCS_FA_OPERANDS_IO : MCS_FA_CLOBBERS
 #define MCS_FL_OPERANDS MCS_FA_OPERANDS_IO : MCS_FL_CLOBBERS
-#define MCS_FT_OPERANDS MCS_FA_OPERANDS_IO : MCS_FT_CLOBBERS
     if constexpr (LOOK) {
 #ifndef MCS_STAMPS
         if constexpr (DIAG) asm volatile(MCS_FL_LOOP(D1) MCS_FL_OPERANDS);
         else asm volatile(MCS_FL_LOOP(D0) MCS_FL_OPERANDS);
-#endif
-    } else if constexpr (TRACK) {
-#ifndef MCS_STAMPS
-        if constexpr (DIAG) asm volatile(MCS_FA_LOOP(16T, D1) MCS_FT_OPERANDS);
-        else asm volatile(MCS_FA_LOOP(16T, D0) MCS_FT_OPERANDS);
 #endif
     } else if constexpr (W == 32)
         if constexpr (DIAG) asm volatile(MCS_FA_LOOP(32, D1) MCS_FA_OPERANDS);
@@ -760,7 +754,6 @@ __global__ __launch_bounds__(64) void fifo_asm_kernel(FifoArgs a) {
         else asm volatile(MCS_FA_LOOP(16, D0) MCS_FA_OPERANDS);
 #undef MCS_FA_OPERANDS
 #undef MCS_FL_OPERANDS
-#undef MCS_FT_OPERANDS
 #undef MCS_FA_OPERANDS_IO
 #pragma clang diagnostic pop
 
@@ -1013,8 +1006,7 @@ __global__ __launch_bounds__(2 * kWave) void fifo_duo_kernel(FifoArgs a) {
 
 }  // namespace
 
-// Form codes: 23 = W16R with the tracked insert (W16T), 22 = W16R's one-job lookahead loop (W16L),
-// 21 = W16R's duo loop (a decision and a release wave per cluster, small grids),
+// Form codes: 22 = W16R's one-job lookahead loop (W16L), 21 = W16R's duo loop (a decision and a release wave per cluster, small grids),
 // 17 = W16R and 18 = W16S (where the 16-bit format fits), 16 = W16 with LDS slots,
 // 32 = W32, 19 / 20 = W16R / W16S on a fused job stream, 0 = the compiled kernel.  MCS_FIFO_ASM=0
 // turns the hand-scheduled loop off, =16 / =32 force a form (A/B timing, the variant tests; neither
@@ -1047,13 +1039,7 @@ int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor) {
         // wave per SIMD and fewer); MCS_FIFO_LOOK=0|1 forces either
         const char* look = getenv("MCS_FIFO_LOOK");
         const bool l = look ? atoi(look) != 0 : a.n_items <= kLookMaxItems;
-        if (l) return 22;
-#ifndef MCS_STAMPS
-        // the tracked-insert loop (W16T): MCS_FIFO_TRACK=0|1 (default kFifoTrack)
-        const char* tr = getenv("MCS_FIFO_TRACK");
-        if (tr ? atoi(tr) != 0 : kFifoTrack) return 23;
-#endif
-        return 17;
+        return l ? 22 : 17;
     }
     return (a.guard_ok & 1u) ? 32 : 0;
 }
@@ -1072,7 +1058,6 @@ static hipError_t launch_form(const FifoArgs& a, int form, hipStream_t s) {
         case 17: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
 #ifndef MCS_STAMPS
         case 22: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 4, 8, DIAG, true>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
-        case 23: hipLaunchKernelGGL((fifo_asm_kernel<16, true, 4, 8, DIAG, false, true>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
 #endif
         case 16: hipLaunchKernelGGL((fifo_asm_kernel<16, false, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;
         case 32: hipLaunchKernelGGL((fifo_asm_kernel<32, false, 4, 8, DIAG>), dim3(a.n_items), dim3(kWave), 0, s, a); break;

@@ -23,8 +23,6 @@ constexpr uint32_t kAsmMaxJobs = (1u << 28) - 128u;  // hand-scheduled loop: 32-
 constexpr uint32_t kDuoMaxItems = 0u;
 // the W16L lookahead loop: picked for grids of at most this many clusters (0: only MCS_FIFO_LOOK=1)
 constexpr uint32_t kLookMaxItems = 0u;
-// the W16T tracked-insert loop instead of W16R (MCS_FIFO_TRACK overrides)
-constexpr bool kFifoTrack = false;
 constexpr uint32_t kJobPad = 128;  // records of slack after the job array (unmasked batch loads)
 
 struct Totals {  // device-side accumulation of mcs_stats (only clusters that did not overflow)
@@ -151,7 +149,7 @@ bool fifo_variant_exists(int npl, int pool);
 // the hand-scheduled decision loop (mcs_fifo_asm.hip): NPL 4 / P 8 or NPL 1 / P 2, streamed
 // batch runs; MCS_FIFO_ASM=0 turns it off
 bool fifo_asm_eligible(const FifoArgs& a, int npl, int pool, bool hor);
-int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor);  // 23, 22, 21, 20, 19, 18, 17, 16, 32 or 0
+int fifo_asm_form(const FifoArgs& a, int npl, int pool, bool hor);  // 22, 21, 20, 19, 18, 17, 16, 32 or 0
 hipError_t launch_fifo_asm(const FifoArgs& a, int npl, int pool, hipStream_t s);
 hipError_t launch_gen_attrs(uint4* jobs, const uint64_t* job_off, const uint32_t* max_c,
                             const uint32_t* max_m, uint32_t n_clusters, uint64_t seed,

@@ -22,7 +22,6 @@ KATS = load_kats()
 W16R = "mcs::fifo_asm_kernel<16, true, 4, 8>"
 DUO = "mcs::fifo_duo_kernel"
 LOOK = "mcs::fifo_asm_kernel<16, true, 4, 8, look>"
-TRACK = "mcs::fifo_asm_kernel<16, true, 4, 8, track>"
 
 
 def w16r_form(n_clusters):
@@ -32,17 +31,13 @@ def w16r_form(n_clusters):
     kDuoMaxItems = kLookMaxItems = 0)."""
     if os.environ.get("MCS_FIFO_DUO") == "1":
         return DUO
-    if os.environ.get("MCS_FIFO_LOOK") == "1":
-        return LOOK
-    return TRACK if os.environ.get("MCS_FIFO_TRACK") == "1" else W16R
+    return LOOK if os.environ.get("MCS_FIFO_LOOK") == "1" else W16R
 
 
 def set_form(monkeypatch, form):
-    """form: "0" W16R, "1" the duo loop, "look" the lookahead loop, "track" the tracked-insert loop
-    (the parametrisations below)."""
+    """form: "0" W16R, "1" the duo loop, "look" the lookahead loop (the parametrisations below)."""
     monkeypatch.setenv("MCS_FIFO_DUO", "1" if form == "1" else "0")
     monkeypatch.setenv("MCS_FIFO_LOOK", "1" if form == "look" else "0")
-    monkeypatch.setenv("MCS_FIFO_TRACK", "1" if form == "track" else "0")
 
 def run_engine(eng, arrays, streams):
     eng.load_clusters(arrays)
@@ -172,7 +167,7 @@ def test_config3_small_replicas(engine):
     assert_parity(arrays, streams, node, start, fin, cs)
 
 
-@pytest.mark.parametrize("form", ["0", "look", "track"])
+@pytest.mark.parametrize("form", ["0", "look"])
 @pytest.mark.parametrize("kind", ["n256", "n256_hot"])
 def test_config4_shape_reduced(engine, kind, form, monkeypatch):
     """BASELINE config 4 shape (256 nodes, scaled arrivals) at 128 clusters x 6k jobs (W16R and the
@@ -320,7 +315,7 @@ def test_heterogeneous_cluster_sizes(engine):
 
 @pytest.mark.parametrize("sizes", [[0, 1, 5, 63, 64, 65, 130, 200, 256], [0, 1, 2, 5, 33, 63, 64]],
                          ids=["asm_4x8", "asm_1x2"])
-@pytest.mark.parametrize("duo", ["0", "1", "look", "track"])
+@pytest.mark.parametrize("duo", ["0", "1", "look"])
 def test_heterogeneous_cluster_sizes_hand_scheduled(engine, sizes, duo, monkeypatch):
     """Clusters of many sizes in one launch of each hand-scheduled loop shape (the largest picks it:
     129-256 nodes -> 4 chunks x 8 slot rows, <= 64 nodes -> 1 chunk x 2 rows): padding nodes, an
@@ -354,7 +349,7 @@ def test_heterogeneous_cluster_sizes_hand_scheduled(engine, sizes, duo, monkeypa
     assert cs[0]["flags"] & L.MCS_FLAG_DEADLOCK  # zero nodes: the first job never fits
 
 
-@pytest.mark.parametrize("nodes,duo", [(256, "0"), (256, "1"), (256, "look"), (256, "track"), (5, "0")])
+@pytest.mark.parametrize("nodes,duo", [(256, "0"), (256, "1"), (256, "look"), (5, "0")])
 def test_hand_scheduled_diag_build(nodes, duo, monkeypatch):
     """MCS_FIFO_DIAG=1 launches the counting build of the hand-scheduled loop: the same placements
     and per-cluster results, plus the pass and release-scan counters (which the production build
@@ -380,7 +375,7 @@ def test_hand_scheduled_diag_build(nodes, duo, monkeypatch):
     assert_parity(arrays, streams, *res["1"][:3], c1)
 
 
-@pytest.mark.parametrize("shape", ["w16s", "w16r", "duo", "look", "track", "w32"])
+@pytest.mark.parametrize("shape", ["w16s", "w16r", "duo", "look", "w32"])
 @pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6])
 def test_hand_scheduled_fuzz(engine, shape, seed, monkeypatch):
     """Randomised clusters and streams through each hand-scheduled loop form, bit-exact against the
@@ -388,11 +383,11 @@ def test_hand_scheduled_fuzz(engine, shape, seed, monkeypatch):
     availability, bursts of simultaneous arrivals, zero-duration and zero-resource jobs, requests
     equal to a node's free value, and one request per cluster that fits no node (a head-of-line
     deadlock at a random point of the stream)."""
-    set_form(monkeypatch, {"duo": "1", "look": "look", "track": "track"}.get(shape, "0"))
-    arrays, s = fuzz_workload("w16r" if shape in ("duo", "look", "track") else shape, seed)
+    set_form(monkeypatch, {"duo": "1", "look": "look"}.get(shape, "0"))
+    arrays, s = fuzz_workload("w16r" if shape in ("duo", "look") else shape, seed)
     node, start, fin, st, cs = run_engine(engine, arrays, s)
     want = {"w16s": "mcs::fifo_asm_kernel<16, true, 1, 2>", "w16r": W16R, "duo": DUO, "look": LOOK,
-            "track": TRACK, "w32": "mcs::fifo_asm_kernel<32, false, 4, 8>"}[shape]
+            "w32": "mcs::fifo_asm_kernel<32, false, 4, 8>"}[shape]
     if st.escalations == 0:
         assert engine.last_kernel == want
     assert_parity(arrays, s, node, start, fin, cs)
@@ -427,12 +422,10 @@ def test_slot_pool_escalation():
     eng.close()
 
 
-@pytest.mark.parametrize("form", ["0", "track"])
-def test_slot_pool_escalation_from_hand_scheduled_loop(form, monkeypatch):
+def test_slot_pool_escalation_from_hand_scheduled_loop():
     """More than 512 jobs running at once on a 200-node cluster: the hand-scheduled loop (8 slot rows)
     reports the overflow, the engine re-runs the cluster with a doubled pool on the compiled kernel,
-    and the result is still bit-exact (W16R, and W16T through its full-pool state)."""
-    set_form(monkeypatch, form)
+    and the result is still bit-exact."""
     eng = Engine(0)
     arrays = replicate(uniform_cluster(200), 2)
     n = 1500
@@ -532,17 +525,14 @@ def test_every_kernel_variant(policy):
             # (and the duo loop, MCS_FIFO_DUO=1, the register-slot form's two-wave variant)
             for fused, lat, asm, duo in ((False, "1", "0", None), (False, "0", "0", None), (False, None, "1", "0"),
                                          (False, None, "1", "1"), (False, None, "1", "look"),
-                                         (False, None, "1", "track"),
                                          (False, None, "16", None), (False, None, "32", None),
                                          (True, None, None, None)):
                 if policy == "DELAY" and lat == "0":
                     continue
                 if policy == "DELAY" and asm in ("1", "16", "32"):
                     continue
-                env = {"MCS_FIFO_LAT": lat, "MCS_FIFO_ASM": asm,
-                       "MCS_FIFO_DUO": "0" if duo in ("look", "track") else duo,
-                       "MCS_FIFO_LOOK": "1" if duo == "look" else None,
-                       "MCS_FIFO_TRACK": "1" if duo == "track" else None}
+                env = {"MCS_FIFO_LAT": lat, "MCS_FIFO_ASM": asm, "MCS_FIFO_DUO": "0" if duo == "look" else duo,
+                       "MCS_FIFO_LOOK": "1" if duo == "look" else None}
                 old = {k: os.environ.get(k) for k in env}
                 for k, v in env.items():
                     if v is not None:
