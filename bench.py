@@ -291,13 +291,15 @@ def main_c5_delay(args, world, rank, local_rank):
                                                     else "one launch per tick, captured with the all-gather in a hipGraph" if ts["loop_form"] == 7
                                                     else "one launch per tick, eager" if ts["loop_form"] == 8
                                                     else "one launch per tick, caller-driven" if ts["loop_form"] == 9
-                                                    else "resident, one workgroup per 4 clusters"
-                                                    + (", all on one XCD (L2 exchange)" if ts["loop_form"] == 5 else "")) + ")",
+                                                    else "resident, one wave per cluster (4 per workgroup) and a "
+                                                         "trader wave, all on one XCD (L2 exchange)") + ")",
             },
             "roofline": {
                 "bound": "hbm",
                 "limiter": ("latency: one workgroup runs every cluster's Delay iteration, then the trader rounds, "
                             "per tick (DESIGN.md §11)" if ts["loop_form"] == 3 else
+                            "latency: the slowest cluster's Delay iteration, then the trader rounds, per tick, "
+                            "with two granule exchanges (DESIGN.md §11)" if ts["loop_form"] == 5 else
                             "launch/latency: a tick is dependent launches of a few us (DESIGN.md §11)"),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
@@ -305,6 +307,8 @@ def main_c5_delay(args, world, rank, local_rank):
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
                 "kernel": ("dt_res_kernel (resident tick, the whole system in one workgroup)" if ts["loop_form"] == 3
+                           else "dt_mw_kernel (resident tick, one wave per cluster and a trader wave)"
+                           if ts["loop_form"] == 5
                            else "lock-step tick (dt_step with the sample, dt_trader), launch/latency-bound"),
                 "kernel_ms_avg": avg_kernel_s * 1e3,
                 "bytes_per_placement": BYTES_PER_PLACEMENT,

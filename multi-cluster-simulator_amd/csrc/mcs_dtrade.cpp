@@ -44,6 +44,12 @@ struct DtradeDev {
     uint32_t tag[4] = {0, 0, 0, 0};          // caller-driven blocks: the layout tag (kDtTagBytes at the end)
     hipGraphExec_t graph = nullptr;
     hipGraphExec_t rgraph = nullptr;  // RCCL loop: kernels + all-gathers of kDtGraphTicks ticks
+    // the resident tick (mcs_dtrade_mw.hip): exchange granules, placement granules + failure word
+    // (uncached), the queued side effects of phase D
+    unsigned long long* gx = nullptr;
+    unsigned long long* gu = nullptr;
+    void* ops = nullptr;
+    uint32_t ops_cap = 0;
     bool rgraph_tried = false;
     uint32_t loop_form = kLoopGraph;
     bool begun = false;  // caller-driven lock-step in progress
@@ -54,6 +60,8 @@ namespace {
 
 constexpr uint64_t kDtTagBytes = 16;  // caller-driven exchange blocks end in the layout tag
 constexpr uint32_t kDtGraphTicks = 256;  // (r05: 64 -> 256, A/B 14.57 -> 14.44 us per C5-DELAY tick)
+constexpr uint32_t kDtResTicks = 1u << 16;  // ticks per launch of the resident tick
+constexpr int kDtResFallback = -100;       // dt_run_res: the launch failed over (dtrade_run re-runs)
 
 int dt_hip_fail(mcs_engine* e, const char* what, hipError_t st) {
     return fail(e, MCS_E_HIP, std::string(what) + ": " + hipGetErrorString(st));
@@ -209,6 +217,61 @@ int dt_run_once(mcs_engine* e, double* kernel_ms) {
     return MCS_OK;
 }
 
+// MCS_DT_RESIDENT=0 forces the replayed kernels; the resident tick needs the whole system on this
+// engine (no communicator, world 1), at most 64 clusters of at most 320 nodes (physical + virtual)
+// and 1024 slots each.
+bool dt_res_ok(mcs_engine* e) {
+    const char* env = getenv("MCS_DT_RESIDENT");
+    if ((env && atoi(env) == 0) || e->tr_no_resident || e->comm || e->world != 1) return false;
+    const DtArgs& a = e->dtd->a;
+    return a.Ct == a.C && a.C <= kDtResMaxClusters && e->max_n + a.V <= kDtResMaxNN && a.S <= kDtResMaxSlots &&
+           a.S % 64u == 0u;
+}
+
+// the resident tick: one launch per kDtResTicks ticks (MCS_DT_RES_TICKS: fewer, so tests cross
+// launch boundaries); kDtResFallback when a launch's workers were not all on one XCD or an
+// exchange timed out, with nothing of the run kept
+int dt_run_res(mcs_engine* e, double* kernel_ms) {
+    DtradeDev* d = e->dtd;
+    hipError_t st = launch_dtrade_init(d->a, e->stream);
+    if (st != hipSuccess) return dt_hip_fail(e, "DELAY trading init", st);
+    DtResArgs m{};
+    m.ops_cap = d->a.S + d->a.V + 8u;  // a tick's side effects on a cluster: one per slot it takes, per virtual node
+    if (!d->gx) {
+        HIPCHK(e, hipMalloc(&d->gx, dtrade_mw_gx_bytes()));
+        HIPCHK(e, hipExtMallocWithFlags((void**)&d->gu, dtrade_mw_gu_bytes(), hipDeviceMallocUncached));
+        HIPCHK(e, hipMalloc(&d->ops, (size_t)d->a.C * m.ops_cap * dtrade_mw_op_bytes()));
+        d->ops_cap = m.ops_cap;
+    }
+    m.gx = d->gx;
+    m.gu = d->gu;
+    m.ops = d->ops;
+    m.ops_cap = d->ops_cap;
+    const char* tenv = getenv("MCS_DT_RES_TICKS");
+    const long tv = tenv ? atol(tenv) : 0;
+    m.budget = tv > 0 && tv < (long)kDtResTicks ? (uint32_t)tv : kDtResTicks;
+    m.nwg = (d->a.C + 3u) / 4u;
+    d->loop_form = kLoopResidentMwXcd;
+    HIPCHK(e, hipEventRecord(e->ev0, e->stream));
+    for (;;) {
+        st = launch_dtrade_mw(d->a, m, e->stream);
+        if (st != hipSuccess) return dt_hip_fail(e, "resident DELAY trading tick", st);
+        unsigned long long fw = 0;
+        HIPCHK(e, hipMemcpyAsync(&fw, d->gu + dtrade_mw_fail_word(), sizeof(fw), hipMemcpyDeviceToHost, e->stream));
+        if (int s = dt_poll(e)) return s;
+        if (fw != 0ull) return kDtResFallback;
+        // (MCS_DT_RES_FORCE_FAIL=1: tests take the fail-over path after the first launch)
+        if (const char* ff = getenv("MCS_DT_RES_FORCE_FAIL"); ff && atoi(ff) != 0) return kDtResFallback;
+        if (d->h_ctl->done) break;
+    }
+    HIPCHK(e, hipEventRecord(e->ev1, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    float ms = 0.0f;
+    HIPCHK(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+    *kernel_ms = ms;
+    return MCS_OK;
+}
+
 // N engines (one per GPU): the exchange blocks are all-gathered in place over xGMI between the two
 // kernels of every tick; one host poll per kDtGraphTicks ticks (the kernels of finished ticks
 // return at once on ctl->done, identically on every rank)
@@ -322,6 +385,9 @@ void dtrade_free(mcs_engine* e) {
     dfree(d->foreign);
     dfree(d->xb);
     dfree(d->nv_all);
+    dfree(d->gx);
+    dfree(d->gu);
+    dfree(d->ops);
     if (d->h_ctl) (void)hipHostFree(d->h_ctl);
     for (hipEvent_t& ev : d->pev)
         if (ev) (void)hipEventDestroy(ev);
@@ -342,6 +408,11 @@ int dtrade_run(mcs_engine* e, mcs_stats* stats) {
     e->dt_vnodes = e->dt_learn_v;
     // a communicator selects the RCCL loop (world 1 included: one rank's all-gather is a copy)
     const bool rccl = e->comm != nullptr;
+    e->tr_no_resident = false;  // (set when the resident tick fails over, for the rest of this run)
+    struct Reset {
+        mcs_engine* e;
+        ~Reset() { e->tr_no_resident = false; }
+    } reset{e};
     if (rccl) {
         dtrade_free(e);
         if (int s = dt_agree_shape(e)) return s;
@@ -353,7 +424,21 @@ int dtrade_run(mcs_engine* e, mcs_stats* stats) {
     for (;;) {
         if (int s = dtrade_alloc(e)) return s;
         double ms = 0.0;
-        if (int s = rccl ? dt_run_rccl(e, &ms) : dt_run_once(e, &ms)) return s;
+        int s = MCS_OK;
+        if (rccl) {
+            s = dt_run_rccl(e, &ms);
+        } else if (dt_res_ok(e)) {
+            s = dt_run_res(e, &ms);
+            if (s == kDtResFallback) {  // (the run is redone from its start on the replayed kernels)
+                e->tr_no_resident = true;
+                s = dt_run_once(e, &ms);
+                e->dtd->loop_form = kLoopGraphAfterTimeout;
+            }
+        } else {
+            s = dt_run_once(e, &ms);
+            if (e->tr_no_resident) e->dtd->loop_form = kLoopGraphAfterTimeout;
+        }
+        if (s) return s;
         kms += ms;
         if (int s = dt_poll(e)) return s;
         // ctl->flags is replicated (it ORs every cluster's record), so every rank escalates alike

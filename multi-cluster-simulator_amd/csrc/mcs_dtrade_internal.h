@@ -130,6 +130,23 @@ struct DtArgs {
     mcs_foreign_rec* foreign_log;
 };
 
+// The resident tick (mcs_dtrade_mw.hip, world 1): one wave per cluster, 4 per workgroup, and a
+// trader wave, exchanging granules through one XCD's L2; a launch runs up to `budget` ticks.
+constexpr uint32_t kDtResMaxClusters = 64;  // clusters in the system
+constexpr uint32_t kDtResMaxNN = 320;       // physical + virtual nodes per cluster
+constexpr uint32_t kDtResMaxSlots = 1024;   // running slots per cluster
+struct DtResArgs {
+    unsigned long long* gx;  // exchange granules (cached device memory), dtrade_mw_gx_bytes()
+    unsigned long long* gu;  // placement granules and the failure word (uncached), dtrade_mw_gu_bytes()
+    void* ops;               // phase D's side effects, [cluster][ops_cap] of dtrade_mw_op_bytes() each
+    uint32_t ops_cap, budget, nwg, pad;
+};
+size_t dtrade_mw_gx_bytes();
+size_t dtrade_mw_gu_bytes();
+size_t dtrade_mw_op_bytes();
+uint32_t dtrade_mw_fail_word();  // index in gu: 0 ok, 1 placement, 2 a cluster wave's wait, 3 the trader's
+hipError_t launch_dtrade_mw(const DtArgs& a, const DtResArgs& m, hipStream_t s);
+
 hipError_t launch_dtrade_init(const DtArgs& a, hipStream_t s);
 hipError_t launch_approve(const mcs_approve_query* q, uint32_t n, int32_t* out, hipStream_t s);  // the mirror
 // one tick: phases A and C (dt_step_kernel, writes this rank's exchange block), then phase D

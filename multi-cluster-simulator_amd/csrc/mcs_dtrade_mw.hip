@@ -1,0 +1,361 @@
+// mcs_dtrade_mw.hip — the lock-step trading system with DELAY schedulers resident
+// in a few workgroups on one XCD: up to 64 clusters of <= 320 nodes (physical + virtual), one wave
+// per cluster, four per workgroup, plus one trader wave; a launch runs up to `budget` ticks.
+//   A+C  each cluster wave, its cluster, with its nodes, running slots and DtCluster state held in
+//        the wave's LDS and registers from tick to tick (the replayed step kernel copies them in and
+//        out of HBM every tick): phase A and the sample (dt_phase_a, dt_sample of
+//        mcs_dtrade_dev.h), then its exchange record and, when a trader round is due, its node
+//        snapshot and both contract sizes; it publishes the record (X1)
+//   D    the trader wave gathers every record (X1), runs the trader rounds in cluster order on its
+//        own copy of the trader state (dt_rounds<true>: the same code as dt_trader_kernel), and
+//        publishes the next tick's clock and, per cluster, the count of the rounds' side effects on
+//        that cluster's live state, queued in HBM in the rounds' order (X2)
+//   X2   each cluster wave applies its side effects (Foreign commits to a node and a running slot,
+//        virtual nodes: pkg/scheduler/cluster.go:65-125) and starts the next tick
+// Exchange: the worker workgroups run 8 blocks apart, which the dispatcher's round-robin puts on
+// one XCD (checked at the launch's start: a launch whose workers landed on more than one XCD does
+// nothing, and the engine runs the replayed kernels instead), so that XCD's L2 is the meeting
+// point.  Every exchanged word travels as an 8-byte granule {value, tag} written with a plain store
+// (write-through L1, so it lands in the L2) and read with agent-scope loads (L1 bypassed) until
+// its tag is the exchange's epoch (2 * tick + 1 for X1, + 2 for X2; the granules are zeroed before
+// every launch): the data is the flag (cdna_hip_programming.md Guideline 16).  The bulk data behind
+// a granule (node snapshots, the queued operations) is stored before it and drained with
+// s_waitcnt vmcnt(0).  A cluster wave publishes X1 of tick n + 1 only after reading X2 of tick n,
+// which the trader publishes after its last read of tick n's records and snapshots, so one buffer
+// of each suffices.  Every wait is bounded (1 s without the epoch ends the launch with a failure
+// word, and the engine redoes the run on the replayed kernels).  Same results bit for bit as the
+// replayed tick (tests/test_gpu_dtrade.py).
+#include "mcs_dtrade_dev.h"
+
+namespace mcs {
+namespace {
+
+constexpr uint32_t kDmWaves = 4;  // cluster waves per workgroup, one per SIMD
+constexpr uint32_t kDmThreads = kDmWaves * kWave;
+constexpr uint32_t kDmRecWords = (uint32_t)(sizeof(DtRec) / 4u);
+static_assert(sizeof(DtRec) % 4u == 0u && kDmRecWords <= (uint32_t)kWave, "a record word per lane");
+// granules (u64) of gx: X1 records word-major [kDmRecWords][64] (word w of cluster q at w * 64 + q),
+// X2 per-cluster words [64] (queued operations | this cluster's trader round due << 31), X2 clock
+// words [4] (T, done, any_due)
+constexpr uint32_t kDmX2 = kDmRecWords * kDtResMaxClusters;
+constexpr uint32_t kDmX2Ctl = kDmX2 + kDtResMaxClusters;
+constexpr uint32_t kDmGranules = kDmX2Ctl + 4u;
+// gu (uncached): [0, 32) one placement granule per worker, [32] the failure word
+constexpr uint32_t kDmMaxWorkers = 32;  // one XCD's CUs
+constexpr uint32_t kDmFail = kDmMaxWorkers;
+static_assert(kDtResMaxClusters / kDmWaves + 1u <= kDmMaxWorkers, "workers on one XCD");
+constexpr uint64_t kDmTimeout = 100000000ull;  // s_memrealtime ticks (100 MHz): 1 s
+
+__device__ __forceinline__ void dm_put(unsigned long long* g, uint32_t tag, uint32_t v) {
+    const unsigned long long x = ((unsigned long long)tag << 32) | v;
+    asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(g), "v"(x) : "memory");
+}
+__device__ __forceinline__ unsigned long long dm_get(const unsigned long long* g) {
+    return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t dm_xcc() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 0xFu;
+}
+__device__ __forceinline__ void dm_fail(const DtResArgs& m, uint32_t why) {
+    __hip_atomic_store(m.gu + kDmFail, (unsigned long long)why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- a cluster wave: phases A and C of its cluster every tick, X1, X2 and the queued side effects ----
+__device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, const uint32_t c, const uint32_t lane,
+                                           unsigned long long* nodes, uint32_t* sfin, uint32_t* hist, float* dc,
+                                           float* dm, DtRec* rec) {
+    const uint32_t n0 = a.node_off[c], N = a.node_off[c + 1] - n0;
+    const uint64_t j0 = a.job_off[c];
+    const uint32_t J = (uint32_t)(a.job_off[c + 1] - j0);
+    const uint4* jobs = a.jobs + j0;
+    unsigned long long* l1cm = a.l1cm + j0;
+    unsigned long long* l1jd = a.l1jd + j0;
+    unsigned long long* l1al = a.l1al + j0;
+    const size_t sb = (size_t)c * a.S;
+    const uint32_t S = a.S;
+    DtCluster st = a.cl[c];
+    const DtCtl c0 = *a.ctl;
+    const bool due0 = a.tr[c].next_due <= c0.T;
+    uint32_t NN = N + st.nv;
+    // (the replayed step kernel's per-tick state in, once per launch)
+    unsigned long long snap_l = NN <= (uint32_t)kWave && lane < NN ? a.l1snap[(size_t)c * a.W + lane] : 0ull;
+    copy_rounds<4>(nodes, a.tn + n0, N, lane);
+    copy_rounds<2>(nodes + N, a.vn + (size_t)c * a.V, NN - N, lane);
+    copy_rounds<8>(sfin, a.sfin + sb, S, lane);
+    uint32_t T = c0.T;
+    bool done = c0.done != 0u;
+    bool any_due = a.period != 0u && c0.any_due != 0u;
+    bool due = any_due && due0;
+    unsigned long long* const gx = m.gx;
+    unsigned long long* const snap = dt_snap(a, c);
+    const unsigned long long* const ops =
+        reinterpret_cast<const unsigned long long*>(m.ops) + (size_t)c * m.ops_cap * (sizeof(DtOp) / 8u);
+    dt_wave_sync();
+#ifdef MCS_STAMPS
+    uint64_t dt_acc[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint64_t dt_last = 0;
+#endif
+    bool failed = false;
+    for (uint32_t it = 0; it < m.budget && !done; ++it) {
+        NN = N + st.nv;
+        const bool exact = NN <= (uint32_t)kWave;
+        if (!exact) snap_l = 0ull;  // (the replayed kernel loads it for exact clusters only)
+        bool snap_dirty = false;
+        st = dt_phase_a<true>(a, c, lane, T, N, NN, exact, j0, J, jobs, l1cm, l1jd, l1al, sb, S, nodes, sfin, hist, st,
+                              snap_l, snap_dirty DT_STAMP_ARGS);
+        (void)snap_dirty;  // (written back at the launch's end)
+        dt_sample<true>(a, c, lane, T, n0, N, NN, nodes, dc, dm, st);
+        // the record, and when a trader round is due the node snapshot and the contract sizes
+        if (any_due)
+            for (uint32_t i = lane; i < NN; i += kWave) snap[i < N ? i : a.NS + (i - N)] = nodes[i];
+        uint32_t fsc = 0, fsm = 0, fmd = 0, ssc = 0, ssm = 0, sst = 0;
+        dt_contracts<true>(due, lane, st.l1n, l1cm, l1jd, hist, fsc, fsm, fmd, ssc, ssm, sst);
+        if (lane == 0u) {
+            DtRec r;
+            r.cu = st.cu;
+            r.mu = st.mu;
+            r.avgw = st.avgw;
+            r.total_c = st.total_c;
+            r.total_m = st.total_m;
+            r.nv = st.nv;
+            r.N = N;
+            r.nfree = S - st.nrun;
+            r.flags = st.flags;
+            r.done = st.decided == J ? 1u : 0u;
+            r.queued = (st.l1n > 0u || st.next_arr > st.l0_head) ? 1u : 0u;
+            r.nxt = st.next_arr < J ? jobs[st.next_arr].x : kEmpty;
+            r.fc = fsc;
+            r.fm = fsm;
+            r.ft = fmd;
+            r.sc = ssc;
+            r.sm = ssm;
+            r.st = sst;
+            r.pad = 0u;
+            *rec = r;
+        }
+        dt_wave_sync();
+        if (any_due) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the snapshot lands before X1
+        const uint32_t tag1 = 2u * it + 1u, tag2 = tag1 + 1u;
+        if (lane < kDmRecWords)
+            dm_put(gx + (size_t)lane * kDtResMaxClusters + c, tag1, reinterpret_cast<const uint32_t*>(rec)[lane]);
+        // X2: lane 0 this cluster's word, lanes 1-3 the clock
+        const unsigned long long* src = gx + (lane == 0u ? kDmX2 + c : kDmX2Ctl + (lane < 4u ? lane - 1u : 0u));
+        uint32_t v = 0u;
+        const uint64_t t0 = wall_clock64();
+        for (;;) {
+            const unsigned long long x = lane < 4u ? dm_get(src) : ((unsigned long long)tag2 << 32);
+            v = (uint32_t)x;
+            if (__all((uint32_t)(x >> 32) == tag2)) break;
+            if (wall_clock64() - t0 > kDmTimeout) {
+                failed = true;
+                break;
+            }
+        }
+        if (failed) break;
+        const uint32_t w0 = readlane(v, 0u);
+        T = readlane(v, 1u);
+        done = readlane(v, 2u) != 0u;
+        any_due = a.period != 0u && readlane(v, 3u) != 0u;
+        due = any_due && (w0 >> 31) != 0u;
+        // phase D's side effects on this cluster, in the rounds' order (what dt_trader_kernel writes
+        // to the live state of a local cluster)
+        const uint32_t nops = w0 & 0x7FFFFFFFu;
+        for (uint32_t i = 0; i < nops; ++i) {
+            const unsigned long long* op = ops + (size_t)i * (sizeof(DtOp) / 8u);
+            const unsigned long long q0 = dm_get(op), q1 = dm_get(op + 1), q2 = dm_get(op + 2), q3 = dm_get(op + 3);
+            const uint32_t kind = (uint32_t)q0, nd = (uint32_t)(q0 >> 32);
+            if (kind == 1u) {  // go node.RunJob(Foreign) (cluster.go:116): the node and a running slot
+                const uint32_t fin = (uint32_t)q2;
+                uint32_t slot = kEmpty;
+                for (uint32_t b = 0; b < S; b += kWave) {
+                    const unsigned long long fr = __ballot(sfin[b + lane] == kEmpty);
+                    if (fr) {
+                        slot = b + (uint32_t)__builtin_ctzll(fr);
+                        break;
+                    }
+                }
+                if (slot != kEmpty) {
+                    if (lane == 0u) {
+                        nodes[nd] = q1;
+                        sfin[slot] = fin;
+                        a.snode[sb + slot] = nd;
+                        a.scm[sb + slot] = (q2 >> 32) | (q3 << 32);
+                    }
+                    ++st.nrun;
+                    st.minf = fin < st.minf ? fin : st.minf;
+                    st.l1_dirty = 1u;  // the commit may wrap a counter
+                }
+            } else if (kind == 2u) {  // AddVirtualNode (cluster.go:65-85)
+                if (lane == 0u) {
+                    nodes[N + nd] = q1;
+                    a.vcap[(size_t)c * a.V + nd] = make_uint2((uint32_t)q1, (uint32_t)(q1 >> 32));
+                }
+                ++st.nv;
+                st.l1_dirty = 1u;
+            } else {
+                st.flags |= MCS_FLAG_VNODE_OVERFLOW;
+            }
+            dt_wave_sync();
+        }
+    }
+    if (failed) {
+        if (lane == 0u) dm_fail(m, 2u);
+        return;
+    }
+    // the state out, for the next launch and the engine's readers
+    dt_wave_sync();
+    if (lane == 0u) a.cl[c] = st;
+    NN = N + st.nv;
+    copy_rounds<4>(a.tn + n0, nodes, N, lane);
+    copy_rounds<2>(a.vn + (size_t)c * a.V, nodes + N, NN - N, lane);
+    copy_rounds<8>(a.sfin + sb, sfin, S, lane);
+    if (NN <= (uint32_t)kWave && lane < NN) a.l1snap[(size_t)c * a.W + lane] = snap_l;
+}
+
+// ---- the trader wave: X1, phase D (the rounds and the next tick), X2 ----
+__device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, const uint32_t lane, DtTrader* trs,
+                                          DtRec* srec, uint32_t* appr, uint32_t* nvs, uint32_t* nfr, uint32_t* opn) {
+    const uint32_t Ct = a.Ct;
+    for (uint32_t q = lane; q < Ct; q += kWave) trs[q] = a.tr[q];
+    DtCtl c0 = *a.ctl;
+    dt_wave_sync();
+    if (c0.done) return;
+    unsigned long long n_trades = c0.n_trades, n_won = c0.n_won, n_for = c0.n_foreign;
+    unsigned long long* const gx = m.gx;
+    DtOp* const ops = reinterpret_cast<DtOp*>(m.ops);
+    bool failed = false;
+    for (uint32_t it = 0; it < m.budget; ++it) {
+        const uint32_t T = c0.T;
+        const bool any_due = c0.any_due != 0u;
+        const uint32_t tag1 = 2u * it + 1u, tag2 = tag1 + 1u;
+        // X1: lane q gathers cluster q's record
+        uint32_t w[kDmRecWords];
+        const uint64_t t0 = wall_clock64();
+        for (;;) {
+            bool ok = true;
+#pragma unroll
+            for (uint32_t k = 0; k < kDmRecWords; ++k) {
+                const unsigned long long x = lane < Ct ? dm_get(gx + (size_t)k * kDtResMaxClusters + lane)
+                                                       : ((unsigned long long)tag1 << 32);
+                w[k] = (uint32_t)x;
+                ok = ok && (uint32_t)(x >> 32) == tag1;
+            }
+            if (__all(ok)) break;
+            if (wall_clock64() - t0 > kDmTimeout) {
+                failed = true;
+                break;
+            }
+        }
+        if (failed) break;
+        if (lane < Ct) {
+            uint32_t* d = reinterpret_cast<uint32_t*>(&srec[lane]);
+#pragma unroll
+            for (uint32_t k = 0; k < kDmRecWords; ++k) d[k] = w[k];
+            nvs[lane] = srec[lane].nv;
+            nfr[lane] = srec[lane].nfree;
+            opn[lane] = 0u;
+        }
+        dt_wave_sync();
+        const DtCounts k = dt_rounds<true>(a, lane, T, any_due, trs, srec, appr, nvs, nfr,
+                                           DtCounts{n_trades, n_won, n_for, 0u}, DtOpQueue{ops, opn, m.ops_cap});
+        n_trades = k.n_trades;
+        n_won = k.n_won;
+        n_for = k.n_for;
+        const uint32_t lflags = k.lflags;
+        const DtCtl nc = dt_next_ctl(a, lane, c0, trs, srec, lflags, n_trades, n_won, n_for);
+        dt_wave_sync();
+        const uint32_t on = lane < Ct ? opn[lane] : 0u;
+        if (__ballot(on > m.ops_cap)) {  // (the run fails over; the cluster waves time out)
+            failed = true;
+            break;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the operations and snapshot writes before X2
+        if (lane < Ct) dm_put(gx + kDmX2 + lane, tag2, on | (trs[lane].next_due <= nc.T ? 0x80000000u : 0u));
+        if (lane < 3u) dm_put(gx + kDmX2Ctl + lane, tag2, lane == 0u ? nc.T : (lane == 1u ? nc.done : nc.any_due));
+        c0 = nc;
+        if (nc.done) break;
+    }
+    if (failed) {
+        if (lane == 0u) dm_fail(m, 3u);
+        return;
+    }
+    dt_wave_sync();
+    for (uint32_t q = lane; q < Ct; q += kWave) {
+        a.tr[q] = trs[q];
+        a.nv_all[q] = nvs[q];
+    }
+    if (lane == 0u) *a.ctl = c0;
+}
+
+__global__ __launch_bounds__(kDmThreads) void dt_mw_kernel(DtArgs a, DtResArgs m) {
+    // the workers are blocks 0, 8, 16, ...: one XCD under the dispatcher's round-robin placement
+    if (blockIdx.x % 8u != 0u) return;
+    __shared__ unsigned long long s_nodes[kDmWaves][kDtResMaxNN];
+    __shared__ uint32_t s_sfin[kDmWaves][kDtResMaxSlots];
+    __shared__ uint32_t s_hist[kDmWaves][kWave];
+    __shared__ float s_dcm[kDmWaves][2 * kDtResMaxNN];  // the sample's per-node differences
+    __shared__ DtRec s_rec[kDmWaves];
+    __shared__ DtTrader s_trs[kDtResMaxClusters];
+    __shared__ DtRec s_srec[kDtResMaxClusters];
+    __shared__ uint32_t s_appr[kDtResMaxClusters], s_nvs[kDtResMaxClusters], s_nfr[kDtResMaxClusters],
+        s_opn[kDtResMaxClusters];
+    __shared__ uint32_t s_ok;
+    const uint32_t wg = blockIdx.x / 8u, lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t nw = m.nwg + 1u;  // the cluster workgroups and the trader's
+    const bool trader = wg == m.nwg;
+    if (trader && wave != 0u) return;
+    // the placement: every worker publishes its XCD (uncached memory: valid on any XCD)
+    if (wave == 0u) {
+        if (lane == 0u)
+            __hip_atomic_store(m.gu + wg, (1ull << 32) | dm_xcc(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = false;
+        uint32_t v = 0u;
+        const uint64_t t0 = wall_clock64();
+        for (;;) {
+            const unsigned long long x =
+                lane < nw ? __hip_atomic_load(m.gu + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (1ull << 32);
+            v = (uint32_t)x;
+            if (__all((uint32_t)(x >> 32) == 1u)) {
+                ok = true;
+                break;
+            }
+            if (wall_clock64() - t0 > kDmTimeout) break;
+        }
+        const uint32_t v0 = readlane(v, 0u);
+        const bool same = ok && __all(lane >= nw || v == v0);
+        if (!same && lane == 0u) dm_fail(m, 1u);
+        if (lane == 0u) s_ok = same ? 1u : 0u;
+    }
+    if (!trader) __syncthreads();  // (the trader's workgroup is its wave 0 alone)
+    if (s_ok == 0u) return;
+    if (trader) {
+        dm_trader(a, m, lane, s_trs, s_srec, s_appr, s_nvs, s_nfr, s_opn);
+        return;
+    }
+    const uint32_t c = wg * kDmWaves + wave;
+    if (c >= a.C) return;
+    dm_cluster(a, m, c, lane, s_nodes[wave], s_sfin[wave], s_hist[wave], s_dcm[wave], s_dcm[wave] + kDtResMaxNN,
+               &s_rec[wave]);
+}
+
+}  // namespace
+
+size_t dtrade_mw_gx_bytes() { return (size_t)kDmGranules * 8u; }
+size_t dtrade_mw_gu_bytes() { return (size_t)(kDmFail + 1u) * 8u; }
+size_t dtrade_mw_op_bytes() { return sizeof(DtOp); }
+uint32_t dtrade_mw_fail_word() { return kDmFail; }
+
+hipError_t launch_dtrade_mw(const DtArgs& a, const DtResArgs& m, hipStream_t s) {
+    if (a.Ct != a.C || a.C > kDtResMaxClusters || a.S > kDtResMaxSlots || m.nwg != (a.C + kDmWaves - 1) / kDmWaves)
+        return hipErrorInvalidValue;
+    hipError_t st = hipMemsetAsync(m.gx, 0, dtrade_mw_gx_bytes(), s);
+    if (st != hipSuccess) return st;
+    st = hipMemsetAsync(m.gu, 0, dtrade_mw_gu_bytes(), s);
+    if (st != hipSuccess) return st;
+    hipLaunchKernelGGL(dt_mw_kernel, dim3(8u * m.nwg + 1u), dim3(kDmThreads), 0, s, a, m);
+    return hipGetLastError();
+}
+
+}  // namespace mcs

@@ -252,15 +252,18 @@ def test_gpu_dtrade_fuzz(shape, seed, J):
         np.testing.assert_array_equal(g["ds"][f], o["stats"][f], err_msg=f)
 
 
+@pytest.mark.parametrize("form", ["res", "graph"])
 @pytest.mark.parametrize("kind,C,J", [("small", 64, 500), ("big", 8, 800), ("n64_hot", 8, 1500), ("small", 16, 3000)])
-def test_gpu_dtrade_level1_rows_equal_oracle(kind, C, J):
+def test_gpu_dtrade_level1_rows_equal_oracle(kind, C, J, form, monkeypatch):
     """The Level1 pass over the list with holes (DtRow summaries: only rows where a job may fit are
     visited job by job, the others take their JobsMap moves in O(1)) equals the oracle's compacted
     slice on every output: placements, contracts, Foreign jobs, virtual nodes and the WaitTime sums
-    (exact clusters through the grown-node test, "big" ones through the histogram filter)."""
+    (exact clusters through the grown-node test, "big" ones through the histogram filter), in the
+    resident tick (mcs_dtrade_mw.hip, loop_form 5) and the replayed kernels (MCS_DT_RESIDENT=0, 0)."""
+    monkeypatch.setenv("MCS_DT_RESIDENT", "1" if form == "res" else "0")
     arrays, streams, _ = seeded_workload(kind, C, J)
     g = run(arrays, streams)
-    assert g["ts"]["loop_form"] == 0
+    assert g["ts"]["loop_form"] == (5 if form == "res" else 0)
     o = O.dtrade_run(arrays, streams)
     for k in ("node", "start", "finish"):
         np.testing.assert_array_equal(g[k], o[k], err_msg=k)
@@ -273,10 +276,14 @@ def test_gpu_dtrade_level1_rows_equal_oracle(kind, C, J):
     assert g["ts"]["t_final"] == o["t_final"]
 
 
-def test_gpu_dtrade_learned_capacity():
+@pytest.mark.parametrize("form", ["res", "graph"])
+def test_gpu_dtrade_learned_capacity(form, monkeypatch):
     """C5-DELAY's own system (64 cluster_small clusters x 2000 jobs) peaks at 331 running jobs in one
     cluster: the first run overflows the 256 auto slots and escalates by half to 384; a second run of
-    the same inputs starts at the learned 384 (no overflowed run), and both equal the oracle."""
+    the same inputs starts at the learned 384 (no overflowed run), and both equal the oracle; in the
+    resident tick (loop_form 5) and the replayed kernels (0)."""
+    monkeypatch.setenv("MCS_DT_RESIDENT", "1" if form == "res" else "0")
+    lf = 5 if form == "res" else 0
     arrays, streams, _ = seeded_workload("small", 64, 2000)
     with Engine(0, policy="DELAY", trader=True) as eng:
         eng.load_clusters(arrays)
@@ -287,8 +294,8 @@ def test_gpu_dtrade_learned_capacity():
         st2 = eng.run()
         ts2 = eng.trade_stats()
         n2, s2, f2 = eng.placements()
-    assert st1.escalations == 1 and st1.slot_pool == 6 and ts1["loop_form"] == 0
-    assert st2.escalations == 0 and st2.slot_pool == 6 and ts2["loop_form"] == 0
+    assert st1.escalations == 1 and st1.slot_pool == 6 and ts1["loop_form"] == lf
+    assert st2.escalations == 0 and st2.slot_pool == 6 and ts2["loop_form"] == lf
     for a, b in ((n1, n2), (s1, s2), (f1, f2)):
         np.testing.assert_array_equal(a, b)
     o = O.dtrade_run(arrays, streams)
@@ -296,3 +303,70 @@ def test_gpu_dtrade_learned_capacity():
     np.testing.assert_array_equal(s1, o["start"])
     np.testing.assert_array_equal(f1, o["finish"])
     assert ts1["t_final"] == o["t_final"]
+
+
+def check_equal(g, o):
+    """every output of two runs of one system (run() dicts), bit for bit"""
+    for k in ("node", "start", "finish"):
+        np.testing.assert_array_equal(g[k], o[k], err_msg=k)
+    assert g["trades"].tobytes() == o["trades"].tobytes()
+    assert g["foreign"].tobytes() == o["foreign"].tobytes()
+    assert g["vnodes"] == o["vnodes"]
+    for f in ("total_wait_ms", "jobs_count", "moved_l1", "placed_l1"):
+        np.testing.assert_array_equal(g["ds"][f], o["ds"][f], err_msg=f)
+    for f in ("t_final", "ticks", "trades", "trades_won", "flags"):
+        assert g["ts"][f] == o["ts"][f], f
+
+
+@pytest.mark.parametrize("ticks", ["65536", "7"])
+@pytest.mark.parametrize("case", ["small:64:500", "n64_hot:8:1500", "big:8:800", "small:16:3000", "n64_hot:61:400",
+                                  "fuzz:w16s:4:900", "fuzz:mid:8:1500", "fuzz:w16s:6:1500"])
+def test_gpu_dtrade_resident_equals_replayed(case, ticks, monkeypatch):
+    """The resident tick (mcs_dtrade_mw.hip, loop_form 5: one wave per cluster keeping its nodes,
+    slots and state on chip across ticks, a trader wave, granule exchange in one XCD's L2) == the
+    replayed two-kernel tick (MCS_DT_RESIDENT=0, loop_form 0) on every output, and == the oracle's
+    placements; MCS_DT_RES_TICKS=7 ends a launch every 7 ticks (state out and back in)."""
+    p = case.split(":")
+    if p[0] == "fuzz":
+        arrays, streams = fuzz_workload(p[1], int(p[2]), n_clusters=8, J=int(p[3]), blocking=False)
+    else:
+        arrays, streams, _ = seeded_workload(p[0], int(p[1]), int(p[2]))
+    monkeypatch.setenv("MCS_DT_RESIDENT", "0")
+    b = run(arrays, streams)
+    assert b["ts"]["loop_form"] == 0
+    monkeypatch.setenv("MCS_DT_RESIDENT", "1")
+    monkeypatch.setenv("MCS_DT_RES_TICKS", ticks)
+    g = run(arrays, streams)
+    assert g["ts"]["loop_form"] == 5, g["ts"]["loop_form"]
+    check_equal(g, b)
+    o = O.dtrade_run(arrays, streams)
+    for k in ("node", "start", "finish"):
+        np.testing.assert_array_equal(g[k], o[k], err_msg=k)
+    assert g["ts"]["t_final"] == o["t_final"]
+
+
+@pytest.mark.parametrize("k", DT, ids=[k["name"] for k in DT])
+def test_gpu_dtrade_kats_resident(k, monkeypatch):
+    """The DELAY trading KATs through the resident tick (loop_form 5), 3 ticks per launch."""
+    monkeypatch.setenv("MCS_DT_RESIDENT", "1")
+    monkeypatch.setenv("MCS_DT_RES_TICKS", "3")
+    arrays, s = dt_system(k)
+    r = run(arrays, s, t_max_s=k["t_max"])
+    assert r["ts"]["loop_form"] == 5, r["ts"]["loop_form"]
+    check_kat(k, r["node"], r["start"], r["finish"], r["trades"], r["foreign"], len(r["foreign"]), r["vnodes"],
+              r["ts"]["t_final"])
+
+
+def test_gpu_dtrade_resident_fail_over(monkeypatch):
+    """A resident launch that fails over (forced after the first launch by MCS_DT_RES_FORCE_FAIL=1;
+    in production: workers not all on one XCD, or an exchange timeout) redoes the run on the
+    replayed kernels (loop_form 6) with the same results."""
+    arrays, streams, _ = seeded_workload("n64_hot", 8, 1500)
+    monkeypatch.setenv("MCS_DT_RESIDENT", "0")
+    b = run(arrays, streams)
+    monkeypatch.setenv("MCS_DT_RESIDENT", "1")
+    monkeypatch.setenv("MCS_DT_RES_TICKS", "5")
+    monkeypatch.setenv("MCS_DT_RES_FORCE_FAIL", "1")
+    g = run(arrays, streams)
+    assert g["ts"]["loop_form"] == 6, g["ts"]["loop_form"]
+    check_equal(g, b)
