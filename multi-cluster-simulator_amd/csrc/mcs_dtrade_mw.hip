@@ -46,6 +46,18 @@ constexpr uint32_t kDmFail = kDmMaxWorkers;
 static_assert(kDtResMaxClusters / kDmWaves + 1u <= kDmMaxWorkers, "workers on one XCD");
 constexpr uint64_t kDmTimeout = 100000000ull;  // s_memrealtime ticks (100 MHz): 1 s
 
+#ifdef MCS_STAMPS
+// the probe build's tick timeline (s_memrealtime, 100 MHz), tools/stamp_dm.py: per cluster wave
+// [c][0..4] phase A, sample, record + snapshot + contracts + X1 put, the X2 wait, the side effects;
+// [c][5] ticks.  Per tick (ring of 1024, read and cleared by the trader after X1): [0] the slowest
+// wave's side effects of the previous tick + its work up to its X1 put, [1] the slowest phase A.
+// Trader sums: [0] X1 wait (from its X2 put), [1] the rounds, [2] next clock + X2 put, [3] ticks,
+// [4] the per-tick max [0] summed, [5] the per-tick max [1] summed
+__device__ unsigned long long g_dm_cl[kDtResMaxClusters][6];
+__device__ unsigned long long g_dm_tick[1024][2];
+__device__ unsigned long long g_dm_tr[8];
+#endif
+
 __device__ __forceinline__ void dm_put(unsigned long long* g, uint32_t tag, uint32_t v) {
     const unsigned long long x = ((unsigned long long)tag << 32) | v;
     asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(g), "v"(x) : "memory");
@@ -98,7 +110,13 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
     uint64_t dt_last = 0;
 #endif
     bool failed = false;
+#ifdef MCS_STAMPS
+    uint64_t sm[5] = {0, 0, 0, 0, 0}, sticks = 0, s_prev = wall_clock64(), s_ops = 0;
+#endif
     for (uint32_t it = 0; it < m.budget && !done; ++it) {
+#ifdef MCS_STAMPS
+        const uint64_t s0 = wall_clock64();
+#endif
         NN = N + st.nv;
         const bool exact = NN <= (uint32_t)kWave;
         if (!exact) snap_l = 0ull;  // (the replayed kernel loads it for exact clusters only)
@@ -106,7 +124,13 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
         st = dt_phase_a<true>(a, c, lane, T, N, NN, exact, j0, J, jobs, l1cm, l1jd, l1al, sb, S, nodes, sfin, hist, st,
                               snap_l, snap_dirty DT_STAMP_ARGS);
         (void)snap_dirty;  // (written back at the launch's end)
+#ifdef MCS_STAMPS
+        const uint64_t s1 = wall_clock64();
+#endif
         dt_sample<true>(a, c, lane, T, n0, N, NN, nodes, dc, dm, st);
+#ifdef MCS_STAMPS
+        const uint64_t s2 = wall_clock64();
+#endif
         // the record, and when a trader round is due the node snapshot and the contract sizes
         if (any_due)
             for (uint32_t i = lane; i < NN; i += kWave) snap[i < N ? i : a.NS + (i - N)] = nodes[i];
@@ -140,6 +164,16 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
         const uint32_t tag1 = 2u * it + 1u, tag2 = tag1 + 1u;
         if (lane < kDmRecWords)
             dm_put(gx + (size_t)lane * kDtResMaxClusters + c, tag1, reinterpret_cast<const uint32_t*>(rec)[lane]);
+#ifdef MCS_STAMPS
+        const uint64_t s3 = wall_clock64();
+        if (lane == 0u) {
+            atomicMax(&g_dm_tick[it & 1023u][0], (unsigned long long)(s_ops + (s3 - s0)));
+            atomicMax(&g_dm_tick[it & 1023u][1], (unsigned long long)(s1 - s0));
+        }
+        sm[0] += s1 - s0;
+        sm[1] += s2 - s1;
+        sm[2] += s3 - s2;
+#endif
         // X2: lane 0 this cluster's word, lanes 1-3 the clock
         const unsigned long long* src = gx + (lane == 0u ? kDmX2 + c : kDmX2Ctl + (lane < 4u ? lane - 1u : 0u));
         uint32_t v = 0u;
@@ -154,6 +188,10 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
             }
         }
         if (failed) break;
+#ifdef MCS_STAMPS
+        const uint64_t s4 = wall_clock64();
+        sm[3] += s4 - s3;
+#endif
         const uint32_t w0 = readlane(v, 0u);
         T = readlane(v, 1u);
         done = readlane(v, 2u) != 0u;
@@ -199,7 +237,20 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
             }
             dt_wave_sync();
         }
+#ifdef MCS_STAMPS
+        s_prev = wall_clock64();
+        s_ops = s_prev - s4;
+        sm[4] += s_ops;
+        ++sticks;
+#endif
     }
+#ifdef MCS_STAMPS
+    (void)s_prev;
+    if (lane == 0u) {
+        for (int i = 0; i < 5; ++i) atomicAdd(&g_dm_cl[c][i], (unsigned long long)sm[i]);
+        atomicAdd(&g_dm_cl[c][5], (unsigned long long)sticks);
+    }
+#endif
     if (failed) {
         if (lane == 0u) dm_fail(m, 2u);
         return;
@@ -226,6 +277,9 @@ __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, c
     unsigned long long* const gx = m.gx;
     DtOp* const ops = reinterpret_cast<DtOp*>(m.ops);
     bool failed = false;
+#ifdef MCS_STAMPS
+    uint64_t tsum[6] = {0, 0, 0, 0, 0, 0}, t_put = wall_clock64();
+#endif
     for (uint32_t it = 0; it < m.budget; ++it) {
         const uint32_t T = c0.T;
         const bool any_due = c0.any_due != 0u;
@@ -249,6 +303,13 @@ __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, c
             }
         }
         if (failed) break;
+#ifdef MCS_STAMPS
+        const uint64_t t1 = wall_clock64();
+        tsum[0] += t1 - t_put;
+        if (lane < 2u)  // (lane 0 sums the tick's [0], lane 1 its [1])
+            tsum[4] += __hip_atomic_exchange(&g_dm_tick[it & 1023u][lane], 0ull, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+#endif
         if (lane < Ct) {
             uint32_t* d = reinterpret_cast<uint32_t*>(&srec[lane]);
 #pragma unroll
@@ -258,8 +319,15 @@ __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, c
             opn[lane] = 0u;
         }
         dt_wave_sync();
+#ifdef MCS_STAMPS
+        const uint64_t t2 = wall_clock64();
+#endif
         const DtCounts k = dt_rounds<true>(a, lane, T, any_due, trs, srec, appr, nvs, nfr,
                                            DtCounts{n_trades, n_won, n_for, 0u}, DtOpQueue{ops, opn, m.ops_cap});
+#ifdef MCS_STAMPS
+        const uint64_t t3 = wall_clock64();
+        tsum[1] += t3 - t2;
+#endif
         n_trades = k.n_trades;
         n_won = k.n_won;
         n_for = k.n_for;
@@ -274,6 +342,11 @@ __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, c
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the operations and snapshot writes before X2
         if (lane < Ct) dm_put(gx + kDmX2 + lane, tag2, on | (trs[lane].next_due <= nc.T ? 0x80000000u : 0u));
         if (lane < 3u) dm_put(gx + kDmX2Ctl + lane, tag2, lane == 0u ? nc.T : (lane == 1u ? nc.done : nc.any_due));
+#ifdef MCS_STAMPS
+        t_put = wall_clock64();
+        tsum[2] += t_put - t3;
+        tsum[3] += 1u;
+#endif
         c0 = nc;
         if (nc.done) break;
     }
@@ -281,6 +354,11 @@ __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, c
         if (lane == 0u) dm_fail(m, 3u);
         return;
     }
+#ifdef MCS_STAMPS
+    if (lane == 0u)
+        for (int i = 0; i < 4; ++i) atomicAdd(&g_dm_tr[i], (unsigned long long)tsum[i]);
+    if (lane < 2u) atomicAdd(&g_dm_tr[4 + lane], (unsigned long long)tsum[4]);
+#endif
     dt_wave_sync();
     for (uint32_t q = lane; q < Ct; q += kWave) {
         a.tr[q] = trs[q];
@@ -346,6 +424,29 @@ size_t dtrade_mw_gx_bytes() { return (size_t)kDmGranules * 8u; }
 size_t dtrade_mw_gu_bytes() { return (size_t)(kDmFail + 1u) * 8u; }
 size_t dtrade_mw_op_bytes() { return sizeof(DtOp); }
 uint32_t dtrade_mw_fail_word() { return kDmFail; }
+
+}  // namespace mcs
+
+// the probe build's tick timeline (g_dm_cl [64][6] then g_dm_tr [8]), read and cleared; -2 in the
+// product build
+extern "C" int mcs_debug_dm_stamps(unsigned long long* out) {
+#ifdef MCS_STAMPS
+    static unsigned long long z[mcs::kDtResMaxClusters * 6 + 8];
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_dm_cl), sizeof(mcs::g_dm_cl)) != hipSuccess ||
+        hipMemcpyFromSymbol(out + mcs::kDtResMaxClusters * 6, HIP_SYMBOL(mcs::g_dm_tr), sizeof(mcs::g_dm_tr)) !=
+            hipSuccess)
+        return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_dm_cl), z, sizeof(mcs::g_dm_cl)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_dm_tr), z, sizeof(mcs::g_dm_tr)) != hipSuccess)
+        return -1;
+    return 0;
+#else
+    (void)out;
+    return -2;
+#endif
+}
+
+namespace mcs {
 
 hipError_t launch_dtrade_mw(const DtArgs& a, const DtResArgs& m, hipStream_t s) {
     if (a.Ct != a.C || a.C > kDtResMaxClusters || a.S > kDtResMaxSlots || m.nwg != (a.C + kDmWaves - 1) / kDmWaves)
