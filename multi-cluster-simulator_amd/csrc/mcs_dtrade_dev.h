@@ -87,8 +87,10 @@ __device__ unsigned long long g_dt_stamps[8];
 __device__ unsigned long long g_dt_cur[8];
 __device__ unsigned long long g_dt_maxsum[10];
 // inside the Level1 pass, summed over every row of every pass: [0] the fit tests and placements,
-// [1] the WaitTime and compaction bookkeeping, [2] rows, [3] placements
-__device__ unsigned long long g_dt_rows[4];
+// [1] the WaitTime and compaction bookkeeping, [2] rows, [3] placements (of the general rows);
+// [4] quiet rows, [5] passes, [6] candidates given a first fit, [7] the passes' time; of which
+// [8] before the row loop, [9] the row loop, [10] after it
+__device__ unsigned long long g_dt_rows[12];
 #define DT_MARK(i)                                  \
     do {                                            \
         const uint64_t dt_now = wall_clock64();     \
@@ -184,6 +186,8 @@ __device__ __forceinline__ DtCluster dt_phase_a(const DtArgs& a, const uint32_t 
 
     // the Level1 pass's first rows, in flight from here (vmcnt waits in issue order: a load issued
     // before the copies, the releases or the arrivals would be drained by their waits)
+    // (8 or 12 rows ahead in the resident tick measured slower: 10.85 -> 11.03 / 11.37 us per C5-DELAY
+    // tick, profiles/r06_dm/ab_ahead.txt)
     constexpr int kL1Ahead = 4;
     unsigned long long pcm[kL1Ahead], pjd[kL1Ahead], pal[kL1Ahead];
     // (every lane loads, at an index clamped into the list: a load under a lane condition ends in a
@@ -251,6 +255,9 @@ __device__ __forceinline__ DtCluster dt_phase_a(const DtArgs& a, const uint32_t 
         st.s_last = (unsigned long long)st.l1n * T;
         st.t_all = T;
     } else if (st.l1n != 0u) {
+#ifdef MCS_STAMPS
+        const uint64_t pt0 = wall_clock64();
+#endif
         // bigger clusters: exact fit filter (see mcs_delay.hip): lane l holds the max free memory
         // over nodes with min(free cores, 63) >= l; conservative for wrapped counters
         uint32_t best = 0u, max_c = 0u;
@@ -331,10 +338,13 @@ __device__ __forceinline__ DtCluster dt_phase_a(const DtArgs& a, const uint32_t 
         uint32_t wr = 0;
         bool carry_skip = false;  // the last entry of the previous row was placed
         const uint32_t n1 = st.l1n, t_all = st.t_all;
-        // per-lane partial sums of the JobsMap moves and of the kept entries' last examinations,
-        // reduced once after the sweep (a wave reduction per row would serialise the pass)
-        long long tot_l = 0ll;
-        unsigned long long snew_l = 0ull;
+        // WaitTime in closed form: s_last is the sum of every entry's effective last examination, so
+        // the pass's JobsMap moves are 1000 * (n_examined * T - (s_last - the skipped entries' sum))
+        // and the kept entries' new sum is (kept - skipped) * T + the skipped entries' sum; only the
+        // entries a D6 skip passes over (general rows) need their own stamp (per-lane partial sum,
+        // reduced once after the sweep), and a quiet row does no WaitTime arithmetic
+        unsigned long long sk_eff = 0ull;
+        uint32_t n_skip = 0;
         // rows of 64 entries; each row's three coalesced loads are issued kL1Ahead rows ahead (the
         // first ones before the pass), so a row's HBM latency hides behind the rows before it
         // (compaction writes only at or below the row in hand: never into a prefetched row)
@@ -368,6 +378,9 @@ __device__ __forceinline__ DtCluster dt_phase_a(const DtArgs& a, const uint32_t 
                     const uint32_t b = (uint32_t)__builtin_ctzll(fitm);
                     const uint32_t jc = readlane(jc_l, b), jm = readlane(jm_l, b);
                     const uint32_t k = first_fit(jc, jm);
+#ifdef MCS_STAMPS
+                    if (lane == 0) atomicAdd(&g_dt_rows[6], 1ull);
+#endif
                     if (k == kEmpty) {  // an untested job that fits no node after all
                         from = b + 1u;
                         continue;
@@ -441,8 +454,8 @@ __device__ __forceinline__ DtCluster dt_phase_a(const DtArgs& a, const uint32_t 
             // the entry's last examination: its own stamp while it is marked untested (a D6 skip
             // materialised it), else the later of the stamp and the list's floor t_all
             const uint32_t eff = ((uint32_t)jdv >> 31) != 0u ? sl : (sl > t_all ? sl : t_all);
-            const long long delta = examined ? (long long)(T - eff) * 1000ll : 0ll;
-            tot_l += delta;
+            sk_eff += live && !examined ? (unsigned long long)eff : 0ull;
+            n_skip += (uint32_t)__builtin_popcountll(skipm & livem);
             // compaction in the same sweep (append(Level1[:i], Level1[i+1:]...), :319)
             const unsigned long long kept = livem & ~placedm;
             const uint32_t nl = examined ? T : eff;  // the kept entry's last examination
@@ -466,7 +479,6 @@ __device__ __forceinline__ DtCluster dt_phase_a(const DtArgs& a, const uint32_t 
                 // more SGPR spills: rows with a candidate are rare, quiet rows skip the store)
                 if (np != pos || nl != sl) l1al[np] = (al & 0xFFFFFFFFull) | ((unsigned long long)nl << 32);
             }
-            snew_l += live && !placed ? (unsigned long long)nl : 0ull;
             wr += (uint32_t)__builtin_popcountll(kept);
 #ifdef MCS_STAMPS
             if (lane == 0) {
@@ -479,36 +491,24 @@ __device__ __forceinline__ DtCluster dt_phase_a(const DtArgs& a, const uint32_t 
             return true;
         };
         // a quiet row: no job of it fits now (none fits a grown node, none is untested) and its first
-        // job is examined (no skip carried in): only the WaitTime and compaction bookkeeping, as the
-        // general row does it with nothing placed (the live jobs are a prefix: rank = lane)
+        // job is examined (no skip carried in): only the compaction, as the general row does it with
+        // nothing placed (the live jobs are a prefix: rank = lane; the shift wr0 - base is uniform, no
+        // entry is untested, and a moved entry keeps its stamp: its last examination is the floor
+        // t_all = T set after the pass)
         auto quiet_row = [&](const uint32_t base, const unsigned long long cm, const unsigned long long jdv,
                              const unsigned long long al, const uint32_t wr0) {
-            const uint32_t pos = base + lane;
-            const bool live = pos < n1;
-            const uint32_t sl = (uint32_t)(al >> 32);
-            const uint32_t eff = sl > t_all ? sl : t_all;
-            tot_l += live ? (long long)(T - eff) * 1000ll : 0ll;
-            snew_l += live ? (unsigned long long)T : 0ull;
-            if (live) {
+            if (wr0 != base && base + lane < n1) {
                 const uint32_t np = wr0 + lane;
-                const unsigned long long jdn = jdv & ~0x80000000ull;
-                if (np != pos) {
-                    l1cm[np] = cm;
-                    l1jd[np] = jdn;
-                } else if (jdn != jdv) {
-                    l1jd[np] = jdn;
-                }
-                if (np != pos) l1al[np] = (al & 0xFFFFFFFFull) | ((unsigned long long)T << 32);
+                l1cm[np] = cm;
+                l1jd[np] = jdv;
+                l1al[np] = al;
             }
-        };
-        // is the row quiet?  (every lane active: the test reads across lanes)
-        auto is_quiet = [&](const uint32_t base, const unsigned long long cm, const unsigned long long jdv) -> bool {
-            const bool live = base + lane < n1;
-            const bool f = g_fit((uint32_t)cm, (uint32_t)(cm >> 32)) || ((uint32_t)jdv >> 31) != 0u;
-            return __ballot(live && f) == 0ull;
         };
         const bool quiet_ok = exact && !g_all;
         bool ok_pass = true;
+#ifdef MCS_STAMPS
+        const uint64_t pt1 = wall_clock64();
+#endif
         // rows in pairs: two quiet rows are tested and booked together (independent instruction
         // streams for the one wave of the CU); a row with a candidate, or with a skip carried into
         // it, goes through row()  (r04: 19.2 -> 17.1 us per C5-DELAY tick; testing and booking a
@@ -530,10 +530,15 @@ __device__ __forceinline__ DtCluster dt_phase_a(const DtArgs& a, const uint32_t 
                 pal[r + 1] = l1al[nib];
                 const bool has_b = bb < n1;
                 bool qa = false, qb = false;
-                if (quiet_ok && !carry_skip) {
-                    qa = is_quiet(ba, cma, jda);
-                    qb = has_b && is_quiet(bb, cmb, jdb);
+                if (quiet_ok && !carry_skip) {  // (both rows' permutes in flight together)
+                    const bool fa = g_fit((uint32_t)cma, (uint32_t)(cma >> 32)) || ((uint32_t)jda >> 31) != 0u;
+                    const bool fb = g_fit((uint32_t)cmb, (uint32_t)(cmb >> 32)) || ((uint32_t)jdb >> 31) != 0u;
+                    qa = __ballot(ba + lane < n1 && fa) == 0ull;
+                    qb = has_b && __ballot(bb + lane < n1 && fb) == 0ull;
                 }
+#ifdef MCS_STAMPS
+                if (lane == 0 && (qa || qb)) atomicAdd(&g_dt_rows[4], (unsigned long long)(qa ? 1 : 0) + (qa && qb ? 1 : 0));
+#endif
                 if (qa) {
                     const uint32_t ka = n1 - ba < (uint32_t)kWave ? n1 - ba : (uint32_t)kWave;
                     quiet_row(ba, cma, jda, ala, wr);
@@ -547,15 +552,31 @@ __device__ __forceinline__ DtCluster dt_phase_a(const DtArgs& a, const uint32_t 
                 }
             }
         }
+#ifdef MCS_STAMPS
+        const uint64_t pt2 = wall_clock64();
+#endif
         st.l1n = wr;
-        st.total += dt_wave_sum_i64(tot_l);
-        st.s_last = (unsigned long long)dt_wave_sum_i64((long long)snew_l);
+        {
+            const unsigned long long s_sk = (unsigned long long)dt_wave_sum_i64((long long)sk_eff);
+            st.total += 1000ll * ((long long)(n1 - n_skip) * (long long)T - (long long)(st.s_last - s_sk));
+            st.s_last = (unsigned long long)(wr - n_skip) * T + s_sk;
+        }
         st.t_all = T;  // every entry examined at T: its stamp is not rewritten (the skipped ones are marked)
         st.l1_dirty = wr != n1 ? 1u : 0u;  // a pass that placed: its skipped entries come next
         if (exact) {  // the jobs left failed every node as they are now
             snap_l = lane < NN ? nodes[lane] : 0ull;
             snap_dirty = true;
         }
+#ifdef MCS_STAMPS
+        if (lane == 0) {
+            const uint64_t pt3 = wall_clock64();
+            atomicAdd(&g_dt_rows[8], (unsigned long long)(pt1 - pt0));
+            atomicAdd(&g_dt_rows[9], (unsigned long long)(pt2 - pt1));
+            atomicAdd(&g_dt_rows[10], (unsigned long long)(pt3 - pt2));
+            atomicAdd(&g_dt_rows[5], 1ull);
+            atomicAdd(&g_dt_rows[7], (unsigned long long)(pt3 - pt0));
+        }
+#endif
     }
 
     DT_MARK(3);

@@ -49,13 +49,15 @@ constexpr uint64_t kDmTimeout = 100000000ull;  // s_memrealtime ticks (100 MHz):
 #ifdef MCS_STAMPS
 // the probe build's tick timeline (s_memrealtime, 100 MHz), tools/stamp_dm.py: per cluster wave
 // [c][0..4] phase A, sample, record + snapshot + contracts + X1 put, the X2 wait, the side effects;
-// [c][5] ticks.  Per tick (ring of 1024, read and cleared by the trader after X1): [0] the slowest
-// wave's side effects of the previous tick + its work up to its X1 put, [1] the slowest phase A.
+// [c][5] ticks.  Per tick (ring of 1024, read and cleared by the trader after X1), each the slowest
+// wave's: [0] side effects of the previous tick + work up to the X1 put, [1] phase A, [2] releases,
+// [3] arrivals (+ the pass's first loads), [4] the Level1 pass, [5] the Level0 head, [6] the sample,
+// [7] record + snapshot + contracts + X1 put.
 // Trader sums: [0] X1 wait (from its X2 put), [1] the rounds, [2] next clock + X2 put, [3] ticks,
-// [4] the per-tick max [0] summed, [5] the per-tick max [1] summed
+// [6] ticks with a round due, [8 + i] the per-tick maxima [i] summed
 __device__ unsigned long long g_dm_cl[kDtResMaxClusters][6];
-__device__ unsigned long long g_dm_tick[1024][2];
-__device__ unsigned long long g_dm_tr[8];
+__device__ unsigned long long g_dm_tick[1024][8];
+__device__ unsigned long long g_dm_tr[16];
 #endif
 
 __device__ __forceinline__ void dm_put(unsigned long long* g, uint32_t tag, uint32_t v) {
@@ -116,6 +118,8 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
     for (uint32_t it = 0; it < m.budget && !done; ++it) {
 #ifdef MCS_STAMPS
         const uint64_t s0 = wall_clock64();
+        dt_last = s0;
+        const uint64_t p1 = dt_acc[1], p2 = dt_acc[2], p3 = dt_acc[3];
 #endif
         NN = N + st.nv;
         const bool exact = NN <= (uint32_t)kWave;
@@ -167,8 +171,15 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
 #ifdef MCS_STAMPS
         const uint64_t s3 = wall_clock64();
         if (lane == 0u) {
-            atomicMax(&g_dm_tick[it & 1023u][0], (unsigned long long)(s_ops + (s3 - s0)));
-            atomicMax(&g_dm_tick[it & 1023u][1], (unsigned long long)(s1 - s0));
+            unsigned long long* tk = g_dm_tick[it & 1023u];
+            atomicMax(&tk[0], (unsigned long long)(s_ops + (s3 - s0)));
+            atomicMax(&tk[1], (unsigned long long)(s1 - s0));
+            atomicMax(&tk[2], (unsigned long long)(dt_acc[1] - p1));
+            atomicMax(&tk[3], (unsigned long long)(dt_acc[2] - p2));
+            atomicMax(&tk[4], (unsigned long long)(dt_acc[3] - p3));
+            atomicMax(&tk[5], (unsigned long long)(s1 - dt_last));
+            atomicMax(&tk[6], (unsigned long long)(s2 - s1));
+            atomicMax(&tk[7], (unsigned long long)(s3 - s2));
         }
         sm[0] += s1 - s0;
         sm[1] += s2 - s1;
@@ -306,7 +317,7 @@ __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, c
 #ifdef MCS_STAMPS
         const uint64_t t1 = wall_clock64();
         tsum[0] += t1 - t_put;
-        if (lane < 2u)  // (lane 0 sums the tick's [0], lane 1 its [1])
+        if (lane < 8u)  // (lane i sums the tick's [i])
             tsum[4] += __hip_atomic_exchange(&g_dm_tick[it & 1023u][lane], 0ull, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
 #endif
@@ -346,6 +357,7 @@ __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, c
         t_put = wall_clock64();
         tsum[2] += t_put - t3;
         tsum[3] += 1u;
+        tsum[5] += any_due ? 1u : 0u;
 #endif
         c0 = nc;
         if (nc.done) break;
@@ -357,7 +369,8 @@ __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, c
 #ifdef MCS_STAMPS
     if (lane == 0u)
         for (int i = 0; i < 4; ++i) atomicAdd(&g_dm_tr[i], (unsigned long long)tsum[i]);
-    if (lane < 2u) atomicAdd(&g_dm_tr[4 + lane], (unsigned long long)tsum[4]);
+    if (lane == 0u) atomicAdd(&g_dm_tr[6], (unsigned long long)tsum[5]);
+    if (lane < 8u) atomicAdd(&g_dm_tr[8 + lane], (unsigned long long)tsum[4]);
 #endif
     dt_wave_sync();
     for (uint32_t q = lane; q < Ct; q += kWave) {
@@ -427,11 +440,11 @@ uint32_t dtrade_mw_fail_word() { return kDmFail; }
 
 }  // namespace mcs
 
-// the probe build's tick timeline (g_dm_cl [64][6] then g_dm_tr [8]), read and cleared; -2 in the
+// the probe build's tick timeline (g_dm_cl [64][6] then g_dm_tr [16]), read and cleared; -2 in the
 // product build
 extern "C" int mcs_debug_dm_stamps(unsigned long long* out) {
 #ifdef MCS_STAMPS
-    static unsigned long long z[mcs::kDtResMaxClusters * 6 + 8];
+    static unsigned long long z[mcs::kDtResMaxClusters * 6 + 16];
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_dm_cl), sizeof(mcs::g_dm_cl)) != hipSuccess ||
         hipMemcpyFromSymbol(out + mcs::kDtResMaxClusters * 6, HIP_SYMBOL(mcs::g_dm_tr), sizeof(mcs::g_dm_tr)) !=
             hipSuccess)
@@ -440,6 +453,17 @@ extern "C" int mcs_debug_dm_stamps(unsigned long long* out) {
         hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_dm_tr), z, sizeof(mcs::g_dm_tr)) != hipSuccess)
         return -1;
     return 0;
+#else
+    (void)out;
+    return -2;
+#endif
+}
+// the probe build's Level1 row counters of the resident tick (g_dt_rows [12]), read and cleared
+extern "C" int mcs_debug_dm_rows(unsigned long long* out) {
+#ifdef MCS_STAMPS
+    unsigned long long z[12] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_dt_rows), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_dt_rows), z, sizeof(z)) == hipSuccess ? 0 : -1;
 #else
     (void)out;
     return -2;

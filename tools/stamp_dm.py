@@ -20,11 +20,14 @@ eng = Engine(0, policy="DELAY", trader=True)
 eng.load_clusters(replicate(spec, 64))
 eng.generate_jobs(GenParams(seed=0x4D43535F53494D31), J)
 fn = L.lib().mcs_debug_dm_stamps
-buf = (C.c_ulonglong * (64 * 6 + 8))()
-eng.run(); assert fn(buf) == 0
-st = eng.run(); assert fn(buf) == 0
+buf = (C.c_ulonglong * (64 * 6 + 16))()
+rows = (C.c_ulonglong * 12)()
+fr = L.lib().mcs_debug_dm_rows
+eng.run(); assert fn(buf) == 0 and fr(rows) == 0
+st = eng.run(); assert fn(buf) == 0 and fr(rows) == 0
 ts = eng.trade_stats()
-print(json.dumps({"ms": st.kernel_ms, "ticks": int(ts["ticks"]), "loop_form": int(ts["loop_form"]), "s": list(buf)}))
+print(json.dumps({"ms": st.kernel_ms, "ticks": int(ts["ticks"]), "loop_form": int(ts["loop_form"]), "s": list(buf),
+                  "rows": list(rows)}))
 '''
 SEG = ["phase_a", "sample", "record+snapshot+contracts+x1_put", "x2_wait", "side_effects"]
 US = 10.0 / 1e3  # s_memrealtime ticks (100 MHz) -> us
@@ -41,7 +44,7 @@ def main():
     d = json.loads(out.stdout.strip().splitlines()[-1])
     s = d["s"]
     cl = [s[6 * c:6 * c + 6] for c in range(64)]
-    tr = s[64 * 6:64 * 6 + 8]
+    tr = s[64 * 6:64 * 6 + 16]
     nt = max(tr[3], 1)
     res = {"jobs_per_cluster": int(jobs), "ticks": d["ticks"], "loop_form": d["loop_form"],
            "us_per_tick": round(d["ms"] * 1e3 / d["ticks"], 3)}
@@ -52,9 +55,21 @@ def main():
     res["busiest_cluster_us_per_tick"] = {SEG[i]: round(busy[i], 3) for i in range(5)}
     res["trader_us_per_tick"] = {"x1_wait": round(tr[0] * US / nt, 3), "rounds": round(tr[1] * US / nt, 3),
                                  "next_clock+x2_put": round(tr[2] * US / nt, 3)}
-    res["per_tick_slowest_wave_work_us"] = round(tr[4] * US / nt, 3)
-    res["per_tick_slowest_phase_a_us"] = round(tr[5] * US / nt, 3)
-    res["exchange_us_per_tick"] = round((tr[0] - tr[4]) * US / nt, 3)
+    TSEG = ["work(side_effects+phase_a+sample+record)", "phase_a", "releases", "arrivals+first_row_loads",
+            "level1_pass", "level0_head", "sample", "record+snapshot+contracts+x1_put"]
+    res["per_tick_slowest_wave_us"] = {TSEG[i]: round(tr[8 + i] * US / nt, 3) for i in range(8)}
+    res["ticks_with_a_round_due"] = tr[6]
+    res["exchange_us_per_tick"] = round((tr[0] - tr[8]) * US / nt, 3)
+    rw = d["rows"]
+    np_ = max(rw[5], 1)
+    res["level1"] = {"passes": rw[5], "passes_per_tick": round(rw[5] / nt, 3),
+                     "us_per_pass": round(rw[7] * US / np_, 3),
+                     "general_rows_per_pass": round(rw[2] / np_, 2), "quiet_rows_per_pass": round(rw[4] / np_, 2),
+                     "candidates_per_pass": round(rw[6] / np_, 2), "placements_per_pass": round(rw[3] / np_, 2),
+                     "us_per_general_row_tests_and_placements": round(rw[0] * US / max(rw[2], 1), 3),
+                     "us_per_general_row_bookkeeping": round(rw[1] * US / max(rw[2], 1), 3),
+                     "us_per_pass_setup": round(rw[8] * US / np_, 3), "us_per_pass_row_loop": round(rw[9] * US / np_, 3),
+                     "us_per_pass_end": round(rw[10] * US / np_, 3)}
     print(json.dumps(res, indent=1))
 
 
