@@ -6,25 +6,31 @@
 //        out of HBM every tick): phase A and the sample (dt_phase_a, dt_sample of
 //        mcs_dtrade_dev.h), then its exchange record and, when a trader round is due, its node
 //        snapshot and both contract sizes; it publishes the record (X1)
-//   D    the trader wave gathers every record (X1), runs the trader rounds in cluster order on its
-//        own copy of the trader state (dt_rounds<true>: the same code as dt_trader_kernel), and
-//        publishes the next tick's clock and, per cluster, the count of the rounds' side effects on
-//        that cluster's live state, queued in HBM in the rounds' order (X2)
-//   X2   each cluster wave applies its side effects (Foreign commits to a node and a running slot,
-//        virtual nodes: pkg/scheduler/cluster.go:65-125) and starts the next tick
+//   D    on a tick with a trader round due (any_due), the trader wave gathers every record (X1), runs
+//        the rounds in cluster order on its own copy of the trader state (dt_rounds<true>: the same
+//        code as dt_trader_kernel), and publishes the next tick's clock, each cluster's next round
+//        and the count of the rounds' side effects on that cluster's live state, queued in HBM in
+//        the rounds' order (X2); each cluster wave applies them (Foreign commits to a node and a
+//        running slot, virtual nodes: pkg/scheduler/cluster.go:65-125) and starts the next tick
+//   --   on a tick without a round (9 in 10 of C5-DELAY's) there is no phase D: every cluster wave
+//        reads every cluster's four clock words of X1 and computes the next clock itself
+//        (dm_next_clock: dt_next_ctl's T, done and any_due); the trader reads the same words to keep
+//        the control block, and no X2 is exchanged (r06: 10.0 -> 9.0 us per C5-DELAY tick)
 // Exchange: the worker workgroups run 8 blocks apart, which the dispatcher's round-robin puts on
 // one XCD (checked at the launch's start: a launch whose workers landed on more than one XCD does
 // nothing, and the engine runs the replayed kernels instead), so that XCD's L2 is the meeting
 // point.  Every exchanged word travels as an 8-byte granule {value, tag} written with a plain store
 // (write-through L1, so it lands in the L2) and read with agent-scope loads (L1 bypassed) until
-// its tag is the exchange's epoch (2 * tick + 1 for X1, + 2 for X2; the granules are zeroed before
-// every launch): the data is the flag (cdna_hip_programming.md Guideline 16).  The bulk data behind
-// a granule (node snapshots, the queued operations) is stored before it and drained with
-// s_waitcnt vmcnt(0).  A cluster wave publishes X1 of tick n + 1 only after reading X2 of tick n,
-// which the trader publishes after its last read of tick n's records and snapshots, so one buffer
-// of each suffices.  Every wait is bounded (1 s without the epoch ends the launch with a failure
-// word, and the engine redoes the run on the replayed kernels).  Same results bit for bit as the
-// replayed tick (tests/test_gpu_dtrade.py).
+// its tag is the exchange's epoch (tick + 1; the granules are zeroed before every launch): the data
+// is the flag (cdna_hip_programming.md Guideline 16).  The bulk data behind a granule (node
+// snapshots, the queued operations) is stored before it and drained with s_waitcnt vmcnt(0).
+// X1 has one buffer per tick parity: a cluster wave publishes tick n + 2's records only after it
+// read tick n + 1's clock words from every cluster (each of which read tick n's first) and after
+// the trader's progress granule says it has read tick n's.  X2 needs one buffer: the trader
+// publishes the next round's only after every cluster wave has published a later tick's records.
+// Every wait is bounded (1 s without the epoch ends the launch with a failure word, and the engine
+// redoes the run on the replayed kernels).  Same results bit for bit as the replayed tick
+// (tests/test_gpu_dtrade.py).
 #include "mcs_dtrade_dev.h"
 
 namespace mcs {
@@ -34,12 +40,22 @@ constexpr uint32_t kDmWaves = 4;  // cluster waves per workgroup, one per SIMD
 constexpr uint32_t kDmThreads = kDmWaves * kWave;
 constexpr uint32_t kDmRecWords = (uint32_t)(sizeof(DtRec) / 4u);
 static_assert(sizeof(DtRec) % 4u == 0u && kDmRecWords <= (uint32_t)kWave, "a record word per lane");
-// granules (u64) of gx: X1 records word-major [kDmRecWords][64] (word w of cluster q at w * 64 + q),
-// X2 per-cluster words [64] (queued operations | this cluster's trader round due << 31), X2 clock
-// words [4] (T, done, any_due)
-constexpr uint32_t kDmX2 = kDmRecWords * kDtResMaxClusters;
-constexpr uint32_t kDmX2Ctl = kDmX2 + kDtResMaxClusters;
-constexpr uint32_t kDmGranules = kDmX2Ctl + 4u;
+// granules (u64) of gx: X1 records word-major [2][kDmRecWords][64] (word w of cluster q at w * 64 + q,
+// one buffer per tick parity), X2 per-cluster words [64] (queued operations) and [64] (the cluster's
+// next trader round), X2 clock words [4] (T, done, any_due, the earliest next round over the system),
+// the trader's progress [1] (tag: the last tick whose records it has read, + 1)
+constexpr uint32_t kDmX1Buf = kDmRecWords * kDtResMaxClusters;
+constexpr uint32_t kDmX2 = 2u * kDmX1Buf;
+constexpr uint32_t kDmX2Due = kDmX2 + kDtResMaxClusters;
+constexpr uint32_t kDmX2Ctl = kDmX2Due + kDtResMaxClusters;
+constexpr uint32_t kDmTR = kDmX2Ctl + 4u;
+constexpr uint32_t kDmGranules = kDmTR + 1u;
+// the record words the next tick's clock needs (DtRec: flags, done, queued, nxt), and nv
+constexpr uint32_t kDmWFlags = (uint32_t)(offsetof(DtRec, flags) / 4u);
+constexpr uint32_t kDmWNv = (uint32_t)(offsetof(DtRec, nv) / 4u);
+static_assert(offsetof(DtRec, done) == offsetof(DtRec, flags) + 4 && offsetof(DtRec, queued) == offsetof(DtRec, flags) + 8 &&
+                  offsetof(DtRec, nxt) == offsetof(DtRec, flags) + 12,
+              "clock words contiguous");
 // gu (uncached): [0, 32) one placement granule per worker, [32] the failure word
 constexpr uint32_t kDmMaxWorkers = 32;  // one XCD's CUs
 constexpr uint32_t kDmFail = kDmMaxWorkers;
@@ -76,6 +92,35 @@ __device__ __forceinline__ void dm_fail(const DtResArgs& m, uint32_t why) {
     __hip_atomic_store(m.gu + kDmFail, (unsigned long long)why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The clock after a tick with no trader round, from every cluster's record words of the tick (lane q:
+// cluster q's flags, done, queued, nxt) and the earliest next round ndue: dt_next_ctl's T, done and
+// any_due (its OVERFLOW test reads the records' flags alone: a round's overflow ends the run at its
+// own tick, and a cluster's flags are sticky)
+struct DmClock {
+    uint32_t T;
+    bool done, any_due;
+};
+__device__ __forceinline__ DmClock dm_next_clock(const DtArgs& a, const uint32_t lane, const uint32_t T,
+                                                 const uint32_t fw, const uint32_t dw, const uint32_t qw,
+                                                 const uint32_t xw, const uint32_t ndue) {
+    const bool valid = lane < a.Ct;
+    const bool done_all = __ballot(valid && dw == 0u) == 0ull;
+    const bool queued_any = __ballot(valid && qw != 0u) != 0ull;
+    uint32_t nxt = T + a.sample_period - T % a.sample_period;
+    const uint32_t rn = wave_min_u32(valid ? xw : kEmpty);
+    nxt = rn < nxt ? rn : nxt;
+    nxt = ndue < nxt ? ndue : nxt;
+    const bool ovf = __ballot(valid && (fw & MCS_FLAG_OVERFLOW) != 0u) != 0ull;
+    DmClock k{T, false, false};
+    if (done_all || ovf || T >= a.t_max) {
+        k.done = true;
+    } else {
+        k.T = (queued_any || nxt <= T + 1u) ? T + 1u : nxt;
+    }
+    k.any_due = ndue <= k.T;
+    return k;
+}
+
 // ---- a cluster wave: phases A and C of its cluster every tick, X1, X2 and the queued side effects ----
 __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, const uint32_t c, const uint32_t lane,
                                            unsigned long long* nodes, uint32_t* sfin, uint32_t* hist, float* dc,
@@ -91,7 +136,9 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
     const uint32_t S = a.S;
     DtCluster st = a.cl[c];
     const DtCtl c0 = *a.ctl;
-    const bool due0 = a.tr[c].next_due <= c0.T;
+    uint32_t my_due = a.tr[c].next_due;  // this cluster's next trader round
+    // the earliest next round over the system (kEmpty without traders)
+    uint32_t ndue = wave_min_u32(a.period != 0u && lane < a.Ct ? a.tr[lane].next_due : kEmpty);
     uint32_t NN = N + st.nv;
     // (the replayed step kernel's per-tick state in, once per launch)
     unsigned long long snap_l = NN <= (uint32_t)kWave && lane < NN ? a.l1snap[(size_t)c * a.W + lane] : 0ull;
@@ -101,7 +148,7 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
     uint32_t T = c0.T;
     bool done = c0.done != 0u;
     bool any_due = a.period != 0u && c0.any_due != 0u;
-    bool due = any_due && due0;
+    bool due = any_due && my_due <= T;
     unsigned long long* const gx = m.gx;
     unsigned long long* const snap = dt_snap(a, c);
     const unsigned long long* const ops =
@@ -165,9 +212,24 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
         }
         dt_wave_sync();
         if (any_due) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the snapshot lands before X1
-        const uint32_t tag1 = 2u * it + 1u, tag2 = tag1 + 1u;
+        const uint32_t tag = it + 1u;
+        unsigned long long* const x1 = gx + (size_t)(it & 1u) * kDmX1Buf;
+        // the buffer's last records (tick it - 2): every cluster wave read them before publishing tick
+        // it - 1's, which this wave has read; the trader's progress granule says it has too
+        if (it >= 2u) {
+            const uint64_t t0 = wall_clock64();
+            for (;;) {
+                const unsigned long long x = lane == 0u ? dm_get(gx + kDmTR) : 0ull;
+                if (readlane((uint32_t)(x >> 32), 0u) + 1u >= it) break;
+                if (wall_clock64() - t0 > kDmTimeout) {
+                    failed = true;
+                    break;
+                }
+            }
+            if (failed) break;
+        }
         if (lane < kDmRecWords)
-            dm_put(gx + (size_t)lane * kDtResMaxClusters + c, tag1, reinterpret_cast<const uint32_t*>(rec)[lane]);
+            dm_put(x1 + (size_t)lane * kDtResMaxClusters + c, tag, reinterpret_cast<const uint32_t*>(rec)[lane]);
 #ifdef MCS_STAMPS
         const uint64_t s3 = wall_clock64();
         if (lane == 0u) {
@@ -185,32 +247,67 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
         sm[1] += s2 - s1;
         sm[2] += s3 - s2;
 #endif
-        // X2: lane 0 this cluster's word, lanes 1-3 the clock
-        const unsigned long long* src = gx + (lane == 0u ? kDmX2 + c : kDmX2Ctl + (lane < 4u ? lane - 1u : 0u));
-        uint32_t v = 0u;
-        const uint64_t t0 = wall_clock64();
-        for (;;) {
-            const unsigned long long x = lane < 4u ? dm_get(src) : ((unsigned long long)tag2 << 32);
-            v = (uint32_t)x;
-            if (__all((uint32_t)(x >> 32) == tag2)) break;
-            if (wall_clock64() - t0 > kDmTimeout) {
-                failed = true;
-                break;
+        uint32_t nops = 0u;
+        if (any_due) {
+            // X2 of a tick with trader rounds: lane 0 this cluster's queued operations, lane 1 its next
+            // round, lanes 2-5 the clock
+            const unsigned long long* src =
+                gx + (lane == 0u ? kDmX2 + c : lane == 1u ? kDmX2Due + c : kDmX2Ctl + (lane < 6u ? lane - 2u : 0u));
+            uint32_t v = 0u;
+            const uint64_t t0 = wall_clock64();
+            for (;;) {
+                const unsigned long long x = lane < 6u ? dm_get(src) : ((unsigned long long)tag << 32);
+                v = (uint32_t)x;
+                if (__all((uint32_t)(x >> 32) == tag)) break;
+                if (wall_clock64() - t0 > kDmTimeout) {
+                    failed = true;
+                    break;
+                }
             }
+            if (failed) break;
+            nops = readlane(v, 0u);
+            my_due = readlane(v, 1u);
+            T = readlane(v, 2u);
+            done = readlane(v, 3u) != 0u;
+            any_due = a.period != 0u && readlane(v, 4u) != 0u;
+            ndue = readlane(v, 5u);
+        } else {
+            // no round: the clock from every cluster's records of the tick (lane q: cluster q)
+            uint32_t fw = 0u, dw = 0u, qw = 0u, xw = 0u;
+            const unsigned long long* src = x1 + (size_t)kDmWFlags * kDtResMaxClusters + lane;
+            const bool valid = lane < a.Ct;
+            const uint64_t t0 = wall_clock64();
+            for (;;) {
+                const unsigned long long tg = (unsigned long long)tag << 32;
+                const unsigned long long x0 = valid ? dm_get(src) : tg;
+                const unsigned long long x1w = valid ? dm_get(src + kDtResMaxClusters) : tg;
+                const unsigned long long x2w = valid ? dm_get(src + 2u * kDtResMaxClusters) : tg;
+                const unsigned long long x3w = valid ? dm_get(src + 3u * kDtResMaxClusters) : tg;
+                fw = (uint32_t)x0;
+                dw = (uint32_t)x1w;
+                qw = (uint32_t)x2w;
+                xw = (uint32_t)x3w;
+                if (__all((uint32_t)(x0 >> 32) == tag && (uint32_t)(x1w >> 32) == tag &&
+                          (uint32_t)(x2w >> 32) == tag && (uint32_t)(x3w >> 32) == tag))
+                    break;
+                if (wall_clock64() - t0 > kDmTimeout) {
+                    failed = true;
+                    break;
+                }
+            }
+            if (failed) break;
+            const DmClock k = dm_next_clock(a, lane, T, fw, dw, qw, xw, ndue);
+            T = k.T;
+            done = k.done;
+            any_due = a.period != 0u && k.any_due;
         }
-        if (failed) break;
+        due = any_due && my_due <= T;
 #ifdef MCS_STAMPS
         const uint64_t s4 = wall_clock64();
         sm[3] += s4 - s3;
 #endif
-        const uint32_t w0 = readlane(v, 0u);
-        T = readlane(v, 1u);
-        done = readlane(v, 2u) != 0u;
-        any_due = a.period != 0u && readlane(v, 3u) != 0u;
-        due = any_due && (w0 >> 31) != 0u;
         // phase D's side effects on this cluster, in the rounds' order (what dt_trader_kernel writes
         // to the live state of a local cluster)
-        const uint32_t nops = w0 & 0x7FFFFFFFu;
         for (uint32_t i = 0; i < nops; ++i) {
             const unsigned long long* op = ops + (size_t)i * (sizeof(DtOp) / 8u);
             const unsigned long long q0 = dm_get(op), q1 = dm_get(op + 1), q2 = dm_get(op + 2), q3 = dm_get(op + 3);
@@ -276,7 +373,7 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
     if (NN <= (uint32_t)kWave && lane < NN) a.l1snap[(size_t)c * a.W + lane] = snap_l;
 }
 
-// ---- the trader wave: X1, phase D (the rounds and the next tick), X2 ----
+// ---- the trader wave: X1 every tick; on a tick with a round due, phase D and X2 ----
 __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, const uint32_t lane, DtTrader* trs,
                                           DtRec* srec, uint32_t* appr, uint32_t* nvs, uint32_t* nfr, uint32_t* opn) {
     const uint32_t Ct = a.Ct;
@@ -294,26 +391,66 @@ __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, c
     for (uint32_t it = 0; it < m.budget; ++it) {
         const uint32_t T = c0.T;
         const bool any_due = c0.any_due != 0u;
-        const uint32_t tag1 = 2u * it + 1u, tag2 = tag1 + 1u;
-        // X1: lane q gathers cluster q's record
-        uint32_t w[kDmRecWords];
+        const uint32_t tag = it + 1u;
+        const unsigned long long* const x1 = gx + (size_t)(it & 1u) * kDmX1Buf;
         const uint64_t t0 = wall_clock64();
-        for (;;) {
-            bool ok = true;
+        if (any_due) {
+            // X1: lane q gathers cluster q's record
+            uint32_t w[kDmRecWords];
+            for (;;) {
+                bool ok = true;
 #pragma unroll
-            for (uint32_t k = 0; k < kDmRecWords; ++k) {
-                const unsigned long long x = lane < Ct ? dm_get(gx + (size_t)k * kDtResMaxClusters + lane)
-                                                       : ((unsigned long long)tag1 << 32);
-                w[k] = (uint32_t)x;
-                ok = ok && (uint32_t)(x >> 32) == tag1;
+                for (uint32_t k = 0; k < kDmRecWords; ++k) {
+                    const unsigned long long x = lane < Ct ? dm_get(x1 + (size_t)k * kDtResMaxClusters + lane)
+                                                           : ((unsigned long long)tag << 32);
+                    w[k] = (uint32_t)x;
+                    ok = ok && (uint32_t)(x >> 32) == tag;
+                }
+                if (__all(ok)) break;
+                if (wall_clock64() - t0 > kDmTimeout) {
+                    failed = true;
+                    break;
+                }
             }
-            if (__all(ok)) break;
-            if (wall_clock64() - t0 > kDmTimeout) {
-                failed = true;
-                break;
+            if (failed) break;
+            if (lane == 0u) dm_put(gx + kDmTR, tag, 0u);  // (this tick's records read)
+            if (lane < Ct) {
+                uint32_t* d = reinterpret_cast<uint32_t*>(&srec[lane]);
+#pragma unroll
+                for (uint32_t k = 0; k < kDmRecWords; ++k) d[k] = w[k];
+                nvs[lane] = srec[lane].nv;
+                nfr[lane] = srec[lane].nfree;
+                opn[lane] = 0u;
+            }
+        } else {
+            // a tick without rounds: the words of the next clock (and nv, for nv_all)
+            uint32_t w[5];
+            for (;;) {
+                bool ok = true;
+#pragma unroll
+                for (uint32_t k = 0; k < 5u; ++k) {
+                    const uint32_t wi = k == 4u ? kDmWNv : kDmWFlags + k;
+                    const unsigned long long x = lane < Ct ? dm_get(x1 + (size_t)wi * kDtResMaxClusters + lane)
+                                                           : ((unsigned long long)tag << 32);
+                    w[k] = (uint32_t)x;
+                    ok = ok && (uint32_t)(x >> 32) == tag;
+                }
+                if (__all(ok)) break;
+                if (wall_clock64() - t0 > kDmTimeout) {
+                    failed = true;
+                    break;
+                }
+            }
+            if (failed) break;
+            if (lane == 0u) dm_put(gx + kDmTR, tag, 0u);
+            if (lane < Ct) {
+                srec[lane].flags = w[0];
+                srec[lane].done = w[1];
+                srec[lane].queued = w[2];
+                srec[lane].nxt = w[3];
+                nvs[lane] = w[4];
             }
         }
-        if (failed) break;
 #ifdef MCS_STAMPS
         const uint64_t t1 = wall_clock64();
         tsum[0] += t1 - t_put;
@@ -321,14 +458,6 @@ __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, c
             tsum[4] += __hip_atomic_exchange(&g_dm_tick[it & 1023u][lane], 0ull, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
 #endif
-        if (lane < Ct) {
-            uint32_t* d = reinterpret_cast<uint32_t*>(&srec[lane]);
-#pragma unroll
-            for (uint32_t k = 0; k < kDmRecWords; ++k) d[k] = w[k];
-            nvs[lane] = srec[lane].nv;
-            nfr[lane] = srec[lane].nfree;
-            opn[lane] = 0u;
-        }
         dt_wave_sync();
 #ifdef MCS_STAMPS
         const uint64_t t2 = wall_clock64();
@@ -344,15 +473,24 @@ __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, c
         n_for = k.n_for;
         const uint32_t lflags = k.lflags;
         const DtCtl nc = dt_next_ctl(a, lane, c0, trs, srec, lflags, n_trades, n_won, n_for);
-        dt_wave_sync();
-        const uint32_t on = lane < Ct ? opn[lane] : 0u;
-        if (__ballot(on > m.ops_cap)) {  // (the run fails over; the cluster waves time out)
-            failed = true;
-            break;
+        if (any_due) {  // X2: the rounds' side effects, every cluster's next round and the clock
+            dt_wave_sync();
+            const uint32_t on = lane < Ct ? opn[lane] : 0u;
+            if (__ballot(on > m.ops_cap)) {  // (the run fails over; the cluster waves time out)
+                failed = true;
+                break;
+            }
+            const uint32_t nd = lane < Ct ? trs[lane].next_due : kEmpty;
+            const uint32_t ndue = a.period != 0u ? wave_min_u32(nd) : kEmpty;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the operations and snapshot writes before X2
+            if (lane < Ct) {
+                dm_put(gx + kDmX2 + lane, tag, on);
+                dm_put(gx + kDmX2Due + lane, tag, nd);
+            }
+            if (lane < 4u)
+                dm_put(gx + kDmX2Ctl + lane, tag,
+                       lane == 0u ? nc.T : (lane == 1u ? nc.done : (lane == 2u ? nc.any_due : ndue)));
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the operations and snapshot writes before X2
-        if (lane < Ct) dm_put(gx + kDmX2 + lane, tag2, on | (trs[lane].next_due <= nc.T ? 0x80000000u : 0u));
-        if (lane < 3u) dm_put(gx + kDmX2Ctl + lane, tag2, lane == 0u ? nc.T : (lane == 1u ? nc.done : nc.any_due));
 #ifdef MCS_STAMPS
         t_put = wall_clock64();
         tsum[2] += t_put - t3;
