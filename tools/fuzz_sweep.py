@@ -1,7 +1,8 @@
 """Run the GPU fuzz parity cases over a range of fresh seeds (beyond the ones the test suite pins)
 and report every failing (test, shape/policy, seed); exit status 1 if any failed.
 
-    python tools/fuzz_sweep.py BASE COUNT      (SWEEP_BIG=1: larger FIFO and DELAY cases only)
+    python tools/fuzz_sweep.py BASE COUNT      (SWEEP_BIG=1: larger FIFO and DELAY cases only;
+                                                SWEEP_DT=1: the DELAY-trading cases only)
 """
 import os
 import sys
@@ -85,6 +86,15 @@ with Engine(0) as eng, Engine(0, policy="DELAY") as deng:
                         assert (g[k] == o[k]).all(), k
                 cases = [(f"trade-big/{s}", lambda s=s: tbig(s)) for s in ("w16s", "mid", "w16r")]
                 cases += [(f"dtrade-big/{s}", lambda s=s: dtbig(s)) for s in ("w16s", "mid")]
+        if os.environ.get("SWEEP_DT"):  # DELAY trading only: the fuzz cases and 16 x 800-job systems
+            def dtsys(shape, seed=seed):
+                arrays, st = TP.fuzz_workload(shape, seed, n_clusters=16, J=800, blocking=False)
+                g, o = TDT.run(arrays, st), TDT.O.dtrade_run(arrays, st)
+                for k in ("node", "start", "finish"):
+                    assert (g[k] == o[k]).all(), k
+                assert g["ts"]["t_final"] == o["t_final"] and g["ts"]["loop_form"] == 5
+            cases = [(f"dtrade/{s}", lambda s=s: TDT.test_gpu_dtrade_fuzz(s, seed, 600)) for s in ("w16s", "mid")]
+            cases += [(f"dtrade-sys/{s}", lambda s=s: dtsys(s)) for s in ("w16s", "mid")]
         for name, fn in cases:
             runs += 1
             if os.environ.get("SWEEP_VERBOSE"):
