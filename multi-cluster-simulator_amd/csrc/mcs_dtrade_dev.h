@@ -308,6 +308,8 @@ __device__ __forceinline__ DtCluster dt_phase_a(const DtArgs& a, const uint32_t 
         // superset (cores clamped at 63, m = 0): every candidate still gets the real first fit, and a
         // quiet row is one where nothing passes.  Rebuilt after each commit (nodes only shrink).
         uint32_t gtab = 0u;
+        // (r06: one or two grown nodes tested exactly against their values in scalars instead, no
+        // permute: 8.92 -> 10.69 us per C5-DELAY tick, profiles/r06_dm/ab_ct.txt)
         auto g_build = [&]() {
             hist[lane] = 0u;
             dt_wave_sync();
@@ -671,15 +673,28 @@ __device__ __forceinline__ void dt_contracts(const bool due, const uint32_t lane
         if constexpr (RES) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         dt_bar<RES>();
-        for (uint32_t i = lane; i < ln; i += kWave) {
-            const unsigned long long cm = ld64(&l1cm[i]);
-            const uint32_t jc = (uint32_t)cm, jm = (uint32_t)(cm >> 32);
-            const uint32_t d = (uint32_t)(ld64(&l1jd[i]) >> 32);
-            fsc += jc;  // fast node: uint32 sums and the longest duration (:138-155)
-            fsm += jm;
-            fmd = d > fmd ? d : fmd;
-            ssc += (int32_t)(0u - jc) < 0 ? jc : 0u;  // small node: int32 arithmetic (:232-259)
-            ssm += (int32_t)(0u - jm) < 0 ? jm : 0u;
+        // 8 rows of loads in flight per round (every lane loads, at an index clamped into the list;
+        // a row at a time waited one L2 round trip per 64 entries)
+        constexpr uint32_t kR = 8;
+        for (uint32_t b = 0; b < ln; b += kR * kWave) {
+            unsigned long long cmv[kR], jdv[kR];
+#pragma unroll
+            for (uint32_t u = 0; u < kR; ++u) {
+                const uint32_t i = b + u * kWave + lane, pi = i < ln ? i : ln - 1u;
+                cmv[u] = ld64(&l1cm[pi]);
+                jdv[u] = ld64(&l1jd[pi]);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kR; ++u) {
+                const bool in = b + u * kWave + lane < ln;
+                const uint32_t jc = in ? (uint32_t)cmv[u] : 0u, jm = in ? (uint32_t)(cmv[u] >> 32) : 0u;
+                const uint32_t d = in ? (uint32_t)(jdv[u] >> 32) : 0u;
+                fsc += jc;  // fast node: uint32 sums and the longest duration (:138-155)
+                fsm += jm;
+                fmd = d > fmd ? d : fmd;
+                ssc += (int32_t)(0u - jc) < 0 ? jc : 0u;  // small node: int32 arithmetic (:232-259)
+                ssm += (int32_t)(0u - jm) < 0 ? jm : 0u;
+            }
         }
         fsc = dt_wave_sum_u32(fsc);
         fsm = dt_wave_sum_u32(fsm);
@@ -687,18 +702,31 @@ __device__ __forceinline__ void dt_contracts(const bool due, const uint32_t lane
         ssc = dt_wave_sum_u32(ssc);
         ssm = dt_wave_sum_u32(ssm);
         // small node contract.Time per job: endTime if the previous time < endTime, else 0
-        // (:263-265); a padded last batch (len % 20 != 0) ends with zero jobs -> 0.  Durations are
-        // staged 64 at a time in LDS, then scanned by one lane.
-        if (ln % 20u == 0u) {
-            for (uint32_t b = 0; b < ln; b += kWave) {
-                dt_bar<RES>();
-                if (b + lane < ln) hist[lane] = (uint32_t)(ld64(&l1jd[b + lane]) >> 32);
-                dt_bar<RES>();
-                if (lane == 0) {
-                    const uint32_t m = ln - b < (uint32_t)kWave ? ln - b : (uint32_t)kWave;
-                    for (uint32_t i = 0; i < m; ++i) sst = sst < hist[i] ? hist[i] : 0u;
+        // (:263-265); a padded last batch (len % 20 != 0) ends with zero jobs -> 0.  The recurrence
+        // s = s < d ? d : 0 from s = 0 leaves s = d_k exactly when the run of "falls" (d_(i-1) >= d_i)
+        // ending at k is even (a non-fall takes d_i whatever s was; a fall takes it only after a 0),
+        // so the answer is the last duration or 0 by the parity of the list's trailing run of falls,
+        // read backwards a row at a time from the end (usually one row)
+        if (ln % 20u == 0u && ln != 0u) {
+            const uint32_t dl = (uint32_t)(ld64(&l1jd[ln - 1u]) >> 32);
+            uint32_t run = 0;  // falls ending at the list's last entry
+            for (uint32_t top = ln;;) {  // entries [top - 64, top) by lane (the row's last in lane 63)
+                const uint32_t base = top > (uint32_t)kWave ? top - (uint32_t)kWave : 0u;
+                const uint32_t k = base + lane;  // entry k: a fall when d_(k-1) >= d_k (k >= 1)
+                const bool in = k < top;
+                const uint32_t dk = (uint32_t)(ld64(&l1jd[in ? k : top - 1u]) >> 32);
+                const uint32_t dp = k >= 1u && in ? (uint32_t)(ld64(&l1jd[k - 1u]) >> 32) : 0u;
+                const bool fall = in && k >= 1u && dp >= dk;
+                // the last non-fall in the row (entry 0 counts as one)
+                const unsigned long long nf = __ballot(in && !fall);
+                if (nf) {
+                    run += top - 1u - (base + 63u - (uint32_t)__builtin_clzll(nf));
+                    break;
                 }
+                run += top - base;
+                top = base;
             }
+            sst = (run & 1u) == 0u ? dl : 0u;
         }
     }
 }

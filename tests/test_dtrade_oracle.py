@@ -103,3 +103,23 @@ def test_dtrade_overloaded_system_trades_and_uses_virtual_nodes():
     for q in range(8):
         wq = won[won["requester"] == q]
         assert [(int(a), int(b)) for a, b in zip(wq["cores"], wq["mem"])] == r["vnodes"][q]
+
+
+def test_small_node_time_is_the_parity_of_the_trailing_falls():
+    """The small-node contract time (scheduler_client.go:263-265: endTime when the previous time is
+    below it, else 0, over GetLevel1() in order) that dt_contracts computes in parallel: the last
+    duration when the run of falls (d[i-1] >= d[i]) ending at the list's end is even, else 0."""
+    rng = np.random.default_rng(7)
+    for n in list(range(1, 70)) + [127, 128, 129, 640, 1000]:
+        for hi in (1, 3, 50, 1 << 31):
+            d = rng.integers(0, hi, n, dtype=np.uint64).astype(np.uint32)
+            s = 0
+            for x in d:
+                s = int(x) if s < int(x) else 0
+            run = 0
+            for k in range(n - 1, 0, -1):
+                if d[k - 1] >= d[k]:
+                    run += 1
+                else:
+                    break
+            assert s == (int(d[-1]) if run % 2 == 0 else 0), (n, hi)
