@@ -21,7 +21,7 @@ eng.load_clusters(replicate(spec, 64))
 eng.generate_jobs(GenParams(seed=0x4D43535F53494D31), J)
 fn = L.lib().mcs_debug_dm_stamps
 buf = (C.c_ulonglong * (64 * 6 + 16))()
-rows = (C.c_ulonglong * 12)()
+rows = (C.c_ulonglong * 17)()
 fr = L.lib().mcs_debug_dm_rows
 eng.run(); assert fn(buf) == 0 and fr(rows) == 0
 st = eng.run(); assert fn(buf) == 0 and fr(rows) == 0
@@ -70,6 +70,9 @@ def main():
                      "us_per_general_row_bookkeeping": round(rw[1] * US / max(rw[2], 1), 3),
                      "us_per_pass_setup": round(rw[8] * US / np_, 3), "us_per_pass_row_loop": round(rw[9] * US / np_, 3),
                      "us_per_pass_end": round(rw[10] * US / np_, 3)}
+    for i, nm in enumerate(("quiet_pairs_unshifted", "quiet_pairs_shifted", "other_pairs")):
+        res["level1"][nm] = {"per_pass": round(rw[12 + 2 * i] / np_, 2),
+                             "us_each": round(rw[11 + 2 * i] * US / max(rw[12 + 2 * i], 1), 3)}
     print(json.dumps(res, indent=1))
 
 
