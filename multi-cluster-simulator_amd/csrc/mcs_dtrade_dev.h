@@ -90,7 +90,9 @@ __device__ unsigned long long g_dt_maxsum[10];
 // [1] the WaitTime and compaction bookkeeping, [2] rows, [3] placements (of the general rows);
 // [4] quiet rows, [5] passes, [6] candidates given a first fit, [7] the passes' time; of which
 // [8] before the row loop, [9] the row loop, [10] after it
-__device__ unsigned long long g_dt_rows[12];
+// (the probe's per-pair split, [11]-[16], is not built here); the trader rounds: [17]/[18] time/count
+// of stage steps that trade (a request), [19]/[20] of those that do not
+__device__ unsigned long long g_dt_rows[21];
 #define DT_MARK(i)                                  \
     do {                                            \
         const uint64_t dt_now = wall_clock64();     \
@@ -759,6 +761,9 @@ __device__ __forceinline__ DtCounts dt_rounds(const DtArgs& a, const uint32_t la
             const bool qloc = ql_ < a.C;
             // RequestPolicyMonitor of requester q (trader.go:282-324): two-stage machine
             while (trs[q].next_due <= T) {
+#ifdef MCS_STAMPS
+                const uint64_t rq0 = wall_clock64();
+#endif
                 DtTrader tq = trs[q];
                 if (tq.stage == 0u) {  // cs := t.State.getState() (:284)
                     tq.cs_cu = rq->cu;
@@ -774,6 +779,12 @@ __device__ __forceinline__ DtCounts dt_rounds(const DtArgs& a, const uint32_t la
                     dt_bar<RES>();
                     if (lane == 0) trs[q] = tq;
                     dt_bar<RES>();
+#ifdef MCS_STAMPS
+                    if (lane == 0) {
+                        atomicAdd(&g_dt_rows[19], (unsigned long long)(wall_clock64() - rq0));
+                        atomicAdd(&g_dt_rows[20], 1ull);
+                    }
+#endif
                     continue;
                 }
                 // calculateContractRequest over GetLevel1() (scheduler_client.go:126-289), sized
@@ -961,6 +972,12 @@ __device__ __forceinline__ DtCounts dt_rounds(const DtArgs& a, const uint32_t la
                 }
                 ++n_trades;
                 dt_bar<RES>();
+#ifdef MCS_STAMPS
+                if (lane == 0) {
+                    atomicAdd(&g_dt_rows[17], (unsigned long long)(wall_clock64() - rq0));
+                    atomicAdd(&g_dt_rows[18], 1ull);
+                }
+#endif
                 if (lflags & MCS_FLAG_OVERFLOW) break;
             }
             if (lflags & MCS_FLAG_OVERFLOW) break;

@@ -596,10 +596,10 @@ extern "C" int mcs_debug_dm_stamps(unsigned long long* out) {
     return -2;
 #endif
 }
-// the probe build's Level1 row counters of the resident tick (g_dt_rows [12]), read and cleared
+// the probe build's Level1 row counters of the resident tick (g_dt_rows [21]), read and cleared
 extern "C" int mcs_debug_dm_rows(unsigned long long* out) {
 #ifdef MCS_STAMPS
-    unsigned long long z[12] = {};
+    unsigned long long z[21] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mcs::g_dt_rows), sizeof(z)) != hipSuccess) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(mcs::g_dt_rows), z, sizeof(z)) == hipSuccess ? 0 : -1;
 #else

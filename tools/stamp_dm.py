@@ -21,7 +21,7 @@ eng.load_clusters(replicate(spec, 64))
 eng.generate_jobs(GenParams(seed=0x4D43535F53494D31), J)
 fn = L.lib().mcs_debug_dm_stamps
 buf = (C.c_ulonglong * (64 * 6 + 16))()
-rows = (C.c_ulonglong * 17)()
+rows = (C.c_ulonglong * 21)()
 fr = L.lib().mcs_debug_dm_rows
 eng.run(); assert fn(buf) == 0 and fr(rows) == 0
 st = eng.run(); assert fn(buf) == 0 and fr(rows) == 0
@@ -73,6 +73,8 @@ def main():
     for i, nm in enumerate(("quiet_pairs_unshifted", "quiet_pairs_shifted", "other_pairs")):
         res["level1"][nm] = {"per_pass": round(rw[12 + 2 * i] / np_, 2),
                              "us_each": round(rw[11 + 2 * i] * US / max(rw[12 + 2 * i], 1), 3)}
+    res["trader_steps"] = {"requests": rw[18], "us_per_request": round(rw[17] * US / max(rw[18], 1), 3),
+                           "other_steps": rw[20], "us_per_other_step": round(rw[19] * US / max(rw[20], 1), 3)}
     print(json.dumps(res, indent=1))
 
 
