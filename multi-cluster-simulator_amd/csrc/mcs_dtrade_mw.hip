@@ -44,12 +44,15 @@ static_assert(sizeof(DtRec) % 4u == 0u && kDmRecWords <= (uint32_t)kWave, "a rec
 // one buffer per tick parity), X2 per-cluster words [64] (queued operations) and [64] (the cluster's
 // next trader round), X2 clock words [4] (T, done, any_due, the earliest next round over the system),
 // the trader's progress [1] (tag: the last tick whose records it has read, + 1)
+constexpr uint32_t kDmRing = 8;  // X1 buffers: a cluster wave runs up to kDmRing ticks ahead of X1's readers
 constexpr uint32_t kDmX1Buf = kDmRecWords * kDtResMaxClusters;
-constexpr uint32_t kDmX2 = 2u * kDmX1Buf;
+constexpr uint32_t kDmX2 = kDmRing * kDmX1Buf;
 constexpr uint32_t kDmX2Due = kDmX2 + kDtResMaxClusters;
 constexpr uint32_t kDmX2Ctl = kDmX2Due + kDtResMaxClusters;
 constexpr uint32_t kDmTR = kDmX2Ctl + 4u;
-constexpr uint32_t kDmGranules = kDmTR + 1u;
+constexpr uint32_t kDmP = kDmTR + 1u;                      // [64] each cluster wave's progress (tag: tick + 1)
+constexpr uint32_t kDmAbort = kDmP + kDtResMaxClusters;    // an overflow's tick (tag 1: set)
+constexpr uint32_t kDmGranules = kDmAbort + 1u;
 // the record words the next tick's clock needs (DtRec: flags, done, queued, nxt), and nv
 constexpr uint32_t kDmWFlags = (uint32_t)(offsetof(DtRec, flags) / 4u);
 constexpr uint32_t kDmWNv = (uint32_t)(offsetof(DtRec, nv) / 4u);
@@ -159,6 +162,8 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
     uint64_t dt_last = 0;
 #endif
     bool failed = false;
+    bool aborted = false;  // another cluster's slot overflow ended the run (it is redone bigger)
+    uint32_t seen = 0;     // every reader has read X1 up to this tick (cached)
 #ifdef MCS_STAMPS
     uint64_t sm[5] = {0, 0, 0, 0, 0}, sticks = 0, s_prev = wall_clock64(), s_ops = 0;
 #endif
@@ -213,20 +218,32 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
         dt_wave_sync();
         if (any_due) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the snapshot lands before X1
         const uint32_t tag = it + 1u;
-        unsigned long long* const x1 = gx + (size_t)(it & 1u) * kDmX1Buf;
-        // the buffer's last records (tick it - 2): every cluster wave read them before publishing tick
-        // it - 1's, which this wave has read; the trader's progress granule says it has too
-        if (it >= 2u) {
+        unsigned long long* const x1 = gx + (size_t)(it % kDmRing) * kDmX1Buf;
+        // the buffer's last records (tick it - kDmRing) must have been read by every reader: the
+        // trader and every cluster wave (each publishes its progress after its tick's clock); the
+        // minimum seen is cached, so the sweep runs about once per kDmRing ticks
+        if (it >= kDmRing && it - kDmRing + 1u > seen) {
             const uint64_t t0 = wall_clock64();
             for (;;) {
-                const unsigned long long x = lane == 0u ? dm_get(gx + kDmTR) : 0ull;
-                if (readlane((uint32_t)(x >> 32), 0u) + 1u >= it) break;
+                const unsigned long long x = lane < a.Ct ? dm_get(gx + kDmP + lane) : ~0ull;
+                const unsigned long long tr = lane == 0u ? dm_get(gx + kDmTR) : 0ull;
+                const unsigned long long ab = lane == 0u ? dm_get(gx + kDmAbort) : 0ull;
+                const uint32_t mp = wave_min_u32((uint32_t)(x >> 32)), mt = readlane((uint32_t)(tr >> 32), 0u);
+                const uint32_t mn = mp < mt ? mp : mt;
+                if (readlane((uint32_t)(ab >> 32), 0u) != 0u) {  // (a run that overflowed: stop)
+                    aborted = true;
+                    break;
+                }
+                if (mn >= it - kDmRing + 1u) {
+                    seen = mn;
+                    break;
+                }
                 if (wall_clock64() - t0 > kDmTimeout) {
                     failed = true;
                     break;
                 }
             }
-            if (failed) break;
+            if (failed || aborted) break;
         }
         if (lane < kDmRecWords)
             dm_put(x1 + (size_t)lane * kDtResMaxClusters + c, tag, reinterpret_cast<const uint32_t*>(rec)[lane]);
@@ -256,21 +273,33 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
             uint32_t v = 0u;
             const uint64_t t0 = wall_clock64();
             for (;;) {
-                const unsigned long long x = lane < 6u ? dm_get(src) : ((unsigned long long)tag << 32);
+                const unsigned long long x = lane < 6u ? dm_get(src)
+                                             : lane == 63u ? dm_get(gx + kDmAbort) : ((unsigned long long)tag << 32);
                 v = (uint32_t)x;
-                if (__all((uint32_t)(x >> 32) == tag)) break;
+                if (readlane((uint32_t)(x >> 32), 63u) != 0u && readlane((uint32_t)x, 63u) < it) {
+                    aborted = true;  // (the trader stopped at an earlier tick)
+                    break;
+                }
+                if (__all(lane == 63u || (uint32_t)(x >> 32) == tag)) break;
                 if (wall_clock64() - t0 > kDmTimeout) {
                     failed = true;
                     break;
                 }
             }
-            if (failed) break;
+            if (failed || aborted) break;
             nops = readlane(v, 0u);
             my_due = readlane(v, 1u);
             T = readlane(v, 2u);
             done = readlane(v, 3u) != 0u;
             any_due = a.period != 0u && readlane(v, 4u) != 0u;
             ndue = readlane(v, 5u);
+        } else if (rec->queued != 0u && !(st.flags & MCS_FLAG_OVERFLOW) && T < a.t_max) {
+            // no round, and this cluster has queued jobs: dt_next_ctl's clock is T + 1 whatever the
+            // other records hold (queued_any; not every job is decided; an overflow elsewhere ends
+            // the run, which is redone), so the wave goes on without reading them
+            T = T + 1u;
+            done = false;
+            any_due = a.period != 0u && ndue <= T;
         } else {
             // no round: the clock from every cluster's records of the tick (lane q: cluster q)
             uint32_t fw = 0u, dw = 0u, qw = 0u, xw = 0u;
@@ -290,18 +319,33 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
                 if (__all((uint32_t)(x0 >> 32) == tag && (uint32_t)(x1w >> 32) == tag &&
                           (uint32_t)(x2w >> 32) == tag && (uint32_t)(x3w >> 32) == tag))
                     break;
+                const unsigned long long ab = lane == 0u ? dm_get(gx + kDmAbort) : 0ull;
+                if (readlane((uint32_t)(ab >> 32), 0u) != 0u && readlane((uint32_t)ab, 0u) < it) {
+                    aborted = true;  // (a cluster stopped at an earlier tick)
+                    break;
+                }
                 if (wall_clock64() - t0 > kDmTimeout) {
                     failed = true;
                     break;
                 }
             }
-            if (failed) break;
+            if (failed || aborted) break;
             const DmClock k = dm_next_clock(a, lane, T, fw, dw, qw, xw, ndue);
             T = k.T;
             done = k.done;
             any_due = a.period != 0u && k.any_due;
         }
         due = any_due && my_due <= T;
+        // this wave is done with tick it's records; a slot overflow here ends the run at tick it for
+        // every wave (the others finish tick it, so every reader finds its records, and stop)
+        if (lane == 0u) {
+            dm_put(gx + kDmP + c, tag, 0u);
+            if (st.flags & MCS_FLAG_OVERFLOW) dm_put(gx + kDmAbort, 1u, it);
+        }
+        {
+            const unsigned long long ab = lane == 0u ? dm_get(gx + kDmAbort) : 0ull;
+            if (readlane((uint32_t)(ab >> 32), 0u) != 0u && readlane((uint32_t)ab, 0u) <= it) done = true;
+        }
 #ifdef MCS_STAMPS
         const uint64_t s4 = wall_clock64();
         sm[3] += s4 - s3;
@@ -363,6 +407,7 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
         if (lane == 0u) dm_fail(m, 2u);
         return;
     }
+    if (aborted) return;  // (the run overflowed and is redone: no state out)
     // the state out, for the next launch and the engine's readers
     dt_wave_sync();
     if (lane == 0u) a.cl[c] = st;
@@ -392,7 +437,7 @@ __device__ __forceinline__ void dm_trader(const DtArgs& a, const DtResArgs& m, c
         const uint32_t T = c0.T;
         const bool any_due = c0.any_due != 0u;
         const uint32_t tag = it + 1u;
-        const unsigned long long* const x1 = gx + (size_t)(it & 1u) * kDmX1Buf;
+        const unsigned long long* const x1 = gx + (size_t)(it % kDmRing) * kDmX1Buf;
         const uint64_t t0 = wall_clock64();
         if (any_due) {
             // X1: lane q gathers cluster q's record
