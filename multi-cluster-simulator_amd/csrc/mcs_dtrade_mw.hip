@@ -12,10 +12,14 @@
 //        and the count of the rounds' side effects on that cluster's live state, queued in HBM in
 //        the rounds' order (X2); each cluster wave applies them (Foreign commits to a node and a
 //        running slot, virtual nodes: pkg/scheduler/cluster.go:65-125) and starts the next tick
-//   --   on a tick without a round (9 in 10 of C5-DELAY's) there is no phase D: every cluster wave
-//        reads every cluster's four clock words of X1 and computes the next clock itself
-//        (dm_next_clock: dt_next_ctl's T, done and any_due); the trader reads the same words to keep
-//        the control block, and no X2 is exchanged (r06: 10.0 -> 9.0 us per C5-DELAY tick)
+//   --   on a tick without a round (9 in 10 of C5-DELAY's) there is no phase D and no X2: a cluster
+//        wave with queued jobs of its own knows the next clock is T + 1 (dt_next_ctl: queued_any,
+//        not every job decided) and goes straight on; one with nothing queued reads every cluster's
+//        four clock words of X1 and computes the clock itself (dm_next_clock: dt_next_ctl's T, done
+//        and any_due).  So between two ticks with rounds the waves run ahead of each other, and a
+//        tick costs the busiest cluster's average work rather than the maximum over the clusters of
+//        every tick's (r06: 10.0 -> 9.0 us per C5-DELAY tick without X2, 8.2 -> 4.55 running ahead).
+//        The trader reads every tick's clock words in order to keep the control block.
 // Exchange: the worker workgroups run 8 blocks apart, which the dispatcher's round-robin puts on
 // one XCD (checked at the launch's start: a launch whose workers landed on more than one XCD does
 // nothing, and the engine runs the replayed kernels instead), so that XCD's L2 is the meeting
@@ -24,10 +28,12 @@
 // its tag is the exchange's epoch (tick + 1; the granules are zeroed before every launch): the data
 // is the flag (cdna_hip_programming.md Guideline 16).  The bulk data behind a granule (node
 // snapshots, the queued operations) is stored before it and drained with s_waitcnt vmcnt(0).
-// X1 has one buffer per tick parity: a cluster wave publishes tick n + 2's records only after it
-// read tick n + 1's clock words from every cluster (each of which read tick n's first) and after
-// the trader's progress granule says it has read tick n's.  X2 needs one buffer: the trader
-// publishes the next round's only after every cluster wave has published a later tick's records.
+// X1 is a ring of kDmRing buffers: a wave publishes tick n's records only after every reader (the
+// trader and each cluster wave, through their progress granules) is done with tick n - kDmRing's.
+// X2 needs one buffer: at a tick with rounds every wave waits for it, and the trader publishes the
+// next one only after every wave has published a later tick's records.  A slot overflow (the run
+// is redone with more slots) publishes its tick in an abort granule: every wave finishes that tick,
+// so the trader finds its records and stops, and every wait watches the granule.
 // Every wait is bounded (1 s without the epoch ends the launch with a failure word, and the engine
 // redoes the run on the replayed kernels).  Same results bit for bit as the replayed tick
 // (tests/test_gpu_dtrade.py).
