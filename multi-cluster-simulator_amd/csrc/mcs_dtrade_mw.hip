@@ -28,7 +28,7 @@
 // its tag is the exchange's epoch (tick + 1; the granules are zeroed before every launch): the data
 // is the flag (cdna_hip_programming.md Guideline 16).  The bulk data behind a granule (node
 // snapshots, the queued operations) is stored before it and drained with s_waitcnt vmcnt(0).
-// X1 is a ring of kDmRing buffers: a wave publishes tick n's records only after every reader (the
+// X1 is a ring of kDmRing (32) buffers: a wave publishes tick n's records only after every reader (the
 // trader and each cluster wave, through their progress granules) is done with tick n - kDmRing's.
 // X2 needs one buffer: at a tick with rounds every wave waits for it, and the trader publishes the
 // next one only after every wave has published a later tick's records.  A slot overflow (the run
@@ -50,7 +50,7 @@ static_assert(sizeof(DtRec) % 4u == 0u && kDmRecWords <= (uint32_t)kWave, "a rec
 // one buffer per tick parity), X2 per-cluster words [64] (queued operations) and [64] (the cluster's
 // next trader round), X2 clock words [4] (T, done, any_due, the earliest next round over the system),
 // the trader's progress [1] (tag: the last tick whose records it has read, + 1)
-constexpr uint32_t kDmRing = 8;  // X1 buffers: a cluster wave runs up to kDmRing ticks ahead of X1's readers
+constexpr uint32_t kDmRing = 32;  // X1 buffers: a cluster wave runs up to kDmRing ticks ahead of X1's readers (8: +0.8 %)
 constexpr uint32_t kDmX1Buf = kDmRecWords * kDtResMaxClusters;
 constexpr uint32_t kDmX2 = kDmRing * kDmX1Buf;
 constexpr uint32_t kDmX2Due = kDmX2 + kDtResMaxClusters;
