@@ -298,8 +298,9 @@ def main_c5_delay(args, world, rank, local_rank):
                 "bound": "hbm",
                 "limiter": ("latency: one workgroup runs every cluster's Delay iteration, then the trader rounds, "
                             "per tick (DESIGN.md §11)" if ts["loop_form"] == 3 else
-                            "latency: the slowest cluster's Delay iteration, then the trader rounds, per tick, "
-                            "with two granule exchanges (DESIGN.md §11)" if ts["loop_form"] == 5 else
+                            "latency: the busiest cluster's own Delay iterations (the waves run ahead of each other "
+                            "between trader rounds), and a meeting of every wave at each tick with a round "
+                            "(DESIGN.md §11)" if ts["loop_form"] == 5 else
                             "launch/latency: a tick is dependent launches of a few us (DESIGN.md §11)"),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
