@@ -110,8 +110,9 @@ __global__ __launch_bounds__(64) void dt_step_kernel(DtArgs a) {
     __syncthreads();
     DT_MARK(0);
 
+    DtArrWin aw{kEmpty, kEmpty};  // (a fresh window every tick: the step kernel keeps nothing)
     st = dt_phase_a<false>(a, c, lane, T, N, NN, exact, j0, J, jobs, l1cm, l1jd, l1al, sb, S, nodes, sfin, hist, st, snap_l,
-                      snap_dirty DT_STAMP_ARGS);
+                      snap_dirty, aw DT_STAMP_ARGS);
 
     DT_MARK(4);
     if (snap_dirty && lane < NN) a.l1snap[(size_t)c * a.W + lane] = snap_l;

@@ -136,6 +136,23 @@ struct DtOpQueue {
     }
 };
 
+// The arrival times of 64 jobs from `base` (lane i: job base + i, kEmpty past the cluster's last):
+// the resident tick keeps them in a register from tick to tick, so the arrivals and the record's next
+// arrival read no job record from HBM until the window is used up (the replayed step kernel starts
+// every tick with base = kEmpty: one load, as before)
+struct DtArrWin {
+    uint32_t base;
+    uint32_t arr;
+};
+__device__ __forceinline__ void dt_win_at(DtArrWin& w, const uint32_t at, const uint32_t J, const uint4* jobs,
+                                          const uint32_t lane) {
+    if (at < w.base || at - w.base >= (uint32_t)kWave) {
+        w.base = at;
+        const uint32_t i = at + lane;
+        w.arr = i < J ? jobs[i].x : kEmpty;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Phase A of cluster c at tick T, after its state, nodes and slots are in place (nodes and sfin in
 // LDS, the cluster state st): releases, "/delay" arrivals, the Level1 pass, the Level0 head.  j0, J:
@@ -147,7 +164,7 @@ __device__ __forceinline__ DtCluster dt_phase_a(const DtArgs& a, const uint32_t 
                                            unsigned long long* l1jd, unsigned long long* l1al, const size_t sb,
                                            const uint32_t S,
                                            unsigned long long* nodes, uint32_t* sfin, uint32_t* hist, DtCluster st,
-                                           unsigned long long& snap_l, bool& snap_dirty DT_STAMP_PARAMS) {
+                                           unsigned long long& snap_l, bool& snap_dirty, DtArrWin& aw DT_STAMP_PARAMS) {
 
     // releases due at T (cluster.go:153-157), Foreign jobs included
     if (st.minf <= T) {
@@ -177,11 +194,13 @@ __device__ __forceinline__ DtCluster dt_phase_a(const DtArgs& a, const uint32_t 
     {
         const uint32_t before = st.next_arr;
         while (st.next_arr < J) {
-            const uint32_t i = st.next_arr + lane;
-            const bool ok = i < J && jobs[i].x <= T;
+            dt_win_at(aw, st.next_arr, J, jobs, lane);
+            const uint32_t off = st.next_arr - aw.base;
+            // (arrival-sorted: the jobs arrived by T are the window's lanes [off, off + n))
+            const bool ok = lane >= off && aw.arr <= T;
             const uint32_t n = (uint32_t)__builtin_popcountll(__ballot(ok));
             st.next_arr += n;
-            if (n < (uint32_t)kWave) break;
+            if (off + n < (uint32_t)kWave) break;
         }
         st.count += (long long)(st.next_arr - before);
     }

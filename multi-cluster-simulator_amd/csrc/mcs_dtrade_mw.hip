@@ -169,6 +169,7 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
 #endif
     bool failed = false;
     bool aborted = false;  // another cluster's slot overflow ended the run (it is redone bigger)
+    DtArrWin aw{kEmpty, kEmpty};  // the next 64 arrival times, kept from tick to tick
     uint32_t seen = 0;     // every reader has read X1 up to this tick (cached)
 #ifdef MCS_STAMPS
     uint64_t sm[5] = {0, 0, 0, 0, 0}, sticks = 0, s_prev = wall_clock64(), s_ops = 0;
@@ -184,7 +185,7 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
         if (!exact) snap_l = 0ull;  // (the replayed kernel loads it for exact clusters only)
         bool snap_dirty = false;
         st = dt_phase_a<true>(a, c, lane, T, N, NN, exact, j0, J, jobs, l1cm, l1jd, l1al, sb, S, nodes, sfin, hist, st,
-                              snap_l, snap_dirty DT_STAMP_ARGS);
+                              snap_l, snap_dirty, aw DT_STAMP_ARGS);
         (void)snap_dirty;  // (written back at the launch's end)
 #ifdef MCS_STAMPS
         const uint64_t s1 = wall_clock64();
@@ -198,6 +199,11 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
             for (uint32_t i = lane; i < NN; i += kWave) snap[i < N ? i : a.NS + (i - N)] = nodes[i];
         uint32_t fsc = 0, fsm = 0, fmd = 0, ssc = 0, ssm = 0, sst = 0;
         dt_contracts<true>(due, lane, st.l1n, l1cm, l1jd, hist, fsc, fsm, fmd, ssc, ssm, sst);
+        uint32_t nxt = kEmpty;  // the next arrival, from the window (moved on when it is used up)
+        if (st.next_arr < J) {
+            dt_win_at(aw, st.next_arr, J, jobs, lane);
+            nxt = readlane(aw.arr, st.next_arr - aw.base);
+        }
         if (lane == 0u) {
             DtRec r;
             r.cu = st.cu;
@@ -211,7 +217,7 @@ __device__ __forceinline__ void dm_cluster(const DtArgs& a, const DtResArgs& m, 
             r.flags = st.flags;
             r.done = st.decided == J ? 1u : 0u;
             r.queued = (st.l1n > 0u || st.next_arr > st.l0_head) ? 1u : 0u;
-            r.nxt = st.next_arr < J ? jobs[st.next_arr].x : kEmpty;
+            r.nxt = nxt;
             r.fc = fsc;
             r.fm = fsm;
             r.ft = fmd;
